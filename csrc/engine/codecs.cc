@@ -1,0 +1,345 @@
+// codecs.cc — host-side reference codecs and checksums.
+//
+// These are the CPU references the GPU kernels are tested against, and the
+// producers of compressed test data (no LZ4/snappy library is installed):
+//   - CRC32C (Castagnoli, reflected 0x82F63B78), slicing-by-8;
+//   - PostgreSQL's page checksum (FNV-1a variant over 32 interleaved sums,
+//     pg_checksum_page semantics, BLCKSZ-generic);
+//   - LZ4 raw block format: greedy single-probe compressor + safe decoder;
+//   - snappy raw format: greedy compressor + safe decoder.
+#include <errno.h>
+#include <string.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "strom/strom.h"
+
+namespace {
+
+struct Crc32cTables {
+  uint32_t t[8][256];
+  Crc32cTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xff];
+  }
+};
+const Crc32cTables &crc_tables() {
+  static Crc32cTables t;
+  return t;
+}
+
+const uint32_t kPgBase[32] = {
+    0x5B1F36E9, 0xB8525960, 0x02AB50AA, 0x1DE66D2A, 0x79FF467A, 0x9BB9F8A3, 0x217E7CD2,
+    0x83E13D2C, 0xF8D4474F, 0xE39EB970, 0x42C6AE16, 0x993216FA, 0x7B093B5D, 0x98DAFF3C,
+    0xF718902A, 0x0B1C9CDB, 0xE58F764B, 0x187636BC, 0x5D7B3BB1, 0xE73DE7DE, 0x92BEC979,
+    0xCCA6C0B2, 0x304A0979, 0x85AA43D4, 0x783125BB, 0x6CA8EAA2, 0xE407EAC6, 0x4B5CFC3E,
+    0x9FBF8C76, 0x15CA20BE, 0xF2CA9FFF, 0x3ED50F2B};
+
+inline uint32_t pg_mix(uint32_t sum, uint32_t v) {
+  uint32_t t = sum ^ v;
+  return t * 16777619u ^ (t >> 17);
+}
+
+inline uint32_t rd32(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+
+// ---------------------------------------------------------------- LZ4
+constexpr int kMinMatch = 4;
+constexpr int kLastLiterals = 5;
+constexpr int kMfLimit = 12;
+
+uint8_t *lz4_put_len(uint8_t *op, uint8_t *oend, size_t len) {
+  while (len >= 255) {
+    if (op >= oend) return nullptr;
+    *op++ = 255;
+    len -= 255;
+  }
+  if (op >= oend) return nullptr;
+  *op++ = (uint8_t)len;
+  return op;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t strom_crc32c_host(uint32_t crc, const void *buf, size_t len) {
+  const Crc32cTables &T = crc_tables();
+  const uint8_t *p = (const uint8_t *)buf;
+  uint32_t c = ~crc;
+  while (len >= 8) {
+    uint32_t lo = rd32(p) ^ c, hi = rd32(p + 4);
+    c = T.t[7][lo & 0xff] ^ T.t[6][(lo >> 8) & 0xff] ^ T.t[5][(lo >> 16) & 0xff] ^
+        T.t[4][lo >> 24] ^ T.t[3][hi & 0xff] ^ T.t[2][(hi >> 8) & 0xff] ^
+        T.t[1][(hi >> 16) & 0xff] ^ T.t[0][hi >> 24];
+    p += 8;
+    len -= 8;
+  }
+  while (len--) c = (c >> 8) ^ T.t[0][(c ^ *p++) & 0xff];
+  return ~c;
+}
+
+uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno, uint32_t page_sz) {
+  const uint8_t *p = (const uint8_t *)page;
+  uint32_t sums[32];
+  memcpy(sums, kPgBase, sizeof sums);
+  const uint32_t rows = page_sz / 4 / 32;
+  for (uint32_t i = 0; i < rows; ++i)
+    for (int j = 0; j < 32; ++j) {
+      uint32_t off = (i * 32 + j) * 4;
+      uint32_t v = rd32(p + off);
+      if (off == 8) v &= 0xffff0000u;  // pd_checksum (bytes 8..9) reads as zero
+      sums[j] = pg_mix(sums[j], v);
+    }
+  for (int r = 0; r < 2; ++r)
+    for (int j = 0; j < 32; ++j) sums[j] = pg_mix(sums[j], 0);
+  uint32_t x = 0;
+  for (int j = 0; j < 32; ++j) x ^= sums[j];
+  x ^= blkno;
+  return (uint16_t)((x % 65535u) + 1);
+}
+
+long strom_lz4_compress_host(const void *src, size_t n, void *dst, size_t cap) {
+  const uint8_t *ip = (const uint8_t *)src, *base = ip, *iend = ip + n;
+  const uint8_t *anchor = ip;
+  uint8_t *op = (uint8_t *)dst, *oend = op + cap;
+  std::vector<int32_t> table(1 << 16, -1);
+  const uint8_t *mflimit = n > (size_t)kMfLimit ? iend - kMfLimit : base;
+  const uint8_t *matchlimit = iend - kLastLiterals;
+  if (n > (size_t)kMfLimit) {
+    while (ip < mflimit) {
+      uint32_t seq = rd32(ip);
+      uint32_t h = (seq * 2654435761u) >> 16;
+      int32_t cand = table[h];
+      table[h] = (int32_t)(ip - base);
+      if (cand < 0 || ip - (base + cand) > 65535 || rd32(base + cand) != seq) {
+        ++ip;
+        continue;
+      }
+      const uint8_t *match = base + cand;
+      // extend backwards over pending literals
+      while (ip > anchor && match > base && ip[-1] == match[-1]) {
+        --ip;
+        --match;
+      }
+      const uint8_t *mp = ip + kMinMatch, *mm = match + kMinMatch;
+      while (mp < matchlimit && *mp == *mm) {
+        ++mp;
+        ++mm;
+      }
+      size_t lit = ip - anchor, mlen = mp - ip - kMinMatch;
+      if (op + 1 + lit / 255 + lit + 2 + mlen / 255 + 2 > oend) return -ENOSPC;
+      uint8_t *token = op++;
+      *token = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+      if (lit >= 15) op = lz4_put_len(op, oend, lit - 15);
+      memcpy(op, anchor, lit);
+      op += lit;
+      uint16_t off = (uint16_t)(ip - match);
+      *op++ = (uint8_t)off;
+      *op++ = (uint8_t)(off >> 8);
+      *token |= (uint8_t)(mlen >= 15 ? 15 : mlen);
+      if (mlen >= 15) op = lz4_put_len(op, oend, mlen - 15);
+      if (!op) return -ENOSPC;
+      ip = mp;
+      anchor = ip;
+      if (ip < mflimit) {
+        // seed the table inside the match tail for better ratio
+        table[(rd32(ip - 2) * 2654435761u) >> 16] = (int32_t)(ip - 2 - base);
+      }
+    }
+  }
+  size_t lit = iend - anchor;
+  if (op + 1 + lit / 255 + 1 + lit > oend) return -ENOSPC;
+  uint8_t *token = op++;
+  *token = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+  if (lit >= 15) op = lz4_put_len(op, oend, lit - 15);
+  memcpy(op, anchor, lit);
+  op += lit;
+  return op - (uint8_t *)dst;
+}
+
+long strom_lz4_decompress_host(const void *src, size_t n, void *dst, size_t cap) {
+  const uint8_t *ip = (const uint8_t *)src, *iend = ip + n;
+  uint8_t *op = (uint8_t *)dst, *ostart = op, *oend = op + cap;
+  while (ip < iend) {
+    uint8_t token = *ip++;
+    size_t lit = token >> 4;
+    if (lit == 15) {
+      uint8_t b;
+      do {
+        if (ip >= iend) return -EINVAL;
+        b = *ip++;
+        lit += b;
+      } while (b == 255);
+    }
+    if ((size_t)(iend - ip) < lit || (size_t)(oend - op) < lit) return -EINVAL;
+    memcpy(op, ip, lit);
+    op += lit;
+    ip += lit;
+    if (ip >= iend) break;  // last sequence: literals only
+    if (iend - ip < 2) return -EINVAL;
+    size_t off = ip[0] | (ip[1] << 8);
+    ip += 2;
+    if (off == 0 || off > (size_t)(op - ostart)) return -EINVAL;
+    size_t mlen = token & 15;
+    if (mlen == 15) {
+      uint8_t b;
+      do {
+        if (ip >= iend) return -EINVAL;
+        b = *ip++;
+        mlen += b;
+      } while (b == 255);
+    }
+    mlen += kMinMatch;
+    if ((size_t)(oend - op) < mlen) return -EINVAL;
+    const uint8_t *m = op - off;
+    for (size_t i = 0; i < mlen; ++i) op[i] = m[i];  // overlap-safe forward copy
+    op += mlen;
+  }
+  return op - ostart;
+}
+
+long strom_snappy_compress_host(const void *src, size_t n, void *dst, size_t cap) {
+  const uint8_t *base = (const uint8_t *)src, *ip = base, *iend = base + n;
+  uint8_t *op = (uint8_t *)dst, *oend = op + cap;
+  // varint preamble
+  size_t v = n;
+  do {
+    if (op >= oend) return -ENOSPC;
+    uint8_t b = v & 0x7f;
+    v >>= 7;
+    *op++ = b | (v ? 0x80 : 0);
+  } while (v);
+  auto emit_literal = [&](const uint8_t *p, size_t len) -> bool {
+    while (len) {
+      size_t l = len;
+      size_t m = l - 1;
+      if (m < 60) {
+        if (op + 1 + l > oend) return false;
+        *op++ = (uint8_t)(m << 2);
+      } else {
+        int nb = m < 256 ? 1 : m < 65536 ? 2 : m < (1u << 24) ? 3 : 4;
+        if (op + 1 + nb + l > oend) return false;
+        *op++ = (uint8_t)((59 + nb) << 2);
+        for (int i = 0; i < nb; ++i) *op++ = (uint8_t)(m >> (8 * i));
+      }
+      memcpy(op, p, l);
+      op += l;
+      p += l;
+      len -= l;
+    }
+    return true;
+  };
+  auto emit_copy = [&](size_t off, size_t len) -> bool {
+    while (len > 0) {
+      size_t l = len > 64 ? 64 : len;
+      if (len > 64 && len - 64 < 4) l = 60;  // keep the remainder >= 4
+      if (l >= 4 && l <= 11 && off < 2048) {
+        if (op + 2 > oend) return false;
+        *op++ = (uint8_t)(1 | ((l - 4) << 2) | ((off >> 8) << 5));
+        *op++ = (uint8_t)off;
+      } else {
+        if (op + 3 > oend) return false;
+        *op++ = (uint8_t)(2 | ((l - 1) << 2));
+        *op++ = (uint8_t)off;
+        *op++ = (uint8_t)(off >> 8);
+      }
+      len -= l;
+    }
+    return true;
+  };
+  std::vector<int32_t> table(1 << 15, -1);
+  const uint8_t *anchor = ip;
+  if (n >= 8) {
+    const uint8_t *limit = iend - 4;
+    while (ip < limit) {
+      uint32_t seq = rd32(ip);
+      uint32_t h = (seq * 0x1e35a7bdu) >> 17;
+      int32_t cand = table[h];
+      table[h] = (int32_t)(ip - base);
+      if (cand < 0 || ip - (base + cand) > 65535 || rd32(base + cand) != seq) {
+        ++ip;
+        continue;
+      }
+      const uint8_t *m = base + cand;
+      size_t len = 4;
+      while (ip + len < iend && ip[len] == m[len]) ++len;
+      if (!emit_literal(anchor, ip - anchor)) return -ENOSPC;
+      if (!emit_copy(ip - m, len)) return -ENOSPC;
+      ip += len;
+      anchor = ip;
+    }
+  }
+  if (!emit_literal(anchor, iend - anchor)) return -ENOSPC;
+  return op - (uint8_t *)dst;
+}
+
+long strom_snappy_decompress_host(const void *src, size_t n, void *dst, size_t cap) {
+  const uint8_t *ip = (const uint8_t *)src, *iend = ip + n;
+  uint64_t ulen = 0;
+  int shift = 0;
+  for (;;) {
+    if (ip >= iend || shift > 35) return -EINVAL;
+    uint8_t b = *ip++;
+    ulen |= (uint64_t)(b & 0x7f) << shift;
+    shift += 7;
+    if (!(b & 0x80)) break;
+  }
+  if (ulen > cap) return -ENOSPC;
+  uint8_t *op = (uint8_t *)dst, *ostart = op, *oend = op + ulen;
+  while (ip < iend) {
+    uint8_t tag = *ip++;
+    size_t len, off;
+    switch (tag & 3) {
+      case 0: {
+        len = (tag >> 2) + 1;
+        if (len > 60) {
+          int nb = (int)len - 60;
+          if (iend - ip < nb) return -EINVAL;
+          len = 0;
+          for (int i = 0; i < nb; ++i) len |= (size_t)ip[i] << (8 * i);
+          len += 1;
+          ip += nb;
+        }
+        if ((size_t)(iend - ip) < len || (size_t)(oend - op) < len) return -EINVAL;
+        memcpy(op, ip, len);
+        op += len;
+        ip += len;
+        continue;
+      }
+      case 1:
+        if (ip >= iend) return -EINVAL;
+        len = 4 + ((tag >> 2) & 7);
+        off = ((size_t)(tag >> 5) << 8) | *ip++;
+        break;
+      case 2:
+        if (iend - ip < 2) return -EINVAL;
+        len = (tag >> 2) + 1;
+        off = ip[0] | (ip[1] << 8);
+        ip += 2;
+        break;
+      default:
+        if (iend - ip < 4) return -EINVAL;
+        len = (tag >> 2) + 1;
+        off = rd32(ip);
+        ip += 4;
+        break;
+    }
+    if (off == 0 || off > (size_t)(op - ostart) || (size_t)(oend - op) < len) return -EINVAL;
+    const uint8_t *m = op - off;
+    for (size_t i = 0; i < len; ++i) op[i] = m[i];
+    op += len;
+  }
+  return op == oend ? (long)ulen : -EINVAL;
+}
+
+}  // extern "C"

@@ -1,0 +1,521 @@
+// engine.cc — ioctl dispatch, SSD2GPU / SSD2RAM drivers, the C ABI.
+//
+// Dispatch mirrors strom_proc_ioctl (reference kmod/nvme_strom.c:2093-2147);
+// the two copy drivers follow ioctl_memcpy_ssd2gpu (:1610-1681) and
+// ioctl_memcpy_ssd2ram (:1890-1981): resolve the destination, classify the
+// file, plan the chunks, copy page-cache chunks on the caller's thread,
+// hand storage requests to the I/O engine, freeze the task and drop the
+// submitter's reference, then copy the output prefix back.  Unlike the
+// reference, storage requests are submitted BEFORE the page-cache copies
+// so both proceed in parallel; a failure after submission drains the task
+// before returning (reference :1674-1677).
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/ioctl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+
+#include "engine.h"
+
+namespace strom {
+
+struct Engine::OpenFile {
+  dev_t dev = 0;
+  ino_t ino = 0;
+  int fd_direct = -1;
+  int fd_buffered = -1;
+  FileClass fc;
+  std::mutex mu;
+  void *map = nullptr;        // PROT_READ mapping for mincore residency
+  size_t map_len = 0;
+  ~OpenFile() {
+    if (map) munmap(map, map_len);
+    if (fd_direct >= 0 && fd_direct != fd_buffered) close(fd_direct);
+    if (fd_buffered >= 0) close(fd_buffered);
+  }
+  // resident 4 KiB pages of [off, off+len)
+  long resident(uint64_t off, uint32_t len) {
+    if (!map) return -1;
+    if (off >= map_len) return 0;
+    uint32_t n = (uint32_t)std::min<uint64_t>(len, map_len - off);
+    unsigned char vec[1024];
+    uint32_t pages = (n + 4095) / 4096;
+    long res = 0;
+    for (uint32_t p = 0; p < pages; p += 1024) {
+      uint32_t cnt = std::min<uint32_t>(1024, pages - p);
+      if (mincore((char *)map + off + (uint64_t)p * 4096, (size_t)cnt * 4096, vec) != 0) return -1;
+      for (uint32_t i = 0; i < cnt; ++i) res += vec[i] & 1;
+    }
+    return res;
+  }
+};
+
+static std::mutex g_engine_mu;
+static Engine *g_engine = nullptr;
+
+Engine &engine() {
+  std::lock_guard<std::mutex> g(g_engine_mu);
+  if (!g_engine) g_engine = new Engine();
+  return *g_engine;
+}
+
+void engine_reset() {
+  std::lock_guard<std::mutex> g(g_engine_mu);
+  delete g_engine;
+  g_engine = nullptr;
+}
+
+Engine::Engine() { io_ = std::make_unique<IoEngine>(config()); }
+Engine::~Engine() { io_.reset(); }
+
+std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    *err = -errno;
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> g(files_mu_);
+  auto key = std::make_pair(st.st_dev, st.st_ino);
+  auto it = files_.find(key);
+  if (it != files_.end()) {
+    std::shared_ptr<OpenFile> f = it->second;
+    struct stat cst;
+    bool stale = fstat(f->fd_buffered, &cst) != 0 || cst.st_nlink == 0 ||
+                 cst.st_ino != st.st_ino;
+    if (!stale) {
+      if ((off_t)f->fc.size != st.st_size) {
+        std::lock_guard<std::mutex> fg(f->mu);
+        f->fc.size = st.st_size;
+        if (f->map) munmap(f->map, f->map_len);
+        f->map = nullptr;
+        if (config().pgcache_probe && st.st_size > 0) {
+          void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, f->fd_buffered, 0);
+          if (m != MAP_FAILED) {
+            f->map = m;
+            f->map_len = (size_t)st.st_size;
+          }
+        }
+      }
+      return f;
+    }
+    files_.erase(it);
+  }
+  auto f = std::make_shared<OpenFile>();
+  int rc = classify_file(fd, &f->fc, config().strict);
+  if (rc) {
+    *err = rc;
+    return nullptr;
+  }
+  char path[64];
+  snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+  f->fd_buffered = open(path, O_RDONLY | O_CLOEXEC);
+  if (f->fd_buffered < 0) f->fd_buffered = fcntl(fd, F_DUPFD_CLOEXEC, 0);
+  if (f->fd_buffered < 0) {
+    *err = -errno;
+    return nullptr;
+  }
+  f->fd_direct = f->fd_buffered;
+  if (config().direct_io) {
+    int d = open(path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+    if (d >= 0) f->fd_direct = d;
+  }
+  f->dev = st.st_dev;
+  f->ino = st.st_ino;
+  if (config().pgcache_probe && st.st_size > 0) {
+    void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, f->fd_buffered, 0);
+    if (m != MAP_FAILED) {
+      f->map = m;
+      f->map_len = (size_t)st.st_size;
+    }
+  }
+  if (files_.size() > 256) files_.clear();  // bound the cache
+  files_[key] = f;
+  return f;
+}
+
+int Engine::check_file(strom_check_file *a) {
+  FileClass fc;
+  int rc = classify_file(a->fdesc, &fc, config().strict);
+  if (rc) return rc;
+  a->numa_node_id = fc.numa_node;
+  a->support_dma64 = fc.dma64 ? 1 : 0;
+  return 0;
+}
+
+// copy page-cache chunks (buffered reads) into user memory
+static int copy_ram_chunks(int fd, const ChunkPlan &plan, uint32_t chunk_sz, uint64_t file_size,
+                           char *dest_base) {
+  uint64_t t0 = tsc_now();
+  for (size_t i = 0; i < plan.ram_fpos.size(); ++i) {
+    char *dst = dest_base + plan.ram_dest[i];
+    uint64_t fpos = plan.ram_fpos[i];
+    uint32_t want = (uint32_t)std::min<uint64_t>(chunk_sz, file_size - fpos);
+    uint32_t done = 0;
+    while (done < want) {
+      ssize_t n = pread(fd, dst + done, want - done, (off_t)(fpos + done));
+      if (n < 0) {
+        if (errno == EINTR) continue;
+        return -errno;
+      }
+      if (n == 0) break;
+      done += (uint32_t)n;
+    }
+    if (done < chunk_sz) memset(dst + done, 0, chunk_sz - done);
+  }
+  stats().nr_debug[1].fetch_add(plan.ram_fpos.size(), std::memory_order_relaxed);
+  stats().clk_debug[1].fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+  return 0;
+}
+
+static void build_requests(Task *t, const ChunkPlan &plan, int fd_direct, int fd_buffered,
+                           uint64_t file_size, GpuMapping *gmap, uint64_t dest_base,
+                           bool dest_is_host, std::vector<IoReq> *out) {
+  uint64_t t0 = tsc_now();
+  out->reserve(plan.ssd.size());
+  uint64_t now_ns = mono_ns();
+  for (const IoRange &r : plan.ssd) {
+    IoReq q;
+    q.task = t;
+    q.fd = fd_direct;
+    q.fd_buffered = fd_buffered;
+    q.off = r.file_off;
+    q.len = r.len;
+    q.valid = (uint32_t)std::min<uint64_t>(r.len, file_size > r.file_off ? file_size - r.file_off : 0);
+    if (dest_is_host) {
+      q.host_dst = (uint8_t *)(dest_base + r.dest_off);
+    } else {
+      q.gpu_dst = dest_base + r.dest_off;
+      q.device = gmap->device;
+    }
+    q.gmap = gmap;
+    q.t_submit_ns = now_ns;
+    q.t_submit_tsc = tsc_now();
+    tasks().get(t);
+    if (gmap) gmap->inflight.fetch_add(1);
+    stats().inflight_inc();
+    out->push_back(q);
+  }
+  stats().nr_setup_prps.fetch_add(plan.ssd.size(), std::memory_order_relaxed);
+  stats().clk_setup_prps.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+}
+
+int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
+  a->nr_ram2gpu = a->nr_ssd2gpu = a->nr_dma_submit = a->nr_dma_blocks = 0;
+  a->dma_task_id = 0;
+  if (a->nr_chunks == 0) return -EINVAL;
+  if (!a->chunk_ids) return -EFAULT;
+  auto gmap = gpu_registry().get(a->handle);
+  if (!gmap) return -ENOENT;
+  uint64_t bytes = (uint64_t)a->nr_chunks * a->chunk_sz;
+  if (gmap->map_offset + a->offset + bytes > gmap->map_length) return -ERANGE;
+  int err = 0;
+  auto f = open_file(a->file_desc, &err);
+  if (!f) return err;
+
+  PlanParams pp;
+  pp.ids = a->chunk_ids;
+  pp.nr_chunks = a->nr_chunks;
+  pp.chunk_sz = a->chunk_sz;
+  pp.relseg_sz = a->relseg_sz;
+  pp.file_size = (uint64_t)f->fc.size;
+  pp.max_request = config().max_request;
+  pp.reorder = true;
+  OpenFile *fp = f.get();
+  if (config().pgcache_probe && f->map) {
+    pp.resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
+  }
+  ChunkPlan plan;
+  int rc = plan_chunks(pp, &plan);
+  if (rc) return rc;
+  if (plan.nr_ram && !a->wb_buffer) return -EFAULT;
+
+  Task *t = tasks().create(session);
+  t->gmap = gmap;
+  bool host_dest = gmap->device < 0;  // emulated GPU memory (CPU tests)
+  std::vector<IoReq> reqs;
+  build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, gmap.get(),
+                 gmap->va + a->offset, host_dest, &reqs);
+  uint64_t t0 = tsc_now();
+  io_->submit(reqs);
+  stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
+  stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+
+  // page-cache chunks overlap with the storage reads
+  if (plan.nr_ram) rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, a->wb_buffer);
+  t->frozen = true;
+  uint64_t id = t->id;
+  tasks().put(t, rc);
+  if (rc) {
+    long st;
+    tasks().wait(id, &st, -1);  // drain in-flight requests
+    return rc;
+  }
+  a->dma_task_id = id;
+  a->nr_ram2gpu = plan.nr_ram;
+  a->nr_ssd2gpu = plan.nr_ssd;
+  a->nr_dma_submit = plan.nr_submit;
+  a->nr_dma_blocks = plan.nr_blocks;
+  memcpy(a->chunk_ids, plan.ids_out.data(), sizeof(uint32_t) * a->nr_chunks);
+  return 0;
+}
+
+int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
+  a->nr_ram2ram = a->nr_ssd2ram = a->nr_dma_submit = a->nr_dma_blocks = 0;
+  a->dma_task_id = 0;
+  if (a->nr_chunks == 0) return -EINVAL;
+  if (!a->chunk_ids || !a->dest_uaddr) return -EFAULT;
+  uint64_t bytes = (uint64_t)a->nr_chunks * a->chunk_sz;
+  std::shared_ptr<DmaBuffer> dbuf;
+  size_t dest_off = 0;
+  int rc = dmabuf_registry().resolve(a->dest_uaddr, bytes, &dbuf, &dest_off);
+  if (rc) return rc;
+  int err = 0;
+  auto f = open_file(a->file_desc, &err);
+  if (!f) return err;
+
+  PlanParams pp;
+  pp.ids = a->chunk_ids;
+  pp.nr_chunks = a->nr_chunks;
+  pp.chunk_sz = a->chunk_sz;
+  pp.relseg_sz = a->relseg_sz;
+  pp.file_size = (uint64_t)f->fc.size;
+  pp.max_request = config().max_request;
+  pp.reorder = false;
+  OpenFile *fp = f.get();
+  if (config().pgcache_probe && f->map) {
+    pp.resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
+  }
+  ChunkPlan plan;
+  rc = plan_chunks(pp, &plan);
+  if (rc) return rc;
+
+  Task *t = tasks().create(session);
+  t->dbuf = dbuf;
+  std::vector<IoReq> reqs;
+  build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, nullptr,
+                 (uint64_t)a->dest_uaddr, true, &reqs);
+  uint64_t t0 = tsc_now();
+  io_->submit(reqs);
+  stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
+  stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+  if (plan.nr_ram)
+    rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, (char *)a->dest_uaddr);
+  t->frozen = true;
+  uint64_t id = t->id;
+  tasks().put(t, rc);
+  if (rc) {
+    long st;
+    tasks().wait(id, &st, -1);
+    return rc;
+  }
+  a->dma_task_id = id;
+  a->nr_ram2ram = plan.nr_ram;
+  a->nr_ssd2ram = plan.nr_ssd;
+  a->nr_dma_submit = plan.nr_submit;
+  a->nr_dma_blocks = plan.nr_blocks;
+  return 0;
+}
+
+int Engine::memcpy_wait(strom_memcpy_wait *a) {
+  long st = 0;
+  int rc = tasks().wait(a->dma_task_id, &st, -1);
+  a->status = st;
+  return rc;
+}
+
+int Engine::memcpy_wait_timed(strom_memcpy_wait_timed *a) {
+  long st = 0;
+  int rc = tasks().wait(a->dma_task_id, &st, (int64_t)a->timeout_ns);
+  a->status = st;
+  return rc;
+}
+
+int Engine::ioctl(int session, unsigned long cmd, void *arg) {
+  if (!arg) return -EFAULT;
+  switch (cmd) {
+    case STROM_IOCTL__CHECK_FILE:
+      return check_file((strom_check_file *)arg);
+    case STROM_IOCTL__MAP_GPU_MEMORY: {
+      auto *a = (strom_map_gpu_memory *)arg;
+      return gpu_registry().map(a->vaddress, a->length, -1, a);
+    }
+    case STROM_IOCTL__MAP_GPU_DMABUF: {
+      auto *a = (strom_map_gpu_dmabuf *)arg;
+      strom_map_gpu_memory m{};
+      int rc = gpu_registry().map(a->vaddress, a->length, a->dmabuf_fd, &m);
+      a->handle = m.handle;
+      a->gpu_page_sz = m.gpu_page_sz;
+      a->gpu_npages = m.gpu_npages;
+      return rc;
+    }
+    case STROM_IOCTL__UNMAP_GPU_MEMORY:
+      return gpu_registry().unmap(((strom_unmap_gpu_memory *)arg)->handle);
+    case STROM_IOCTL__LIST_GPU_MEMORY:
+      return gpu_registry().list((strom_list_gpu_memory *)arg);
+    case STROM_IOCTL__INFO_GPU_MEMORY:
+      return gpu_registry().info((strom_info_gpu_memory *)arg);
+    case STROM_IOCTL__ALLOC_DMA_BUFFER: {
+      auto *a = (strom_alloc_dma_buffer *)arg;
+      return dmabuf_registry().alloc(a->length, a->node_id, &a->dmabuf_fdesc);
+    }
+    case STROM_IOCTL__MEMCPY_SSD2GPU:
+      return memcpy_ssd2gpu(session, (strom_memcpy_ssd2gpu *)arg);
+    case STROM_IOCTL__MEMCPY_SSD2RAM:
+      return memcpy_ssd2ram(session, (strom_memcpy_ssd2ram *)arg);
+    case STROM_IOCTL__MEMCPY_WAIT:
+      return memcpy_wait((strom_memcpy_wait *)arg);
+    case STROM_IOCTL__MEMCPY_WAIT_TIMED:
+      return memcpy_wait_timed((strom_memcpy_wait_timed *)arg);
+    case STROM_IOCTL__STAT_INFO:
+      return stats().fill((strom_stat_info *)arg);
+    case STROM_IOCTL__STAT_HIST:
+      return stats().fill_hist((strom_stat_hist *)arg);
+    default:
+      return -EINVAL;
+  }
+}
+
+}  // namespace strom
+
+// ===================================================================== C ABI
+using namespace strom;
+
+static std::mutex g_sess_mu;
+static int g_next_session = 1;
+static int g_kernel_fd = -2;  // -2 unknown, -1 none
+
+static int kernel_fd() {
+  if (g_kernel_fd != -2) return g_kernel_fd;
+  const char *prov = getenv("STROM_PROVIDER");
+  if (prov && strcmp(prov, "user") == 0) return g_kernel_fd = -1;
+  int fd = open(STROM_DEVICE_PATHNAME, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) fd = open(NVME_STROM_IOCTL_PATHNAME, O_RDONLY | O_CLOEXEC);
+  return g_kernel_fd = fd;
+}
+
+extern "C" {
+
+const char *strom_version(void) { return "strom-mi355x 0.1.0 (abi nvme-strom 0.6)"; }
+
+int strom_provider(void) {
+  std::lock_guard<std::mutex> g(g_sess_mu);
+  return kernel_fd() >= 0 ? 1 : 0;
+}
+
+int strom_open(void) {
+  std::lock_guard<std::mutex> g(g_sess_mu);
+  return g_next_session++;
+}
+
+int strom_close(int session) {
+  if (session <= 0) return -EBADF;
+  int n = tasks().reclaim(session);
+  if (n) STROM_LOG(0, "session %d closed with %d unclaimed failed task(s)", session, n);
+  return n;
+}
+
+int strom_ioctl(int session, unsigned long cmd, void *arg) {
+  int kfd;
+  {
+    std::lock_guard<std::mutex> g(g_sess_mu);
+    kfd = kernel_fd();
+  }
+  if (kfd >= 0) {
+    int r = ioctl(kfd, cmd, arg);
+    return r < 0 ? -errno : r;
+  }
+  return engine().ioctl(session, cmd, arg);
+}
+
+int nvme_strom_ioctl(unsigned long cmd, const void *arg) {
+  static thread_local int session = 0;
+  if (session == 0) session = strom_open();
+  int r = strom_ioctl(session, cmd, (void *)arg);
+  if (r < 0) {
+    errno = -r;
+    return -1;
+  }
+  return r;
+}
+
+int strom_config_set(const char *key, const char *value) {
+  std::lock_guard<std::mutex> g(g_engine_mu);
+  return config().set(key, value);
+}
+
+int strom_config_get(const char *key, char *buf, size_t buflen) {
+  std::string v;
+  int rc = config().get(key, &v);
+  if (rc) return rc;
+  if (v.size() + 1 > buflen) return -ENOSPC;
+  memcpy(buf, v.c_str(), v.size() + 1);
+  return 0;
+}
+
+int strom_engine_reset(void) {
+  engine_reset();
+  return 0;
+}
+
+int strom_fault_inject(long fail_at, int err, long short_at, int short_bytes, int delay_us) {
+  FaultInjector &f = faults();
+  f.counter = 0;
+  f.fail_at = fail_at;
+  f.err = err ? err : EIO;
+  f.short_at = short_at;
+  f.short_bytes = short_bytes;
+  f.delay_us = delay_us;
+  return 0;
+}
+
+long strom_resident_bytes(int fd, uint64_t offset, uint64_t length) {
+  struct stat st;
+  if (fstat(fd, &st) != 0) return -errno;
+  if (offset >= (uint64_t)st.st_size) return 0;
+  length = std::min<uint64_t>(length, (uint64_t)st.st_size - offset);
+  uint64_t lo = offset & ~4095ull;
+  size_t maplen = (size_t)(offset + length - lo);
+  void *m = mmap(nullptr, maplen, PROT_READ, MAP_SHARED, fd, (off_t)lo);
+  if (m == MAP_FAILED) return -errno;
+  size_t pages = (maplen + 4095) / 4096;
+  std::vector<unsigned char> vec(pages);
+  long res = 0;
+  if (mincore(m, maplen, vec.data()) == 0) {
+    for (auto v : vec) res += v & 1;
+  } else {
+    res = -errno;
+  }
+  munmap(m, maplen);
+  return res < 0 ? res : res * 4096;
+}
+
+int strom_evict_file(int fd) {
+  fdatasync(fd);
+  int r = posix_fadvise(fd, 0, 0, POSIX_FADV_DONTNEED);
+  return -r;
+}
+
+int strom_raid0_map(const uint64_t *zone_end, const uint64_t *zone_dev_start,
+                    const int *zone_nb_dev, int nzones, uint32_t chunk_sects,
+                    const uint64_t *data_offset, int raid_disks, uint64_t sector,
+                    uint32_t nr_sects, int *member, uint64_t *member_sector) {
+  Raid0Geometry g;
+  g.chunk_sects = chunk_sects;
+  for (int z = 0; z < nzones; ++z) {
+    g.zone_end.push_back(zone_end[z]);
+    g.zone_dev_start.push_back(zone_dev_start[z]);
+    // zone z holds the last nb_dev members (smaller members drop out)
+    std::vector<int> devs;
+    for (int d = raid_disks - zone_nb_dev[z]; d < raid_disks; ++d) devs.push_back(d);
+    g.zone_devs.push_back(devs);
+  }
+  for (int d = 0; d < raid_disks; ++d) g.data_offset.push_back(data_offset ? data_offset[d] : 0);
+  return g.map(sector, nr_sects, member, member_sector);
+}
+
+}  // extern "C"

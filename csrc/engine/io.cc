@@ -1,0 +1,480 @@
+// io.cc — request execution: io_uring / pread workers with HBM staging.
+//
+// Replaces the reference's PRP-list pool + blk-mq async submit/complete
+// (kmod/nvme_strom.c:822-1120) for an unprivileged process on MI355X:
+//
+//   caller thread ── submit() ──► per-worker queue (batched, one lock)
+//   worker k:  io_uring READs (O_DIRECT) up to queue_depth in flight
+//              ├─ host destination (SSD2RAM): done on CQE
+//              └─ HBM destination: CQE ► hipMemcpyAsync(slot → HBM) on the
+//                 worker's own non-blocking stream (its own SDMA queue),
+//                 hipEventRecord; the worker retires events in FIFO order,
+//                 returning the pinned slot and putting the task.
+//
+// Each worker owns its ring, its staging slots and its stream, so the hot
+// path takes no shared lock.  Workers are pinned to the CPUs of the GPU's
+// NUMA node and allocate staging there (PAR5 in SURVEY §2.3).
+#include <hip/hip_runtime.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <linux/io_uring.h>
+#include <sched.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <fstream>
+
+#include "engine.h"
+
+#ifndef MPOL_PREFERRED
+#define MPOL_PREFERRED 1
+#endif
+
+namespace strom {
+
+// ------------------------------------------------------------ raw io_uring
+class Uring {
+ public:
+  ~Uring() { close_ring(); }
+  int init(unsigned entries) {
+    io_uring_params p;
+    memset(&p, 0, sizeof p);
+    fd_ = (int)syscall(__NR_io_uring_setup, entries, &p);
+    if (fd_ < 0) return -errno;
+    sq_sz_ = p.sq_off.array + p.sq_entries * sizeof(unsigned);
+    cq_sz_ = p.cq_off.cqes + p.cq_entries * sizeof(io_uring_cqe);
+    bool single = p.features & IORING_FEAT_SINGLE_MMAP;
+    if (single) sq_sz_ = cq_sz_ = std::max(sq_sz_, cq_sz_);
+    sq_ptr_ = mmap(nullptr, sq_sz_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_,
+                   IORING_OFF_SQ_RING);
+    if (sq_ptr_ == MAP_FAILED) return fail();
+    cq_ptr_ = single ? sq_ptr_
+                     : mmap(nullptr, cq_sz_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE,
+                            fd_, IORING_OFF_CQ_RING);
+    if (cq_ptr_ == MAP_FAILED) return fail();
+    sqe_sz_ = p.sq_entries * sizeof(io_uring_sqe);
+    sqes_ = (io_uring_sqe *)mmap(nullptr, sqe_sz_, PROT_READ | PROT_WRITE,
+                                 MAP_SHARED | MAP_POPULATE, fd_, IORING_OFF_SQES);
+    if (sqes_ == MAP_FAILED) return fail();
+    char *sq = (char *)sq_ptr_, *cq = (char *)cq_ptr_;
+    sq_head_ = (unsigned *)(sq + p.sq_off.head);
+    sq_tail_ = (unsigned *)(sq + p.sq_off.tail);
+    sq_mask_ = *(unsigned *)(sq + p.sq_off.ring_mask);
+    sq_array_ = (unsigned *)(sq + p.sq_off.array);
+    cq_head_ = (unsigned *)(cq + p.cq_off.head);
+    cq_tail_ = (unsigned *)(cq + p.cq_off.tail);
+    cq_mask_ = *(unsigned *)(cq + p.cq_off.ring_mask);
+    cqes_ = (io_uring_cqe *)(cq + p.cq_off.cqes);
+    entries_ = p.sq_entries;
+    return 0;
+  }
+  io_uring_sqe *next_sqe() {
+    unsigned tail = *sq_tail_;
+    unsigned head = __atomic_load_n(sq_head_, __ATOMIC_ACQUIRE);
+    if (tail - head >= entries_) return nullptr;
+    unsigned idx = tail & sq_mask_;
+    io_uring_sqe *s = &sqes_[idx];
+    memset(s, 0, sizeof *s);
+    sq_array_[idx] = idx;
+    __atomic_store_n(sq_tail_, tail + 1, __ATOMIC_RELEASE);
+    ++pending_;
+    return s;
+  }
+  int enter(unsigned min_complete) {
+    unsigned flags = min_complete ? IORING_ENTER_GETEVENTS : 0;
+    int r = (int)syscall(__NR_io_uring_enter, fd_, pending_, min_complete, flags, nullptr, 0);
+    if (r < 0) return -errno;
+    pending_ -= (unsigned)r <= pending_ ? (unsigned)r : pending_;
+    return r;
+  }
+  bool peek(io_uring_cqe *out) {
+    unsigned head = *cq_head_;
+    if (head == __atomic_load_n(cq_tail_, __ATOMIC_ACQUIRE)) return false;
+    *out = cqes_[head & cq_mask_];
+    __atomic_store_n(cq_head_, head + 1, __ATOMIC_RELEASE);
+    return true;
+  }
+  unsigned pending() const { return pending_; }
+  bool ok() const { return fd_ >= 0; }
+
+ private:
+  int fail() {
+    int e = errno;
+    close_ring();
+    return -e;
+  }
+  void close_ring() {
+    if (sqes_ && sqes_ != MAP_FAILED) munmap(sqes_, sqe_sz_);
+    if (cq_ptr_ && cq_ptr_ != MAP_FAILED && cq_ptr_ != sq_ptr_) munmap(cq_ptr_, cq_sz_);
+    if (sq_ptr_ && sq_ptr_ != MAP_FAILED) munmap(sq_ptr_, sq_sz_);
+    if (fd_ >= 0) close(fd_);
+    fd_ = -1;
+    sqes_ = nullptr;
+    sq_ptr_ = cq_ptr_ = nullptr;
+  }
+  int fd_ = -1;
+  void *sq_ptr_ = nullptr, *cq_ptr_ = nullptr;
+  size_t sq_sz_ = 0, cq_sz_ = 0, sqe_sz_ = 0;
+  io_uring_sqe *sqes_ = nullptr;
+  io_uring_cqe *cqes_ = nullptr;
+  unsigned *sq_head_ = nullptr, *sq_tail_ = nullptr, *sq_array_ = nullptr;
+  unsigned *cq_head_ = nullptr, *cq_tail_ = nullptr;
+  unsigned sq_mask_ = 0, cq_mask_ = 0, entries_ = 0, pending_ = 0;
+};
+
+// ------------------------------------------------------------- completion
+void finish_request(IoReq &r, long status) {
+  Stats &st = stats();
+  st.nr_ssd2gpu.fetch_add(1, std::memory_order_relaxed);
+  st.clk_ssd2gpu.fetch_add(tsc_now() - r.t_submit_tsc, std::memory_order_relaxed);
+  st.inflight_dec();
+  if (r.gmap) {
+    if (r.gmap->inflight.fetch_sub(1) == 1) {
+      std::lock_guard<std::mutex> g(r.gmap->mu);
+      r.gmap->cv.notify_all();
+    }
+  }
+  tasks().put(r.task, status);
+}
+
+// read [off, off+len) fully; returns bytes read or -errno.
+static long pread_full(int fd, uint8_t *buf, uint32_t len, uint64_t off) {
+  uint32_t done = 0;
+  while (done < len) {
+    ssize_t n = pread(fd, buf + done, len - done, (off_t)(off + done));
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return -errno;
+    }
+    if (n == 0) break;
+    done += (uint32_t)n;
+  }
+  return done;
+}
+
+// ------------------------------------------------------------------ worker
+struct IoEngine::Worker {
+  struct Slot {
+    uint8_t *buf = nullptr;
+    hipEvent_t ev = nullptr;
+    int ev_dev = -1;
+    IoReq req;
+    uint64_t t_copy_ns = 0;
+  };
+  struct Ctx {           // one in-flight storage read
+    IoReq req;
+    int slot = -1;       // staging slot (HBM destination) or -1
+    uint8_t *dst = nullptr;
+    uint32_t len = 0;
+    uint64_t t0 = 0;
+  };
+
+  int idx = 0;
+  Config cfg;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<IoReq> q;
+  bool stop = false;
+  std::vector<Slot> slots;
+  std::vector<int> free_slots;
+  std::deque<int> copying;        // FIFO of slots with copies in flight
+  std::vector<hipStream_t> streams;
+  int cur_dev = -2;
+  Uring ring;
+  std::vector<Ctx> ctx;
+  std::vector<int> free_ctx;
+  int reads_inflight = 0;
+  int numa_node = -1;
+
+  void bind_numa() {
+    if (!cfg.numa_bind || numa_node < 0) return;
+    std::ifstream f("/sys/devices/system/node/node" + std::to_string(numa_node) + "/cpulist");
+    std::string list;
+    if (!(f >> list)) return;
+    cpu_set_t want, allowed, use;
+    CPU_ZERO(&want);
+    size_t pos = 0;
+    while (pos < list.size()) {
+      size_t comma = list.find(',', pos);
+      std::string part = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+      int a = 0, b = 0;
+      if (sscanf(part.c_str(), "%d-%d", &a, &b) == 2) {
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &want);
+      } else if (sscanf(part.c_str(), "%d", &a) == 1 && a < CPU_SETSIZE) {
+        CPU_SET(a, &want);
+      }
+      if (comma == std::string::npos) break;
+      pos = comma + 1;
+    }
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+    CPU_AND(&use, &want, &allowed);
+    if (CPU_COUNT(&use) > 0) sched_setaffinity(0, sizeof use, &use);
+    unsigned long mask[16] = {0};
+    if (numa_node < 1024) {
+      mask[numa_node / 64] = 1ul << (numa_node % 64);
+      syscall(SYS_set_mempolicy, MPOL_PREFERRED, mask, 1024ul);
+    }
+  }
+
+  bool ensure_slots() {
+    if (!slots.empty()) return true;
+    slots.resize(cfg.staging_slots);
+    for (int i = 0; i < cfg.staging_slots; ++i) {
+      slots[i].buf = (uint8_t *)hip::host_alloc(cfg.max_request);
+      if (!slots[i].buf) {
+        STROM_LOG(0, "worker %d: pinned staging allocation failed", idx);
+        for (auto &s : slots) hip::host_free(s.buf);
+        slots.clear();
+        return false;
+      }
+      free_slots.push_back(i);
+    }
+    return true;
+  }
+
+  hipStream_t stream_for(int dev) {
+    if (dev != cur_dev) {
+      (void)hipSetDevice(dev);
+      cur_dev = dev;
+    }
+    if ((int)streams.size() <= dev) streams.resize(dev + 1, nullptr);
+    if (!streams[dev]) (void)hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking);
+    return streams[dev];
+  }
+
+  // storage read finished for ctx c with `got` bytes or -errno
+  void on_read_done(Ctx &c, long got) {
+    IoReq &r = c.req;
+    uint64_t now = mono_ns();
+    stats().io_ns.add(now - c.t0);
+    long status = 0;
+    if (got == -EINVAL && r.fd_buffered >= 0 && r.fd_buffered != r.fd) {
+      // O_DIRECT refused (buffer alignment / filesystem): redo buffered
+      got = pread_full(r.fd_buffered, c.dst, c.len, r.off);
+    }
+    if (got < 0) {
+      status = got;
+    } else if ((uint32_t)got < r.valid) {
+      status = -EIO;  // short read before EOF
+    }
+    if (status == 0 && (uint32_t)got < r.len) memset(c.dst + got, 0, r.len - (uint32_t)got);
+    if (c.slot < 0) {
+      finish_request(r, status);
+      return;
+    }
+    Slot &s = slots[c.slot];
+    if (status != 0) {
+      free_slots.push_back(c.slot);
+      finish_request(r, status);
+      return;
+    }
+    hipStream_t st = stream_for(r.device);
+    if (!s.ev || s.ev_dev != r.device) {
+      if (s.ev) (void)hipEventDestroy(s.ev);
+      (void)hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+      s.ev_dev = r.device;
+    }
+    hipError_t e = hipMemcpyAsync((void *)r.gpu_dst, s.buf, r.len, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(s.ev, st);
+    if (e != hipSuccess) {
+      STROM_LOG(0, "hipMemcpyAsync failed: %s", hipGetErrorString(e));
+      free_slots.push_back(c.slot);
+      finish_request(r, -EIO);
+      return;
+    }
+    stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+    s.req = r;
+    s.t_copy_ns = now;
+    copying.push_back(c.slot);
+  }
+
+  // retire finished HBM copies; block on the oldest when `block`
+  void retire(bool block) {
+    while (!copying.empty()) {
+      Slot &s = slots[copying.front()];
+      hipError_t e = block ? hipEventSynchronize(s.ev) : hipEventQuery(s.ev);
+      if (e == hipErrorNotReady) return;
+      uint64_t dt = mono_ns() - s.t_copy_ns;
+      stats().copy_ns.add(dt);
+      stats().clk_debug[0].fetch_add(dt, std::memory_order_relaxed);
+      int si = copying.front();
+      copying.pop_front();
+      free_slots.push_back(si);
+      finish_request(s.req, e == hipSuccess ? 0 : -EIO);
+      block = false;
+    }
+  }
+
+  // start one request; false when it has to wait for a staging slot
+  bool start(IoReq &r, bool use_ring) {
+    int slot = -1;
+    uint8_t *dst = r.host_dst;
+    if (!dst) {
+      if (!ensure_slots()) {
+        finish_request(r, -ENOMEM);
+        return true;
+      }
+      if (free_slots.empty()) return false;
+      slot = free_slots.back();
+      free_slots.pop_back();
+      dst = slots[slot].buf;
+    }
+    uint32_t len = r.len;
+    int frc = faults().on_request(&len);
+    Ctx c;
+    c.req = r;
+    c.slot = slot;
+    c.dst = dst;
+    c.len = len;
+    c.t0 = mono_ns();
+    if (frc) {
+      on_read_done(c, frc);
+      return true;
+    }
+    if (use_ring) {
+      int ci;
+      if (free_ctx.empty()) {
+        ci = (int)ctx.size();
+        ctx.push_back(c);
+      } else {
+        ci = free_ctx.back();
+        free_ctx.pop_back();
+        ctx[ci] = c;
+      }
+      io_uring_sqe *sqe = ring.next_sqe();
+      if (!sqe) {  // ring full: flush and retry synchronously
+        ring.enter(0);
+        sqe = ring.next_sqe();
+      }
+      sqe->opcode = IORING_OP_READ;
+      sqe->fd = r.fd;
+      sqe->addr = (uint64_t)dst;
+      sqe->len = len;
+      sqe->off = r.off;
+      sqe->user_data = (uint64_t)ci;
+      ++reads_inflight;
+      return true;
+    }
+    long got = pread_full(r.fd, dst, len, r.off);
+    on_read_done(c, got);
+    return true;
+  }
+
+  void reap() {
+    io_uring_cqe cqe;
+    while (ring.peek(&cqe)) {
+      int ci = (int)cqe.user_data;
+      Ctx c = ctx[ci];
+      free_ctx.push_back(ci);
+      --reads_inflight;
+      long got = cqe.res;
+      if (got >= 0 && (uint32_t)got < c.len) {
+        // partial completion: finish the remainder synchronously
+        long more = pread_full(c.req.fd, c.dst + got, c.len - (uint32_t)got, c.req.off + got);
+        got = more < 0 ? more : got + more;
+      }
+      on_read_done(c, got);
+    }
+  }
+
+  void run() {
+    bind_numa();
+    bool use_ring = cfg.backend == BackendKind::kUring;
+    if (use_ring && ring.init((unsigned)std::max(8, cfg.queue_depth * 2)) != 0) use_ring = false;
+    int qd = use_ring ? cfg.queue_depth : 1;
+    std::deque<IoReq> local;
+    for (;;) {
+      if (local.empty()) {
+        std::unique_lock<std::mutex> g(mu);
+        if (q.empty() && reads_inflight == 0 && copying.empty()) {
+          if (stop) break;
+          cv.wait(g, [&] { return stop || !q.empty(); });
+        }
+        local.swap(q);
+      }
+      // issue as much as the queue depth and staging allow
+      bool blocked = false;
+      while (!local.empty() && reads_inflight < qd) {
+        if (!start(local.front(), use_ring)) {
+          blocked = true;
+          break;
+        }
+        local.pop_front();
+      }
+      if (use_ring && ring.pending()) ring.enter(0);
+      retire(false);
+      if (use_ring) reap();
+      if (!local.empty() && !blocked && reads_inflight < qd) continue;
+      // nothing more can start: wait for a read, a copy, or new work
+      if (reads_inflight > 0 && copying.empty()) {
+        ring.enter(1);
+        reap();
+      } else if (reads_inflight == 0 && !copying.empty()) {
+        if (local.empty()) {
+          std::lock_guard<std::mutex> g(mu);
+          if (!q.empty()) continue;
+        }
+        retire(true);
+      } else if (reads_inflight > 0) {
+        sched_yield();  // both pipes busy
+      }
+    }
+    for (auto &s : slots) {
+      if (s.ev) (void)hipEventDestroy(s.ev);
+      hip::host_free(s.buf);
+    }
+    for (auto st : streams)
+      if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+IoEngine::IoEngine(const Config &cfg) {
+  int node = -1;
+  if (cfg.numa_bind && hip::available()) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    node = hip::numa_node_of_device(dev);
+  }
+  for (int i = 0; i < cfg.workers; ++i) {
+    auto w = std::make_unique<Worker>();
+    w->idx = i;
+    w->cfg = cfg;
+    w->numa_node = node;
+    Worker *wp = w.get();
+    w->th = std::thread([wp] { wp->run(); });
+    workers_.push_back(std::move(w));
+  }
+}
+
+IoEngine::~IoEngine() {
+  for (auto &w : workers_) {
+    std::lock_guard<std::mutex> g(w->mu);
+    w->stop = true;
+    w->cv.notify_all();
+  }
+  for (auto &w : workers_) w->th.join();
+}
+
+void IoEngine::submit(std::vector<IoReq> &reqs) {
+  const size_t n = workers_.size();
+  if (reqs.empty()) return;
+  uint32_t start = rr_.fetch_add((uint32_t)reqs.size());
+  // contiguous runs per worker keep each ring's reads sequential
+  size_t per = (reqs.size() + n - 1) / n;
+  for (size_t k = 0; k < n; ++k) {
+    size_t lo = k * per, hi = std::min(reqs.size(), lo + per);
+    if (lo >= hi) break;
+    Worker &w = *workers_[(start + k) % n];
+    {
+      std::lock_guard<std::mutex> g(w.mu);
+      for (size_t i = lo; i < hi; ++i) w.q.push_back(reqs[i]);
+    }
+    w.cv.notify_one();
+  }
+}
+
+}  // namespace strom

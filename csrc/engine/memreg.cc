@@ -1,0 +1,230 @@
+// memreg.cc — GPU memory mapping registry and NUMA DMA buffers.
+//
+// GpuRegistry re-designs the reference's mapped_gpu_memory table
+// (kmod/pmemmap.c:33-495) for HIP: a mapping is a validated HBM range of a
+// hipMalloc allocation (hipPointerGetAttributes + hipMemGetAddressRange),
+// aligned down to the same 64 KiB granule, owned by the caller's euid.
+// Handles are opaque tagged counters (never kernel pointers).  UNMAP waits
+// for in-flight requests that target the range and then frees the record,
+// fixing reference defect #7 (pmemmap.c:375-388 never freed nor waited).
+// INFO returns per-page device addresses; the kmod fills bus addresses
+// from the imported dma-buf sg_table instead.
+//
+// DmaBufRegistry replaces the anon-inode DMA buffer (pmemmap.c:497-717):
+// a memfd named "strom-dmabuf<node>:<size>", whose shared NUMA policy is
+// bound to the requested node and whose pages are pre-faulted there.  The
+// SSD2RAM destination check is the find_vma()/f_op test re-done against
+// /proc/self/maps: the address range must lie inside a mapping of one of
+// our memfds, and the byte offset is vm_pgoff + (uaddr - vm_start).
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <sstream>
+
+#include "engine.h"
+
+#ifndef MPOL_BIND
+#define MPOL_BIND 2
+#endif
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+
+namespace strom {
+
+// ------------------------------------------------------- GPU registry
+int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memory *out) {
+  if (va == 0 || len == 0) return -EINVAL;
+  if (va + len < va) return -EINVAL;
+  int device = -1;
+  uint64_t abase = 0;
+  size_t asize = 0;
+  if (hip::available()) device = hip::pointer_device(va, &abase, &asize);
+  if (device >= 0) {
+    if (asize && (va < abase || va + len > abase + asize)) return -ERANGE;
+  } else if (!config().gpu_emulation) {
+    return -EINVAL;  // not device memory
+  }
+  auto m = std::make_shared<GpuMapping>();
+  m->va = va;
+  m->base = va & ~(uint64_t)(STROM_GPU_BOUND_SIZE - 1);
+  m->map_offset = va - m->base;
+  m->length = len;
+  m->map_length = m->map_offset + len;
+  m->device = device;
+  m->owner = geteuid();
+  m->dmabuf_fd = dmabuf_fd;
+  uint64_t npages = (m->map_length + STROM_GPU_BOUND_SIZE - 1) >> STROM_GPU_BOUND_SHIFT;
+  if (npages > 0xffffffffull) return -E2BIG;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    m->handle = ++next_;
+    maps_.emplace(m->handle, m);
+  }
+  out->handle = m->handle;
+  out->gpu_page_sz = (uint32_t)STROM_GPU_BOUND_SIZE;
+  out->gpu_npages = (uint32_t)npages;
+  STROM_LOG(1, "map va=%#lx len=%zu dev=%d handle=%#lx", (unsigned long)va, len, device,
+            m->handle);
+  return 0;
+}
+
+std::shared_ptr<GpuMapping> GpuRegistry::get(unsigned long handle) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = maps_.find(handle);
+  if (it == maps_.end() || it->second->owner != geteuid()) return nullptr;
+  return it->second;
+}
+
+int GpuRegistry::unmap(unsigned long handle) {
+  std::shared_ptr<GpuMapping> m;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = maps_.find(handle);
+    if (it == maps_.end()) return -ENOENT;
+    if (it->second->owner != geteuid()) return -EACCES;
+    m = it->second;
+    maps_.erase(it);
+  }
+  // wait for in-flight DMA targeting the range (free-callback semantics)
+  std::unique_lock<std::mutex> g(m->mu);
+  m->cv.wait(g, [&] { return m->inflight.load() == 0; });
+  m->detached = true;
+  return 0;
+}
+
+int GpuRegistry::list(strom_list_gpu_memory *out) {
+  std::lock_guard<std::mutex> g(mu_);
+  uint32_t n = 0;
+  uid_t me = geteuid();
+  for (auto &kv : maps_) {
+    if (kv.second->owner != me) continue;
+    if (n < out->nrooms) out->handles[n] = kv.first;
+    ++n;
+  }
+  out->nitems = n;
+  return 0;
+}
+
+int GpuRegistry::info(strom_info_gpu_memory *out) {
+  auto m = get(out->handle);
+  if (!m) return -ENOENT;
+  uint32_t npages =
+      (uint32_t)((m->map_length + STROM_GPU_BOUND_SIZE - 1) >> STROM_GPU_BOUND_SHIFT);
+  out->nitems = npages;
+  out->version = m->version;
+  out->gpu_page_sz = (uint32_t)STROM_GPU_BOUND_SIZE;
+  out->owner = (uint32_t)m->owner;
+  out->map_offset = m->map_offset;
+  out->map_length = m->map_length;
+  for (uint32_t i = 0; i < npages && i < out->nrooms; ++i)
+    out->paddrs[i] = m->base + (uint64_t)i * STROM_GPU_BOUND_SIZE;
+  return 0;
+}
+
+GpuRegistry &gpu_registry() {
+  static GpuRegistry r;
+  return r;
+}
+
+// ---------------------------------------------------------- DMA buffers
+DmaBuffer::~DmaBuffer() {
+  if (self_map) munmap(self_map, length);
+  if (fd >= 0) close(fd);
+}
+
+int DmaBufRegistry::alloc(size_t length, int node, int *user_fd) {
+  if (length == 0) return -EINVAL;
+  size_t len = (length + STROM_DMABUF_SEGMENT - 1) / STROM_DMABUF_SEGMENT * STROM_DMABUF_SEGMENT;
+  char name[64];
+  snprintf(name, sizeof name, "strom-dmabuf%d:%zu", node, len);
+  int fd = (int)syscall(SYS_memfd_create, name, 0u);
+  if (fd < 0) return -errno;
+  if (ftruncate(fd, (off_t)len) != 0) {
+    int e = errno;
+    close(fd);
+    return -e;
+  }
+  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) {
+    int e = errno;
+    close(fd);
+    return -e;
+  }
+  if (node >= 0) {
+    unsigned long mask[16] = {0};
+    if (node < 1024) {
+      mask[node / 64] = 1ul << (node % 64);
+      // shared policy lives in the shmem inode: every mapping inherits it
+      if (syscall(SYS_mbind, p, len, MPOL_BIND, mask, 1024ul, 0u) != 0)
+        STROM_LOG(1, "mbind(node=%d) failed: %s", node, strerror(errno));
+    }
+  }
+  if (madvise(p, len, MADV_POPULATE_WRITE) != 0) {
+    for (size_t off = 0; off < len; off += 4096) ((volatile char *)p)[off] = 0;
+  }
+  munmap(p, len);  // pages stay with the memfd; the user's fd owns them
+  struct stat st;
+  fstat(fd, &st);
+  auto b = std::make_shared<DmaBuffer>();
+  b->dev = st.st_dev;
+  b->ino = st.st_ino;
+  b->length = len;
+  b->node = node;
+  int ufd = fd;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    bufs_[{b->dev, b->ino}] = b;
+  }
+  *user_fd = ufd;
+  return 0;
+}
+
+int DmaBufRegistry::resolve(const void *uaddr, size_t len, std::shared_ptr<DmaBuffer> *buf,
+                            size_t *offset) {
+  uint64_t a = (uint64_t)uaddr;
+  FILE *f = fopen("/proc/self/maps", "r");
+  if (!f) return -errno;
+  char line[4096];
+  int rc = -EINVAL;
+  while (fgets(line, sizeof line, f)) {
+    unsigned long lo, hi, off, ino;
+    unsigned dmaj, dmin;
+    char perms[8];
+    int pos = 0;
+    if (sscanf(line, "%lx-%lx %7s %lx %x:%x %lu %n", &lo, &hi, perms, &off, &dmaj, &dmin, &ino,
+               &pos) < 7)
+      continue;
+    if (a < lo || a >= hi) continue;
+    const char *path = line + pos;
+    if (!strstr(path, "strom-dmabuf")) break;        // wrong kind of mapping
+    if (a + len > hi) break;                         // crosses the VMA end
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto &kv : bufs_) {
+      if (kv.first.second != (ino_t)ino) continue;
+      size_t o = off + (a - lo);
+      if (o + len > kv.second->length) break;
+      *buf = kv.second;
+      *offset = o;
+      rc = 0;
+      break;
+    }
+    break;
+  }
+  fclose(f);
+  return rc;
+}
+
+DmaBufRegistry &dmabuf_registry() {
+  static DmaBufRegistry r;
+  return r;
+}
+
+}  // namespace strom

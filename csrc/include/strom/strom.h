@@ -1,0 +1,145 @@
+/*
+ * strom/strom.h — C ABI of libstrom, the MI355X-native direct-storage
+ * engine.  Everything a client needs: the ioctl-compatible entry points
+ * (sessions stand in for open file descriptors on /proc/nvme-strom), engine
+ * configuration, and the CDNA4 post-read kernels (verify, reorder, scan,
+ * decompress, filter) that run on HBM-resident data.
+ *
+ * Return convention: 0 or a non-negative count on success, -errno on error
+ * (never sets errno) — except nvme_strom_ioctl(), which mimics ioctl(2).
+ */
+#ifndef STROM_STROM_H
+#define STROM_STROM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "strom/uapi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- sessions + dispatch ---------------------------------------------- */
+const char *strom_version(void);
+/* 0 = userspace engine, 1 = kernel module (/proc or /dev node present). */
+int strom_provider(void);
+int strom_open(void);                    /* new session id (> 0) */
+int strom_close(int session);            /* reclaims failed tasks: count */
+int strom_ioctl(int session, unsigned long cmd, void *arg);
+/* v0.6-style wrapper (utils_common.h): lazily opened per-thread session,
+ * returns 0 / -1 with errno set. */
+int nvme_strom_ioctl(unsigned long cmd, const void *arg);
+
+/* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
+int strom_config_set(const char *key, const char *value);
+int strom_config_get(const char *key, char *buf, size_t buflen);
+/* Tear the engine down (waits for in-flight I/O); next call re-creates it
+ * with the current configuration. */
+int strom_engine_reset(void);
+
+/* ---- fault injection (fake + real backends; CPU tests) ---------------- */
+/* Fail the n-th storage request after this call (1-based) with -err; 0
+ * disables.  short_at makes the n-th request read `short_bytes` less. */
+int strom_fault_inject(long fail_at, int err, long short_at, int short_bytes,
+                       int delay_us);
+
+/* ---- host helpers ------------------------------------------------------ */
+/* Bytes of a file range resident in the page cache (mincore). */
+long strom_resident_bytes(int fd, uint64_t offset, uint64_t length);
+/* Drop clean page-cache pages of a file (posix_fadvise DONTNEED). */
+int strom_evict_file(int fd);
+/* CRC32C (Castagnoli) on the host, same convention as the GPU kernels. */
+uint32_t strom_crc32c_host(uint32_t crc, const void *buf, size_t len);
+/* md raid0 remap for a described geometry (tests + kmod parity). */
+int strom_raid0_map(const uint64_t *zone_end, const uint64_t *zone_dev_start,
+                    const int *zone_nb_dev, int nzones,
+                    uint32_t chunk_sects, const uint64_t *data_offset,
+                    int raid_disks, uint64_t sector, uint32_t nr_sects,
+                    int *member, uint64_t *member_sector);
+/* Host LZ4 / snappy block codecs (test-data generation + CPU reference). */
+long strom_lz4_compress_host(const void *src, size_t n, void *dst, size_t cap);
+long strom_lz4_decompress_host(const void *src, size_t n, void *dst, size_t cap);
+long strom_snappy_compress_host(const void *src, size_t n, void *dst, size_t cap);
+long strom_snappy_decompress_host(const void *src, size_t n, void *dst, size_t cap);
+
+/* ---- CDNA4 kernels (device pointers, hipStream_t passed as void*) ----- */
+int strom_gpu_count(void);
+/* Per-chunk CRC32C: out[i] = crc32c(in + i*chunk, min(chunk, n - i*chunk)). */
+int strom_crc32c_chunks(const void *d_in, uint64_t nbytes, uint32_t chunk,
+                        uint32_t *d_out, void *stream);
+/* Fold per-chunk CRCs (equal chunk sizes, last may be short) into the CRC
+ * of the whole buffer; d_out is one u32. */
+int strom_crc32c_combine(const uint32_t *d_crcs, uint32_t nchunks,
+                         uint32_t chunk, uint64_t nbytes, uint32_t *d_out,
+                         void *stream);
+/* Chunk scatter: dst + pos[i]*chunk <- src + i*chunk, i < n. */
+int strom_chunk_scatter(const void *d_src, void *d_dst, const uint32_t *d_pos,
+                        uint32_t n, uint32_t chunk, void *stream);
+/* Chunk gather: dst + i*chunk <- src + idx[i]*chunk. */
+int strom_chunk_gather(const void *d_src, void *d_dst, const uint32_t *d_idx,
+                       uint32_t n, uint32_t chunk, void *stream);
+/* Compare against a 32-bit pattern / a reference buffer: out[0] = mismatching
+ * 4-byte words, out[1] = first mismatching byte offset (or ~0). */
+int strom_verify_pattern(const void *d_buf, uint64_t nbytes, uint32_t pattern,
+                         uint64_t *d_out, void *stream);
+int strom_verify_equal(const void *d_a, const void *d_b, uint64_t nbytes,
+                       uint64_t *d_out, void *stream);
+int strom_fill_pattern(void *d_buf, uint64_t nbytes, uint32_t pattern,
+                       void *stream);
+
+/* PostgreSQL heap pages (8 KiB by default). */
+struct strom_heap_scan_args {
+	const void *pages;       /* device: npages * page_sz bytes */
+	uint32_t npages;
+	uint32_t page_sz;
+	uint32_t flags;          /* STROM_HEAP_* */
+	int32_t  attr_off;       /* byte offset of the filtered int column in
+	                            tuple data (after t_hoff), -1 = no filter */
+	int32_t  attr_width;     /* 4 or 8 */
+	int64_t  lo, hi;         /* keep rows with lo <= v <= hi */
+	uint32_t *out_items;     /* device: (page << 16) | lineno, capacity below */
+	uint32_t out_cap;
+	uint32_t *out_count;     /* device: u32[1], total qualifying */
+	uint32_t *page_status;   /* device: per page bitfield (STROM_PAGE_*) */
+	uint32_t blkno_base;     /* block number of page 0 (checksum input) */
+};
+#define STROM_HEAP_VERIFY_CHECKSUM 1u
+#define STROM_HEAP_SKIP_INVISIBLE  2u   /* honour xmin/xmax hint bits */
+#define STROM_PAGE_BAD_HEADER  1u
+#define STROM_PAGE_BAD_CHECKSUM 2u
+#define STROM_PAGE_EMPTY       4u
+int strom_heap_scan(const struct strom_heap_scan_args *a, void *stream);
+uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
+                                uint32_t page_sz);
+
+/* LZ4 / snappy raw-block batch decode: one block per wavefront. */
+struct strom_decomp_desc {
+	uint64_t src_off;      /* into d_src */
+	uint64_t dst_off;      /* into d_dst */
+	uint32_t src_len;
+	uint32_t dst_len;      /* exact decoded size (or capacity) */
+};
+#define STROM_CODEC_LZ4    1
+#define STROM_CODEC_SNAPPY 2
+#define STROM_CODEC_COPY   3   /* stored block */
+int strom_decompress(int codec, const void *d_src, void *d_dst,
+                     const struct strom_decomp_desc *d_desc, uint32_t nblocks,
+                     int32_t *d_status, void *stream);
+
+/* Columnar filter: bitmap[i/64] bit i%64 = valid(i) && lo <= v[i] <= hi. */
+#define STROM_COL_I32 1
+#define STROM_COL_I64 2
+#define STROM_COL_F32 3
+#define STROM_COL_F64 4
+int strom_column_filter(int type, const void *d_values, const uint8_t *d_valid,
+                        uint64_t n, double lo, double hi, uint64_t *d_bitmap,
+                        uint64_t *d_count, void *stream);
+/* Compact selected row indices from a bitmap (stable order). */
+int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n,
+                            uint32_t *d_out, uint64_t *d_count, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STROM_STROM_H */

@@ -1,0 +1,194 @@
+// copyops.hip — chunk scatter/gather, verify and fill on HBM.
+//
+// chunk_scatter restores file order after MEMCPY_SSD2GPU, which lands
+// storage chunks packed from the head and page-cache chunks at the tail
+// and rewrites chunk_ids to that landing order (reference
+// kmod/nvme_strom.c:1546-1571).  With pos[i] = the file-order slot of
+// landed chunk i, dst[pos[i]] = src[i].  The reference's own benchmark got
+// this mapping wrong (SURVEY §4 defects #1-#2); here it is one kernel.
+//
+// Streaming copies: 16 B per lane (global_load/store_dwordx4), 4 loads in
+// flight per lane, one 256-thread workgroup per chunk (grid-stride).
+// verify_* replace the DtoH + memcmp of nvme_test -c
+// (utils/nvme_test.c:226-267) with a device-side count + first offset.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "strom/strom.h"
+
+namespace {
+
+__device__ __forceinline__ void copy_chunk(const uint4 *__restrict__ s, uint4 *__restrict__ d,
+                                           uint32_t nvec) {
+  uint32_t i = threadIdx.x;
+  for (; i + 3 * 256 < nvec; i += 4 * 256) {
+    uint4 a = s[i], b = s[i + 256], c = s[i + 512], e = s[i + 768];
+    d[i] = a;
+    d[i + 256] = b;
+    d[i + 512] = c;
+    d[i + 768] = e;
+  }
+  for (; i < nvec; i += 256) d[i] = s[i];
+}
+
+__global__ __launch_bounds__(256) void chunk_scatter_kernel(const uint8_t *__restrict__ src,
+                                                            uint8_t *__restrict__ dst,
+                                                            const uint32_t *__restrict__ pos,
+                                                            uint32_t n, uint32_t chunk) {
+  const uint32_t nvec = chunk / 16;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    copy_chunk((const uint4 *)(src + (uint64_t)i * chunk),
+               (uint4 *)(dst + (uint64_t)pos[i] * chunk), nvec);
+  }
+}
+
+__global__ __launch_bounds__(256) void chunk_gather_kernel(const uint8_t *__restrict__ src,
+                                                           uint8_t *__restrict__ dst,
+                                                           const uint32_t *__restrict__ idx,
+                                                           uint32_t n, uint32_t chunk) {
+  const uint32_t nvec = chunk / 16;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    copy_chunk((const uint4 *)(src + (uint64_t)idx[i] * chunk),
+               (uint4 *)(dst + (uint64_t)i * chunk), nvec);
+  }
+}
+
+__device__ __forceinline__ void report(uint64_t bad, uint64_t first, uint64_t *out) {
+  // wave reduce, then one atomic pair per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    bad += __shfl_xor(bad, o, 64);
+    uint64_t f2 = __shfl_xor(first, o, 64);
+    first = f2 < first ? f2 : first;
+  }
+  if ((threadIdx.x & 63) == 0 && bad) {
+    atomicAdd((unsigned long long *)&out[0], (unsigned long long)bad);
+    atomicMin((unsigned long long *)&out[1], (unsigned long long)first);
+  }
+}
+
+__global__ __launch_bounds__(256) void verify_pattern_kernel(const uint32_t *__restrict__ buf,
+                                                             uint64_t nwords, uint32_t pat,
+                                                             uint64_t *out) {
+  uint64_t bad = 0, first = ~0ull;
+  const uint64_t nvec = nwords / 4;
+  const uint4 *v = (const uint4 *)buf;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256) {
+    uint4 w = v[i];
+    uint32_t m = (w.x != pat) | ((w.y != pat) << 1) | ((w.z != pat) << 2) | ((w.w != pat) << 3);
+    if (m) {
+      bad += __popc(m);
+      uint64_t f = i * 16 + 4 * (__ffs(m) - 1);
+      first = f < first ? f : first;
+    }
+  }
+  for (uint64_t i = nvec * 4 + blockIdx.x * 256ull + threadIdx.x; i < nwords;
+       i += (uint64_t)gridDim.x * 256) {
+    if (buf[i] != pat) {
+      ++bad;
+      first = i * 4 < first ? i * 4 : first;
+    }
+  }
+  report(bad, first, out);
+}
+
+__global__ __launch_bounds__(256) void verify_equal_kernel(const uint32_t *__restrict__ a,
+                                                           const uint32_t *__restrict__ b,
+                                                           uint64_t nwords, uint64_t *out) {
+  uint64_t bad = 0, first = ~0ull;
+  const uint64_t nvec = nwords / 4;
+  const uint4 *va = (const uint4 *)a, *vb = (const uint4 *)b;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256) {
+    uint4 x = va[i], y = vb[i];
+    uint32_t m = (x.x != y.x) | ((x.y != y.y) << 1) | ((x.z != y.z) << 2) | ((x.w != y.w) << 3);
+    if (m) {
+      bad += __popc(m);
+      uint64_t f = i * 16 + 4 * (__ffs(m) - 1);
+      first = f < first ? f : first;
+    }
+  }
+  for (uint64_t i = nvec * 4 + blockIdx.x * 256ull + threadIdx.x; i < nwords;
+       i += (uint64_t)gridDim.x * 256) {
+    if (a[i] != b[i]) {
+      ++bad;
+      first = i * 4 < first ? i * 4 : first;
+    }
+  }
+  report(bad, first, out);
+}
+
+__global__ __launch_bounds__(256) void fill_kernel(uint32_t *__restrict__ buf, uint64_t nwords,
+                                                   uint32_t pat) {
+  const uint64_t nvec = nwords / 4;
+  uint4 p = make_uint4(pat, pat, pat, pat);
+  uint4 *v = (uint4 *)buf;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256)
+    v[i] = p;
+  for (uint64_t i = nvec * 4 + blockIdx.x * 256ull + threadIdx.x; i < nwords;
+       i += (uint64_t)gridDim.x * 256)
+    buf[i] = pat;
+}
+
+__global__ void report_init_kernel(uint64_t *out) {
+  out[0] = 0;
+  out[1] = ~0ull;
+}
+
+inline uint32_t grid_for(uint64_t items, uint32_t per_block) {
+  uint64_t g = (items + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (uint32_t)(g > 4096 ? 4096 : g);
+}
+
+inline int launched() { return hipGetLastError() == hipSuccess ? 0 : -5; }
+
+}  // namespace
+
+extern "C" int strom_chunk_scatter(const void *d_src, void *d_dst, const uint32_t *d_pos,
+                                   uint32_t n, uint32_t chunk, void *stream) {
+  if (!n) return 0;
+  if ((chunk & 15) || ((uintptr_t)d_src & 15) || ((uintptr_t)d_dst & 15)) return -22;
+  hipLaunchKernelGGL(chunk_scatter_kernel, dim3(grid_for(n, 1)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint8_t *)d_src, (uint8_t *)d_dst, d_pos, n,
+                     chunk);
+  return launched();
+}
+
+extern "C" int strom_chunk_gather(const void *d_src, void *d_dst, const uint32_t *d_idx,
+                                  uint32_t n, uint32_t chunk, void *stream) {
+  if (!n) return 0;
+  if ((chunk & 15) || ((uintptr_t)d_src & 15) || ((uintptr_t)d_dst & 15)) return -22;
+  hipLaunchKernelGGL(chunk_gather_kernel, dim3(grid_for(n, 1)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint8_t *)d_src, (uint8_t *)d_dst, d_idx, n,
+                     chunk);
+  return launched();
+}
+
+extern "C" int strom_verify_pattern(const void *d_buf, uint64_t nbytes, uint32_t pattern,
+                                    uint64_t *d_out, void *stream) {
+  if (((uintptr_t)d_buf & 15) || (nbytes & 3)) return -22;
+  hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, d_out);
+  uint64_t nw = nbytes / 4;
+  hipLaunchKernelGGL(verify_pattern_kernel, dim3(grid_for(nw / 4 + 1, 256 * 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint32_t *)d_buf, nw, pattern, d_out);
+  return launched();
+}
+
+extern "C" int strom_verify_equal(const void *d_a, const void *d_b, uint64_t nbytes,
+                                  uint64_t *d_out, void *stream) {
+  if (((uintptr_t)d_a & 15) || ((uintptr_t)d_b & 15) || (nbytes & 3)) return -22;
+  hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, d_out);
+  uint64_t nw = nbytes / 4;
+  hipLaunchKernelGGL(verify_equal_kernel, dim3(grid_for(nw / 4 + 1, 256 * 4)), dim3(256), 0,
+                     (hipStream_t)stream, (const uint32_t *)d_a, (const uint32_t *)d_b, nw,
+                     d_out);
+  return launched();
+}
+
+extern "C" int strom_fill_pattern(void *d_buf, uint64_t nbytes, uint32_t pattern, void *stream) {
+  if (((uintptr_t)d_buf & 15) || (nbytes & 3)) return -22;
+  uint64_t nw = nbytes / 4;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(nw / 4 + 1, 256 * 4)), dim3(256), 0,
+                     (hipStream_t)stream, (uint32_t *)d_buf, nw, pattern);
+  return launched();
+}

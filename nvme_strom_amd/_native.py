@@ -1,0 +1,216 @@
+"""ctypes binding of libstrom (csrc/, built by ``make`` / ``nvme_strom_amd.build``).
+
+The argument blocks below are the x86-64 layouts of ``csrc/include/strom/uapi.h``
+(byte-compatible with the reference's ``kmod/nvme_strom.h:33-165``); the ABI
+test (tests/test_abi.py) checks them against the C static assertions.
+
+The library is always loaded from the package tree (``nvme_strom_amd/lib``)
+and loading fails loudly when it is missing: there is no pure-Python
+fallback for anything that claims to run native code.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(_LIB_DIR, "libstrom.so")
+
+# ---------------------------------------------------------------- ioctl codes
+def _IO(t: str, nr: int) -> int:
+    return (ord(t) << 8) | nr
+
+
+CHECK_FILE = _IO("S", 0x80)
+MAP_GPU_MEMORY = _IO("S", 0x81)
+UNMAP_GPU_MEMORY = _IO("S", 0x82)
+LIST_GPU_MEMORY = _IO("S", 0x83)
+INFO_GPU_MEMORY = _IO("S", 0x84)
+ALLOC_DMA_BUFFER = _IO("S", 0x85)
+MAP_GPU_DMABUF = _IO("S", 0x86)
+MEMCPY_SSD2GPU = _IO("S", 0x90)
+MEMCPY_SSD2RAM = _IO("S", 0x91)
+MEMCPY_WAIT = _IO("S", 0x92)
+MEMCPY_WAIT_TIMED = _IO("S", 0x93)
+STAT_INFO = _IO("S", 0x99)
+STAT_HIST = _IO("S", 0x9A)
+
+GPU_BOUND_SIZE = 1 << 16
+HIST_BUCKETS = 48
+
+
+# ------------------------------------------------------------- arg structs
+class CheckFile(C.Structure):
+    _fields_ = [("fdesc", C.c_int), ("numa_node_id", C.c_int), ("support_dma64", C.c_int)]
+
+
+class MapGpuMemory(C.Structure):
+    _fields_ = [("handle", C.c_ulong), ("gpu_page_sz", C.c_uint32), ("gpu_npages", C.c_uint32),
+                ("vaddress", C.c_uint64), ("length", C.c_size_t)]
+
+
+class MapGpuDmabuf(C.Structure):
+    _fields_ = [("handle", C.c_ulong), ("gpu_page_sz", C.c_uint32), ("gpu_npages", C.c_uint32),
+                ("dmabuf_fd", C.c_int), ("device_id", C.c_int), ("vaddress", C.c_uint64),
+                ("length", C.c_size_t)]
+
+
+class UnmapGpuMemory(C.Structure):
+    _fields_ = [("handle", C.c_ulong)]
+
+
+def list_gpu_memory_struct(nrooms: int):
+    class ListGpuMemory(C.Structure):
+        _fields_ = [("nrooms", C.c_uint32), ("nitems", C.c_uint32),
+                    ("handles", C.c_ulong * max(1, nrooms))]
+    return ListGpuMemory
+
+
+def info_gpu_memory_struct(nrooms: int):
+    class InfoGpuMemory(C.Structure):
+        _fields_ = [("handle", C.c_ulong), ("nrooms", C.c_uint32), ("nitems", C.c_uint32),
+                    ("version", C.c_uint32), ("gpu_page_sz", C.c_uint32), ("owner", C.c_uint32),
+                    ("map_offset", C.c_ulong), ("map_length", C.c_ulong),
+                    ("paddrs", C.c_uint64 * max(1, nrooms))]
+    return InfoGpuMemory
+
+
+ListGpuMemory = list_gpu_memory_struct(1)
+InfoGpuMemory = info_gpu_memory_struct(1)
+
+
+class MemCopySsdToGpu(C.Structure):
+    _fields_ = [("dma_task_id", C.c_ulong), ("nr_ram2gpu", C.c_uint), ("nr_ssd2gpu", C.c_uint),
+                ("nr_dma_submit", C.c_uint), ("nr_dma_blocks", C.c_uint), ("handle", C.c_ulong),
+                ("offset", C.c_size_t), ("file_desc", C.c_int), ("nr_chunks", C.c_uint),
+                ("chunk_sz", C.c_uint), ("relseg_sz", C.c_uint),
+                ("chunk_ids", C.POINTER(C.c_uint32)), ("wb_buffer", C.c_void_p)]
+
+
+class MemCopyWait(C.Structure):
+    _fields_ = [("dma_task_id", C.c_ulong), ("status", C.c_long)]
+
+
+class MemCopyWaitTimed(C.Structure):
+    _fields_ = [("dma_task_id", C.c_ulong), ("status", C.c_long), ("timeout_ns", C.c_uint64)]
+
+
+class MemCopySsdToRam(C.Structure):
+    _fields_ = [("dma_task_id", C.c_ulong), ("nr_ram2ram", C.c_uint), ("nr_ssd2ram", C.c_uint),
+                ("nr_dma_submit", C.c_uint), ("nr_dma_blocks", C.c_uint),
+                ("dest_uaddr", C.c_void_p), ("file_desc", C.c_int), ("nr_chunks", C.c_uint),
+                ("chunk_sz", C.c_uint), ("relseg_sz", C.c_uint),
+                ("chunk_ids", C.POINTER(C.c_uint32))]
+
+
+class AllocDMABuffer(C.Structure):
+    _fields_ = [("length", C.c_size_t), ("node_id", C.c_int), ("dmabuf_fdesc", C.c_int)]
+
+
+class StatInfo(C.Structure):
+    _fields_ = [("version", C.c_uint), ("has_debug", C.c_ubyte), ("tsc", C.c_uint64)] + [
+        (n, C.c_uint64) for n in (
+            "nr_ssd2gpu", "clk_ssd2gpu", "nr_setup_prps", "clk_setup_prps", "nr_submit_dma",
+            "clk_submit_dma", "nr_wait_dtask", "clk_wait_dtask", "nr_wrong_wakeup",
+            "cur_dma_count", "max_dma_count", "nr_debug1", "clk_debug1", "nr_debug2",
+            "clk_debug2", "nr_debug3", "clk_debug3", "nr_debug4", "clk_debug4")]
+
+
+class StatHist(C.Structure):
+    _fields_ = [("version", C.c_uint), ("reset", C.c_uint),
+                ("io_ns", C.c_uint64 * HIST_BUCKETS), ("copy_ns", C.c_uint64 * HIST_BUCKETS),
+                ("task_ns", C.c_uint64 * HIST_BUCKETS)]
+
+
+class HeapScanArgs(C.Structure):
+    _fields_ = [("pages", C.c_void_p), ("npages", C.c_uint32), ("page_sz", C.c_uint32),
+                ("flags", C.c_uint32), ("attr_off", C.c_int32), ("attr_width", C.c_int32),
+                ("lo", C.c_int64), ("hi", C.c_int64), ("out_items", C.c_void_p),
+                ("out_cap", C.c_uint32), ("out_count", C.c_void_p), ("page_status", C.c_void_p),
+                ("blkno_base", C.c_uint32)]
+
+
+class DecompDesc(C.Structure):
+    _fields_ = [("src_off", C.c_uint64), ("dst_off", C.c_uint64), ("src_len", C.c_uint32),
+                ("dst_len", C.c_uint32)]
+
+
+# ----------------------------------------------------------------- loading
+_lib = None
+_lock = threading.Lock()
+
+_SIGS = {
+    "strom_version": (C.c_char_p, []),
+    "strom_provider": (C.c_int, []),
+    "strom_open": (C.c_int, []),
+    "strom_close": (C.c_int, [C.c_int]),
+    "strom_ioctl": (C.c_int, [C.c_int, C.c_ulong, C.c_void_p]),
+    "nvme_strom_ioctl": (C.c_int, [C.c_ulong, C.c_void_p]),
+    "strom_config_set": (C.c_int, [C.c_char_p, C.c_char_p]),
+    "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "strom_engine_reset": (C.c_int, []),
+    "strom_fault_inject": (C.c_int, [C.c_long, C.c_int, C.c_long, C.c_int, C.c_int]),
+    "strom_resident_bytes": (C.c_long, [C.c_int, C.c_uint64, C.c_uint64]),
+    "strom_evict_file": (C.c_int, [C.c_int]),
+    "strom_crc32c_host": (C.c_uint32, [C.c_uint32, C.c_void_p, C.c_size_t]),
+    "strom_raid0_map": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_int), C.c_int, C.c_uint32,
+                                  C.POINTER(C.c_uint64), C.c_int, C.c_uint64, C.c_uint32,
+                                  C.POINTER(C.c_int), C.POINTER(C.c_uint64)]),
+    "strom_lz4_compress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
+    "strom_lz4_decompress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
+    "strom_snappy_compress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
+    "strom_snappy_decompress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
+    "strom_pg_checksum_host": (C.c_uint16, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "strom_gpu_count": (C.c_int, []),
+    "strom_crc32c_chunks": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "strom_crc32c_combine": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,
+                                       C.c_void_p, C.c_void_p]),
+    "strom_chunk_scatter": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                      C.c_uint32, C.c_void_p]),
+    "strom_chunk_gather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.c_uint32, C.c_void_p]),
+    "strom_verify_pattern": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p,
+                                       C.c_void_p]),
+    "strom_verify_equal": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                     C.c_void_p]),
+    "strom_fill_pattern": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
+    "strom_heap_scan": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p]),
+    "strom_decompress": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                   C.c_void_p, C.c_void_p]),
+    "strom_column_filter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_double,
+                                      C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "strom_bitmap_to_indices": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]),
+}
+
+
+class NativeMissing(ImportError):
+    pass
+
+
+def lib():
+    """Load libstrom.so from the package tree (raises NativeMissing if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeMissing(
+                f"{LIB_PATH} not built: run `make -j16` or `python -m nvme_strom_amd.build`")
+        handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+        return _lib
+
+
+def has(name: str) -> bool:
+    return getattr(lib(), name, None) is not None

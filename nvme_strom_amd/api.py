@@ -1,0 +1,331 @@
+"""Pythonic surface over the ioctl ABI.
+
+One call per reference ioctl (kmod/nvme_strom.h:17-28): ``check_file``,
+``map_gpu_memory`` / ``unmap_gpu_memory`` / ``list_gpu_memory`` /
+``info_gpu_memory``, ``alloc_dma_buffer``, ``memcpy_ssd2gpu``,
+``memcpy_ssd2ram``, ``memcpy_wait`` and ``stat_info``, plus the MI355X
+additions (timed wait, latency histograms, dma-buf mapping).  Errors come
+back as :class:`StromError` carrying the errno and, for WAIT, the device
+status of the failed task.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import errno as _errno
+import mmap
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native as N
+
+
+class StromError(OSError):
+    def __init__(self, err: int, what: str, status: int = 0):
+        super().__init__(err, f"{what}: {os.strerror(err)}" + (f" (status {status})" if status else ""))
+        self.status = status
+
+
+def _check(rc: int, what: str, status: int = 0) -> int:
+    if rc < 0:
+        raise StromError(-rc, what, status)
+    return rc
+
+
+# ----------------------------------------------------------------- sessions
+class Session:
+    """Equivalent of one open file descriptor on /proc/nvme-strom.
+
+    Closing a session reclaims the records of failed tasks nobody waited
+    for (reference strom_proc_release, kmod/nvme_strom.c:2064-2091).
+    """
+
+    def __init__(self):
+        self.lib = N.lib()
+        self.sid = _check(self.lib.strom_open(), "strom_open")
+        self.closed = False
+
+    def ioctl(self, cmd: int, arg, what: str = "ioctl") -> int:
+        rc = self.lib.strom_ioctl(self.sid, cmd, C.byref(arg))
+        return _check(rc, what)
+
+    def ioctl_rc(self, cmd: int, arg) -> int:
+        return self.lib.strom_ioctl(self.sid, cmd, C.byref(arg))
+
+    def close(self) -> int:
+        if self.closed:
+            return 0
+        self.closed = True
+        return self.lib.strom_close(self.sid)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+_default: Optional[Session] = None
+
+
+def session() -> Session:
+    global _default
+    if _default is None or _default.closed:
+        _default = Session()
+    return _default
+
+
+# ------------------------------------------------------------- config etc.
+def version() -> str:
+    return N.lib().strom_version().decode()
+
+
+def provider() -> str:
+    return "kernel" if N.lib().strom_provider() == 1 else "userspace"
+
+
+def config_set(key: str, value) -> None:
+    if isinstance(value, bool):
+        value = int(value)
+    _check(N.lib().strom_config_set(key.encode(), str(value).encode()), f"config {key}")
+
+
+def config_get(key: str) -> str:
+    buf = C.create_string_buffer(64)
+    _check(N.lib().strom_config_get(key.encode(), buf, 64), f"config {key}")
+    return buf.value.decode()
+
+
+def configure(reset: bool = True, **kv) -> None:
+    """Set several engine knobs; restarts the I/O workers by default."""
+    for k, v in kv.items():
+        config_set(k, v)
+    if reset:
+        engine_reset()
+
+
+def engine_reset() -> None:
+    N.lib().strom_engine_reset()
+
+
+def fault_inject(fail_at: int = 0, err: int = _errno.EIO, short_at: int = 0,
+                 short_bytes: int = 0, delay_us: int = 0) -> None:
+    N.lib().strom_fault_inject(fail_at, err, short_at, short_bytes, delay_us)
+
+
+def resident_bytes(fd: int, offset: int = 0, length: int = 1 << 62) -> int:
+    return _check(N.lib().strom_resident_bytes(fd, offset, length), "resident_bytes")
+
+
+def evict_file(fd: int) -> None:
+    _check(N.lib().strom_evict_file(fd), "evict_file")
+
+
+def crc32c_host(data, crc: int = 0) -> int:
+    buf = memoryview(data).cast("B")
+    arr = (C.c_char * len(buf)).from_buffer_copy(buf) if buf.readonly else (C.c_char * len(buf)).from_buffer(buf)
+    return N.lib().strom_crc32c_host(crc, arr, len(buf))
+
+
+# ---------------------------------------------------------------- CHECK_FILE
+@dataclass
+class FileInfo:
+    numa_node_id: int
+    support_dma64: bool
+
+
+def check_file(fd: int, sess: Optional[Session] = None) -> FileInfo:
+    a = N.CheckFile(fdesc=fd)
+    (sess or session()).ioctl(N.CHECK_FILE, a, "CHECK_FILE")
+    return FileInfo(a.numa_node_id, bool(a.support_dma64))
+
+
+# ------------------------------------------------------- GPU memory mappings
+@dataclass
+class GpuMapping:
+    handle: int
+    gpu_page_sz: int
+    gpu_npages: int
+    vaddress: int
+    length: int
+    sess: Session = field(repr=False, default=None)
+
+    def unmap(self) -> None:
+        if self.handle:
+            unmap_gpu_memory(self.handle, self.sess)
+            self.handle = 0
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.unmap()
+
+
+def map_gpu_memory(vaddress: int, length: int, sess: Optional[Session] = None) -> GpuMapping:
+    s = sess or session()
+    a = N.MapGpuMemory(vaddress=vaddress, length=length)
+    s.ioctl(N.MAP_GPU_MEMORY, a, "MAP_GPU_MEMORY")
+    return GpuMapping(a.handle, a.gpu_page_sz, a.gpu_npages, vaddress, length, s)
+
+
+def unmap_gpu_memory(handle: int, sess: Optional[Session] = None) -> None:
+    a = N.UnmapGpuMemory(handle=handle)
+    (sess or session()).ioctl(N.UNMAP_GPU_MEMORY, a, "UNMAP_GPU_MEMORY")
+
+
+def list_gpu_memory(sess: Optional[Session] = None) -> List[int]:
+    s = sess or session()
+    nrooms = 64
+    while True:
+        a = N.list_gpu_memory_struct(nrooms)(nrooms=nrooms)
+        s.ioctl(N.LIST_GPU_MEMORY, a, "LIST_GPU_MEMORY")
+        if a.nitems <= nrooms:
+            return [int(a.handles[i]) for i in range(a.nitems)]
+        nrooms = a.nitems
+
+
+def info_gpu_memory(handle: int, sess: Optional[Session] = None) -> dict:
+    s = sess or session()
+    nrooms = 16
+    while True:
+        a = N.info_gpu_memory_struct(nrooms)(handle=handle, nrooms=nrooms)
+        s.ioctl(N.INFO_GPU_MEMORY, a, "INFO_GPU_MEMORY")
+        if a.nitems <= nrooms:
+            break
+        nrooms = a.nitems
+    return dict(handle=handle, nitems=a.nitems, version=a.version, gpu_page_sz=a.gpu_page_sz,
+                owner=a.owner, map_offset=a.map_offset, map_length=a.map_length,
+                paddrs=[int(a.paddrs[i]) for i in range(a.nitems)])
+
+
+# ------------------------------------------------------------ DMA buffers
+class DmaBuffer:
+    """NUMA-local host buffer usable as an SSD2RAM destination.
+
+    ``array`` is a writable numpy uint8 view of the mapping; ``address`` is
+    the mapping's VA (what MEMCPY_SSD2RAM takes as ``dest_uaddr``).
+    """
+
+    def __init__(self, length: int, node: int = -1, sess: Optional[Session] = None):
+        a = N.AllocDMABuffer(length=length, node_id=node)
+        (sess or session()).ioctl(N.ALLOC_DMA_BUFFER, a, "ALLOC_DMA_BUFFER")
+        self.fd = a.dmabuf_fdesc
+        self.length = os.fstat(self.fd).st_size
+        self.node = node
+        self.mm = mmap.mmap(self.fd, self.length, flags=mmap.MAP_SHARED,
+                            prot=mmap.PROT_READ | mmap.PROT_WRITE)
+        self.array = np.frombuffer(self.mm, dtype=np.uint8)
+        self.address = self.array.ctypes.data
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            self.array = None
+            try:
+                self.mm.close()
+            except BufferError:
+                pass
+            os.close(self.fd)
+            self.fd = -1
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def alloc_dma_buffer(length: int, node: int = -1, sess: Optional[Session] = None) -> DmaBuffer:
+    return DmaBuffer(length, node, sess)
+
+
+# ---------------------------------------------------------------- MEMCPY_*
+@dataclass
+class CopyResult:
+    dma_task_id: int
+    nr_ram: int      # chunks served from the page cache
+    nr_ssd: int      # chunks read from storage
+    nr_dma_submit: int
+    nr_dma_blocks: int
+
+    @property
+    def avg_request_bytes(self) -> float:
+        return 512.0 * self.nr_dma_blocks / self.nr_dma_submit if self.nr_dma_submit else 0.0
+
+
+def _ids_array(chunk_ids) -> np.ndarray:
+    ids = np.ascontiguousarray(chunk_ids, dtype=np.uint32)
+    return ids
+
+
+def memcpy_ssd2gpu(handle: int, offset: int, fd: int, chunk_ids: np.ndarray, chunk_sz: int,
+                   relseg_sz: int = 0, wb_buffer: int = 0,
+                   sess: Optional[Session] = None) -> CopyResult:
+    """Issue MEMCPY_SSD2GPU.  ``chunk_ids`` (uint32, contiguous) is rewritten
+    in place to the landing order: storage chunks from the head of the
+    destination, page-cache chunks (copied into ``wb_buffer``'s tail) last."""
+    if not (isinstance(chunk_ids, np.ndarray) and chunk_ids.dtype == np.uint32
+            and chunk_ids.flags.c_contiguous):
+        raise TypeError("chunk_ids must be a contiguous numpy uint32 array (rewritten in place)")
+    a = N.MemCopySsdToGpu(handle=handle, offset=offset, file_desc=fd, nr_chunks=len(chunk_ids),
+                          chunk_sz=chunk_sz, relseg_sz=relseg_sz,
+                          chunk_ids=chunk_ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+                          wb_buffer=wb_buffer or None)
+    (sess or session()).ioctl(N.MEMCPY_SSD2GPU, a, "MEMCPY_SSD2GPU")
+    return CopyResult(a.dma_task_id, a.nr_ram2gpu, a.nr_ssd2gpu, a.nr_dma_submit, a.nr_dma_blocks)
+
+
+def memcpy_ssd2ram(dest_addr: int, fd: int, chunk_ids, chunk_sz: int, relseg_sz: int = 0,
+                   sess: Optional[Session] = None) -> CopyResult:
+    ids = _ids_array(chunk_ids)
+    a = N.MemCopySsdToRam(dest_uaddr=dest_addr, file_desc=fd, nr_chunks=len(ids),
+                          chunk_sz=chunk_sz, relseg_sz=relseg_sz,
+                          chunk_ids=ids.ctypes.data_as(C.POINTER(C.c_uint32)))
+    (sess or session()).ioctl(N.MEMCPY_SSD2RAM, a, "MEMCPY_SSD2RAM")
+    return CopyResult(a.dma_task_id, a.nr_ram2ram, a.nr_ssd2ram, a.nr_dma_submit, a.nr_dma_blocks)
+
+
+def memcpy_wait(task_id: int, timeout: Optional[float] = None,
+                sess: Optional[Session] = None) -> None:
+    """Block until the task finishes; raises StromError(EIO, status=...) on a
+    device error, ETIME on timeout, ENOENT for an id that was never issued."""
+    s = sess or session()
+    if timeout is None:
+        a = N.MemCopyWait(dma_task_id=task_id)
+        rc = s.ioctl_rc(N.MEMCPY_WAIT, a)
+    else:
+        a = N.MemCopyWaitTimed(dma_task_id=task_id, timeout_ns=int(timeout * 1e9))
+        rc = s.ioctl_rc(N.MEMCPY_WAIT_TIMED, a)
+    _check(rc, f"MEMCPY_WAIT({task_id})", a.status)
+
+
+# --------------------------------------------------------------- statistics
+def stat_info(sess: Optional[Session] = None) -> dict:
+    a = N.StatInfo(version=1)
+    (sess or session()).ioctl(N.STAT_INFO, a, "STAT_INFO")
+    return {name: getattr(a, name) for name, _ in N.StatInfo._fields_}
+
+
+def stat_hist(reset: bool = False, sess: Optional[Session] = None) -> dict:
+    a = N.StatHist(version=1, reset=int(reset))
+    (sess or session()).ioctl(N.STAT_HIST, a, "STAT_HIST")
+    return {k: np.array(getattr(a, k)[:], dtype=np.uint64) for k in ("io_ns", "copy_ns", "task_ns")}
+
+
+def hist_percentile(hist: np.ndarray, q: float) -> float:
+    """Approximate percentile (ns) of a log2 histogram (bucket k = [2^(k-1), 2^k))."""
+    total = int(hist.sum())
+    if total == 0:
+        return float("nan")
+    target = q / 100.0 * total
+    run = 0
+    for k, c in enumerate(hist):
+        if run + int(c) >= target and c:
+            lo = 0.0 if k == 0 else float(1 << (k - 1))
+            hi = float(1 << k)
+            frac = (target - run) / float(c)
+            return lo + (hi - lo) * frac
+        run += int(c)
+    return float(1 << (len(hist) - 1))

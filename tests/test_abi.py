@@ -1,0 +1,81 @@
+"""ABI layout: the argument blocks must stay byte-compatible with nvme-strom
+v0.6 (reference kmod/nvme_strom.h:17-165, measured layout in SURVEY §2.2)."""
+import ctypes as C
+import os
+import subprocess
+
+import pytest
+
+from nvme_strom_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+EXPECTED_SIZES = {
+    N.CheckFile: 12, N.MapGpuMemory: 32, N.UnmapGpuMemory: 8, N.ListGpuMemory: 16,
+    N.InfoGpuMemory: 56, N.MemCopySsdToGpu: 72, N.MemCopyWait: 16, N.MemCopySsdToRam: 56,
+    N.AllocDMABuffer: 16, N.StatInfo: 168,
+}
+
+EXPECTED_OFFSETS = [
+    (N.MapGpuMemory, "vaddress", 16), (N.MapGpuMemory, "length", 24),
+    (N.ListGpuMemory, "handles", 8),
+    (N.InfoGpuMemory, "map_offset", 32), (N.InfoGpuMemory, "paddrs", 48),
+    (N.MemCopySsdToGpu, "handle", 24), (N.MemCopySsdToGpu, "offset", 32),
+    (N.MemCopySsdToGpu, "file_desc", 40), (N.MemCopySsdToGpu, "chunk_ids", 56),
+    (N.MemCopySsdToGpu, "wb_buffer", 64),
+    (N.MemCopySsdToRam, "dest_uaddr", 24), (N.MemCopySsdToRam, "chunk_ids", 48),
+    (N.StatInfo, "tsc", 8), (N.StatInfo, "nr_debug1", 104),
+]
+
+
+@pytest.mark.parametrize("cls,size", list(EXPECTED_SIZES.items()), ids=lambda x: getattr(x, "__name__", str(x)))
+def test_struct_sizes(cls, size):
+    assert C.sizeof(cls) == size
+
+
+@pytest.mark.parametrize("cls,field,off", EXPECTED_OFFSETS)
+def test_field_offsets(cls, field, off):
+    assert getattr(cls, field).offset == off
+
+
+def test_ioctl_codes():
+    assert N.CHECK_FILE == 0x5380
+    assert N.MAP_GPU_MEMORY == 0x5381
+    assert N.UNMAP_GPU_MEMORY == 0x5382
+    assert N.LIST_GPU_MEMORY == 0x5383
+    assert N.INFO_GPU_MEMORY == 0x5384
+    assert N.ALLOC_DMA_BUFFER == 0x5385
+    assert N.MEMCPY_SSD2GPU == 0x5390
+    assert N.MEMCPY_SSD2RAM == 0x5391
+    assert N.MEMCPY_WAIT == 0x5392
+    assert N.STAT_INFO == 0x5399
+
+
+def test_header_compiles_as_c_and_cxx(tmp_path):
+    """The uapi header carries its own static assertions; compiling it in C
+    and C++ proves the C layout equals the pinned one."""
+    src = tmp_path / "probe.c"
+    src.write_text('#include "strom/uapi.h"\nint main(void){return 0;}\n')
+    inc = os.path.join(ROOT, "csrc", "include")
+    subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-I", inc, str(src)], check=True)
+    cpp = tmp_path / "probe.cc"
+    cpp.write_text('#include "strom/strom.h"\nint main(){return 0;}\n')
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", inc, str(cpp)], check=True)
+
+
+def test_reference_field_names_compile(tmp_path):
+    """Source compatibility: code written against the v0.6 names compiles."""
+    src = tmp_path / "compat.c"
+    src.write_text(r'''
+#include "strom/uapi.h"
+int f(void) {
+  StromCmd__MemCopySsdToGpu a; StromCmd__StatInfo s; StromCmd__CheckFile c;
+  StromCmd__AllocDMABuffer d; StromCmd__MemCopyWait w; StromCmd__InfoGpuMemory i;
+  a.nr_ram2gpu = a.nr_ssd2gpu = 0; a.wb_buffer = 0; a.relseg_sz = 0;
+  s.version = 1; c.support_dma64 = 0; d.dmabuf_fdesc = -1; w.status = 0; i.paddrs[0] = 0;
+  return (int)sizeof(a) + STROM_IOCTL__MEMCPY_SSD2GPU + (int)sizeof(s) + c.fdesc +
+         d.node_id + (int)w.dma_task_id + (int)i.map_offset;
+}
+''')
+    inc = os.path.join(ROOT, "csrc", "include")
+    subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-I", inc, str(src)], check=True)
