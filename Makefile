@@ -14,7 +14,7 @@ ENGINE_SRC := $(wildcard csrc/engine/*.cc)
 KERNEL_SRC := $(wildcard csrc/kernels/*.hip)
 ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
-TOOLS      := $(OUT)/strom_test $(OUT)/ssd2ram_test $(OUT)/strom_stat $(OUT)/abi_probe
+TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
 all: $(OUT)/libstrom.so tools
 

@@ -138,6 +138,41 @@ std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
   return f;
 }
 
+// Residency scoring input.  One mincore() over the span the chunks cover
+// when it is dense (sequential windows: the common case), else per chunk.
+static void attach_residency(Engine::OpenFile *fp, PlanParams *pp,
+                             std::vector<unsigned char> *vec, uint64_t *lo_out) {
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (uint32_t i = 0; i < pp->nr_chunks; ++i) {
+    uint64_t c = pp->relseg_sz ? pp->ids[i] % pp->relseg_sz : pp->ids[i];
+    uint64_t f = c * pp->chunk_sz;
+    lo = std::min(lo, f);
+    hi = std::max(hi, f + pp->chunk_sz);
+  }
+  hi = std::min<uint64_t>(hi, fp->map_len);
+  uint64_t total = (uint64_t)pp->nr_chunks * pp->chunk_sz;
+  uint64_t t0 = tsc_now();
+  if (lo < hi && hi - lo <= 4 * total) {
+    vec->resize((hi - lo + 4095) / 4096);
+    if (mincore((char *)fp->map + lo, hi - lo, vec->data()) == 0) {
+      *lo_out = lo;
+      std::vector<unsigned char> *v = vec;
+      uint64_t base = lo, end = hi;
+      pp->resident = [v, base, end](uint64_t off, uint32_t len) -> long {
+        if (off >= end) return 0;
+        uint64_t e = std::min<uint64_t>(off + len, end);
+        long r = 0;
+        for (uint64_t p = (off - base) >> 12; p < ((e - base + 4095) >> 12); ++p) r += (*v)[p] & 1;
+        return r;
+      };
+      stats().nr_debug[2].fetch_add(1, std::memory_order_relaxed);
+      stats().clk_debug[2].fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+      return;
+    }
+  }
+  pp->resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
+}
+
 int Engine::check_file(strom_check_file *a) {
   FileClass fc;
   int rc = classify_file(a->fdesc, &fc, config().strict);
@@ -225,10 +260,9 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   pp.file_size = (uint64_t)f->fc.size;
   pp.max_request = config().max_request;
   pp.reorder = true;
-  OpenFile *fp = f.get();
-  if (config().pgcache_probe && f->map) {
-    pp.resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
-  }
+  std::vector<unsigned char> resv;
+  uint64_t res_lo = 0;
+  if (config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
   ChunkPlan plan;
   int rc = plan_chunks(pp, &plan);
   if (rc) return rc;
@@ -286,10 +320,9 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   pp.file_size = (uint64_t)f->fc.size;
   pp.max_request = config().max_request;
   pp.reorder = false;
-  OpenFile *fp = f.get();
-  if (config().pgcache_probe && f->map) {
-    pp.resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
-  }
+  std::vector<unsigned char> resv;
+  uint64_t res_lo = 0;
+  if (config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
   ChunkPlan plan;
   rc = plan_chunks(pp, &plan);
   if (rc) return rc;

@@ -316,6 +316,7 @@ class Engine {
   ~Engine();
   int ioctl(int session, unsigned long cmd, void *arg);
   IoEngine &io() { return *io_; }
+  struct OpenFile;
 
  private:
   int check_file(strom_check_file *a);
@@ -324,7 +325,6 @@ class Engine {
   int memcpy_wait(strom_memcpy_wait *a);
   int memcpy_wait_timed(strom_memcpy_wait_timed *a);
 
-  struct OpenFile;
   std::shared_ptr<OpenFile> open_file(int fd, int *err);
 
   std::unique_ptr<IoEngine> io_;

@@ -1,0 +1,163 @@
+"""HBM buffers as PyTorch-ROCm tensors + file → HBM loaders.
+
+``HbmBuffer`` owns a device tensor and its engine mapping (MAP_GPU_MEMORY,
+reference kmod/pmemmap.c:216-343).  ``FileReader`` drives MEMCPY_SSD2GPU for
+a file: it owns the pinned write-back buffer for page-cache chunks, copies
+that tail into HBM at the right place (after the storage chunks — the
+reference's nvme_test copied it to offset 0, SURVEY §4 defect #1), waits,
+and restores the requested chunk order with the scatter kernel when the
+landing order differs.  ``load_file`` streams a whole file into one tensor
+with several ioctls in flight (the PAR3 ring of SURVEY §2.3).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import api
+from .ops.reorder import chunk_scatter, landing_positions
+
+
+class HbmBuffer:
+    """A device allocation registered with the engine (64 KiB map granule)."""
+
+    def __init__(self, nbytes: int, device=None, tensor: Optional[torch.Tensor] = None,
+                 sess: Optional[api.Session] = None):
+        if tensor is None:
+            dev = torch.device(device) if device is not None else torch.device("cuda")
+            tensor = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
+        if not tensor.is_cuda or not tensor.is_contiguous():
+            raise ValueError("HbmBuffer needs a contiguous device tensor")
+        self.tensor = tensor.view(torch.uint8).reshape(-1)
+        self.nbytes = self.tensor.numel()
+        self.mapping = api.map_gpu_memory(self.tensor.data_ptr(), self.nbytes, sess)
+
+    @property
+    def handle(self) -> int:
+        return self.mapping.handle
+
+    def view(self, dtype: torch.dtype, shape: Sequence[int], offset: int = 0) -> torch.Tensor:
+        n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        return self.tensor[offset:offset + n].view(dtype).reshape(tuple(shape))
+
+    def close(self) -> None:
+        self.mapping.unmap()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class FileReader:
+    """MEMCPY_SSD2GPU driver for one file."""
+
+    def __init__(self, path: str, chunk_sz: int = 8192, relseg_sz: int = 0,
+                 max_chunks: int = 4096, sess: Optional[api.Session] = None):
+        self.path = path
+        self.fd = os.open(path, os.O_RDONLY)
+        self.size = os.fstat(self.fd).st_size
+        self.chunk_sz = chunk_sz
+        self.relseg_sz = relseg_sz
+        self.sess = sess or api.session()
+        self.info = api.check_file(self.fd, self.sess)
+        # pinned write-back buffer for page-cache chunks (one per reader)
+        self._wb = torch.empty(max_chunks * chunk_sz, dtype=torch.uint8, pin_memory=True)
+        self.max_chunks = max_chunks
+
+    @property
+    def nchunks(self) -> int:
+        return (self.size + self.chunk_sz - 1) // self.chunk_sz
+
+    def submit(self, buf: HbmBuffer, offset: int, chunk_ids, wb: Optional[torch.Tensor] = None):
+        """Start a copy; returns (CopyResult, landed ids).  Caller must
+        ``finish()`` it.  ``wb`` overrides the reader's write-back buffer
+        (needed when several submissions are in flight)."""
+        ids = np.array(chunk_ids, dtype=np.uint32, copy=True)
+        if len(ids) > self.max_chunks and wb is None:
+            raise ValueError("too many chunks for the write-back buffer")
+        wbt = self._wb if wb is None else wb
+        res = api.memcpy_ssd2gpu(buf.handle, offset, self.fd, ids, self.chunk_sz,
+                                 self.relseg_sz, wbt.data_ptr(), self.sess)
+        if res.nr_ram:
+            # RAM tail belongs right after the storage chunks in HBM
+            lo = res.nr_ssd * self.chunk_sz
+            hi = len(ids) * self.chunk_sz
+            buf.tensor[offset + lo:offset + hi].copy_(wbt[lo:hi], non_blocking=True)
+        return res, ids
+
+    def finish(self, res) -> None:
+        api.memcpy_wait(res.dma_task_id, sess=self.sess)
+
+    def read_chunks(self, buf: HbmBuffer, offset: int, chunk_ids,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Load ``chunk_ids`` into ``buf`` at ``offset`` and return them in
+        the requested order (scattered into ``out`` when the engine had to
+        land them in a different order)."""
+        req = np.asarray(chunk_ids, dtype=np.uint32)
+        res, landed = self.submit(buf, offset, req)
+        self.finish(res)
+        n = len(req) * self.chunk_sz
+        region = buf.tensor[offset:offset + n]
+        if np.array_equal(landed, req):
+            return region
+        pos = landing_positions(req, landed, res.nr_ssd)
+        if out is None:
+            out = torch.empty(n, dtype=torch.uint8, device=buf.tensor.device)
+        chunk_scatter(region, out, pos, self.chunk_sz)
+        return out
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def load_file(path: str, device=None, chunk_sz: int = 1 << 20, window: int = 64 << 20,
+              inflight: int = 4, buf: Optional[HbmBuffer] = None) -> torch.Tensor:
+    """Read a whole file into a device uint8 tensor through the engine.
+
+    Windows of ``window`` bytes are issued ``inflight`` at a time so storage
+    reads, SDMA copies and ioctl submission overlap."""
+    size = os.path.getsize(path)
+    padded = (size + chunk_sz - 1) // chunk_sz * chunk_sz
+    own = buf is None
+    if own:
+        buf = HbmBuffer(max(padded, chunk_sz), device)
+    per_win = max(1, window // chunk_sz)
+    nchunks = padded // chunk_sz
+    with FileReader(path, chunk_sz=chunk_sz, max_chunks=per_win) as rd:
+        # one pinned write-back buffer per in-flight window
+        wbs = [rd._wb] + [torch.empty_like(rd._wb, pin_memory=True) for _ in range(inflight - 1)]
+        pending = []
+        dirty = [False] * inflight       # wb slot still feeding an async HtoD
+        for k, first in enumerate(range(0, nchunks, per_win)):
+            ids = np.arange(first, min(nchunks, first + per_win), dtype=np.uint32)
+            if dirty[k % inflight]:
+                torch.cuda.current_stream().synchronize()
+                dirty = [False] * inflight
+            res, landed = rd.submit(buf, first * chunk_sz, ids, wb=wbs[k % inflight])
+            dirty[k % inflight] = res.nr_ram > 0
+            if res.nr_ram and not np.array_equal(landed, ids):
+                rd.finish(res)
+                region = buf.tensor[first * chunk_sz:(first + len(ids)) * chunk_sz]
+                tmp = region.clone()
+                chunk_scatter(tmp, region, landing_positions(ids, landed, res.nr_ssd), chunk_sz)
+                continue
+            pending.append(res)
+            if len(pending) >= inflight:
+                rd.finish(pending.pop(0))
+        for res in pending:
+            rd.finish(res)
+    torch.cuda.current_stream().synchronize()
+    return buf.tensor[:size]

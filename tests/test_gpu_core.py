@@ -1,0 +1,157 @@
+"""GPU tests (MI355X): kernel numerics vs host references, SSD→HBM end to end."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import nvme_strom_amd as S
+    S.configure(gpu_emulation=0, backend="uring", max_request=1 << 20, workers=4,
+                pgcache_probe=1, direct_io=1)
+    return S
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("n,chunk", [(1, 16), (3, 16), (4, 16), (17, 16), (1000, 1024),
+                                     (8192 * 5 + 77, 8192), (1 << 20, 1 << 20),
+                                     ((3 << 20) + 4096 + 5, 1 << 16), (100000, 4096)])
+def test_crc32c_chunks_vs_host(S, n, chunk):
+    from nvme_strom_amd.ops import verify as V
+    data = np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8)
+    dev = V.u32(V.crc32c_chunks(_dev(data), chunk))
+    ref = [S.crc32c_host(data[i:i + chunk].tobytes()) for i in range(0, n, chunk)]
+    assert list(dev) == ref
+    assert V.crc32c(_dev(data), chunk=chunk) == S.crc32c_host(data.tobytes())
+
+
+def test_crc32c_known_vector(S):
+    from nvme_strom_amd.ops import verify as V
+    assert S.crc32c_host(b"123456789") == 0xE3069283
+    t = _dev(np.frombuffer(b"123456789" + b"\0" * 7, dtype=np.uint8))
+    assert V.crc32c(t, nbytes=9, chunk=16) == 0xE3069283
+
+
+def test_scatter_gather(S):
+    from nvme_strom_amd.ops.reorder import chunk_gather, chunk_scatter
+    ch, n = 8192, 97
+    src = torch.randint(0, 256, (n * ch,), dtype=torch.uint8, device="cuda")
+    perm = np.random.default_rng(0).permutation(n).astype(np.uint32)
+    dst = torch.empty_like(src)
+    chunk_scatter(src, dst, perm, ch)
+    ref = torch.empty_like(src).view(n, ch)
+    ref[torch.from_numpy(perm.astype(np.int64)).cuda()] = src.view(n, ch)
+    assert torch.equal(dst.view(n, ch), ref)
+    back = torch.empty_like(src)
+    chunk_gather(dst, back, perm, ch)
+    assert torch.equal(back, src)
+
+
+def test_verify_and_fill(S):
+    from nvme_strom_amd.ops import verify as V
+    t = torch.empty(1 << 20, dtype=torch.uint8, device="cuda")
+    V.fill_pattern(t, 0x41424344)
+    assert V.verify_pattern(t, 0x41424344) == (0, -1)
+    t[4096 + 5] = 0
+    t[8000] = 1
+    assert V.verify_pattern(t, 0x41424344) == (2, 4096 + 4)
+    u = t.clone()
+    assert V.verify_equal(t, u) == (0, -1)
+    u[12] = 7
+    assert V.verify_equal(t, u)[1] == 12
+
+
+def _mkfile(tmp_path, n, seed=0):
+    data = np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+    p = str(tmp_path / f"f{seed}.bin")
+    with open(p, "wb") as f:
+        f.write(data.tobytes())
+        f.flush()
+        os.fsync(f.fileno())
+    fd = os.open(p, os.O_RDONLY)
+    os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+    os.close(fd)
+    return p, data
+
+
+@pytest.mark.parametrize("backend", ["uring", "psync"])
+def test_load_file_end_to_end(S, tmp_path, backend):
+    from nvme_strom_amd.ops import verify as V
+    from nvme_strom_amd.tensor import load_file
+    S.configure(backend=backend)
+    p, data = _mkfile(tmp_path, (16 << 20) + 12345)
+    t = load_file(p, device="cuda", chunk_sz=1 << 16, window=4 << 20)
+    assert torch.equal(t.cpu(), torch.from_numpy(data))
+    assert V.crc32c(t) == S.crc32c_host(data.tobytes())
+    S.configure(backend="uring")
+
+
+def test_read_chunks_hybrid_reorder(S, tmp_path):
+    """Page-cache chunks land at the tail via the write-back buffer; the
+    reader scatters everything back into the requested order on the GPU."""
+    from nvme_strom_amd.tensor import FileReader, HbmBuffer
+    ch, n = 8192, 256
+    p, data = _mkfile(tmp_path, ch * n, seed=3)
+    fd = os.open(p, os.O_RDONLY)
+    os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)
+    for c in (5, 6, 100, 200, 255):
+        os.pread(fd, ch, c * ch)
+    os.close(fd)
+    req = np.random.default_rng(1).permutation(n).astype(np.uint32)
+    with FileReader(p, chunk_sz=ch, max_chunks=n) as rd, HbmBuffer(n * ch, "cuda") as hb:
+        res, landed = rd.submit(hb, 0, req)
+        rd.finish(res)
+        assert res.nr_ram >= 1
+        rd2 = FileReader(p, chunk_sz=ch, max_chunks=n)
+        out = rd2.read_chunks(hb, 0, req)
+        rd2.close()
+        ref = data.reshape(n, ch)[req.astype(np.int64)].reshape(-1)
+        assert torch.equal(out.cpu(), torch.from_numpy(ref))
+
+
+def test_stream_loader_verify(S, tmp_path):
+    from nvme_strom_amd.models.ssd2gpu_stream import StreamLoader
+    p, data = _mkfile(tmp_path, 64 << 20, seed=5)
+    ld = StreamLoader(p, segment_sz=8 << 20, nr_segments=4, chunk_sz=8192, device="cuda", depth=3)
+    st = ld.run(0, 64 << 20, verify=True)
+    assert st.crc_mismatch == 0
+    assert st.nr_ssd + st.nr_ram == (64 << 20) // 8192
+    ld.close()
+
+
+def test_map_real_hbm_and_info(S):
+    t = torch.empty(3 << 20, dtype=torch.uint8, device="cuda")
+    m = S.map_gpu_memory(t.data_ptr(), t.numel())
+    info = S.info_gpu_memory(m.handle)
+    assert info["map_length"] == info["map_offset"] + t.numel()
+    m.unmap()
+    # host memory is not GPU memory when emulation is off
+    h = np.zeros(1 << 16, dtype=np.uint8)
+    with pytest.raises(S.StromError):
+        S.map_gpu_memory(h.ctypes.data, h.nbytes)
+
+
+def test_latency_4k(S, tmp_path):
+    import time
+    from nvme_strom_amd.tensor import FileReader, HbmBuffer
+    p, data = _mkfile(tmp_path, 64 << 20, seed=9)
+    with FileReader(p, chunk_sz=4096, max_chunks=1) as rd, HbmBuffer(1 << 20, "cuda") as hb:
+        lat = []
+        for cid in np.random.default_rng(0).integers(0, (64 << 20) // 4096, 300):
+            t0 = time.perf_counter()
+            res, _ = rd.submit(hb, 0, np.array([cid], dtype=np.uint32))
+            rd.finish(res)
+            lat.append(time.perf_counter() - t0)
+            got = hb.tensor[:4096].cpu().numpy()
+            assert np.array_equal(got, data[cid * 4096:(cid + 1) * 4096])
+        assert np.median(lat) < 0.01
