@@ -33,7 +33,7 @@ $(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ)
 	$(HIPCC) $(LDFLAGS) --offload-arch=$(ARCH) -o $@ $^
 
 $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
-	$(HIPCC) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
+	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
 	rm -rf build $(OUT)/libstrom.so $(TOOLS)

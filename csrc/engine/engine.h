@@ -41,9 +41,10 @@ namespace strom {
 enum class BackendKind { kPsync, kUring, kFake };
 
 struct Config {
+  // defaults from the MI355X-host sweep (nvme_strom_amd/tools/tune.py)
   BackendKind backend = BackendKind::kUring;
-  int workers = 8;               // I/O worker threads
-  int queue_depth = 16;          // in-flight reads per worker (uring)
+  int workers = 4;               // I/O worker threads (one SDMA stream each)
+  int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
   int staging_slots = 8;         // pinned slots per worker (GPU dest)
   bool strict = false;           // reference CHECK_FILE rules only
@@ -306,6 +307,8 @@ int device_count();
 int pointer_device(uint64_t va, uint64_t *alloc_base, size_t *alloc_size);
 void *host_alloc(size_t bytes);            // pinned, portable
 void host_free(void *p);
+void *host_alloc_thp(size_t bytes);        // THP-backed, hipHostRegister'ed
+void host_free_thp(void *p, size_t bytes);
 int numa_node_of_device(int device);
 }  // namespace hip
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <cctype>
 #include <mutex>
@@ -70,6 +71,39 @@ void *host_alloc(size_t bytes) {
 
 void host_free(void *p) {
   if (p) (void)hipHostFree(p);
+}
+
+// Staging for O_DIRECT reads: anonymous memory backed by transparent huge
+// pages, then registered (pinned + GPU-mapped).  Measured on MI355X hosts:
+// O_DIRECT into 2 MiB pages costs the kernel far less page pinning than
+// into hipHostMalloc's 4 KiB pages (single-thread 19-20 vs 14 GiB/s), and
+// SDMA reads it at the same ~50 GiB/s.
+void *host_alloc_thp(size_t bytes) {
+  const size_t huge = 2u << 20;
+  size_t len = (bytes + huge - 1) / huge * huge;
+  void *raw = mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) return nullptr;
+  uintptr_t a = ((uintptr_t)raw + huge - 1) & ~(uintptr_t)(huge - 1);
+  if (a > (uintptr_t)raw) munmap(raw, a - (uintptr_t)raw);
+  size_t tail = (uintptr_t)raw + len + huge - (a + len);
+  if (tail) munmap((void *)(a + len), tail);
+  void *p = (void *)a;
+  madvise(p, len, MADV_HUGEPAGE);
+  memset(p, 0, len);  // fault in (under the caller's NUMA policy)
+  if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(p, len);
+    return nullptr;
+  }
+  return p;
+}
+
+void host_free_thp(void *p, size_t bytes) {
+  if (!p) return;
+  const size_t huge = 2u << 20;
+  size_t len = (bytes + huge - 1) / huge * huge;
+  (void)hipHostUnregister(p);
+  munmap(p, len);
 }
 
 int numa_node_of_device(int device) {

@@ -180,6 +180,9 @@ struct IoEngine::Worker {
   std::deque<IoReq> q;
   bool stop = false;
   std::vector<Slot> slots;
+  uint8_t *staging = nullptr;     // one registered region, cut into slots
+  size_t staging_bytes = 0;
+  bool staging_thp = false;
   std::vector<int> free_slots;
   std::deque<int> copying;        // FIFO of slots with copies in flight
   std::vector<hipStream_t> streams;
@@ -222,18 +225,28 @@ struct IoEngine::Worker {
 
   bool ensure_slots() {
     if (!slots.empty()) return true;
+    size_t bytes = (size_t)cfg.staging_slots * cfg.max_request;
+    staging = (uint8_t *)hip::host_alloc_thp(bytes);
+    staging_thp = staging != nullptr;
+    if (!staging) staging = (uint8_t *)hip::host_alloc(bytes);
+    if (!staging) {
+      STROM_LOG(0, "worker %d: pinned staging allocation failed", idx);
+      return false;
+    }
+    staging_bytes = bytes;
     slots.resize(cfg.staging_slots);
     for (int i = 0; i < cfg.staging_slots; ++i) {
-      slots[i].buf = (uint8_t *)hip::host_alloc(cfg.max_request);
-      if (!slots[i].buf) {
-        STROM_LOG(0, "worker %d: pinned staging allocation failed", idx);
-        for (auto &s : slots) hip::host_free(s.buf);
-        slots.clear();
-        return false;
-      }
+      slots[i].buf = staging + (size_t)i * cfg.max_request;
       free_slots.push_back(i);
     }
     return true;
+  }
+
+  void free_staging() {
+    if (!staging) return;
+    if (staging_thp) hip::host_free_thp(staging, staging_bytes);
+    else hip::host_free(staging);
+    staging = nullptr;
   }
 
   hipStream_t stream_for(int dev) {
@@ -423,10 +436,9 @@ struct IoEngine::Worker {
         sched_yield();  // both pipes busy
       }
     }
-    for (auto &s : slots) {
+    for (auto &s : slots)
       if (s.ev) (void)hipEventDestroy(s.ev);
-      hip::host_free(s.buf);
-    }
+    free_staging();
     for (auto st : streams)
       if (st) (void)hipStreamDestroy(st);
   }

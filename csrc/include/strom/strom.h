@@ -123,6 +123,9 @@ struct strom_decomp_desc {
 #define STROM_CODEC_LZ4    1
 #define STROM_CODEC_SNAPPY 2
 #define STROM_CODEC_COPY   3   /* stored block */
+#define STROM_CODEC_LZ4_FRAME     4  /* LZ4 frame data blocks (after header) */
+#define STROM_CODEC_LZ4_FRAME_BCS 5  /*   ... with 4-byte block checksums */
+/* status[i] = decoded bytes, or -1 malformed / -2 overflow / -3 distance */
 int strom_decompress(int codec, const void *d_src, void *d_dst,
                      const struct strom_decomp_desc *d_desc, uint32_t nblocks,
                      int32_t *d_status, void *stream);

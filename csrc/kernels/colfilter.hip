@@ -1,0 +1,161 @@
+// colfilter.hip — columnar predicate evaluation + selection compaction.
+//
+// PG-Strom-style scan (BASELINE config 5): after an Arrow column lands in HBM
+// (and is decompressed), evaluate lo <= v <= hi for every row and produce an
+// Arrow-compatible selection bitmap (LSB-first, 64 rows per word) plus the
+// selected-row count.  One lane per row, one wavefront per 64-row word: the
+// predicate's __ballot IS the bitmap word, ANDed with the validity word, so
+// the bitmap is written with one 8-byte store per wave and no atomics on the
+// data path (one count atomic per workgroup).
+//
+// bitmap_to_indices turns the bitmap into a dense, ordered row-index list
+// (three launches: per-block popcounts, single-block exclusive scan,
+// per-block LDS scan + write), deterministic regardless of scheduling.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "strom/strom.h"
+
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void filter_kernel(const T *__restrict__ v,
+                                                     const uint64_t *__restrict__ valid,
+                                                     uint64_t n, T lo, T hi,
+                                                     uint64_t *__restrict__ bitmap,
+                                                     unsigned long long *__restrict__ count) {
+  __shared__ uint32_t wave_cnt[4];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t nwords = (n + 63) / 64;
+  uint32_t local = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * 4 + wid; w < nwords; w += (uint64_t)gridDim.x * 4) {
+    uint64_t i = w * 64 + lane;
+    bool ok = false;
+    if (i < n) {
+      T x = v[i];
+      ok = x >= lo && x <= hi;
+    }
+    uint64_t word = __ballot(ok);
+    if (valid) word &= valid[w];
+    if (lane == 0) bitmap[w] = word;
+    local += __popcll(word);
+  }
+  if (lane == 0) wave_cnt[wid] = local;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicAdd(count, (unsigned long long)(wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3]));
+}
+
+constexpr uint32_t kWordsPerBlock = 256;
+
+__global__ __launch_bounds__(256) void block_popc_kernel(const uint64_t *__restrict__ bm,
+                                                         uint64_t nwords,
+                                                         uint32_t *__restrict__ block_cnt) {
+  __shared__ uint32_t s[4];
+  uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint32_t c = w < nwords ? __popcll(bm[w]) : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+// exclusive scan of block counts in one workgroup (sequential chunks per thread)
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(uint32_t *__restrict__ cnt, uint32_t nb,
+                                                           unsigned long long *__restrict__ total) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nb + 1023) / 1024;
+  const uint32_t lo = min(nb, t * per), hi = min(nb, lo + per);
+  uint64_t s = 0;
+  for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint64_t add = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += add;
+    __syncthreads();
+  }
+  uint64_t run = t ? part[t - 1] : 0;
+  for (uint32_t i = lo; i < hi; ++i) {
+    uint32_t c = cnt[i];
+    cnt[i] = (uint32_t)run;
+    run += c;
+  }
+  if (t == 1023) *total = part[1023];
+}
+
+__global__ __launch_bounds__(256) void emit_indices_kernel(const uint64_t *__restrict__ bm,
+                                                           uint64_t nwords, uint64_t n,
+                                                           const uint32_t *__restrict__ base,
+                                                           uint32_t *__restrict__ out) {
+  __shared__ uint32_t s[256];
+  uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint64_t word = w < nwords ? bm[w] : 0;
+  if (w == nwords - 1 && (n & 63)) word &= (1ull << (n & 63)) - 1;
+  uint32_t c = __popcll(word);
+  s[threadIdx.x] = c;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    uint32_t add = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+    __syncthreads();
+    s[threadIdx.x] += add;
+    __syncthreads();
+  }
+  uint32_t pos = base[blockIdx.x] + s[threadIdx.x] - c;
+  while (word) {
+    uint32_t b = __ffsll((unsigned long long)word) - 1;
+    out[pos++] = (uint32_t)(w * 64 + b);
+    word &= word - 1;
+  }
+}
+
+template <typename T>
+int launch_filter(const void *v, const uint8_t *valid, uint64_t n, double lo, double hi,
+                  uint64_t *bm, uint64_t *cnt, hipStream_t st) {
+  uint64_t words = (n + 63) / 64;
+  uint64_t g = (words + 3) / 4;
+  uint32_t grid = (uint32_t)(g > 4096 ? 4096 : (g ? g : 1));
+  (void)hipMemsetAsync(cnt, 0, sizeof(uint64_t), st);
+  hipLaunchKernelGGL(filter_kernel<T>, dim3(grid), dim3(256), 0, st, (const T *)v,
+                     (const uint64_t *)valid, n, (T)lo, (T)hi, bm, (unsigned long long *)cnt);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace
+
+extern "C" int strom_column_filter(int type, const void *d_values, const uint8_t *d_valid,
+                                   uint64_t n, double lo, double hi, uint64_t *d_bitmap,
+                                   uint64_t *d_count, void *stream) {
+  if (!n) return 0;
+  if (((uintptr_t)d_valid & 7) || ((uintptr_t)d_bitmap & 7)) return -22;
+  hipStream_t st = (hipStream_t)stream;
+  switch (type) {
+    case STROM_COL_I32: return launch_filter<int32_t>(d_values, d_valid, n, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_I64: return launch_filter<int64_t>(d_values, d_valid, n, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_F32: return launch_filter<float>(d_values, d_valid, n, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_F64: return launch_filter<double>(d_values, d_valid, n, lo, hi, d_bitmap, d_count, st);
+    default: return -22;
+  }
+}
+
+// d_out needs room for every selected row; d_count receives the total.
+// Scratch for the block counts is carved from the tail of d_out's capacity
+// by the caller contract: we allocate it here with hipMallocAsync instead.
+extern "C" int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n, uint32_t *d_out,
+                                       uint64_t *d_count, void *stream) {
+  if (!n) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t words = (n + 63) / 64;
+  uint32_t nb = (uint32_t)((words + kWordsPerBlock - 1) / kWordsPerBlock);
+  uint32_t *cnt = nullptr;
+  if (hipMallocAsync((void **)&cnt, sizeof(uint32_t) * nb, st) != hipSuccess) return -12;
+  hipLaunchKernelGGL(block_popc_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, words, cnt);
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
+                     (unsigned long long *)d_count);
+  hipLaunchKernelGGL(emit_indices_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, words, n, cnt, d_out);
+  (void)hipFreeAsync(cnt, st);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

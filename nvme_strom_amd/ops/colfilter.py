@@ -1,0 +1,57 @@
+"""Columnar range filter + selection compaction (csrc/kernels/colfilter.hip)."""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ._util import check, lib, ptr, require_cuda, stream_handle
+
+_TYPES = {torch.int32: 1, torch.int64: 2, torch.float32: 3, torch.float64: 4}
+
+
+def column_filter(values: torch.Tensor, lo, hi, valid: Optional[torch.Tensor] = None,
+                  stream=None) -> Tuple[torch.Tensor, int]:
+    """Selection bitmap (int64 words, LSB-first like Arrow validity) of
+    ``lo <= v <= hi`` AND valid, plus the selected count."""
+    require_cuda(values, "values")
+    if values.dtype not in _TYPES:
+        raise ValueError(f"unsupported dtype {values.dtype}")
+    n = values.numel()
+    words = (n + 63) // 64
+    bm = torch.empty(max(words, 1), dtype=torch.int64, device=values.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=values.device)
+    vptr = 0
+    if valid is not None:
+        require_cuda(valid, "valid")
+        if valid.numel() * valid.element_size() < words * 8:
+            # Arrow pads validity to 64 bytes; pad here when a caller did not
+            pad = torch.zeros(words * 8, dtype=torch.uint8, device=values.device)
+            vb = valid.view(torch.uint8)
+            pad[:vb.numel()] = vb
+            valid = pad
+        vptr = ptr(valid)
+    check(lib().strom_column_filter(_TYPES[values.dtype], ptr(values), vptr, n, float(lo),
+                                    float(hi), ptr(bm), ptr(cnt), stream_handle(stream)),
+          "column_filter")
+    return bm, int(cnt.item())
+
+
+def bitmap_to_indices(bitmap: torch.Tensor, n: int, count: Optional[int] = None,
+                      stream=None) -> torch.Tensor:
+    """Ordered int32 row indices of the set bits (first ``n`` rows)."""
+    require_cuda(bitmap, "bitmap")
+    if count is None:
+        count = int(_popcount(bitmap, n))
+    out = torch.empty(max(count, 1), dtype=torch.int32, device=bitmap.device)
+    total = torch.zeros(1, dtype=torch.int64, device=bitmap.device)
+    check(lib().strom_bitmap_to_indices(ptr(bitmap), n, ptr(out), ptr(total),
+                                        stream_handle(stream)), "bitmap_to_indices")
+    return out[:count]
+
+
+def _popcount(bitmap: torch.Tensor, n: int) -> int:
+    b = bitmap.cpu().numpy().view(np.uint8)
+    bits = np.unpackbits(b, bitorder="little")[:n]
+    return int(bits.sum())

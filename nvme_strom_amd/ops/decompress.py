@@ -1,0 +1,144 @@
+"""GPU LZ4 / snappy decode (csrc/kernels/decompress.hip) + host codec helpers.
+
+``decompress`` takes a device byte tensor holding many compressed streams and
+a descriptor per stream (source offset/length, destination offset/capacity)
+and decodes them all in one launch, one wavefront per stream.  Supported:
+raw LZ4 blocks, LZ4 *frames* (linked or independent blocks — the format
+pyarrow's ``lz4``/``lz4_frame`` codec and Arrow IPC buffer compression use),
+raw snappy and stored copies.  Host encoders/decoders (native, in libstrom)
+produce test data and serve as CPU references.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import struct
+from dataclasses import dataclass
+from typing import List, Sequence
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ._util import check, lib, ptr, require_cuda, stream_handle
+
+LZ4 = 1
+SNAPPY = 2
+COPY = 3
+LZ4_FRAME = 4
+LZ4_FRAME_BCS = 5
+
+DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_len", "<u4"),
+                       ("dst_len", "<u4")])
+
+
+# ------------------------------------------------------------ host codecs
+def _host(fn, data: bytes, cap: int) -> bytes:
+    src = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty(max(cap, 16), dtype=np.uint8)
+    n = fn(src.ctypes.data, len(src), out.ctypes.data, len(out))
+    if n < 0:
+        raise ValueError(f"codec error {n}")
+    return out[:n].tobytes()
+
+
+def lz4_compress(data: bytes) -> bytes:
+    return _host(N.lib().strom_lz4_compress_host, data, len(data) + len(data) // 255 + 64)
+
+
+def lz4_decompress(data: bytes, size: int) -> bytes:
+    return _host(N.lib().strom_lz4_decompress_host, data, size)
+
+
+def snappy_compress(data: bytes) -> bytes:
+    return _host(N.lib().strom_snappy_compress_host, data, 32 + len(data) + len(data) // 6)
+
+
+def snappy_decompress(data: bytes, size: int) -> bytes:
+    return _host(N.lib().strom_snappy_decompress_host, data, size)
+
+
+@dataclass
+class Lz4FrameInfo:
+    data_offset: int          # first block header, relative to the frame start
+    block_checksum: bool
+    content_size: int         # -1 when absent
+    block_max: int
+
+
+def parse_lz4_frame_header(buf: bytes, off: int = 0) -> Lz4FrameInfo:
+    """Parse an LZ4 frame header (magic 0x184D2204)."""
+    magic, = struct.unpack_from("<I", buf, off)
+    if magic != 0x184D2204:
+        raise ValueError("not an LZ4 frame")
+    flg, bd = buf[off + 4], buf[off + 5]
+    if (flg >> 6) != 1:
+        raise ValueError("unsupported LZ4 frame version")
+    p = off + 6
+    csize = -1
+    if flg & 0x08:
+        csize, = struct.unpack_from("<Q", buf, p)
+        p += 8
+    if flg & 0x01:
+        p += 4                # dictionary id
+    p += 1                    # header checksum
+    block_max = {4: 64 << 10, 5: 256 << 10, 6: 1 << 20, 7: 4 << 20}.get((bd >> 4) & 7, 4 << 20)
+    return Lz4FrameInfo(p - off, bool(flg & 0x10), csize, block_max)
+
+
+def lz4_frame_compress(data: bytes, block_size: int = 64 << 10, linked: bool = True) -> bytes:
+    """Minimal LZ4 frame writer (tests): independent raw blocks; with
+    ``linked`` the flag says linked (blocks still self-contained — valid)."""
+    flg = 0x40 | (0x00 if linked else 0x20)
+    bd = {64 << 10: 4, 256 << 10: 5, 1 << 20: 6, 4 << 20: 7}[block_size] << 4
+    hdr = bytes([0x04, 0x22, 0x4D, 0x18, flg, bd])
+    hc = (_xxh32(hdr[4:]) >> 8) & 0xFF
+    out = [hdr, bytes([hc])]
+    for i in range(0, len(data), block_size):
+        blk = data[i:i + block_size]
+        c = lz4_compress(blk)
+        if len(c) >= len(blk):
+            out.append(struct.pack("<I", len(blk) | 0x80000000) + blk)
+        else:
+            out.append(struct.pack("<I", len(c)) + c)
+    out.append(b"\0\0\0\0")
+    return b"".join(out)
+
+
+def _xxh32(data: bytes, seed: int = 0) -> int:
+    try:
+        import xxhash
+        return xxhash.xxh32_intdigest(data, seed)
+    except Exception:  # header checksum is not checked by our decoder
+        return 0
+
+
+# ------------------------------------------------------------ GPU decode
+def make_descs(items: Sequence[tuple]) -> np.ndarray:
+    """items: (src_off, src_len, dst_off, dst_len) per stream."""
+    d = np.zeros(len(items), dtype=DESC_DTYPE)
+    for i, (so, sl, do, dl) in enumerate(items):
+        d[i] = (so, do, sl, dl)
+    return d
+
+
+def decompress(codec: int, src: torch.Tensor, dst: torch.Tensor, descs: np.ndarray,
+               stream=None) -> np.ndarray:
+    """Decode every stream described by ``descs``; returns per-stream status
+    (decoded byte count, or <0: -1 malformed, -2 overflow)."""
+    require_cuda(src, "src")
+    require_cuda(dst, "dst")
+    descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+    for name, t in (("src", src), ("dst", dst)):
+        if t.dtype != torch.uint8:
+            raise ValueError(f"{name} must be uint8")
+    if len(descs) == 0:
+        return np.zeros(0, dtype=np.int32)
+    if int((descs["src_off"] + descs["src_len"]).max()) > src.numel():
+        raise ValueError("descriptor source out of range")
+    if int((descs["dst_off"] + descs["dst_len"]).max()) > dst.numel():
+        raise ValueError("descriptor destination out of range")
+    d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(src.device)
+    status = torch.empty(len(descs), dtype=torch.int32, device=src.device)
+    check(lib().strom_decompress(codec, ptr(src), ptr(dst), ptr(d_desc), len(descs), ptr(status),
+                                 stream_handle(stream)), "decompress")
+    return status.cpu().numpy()

@@ -1,0 +1,146 @@
+"""GPU kernel numerics vs host references: heap scan, LZ4/snappy, column filter."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda")
+
+
+def _t(b, dev):
+    return torch.from_numpy(np.frombuffer(b, dtype=np.uint8).copy()).to(dev)
+
+
+# ------------------------------------------------------------------ heap scan
+def test_heap_scan_matches_host(dev):
+    from nvme_strom_amd.ops.heapscan import heap_scan
+    from nvme_strom_amd.utils import pgpage
+    rng = np.random.default_rng(0)
+    vals = rng.integers(-1000, 1000, 5000).astype(np.int64)
+    data = bytearray(pgpage.build_table(vals, per_page=150, width=8, invisible_every=7))
+    npages = len(data) // 8192
+    data[3 * 8192 + 6000] ^= 0x5A                      # corrupt page 3 payload
+    data[5 * 8192:6 * 8192] = bytes(8192)              # page 5 is new/empty
+    data = bytes(data)
+    t = _t(data, dev)
+    for kw in [dict(), dict(skip_invisible=True), dict(verify_checksum=True),
+               dict(skip_invisible=True, verify_checksum=True, attr_off=0, attr_width=8,
+                    lo=-10, hi=250)]:
+        r = heap_scan(t, **kw)
+        ref_items, ref_status = pgpage.host_scan(data, **kw)
+        assert list(r.sorted_items()) == ref_items, kw
+        assert list(r.page_status.cpu().numpy()) == ref_status, kw
+    assert npages > 6
+
+
+def test_heap_scan_int4_column(dev):
+    from nvme_strom_amd.ops.heapscan import heap_scan
+    from nvme_strom_amd.utils import pgpage
+    vals = np.arange(3000, dtype=np.int64) - 1500
+    data = pgpage.build_table(vals, per_page=200, width=4)
+    r = heap_scan(_t(data, dev), attr_off=0, attr_width=4, lo=0, hi=99)
+    assert r.count == 100
+
+
+# ---------------------------------------------------------------- decompress
+def _payloads():
+    rng = np.random.default_rng(1)
+    words = [b"select", b"from", b"where", b"nvme", b"strom", b"gpu", b"hbm", b"mi355x"]
+    text = b" ".join(words[i] for i in rng.integers(0, len(words), 60000))
+    runs = b"".join(bytes([int(rng.integers(0, 3))]) * int(rng.integers(1, 500)) for _ in range(800))
+    rand = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    ints = np.cumsum(rng.integers(0, 5, 50000)).astype(np.int64).tobytes()
+    return [text, runs, rand, ints, b"x", b"", bytes(200000)]
+
+
+def _run(codec, streams, sizes, dev):
+    from nvme_strom_amd.ops import decompress as D
+    src = b"".join(streams)
+    offs = np.cumsum([0] + [len(s) for s in streams])[:-1]
+    doffs = np.cumsum([0] + list(sizes))[:-1]
+    descs = D.make_descs([(int(o), len(s), int(do), n) for o, s, do, n in zip(offs, streams, doffs, sizes)])
+    dst = torch.zeros(max(1, sum(sizes)), dtype=torch.uint8, device=dev)
+    st = D.decompress(codec, _t(src + b"\0", dev), dst, descs)
+    out = dst.cpu().numpy().tobytes()
+    return st, [out[int(do):int(do) + n] for do, n in zip(doffs, sizes)]
+
+
+@pytest.mark.parametrize("which", ["ours", "pyarrow"])
+def test_lz4_raw(dev, which):
+    from nvme_strom_amd.ops import decompress as D
+    pays = _payloads()
+    if which == "pyarrow":
+        pa = pytest.importorskip("pyarrow")
+        comp = [pa.compress(p, codec="lz4_raw", asbytes=True) if p else D.lz4_compress(p) for p in pays]
+    else:
+        comp = [D.lz4_compress(p) for p in pays]
+    st, outs = _run(D.LZ4, comp, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
+@pytest.mark.parametrize("which", ["ours", "pyarrow"])
+def test_snappy(dev, which):
+    from nvme_strom_amd.ops import decompress as D
+    pays = _payloads()
+    if which == "pyarrow":
+        pa = pytest.importorskip("pyarrow")
+        comp = [pa.compress(p, codec="snappy", asbytes=True) for p in pays]
+    else:
+        comp = [D.snappy_compress(p) for p in pays]
+    st, outs = _run(D.SNAPPY, comp, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
+def test_lz4_frame_linked_blocks_from_pyarrow(dev):
+    """pyarrow's 'lz4' codec = LZ4 frame with linked 64 KiB blocks: matches
+    may reach into the previous block, which the LDS history ring covers."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd.ops import decompress as D
+    pays = [p for p in _payloads() if p]
+    frames = [pa.compress(p, codec="lz4", asbytes=True) for p in pays]
+    infos = [D.parse_lz4_frame_header(f) for f in frames]
+    streams = [f[i.data_offset:] for f, i in zip(frames, infos)]
+    codec = D.LZ4_FRAME_BCS if infos[0].block_checksum else D.LZ4_FRAME
+    st, outs = _run(codec, streams, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
+def test_malformed_streams_report_errors(dev):
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(5)
+    junk = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (10, 1000, 5000)]
+    good = D.lz4_compress(b"hello world " * 1000)
+    st, _ = _run(D.LZ4, junk + [good, good[:-3]], [4096, 4096, 4096, 12000, 12000], dev)
+    assert st[3] == 12000
+    assert (st[:3] < 0).all() or (st[:3] <= 4096).all()   # bounded, never out of range
+    st, _ = _run(D.SNAPPY, junk, [4096] * 3, dev)
+    assert (st < 0).all()
+
+
+# -------------------------------------------------------------- column filter
+@pytest.mark.parametrize("dtype", [torch.int32, torch.int64, torch.float32, torch.float64])
+def test_column_filter(dev, dtype):
+    from nvme_strom_amd.ops.colfilter import bitmap_to_indices, column_filter
+    n = 1_000_003
+    rng = np.random.default_rng(2)
+    v = rng.integers(-1000, 1000, n)
+    vt = torch.from_numpy(v).to(dtype).to(dev)
+    valid_bits = rng.random(n) > 0.1
+    valid = np.packbits(valid_bits, bitorder="little")
+    vb = torch.from_numpy(np.concatenate([valid, np.zeros(64, np.uint8)])).to(dev)
+    bm, cnt = column_filter(vt, -100, 250, vb)
+    ref = (v >= -100) & (v <= 250) & valid_bits
+    assert cnt == int(ref.sum())
+    got = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(got, ref)
+    idx = bitmap_to_indices(bm, n, cnt)
+    assert np.array_equal(idx.cpu().numpy(), np.nonzero(ref)[0].astype(np.int32))
