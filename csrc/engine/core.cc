@@ -8,9 +8,14 @@
 // that was never issued returns -ENOENT (reference returns success,
 // :1189-1190), and WAIT can carry a deadline.
 #include <errno.h>
+#include <fcntl.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
+#include <unistd.h>
 #include <x86intrin.h>
+
+#include <new>
 
 #include <chrono>
 #include <cstdio>
@@ -162,9 +167,44 @@ int Stats::fill_hist(strom_stat_hist *o) {
   return 0;
 }
 
+// The counters live in /dev/shm/nvme-strom.<pid> when possible so that
+// strom_stat (the nvme_stat analogue, reference utils/nvme_stat.c) can watch
+// a running process: the reference's counters were kernel-global, a
+// userspace engine's are per process.  Layout: StatsShmHeader then Stats.
+static Stats *make_stats() {
+  const char *off = getenv("STROM_STAT_SHM");
+  if (!(off && strcmp(off, "0") == 0)) {
+    char path[96];
+    snprintf(path, sizeof path, "/dev/shm/nvme-strom.%d", (int)getpid());
+    int fd = open(path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+    if (fd >= 0) {
+      size_t len = sizeof(StatsShmHeader) + sizeof(Stats);
+      if (ftruncate(fd, (off_t)len) == 0) {
+        void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (p != MAP_FAILED) {
+          close(fd);
+          auto *h = new (p) StatsShmHeader();
+          h->magic = kStatsShmMagic;
+          h->version = 1;
+          h->pid = getpid();
+          h->stats_bytes = sizeof(Stats);
+          h->tsc_hz_hint = 0;
+          static char saved[96];
+          memcpy(saved, path, sizeof saved);
+          atexit([] { unlink(saved); });
+          return new ((char *)p + sizeof(StatsShmHeader)) Stats();
+        }
+      }
+      close(fd);
+      unlink(path);
+    }
+  }
+  return new Stats();
+}
+
 Stats &stats() {
-  static Stats s;
-  return s;
+  static Stats *s = make_stats();
+  return *s;
 }
 
 // ------------------------------------------------------------- task table

@@ -90,6 +90,21 @@ struct Stats {
 
 Stats &stats();
 
+// Readers (strom_stat, nvme_strom_amd/utils/stat.py) index the export as a
+// flat array of u64: 11 scalars, debug nr[4], debug clk[4], 3 x 48 buckets.
+static_assert(sizeof(Stats) == (11 + 8 + 3 * STROM_HIST_BUCKETS) * 8, "Stats export layout");
+
+// shared-memory export header (/dev/shm/nvme-strom.<pid>), Stats follows
+constexpr uint64_t kStatsShmMagic = 0x53544f524d535431ull;  // "STORMST1"
+struct StatsShmHeader {
+  uint64_t magic;
+  uint32_t version;
+  int32_t pid;
+  uint64_t stats_bytes;
+  uint64_t tsc_hz_hint;
+  uint64_t reserved[4];
+};
+
 // ------------------------------------------------------------- task table
 struct GpuMapping;
 struct DmaBuffer;

@@ -162,7 +162,10 @@ int classify_file(int fd, FileClass *fc, bool strict) {
   int fl = fcntl(fd, F_GETFL);
   if (fl < 0) return -errno;
   if ((fl & O_ACCMODE) == O_WRONLY) return -EBADF;
-  if (!S_ISREG(st.st_mode)) return -ENOTSUP;
+  // directories are accepted too: PostgreSQL probes a tablespace's
+  // database directory (reference pgsql/nvme_strom.c:192-280)
+  const bool is_dir = S_ISDIR(st.st_mode);
+  if (!S_ISREG(st.st_mode) && !is_dir) return -ENOTSUP;
   struct statfs sf;
   if (fstatfs(fd, &sf) != 0) return -errno;
   fc->dev = st.st_dev;
@@ -171,7 +174,7 @@ int classify_file(int fd, FileClass *fc, bool strict) {
   fc->fs_bsize = (uint32_t)sf.f_bsize;
   fc->fs_magic = (uint64_t)sf.f_type;
   fc->fs_name = fs_name_of(fc->fs_magic);
-  if (st.st_size < 4096) return -ENOTSUP;            // i_size >= PAGE_SIZE
+  if (!is_dir && st.st_size < 4096) return -ENOTSUP;  // i_size >= PAGE_SIZE
   if (sf.f_bsize > 4096 && (fc->fs_name == "ext4" || fc->fs_name == "xfs"))
     return -ENOTSUP;                                   // blocksize <= PAGE_SIZE
 

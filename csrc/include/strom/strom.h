@@ -103,6 +103,9 @@ struct strom_heap_scan_args {
 	uint32_t *out_count;     /* device: u32[1], total qualifying */
 	uint32_t *page_status;   /* device: per page bitfield (STROM_PAGE_*) */
 	uint32_t blkno_base;     /* block number of page 0 (checksum input) */
+	const uint32_t *blknos;  /* device, optional: block number per page
+	                            (pages landed out of order); overrides
+	                            blkno_base + page */
 };
 #define STROM_HEAP_VERIFY_CHECKSUM 1u
 #define STROM_HEAP_SKIP_INVISIBLE  2u   /* honour xmin/xmax hint bits */

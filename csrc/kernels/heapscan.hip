@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a) 
       s = fnv_mix(s, 0);
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) s ^= __shfl_xor(s, o, 64);
-      uint32_t c = ((s ^ (a.blkno_base + pg)) % 65535u) + 1u;
+      const uint32_t blkno = a.blknos ? a.blknos[pg] : a.blkno_base + pg;
+      uint32_t c = ((s ^ blkno) % 65535u) + 1u;
       if ((uint16_t)c != pd_checksum) status |= STROM_PAGE_BAD_CHECKSUM;
     }
     if (lane == 0 && a.page_status) a.page_status[pg] = status;

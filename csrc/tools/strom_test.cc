@@ -1,0 +1,255 @@
+// strom_test — SSD→HBM benchmark and correctness test on MI355X
+// (the reference's utils/nvme_test.c, re-designed; same options).
+//
+//   strom_test [-d gpu] [-n nr_segments] [-s segment_MiB] [-b chunk_KiB]
+//              [-c] [-f[KiB]] [-p] [-x passes] FILE
+//
+//   -c      verify every chunk: per-chunk CRC32C computed ON THE GPU compared
+//           with the host CRC of the chunk that landed in that slot (the
+//           reference read the segment back and memcmp'd, with the
+//           src/dst mapping inverted: SURVEY §4 defect #2)
+//   -f[KiB] VFS control: pread into pinned memory + hipMemcpyAsync
+//   -p      print the GPU mapping (LIST/INFO) and exit
+//
+// A ring of nr_segments segments lives in one hipMalloc allocation poisoned
+// with 0x41424344.  MEMCPY_SSD2GPU is issued per segment; page-cache chunks
+// come back in the write-back buffer's tail and are copied to
+// dest + nr_ssd*chunk (the reference copied them to dest + 0: defect #1).
+#include <errno.h>
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <string>
+#include <vector>
+
+#include "strom/strom.h"
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+static double now() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static void die(const char *what) {
+  perror(what);
+  exit(1);
+}
+
+struct Slot {
+  unsigned long task = 0;
+  bool busy = false;
+  std::vector<uint32_t> ids;
+  uint32_t nr_ssd = 0, nr_ram = 0;
+  char *wb = nullptr;
+  hipStream_t st = nullptr;
+};
+
+int main(int argc, char **argv) {
+  int dev = 0, nseg = 6, passes = 1;
+  size_t seg_mib = 32, chunk_kib = 8, vfs_kib = 0;
+  bool check = false, print = false, vfs = false;
+  int opt;
+  while ((opt = getopt(argc, argv, "d:n:s:b:cf::px:")) != -1) {
+    switch (opt) {
+      case 'd': dev = atoi(optarg); break;
+      case 'n': nseg = atoi(optarg); break;
+      case 's': seg_mib = strtoul(optarg, nullptr, 0); break;
+      case 'b': chunk_kib = strtoul(optarg, nullptr, 0); break;
+      case 'c': check = true; break;
+      case 'f': vfs = true; vfs_kib = optarg ? strtoul(optarg, nullptr, 0) : 0; break;
+      case 'p': print = true; break;
+      case 'x': passes = atoi(optarg); break;
+      default:
+        fprintf(stderr,
+                "usage: %s [-d gpu] [-n segments] [-s segment_MiB] [-b chunk_KiB] [-c] [-f[KiB]] "
+                "[-p] [-x passes] FILE\n",
+                argv[0]);
+        return 1;
+    }
+  }
+  if (optind >= argc) {
+    fprintf(stderr, "missing FILE\n");
+    return 1;
+  }
+  const char *path = argv[optind];
+  const size_t seg_sz = seg_mib << 20, chunk = chunk_kib << 10;
+  const uint32_t per_seg = (uint32_t)(seg_sz / chunk);
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) die(path);
+  struct stat sb;
+  fstat(fd, &sb);
+  const size_t fsize = (size_t)sb.st_size;
+
+  strom_check_file cf{};
+  cf.fdesc = fd;
+  if (nvme_strom_ioctl(STROM_IOCTL__CHECK_FILE, &cf) != 0) die("CHECK_FILE");
+
+  int ndev = 0;
+  CK(hipGetDeviceCount(&ndev));
+  if (dev >= ndev) {
+    fprintf(stderr, "GPU %d not present (%d devices)\n", dev, ndev);
+    return 1;
+  }
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, dev));
+  CK(hipSetDevice(dev));
+  void *dbuf = nullptr;
+  CK(hipMalloc(&dbuf, seg_sz * nseg));
+  CK(hipMemsetD32((hipDeviceptr_t)dbuf, 0x41424344, seg_sz * nseg / 4));
+
+  strom_map_gpu_memory mg{};
+  mg.vaddress = (uint64_t)dbuf;
+  mg.length = seg_sz * nseg;
+  if (nvme_strom_ioctl(STROM_IOCTL__MAP_GPU_MEMORY, &mg) != 0) die("MAP_GPU_MEMORY");
+
+  if (print) {
+    std::vector<char> lb(sizeof(strom_list_gpu_memory) + 64 * sizeof(unsigned long));
+    auto *l = (strom_list_gpu_memory *)lb.data();
+    l->nrooms = 64;
+    if (nvme_strom_ioctl(STROM_IOCTL__LIST_GPU_MEMORY, l) != 0) die("LIST_GPU_MEMORY");
+    printf("%u mapped region(s)\n", l->nitems);
+    for (uint32_t i = 0; i < l->nitems && i < 64; ++i) {
+      std::vector<char> ib(sizeof(strom_info_gpu_memory) + 4096 * sizeof(uint64_t));
+      auto *in = (strom_info_gpu_memory *)ib.data();
+      in->handle = l->handles[i];
+      in->nrooms = 4096;
+      if (nvme_strom_ioctl(STROM_IOCTL__INFO_GPU_MEMORY, in) != 0) die("INFO_GPU_MEMORY");
+      printf("handle=%#lx page_sz=%u npages=%u owner=%u map_offset=%lu map_length=%lu\n",
+             in->handle, in->gpu_page_sz, in->nitems, in->owner, in->map_offset, in->map_length);
+      for (uint32_t k = 0; k < in->nitems && k < 4096; ++k)
+        printf("  +%08x: %#016llx\n", k * in->gpu_page_sz, (unsigned long long)in->paddrs[k]);
+    }
+    return 0;
+  }
+
+  std::vector<Slot> ring(nseg);
+  for (auto &s : ring) {
+    CK(hipHostMalloc((void **)&s.wb, seg_sz, hipHostMallocPortable));
+    CK(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+  }
+  uint32_t *d_crc = nullptr;
+  std::vector<uint32_t> h_crc(per_seg);
+  std::vector<char> cbuf(chunk);
+  if (check) CK(hipMalloc((void **)&d_crc, sizeof(uint32_t) * per_seg));
+  uint64_t nr_ram = 0, nr_ssd = 0, nr_submit = 0, nr_blocks = 0, bad = 0, checked = 0;
+  double wait_s = 0;
+
+  auto retire = [&](int k) {
+    Slot &s = ring[k];
+    if (!s.busy) return;
+    double w0 = now();
+    if (!vfs) {
+      strom_memcpy_wait w{};
+      w.dma_task_id = s.task;
+      if (nvme_strom_ioctl(STROM_IOCTL__MEMCPY_WAIT, &w) != 0) {
+        fprintf(stderr, "MEMCPY_WAIT: %s (status %ld)\n", strerror(errno), w.status);
+        exit(1);
+      }
+    }
+    CK(hipStreamSynchronize(s.st));
+    wait_s += now() - w0;
+    if (check) {
+      char *seg = (char *)dbuf + (size_t)k * seg_sz;
+      uint32_t n = (uint32_t)s.ids.size();
+      if (strom_crc32c_chunks(seg, (uint64_t)n * chunk, (uint32_t)chunk, d_crc, s.st) != 0) {
+        fprintf(stderr, "crc kernel launch failed\n");
+        exit(1);
+      }
+      CK(hipMemcpyAsync(h_crc.data(), d_crc, n * 4, hipMemcpyDeviceToHost, s.st));
+      CK(hipStreamSynchronize(s.st));
+      for (uint32_t i = 0; i < n; ++i) {
+        // slot i holds chunk s.ids[i] (landing order)
+        ssize_t got = pread(fd, cbuf.data(), chunk, (off_t)s.ids[i] * chunk);
+        if (got < (ssize_t)chunk) memset(cbuf.data() + (got > 0 ? got : 0), 0, chunk - (got > 0 ? got : 0));
+        if (strom_crc32c_host(0, cbuf.data(), chunk) != h_crc[i]) {
+          if (bad < 8)
+            fprintf(stderr, "corruption: segment %d slot %u chunk %u\n", k, i, s.ids[i]);
+          ++bad;
+        }
+        ++checked;
+      }
+    }
+    s.busy = false;
+  };
+
+  double t0 = now();
+  size_t total = 0;
+  int k = 0;
+  for (int pass = 0; pass < passes; ++pass) {
+    for (size_t off = 0; off < fsize; off += seg_sz, ++k) {
+      int slot = k % nseg;
+      retire(slot);
+      Slot &s = ring[slot];
+      size_t len = std::min(seg_sz, fsize - off);
+      uint32_t n = (uint32_t)((len + chunk - 1) / chunk);
+      char *dst = (char *)dbuf + (size_t)slot * seg_sz;
+      s.ids.resize(n);
+      for (uint32_t i = 0; i < n; ++i) s.ids[i] = (uint32_t)(off / chunk + i);
+      if (vfs) {
+        size_t unit = vfs_kib ? vfs_kib << 10 : len;
+        for (size_t p = 0; p < len; p += unit) {
+          ssize_t got = pread(fd, s.wb + p, std::min(unit, len - p), (off_t)(off + p));
+          if (got < 0) die("pread");
+        }
+        CK(hipMemcpyAsync(dst, s.wb, len, hipMemcpyHostToDevice, s.st));
+        s.nr_ssd = n;
+      } else {
+        strom_memcpy_ssd2gpu a{};
+        a.handle = mg.handle;
+        a.offset = (size_t)slot * seg_sz;
+        a.file_desc = fd;
+        a.nr_chunks = n;
+        a.chunk_sz = (unsigned)chunk;
+        a.relseg_sz = 0;
+        a.chunk_ids = s.ids.data();
+        a.wb_buffer = s.wb;
+        if (nvme_strom_ioctl(STROM_IOCTL__MEMCPY_SSD2GPU, &a) != 0) die("MEMCPY_SSD2GPU");
+        s.task = a.dma_task_id;
+        s.nr_ssd = a.nr_ssd2gpu;
+        s.nr_ram = a.nr_ram2gpu;
+        nr_ram += a.nr_ram2gpu;
+        nr_ssd += a.nr_ssd2gpu;
+        nr_submit += a.nr_dma_submit;
+        nr_blocks += a.nr_dma_blocks;
+        if (a.nr_ram2gpu) {
+          size_t lo = (size_t)a.nr_ssd2gpu * chunk;
+          CK(hipMemcpyAsync(dst + lo, s.wb + lo, (size_t)a.nr_ram2gpu * chunk, hipMemcpyHostToDevice,
+                            s.st));
+        }
+      }
+      s.busy = true;
+      total += len;
+    }
+  }
+  for (int i = 0; i < nseg; ++i) retire((k + i) % nseg);
+  double dt = now() - t0;
+  printf("GPU[%d] %s (%s)\n", dev, prop.name, prop.gcnArchName);
+  printf("file: %s, read: %zu MB, time: %.3f sec, throughput: %.2f GB/s (%.2f GiB/s)\n", path,
+         total >> 20, dt, total / dt / 1e9, total / dt / (1 << 30));
+  printf("mode: %s, segments: %d x %zu MiB, chunk: %zu KiB, wait: %.3f sec\n",
+         vfs ? "VFS (pread+HtoD)" : "SSD2GPU", nseg, seg_mib, chunk_kib, wait_s);
+  if (!vfs)
+    printf("nr_ram2gpu: %llu, nr_ssd2gpu: %llu, average DMA size: %.1f KB\n",
+           (unsigned long long)nr_ram, (unsigned long long)nr_ssd,
+           nr_submit ? 0.5 * nr_blocks / nr_submit : 0.0);
+  if (check) printf("verify: %llu chunks checked, %llu corrupted\n", (unsigned long long)checked,
+                    (unsigned long long)bad);
+  strom_unmap_gpu_memory um{mg.handle};
+  nvme_strom_ioctl(STROM_IOCTL__UNMAP_GPU_MEMORY, &um);
+  return bad ? 2 : 0;
+}

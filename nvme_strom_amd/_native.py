@@ -128,7 +128,7 @@ class HeapScanArgs(C.Structure):
                 ("flags", C.c_uint32), ("attr_off", C.c_int32), ("attr_width", C.c_int32),
                 ("lo", C.c_int64), ("hi", C.c_int64), ("out_items", C.c_void_p),
                 ("out_cap", C.c_uint32), ("out_count", C.c_void_p), ("page_status", C.c_void_p),
-                ("blkno_base", C.c_uint32)]
+                ("blkno_base", C.c_uint32), ("blknos", C.c_void_p)]
 
 
 class DecompDesc(C.Structure):

@@ -28,7 +28,8 @@ import torch
 
 from .. import api
 from ..ops import verify as V
-from ..tensor import FileReader, HbmBuffer
+from ..ops.reorder import chunk_scatter, landing_positions
+from ..tensor import FileReader, HbmBuffer, _sync, host_buffer
 
 
 @dataclass
@@ -64,7 +65,7 @@ class StreamLoader:
         self.chunk_sz = chunk_sz
         self.own_buf = buf is None
         self.buf = buf or HbmBuffer(segment_sz * nr_segments, device)
-        self.wbs = [self.reader._wb] + [torch.empty_like(self.reader._wb, pin_memory=True)
+        self.wbs = [self.reader._wb] + [host_buffer(self.reader._wb.numel())
                                         for _ in range(self.depth - 1)]
         self.stats = StreamStats()
         self.per_seg = segment_sz // chunk_sz
@@ -102,8 +103,15 @@ class StreamLoader:
         w0 = time.perf_counter()
         self.reader.finish(res)
         if res.nr_ram:
+            if not np.array_equal(landed, ids):
+                # page-cache chunks landed at the tail: restore file order
+                lo = slot * self.segment_sz
+                region = dst.tensor[lo:lo + len(ids) * self.chunk_sz]
+                chunk_scatter(region.clone(), region,
+                              landing_positions(ids, landed, res.nr_ssd), self.chunk_sz)
+                landed = ids
             # the write-back slot is reused: its HtoD must be complete
-            torch.cuda.current_stream().synchronize()
+            _sync()
         st.wait_s += time.perf_counter() - w0
         st.nr_ram += res.nr_ram
         st.nr_ssd += res.nr_ssd

@@ -31,7 +31,8 @@ class HeapScanResult:
 def heap_scan(pages: torch.Tensor, page_sz: int = 8192, verify_checksum: bool = False,
               skip_invisible: bool = False, attr_off: int = -1, attr_width: int = 4,
               lo: int = -(1 << 63), hi: int = (1 << 63) - 1, blkno_base: int = 0,
-              out_cap: Optional[int] = None, stream=None) -> HeapScanResult:
+              out_cap: Optional[int] = None, blknos: Optional[torch.Tensor] = None,
+              stream=None) -> HeapScanResult:
     """Scan ``pages`` (uint8, npages*page_sz) for visible LP_NORMAL tuples,
     optionally filtered by lo <= int column at ``attr_off`` (after t_hoff) <= hi."""
     require_cuda(pages, "pages")
@@ -47,7 +48,8 @@ def heap_scan(pages: torch.Tensor, page_sz: int = 8192, verify_checksum: bool = 
     a = N.HeapScanArgs(pages=ptr(pages), npages=npages, page_sz=page_sz, flags=flags,
                        attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi,
                        out_items=ptr(items), out_cap=cap, out_count=ptr(count),
-                       page_status=ptr(status), blkno_base=blkno_base)
+                       page_status=ptr(status), blkno_base=blkno_base,
+                       blknos=ptr(blknos) if blknos is not None else None)
     check(lib().strom_heap_scan(C.byref(a), stream_handle(stream)), "heap_scan")
     n = int(count.item())
     return HeapScanResult(items, min(n, cap), status[:npages])

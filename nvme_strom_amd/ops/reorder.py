@@ -40,6 +40,11 @@ def landing_positions(requested: np.ndarray, landed: np.ndarray, nr_ssd: int) ->
 def chunk_scatter(src: torch.Tensor, dst: torch.Tensor, pos, chunk: int, stream=None) -> None:
     """dst[pos[i]*chunk : +chunk] = src[i*chunk : +chunk] for every landed chunk i."""
     src, dst = as_u8(src), as_u8(dst)
+    if not src.is_cuda and not dst.is_cuda:
+        # host-emulated HBM (CPU tests): same semantics, plain torch indexing
+        p = torch.as_tensor(np.asarray(pos, dtype=np.int64))
+        dst.view(-1, chunk)[p] = src[:len(p) * chunk].view(-1, chunk)
+        return
     require_cuda(src, "src")
     require_cuda(dst, "dst")
     if not isinstance(pos, torch.Tensor):

@@ -21,6 +21,16 @@ from . import api
 from .ops.reorder import chunk_scatter, landing_positions
 
 
+def host_buffer(nbytes: int) -> torch.Tensor:
+    """Write-back / staging host memory: pinned when a GPU is present."""
+    return torch.empty(int(nbytes), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+
+
+def _sync() -> None:
+    if torch.cuda.is_available():
+        torch.cuda.current_stream().synchronize()
+
+
 class HbmBuffer:
     """A device allocation registered with the engine (64 KiB map granule)."""
 
@@ -28,9 +38,11 @@ class HbmBuffer:
                  sess: Optional[api.Session] = None):
         if tensor is None:
             dev = torch.device(device) if device is not None else torch.device("cuda")
+            if dev.type == "cuda" and not torch.cuda.is_available():
+                dev = torch.device("cpu")            # gpu_emulation (CPU tests)
             tensor = torch.empty(int(nbytes), dtype=torch.uint8, device=dev)
-        if not tensor.is_cuda or not tensor.is_contiguous():
-            raise ValueError("HbmBuffer needs a contiguous device tensor")
+        if not tensor.is_contiguous() or (not tensor.is_cuda and api.config_get("gpu_emulation") != "1"):
+            raise ValueError("HbmBuffer needs a contiguous device tensor (or gpu_emulation on CPU)")
         self.tensor = tensor.view(torch.uint8).reshape(-1)
         self.nbytes = self.tensor.numel()
         self.mapping = api.map_gpu_memory(self.tensor.data_ptr(), self.nbytes, sess)
@@ -66,7 +78,7 @@ class FileReader:
         self.sess = sess or api.session()
         self.info = api.check_file(self.fd, self.sess)
         # pinned write-back buffer for page-cache chunks (one per reader)
-        self._wb = torch.empty(max_chunks * chunk_sz, dtype=torch.uint8, pin_memory=True)
+        self._wb = host_buffer(max_chunks * chunk_sz)
         self.max_chunks = max_chunks
 
     @property
@@ -138,13 +150,13 @@ def load_file(path: str, device=None, chunk_sz: int = 1 << 20, window: int = 64 
     nchunks = padded // chunk_sz
     with FileReader(path, chunk_sz=chunk_sz, max_chunks=per_win) as rd:
         # one pinned write-back buffer per in-flight window
-        wbs = [rd._wb] + [torch.empty_like(rd._wb, pin_memory=True) for _ in range(inflight - 1)]
+        wbs = [rd._wb] + [host_buffer(rd._wb.numel()) for _ in range(inflight - 1)]
         pending = []
         dirty = [False] * inflight       # wb slot still feeding an async HtoD
         for k, first in enumerate(range(0, nchunks, per_win)):
             ids = np.arange(first, min(nchunks, first + per_win), dtype=np.uint32)
             if dirty[k % inflight]:
-                torch.cuda.current_stream().synchronize()
+                _sync()
                 dirty = [False] * inflight
             res, landed = rd.submit(buf, first * chunk_sz, ids, wb=wbs[k % inflight])
             dirty[k % inflight] = res.nr_ram > 0
@@ -159,5 +171,5 @@ def load_file(path: str, device=None, chunk_sz: int = 1 << 20, window: int = 64 
                 rd.finish(pending.pop(0))
         for res in pending:
             rd.finish(res)
-    torch.cuda.current_stream().synchronize()
+    _sync()
     return buf.tensor[:size]

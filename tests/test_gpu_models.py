@@ -1,0 +1,82 @@
+"""GPU pipelines: PG heap relation scan vs the CPU executor, Arrow IPC scan vs
+pyarrow, multi-window fan-out at world size 1."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def S():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import nvme_strom_amd as S
+    S.configure(gpu_emulation=0)
+    return S
+
+
+def test_pg_relation_scan_gpu_vs_cpu(S, tmp_path):
+    from nvme_strom_amd.models import pg_scan
+    from nvme_strom_amd.utils import pgpage
+    rng = np.random.default_rng(0)
+    vals = rng.integers(-5000, 5000, 30000).astype(np.int64)
+    data = pgpage.build_table(vals, per_page=150, width=8, invisible_every=9)
+    rel = pg_scan.Relation.write(str(tmp_path / "24576"), data, relseg_size=64)
+    # warm a few blocks so some chunks take the page-cache (RAM) path
+    fd = os.open(rel.segments[1], os.O_RDONLY)
+    os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)
+    for b in (3, 4, 5, 40):
+        os.pread(fd, 8192, b * 8192)
+    os.close(fd)
+    cfg = pg_scan.ScanConfig(chunk_size=16 * 8192, buffer_size=64 * 8192, verify_checksum=True)
+    for workers in (1, 3):
+        g = pg_scan.HeapRelationScan(rel, cfg, "cuda", attr_off=0, attr_width=8, lo=-100,
+                                     hi=2500).run(workers)
+        c = pg_scan.cpu_scan(rel, cfg, attr_off=0, attr_width=8, lo=-100, hi=2500)
+        assert np.array_equal(g.items, c.items)
+        assert g.bad_pages == 0 and g.pages == rel.nblocks
+
+
+def test_arrow_scan_lz4(S, tmp_path):
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+    rng = np.random.default_rng(3)
+    n, nb = 250_000, 5
+    a = rng.integers(-10**6, 10**6, n * nb)
+    b = rng.random(n * nb)
+    mask = rng.random(n * nb) < 0.05
+    tbl = pa.table({"a": pa.array(a, type=pa.int64()),
+                    "b": pa.array(b, type=pa.float64(), mask=mask),
+                    "s": pa.array([str(x % 100) for x in range(n * nb)])})
+    path = str(tmp_path / "t.arrow")
+    for comp in ("lz4", None):
+        with ipc.new_file(path, tbl.schema, options=ipc.IpcWriteOptions(compression=comp)) as w:
+            for k in range(nb):
+                w.write_batch(tbl.slice(k * n, n).to_batches()[0])
+        sc = ArrowScan(path, "cuda")
+        out = sc.filter("a", -1000, 5000)
+        ref = np.nonzero((a >= -1000) & (a <= 5000))[0]
+        assert out.selected == len(ref)
+        assert np.array_equal(out.indices.cpu().numpy(), ref)
+        out = sc.filter("b", 0.25, 0.5)
+        ref = np.nonzero((b >= 0.25) & (b <= 0.5) & ~mask)[0]
+        assert np.array_equal(out.indices.cpu().numpy(), ref)
+        sc.close()
+
+
+def test_sharded_loader_single_rank(S, tmp_path):
+    from nvme_strom_amd.parallel import ShardedLoader
+    data = np.random.default_rng(1).integers(0, 256, 16 << 20, dtype=np.uint8)
+    p = str(tmp_path / "s.bin")
+    data.tofile(p)
+    ld = ShardedLoader(p, 4 << 20, torch.device("cuda"), segment_sz=1 << 20, depth=3)
+    for i in range(5):
+        ld.step(i)
+        ld.flush()
+        exp = data[(i % 4) * (4 << 20):][:4 << 20]
+        assert np.array_equal(ld.current(i).cpu().numpy(), exp)
+    ld.close()

@@ -1,0 +1,107 @@
+"""Pipelines on CPU: SSD2RAM stream, PG scan planner pieces + CPU executor,
+stream loader order restoration with page-cache chunks (emulated HBM)."""
+import os
+
+import numpy as np
+import pytest
+
+import nvme_strom_amd as S
+from nvme_strom_amd.models import pg_scan
+from nvme_strom_amd.models.ssd2ram_stream import ssd2ram_run
+from nvme_strom_amd.utils import pgpage
+
+
+def test_ssd2ram_stream_verified(strom, rand_file):
+    path, data = rand_file(24 << 20)
+    st = ssd2ram_run(path, nthreads=3, unit=1 << 20, buffer_sz=6 << 20, verify=True,
+                     bind_numa=False)
+    assert st.mismatches == 0
+    assert st.nr_ssd + st.nr_ram == (24 << 20) // 8192
+    assert st.bytes == 24 << 20
+
+
+def test_stream_loader_restores_order_with_cached_chunks(strom, rand_file):
+    import torch
+    from nvme_strom_amd.models.ssd2gpu_stream import StreamLoader
+    path, data = rand_file(8 << 20, evict=False)           # fully cached
+    ld = StreamLoader(path, segment_sz=2 << 20, nr_segments=4, chunk_sz=8192, device="cpu", depth=2)
+    st = ld.run(0, 8 << 20)
+    assert st.nr_ram > 0
+    assert np.array_equal(ld.buf.tensor.numpy(), data)
+    ld.close()
+
+
+def test_planner_threshold_and_cost():
+    cfg = pg_scan.ScanConfig()
+    gib = 1 << 30
+    thr = pg_scan.strom_threshold(64 * gib, 8 * gib)
+    assert thr == (56 * gib) * 2 // 3 + 8 * gib
+    assert not pg_scan.use_strom(thr - 1, 64 * gib, 8 * gib, cfg, True)
+    assert pg_scan.use_strom(thr, 64 * gib, 8 * gib, cfg, True)
+    assert not pg_scan.use_strom(thr, 64 * gib, 8 * gib, cfg, False)
+    cfg.debug_no_threshold = True
+    assert pg_scan.use_strom(1, 64 * gib, 8 * gib, cfg, True)
+    assert pg_scan.scan_cost(1000, cfg, 2) < pg_scan.scan_cost(1000, cfg, 0)
+    with pytest.raises(ValueError):
+        pg_scan.ScanConfig(chunk_size=1000).validate()
+
+
+def test_tablespace_cache(strom, tmp_path):
+    c = pg_scan.TablespaceCache()
+    assert c.can_use(str(tmp_path)) is True
+    assert c.can_use(str(tmp_path / "missing")) is False
+    c.invalidate()
+    assert c.can_use(str(tmp_path)) is True
+
+
+def test_parallel_cursor_boundaries():
+    cur = pg_scan.ParallelCursor(100)
+    got = []
+    while True:
+        lo, n = cur.claim(16, boundary=40)
+        if not n:
+            break
+        got.append((lo, n))
+        assert lo // 40 == (lo + n - 1) // 40
+    assert sum(n for _, n in got) == 100
+
+
+def test_cpu_scan_segments_and_filter(strom, tmp_path):
+    vals = np.arange(2000, dtype=np.int64)
+    data = pgpage.build_table(vals, per_page=100, width=8, invisible_every=10)   # 20 pages
+    rel = pg_scan.Relation.write(str(tmp_path / "16384"), data, relseg_size=8)    # 3 segment files
+    assert len(rel.segments) == 3 and rel.nblocks == 20
+    cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192, verify_checksum=True)
+    r = pg_scan.cpu_scan(rel, cfg, attr_off=0, attr_width=8, lo=100, hi=299)
+    exp = [v for v in range(100, 300) if v % 10 != 0]
+    assert r.ntuples == len(exp) and r.bad_pages == 0
+    blocks = (r.items >> np.uint64(16)).astype(int)
+    assert set(blocks.tolist()) == {1, 2}
+
+
+def test_arrow_ipc_metadata(tmp_path):
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.utils.arrow_ipc import read_metadata
+    n = 10000
+    a = np.arange(n, dtype=np.int64) * 3
+    tbl = pa.table({"s": pa.array([str(i) for i in range(n)]), "a": a,
+                    "f": pa.array(np.linspace(0, 1, n), type=pa.float32()),
+                    "l": pa.array([[i, i + 1] for i in range(n)])})
+    for comp in (None, "lz4"):
+        path = str(tmp_path / f"m_{comp}.arrow")
+        with ipc.new_file(path, tbl.schema, options=ipc.IpcWriteOptions(compression=comp)) as w:
+            for k in range(4):
+                w.write_batch(tbl.slice(k * 2500, 2500).to_batches()[0])
+        m = read_metadata(path)
+        assert [c.name for c in m.schema] == ["s", "a", "f", "l"]
+        assert [c.supported for c in m.schema] == [False, True, True, False]
+        assert m.schema[2].numpy_dtype == "f4"
+        assert len(m.batches) == 4 and all(b.length == 2500 for b in m.batches)
+        assert m.batches[0].codec == (None if comp is None else "lz4_frame")
+        if comp is None:
+            raw = np.fromfile(path, dtype=np.uint8)
+            for k, b in enumerate(m.batches):
+                ref = b.columns[1].data
+                vals = raw[ref.offset:ref.offset + 2500 * 8].view(np.int64)
+                assert np.array_equal(vals, a[k * 2500:(k + 1) * 2500])
