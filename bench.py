@@ -176,17 +176,16 @@ def main() -> int:
     # p50/p99 latency of single 4 KiB reads into HBM (QD1, O_DIRECT path)
     lat = []
     if a.lat_samples:
-        rd = FileReader(path, chunk_sz=4096, max_chunks=1)
+        S.evict_file(fd)
         rng = np.random.default_rng(rank)
-        ids = rng.integers(0, F // 4096, size=a.lat_samples + 50).astype(np.uint32)
-        for j, cid in enumerate(ids):
+        offs = (rng.integers(0, F // 4096, size=a.lat_samples + 50) * 4096).tolist()
+        S.stat_hist(reset=True)
+        for j, off in enumerate(offs):
             t1 = time.perf_counter_ns()
-            res, _ = rd.submit(buf, 0, np.array([cid], dtype=np.uint32))
-            rd.finish(res)
+            S.pread_gpu(buf.handle, 0, fd, off, 4096)
             t2 = time.perf_counter_ns()
             if j >= 50:
                 lat.append((t2 - t1) / 1e3)
-        rd.close()
     lat = np.array(lat) if lat else np.array([float("nan")])
     p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
 

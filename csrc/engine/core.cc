@@ -33,7 +33,8 @@ static bool parse_bool(const std::string &v) {
 Config Config::from_env() {
   Config c;
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
-                               "staging_slots", "strict", "direct_io",
+                               "staging_slots", "inline_max", "bar_map", "bar_max",
+                               "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind",
                                "stat_info", "verbose"};
   for (const char *k : keys) {
@@ -69,6 +70,17 @@ int Config::set(const std::string &k, const std::string &v) {
     return 0;
   }
   if (k == "staging_slots") { if (n < 1 || n > 1024) return -EINVAL; staging_slots = (int)n; return 0; }
+  if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
+  if (k == "bar_max") {
+    if (n < 0 || n > (64l << 20)) return -EINVAL;
+    bar_max = (uint32_t)n;
+    return 0;
+  }
+  if (k == "inline_max") {
+    if (n < 0 || n > (16l << 20) || (n & 4095)) return -EINVAL;
+    inline_max = (uint32_t)n;
+    return 0;
+  }
   if (k == "stat_info") { stat_info = (int)n; return 0; }
   if (k == "verbose") { verbose = (int)n; return 0; }
   return -ENOENT;
@@ -85,6 +97,9 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "queue_depth") v = queue_depth;
   else if (k == "max_request") v = max_request;
   else if (k == "staging_slots") v = staging_slots;
+  else if (k == "inline_max") v = inline_max;
+  else if (k == "bar_map") v = bar_map;
+  else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;
   else if (k == "direct_io") v = direct_io;
   else if (k == "pgcache_probe") v = pgcache_probe;

@@ -17,6 +17,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include <algorithm>
 
@@ -266,7 +267,16 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   ChunkPlan plan;
   int rc = plan_chunks(pp, &plan);
   if (rc) return rc;
-  if (plan.nr_ram && !a->wb_buffer) return -EFAULT;
+  // MI355X extension: wb_buffer == NULL asks the engine to put page-cache
+  // chunks straight into HBM (buffered reads into the large-BAR mapping);
+  // they still land at the tail and are reported as nr_ram2gpu.
+  char *ram_dest = a->wb_buffer;
+  if (plan.nr_ram && !ram_dest) {
+    uint64_t dva = gmap->va + a->offset;
+    if (!gmap->bar || dva < gmap->bar_va || dva + bytes > gmap->bar_va + gmap->bar_len)
+      return -EFAULT;
+    ram_dest = (char *)gmap->bar + (dva - gmap->bar_va);
+  }
 
   Task *t = tasks().create(session);
   t->gmap = gmap;
@@ -275,12 +285,21 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, gmap.get(),
                  gmap->va + a->offset, host_dest, &reqs);
   uint64_t t0 = tsc_now();
-  io_->submit(reqs);
+  if (reqs.size() == 1 && reqs[0].len <= config().inline_max)
+    io_->run_inline(reqs[0]);
+  else
+    io_->submit(reqs);
   stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
   stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
 
   // page-cache chunks overlap with the storage reads
-  if (plan.nr_ram) rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, a->wb_buffer);
+  if (plan.nr_ram) {
+    rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, ram_dest);
+    if (rc == 0 && !a->wb_buffer) {
+      _mm_sfence();
+      (void)*(volatile uint32_t *)ram_dest;  // flush posted BAR writes
+    }
+  }
   t->frozen = true;
   uint64_t id = t->id;
   tasks().put(t, rc);
@@ -333,7 +352,10 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, nullptr,
                  (uint64_t)a->dest_uaddr, true, &reqs);
   uint64_t t0 = tsc_now();
-  io_->submit(reqs);
+  if (reqs.size() == 1 && reqs[0].len <= config().inline_max)
+    io_->run_inline(reqs[0]);
+  else
+    io_->submit(reqs);
   stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
   stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
   if (plan.nr_ram)
@@ -474,6 +496,85 @@ int nvme_strom_ioctl(unsigned long cmd, const void *arg) {
     return -1;
   }
   return r;
+}
+
+long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
+                     uint64_t file_off, uint64_t len) {
+  if ((file_off | len) & 4095) return -EINVAL;
+  if (len == 0) return 0;
+  // one chunk per request-sized piece when aligned, else 4 KiB chunks
+  uint32_t chunk = 4096;
+  for (uint32_t c = config().max_request; c > 4096; c >>= 1)
+    if (file_off % c == 0 && len % c == 0) {
+      chunk = c;
+      break;
+    }
+  uint64_t n = len / chunk;
+  if (n > (1u << 24) || (file_off / chunk + n) > 0xffffffffull) return -E2BIG;
+  std::vector<uint32_t> ids(n);
+  for (uint64_t i = 0; i < n; ++i) ids[i] = (uint32_t)(file_off / chunk + i);
+  auto gmap = gpu_registry().get(handle);
+  if (!gmap) return -ENOENT;
+  strom_memcpy_ssd2gpu a{};
+  a.handle = handle;
+  a.offset = offset;
+  a.file_desc = fd;
+  a.nr_chunks = (unsigned)n;
+  a.chunk_sz = chunk;
+  a.chunk_ids = ids.data();
+  // page-cache chunks: straight into HBM when BAR-mapped, else a bounce
+  std::vector<char> wb;
+  if (!gmap->bar) {
+    wb.resize(len);
+    a.wb_buffer = wb.data();
+  }
+  int rc = strom_ioctl(session, STROM_IOCTL__MEMCPY_SSD2GPU, &a);
+  if (rc) return rc;
+  strom_memcpy_wait w{};
+  w.dma_task_id = a.dma_task_id;
+  rc = strom_ioctl(session, STROM_IOCTL__MEMCPY_WAIT, &w);
+  if (rc) return rc;
+  if (a.nr_ram2gpu) {
+    // restore file order: storage chunks sit packed at the head in request
+    // order, page-cache chunks fill the tail backwards
+    uint64_t dva = gmap->va + offset;
+    const bool host = gmap->device < 0;  // emulated GPU memory (CPU tests)
+    auto hipMemcpyDtoH_wrap = [&](void *dst, uint64_t src, size_t nb) -> int {
+      if (host) {
+        memcpy(dst, (const void *)src, nb);
+        return 0;
+      }
+      return hip::copy_dtoh(dst, src, nb);
+    };
+    auto hipMemcpyHtoD_wrap = [&](uint64_t dst, const void *src, size_t nb) -> int {
+      if (host) {
+        memcpy((void *)dst, src, nb);
+        return 0;
+      }
+      return hip::copy_htod(dst, src, nb);
+    };
+    std::vector<char> tmp(len);
+    const char *src = gmap->bar ? (const char *)gmap->bar + (dva - gmap->bar_va) : nullptr;
+    if (!src) {
+      // storage part is in HBM, cached part in wb: assemble on the host
+      if (hipMemcpyDtoH_wrap(tmp.data(), dva, (size_t)a.nr_ssd2gpu * chunk) != 0) return -EIO;
+      memcpy(tmp.data() + (size_t)a.nr_ssd2gpu * chunk, wb.data() + (size_t)a.nr_ssd2gpu * chunk,
+             (size_t)a.nr_ram2gpu * chunk);
+    } else {
+      memcpy(tmp.data(), src, len);  // BAR reads are slow but this is the rare path
+    }
+    std::vector<char> out(len);
+    for (uint64_t i = 0; i < n; ++i) {
+      uint64_t pos = ids[i] - file_off / chunk;
+      memcpy(out.data() + pos * chunk, tmp.data() + i * chunk, chunk);
+    }
+    if (gmap->bar) {
+      if (!gmap->bar_write(dva, out.data(), len)) return -EIO;
+    } else if (hipMemcpyHtoD_wrap(dva, out.data(), len) != 0) {
+      return -EIO;
+    }
+  }
+  return (long)len;
 }
 
 int strom_config_set(const char *key, const char *value) {

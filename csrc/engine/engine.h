@@ -46,7 +46,10 @@ struct Config {
   int workers = 4;               // I/O worker threads (one SDMA stream each)
   int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
-  int staging_slots = 8;         // pinned slots per worker (GPU dest)
+  int staging_slots = 4;         // pinned slots per worker (GPU dest)
+  uint32_t inline_max = 64u << 10;  // single requests up to this run inline
+  bool bar_map = true;           // CPU-map HBM through the large BAR (dma-buf)
+  uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks
   bool pgcache_probe = true;     // residency scoring (mincore)
@@ -157,7 +160,17 @@ struct GpuMapping {
   uid_t owner = 0;
   int dmabuf_fd = -1;
   uint32_t version = 1;
+  // Large-BAR CPU mapping of the range (dma-buf export + mmap), or null.
+  // bar_va is the device VA that bar[0] aliases.
+  uint8_t *bar = nullptr;
+  uint64_t bar_va = 0;
+  size_t bar_len = 0;
   std::atomic<int> inflight{0};
+  // CPU store of [src, src+len) into HBM at device VA dst through the BAR;
+  // false when the range is not BAR-mapped.  Ends with a read-back that
+  // flushes the posted writes, so the data is in HBM when this returns.
+  bool bar_write(uint64_t dst, const void *src, size_t len) const;
+  ~GpuMapping();
   bool detached = false;
   std::mutex mu;
   std::condition_variable cv;
@@ -289,6 +302,9 @@ class IoEngine {
   explicit IoEngine(const Config &cfg);
   ~IoEngine();
   void submit(std::vector<IoReq> &reqs);
+  // Small single-request tasks run on the caller's thread (no worker
+  // hand-off, no WAIT wake-up): the 4 KiB latency path.
+  void run_inline(IoReq &r);
   int workers() const { return (int)workers_.size(); }
 
   struct Worker;
@@ -324,6 +340,12 @@ void *host_alloc(size_t bytes);            // pinned, portable
 void host_free(void *p);
 void *host_alloc_thp(size_t bytes);        // THP-backed, hipHostRegister'ed
 void host_free_thp(void *p, size_t bytes);
+// CPU mapping of device memory [va, va+len) through its dma-buf export;
+// returns the mapping (and sets *map_va/*map_len to what it covers) or null.
+uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len);
+void bar_unmap(uint8_t *p, size_t len);
+int copy_dtoh(void *dst, uint64_t src, size_t len);   // synchronous, 0 / -EIO
+int copy_htod(uint64_t dst, const void *src, size_t len);
 int numa_node_of_device(int device);
 }  // namespace hip
 

@@ -6,9 +6,12 @@
 // calling thread's NUMA policy (hipHostMallocNumaUser), which the I/O
 // workers set to the node of the GPU's PCIe root before allocating.
 #include <hip/hip_runtime.h>
+#include <errno.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <unistd.h>
+#include <x86intrin.h>
 
 #include <cctype>
 #include <mutex>
@@ -104,6 +107,66 @@ void host_free_thp(void *p, size_t bytes) {
   size_t len = (bytes + huge - 1) / huge * huge;
   (void)hipHostUnregister(p);
   munmap(p, len);
+}
+
+uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
+  // Export the WHOLE allocation (caching allocators sub-allocate tensors
+  // inside larger hipMalloc blocks) and map the page-aligned cover of the
+  // range at its offset inside the export.
+  const uint64_t page = 4096;
+  hipDeviceptr_t abase = nullptr;
+  size_t asize = 0;
+  if (hipMemGetAddressRange(&abase, &asize, (hipDeviceptr_t)va) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  uint64_t base = (uint64_t)abase;
+  uint64_t lo = va & ~(page - 1);
+  uint64_t hi = (va + len + page - 1) & ~(page - 1);
+  if (lo < base || hi > base + ((asize + page - 1) & ~(page - 1))) return nullptr;
+  int fd = -1;
+  if (hipMemGetHandleForAddressRange(&fd, abase, asize, hipMemRangeHandleTypeDmaBufFd, 0) !=
+          hipSuccess ||
+      fd < 0) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  void *p = mmap(nullptr, hi - lo, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)(lo - base));
+  close(fd);  // the mapping keeps the dma-buf alive
+  if (p == MAP_FAILED) return nullptr;
+  // Self-check with a canary: the CPU alias must be the bytes the GPU sees.
+  uint8_t *q = (uint8_t *)p + (va - lo);
+  uint64_t orig = 0, canary = 0x5354524f4d424152ull ^ va, back = 0;
+  bool ok = hipMemcpy(&orig, (void *)va, 8, hipMemcpyDeviceToHost) == hipSuccess;
+  if (ok) {
+    memcpy(q, &canary, 8);
+    _mm_sfence();
+    (void)*(volatile uint32_t *)q;
+    ok = hipMemcpy(&back, (void *)va, 8, hipMemcpyDeviceToHost) == hipSuccess && back == canary;
+    memcpy(q, &orig, 8);
+    _mm_sfence();
+    (void)*(volatile uint32_t *)q;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
+    munmap(p, hi - lo);
+    return nullptr;
+  }
+  *map_va = lo;
+  *map_len = hi - lo;
+  return (uint8_t *)p;
+}
+
+void bar_unmap(uint8_t *p, size_t len) {
+  if (p) munmap(p, len);
+}
+
+int copy_dtoh(void *dst, uint64_t src, size_t len) {
+  return hipMemcpy(dst, (const void *)src, len, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
+}
+
+int copy_htod(uint64_t dst, const void *src, size_t len) {
+  return hipMemcpy((void *)dst, src, len, hipMemcpyHostToDevice) == hipSuccess ? 0 : -EIO;
 }
 
 int numa_node_of_device(int device) {

@@ -155,6 +155,19 @@ static long pread_full(int fd, uint8_t *buf, uint32_t len, uint64_t off) {
   return done;
 }
 
+// Post-process a storage read of `len` bytes into dst that returned `got`
+// (bytes or -errno): O_DIRECT refusal falls back to a buffered read, a read
+// shorter than the bytes before EOF is an error, the tail past EOF is
+// zero-filled.  Returns 0 or -errno.
+static long finalize_read(const IoReq &r, uint8_t *dst, uint32_t len, long got) {
+  if (got == -EINVAL && r.fd_buffered >= 0 && r.fd_buffered != r.fd)
+    got = pread_full(r.fd_buffered, dst, len, r.off);
+  if (got < 0) return got;
+  if ((uint32_t)got < r.valid) return -EIO;
+  if ((uint32_t)got < r.len) memset(dst + got, 0, r.len - (uint32_t)got);
+  return 0;
+}
+
 // ------------------------------------------------------------------ worker
 struct IoEngine::Worker {
   struct Slot {
@@ -264,17 +277,7 @@ struct IoEngine::Worker {
     IoReq &r = c.req;
     uint64_t now = mono_ns();
     stats().io_ns.add(now - c.t0);
-    long status = 0;
-    if (got == -EINVAL && r.fd_buffered >= 0 && r.fd_buffered != r.fd) {
-      // O_DIRECT refused (buffer alignment / filesystem): redo buffered
-      got = pread_full(r.fd_buffered, c.dst, c.len, r.off);
-    }
-    if (got < 0) {
-      status = got;
-    } else if ((uint32_t)got < r.valid) {
-      status = -EIO;  // short read before EOF
-    }
-    if (status == 0 && (uint32_t)got < r.len) memset(c.dst + got, 0, r.len - (uint32_t)got);
+    long status = finalize_read(r, c.dst, c.len, got);
     if (c.slot < 0) {
       finish_request(r, status);
       return;
@@ -283,6 +286,13 @@ struct IoEngine::Worker {
     if (status != 0) {
       free_slots.push_back(c.slot);
       finish_request(r, status);
+      return;
+    }
+    if (r.len <= cfg.bar_max && r.gmap && r.gmap->bar_write(r.gpu_dst, c.dst, r.len)) {
+      // small request: CPU stores through the large BAR beat an SDMA round trip
+      stats().copy_ns.add(mono_ns() - now);
+      free_slots.push_back(c.slot);
+      finish_request(r, 0);
       return;
     }
     hipStream_t st = stream_for(r.device);
@@ -469,6 +479,63 @@ IoEngine::~IoEngine() {
     w->cv.notify_all();
   }
   for (auto &w : workers_) w->th.join();
+}
+
+// Per-thread resources of the inline path.  Never freed: the HIP runtime
+// may already be gone when a thread-local destructor would run at exit.
+struct InlineCtx {
+  uint8_t *buf = nullptr;
+  size_t cap = 0;
+  int dev = -1;
+  hipStream_t st = nullptr;
+  hipEvent_t ev = nullptr;
+};
+static thread_local InlineCtx tl_inline;
+
+void IoEngine::run_inline(IoReq &r) {
+  InlineCtx &c = tl_inline;
+  uint32_t len = r.len;
+  int frc = faults().on_request(&len);
+  uint64_t t0 = mono_ns();
+  if (r.host_dst) {
+    long got = frc ? frc : pread_full(r.fd, r.host_dst, len, r.off);
+    stats().io_ns.add(mono_ns() - t0);
+    finish_request(r, finalize_read(r, r.host_dst, len, got));
+    return;
+  }
+  if (c.cap < r.len) {
+    size_t cap = std::max<size_t>(r.len, 64u << 10);
+    uint8_t *b = (uint8_t *)hip::host_alloc_thp(cap);
+    if (!b) b = (uint8_t *)hip::host_alloc(cap);
+    if (!b) {
+      finish_request(r, -ENOMEM);
+      return;
+    }
+    c.buf = b;  // the old buffer (if any) is leaked on purpose: it is small
+    c.cap = cap;
+  }
+  long got = frc ? frc : pread_full(r.fd, c.buf, len, r.off);
+  uint64_t t1 = mono_ns();
+  stats().io_ns.add(t1 - t0);
+  long status = finalize_read(r, c.buf, len, got);
+  if (status == 0 && r.len <= config().bar_max && r.gmap &&
+      r.gmap->bar_write(r.gpu_dst, c.buf, r.len)) {
+    stats().copy_ns.add(mono_ns() - t1);
+    stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+  } else if (status == 0) {
+    if (c.dev != r.device) {
+      (void)hipSetDevice(r.device);
+      (void)hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking);
+      (void)hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+      c.dev = r.device;
+    }
+    hipError_t e = hipMemcpyAsync((void *)r.gpu_dst, c.buf, r.len, hipMemcpyHostToDevice, c.st);
+    if (e == hipSuccess) e = hipStreamSynchronize(c.st);
+    if (e != hipSuccess) status = -EIO;
+    stats().copy_ns.add(mono_ns() - t1);
+    stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+  }
+  finish_request(r, status);
 }
 
 void IoEngine::submit(std::vector<IoReq> &reqs) {

@@ -24,6 +24,7 @@
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include <fstream>
 #include <sstream>
@@ -40,6 +41,18 @@
 namespace strom {
 
 // ------------------------------------------------------- GPU registry
+GpuMapping::~GpuMapping() { hip::bar_unmap(bar, bar_len); }
+
+bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len) const {
+  if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
+  uint8_t *p = bar + (dst - bar_va);
+  memcpy(p, src, len);
+  _mm_sfence();
+  // a read from the device cannot pass the posted writes before it
+  (void)*(volatile uint32_t *)(p + ((len - 1) & ~(size_t)3));
+  return true;
+}
+
 int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memory *out) {
   if (va == 0 || len == 0) return -EINVAL;
   if (va + len < va) return -EINVAL;
@@ -63,6 +76,10 @@ int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memor
   m->dmabuf_fd = dmabuf_fd;
   uint64_t npages = (m->map_length + STROM_GPU_BOUND_SIZE - 1) >> STROM_GPU_BOUND_SHIFT;
   if (npages > 0xffffffffull) return -E2BIG;
+  if (device >= 0 && config().bar_map) {
+    m->bar = hip::bar_map(va, len, &m->bar_va, &m->bar_len);
+    STROM_LOG(1, "bar map of %#lx: %s", (unsigned long)va, m->bar ? "yes" : "no");
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     m->handle = ++next_;

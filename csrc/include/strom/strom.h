@@ -31,6 +31,13 @@ int strom_ioctl(int session, unsigned long cmd, void *arg);
  * returns 0 / -1 with errno set. */
 int nvme_strom_ioctl(unsigned long cmd, const void *arg);
 
+/* Synchronous "pread into HBM": [file_off, file_off+len) of fd lands at
+ * offset of a mapped GPU range, through the same engine path as
+ * MEMCPY_SSD2GPU + WAIT (page-cache pages included, in file order).
+ * file_off and len must be 4 KiB multiples.  Returns len or -errno. */
+long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
+                     uint64_t file_off, uint64_t len);
+
 /* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
 int strom_config_set(const char *key, const char *value);
 int strom_config_get(const char *key, char *buf, size_t buflen);

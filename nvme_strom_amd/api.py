@@ -287,6 +287,15 @@ def memcpy_ssd2ram(dest_addr: int, fd: int, chunk_ids, chunk_sz: int, relseg_sz:
     return CopyResult(a.dma_task_id, a.nr_ram2ram, a.nr_ssd2ram, a.nr_dma_submit, a.nr_dma_blocks)
 
 
+def pread_gpu(handle: int, offset: int, fd: int, file_off: int, length: int,
+              sess: Optional[Session] = None) -> int:
+    """Synchronous read of file bytes into a mapped GPU range, file order
+    preserved (MEMCPY_SSD2GPU + WAIT in one native call)."""
+    s = sess or session()
+    return _check(s.lib.strom_pread_gpu(s.sid, handle, offset, fd, file_off, length),
+                  "pread_gpu")
+
+
 def memcpy_wait(task_id: int, timeout: Optional[float] = None,
                 sess: Optional[Session] = None) -> None:
     """Block until the task finishes; raises StromError(EIO, status=...) on a

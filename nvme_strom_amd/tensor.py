@@ -11,6 +11,7 @@ with several ioctls in flight (the PAR3 ring of SURVEY §2.3).
 """
 from __future__ import annotations
 
+import errno
 import os
 from typing import Optional, Sequence
 
@@ -69,7 +70,8 @@ class FileReader:
     """MEMCPY_SSD2GPU driver for one file."""
 
     def __init__(self, path: str, chunk_sz: int = 8192, relseg_sz: int = 0,
-                 max_chunks: int = 4096, sess: Optional[api.Session] = None):
+                 max_chunks: int = 4096, sess: Optional[api.Session] = None,
+                 direct_ram: bool = True):
         self.path = path
         self.fd = os.open(path, os.O_RDONLY)
         self.size = os.fstat(self.fd).st_size
@@ -77,9 +79,11 @@ class FileReader:
         self.relseg_sz = relseg_sz
         self.sess = sess or api.session()
         self.info = api.check_file(self.fd, self.sess)
-        # pinned write-back buffer for page-cache chunks (one per reader)
+        # pinned write-back buffer for page-cache chunks (one per reader);
+        # unused while the engine can write them into HBM itself (BAR)
         self._wb = host_buffer(max_chunks * chunk_sz)
         self.max_chunks = max_chunks
+        self._direct_ram = None if direct_ram else False
 
     @property
     def nchunks(self) -> int:
@@ -90,6 +94,19 @@ class FileReader:
         ``finish()`` it.  ``wb`` overrides the reader's write-back buffer
         (needed when several submissions are in flight)."""
         ids = np.array(chunk_ids, dtype=np.uint32, copy=True)
+        if self._direct_ram is not False:
+            # page-cache chunks straight into HBM through the large BAR
+            try:
+                res = api.memcpy_ssd2gpu(buf.handle, offset, self.fd, ids, self.chunk_sz,
+                                         self.relseg_sz, 0, self.sess)
+                if res.nr_ram:
+                    self._direct_ram = True
+                return res, ids
+            except api.StromError as e:
+                if e.errno != errno.EFAULT:
+                    raise
+                self._direct_ram = False
+                ids = np.array(chunk_ids, dtype=np.uint32, copy=True)
         if len(ids) > self.max_chunks and wb is None:
             raise ValueError("too many chunks for the write-back buffer")
         wbt = self._wb if wb is None else wb

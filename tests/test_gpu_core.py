@@ -141,6 +141,28 @@ def test_map_real_hbm_and_info(S):
         S.map_gpu_memory(h.ctypes.data, h.nbytes)
 
 
+def test_pread_gpu_mixed_cache(S, tmp_path):
+    """pread_gpu keeps file order even when some pages come from the page
+    cache (landed at the tail, written through the BAR when available)."""
+    from nvme_strom_amd.tensor import HbmBuffer
+    p, data = _mkfile(tmp_path, 4 << 20, seed=11)
+    fd = os.open(p, os.O_RDONLY)
+    os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)
+    for pg in (1, 2, 7, 60, 61):
+        os.pread(fd, 4096, (256 + pg) * 4096)
+    with HbmBuffer(2 << 20, "cuda") as hb:
+        for bar in (1, 0):
+            S.configure(bar_map=bar)
+            hb2 = HbmBuffer(2 << 20, "cuda")
+            n = S.pread_gpu(hb2.handle, 4096, fd, 256 * 4096, 128 * 4096)
+            assert n == 128 * 4096
+            got = hb2.tensor[4096:4096 + n].cpu().numpy()
+            assert np.array_equal(got, data[256 * 4096:256 * 4096 + n])
+            hb2.close()
+    S.configure(bar_map=1)
+    os.close(fd)
+
+
 def test_latency_4k(S, tmp_path):
     import time
     from nvme_strom_amd.tensor import FileReader, HbmBuffer
