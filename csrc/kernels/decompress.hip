@@ -6,17 +6,20 @@
 //
 // One 64-lane workgroup (= one wavefront) decodes one stream at a time
 // (grid-stride over descriptors).  Parsing is wave-uniform; byte moves are
-// spread over the 64 lanes.  Two LDS structures keep latency off the serial
-// parse path:
-//   * a 16 KiB input window: tokens/lengths/offsets are read from LDS, the
-//     window is refilled with one coalesced sweep when the parser leaves it;
-//   * a 64 KiB history ring: LZ4 match distances are < 64 KiB, so every
-//     match source is in LDS.  Output is flushed ring -> HBM in >= 4 KiB
-//     sweeps (coalesced byte stores), never re-read from HBM.
-// Overlapping matches use the periodic form out[s+k] = out[s-off+(k mod off)]
-// so a piece never reads bytes it writes; pieces are <= 4 KiB and fenced by
-// a barrier.  Snappy copies farther than 64 KiB (legal in the format, never
-// produced by 64 KiB-fragment compressors) read the already-flushed HBM.
+// spread over the 64 lanes, one byte per lane per pass:
+//   * an 8 KiB LDS input window: tokens/lengths/offsets/literals are read from
+//     LDS; the window is refilled (one coalesced sweep) ahead of the parser;
+//   * a 64 KiB LDS history ring (LZ4 distances are < 64 KiB) serves every
+//     match source; each output byte is stored to HBM and to the ring in the
+//     same pass, so there is no flush pass and no HBM re-read;
+//   * overlapping matches (distance < length) never use a modulo in the
+//     copy loop: distance >= 64 copies pass by pass (each pass reads bytes a
+//     previous pass wrote); distance < 64 seeds one 64-byte pass from the
+//     pattern (k mod d, computed once per match) and continues with a period
+//     Q = d * ceil(64 / d) in [64, 127].
+// All positions are 32-bit (streams < 4 GiB).  Snappy copies farther than
+// 64 KiB (legal, never produced by 64 KiB-fragment compressors) read the
+// already-stored HBM output with L1-bypassing loads.
 //
 // Codecs: raw LZ4 block, LZ4 frame block sequence (linked or independent
 // blocks, optional per-block checksums skipped), raw snappy, stored copy.
@@ -26,96 +29,173 @@
 
 #include "strom/strom.h"
 
+#ifndef STROM_DECOMP_RING
+#define STROM_DECOMP_RING (8u << 10)
+#endif
+#ifndef STROM_DECOMP_INW
+#define STROM_DECOMP_INW (2u << 10)
+#endif
+
 namespace {
 
-constexpr uint32_t kRing = 1u << 16;
+// 16 KiB history + 4 KiB input = 20 KiB of LDS per wave -> 8 waves per CU.
+// (A full 64 KiB LZ4 window fits only 2 per CU, and a wave-serial decoder
+// is issue-bound: throughput scales with resident waves.)  Matches that
+// reach past the ring read the HBM output this wave already stored.
+constexpr uint32_t kRing = STROM_DECOMP_RING;
 constexpr uint32_t kMask = kRing - 1;
-constexpr uint32_t kInW = 16u << 10;
-constexpr uint32_t kPiece = 4096;
+constexpr uint32_t kInW = STROM_DECOMP_INW;
+constexpr uint32_t kAhead = 512;  // keep this much input in the window
 
-enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3 };
+enum : int32_t { kErrFormat = -1, kErrOverflow = -2 };
+
+// The workgroup is ONE wavefront, so lanes only need their LDS writes
+// ordered before later LDS reads.  __syncthreads() would also wait for every
+// outstanding HBM byte store (vmcnt(0)): ~1 us per call, twice per LZ4
+// sequence, which capped v1 at ~6 GB/s.  The asm also fences the compiler.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t ld_bypass_byte(const uint8_t *p) {
+  // dword-aligned agent-scope relaxed load: global_load ... sc1 (skips L1)
+  const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
+  uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (v >> (8 * ((uintptr_t)p & 3))) & 0xff;
+}
 
 struct Decoder {
   const uint8_t *in;
   uint8_t *out;
-  uint64_t ilen, ocap;
-  uint64_t op = 0, flushed = 0, win = ~0ull;
+  uint32_t ilen, ocap;
+  uint32_t op = 0, win = 0xffffffffu;
   int32_t err = 0;
   uint8_t *ring;
   uint8_t *inw;
   uint32_t lane;
 
-  __device__ void load_window(uint64_t at) {
-    __syncthreads();
-    for (uint32_t k = lane; k < kInW && at + k < ilen; k += 64) inw[k] = in[at + k];
+  // Register window: 256 input bytes, one dword per lane; the wave-uniform
+  // parser reads them with v_readlane (scalar, a few cycles) instead of a
+  // dependent LDS round trip per token/length/offset byte.
+  uint32_t rwin = 0, rbase = 0xffffffffu;
+
+  __device__ void load_reg(uint32_t q) {  // q: 4-aligned, win covers q
+    const uint32_t o = q - win + 4 * lane;
+    rwin = o + 4 <= kInW ? *(const uint32_t *)(inw + o) : 0u;
+    rbase = q;
+  }
+  __device__ void load_window(uint32_t at) {
+    at &= ~3u;  // dword-aligned window base (register window loads)
+    lds_sync();
+    rbase = 0xffffffffu;
+    const uint32_t n = ilen - at < kInW ? ilen - at : kInW;
+    // dword sweep when aligned, bytes otherwise
+    const uint8_t *src = in + at;
+    if (((uintptr_t)src & 3) == 0) {
+      for (uint32_t k = lane * 4; k + 4 <= n; k += 256) *(uint32_t *)(inw + k) = *(const uint32_t *)(src + k);
+      for (uint32_t k = (n & ~3u) + lane; k < n; k += 64) inw[k] = src[k];
+    } else {
+      for (uint32_t k = lane; k < n; k += 64) inw[k] = src[k];
+    }
     win = at;
-    __syncthreads();
+    lds_sync();
   }
-  __device__ uint32_t byte(uint64_t p) {
-    if (p < win || p >= win + kInW) load_window(p);
-    return inw[p - win];
+  // keep [p, p + kAhead) inside the window when the input has it
+  __device__ void ensure(uint32_t p) {
+    const uint32_t end = p + kAhead < ilen ? p + kAhead : ilen;
+    if (p < win || end > win + kInW) load_window(p);
   }
-  __device__ void flush(uint64_t upto) {
-    for (uint64_t k = flushed + lane; k < upto; k += 64) out[k] = ring[k & kMask];
-    flushed = upto;
-  }
-  __device__ void after_piece() {
-    __syncthreads();
-    if (op - flushed >= kPiece) flush(op);
+  __device__ uint32_t byte(uint32_t p) {
+    if (p < rbase || p - rbase >= 256) {  // rbase = ~0 means empty
+      const uint32_t q = p & ~3u;
+      const uint32_t need = q + 256 < ilen ? q + 256 : ilen;
+      if (q < win || need > win + kInW) load_window(q);
+      load_reg(q);
+    }
+    const uint32_t rel = p - rbase;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)rwin, (int)(rel >> 2));
+    return (w >> (8 * (rel & 3))) & 0xffu;
   }
   // literal bytes src[ip, ip+len) -> output
-  __device__ void literal(uint64_t ip, uint64_t len) {
-    for (uint64_t done = 0; done < len;) {
-      uint64_t n = len - done < kPiece ? len - done : kPiece;
-      for (uint64_t k = lane; k < n; k += 64) {
-        uint64_t p = ip + done + k;
-        uint8_t v = (p >= win && p < win + kInW) ? inw[p - win] : in[p];
+  __device__ void literal(uint32_t ip, uint32_t len) {
+    for (uint32_t done = 0; done < len; done += 64) {
+      const uint32_t k = done + lane;
+      if (k < len) {
+        const uint32_t p = ip + k;
+        const uint8_t v = (p - win < kInW) ? inw[p - win] : in[p];
         ring[(op + k) & kMask] = v;
+        out[op + k] = v;
       }
-      op += n;
-      done += n;
-      after_piece();
     }
+    op += len;
+    lds_sync();
   }
-  __device__ void match(uint64_t off, uint64_t len) {
+  __device__ void match(uint32_t off, uint32_t len) {
     if (off == 0 || off > op) {
       err = kErrFormat;
       return;
     }
-    if (off > kRing - 1) {
-      // far copy (snappy only): sources were flushed long ago
-      flush(op);
+    const uint32_t s = op;
+    // near: every source byte stays in the ring for the whole match
+    const bool near = off < 64 || off + len <= kRing;
+    if (!near) {
+      // far copy: sources are in HBM already, written by this wave; make
+      // them visible to L1-bypassing loads
       __threadfence();
-      __syncthreads();
-      for (uint64_t done = 0; done < len;) {
-        uint64_t n = len - done < kPiece ? len - done : kPiece;
-        for (uint64_t k = lane; k < n; k += 64) ring[(op + k) & kMask] = out[op - off + k];
-        op += n;
-        done += n;
-        after_piece();
+      for (uint32_t done = 0; done < len; done += 64) {
+        const uint32_t k = done + lane;
+        if (k < len) {
+          const uint8_t v = (uint8_t)ld_bypass_byte(out + s - off + k);
+          ring[(s + k) & kMask] = v;
+          out[s + k] = v;
+        }
+        if (off < len) {
+          __threadfence();
+          lds_sync();
+        }
       }
+      op += len;
+      lds_sync();
       return;
     }
-    for (uint64_t done = 0; done < len;) {
-      uint64_t n = len - done < kPiece ? len - done : kPiece;
-      if (off > kRing - kPiece && n > kRing - off) n = kRing - off;  // keep sources intact
-      const uint64_t s = op;
-      if (off >= n) {
-        for (uint64_t k = lane; k < n; k += 64) ring[(s + k) & kMask] = ring[(s - off + k) & kMask];
-      } else {
-        for (uint64_t k = lane; k < n; k += 64)
-          ring[(s + k) & kMask] = ring[(s - off + (k % off)) & kMask];
+    if (off >= 64 || off >= len) {
+      const bool overlap = off < len;
+      for (uint32_t done = 0; done < len; done += 64) {
+        const uint32_t k = done + lane;
+        if (k < len) {
+          const uint8_t v = ring[(s - off + k) & kMask];
+          ring[(s + k) & kMask] = v;
+          out[s + k] = v;
+        }
+        if (overlap) lds_sync();  // next pass may read this one
       }
-      op += n;
-      done += n;
-      after_piece();
+    } else {
+      // short period: seed 64 bytes from the pattern, then period Q >= 64
+      const uint32_t q = off * ((64 + off - 1) / off);
+      const uint32_t r = lane % off;
+      if (lane < len) {
+        const uint8_t v = ring[(s - off + r) & kMask];
+        ring[(s + lane) & kMask] = v;
+        out[s + lane] = v;
+      }
+      lds_sync();
+      for (uint32_t done = 64; done < len; done += 64) {
+        const uint32_t k = done + lane;
+        if (k < len) {
+          const uint8_t v = ring[(s + k - q) & kMask];
+          ring[(s + k) & kMask] = v;
+          out[s + k] = v;
+        }
+        lds_sync();
+      }
     }
+    op += len;
+    lds_sync();
   }
   // one raw LZ4 block occupying src[ip, end); returns new ip
-  __device__ uint64_t lz4_block(uint64_t ip, uint64_t end) {
+  __device__ uint32_t lz4_block(uint32_t ip, uint32_t end) {
     while (ip < end && !err) {
-      uint32_t token = byte(ip++);
-      uint64_t lit = token >> 4;
+      ensure(ip);
+      const uint32_t token = byte(ip++);
+      uint32_t lit = token >> 4;
       if (lit == 15) {
         uint32_t b;
         do {
@@ -124,15 +204,15 @@ struct Decoder {
           lit += b;
         } while (b == 255);
       }
-      if (ip + lit > end) { err = kErrFormat; return ip; }
-      if (op + lit > ocap) { err = kErrOverflow; return ip; }
-      literal(ip, lit);
+      if (lit > end - ip) { err = kErrFormat; return ip; }
+      if (lit > ocap - op) { err = kErrOverflow; return ip; }
+      if (lit) literal(ip, lit);
       ip += lit;
       if (ip >= end) break;  // last sequence carries literals only
-      if (ip + 2 > end) { err = kErrFormat; return ip; }
-      uint64_t off = byte(ip) | (byte(ip + 1) << 8);
+      if (end - ip < 2) { err = kErrFormat; return ip; }
+      const uint32_t off = byte(ip) | (byte(ip + 1) << 8);
       ip += 2;
-      uint64_t ml = token & 15;
+      uint32_t ml = token & 15;
       if (ml == 15) {
         uint32_t b;
         do {
@@ -142,35 +222,39 @@ struct Decoder {
         } while (b == 255);
       }
       ml += 4;
-      if (op + ml > ocap) { err = kErrOverflow; return ip; }
+      if (ml > ocap - op) { err = kErrOverflow; return ip; }
       match(off, ml);
     }
     return ip;
   }
   __device__ void snappy() {
-    uint64_t ip = 0, ulen = 0;
+    uint32_t ip = 0;
+    uint64_t ulen = 0;
+    ensure(0);
     for (int shift = 0;; shift += 7) {
       if (ip >= ilen || shift > 35) { err = kErrFormat; return; }
-      uint32_t b = byte(ip++);
+      const uint32_t b = byte(ip++);
       ulen |= (uint64_t)(b & 0x7f) << shift;
       if (!(b & 0x80)) break;
     }
     if (ulen > ocap) { err = kErrOverflow; return; }
+    const uint32_t olen = (uint32_t)ulen;
     while (ip < ilen && !err) {
-      uint32_t tag = byte(ip++);
-      uint64_t len, off;
-      uint32_t kind = tag & 3;
+      ensure(ip);
+      const uint32_t tag = byte(ip++);
+      uint32_t len, off;
+      const uint32_t kind = tag & 3;
       if (kind == 0) {
         len = (tag >> 2) + 1;
         if (len > 60) {
-          uint32_t nb = (uint32_t)len - 60;
-          if (ip + nb > ilen) { err = kErrFormat; return; }
+          const uint32_t nb = len - 60;
+          if (ilen - ip < nb) { err = kErrFormat; return; }
           len = 0;
-          for (uint32_t i = 0; i < nb; ++i) len |= (uint64_t)byte(ip + i) << (8 * i);
+          for (uint32_t i = 0; i < nb; ++i) len |= byte(ip + i) << (8 * i);
           len += 1;
           ip += nb;
         }
-        if (ip + len > ilen || op + len > ulen) { err = kErrFormat; return; }
+        if (len > ilen - ip || len > olen - op) { err = kErrFormat; return; }
         literal(ip, len);
         ip += len;
         continue;
@@ -178,40 +262,45 @@ struct Decoder {
       if (kind == 1) {
         if (ip >= ilen) { err = kErrFormat; return; }
         len = 4 + ((tag >> 2) & 7);
-        off = ((uint64_t)(tag >> 5) << 8) | byte(ip++);
+        off = ((tag >> 5) << 8) | byte(ip++);
       } else if (kind == 2) {
-        if (ip + 2 > ilen) { err = kErrFormat; return; }
+        if (ilen - ip < 2) { err = kErrFormat; return; }
         len = (tag >> 2) + 1;
         off = byte(ip) | (byte(ip + 1) << 8);
         ip += 2;
       } else {
-        if (ip + 4 > ilen) { err = kErrFormat; return; }
+        if (ilen - ip < 4) { err = kErrFormat; return; }
         len = (tag >> 2) + 1;
-        off = byte(ip) | (byte(ip + 1) << 8) | (byte(ip + 2) << 16) | ((uint64_t)byte(ip + 3) << 24);
+        off = byte(ip) | (byte(ip + 1) << 8) | (byte(ip + 2) << 16) | (byte(ip + 3) << 24);
         ip += 4;
       }
-      if (op + len > ulen) { err = kErrFormat; return; }
+      if (len > olen - op) { err = kErrFormat; return; }
       match(off, len);
     }
-    if (!err && op != ulen) err = kErrFormat;
+    if (!err && op != olen) err = kErrFormat;
   }
   // LZ4 frame data blocks (after the frame header): [u32 size|flag][data][u32 bcs?]...
   __device__ void lz4_frame_blocks(bool block_checksum) {
-    uint64_t ip = 0;
+    uint32_t ip = 0;
     while (!err) {
-      if (ip + 4 > ilen) { err = kErrFormat; return; }
+      if (ilen - ip < 4) { err = kErrFormat; return; }
+      ensure(ip);
       uint32_t bs = byte(ip) | (byte(ip + 1) << 8) | (byte(ip + 2) << 16) | (byte(ip + 3) << 24);
       ip += 4;
       if (bs == 0) return;  // end mark
-      bool stored = bs & 0x80000000u;
+      const bool stored = bs & 0x80000000u;
       bs &= 0x7fffffffu;
-      if (ip + bs > ilen) { err = kErrFormat; return; }
+      if (bs > ilen - ip) { err = kErrFormat; return; }
       if (stored) {
-        if (op + bs > ocap) { err = kErrOverflow; return; }
-        literal(ip, bs);
+        if (bs > ocap - op) { err = kErrOverflow; return; }
+        for (uint32_t done = 0; done < bs; done += kInW / 2) {
+          const uint32_t n = bs - done < kInW / 2 ? bs - done : kInW / 2;
+          ensure(ip + done);
+          literal(ip + done, n);
+        }
         ip += bs;
       } else {
-        uint64_t end = ip + bs;
+        const uint32_t end = ip + bs;
         lz4_block(ip, end);
         ip = end;
       }
@@ -225,9 +314,9 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
                                                         const strom_decomp_desc *__restrict__ desc,
                                                         uint32_t nblocks, int32_t *status) {
   __shared__ uint8_t ring[kRing];
-  __shared__ uint8_t inw[kInW];
+  __shared__ __attribute__((aligned(16))) uint8_t inw[kInW];
   for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    strom_decomp_desc d = desc[b];
+    const strom_decomp_desc d = desc[b];
     Decoder dec;
     dec.in = src + d.src_off;
     dec.out = dst + d.dst_off;
@@ -244,17 +333,22 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
         dec.snappy();
         break;
       case STROM_CODEC_COPY:
-        if (dec.ilen > dec.ocap) dec.err = kErrOverflow;
-        else dec.literal(0, dec.ilen);
+        if (dec.ilen > dec.ocap) {
+          dec.err = kErrOverflow;
+        } else {
+          for (uint32_t done = 0; done < dec.ilen; done += kInW / 2) {
+            const uint32_t n = dec.ilen - done < kInW / 2 ? dec.ilen - done : kInW / 2;
+            dec.ensure(done);
+            dec.literal(done, n);
+          }
+        }
         break;
       default:  // LZ4 frame blocks, with (5) or without (4) block checksums
-        dec.lz4_frame_blocks(codec == 5);
+        dec.lz4_frame_blocks(codec == STROM_CODEC_LZ4_FRAME_BCS);
         break;
     }
-    __syncthreads();
-    dec.flush(dec.op);
     if (threadIdx.x == 0) status[b] = dec.err ? dec.err : (int32_t)dec.op;
-    __syncthreads();
+    lds_sync();
   }
 }
 
@@ -263,9 +357,9 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
-  if (codec < STROM_CODEC_LZ4 || codec > 5) return -22;
+  if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_LZ4_FRAME_BCS) return -22;
   if (!nblocks) return 0;
-  uint32_t grid = nblocks < 2048 ? nblocks : 2048;
+  uint32_t grid = nblocks < 4096 ? nblocks : 4096;
   hipLaunchKernelGGL(decompress_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, codec,
                      (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -1,0 +1,275 @@
+// SPDX-License-Identifier: GPL-2.0
+/*
+ * strom_gpumap.c — HBM mappings imported as dma-bufs.
+ *
+ * Replaces the reference's nvidia_p2p_get_pages registry (kmod/pmemmap.c:
+ * 19-495).  amdgpu exports VRAM buffer objects as dma-bufs; we attach with
+ * allow_peer2peer for each NVMe controller that will write into the range,
+ * pin the attachment (so the BO cannot migrate out of VRAM while reads are
+ * in flight — move_notify is therefore a no-op for pinned attachments) and
+ * map it to get bus addresses through the controller's IOMMU domain.
+ *
+ * Lifetime: handle -> kref'd record; UNMAP removes it from the table and
+ * waits until in-flight requests drop to zero before unpinning (fixes
+ * reference defect #7: UNMAP neither freed nor waited).
+ */
+#include <linux/dma-resv.h>
+#include <linux/hashtable.h>
+#include <linux/slab.h>
+#include <linux/uaccess.h>
+
+#include "strom_kmod.h"
+
+static DEFINE_HASHTABLE(gpumap_slots, 6);   /* 64 slots, as in v0.6 */
+static DEFINE_SPINLOCK(gpumap_lock);
+static unsigned long gpumap_next = 0x5350000000000000UL;
+
+static void strom_move_notify(struct dma_buf_attachment *att)
+{
+	/* pinned attachments are never moved by the exporter */
+}
+
+static const struct dma_buf_attach_ops strom_importer_ops = {
+	.allow_peer2peer = true,
+	.move_notify = strom_move_notify,
+};
+
+static void gpumap_release(struct kref *ref)
+{
+	struct strom_gpumap *m = container_of(ref, struct strom_gpumap, ref);
+	int i;
+
+	for (i = 0; i < m->natt; i++) {
+		struct strom_attach *a = &m->att[i];
+
+		dma_resv_lock(m->dmabuf->resv, NULL);
+		dma_buf_unmap_attachment(a->att, a->sgt, DMA_BIDIRECTIONAL);
+		dma_buf_unpin(a->att);
+		dma_resv_unlock(m->dmabuf->resv);
+		dma_buf_detach(m->dmabuf, a->att);
+	}
+	dma_buf_put(m->dmabuf);
+	kfree(m);
+	module_put(THIS_MODULE);
+}
+
+struct strom_gpumap *strom_gpumap_get(unsigned long handle)
+{
+	struct strom_gpumap *m;
+
+	spin_lock(&gpumap_lock);
+	hash_for_each_possible(gpumap_slots, m, node, handle) {
+		if (m->handle == handle && uid_eq(m->owner, current_euid())) {
+			kref_get(&m->ref);
+			spin_unlock(&gpumap_lock);
+			return m;
+		}
+	}
+	spin_unlock(&gpumap_lock);
+	return NULL;
+}
+
+void strom_gpumap_put(struct strom_gpumap *m)
+{
+	kref_put(&m->ref, gpumap_release);
+}
+
+int strom_map_dmabuf(struct strom_map_gpu_dmabuf *arg)
+{
+	struct strom_gpumap *m;
+	struct dma_buf *db;
+
+	if (!arg->length)
+		return -EINVAL;
+	db = dma_buf_get(arg->dmabuf_fd);
+	if (IS_ERR(db))
+		return PTR_ERR(db);
+	if (arg->length > db->size) {
+		dma_buf_put(db);
+		return -ERANGE;
+	}
+	m = kzalloc(sizeof(*m), GFP_KERNEL);
+	if (!m) {
+		dma_buf_put(db);
+		return -ENOMEM;
+	}
+	m->dmabuf = db;
+	m->vaddress = arg->vaddress;
+	m->length = arg->length;
+	m->owner = current_euid();
+	mutex_init(&m->att_lock);
+	atomic_set(&m->inflight, 0);
+	init_waitqueue_head(&m->drain);
+	kref_init(&m->ref);
+	__module_get(THIS_MODULE);
+	spin_lock(&gpumap_lock);
+	m->handle = ++gpumap_next;
+	hash_add(gpumap_slots, &m->node, m->handle);
+	spin_unlock(&gpumap_lock);
+	arg->handle = m->handle;
+	arg->gpu_page_sz = STROM_GPU_BOUND_SIZE;
+	arg->gpu_npages = DIV_ROUND_UP(arg->length, STROM_GPU_BOUND_SIZE);
+	prDebug("map dmabuf fd=%d len=%zu handle=%#lx", arg->dmabuf_fd, arg->length, m->handle);
+	return 0;
+}
+
+int strom_unmap_gpu(unsigned long handle)
+{
+	struct strom_gpumap *m = strom_gpumap_get(handle);
+
+	if (!m)
+		return -ENOENT;
+	spin_lock(&gpumap_lock);
+	hash_del(&m->node);
+	spin_unlock(&gpumap_lock);
+	wait_event(m->drain, atomic_read(&m->inflight) == 0);
+	strom_gpumap_put(m);   /* lookup reference */
+	strom_gpumap_put(m);   /* table reference */
+	return 0;
+}
+
+/* attach + pin + map for `dev` once; caller holds a reference on m */
+static struct strom_attach *gpumap_attach(struct strom_gpumap *m, struct device *dev)
+{
+	struct strom_attach *a = NULL;
+	struct dma_buf_attachment *att;
+	struct sg_table *sgt;
+	int i, rc;
+
+	mutex_lock(&m->att_lock);
+	for (i = 0; i < m->natt; i++)
+		if (m->att[i].dev == dev) {
+			a = &m->att[i];
+			goto out;
+		}
+	if (m->natt == ARRAY_SIZE(m->att))
+		goto out;
+	att = dma_buf_dynamic_attach(m->dmabuf, dev, &strom_importer_ops, m);
+	if (IS_ERR(att))
+		goto out;
+	if (!att->peer2peer) {
+		/* the exporter refused P2P for this device pair */
+		dma_buf_detach(m->dmabuf, att);
+		goto out;
+	}
+	dma_resv_lock(m->dmabuf->resv, NULL);
+	rc = dma_buf_pin(att);
+	if (rc) {
+		dma_resv_unlock(m->dmabuf->resv);
+		dma_buf_detach(m->dmabuf, att);
+		goto out;
+	}
+	sgt = dma_buf_map_attachment(att, DMA_BIDIRECTIONAL);
+	dma_resv_unlock(m->dmabuf->resv);
+	if (IS_ERR(sgt)) {
+		dma_resv_lock(m->dmabuf->resv, NULL);
+		dma_buf_unpin(att);
+		dma_resv_unlock(m->dmabuf->resv);
+		dma_buf_detach(m->dmabuf, att);
+		goto out;
+	}
+	a = &m->att[m->natt++];
+	a->dev = dev;
+	a->att = att;
+	a->sgt = sgt;
+out:
+	mutex_unlock(&m->att_lock);
+	return a;
+}
+
+int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
+		     dma_addr_t *addr, size_t *contig)
+{
+	struct strom_attach *a = gpumap_attach(m, dev);
+	struct scatterlist *sg;
+	int i;
+
+	if (!a)
+		return -EOPNOTSUPP;
+	for_each_sgtable_dma_sg(a->sgt, sg, i) {
+		size_t len = sg_dma_len(sg);
+
+		if (off < len) {
+			*addr = sg_dma_address(sg) + off;
+			*contig = len - off;
+			return 0;
+		}
+		off -= len;
+	}
+	return -ERANGE;
+}
+
+int strom_list_gpu(struct strom_list_gpu_memory __user *uarg)
+{
+	struct strom_gpumap *m;
+	u32 nrooms, n = 0;
+	int bkt;
+
+	if (get_user(nrooms, &uarg->nrooms))
+		return -EFAULT;
+	spin_lock(&gpumap_lock);
+	hash_for_each(gpumap_slots, bkt, m, node) {
+		if (!uid_eq(m->owner, current_euid()))
+			continue;
+		if (n < nrooms) {
+			/* put_user may fault: collect under the lock into a copy */
+			unsigned long h = m->handle;
+
+			spin_unlock(&gpumap_lock);
+			if (put_user(h, &uarg->handles[n]))
+				return -EFAULT;
+			spin_lock(&gpumap_lock);
+		}
+		n++;
+	}
+	spin_unlock(&gpumap_lock);
+	return put_user(n, &uarg->nitems);
+}
+
+int strom_info_gpu(struct strom_info_gpu_memory __user *uarg)
+{
+	struct strom_info_gpu_memory k;
+	struct strom_gpumap *m;
+	u32 i, npages;
+
+	if (copy_from_user(&k, uarg, offsetof(struct strom_info_gpu_memory, paddrs)))
+		return -EFAULT;
+	m = strom_gpumap_get(k.handle);
+	if (!m)
+		return -ENOENT;
+	npages = DIV_ROUND_UP(m->length, STROM_GPU_BOUND_SIZE);
+	k.nitems = npages;
+	k.version = 1;
+	k.gpu_page_sz = STROM_GPU_BOUND_SIZE;
+	k.owner = from_kuid(current_user_ns(), m->owner);
+	k.map_offset = 0;
+	k.map_length = m->length;
+	for (i = 0; i < npages && i < k.nrooms; i++) {
+		/* bus address as seen by the first attached controller, if any */
+		u64 pa = 0;
+
+		if (m->natt) {
+			dma_addr_t a;
+			size_t c;
+
+			if (!strom_gpumap_dma(m, m->att[0].dev, (size_t)i * STROM_GPU_BOUND_SIZE, &a, &c))
+				pa = a;
+		}
+		if (put_user(pa, &uarg->paddrs[i])) {
+			strom_gpumap_put(m);
+			return -EFAULT;
+		}
+	}
+	strom_gpumap_put(m);
+	return copy_to_user(uarg, &k, offsetof(struct strom_info_gpu_memory, paddrs)) ? -EFAULT : 0;
+}
+
+void strom_gpumap_init(void)
+{
+	hash_init(gpumap_slots);
+}
+
+void strom_gpumap_exit(void)
+{
+	/* module refs held by live mappings prevent unload; nothing to do */
+}

@@ -1,0 +1,112 @@
+"""Throughput of the CDNA4 post-read kernels at production sizes.
+
+``python -m nvme_strom_amd.tools.kbench [--gib 1] [--only crc,scatter,...]``
+
+Each kernel runs on an HBM-resident input (default 1 GiB), timed with HIP
+events over several iterations after a warm-up; GB/s counts the bytes the
+kernel must read + write.  Run it under ``rocprofv3 --kernel-trace --stats``
+for per-kernel device time and under ``--pmc`` for counters.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+
+import numpy as np
+import torch
+
+
+def timed(fn, iters=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters / 1e3
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=1.0)
+    ap.add_argument("--only", default="crc,scatter,verify,heap,lz4,snappy,filter")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    only = set(a.only.split(","))
+    from nvme_strom_amd.ops import decompress as D
+    from nvme_strom_amd.ops import verify as V
+    from nvme_strom_amd.ops.colfilter import bitmap_to_indices, column_filter
+    from nvme_strom_amd.ops.heapscan import heap_scan
+    from nvme_strom_amd.ops.reorder import chunk_scatter
+    from nvme_strom_amd.utils import pgpage
+
+    n = int(a.gib * (1 << 30))
+    dev = torch.device("cuda")
+    res = {}
+
+    def log(k, sec, nbytes):
+        res[k] = dict(ms=round(sec * 1e3, 3), GBps=round(nbytes / sec / 1e9, 1))
+        print(k, res[k], file=sys.stderr, flush=True)
+
+    buf = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
+    if "crc" in only:
+        for ch in (8192, 1 << 16, 1 << 20):
+            out = torch.empty((n + ch - 1) // ch, dtype=torch.int32, device=dev)
+            log(f"crc32c_chunks_{ch}", timed(lambda: V.crc32c_chunks(buf, ch, out=out)), n)
+        log("crc32c_full", timed(lambda: V.crc32c(buf)), n)
+    if "scatter" in only:
+        ch = 8192
+        perm = np.random.default_rng(0).permutation(n // ch).astype(np.uint32)
+        dst = torch.empty_like(buf)
+        pos = torch.from_numpy(perm.view(np.int32)).to(dev)
+        log("chunk_scatter_8k", timed(lambda: chunk_scatter(buf, dst, pos, ch)), 2 * n)
+        del dst
+    if "verify" in only:
+        log("verify_pattern", timed(lambda: V.verify_pattern(buf, 0x41424344)), n)
+        log("fill_pattern", timed(lambda: V.fill_pattern(buf, 0x41424344)), n)
+    if "heap" in only:
+        page = pgpage.build_table(np.arange(150 * 64, dtype=np.int64), per_page=150, width=8)
+        reps = max(1, n // len(page))
+        reps = min(reps, 0xFFFF // 64)          # item ids address <= 65535 pages
+        pages = torch.from_numpy(np.frombuffer(page * reps, dtype=np.uint8).copy()).to(dev)
+        nb = pages.numel()
+        log("heap_scan", timed(lambda: heap_scan(pages, skip_invisible=True)), nb)
+        log("heap_scan_checksum_filter",
+            timed(lambda: heap_scan(pages, verify_checksum=True, attr_off=0, attr_width=8,
+                                    lo=100, hi=5000)), nb)
+        del pages
+    for codec in ("lz4", "snappy"):
+        if codec not in only:
+            continue
+        rng = np.random.default_rng(1)
+        words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+        blk = b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10]
+        comp = D.lz4_compress(blk) if codec == "lz4" else D.snappy_compress(blk)
+        nblk = max(1, min(n // len(blk), 16384))
+        src = torch.from_numpy(np.frombuffer(comp * nblk, dtype=np.uint8).copy()).to(dev)
+        dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
+        descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk)) for i in range(nblk)])
+        cid = D.LZ4 if codec == "lz4" else D.SNAPPY
+        st = D.decompress(cid, src, dst, descs)
+        assert (st == len(blk)).all(), st[:4]
+        log(f"decompress_{codec}_64k_ratio{len(blk) / len(comp):.1f}",
+            timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
+        del src, dst
+    if "filter" in only:
+        nv = n // 8
+        v = torch.randint(-1000, 1000, (nv,), dtype=torch.int64, device=dev)
+        log("column_filter_i64", timed(lambda: column_filter(v, -100, 100)), nv * 8)
+        bm, cnt = column_filter(v, -100, 100)
+        log("bitmap_to_indices", timed(lambda: bitmap_to_indices(bm, nv, cnt)), nv // 8 + cnt * 4)
+    js = json.dumps(res)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+
+
+if __name__ == "__main__":
+    main()
