@@ -8,7 +8,7 @@ OUT      := nvme_strom_amd/lib
 OBJ      := build/obj
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Icsrc/include -Icsrc/engine
 HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LDFLAGS  := -shared -fPIC -lpthread
+LDFLAGS  := -shared -fPIC -lpthread -L$(ROCM)/lib -lrocprofiler-sdk-roctx
 
 ENGINE_SRC := $(wildcard csrc/engine/*.cc)
 KERNEL_SRC := $(wildcard csrc/kernels/*.hip)
@@ -39,3 +39,30 @@ clean:
 	rm -rf build $(OUT)/libstrom.so $(TOOLS)
 
 .PHONY: all tools clean
+
+# ---- host-only engine self-test, plain and under sanitizers ---------------
+# The engine's host code builds with g++ (HIP host API only); device kernels
+# are not part of these builds.  GPU sanitizers are not used on this pool.
+SELFTEST_SRC := csrc/tests/engine_selftest.cc $(ENGINE_SRC)
+SELFTEST_FLAGS := -std=c++17 -g -O1 -Icsrc/include -Icsrc/engine -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
+SELFTEST_LIBS := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
+
+build/selftest: $(SELFTEST_SRC) csrc/engine/engine.h
+	@mkdir -p build
+	g++ $(SELFTEST_FLAGS) -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
+
+build/selftest-asan: $(SELFTEST_SRC) csrc/engine/engine.h
+	@mkdir -p build
+	g++ $(SELFTEST_FLAGS) -fsanitize=address,undefined -fno-omit-frame-pointer -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
+
+# TSAN uses ROCm's clang runtime: gcc-11's libtsan lacks the
+# pthread_cond_clockwait interceptor that condition_variable::wait_until
+# compiles to, which yields false "double lock" reports on the task table.
+build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
+	@mkdir -p build
+	$(ROCM)/llvm/bin/clang++ $(SELFTEST_FLAGS) -fsanitize=thread -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
+
+selftest: build/selftest build/selftest-asan build/selftest-tsan
+	STROM_STAT_SHM=0 ./build/selftest && STROM_STAT_SHM=0 ./build/selftest-asan && STROM_STAT_SHM=0 TSAN_OPTIONS=report_signal_unsafe=0 ./build/selftest-tsan
+
+.PHONY: selftest

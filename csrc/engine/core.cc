@@ -33,7 +33,7 @@ static bool parse_bool(const std::string &v) {
 Config Config::from_env() {
   Config c;
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
-                               "staging_slots", "inline_max", "bar_map", "bar_max",
+                               "staging_slots", "inline_max", "bar_map", "bar_max", "trace",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind",
                                "stat_info", "verbose"};
@@ -71,6 +71,7 @@ int Config::set(const std::string &k, const std::string &v) {
   }
   if (k == "staging_slots") { if (n < 1 || n > 1024) return -EINVAL; staging_slots = (int)n; return 0; }
   if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
+  if (k == "trace") { trace = parse_bool(v); return 0; }
   if (k == "bar_max") {
     if (n < 0 || n > (64l << 20)) return -EINVAL;
     bar_max = (uint32_t)n;
@@ -99,6 +100,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "staging_slots") v = staging_slots;
   else if (k == "inline_max") v = inline_max;
   else if (k == "bar_map") v = bar_map;
+  else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;
   else if (k == "direct_io") v = direct_io;

@@ -19,6 +19,8 @@
 #include <unistd.h>
 #include <x86intrin.h>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <algorithm>
 
 #include "engine.h"
@@ -390,8 +392,36 @@ int Engine::memcpy_wait_timed(strom_memcpy_wait_timed *a) {
   return rc;
 }
 
+// roctx ranges around every engine call when STROM_TRACE=1: rocprofv3
+// --marker-trace then shows ioctl spans beside the SDMA copies and kernels.
+namespace {
+const char *cmd_name(unsigned long cmd) {
+  switch (cmd) {
+    case STROM_IOCTL__CHECK_FILE: return "strom:CHECK_FILE";
+    case STROM_IOCTL__MAP_GPU_MEMORY: return "strom:MAP_GPU_MEMORY";
+    case STROM_IOCTL__MAP_GPU_DMABUF: return "strom:MAP_GPU_DMABUF";
+    case STROM_IOCTL__UNMAP_GPU_MEMORY: return "strom:UNMAP_GPU_MEMORY";
+    case STROM_IOCTL__MEMCPY_SSD2GPU: return "strom:MEMCPY_SSD2GPU";
+    case STROM_IOCTL__MEMCPY_SSD2RAM: return "strom:MEMCPY_SSD2RAM";
+    case STROM_IOCTL__MEMCPY_WAIT: return "strom:MEMCPY_WAIT";
+    case STROM_IOCTL__MEMCPY_WAIT_TIMED: return "strom:MEMCPY_WAIT_TIMED";
+    default: return "strom:ioctl";
+  }
+}
+struct TraceRange {
+  bool on;
+  explicit TraceRange(unsigned long cmd) : on(config().trace) {
+    if (on) roctxRangePushA(cmd_name(cmd));
+  }
+  ~TraceRange() {
+    if (on) roctxRangePop();
+  }
+};
+}  // namespace
+
 int Engine::ioctl(int session, unsigned long cmd, void *arg) {
   if (!arg) return -EFAULT;
+  TraceRange tr(cmd);
   switch (cmd) {
     case STROM_IOCTL__CHECK_FILE:
       return check_file((strom_check_file *)arg);

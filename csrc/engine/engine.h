@@ -57,6 +57,7 @@ struct Config {
   bool numa_bind = true;         // pin workers near the GPU / SSD
   int stat_info = 1;             // 0 off, 1 on, 2 +debug fields
   int verbose = 0;
+  bool trace = false;            // roctx ranges around engine calls
 
   static Config from_env();
   int set(const std::string &key, const std::string &value);

@@ -5,7 +5,7 @@
 // when a request targets HBM.  Pinned staging is allocated under the
 // calling thread's NUMA policy (hipHostMallocNumaUser), which the I/O
 // workers set to the node of the GPU's PCIe root before allocating.
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>  // host API only: builds with g++ (sanitizers)
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>

@@ -14,7 +14,7 @@
 // Each worker owns its ring, its staging slots and its stream, so the hot
 // path takes no shared lock.  Workers are pinned to the CPUs of the GPU's
 // NUMA node and allocate staging there (PAR5 in SURVEY §2.3).
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>  // host API only: builds with g++ (sanitizers)
 #include <errno.h>
 #include <fcntl.h>
 #include <linux/io_uring.h>

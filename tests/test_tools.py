@@ -1,0 +1,54 @@
+"""CLI tools: ssd2ram_test on CPU (data check on), strom_test on the GPU."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "nvme_strom_amd", "lib")
+
+
+def _tool(name):
+    p = os.path.join(LIB, name)
+    if not os.path.exists(p):
+        pytest.skip(f"{name} not built")
+    return p
+
+
+def _env():
+    return dict(os.environ, STROM_WORKERS="2")
+
+
+def test_ssd2ram_test_cli(rand_file):
+    path, _ = rand_file(8 << 20)
+    out = subprocess.run([_tool("ssd2ram_test"), "-n", "3", "-s", "4", "-c", path],
+                         capture_output=True, text=True, timeout=120, env=_env())
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "verify: 0 corrupted" in out.stdout
+    assert "throughput" in out.stdout
+
+
+def test_ssd2ram_test_print(rand_file):
+    path, _ = rand_file(1 << 20)
+    out = subprocess.run([_tool("ssd2ram_test"), "-p", path], capture_output=True, text=True,
+                         timeout=60, env=_env())
+    assert out.returncode == 0 and "support_dma64: 1" in out.stdout
+
+
+@pytest.mark.gpu
+def test_strom_test_cli_verify(rand_file):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    path, _ = rand_file(48 << 20)
+    out = subprocess.run([_tool("strom_test"), "-c", "-n", "3", "-s", "8", path],
+                         capture_output=True, text=True, timeout=300, env=_env())
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 corrupted" in out.stdout
+    vfs = subprocess.run([_tool("strom_test"), "-f", "-c", "-n", "3", "-s", "8", path],
+                         capture_output=True, text=True, timeout=300, env=_env())
+    assert vfs.returncode == 0, vfs.stdout + vfs.stderr
+    pr = subprocess.run([_tool("strom_test"), "-p", path], capture_output=True, text=True,
+                        timeout=120, env=_env())
+    assert pr.returncode == 0 and "mapped region" in pr.stdout
