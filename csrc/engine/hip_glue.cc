@@ -125,15 +125,18 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
   uint64_t hi = (va + len + page - 1) & ~(page - 1);
   if (lo < base || hi > base + ((asize + page - 1) & ~(page - 1))) return nullptr;
   int fd = -1;
+  const uint64_t t0 = mono_ns();
   if (hipMemGetHandleForAddressRange(&fd, abase, asize, hipMemRangeHandleTypeDmaBufFd, 0) !=
           hipSuccess ||
       fd < 0) {
     (void)hipGetLastError();
     return nullptr;
   }
+  const uint64_t t1 = mono_ns();
   void *p = mmap(nullptr, hi - lo, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)(lo - base));
   close(fd);  // the mapping keeps the dma-buf alive
   if (p == MAP_FAILED) return nullptr;
+  const uint64_t t2 = mono_ns();
   // Self-check with a canary: the CPU alias must be the bytes the GPU sees.
   uint8_t *q = (uint8_t *)p + (va - lo);
   uint64_t orig = 0, canary = 0x5354524f4d424152ull ^ va, back = 0;
@@ -152,6 +155,8 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
     munmap(p, hi - lo);
     return nullptr;
   }
+  STROM_LOG(1, "bar_map %zu MiB: export %.2f ms, mmap %.2f ms, canary %.2f ms", asize >> 20,
+            (t1 - t0) / 1e6, (t2 - t1) / 1e6, (mono_ns() - t2) / 1e6);
   *map_va = lo;
   *map_len = hi - lo;
   return (uint8_t *)p;

@@ -123,6 +123,11 @@ struct strom_req {
 	dma_addr_t ram_dma[STROM_MAX_REQ / PAGE_SIZE];
 	int nram;
 	u64 t0;
+	/* /proc/diskstats accounting so P2P reads show in iostat, as the
+	 * reference's part_stat_* calls did (kmod/nvme_strom.c:1012-1034) */
+	struct block_device *acct_bdev;
+	unsigned long acct_start;
+	unsigned int acct_sectors;
 };
 
 static enum rq_end_io_ret strom_end_io(struct request *rq, blk_status_t err)
@@ -136,6 +141,7 @@ static enum rq_end_io_ret strom_end_io(struct request *rq, blk_status_t err)
 	atomic64_inc(&strom_stats.nr_ssd2gpu);
 	atomic64_add(strom_tsc() - r->t0, &strom_stats.clk_ssd2gpu);
 	atomic64_dec(&strom_stats.cur_dma_count);
+	bdev_end_io_acct(r->acct_bdev, REQ_OP_READ, r->acct_sectors, r->acct_start);
 	if (r->prp_list)
 		dma_pool_free(r->pool, r->prp_list, r->prp_dma);
 	for (i = 0; i < r->nram; i++)
@@ -229,6 +235,7 @@ static int submit_read(struct strom_task *t, struct nvme_ns *ns, sector_t sect, 
 	u64 t0 = strom_tsc();
 	int rc;
 
+	strom_assert_sleepable();
 	r = kzalloc(sizeof(*r), GFP_KERNEL);
 	if (!r)
 		return -ENOMEM;
@@ -271,6 +278,9 @@ static int submit_read(struct strom_task *t, struct nvme_ns *ns, sector_t sect, 
 		atomic_inc(&gmap->inflight);
 	}
 	strom_stat_inflight_inc();
+	r->acct_bdev = ns->disk->part0;
+	r->acct_sectors = len >> SECTOR_SHIFT;
+	r->acct_start = bdev_start_io_acct(r->acct_bdev, REQ_OP_READ, jiffies);
 	r->t0 = strom_tsc();
 	blk_execute_rq_nowait(rq, false);
 	atomic64_inc(&strom_stats.nr_submit_dma);

@@ -50,6 +50,16 @@ extern int strom_stat_level;
 			pr_info("nvme-strom: " fmt "\n", ##__VA_ARGS__);       \
 	} while (0)
 
+/* invariant checks: panic in debug builds like the reference's Assert(),
+ * warn once otherwise */
+#ifdef STROM_DEBUG
+#define STROM_ASSERT(c) BUG_ON(!(c))
+#define strom_assert_sleepable() might_sleep()
+#else
+#define STROM_ASSERT(c) WARN_ON_ONCE(!(c))
+#define strom_assert_sleepable() do { } while (0)
+#endif
+
 /* ---- per-open-file session (strom_proc_release reclaims failures) ---- */
 struct strom_session {
 	struct list_head failed;         /* strom_task records nobody waited */

@@ -66,7 +66,8 @@ struct strom_task *strom_task_create(struct strom_session *s, struct file *filp,
 
 void strom_task_get(struct strom_task *t)
 {
-	WARN_ON(t->frozen);
+	STROM_ASSERT(!t->frozen);
+	STROM_ASSERT(atomic_read(&t->refcnt) > 0);
 	atomic_inc(&t->refcnt);
 }
 

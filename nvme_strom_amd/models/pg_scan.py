@@ -165,10 +165,50 @@ class ScanResult:
     seconds: float = 0.0
     nr_ram: int = 0
     nr_ssd: int = 0
+    # the per-scan counters the reference kept in its DSM segment
+    # (pgsql/nvme_strom.c:96-102) but never displayed (empty
+    # ExplainNVMEStrom, :1238-1242)
+    nr_dma_submit: int = 0
+    nr_dma_blocks: int = 0
+    chunks: int = 0
+    workers: int = 1
 
     @property
     def ntuples(self) -> int:
         return len(self.items)
+
+    def add_io(self, r) -> None:
+        self.nr_ram += r.nr_ram
+        self.nr_ssd += r.nr_ssd
+        self.nr_dma_submit += r.nr_dma_submit
+        self.nr_dma_blocks += r.nr_dma_blocks
+        self.chunks += 1
+
+    def merge(self, parts: List["ScanResult"]) -> None:
+        for p in parts:
+            self.pages += p.pages
+            self.bad_pages += p.bad_pages
+            self.nr_ram += p.nr_ram
+            self.nr_ssd += p.nr_ssd
+            self.nr_dma_submit += p.nr_dma_submit
+            self.nr_dma_blocks += p.nr_dma_blocks
+            self.chunks += p.chunks
+
+    def explain(self) -> str:
+        """EXPLAIN ANALYZE-style summary of the scan's I/O split and rates."""
+        blocks = self.nr_ram + self.nr_ssd
+        avg_kib = 0.5 * self.nr_dma_blocks / self.nr_dma_submit if self.nr_dma_submit else 0.0
+        mib = self.pages * BLCKSZ / (1 << 20)
+        rate = mib / self.seconds if self.seconds > 0 else 0.0
+        lines = [
+            f"Custom Scan (NVMEStrom)  (actual rows={self.ntuples} pages={self.pages} workers={self.workers})",
+            f"  Blocks: ssd2dev={self.nr_ssd} ram2dev={self.nr_ram}"
+            + (f" ({100.0 * self.nr_ram / blocks:.1f}% page cache)" if blocks else ""),
+            f"  DMA: submits={self.nr_dma_submit} sectors={self.nr_dma_blocks} avg={avg_kib:.1f} KiB chunks={self.chunks}",
+            f"  Bad pages: {self.bad_pages}",
+            f"  Time: {self.seconds * 1e3:.2f} ms ({rate:.1f} MiB/s)",
+        ]
+        return "\n".join(lines)
 
 
 class HeapRelationScan:
@@ -201,9 +241,8 @@ class HeapRelationScan:
         if errors:
             raise errors[0]
         items = np.sort(np.concatenate([r.items for r in results])) if results else np.zeros(0, np.uint64)
-        out = ScanResult(items, sum(r.pages for r in results), sum(r.bad_pages for r in results),
-                         time.perf_counter() - t0, sum(r.nr_ram for r in results),
-                         sum(r.nr_ssd for r in results))
+        out = ScanResult(items, seconds=time.perf_counter() - t0, workers=workers)
+        out.merge(results)
         return out
 
     def _participant(self, cursor: ParallelCursor) -> ScanResult:
@@ -260,8 +299,7 @@ class HeapRelationScan:
         status = r.page_status.cpu().numpy()
         st.pages += n
         st.bad_pages += int(((status & 3) != 0).sum())
-        st.nr_ram += res.nr_ram
-        st.nr_ssd += res.nr_ssd
+        st.add_io(res)
 
 
 def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1,
@@ -289,8 +327,7 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                     items.extend(((base + c0 + (i >> 16)) << 16) | (i & 0xFFFF) for i in its)
                     st.pages += n
                     st.bad_pages += sum(1 for s in status if s & 3)
-                    st.nr_ram += r.nr_ram
-                    st.nr_ssd += r.nr_ssd
+                    st.add_io(r)
             finally:
                 os.close(fd)
     st.items = np.array(sorted(items), dtype=np.uint64)

@@ -72,11 +72,20 @@ def test_cpu_scan_segments_and_filter(strom, tmp_path):
     rel = pg_scan.Relation.write(str(tmp_path / "16384"), data, relseg_size=8)    # 3 segment files
     assert len(rel.segments) == 3 and rel.nblocks == 20
     cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192, verify_checksum=True)
+    for seg in rel.segments:
+        fd = os.open(seg, os.O_RDONLY)
+        S.api.evict_file(fd)
+        os.close(fd)
     r = pg_scan.cpu_scan(rel, cfg, attr_off=0, attr_width=8, lo=100, hi=299)
     exp = [v for v in range(100, 300) if v % 10 != 0]
     assert r.ntuples == len(exp) and r.bad_pages == 0
     blocks = (r.items >> np.uint64(16)).astype(int)
     assert set(blocks.tolist()) == {1, 2}
+    # per-scan counters (the reference's DSM stats) add up and are shown
+    assert r.nr_ram + r.nr_ssd == 20 and r.chunks == 5   # segments of 8+8+4 blocks, 4 per chunk
+    assert r.nr_ssd == 20 and r.nr_dma_submit >= 5 and r.nr_dma_blocks == 20 * 16
+    text = r.explain()
+    assert f"actual rows={len(exp)}" in text and "ssd2dev=" in text and "DMA: submits=" in text
 
 
 def test_arrow_ipc_metadata(tmp_path):
