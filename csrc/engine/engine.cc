@@ -541,7 +541,14 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
     }
   uint64_t n = len / chunk;
   if (n > (1u << 24) || (file_off / chunk + n) > 0xffffffffull) return -E2BIG;
-  std::vector<uint32_t> ids(n);
+  // small reads (the latency path) keep their chunk ids on the stack
+  uint32_t ids_small[16];
+  std::vector<uint32_t> ids_big;
+  uint32_t *ids = ids_small;
+  if (n > 16) {
+    ids_big.resize(n);
+    ids = ids_big.data();
+  }
   for (uint64_t i = 0; i < n; ++i) ids[i] = (uint32_t)(file_off / chunk + i);
   auto gmap = gpu_registry().get(handle);
   if (!gmap) return -ENOENT;
@@ -551,7 +558,7 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
   a.file_desc = fd;
   a.nr_chunks = (unsigned)n;
   a.chunk_sz = chunk;
-  a.chunk_ids = ids.data();
+  a.chunk_ids = ids;
   // page-cache chunks: straight into HBM when BAR-mapped, else a bounce
   std::vector<char> wb;
   if (!gmap->bar) {
@@ -605,6 +612,17 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
     }
   }
   return (long)len;
+}
+
+int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd,
+                        const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t t0 = mono_ns();
+    const long r = strom_pread_gpu(session, handle, offset, fd, file_offs[i], len);
+    ns_out[i] = mono_ns() - t0;
+    if (r < 0) return (int)r;
+  }
+  return 0;
 }
 
 int strom_config_set(const char *key, const char *value) {

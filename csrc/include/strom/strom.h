@@ -37,6 +37,11 @@ int nvme_strom_ioctl(unsigned long cmd, const void *arg);
  * file_off and len must be 4 KiB multiples.  Returns len or -errno. */
 long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
                      uint64_t file_off, uint64_t len);
+/* QD1 latency probe: n strom_pread_gpu calls of len bytes at file_offs[i],
+ * wall time of each in ns_out[i] (native loop, no caller overhead).
+ * Returns 0 or the first failure's -errno. */
+int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd,
+                        const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out);
 
 /* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
 int strom_config_set(const char *key, const char *value);

@@ -296,6 +296,18 @@ def pread_gpu(handle: int, offset: int, fd: int, file_off: int, length: int,
                   "pread_gpu")
 
 
+def pread_gpu_latency(handle: int, offset: int, fd: int, file_offs, length: int = 4096,
+                      sess: Optional[Session] = None) -> np.ndarray:
+    """QD1 latency probe: one synchronous pread_gpu per file offset, timed in
+    the native loop (the reference's C tools' vantage point).  -> ns per read."""
+    s = sess or session()
+    offs = np.ascontiguousarray(file_offs, dtype=np.uint64)
+    out = np.zeros(len(offs), dtype=np.uint64)
+    _check(s.lib.strom_pread_gpu_lat(s.sid, handle, offset, fd, offs.ctypes.data, len(offs),
+                                     length, out.ctypes.data), "pread_gpu_lat")
+    return out
+
+
 def memcpy_wait(task_id: int, timeout: Optional[float] = None,
                 sess: Optional[Session] = None) -> None:
     """Block until the task finishes; raises StromError(EIO, status=...) on a

@@ -170,6 +170,24 @@ def test_ssd2gpu_page_cache_hybrid_reorder(strom, rand_file):
         os.close(fd)
 
 
+def test_pread_gpu_latency_probe(strom, rand_file):
+    """Native QD1 probe: every read lands (last one checked) and is timed."""
+    path, data = rand_file(64 * 4096)
+    fd = _open(path)
+    try:
+        keep, hbm = _host_target(16 * 4096)
+        with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+            offs = np.array([5, 17, 63, 0, 40], dtype=np.uint64) * 4096
+            ns = strom.pread_gpu_latency(m.handle, 4096, fd, offs)
+            assert ns.shape == (5,) and (ns > 0).all()
+            assert np.array_equal(hbm[4096:8192], data[40 * 4096:41 * 4096])
+            with pytest.raises(strom.StromError) as e:
+                strom.pread_gpu_latency(m.handle, 0, fd, np.array([100], dtype=np.uint64) * 4096)
+            assert e.value.errno == errno.ERANGE
+    finally:
+        os.close(fd)
+
+
 def test_ssd2gpu_range_and_handle_checks(strom, rand_file):
     path, _ = rand_file(16 * CH)
     fd = _open(path)
