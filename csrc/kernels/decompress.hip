@@ -4,308 +4,396 @@
 // through the engine and are decompressed on the GPU before the filter.  The
 // reference has no decompressor; this is new MI355X-side work.
 //
-// One 64-lane workgroup (= one wavefront) decodes one stream at a time
-// (grid-stride over descriptors).  Parsing is wave-uniform; byte moves are
-// spread over the 64 lanes, one byte per lane per pass:
-//   * an 8 KiB LDS input window: tokens/lengths/offsets/literals are read from
-//     LDS; the window is refilled (one coalesced sweep) ahead of the parser;
-//   * a 64 KiB LDS history ring (LZ4 distances are < 64 KiB) serves every
-//     match source; each output byte is stored to HBM and to the ring in the
-//     same pass, so there is no flush pass and no HBM re-read;
-//   * overlapping matches (distance < length) never use a modulo in the
-//     copy loop: distance >= 64 copies pass by pass (each pass reads bytes a
-//     previous pass wrote); distance < 64 seeds one 64-byte pass from the
-//     pattern (k mod d, computed once per match) and continues with a period
-//     Q = d * ceil(64 / d) in [64, 127].
-// All positions are 32-bit (streams < 4 GiB).  Snappy copies farther than
-// 64 KiB (legal, never produced by 64 KiB-fragment compressors) read the
-// already-stored HBM output with L1-bypassing loads.
+// Why lane groups.  LZ4/snappy parsing is serial within a stream.  A
+// wave-per-stream decoder runs that parse on the scalar unit, and a CU has
+// ONE scalar unit shared by all its waves: the previous version of this file
+// measured ~130-160 CU-cycles per sequence (25-33 GB/s chip-wide) however
+// many waves were resident.  Here a wave decodes G = 64/GL streams at once,
+// one per group of GL lanes.  Every lane of a group runs the same parse on
+// the same bytes (group-uniform values in VGPRs), so each VALU instruction
+// advances G streams, and the copy work of a sequence is spread over the
+// group's lanes, BPL consecutive bytes per lane per pass.
+//
+// Per stream (LDS, per group):
+//   * an input window of kInW bytes, refilled with dword loads from 4-aligned
+//     addresses ("P space": positions offset by the stream's misalignment);
+//     token / length / offset bytes come from two dword reads + alignbyte;
+//   * a history ring of kRing bytes.  Match bytes are read from the ring
+//     with the period recurrence out[s+k] = out[s-off+(k mod off)], s = the
+//     pass start, so a pass only reads bytes written before it began
+//     (earlier passes' ds_writes precede its ds_reads in the wave's in-order
+//     LDS stream).  Matches farther than kRing - W read the wave's own HBM
+//     output instead (L1-bypassing loads after a fence; one fence covers all
+//     output before it).
+// The hot path issues no vector-memory loads, so it never waits on vmcnt,
+// which on CDNA also counts the wave's in-flight byte stores.
 //
 // Codecs: raw LZ4 block, LZ4 frame block sequence (linked or independent
-// blocks, optional per-block checksums skipped), raw snappy, stored copy.
+// blocks, optional per-block checksums skipped, stored blocks), raw snappy,
+// stored copy.  All positions are 32-bit (streams < 4 GiB).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "strom/strom.h"
 
+#ifndef STROM_DECOMP_GL
+#define STROM_DECOMP_GL 4u
+#endif
 #ifndef STROM_DECOMP_RING
-#define STROM_DECOMP_RING (8u << 10)
+#define STROM_DECOMP_RING (2u << 10)
 #endif
 #ifndef STROM_DECOMP_INW
-#define STROM_DECOMP_INW (2u << 10)
+#define STROM_DECOMP_INW 512u
 #endif
 
 namespace {
 
-// 16 KiB history + 4 KiB input = 20 KiB of LDS per wave -> 8 waves per CU.
-// (A full 64 KiB LZ4 window fits only 2 per CU, and a wave-serial decoder
-// is issue-bound: throughput scales with resident waves.)  Matches that
-// reach past the ring read the HBM output this wave already stored.
+constexpr uint32_t GL = STROM_DECOMP_GL;     // lanes per stream
+constexpr uint32_t G = 64 / GL;              // streams per wave
+constexpr uint32_t BPL = 4;                  // bytes per lane per pass
+constexpr uint32_t W = GL * BPL;             // bytes per pass per stream
 constexpr uint32_t kRing = STROM_DECOMP_RING;
 constexpr uint32_t kMask = kRing - 1;
 constexpr uint32_t kInW = STROM_DECOMP_INW;
-constexpr uint32_t kAhead = 512;  // keep this much input in the window
+constexpr uint32_t kSlot = kRing + kInW;     // LDS bytes per stream
+static_assert(64 % GL == 0 && (kRing & kMask) == 0, "geometry");
+static_assert(kRing >= 4 * W && kInW >= 4 * W && kInW % 4 == 0, "window sizes");
+static_assert(G * kSlot <= 64 * 1024, "LDS per wave");
+static_assert(kRing / 2 + 3 * W + 16 <= kRing, "flush pacing vs ring / far matches");
 
 enum : int32_t { kErrFormat = -1, kErrOverflow = -2 };
-
-// The workgroup is ONE wavefront, so lanes only need their LDS writes
-// ordered before later LDS reads.  __syncthreads() would also wait for every
-// outstanding HBM byte store (vmcnt(0)): ~1 us per call, twice per LZ4
-// sequence, which capped v1 at ~6 GB/s.  The asm also fences the compiler.
-__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+enum : uint32_t { kHdr = 0, kLz4 = 1, kSnappy = 2, kDone = 3 };
 
 __device__ __forceinline__ uint32_t ld_bypass_byte(const uint8_t *p) {
-  // dword-aligned agent-scope relaxed load: global_load ... sc1 (skips L1)
+  // dword-aligned agent-scope relaxed load: skips L1, sees this wave's
+  // fenced stores
   const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
   uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return (v >> (8 * ((uintptr_t)p & 3))) & 0xff;
 }
 
-struct Decoder {
-  const uint8_t *in;
+// Group-uniform stream state (every lane of a group holds the same values).
+struct Stream {
+  const uint8_t *ina;  // 4-aligned input base (= stream start - mis)
   uint8_t *out;
-  uint32_t ilen, ocap;
-  uint32_t op = 0, win = 0xffffffffu;
-  int32_t err = 0;
-  uint8_t *ring;
-  uint8_t *inw;
-  uint32_t lane;
+  uint8_t *ring;       // this group's LDS history ring
+  uint8_t *inw;        // this group's LDS input window
+  uint32_t t;          // lane within the group
+  uint32_t iend;       // input end (P space)
+  uint32_t ocap;       // output capacity
+  uint32_t ip;         // input position (P space)
+  uint32_t op;         // output position
+  uint32_t bend;       // end of the current LZ4 block (P space)
+  uint32_t win;        // window base (P space, 4-aligned); ~0 = empty
+  uint32_t vis;        // output below this is known complete in L2
+  uint32_t flushed;    // output below this has been stored to HBM
+  uint32_t omis;       // out & 15: ring index = (pos + omis) & kMask, so
+                       // 16-B ring chunks are 16-B aligned in HBM too
+  uint32_t olen;       // snappy: declared length
+  uint32_t mode;
+  int32_t err;
 
-  // Register window: 256 input bytes, one dword per lane; the wave-uniform
-  // parser reads them with v_readlane (scalar, a few cycles) instead of a
-  // dependent LDS round trip per token/length/offset byte.
-  uint32_t rwin = 0, rbase = 0xffffffffu;
-
-  __device__ void load_reg(uint32_t q) {  // q: 4-aligned, win covers q
-    const uint32_t o = q - win + 4 * lane;
-    rwin = o + 4 <= kInW ? *(const uint32_t *)(inw + o) : 0u;
-    rbase = q;
-  }
-  __device__ void load_window(uint32_t at) {
-    at &= ~3u;  // dword-aligned window base (register window loads)
-    lds_sync();
-    rbase = 0xffffffffu;
-    const uint32_t n = ilen - at < kInW ? ilen - at : kInW;
-    // dword sweep when aligned, bytes otherwise
-    const uint8_t *src = in + at;
-    if (((uintptr_t)src & 3) == 0) {
-      for (uint32_t k = lane * 4; k + 4 <= n; k += 256) *(uint32_t *)(inw + k) = *(const uint32_t *)(src + k);
-      for (uint32_t k = (n & ~3u) + lane; k < n; k += 64) inw[k] = src[k];
-    } else {
-      for (uint32_t k = lane; k < n; k += 64) inw[k] = src[k];
+  __device__ void refill(uint32_t p) {
+    const uint32_t at = p & ~3u;
+    const uint32_t n = iend - at < kInW ? iend - at : kInW;
+    const uint8_t *src = ina + at;
+    uint32_t k = t * 4;
+    // 8 independent dword loads in flight per lane, then their LDS writes
+    for (; k + 7 * GL * 4 + 4 <= n; k += 8 * GL * 4) {
+      uint32_t v[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) v[u] = *(const uint32_t *)(src + k + u * GL * 4);
+#pragma unroll
+      for (uint32_t u = 0; u < 8; ++u) *(uint32_t *)(inw + k + u * GL * 4) = v[u];
     }
+    for (; k + 4 <= n; k += GL * 4) *(uint32_t *)(inw + k) = *(const uint32_t *)(src + k);
+    for (uint32_t kb = (n & ~3u) + t; kb < n; kb += GL) inw[kb] = src[kb];  // <= 3 tail bytes
     win = at;
-    lds_sync();
   }
-  // keep [p, p + kAhead) inside the window when the input has it
-  __device__ void ensure(uint32_t p) {
-    const uint32_t end = p + kAhead < ilen ? p + kAhead : ilen;
-    if (p < win || end > win + kInW) load_window(p);
+  // window holds [p, p + need) (bytes past iend are never used)
+  __device__ __forceinline__ void ensure(uint32_t p, uint32_t need) {
+    if (p < win || p + need > win + kInW) refill(p);
   }
-  __device__ uint32_t byte(uint32_t p) {
-    if (p < rbase || p - rbase >= 256) {  // rbase = ~0 means empty
-      const uint32_t q = p & ~3u;
-      const uint32_t need = q + 256 < ilen ? q + 256 : ilen;
-      if (q < win || need > win + kInW) load_window(q);
-      load_reg(q);
-    }
-    const uint32_t rel = p - rbase;
-    const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)rwin, (int)(rel >> 2));
-    return (w >> (8 * (rel & 3))) & 0xffu;
+  // bytes p..p+3 (little endian) and, in *b4, byte p+4
+  __device__ __forceinline__ uint32_t rd4(uint32_t p, uint32_t *b4) {
+    ensure(p, 8);
+    const uint32_t o = p - win;
+    const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+    const uint32_t d0 = d[0], d1 = d[1];
+    const uint32_t sh = o & 3;
+    if (b4) *b4 = (d1 >> (8 * sh)) & 0xff;
+    return __builtin_amdgcn_alignbyte(d1, d0, sh);
   }
-  // literal bytes src[ip, ip+len) -> output
-  __device__ void literal(uint32_t ip, uint32_t len) {
-    for (uint32_t done = 0; done < len; done += 64) {
-      const uint32_t k = done + lane;
-      if (k < len) {
-        const uint32_t p = ip + k;
-        const uint8_t v = (p - win < kInW) ? inw[p - win] : in[p];
-        ring[(op + k) & kMask] = v;
-        out[op + k] = v;
+  __device__ __forceinline__ uint32_t rd1(uint32_t p) { return rd4(p, nullptr) & 0xff; }
+
+  __device__ __forceinline__ void put(uint32_t pos, uint8_t v) { ring[(pos + omis) & kMask] = v; }
+
+  // Store ring bytes [flushed, upto) to HBM: whole 16-B chunks as one
+  // dwordx4 store each (GL chunks per group instruction); partial chunks
+  // (stream head/tail) byte by byte.  exact=false leaves a partial last
+  // chunk for later.
+  __device__ void flush(uint32_t upto, bool exact) {
+    const uint32_t rb = flushed + omis, re = upto + omis;
+    const uint32_t cb = rb >> 4, ce = exact ? (re + 15) >> 4 : re >> 4;
+    for (uint32_t c = cb + t; c < ce; c += GL) {
+      const uint32_t r0 = c << 4;
+      const uint32_t lo = r0 < rb ? rb : r0, hi = r0 + 16 > re ? re : r0 + 16;
+      const uint4 v = *(const uint4 *)(ring + (r0 & kMask));
+      if (lo == r0 && hi == r0 + 16) {
+        *(uint4 *)(out + (r0 - omis)) = v;
+      } else {
+        for (uint32_t x = lo; x < hi; ++x) {
+          const uint32_t i = x - r0;
+          const uint32_t w = i < 8 ? (i < 4 ? v.x : v.y) : (i < 12 ? v.z : v.w);
+          out[x - omis] = (uint8_t)(w >> (8 * (i & 3)));
+        }
       }
     }
-    op += len;
-    lds_sync();
+    const uint32_t nf = exact ? upto : (ce << 4) - omis;
+    if (ce > cb && nf > flushed) flushed = nf;
   }
+  // bound the unflushed span so the ring never overwrites it (and far
+  // matches only read flushed output): called after every pass
+  __device__ __forceinline__ void pace(uint32_t cur) {
+    if (cur - flushed >= kRing / 2) flush(cur, false);
+  }
+
+  // literal bytes [p, p+len) of the input -> output
+  __device__ void literal(uint32_t p, uint32_t len) {
+    const uint32_t k = t * BPL;
+    for (uint32_t done = 0; done < len; done += W) {
+      const uint32_t n = len - done < W ? len - done : W;
+      ensure(p + done, W + 8);
+      if (k < n) {
+        const uint32_t o = p + done + k - win;
+        const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+        const uint32_t v = __builtin_amdgcn_alignbyte(d[1], d[0], o & 3);
+        const uint32_t s = op + done + k;
+#pragma unroll
+        for (uint32_t j = 0; j < BPL; ++j)
+          if (k + j < n) put(s + j, (uint8_t)(v >> (8 * j)));
+      }
+      pace(op + done + n);
+    }
+    op += len;
+  }
+
   __device__ void match(uint32_t off, uint32_t len) {
     if (off == 0 || off > op) {
       err = kErrFormat;
       return;
     }
-    const uint32_t s = op;
-    // near: every source byte stays in the ring for the whole match
-    const bool near = off < 64 || off + len <= kRing;
-    if (!near) {
-      // far copy: sources are in HBM already, written by this wave; make
-      // them visible to L1-bypassing loads
-      __threadfence();
-      for (uint32_t done = 0; done < len; done += 64) {
-        const uint32_t k = done + lane;
-        if (k < len) {
-          const uint8_t v = (uint8_t)ld_bypass_byte(out + s - off + k);
-          ring[(s + k) & kMask] = v;
-          out[s + k] = v;
+    const uint32_t k = t * BPL;
+    if (off <= kRing - W) {
+      if (off >= W) {
+        // sources [s-off, s-off+W) lie before the pass: one unaligned
+        // 4-byte read per lane (two dwords, ring-wrapped separately)
+        for (uint32_t done = 0; done < len; done += W) {
+          const uint32_t n = len - done < W ? len - done : W;
+          if (k < n) {
+            const uint32_t s = op + done + k;
+            const uint32_t q = s - off + omis;
+            const uint32_t a0 = q & kMask & ~3u;
+            const uint32_t d0 = *(const uint32_t *)(ring + a0);
+            const uint32_t d1 = *(const uint32_t *)(ring + ((a0 + 4) & kMask));
+            const uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, q & 3);
+#pragma unroll
+            for (uint32_t j = 0; j < BPL; ++j)
+              if (k + j < n) put(s + j, (uint8_t)(v >> (8 * j)));
+          }
+          pace(op + done + n);
         }
-        if (off < len) {
-          __threadfence();
-          lds_sync();
+      } else {
+        // short period: byte k of a pass starting at s repeats s-off+(k mod off)
+        uint32_t r[BPL];
+        r[0] = k % off;
+#pragma unroll
+        for (uint32_t j = 1; j < BPL; ++j) {
+          r[j] = r[j - 1] + 1;
+          if (r[j] >= off) r[j] = 0;
         }
-      }
-      op += len;
-      lds_sync();
-      return;
-    }
-    if (off >= 64 || off >= len) {
-      const bool overlap = off < len;
-      for (uint32_t done = 0; done < len; done += 64) {
-        const uint32_t k = done + lane;
-        if (k < len) {
-          const uint8_t v = ring[(s - off + k) & kMask];
-          ring[(s + k) & kMask] = v;
-          out[s + k] = v;
+        for (uint32_t done = 0; done < len; done += W) {
+          const uint32_t n = len - done < W ? len - done : W;
+          const uint32_t s = op + done;
+          uint8_t v[BPL];
+#pragma unroll
+          for (uint32_t j = 0; j < BPL; ++j) v[j] = ring[(s - off + r[j] + omis) & kMask];
+#pragma unroll
+          for (uint32_t j = 0; j < BPL; ++j)
+            if (k + j < n) put(s + k + j, v[j]);
+          pace(s + n);
         }
-        if (overlap) lds_sync();  // next pass may read this one
       }
     } else {
-      // short period: seed 64 bytes from the pattern, then period Q >= 64
-      const uint32_t q = off * ((64 + off - 1) / off);
-      const uint32_t r = lane % off;
-      if (lane < len) {
-        const uint8_t v = ring[(s - off + r) & kMask];
-        ring[(s + lane) & kMask] = v;
-        out[s + lane] = v;
-      }
-      lds_sync();
-      for (uint32_t done = 64; done < len; done += 64) {
-        const uint32_t k = done + lane;
-        if (k < len) {
-          const uint8_t v = ring[(s + k - q) & kMask];
-          ring[(s + k) & kMask] = v;
-          out[s + k] = v;
+      // far (off > kRing - W >= 3W): sources are this wave's stored output
+      for (uint32_t done = 0; done < len; done += W) {
+        const uint32_t n = len - done < W ? len - done : W;
+        const uint32_t s = op + done;
+        if (s - off + n > vis) {
+          // pace() keeps these sources flushed already; stay safe anyway
+          if (s - off + n > flushed) flush(s, true);
+          __threadfence();
+          vis = flushed;
         }
-        lds_sync();
+        if (k < n) {
+#pragma unroll
+          for (uint32_t j = 0; j < BPL; ++j)
+            if (k + j < n) put(s + k + j, (uint8_t)ld_bypass_byte(out + s + k + j - off));
+        }
+        pace(s + n);
       }
     }
     op += len;
-    lds_sync();
   }
-  // one raw LZ4 block occupying src[ip, end); returns new ip
-  __device__ uint32_t lz4_block(uint32_t ip, uint32_t end) {
-    while (ip < end && !err) {
-      ensure(ip);
-      const uint32_t token = byte(ip++);
-      uint32_t lit = token >> 4;
-      if (lit == 15) {
-        uint32_t b;
-        do {
-          if (ip >= end) { err = kErrFormat; return ip; }
-          b = byte(ip++);
-          lit += b;
-        } while (b == 255);
-      }
-      if (lit > end - ip) { err = kErrFormat; return ip; }
-      if (lit > ocap - op) { err = kErrOverflow; return ip; }
-      if (lit) literal(ip, lit);
-      ip += lit;
-      if (ip >= end) break;  // last sequence carries literals only
-      if (end - ip < 2) { err = kErrFormat; return ip; }
-      const uint32_t off = byte(ip) | (byte(ip + 1) << 8);
-      ip += 2;
-      uint32_t ml = token & 15;
-      if (ml == 15) {
-        uint32_t b;
-        do {
-          if (ip >= end) { err = kErrFormat; return ip; }
-          b = byte(ip++);
-          ml += b;
-        } while (b == 255);
-      }
-      ml += 4;
-      if (ml > ocap - op) { err = kErrOverflow; return ip; }
-      match(off, ml);
+
+  // ---- one LZ4 sequence of the block ending at bend
+  __device__ void lz4_seq() {
+    const uint32_t w = rd4(ip, nullptr);
+    uint32_t lit = (w >> 4) & 15, ml = w & 15;
+    uint32_t p = ip + 1;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (p >= bend) { err = kErrFormat; return; }
+        b = rd1(p++);
+        lit += b;
+      } while (b == 255);
     }
-    return ip;
+    if (lit > bend - p) { err = kErrFormat; return; }
+    if (lit > ocap - op) { err = kErrOverflow; return; }
+    if (lit) literal(p, lit);
+    p += lit;
+    if (p >= bend) { ip = p; return; }  // last sequence: literals only
+    if (bend - p < 2) { err = kErrFormat; return; }
+    // with no literals the offset bytes came with the token
+    const uint32_t off = (lit == 0 ? (w >> 8) : rd4(p, nullptr)) & 0xffff;
+    p += 2;
+    if (ml == 15) {
+      uint32_t b;
+      do {
+        if (p >= bend) { err = kErrFormat; return; }
+        b = rd1(p++);
+        ml += b;
+      } while (b == 255);
+    }
+    ml += 4;
+    if (ml > ocap - op) { err = kErrOverflow; return; }
+    match(off, ml);
+    ip = p;
   }
-  __device__ void snappy() {
-    uint32_t ip = 0;
-    uint64_t ulen = 0;
-    ensure(0);
-    for (int shift = 0;; shift += 7) {
-      if (ip >= ilen || shift > 35) { err = kErrFormat; return; }
-      const uint32_t b = byte(ip++);
-      ulen |= (uint64_t)(b & 0x7f) << shift;
-      if (!(b & 0x80)) break;
-    }
-    if (ulen > ocap) { err = kErrOverflow; return; }
-    const uint32_t olen = (uint32_t)ulen;
-    while (ip < ilen && !err) {
-      ensure(ip);
-      const uint32_t tag = byte(ip++);
-      uint32_t len, off;
-      const uint32_t kind = tag & 3;
-      if (kind == 0) {
-        len = (tag >> 2) + 1;
-        if (len > 60) {
-          const uint32_t nb = len - 60;
-          if (ilen - ip < nb) { err = kErrFormat; return; }
-          len = 0;
-          for (uint32_t i = 0; i < nb; ++i) len |= byte(ip + i) << (8 * i);
-          len += 1;
-          ip += nb;
-        }
-        if (len > ilen - ip || len > olen - op) { err = kErrFormat; return; }
-        literal(ip, len);
-        ip += len;
-        continue;
+
+  // ---- one snappy element (literal run or copy)
+  __device__ void snappy_tag() {
+    uint32_t b4;
+    const uint32_t w = rd4(ip, &b4);
+    const uint32_t tag = w & 0xff, kind = tag & 3;
+    uint32_t p = ip + 1, len, off;
+    if (kind == 0) {
+      len = (tag >> 2) + 1;
+      if (len > 60) {
+        const uint32_t nb = len - 60;  // 1..4 length bytes
+        if (iend - p < nb) { err = kErrFormat; return; }
+        const uint32_t x = nb == 4 ? ((w >> 8) | (b4 << 24)) : (w >> 8) & ((1u << (8 * nb)) - 1);
+        len = x + 1;
+        if (len == 0) { err = kErrFormat; return; }
+        p += nb;
       }
-      if (kind == 1) {
-        if (ip >= ilen) { err = kErrFormat; return; }
-        len = 4 + ((tag >> 2) & 7);
-        off = ((tag >> 5) << 8) | byte(ip++);
-      } else if (kind == 2) {
-        if (ilen - ip < 2) { err = kErrFormat; return; }
-        len = (tag >> 2) + 1;
-        off = byte(ip) | (byte(ip + 1) << 8);
-        ip += 2;
-      } else {
-        if (ilen - ip < 4) { err = kErrFormat; return; }
-        len = (tag >> 2) + 1;
-        off = byte(ip) | (byte(ip + 1) << 8) | (byte(ip + 2) << 16) | (byte(ip + 3) << 24);
-        ip += 4;
-      }
-      if (len > olen - op) { err = kErrFormat; return; }
-      match(off, len);
+      if (len > iend - p || len > olen - op) { err = kErrFormat; return; }
+      literal(p, len);
+      ip = p + len;
+      return;
     }
-    if (!err && op != olen) err = kErrFormat;
+    if (kind == 1) {
+      if (iend - p < 1) { err = kErrFormat; return; }
+      len = 4 + ((tag >> 2) & 7);
+      off = ((tag >> 5) << 8) | ((w >> 8) & 0xff);
+      p += 1;
+    } else if (kind == 2) {
+      if (iend - p < 2) { err = kErrFormat; return; }
+      len = (tag >> 2) + 1;
+      off = (w >> 8) & 0xffff;
+      p += 2;
+    } else {
+      if (iend - p < 4) { err = kErrFormat; return; }
+      len = (tag >> 2) + 1;
+      off = (w >> 8) | (b4 << 24);
+      p += 4;
+    }
+    if (len > olen - op) { err = kErrFormat; return; }
+    match(off, len);
+    ip = p;
   }
-  // LZ4 frame data blocks (after the frame header): [u32 size|flag][data][u32 bcs?]...
-  __device__ void lz4_frame_blocks(bool block_checksum) {
-    uint32_t ip = 0;
-    while (!err) {
-      if (ilen - ip < 4) { err = kErrFormat; return; }
-      ensure(ip);
-      uint32_t bs = byte(ip) | (byte(ip + 1) << 8) | (byte(ip + 2) << 16) | (byte(ip + 3) << 24);
+
+  // ---- stream-level headers: frame block header, snappy preamble, copy
+  __device__ void header(int codec) {
+    if (codec == STROM_CODEC_LZ4) {
+      bend = iend;
+      mode = kLz4;
+    } else if (codec == STROM_CODEC_SNAPPY) {
+      uint32_t p = ip, ulen = 0;
+      for (uint32_t shift = 0;; shift += 7) {
+        if (p >= iend || shift > 28) { err = kErrFormat; return; }
+        const uint32_t b = rd1(p++);
+        if (shift == 28 && (b & 0x70)) { err = kErrOverflow; return; }
+        ulen |= (b & 0x7f) << shift;
+        if (!(b & 0x80)) break;
+      }
+      if (ulen > ocap) { err = kErrOverflow; return; }
+      olen = ulen;
+      ip = p;
+      mode = kSnappy;
+    } else if (codec == STROM_CODEC_COPY) {
+      const uint32_t n = iend - ip;
+      if (n > ocap) { err = kErrOverflow; return; }
+      literal(ip, n);
+      ip = iend;
+      mode = kDone;
+    } else {
+      // LZ4 frame data blocks: [u32 size|stored flag][data][u32 bcs?]... [u32 0]
+      if (iend - ip < 4) { err = kErrFormat; return; }
+      uint32_t bs = rd4(ip, nullptr);
       ip += 4;
-      if (bs == 0) return;  // end mark
+      if (bs == 0) { mode = kDone; return; }
       const bool stored = bs & 0x80000000u;
       bs &= 0x7fffffffu;
-      if (bs > ilen - ip) { err = kErrFormat; return; }
+      if (bs > iend - ip) { err = kErrFormat; return; }
       if (stored) {
         if (bs > ocap - op) { err = kErrOverflow; return; }
-        for (uint32_t done = 0; done < bs; done += kInW / 2) {
-          const uint32_t n = bs - done < kInW / 2 ? bs - done : kInW / 2;
-          ensure(ip + done);
-          literal(ip + done, n);
-        }
+        literal(ip, bs);
         ip += bs;
+        if (codec == STROM_CODEC_LZ4_FRAME_BCS) ip += 4;
       } else {
-        const uint32_t end = ip + bs;
-        lz4_block(ip, end);
-        ip = end;
+        bend = ip + bs;
+        mode = kLz4;
       }
-      if (block_checksum) ip += 4;
     }
+  }
+
+  // one unit of work; false once the stream is finished (or failed)
+  __device__ bool step(int codec) {
+    if (mode == kHdr) {
+      header(codec);
+    } else if (mode == kLz4) {
+      if (ip >= bend) {
+        if (codec == STROM_CODEC_LZ4) {
+          mode = kDone;
+        } else {
+          ip = bend + (codec == STROM_CODEC_LZ4_FRAME_BCS ? 4 : 0);
+          mode = kHdr;
+        }
+      } else {
+        lz4_seq();
+      }
+    } else if (mode == kSnappy) {
+      if (ip >= iend) {
+        if (op != olen) err = kErrFormat;
+        mode = kDone;
+      } else {
+        snappy_tag();
+      }
+    }
+    return !err && mode != kDone;
   }
 };
 
@@ -313,42 +401,43 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
                                                         uint8_t *__restrict__ dst,
                                                         const strom_decomp_desc *__restrict__ desc,
                                                         uint32_t nblocks, int32_t *status) {
-  __shared__ uint8_t ring[kRing];
-  __shared__ __attribute__((aligned(16))) uint8_t inw[kInW];
-  for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-    const strom_decomp_desc d = desc[b];
-    Decoder dec;
-    dec.in = src + d.src_off;
-    dec.out = dst + d.dst_off;
-    dec.ilen = d.src_len;
-    dec.ocap = d.dst_len;
-    dec.ring = ring;
-    dec.inw = inw;
-    dec.lane = threadIdx.x;
-    switch (codec) {
-      case STROM_CODEC_LZ4:
-        dec.lz4_block(0, dec.ilen);
-        break;
-      case STROM_CODEC_SNAPPY:
-        dec.snappy();
-        break;
-      case STROM_CODEC_COPY:
-        if (dec.ilen > dec.ocap) {
-          dec.err = kErrOverflow;
-        } else {
-          for (uint32_t done = 0; done < dec.ilen; done += kInW / 2) {
-            const uint32_t n = dec.ilen - done < kInW / 2 ? dec.ilen - done : kInW / 2;
-            dec.ensure(done);
-            dec.literal(done, n);
-          }
-        }
-        break;
-      default:  // LZ4 frame blocks, with (5) or without (4) block checksums
-        dec.lz4_frame_blocks(codec == STROM_CODEC_LZ4_FRAME_BCS);
-        break;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G * kSlot];
+  const uint32_t lane = threadIdx.x, g = lane / GL;
+  const uint32_t stride = gridDim.x * G;
+  Stream st;
+  st.t = lane % GL;
+  st.ring = lds + g * kSlot;
+  st.inw = st.ring + kRing;
+  uint32_t b = blockIdx.x * G + g;
+  bool live = false;
+  for (;;) {
+    if (!live && b < nblocks) {
+      const strom_decomp_desc d = desc[b];
+      const uint8_t *in = src + d.src_off;
+      const uint32_t mis = (uint32_t)((uintptr_t)in & 3);
+      st.ina = in - mis;
+      st.out = dst + d.dst_off;
+      st.iend = d.src_len + mis;
+      st.ocap = d.dst_len;
+      st.ip = mis;
+      st.op = 0;
+      st.bend = 0;
+      st.win = 0xffffffffu;
+      st.vis = 0;
+      st.flushed = 0;
+      st.omis = (uint32_t)((uintptr_t)st.out & 15);
+      st.olen = 0;
+      st.mode = kHdr;
+      st.err = 0;
+      live = true;
     }
-    if (threadIdx.x == 0) status[b] = dec.err ? dec.err : (int32_t)dec.op;
-    lds_sync();
+    if (!__any(live)) break;
+    if (live && !st.step(codec)) {
+      if (!st.err) st.flush(st.op, true);
+      if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
+      live = false;
+      b += stride;
+    }
   }
 }
 
@@ -359,7 +448,8 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 int32_t *d_status, void *stream) {
   if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_LZ4_FRAME_BCS) return -22;
   if (!nblocks) return 0;
-  uint32_t grid = nblocks < 4096 ? nblocks : 4096;
+  const uint32_t waves = (nblocks + G - 1) / G;
+  const uint32_t grid = waves < 8192 ? waves : 8192;
   hipLaunchKernelGGL(decompress_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, codec,
                      (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;

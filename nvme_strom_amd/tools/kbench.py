@@ -78,23 +78,30 @@ def main(argv=None):
             timed(lambda: heap_scan(pages, verify_checksum=True, attr_off=0, attr_width=8,
                                     lo=100, hi=5000)), nb)
         del pages
+    rng = np.random.default_rng(1)
+    words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+    datasets = {
+        "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
+        # sorted int64 ids (a typical columnar payload)
+        "ints": np.cumsum(rng.integers(0, 5, 8192)).astype(np.int64).tobytes(),
+    }
     for codec in ("lz4", "snappy"):
         if codec not in only:
             continue
-        rng = np.random.default_rng(1)
-        words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
-        blk = b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10]
-        comp = D.lz4_compress(blk) if codec == "lz4" else D.snappy_compress(blk)
-        nblk = max(1, min(n // len(blk), 16384))
-        src = torch.from_numpy(np.frombuffer(comp * nblk, dtype=np.uint8).copy()).to(dev)
-        dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
-        descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk)) for i in range(nblk)])
-        cid = D.LZ4 if codec == "lz4" else D.SNAPPY
-        st = D.decompress(cid, src, dst, descs)
-        assert (st == len(blk)).all(), st[:4]
-        log(f"decompress_{codec}_64k_ratio{len(blk) / len(comp):.1f}",
-            timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
-        del src, dst
+        for dname, blk in datasets.items():
+            comp = D.lz4_compress(blk) if codec == "lz4" else D.snappy_compress(blk)
+            nblk = max(1, min(n // len(blk), 16384))
+            src = torch.from_numpy(np.frombuffer(comp * nblk, dtype=np.uint8).copy()).to(dev)
+            dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
+            descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk)) for i in range(nblk)])
+            cid = D.LZ4 if codec == "lz4" else D.SNAPPY
+            st = D.decompress(cid, src, dst, descs)
+            assert (st == len(blk)).all(), st[:4]
+            assert bytes(dst[:len(blk)].cpu().numpy()) == blk
+            tag = "64k" if dname == "words" else f"{dname}_64k"
+            log(f"decompress_{codec}_{tag}_ratio{len(blk) / len(comp):.1f}",
+                timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
+            del src, dst
     if "filter" in only:
         nv = n // 8
         v = torch.randint(-1000, 1000, (nv,), dtype=torch.int64, device=dev)

@@ -56,7 +56,13 @@ def _payloads():
     runs = b"".join(bytes([int(rng.integers(0, 3))]) * int(rng.integers(1, 500)) for _ in range(800))
     rand = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
     ints = np.cumsum(rng.integers(0, 5, 50000)).astype(np.int64).tobytes()
-    return [text, runs, rand, ints, b"x", b"", bytes(200000)]
+    # matches farther than the 8 KiB LDS ring (read back from HBM output),
+    # and a far match overlapping itself (distance 9000 < length)
+    r1, r2 = (rng.integers(0, 256, 20000, dtype=np.uint8).tobytes() for _ in range(2))
+    far = r1 + r2 + r1[:5000] + r2[3000:9000] + r1
+    r3 = rng.integers(0, 256, 9000, dtype=np.uint8).tobytes()
+    far_overlap = r3 * 5
+    return [text, runs, rand, ints, b"x", b"", bytes(200000), far, far_overlap]
 
 
 def _run(codec, streams, sizes, dev):
