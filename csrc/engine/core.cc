@@ -33,7 +33,8 @@ static bool parse_bool(const std::string &v) {
 Config Config::from_env() {
   Config c;
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
-                               "staging_slots", "inline_max", "bar_map", "bar_max", "trace",
+                               "staging_slots", "staging_bytes", "spin_us", "inline_max",
+                               "bar_map", "bar_max", "trace",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind",
                                "stat_info", "verbose"};
@@ -70,6 +71,12 @@ int Config::set(const std::string &k, const std::string &v) {
     return 0;
   }
   if (k == "staging_slots") { if (n < 1 || n > 1024) return -EINVAL; staging_slots = (int)n; return 0; }
+  if (k == "staging_bytes") {
+    if (n < 0 || n > (1l << 30)) return -EINVAL;
+    staging_bytes = (uint32_t)n;
+    return 0;
+  }
+  if (k == "spin_us") { if (n < 0 || n > 10000) return -EINVAL; spin_us = (uint32_t)n; return 0; }
   if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
   if (k == "trace") { trace = parse_bool(v); return 0; }
   if (k == "bar_max") {
@@ -98,6 +105,8 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "queue_depth") v = queue_depth;
   else if (k == "max_request") v = max_request;
   else if (k == "staging_slots") v = staging_slots;
+  else if (k == "staging_bytes") v = staging_bytes;
+  else if (k == "spin_us") v = spin_us;
   else if (k == "inline_max") v = inline_max;
   else if (k == "bar_map") v = bar_map;
   else if (k == "trace") v = trace;
@@ -252,6 +261,7 @@ void TaskTable::put(Task *t, long status) {
   {
     std::lock_guard<std::mutex> g(s.mu);
     s.running.erase(t->id);
+    s.done_seq.fetch_add(1, std::memory_order_release);
     if (t->status.load() != 0) {
       t->gmap.reset();
       t->dbuf.reset();
@@ -271,6 +281,8 @@ int TaskTable::wait(uint64_t id, long *status, int64_t timeout_ns) {
                   std::chrono::nanoseconds(timeout_ns < 0 ? 0 : timeout_ns);
   std::unique_lock<std::mutex> g(s.mu);
   int rc;
+  bool spun = false;
+  uint64_t spin_end = 0;
   for (;;) {
     auto f = s.failed.find(id);
     if (f != s.failed.end()) {
@@ -282,6 +294,22 @@ int TaskTable::wait(uint64_t id, long *status, int64_t timeout_ns) {
     }
     if (s.running.count(id)) {
       if (timeout_ns == 0) { rc = -ETIME; break; }
+      // short I/O finishes within a futex wake-up's latency: poll the
+      // slot's completion counter (no lock) until one overall deadline
+      if (!spun) {
+        spun = true;
+        uint64_t spin_ns = (uint64_t)config().spin_us * 1000;
+        if (timeout_ns > 0 && (uint64_t)timeout_ns < spin_ns) spin_ns = (uint64_t)timeout_ns;
+        spin_end = mono_ns() + spin_ns;
+      }
+      if (mono_ns() < spin_end) {
+        const uint64_t seq0 = s.done_seq.load(std::memory_order_acquire);
+        g.unlock();
+        while (s.done_seq.load(std::memory_order_acquire) == seq0 && mono_ns() < spin_end)
+          for (int i = 0; i < 32; ++i) _mm_pause();
+        g.lock();
+        continue;
+      }
       if (slept) stats().nr_wrong_wakeup++;
       slept = true;
       if (timeout_ns < 0) {

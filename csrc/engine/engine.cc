@@ -26,6 +26,10 @@
 #include "engine.h"
 
 namespace strom {
+// set while strom_pread_gpu runs: a synchronous caller gains nothing from a
+// worker hand-off, so its single request runs inline at any size
+static thread_local bool tl_sync_call = false;
+
 
 struct Engine::OpenFile {
   dev_t dev = 0;
@@ -287,7 +291,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, gmap.get(),
                  gmap->va + a->offset, host_dest, &reqs);
   uint64_t t0 = tsc_now();
-  if (reqs.size() == 1 && reqs[0].len <= config().inline_max)
+  if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
     io_->run_inline(reqs[0]);
   else
     io_->submit(reqs);
@@ -354,7 +358,7 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, nullptr,
                  (uint64_t)a->dest_uaddr, true, &reqs);
   uint64_t t0 = tsc_now();
-  if (reqs.size() == 1 && reqs[0].len <= config().inline_max)
+  if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
     io_->run_inline(reqs[0]);
   else
     io_->submit(reqs);
@@ -565,7 +569,9 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
     wb.resize(len);
     a.wb_buffer = wb.data();
   }
+  strom::tl_sync_call = true;
   int rc = strom_ioctl(session, STROM_IOCTL__MEMCPY_SSD2GPU, &a);
+  strom::tl_sync_call = false;
   if (rc) return rc;
   strom_memcpy_wait w{};
   w.dma_task_id = a.dma_task_id;

@@ -46,7 +46,14 @@ struct Config {
   int workers = 4;               // I/O worker threads (one SDMA stream each)
   int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
-  int staging_slots = 4;         // pinned slots per worker (GPU dest)
+  int staging_slots = 4;         // minimum pinned slots per worker (GPU dest)
+  uint32_t staging_bytes = 0;    // opt-in: pinned staging per worker, slots =
+                                 // max(staging_slots, staging_bytes / max_request),
+                                 // queue depth grows to match.  Off by default:
+                                 // the box's storage lost throughput with more
+                                 // in flight (profiles/r1e/sweep_*.json)
+  uint32_t spin_us = 20;         // idle workers / WAIT spin this long before
+                                 // sleeping on a futex (hand-off latency)
   uint32_t inline_max = 64u << 10;  // single requests up to this run inline
   bool bar_map = true;           // CPU-map HBM through the large BAR (dma-buf)
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
@@ -141,6 +148,7 @@ class TaskTable {
     std::condition_variable cv;
     std::unordered_map<uint64_t, Task *> running;
     std::unordered_map<uint64_t, Task *> failed;
+    std::atomic<uint64_t> done_seq{0};  // bumped per finished task (lock-free spin)
   };
   Slot &slot_of(uint64_t id) { return slots_[(id * 0x9E3779B97F4A7C15ull) >> 55]; }
   Slot slots_[kSlots];

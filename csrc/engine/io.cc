@@ -24,6 +24,7 @@
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <x86intrin.h>
 
 #include <fstream>
 
@@ -192,6 +193,8 @@ struct IoEngine::Worker {
   std::condition_variable cv;
   std::deque<IoReq> q;
   bool stop = false;
+  bool sleeping = false;            // in cv.wait (guarded by mu)
+  std::atomic<int> pending{0};      // q non-empty hint for the idle spin
   std::vector<Slot> slots;
   uint8_t *staging = nullptr;     // one registered region, cut into slots
   size_t staging_bytes = 0;
@@ -236,9 +239,17 @@ struct IoEngine::Worker {
     }
   }
 
+  // staging slots: at least staging_slots, else as many max_request-sized
+  // slots as staging_bytes holds (small requests keep many in flight)
+  int nslots() const {
+    const size_t by_bytes = cfg.staging_bytes / cfg.max_request;
+    return (int)std::max<size_t>(cfg.staging_slots, std::min<size_t>(by_bytes, 256));
+  }
+
   bool ensure_slots() {
     if (!slots.empty()) return true;
-    size_t bytes = (size_t)cfg.staging_slots * cfg.max_request;
+    const int ns = nslots();
+    size_t bytes = (size_t)ns * cfg.max_request;
     staging = (uint8_t *)hip::host_alloc_thp(bytes);
     staging_thp = staging != nullptr;
     if (!staging) staging = (uint8_t *)hip::host_alloc(bytes);
@@ -247,8 +258,8 @@ struct IoEngine::Worker {
       return false;
     }
     staging_bytes = bytes;
-    slots.resize(cfg.staging_slots);
-    for (int i = 0; i < cfg.staging_slots; ++i) {
+    slots.resize(ns);
+    for (int i = 0; i < ns; ++i) {
       slots[i].buf = staging + (size_t)i * cfg.max_request;
       free_slots.push_back(i);
     }
@@ -407,17 +418,29 @@ struct IoEngine::Worker {
   void run() {
     bind_numa();
     bool use_ring = cfg.backend == BackendKind::kUring;
-    if (use_ring && ring.init((unsigned)std::max(8, cfg.queue_depth * 2)) != 0) use_ring = false;
-    int qd = use_ring ? cfg.queue_depth : 1;
+    const int qd_cfg = std::max(cfg.queue_depth, nslots());
+    if (use_ring && ring.init((unsigned)std::max(8, qd_cfg * 2)) != 0) use_ring = false;
+    int qd = use_ring ? qd_cfg : 1;
+    const uint64_t spin_ns = (uint64_t)cfg.spin_us * 1000;
     std::deque<IoReq> local;
     for (;;) {
       if (local.empty()) {
+        if (spin_ns && reads_inflight == 0 && copying.empty() && !pending.load(std::memory_order_acquire)) {
+          // idle: poll briefly before sleeping, so back-to-back work skips
+          // the futex wake-up (bounded, so stop is still seen promptly)
+          const uint64_t end = mono_ns() + spin_ns;
+          while (!pending.load(std::memory_order_acquire) && mono_ns() < end)
+            for (int i = 0; i < 32; ++i) _mm_pause();
+        }
         std::unique_lock<std::mutex> g(mu);
         if (q.empty() && reads_inflight == 0 && copying.empty()) {
           if (stop) break;
+          sleeping = true;
           cv.wait(g, [&] { return stop || !q.empty(); });
+          sleeping = false;
         }
         local.swap(q);
+        pending.store(0, std::memory_order_relaxed);
       }
       // issue as much as the queue depth and staging allow
       bool blocked = false;
@@ -548,11 +571,14 @@ void IoEngine::submit(std::vector<IoReq> &reqs) {
     size_t lo = k * per, hi = std::min(reqs.size(), lo + per);
     if (lo >= hi) break;
     Worker &w = *workers_[(start + k) % n];
+    bool wake;
     {
       std::lock_guard<std::mutex> g(w.mu);
       for (size_t i = lo; i < hi; ++i) w.q.push_back(reqs[i]);
+      w.pending.store(1, std::memory_order_release);
+      wake = w.sleeping;
     }
-    w.cv.notify_one();
+    if (wake) w.cv.notify_one();
   }
 }
 

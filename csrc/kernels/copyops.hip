@@ -54,16 +54,32 @@ __global__ __launch_bounds__(256) void chunk_gather_kernel(const uint8_t *__rest
   }
 }
 
+// Block-level result: wave reduce, then across the block's waves in LDS, then
+// at most ONE atomic pair per block.  Same-address atomics serialize in L2
+// (~90 per us), so a per-wave pair made a mismatching 1 GiB verify take
+// ~0.4 ms on atomics alone.
 __device__ __forceinline__ void report(uint64_t bad, uint64_t first, uint64_t *out) {
-  // wave reduce, then one atomic pair per wave
+  __shared__ uint64_t s_bad[4], s_first[4];  // blockDim.x == 256
   for (int o = 32; o > 0; o >>= 1) {
     bad += __shfl_xor(bad, o, 64);
     uint64_t f2 = __shfl_xor(first, o, 64);
     first = f2 < first ? f2 : first;
   }
-  if ((threadIdx.x & 63) == 0 && bad) {
-    atomicAdd((unsigned long long *)&out[0], (unsigned long long)bad);
-    atomicMin((unsigned long long *)&out[1], (unsigned long long)first);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_bad[w] = bad;
+    s_first[w] = first;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      bad += s_bad[i];
+      first = s_first[i] < first ? s_first[i] : first;
+    }
+    if (bad) {
+      atomicAdd((unsigned long long *)&out[0], (unsigned long long)bad);
+      atomicMin((unsigned long long *)&out[1], (unsigned long long)first);
+    }
   }
 }
 
@@ -157,6 +173,12 @@ inline uint32_t grid_for(uint64_t items, uint32_t per_block) {
   return (uint32_t)(g > 4096 ? 4096 : g);
 }
 
+// verify: <= 1024 blocks (4 per CU), each sweeping one contiguous range
+inline uint32_t verify_grid(uint64_t nwords) {
+  const uint32_t g = grid_for(nwords / 4 + 1, 256 * 4);
+  return g > 1024 ? 1024 : g;
+}
+
 inline int launched() { return hipGetLastError() == hipSuccess ? 0 : -5; }
 
 }  // namespace
@@ -186,7 +208,7 @@ extern "C" int strom_verify_pattern(const void *d_buf, uint64_t nbytes, uint32_t
   if (((uintptr_t)d_buf & 15) || (nbytes & 3)) return -22;
   hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, d_out);
   uint64_t nw = nbytes / 4;
-  hipLaunchKernelGGL(verify_pattern_kernel, dim3(grid_for(nw / 4 + 1, 256 * 4)), dim3(256), 0,
+  hipLaunchKernelGGL(verify_pattern_kernel, dim3(verify_grid(nw)), dim3(256), 0,
                      (hipStream_t)stream, (const uint32_t *)d_buf, nw, pattern, d_out);
   return launched();
 }
@@ -196,7 +218,7 @@ extern "C" int strom_verify_equal(const void *d_a, const void *d_b, uint64_t nby
   if (((uintptr_t)d_a & 15) || ((uintptr_t)d_b & 15) || (nbytes & 3)) return -22;
   hipLaunchKernelGGL(report_init_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, d_out);
   uint64_t nw = nbytes / 4;
-  hipLaunchKernelGGL(verify_equal_kernel, dim3(grid_for(nw / 4 + 1, 256 * 4)), dim3(256), 0,
+  hipLaunchKernelGGL(verify_equal_kernel, dim3(verify_grid(nw)), dim3(256), 0,
                      (hipStream_t)stream, (const uint32_t *)d_a, (const uint32_t *)d_b, nw,
                      d_out);
   return launched();

@@ -1,0 +1,117 @@
+"""Block-size sweep, 4 KiB - 4 MiB (BASELINE config 2).
+
+For each block size B the engine's request limit is set to B (every storage
+read is at most B bytes, the reference's merge cap, kmod/nvme_strom.c:119-125)
+and the file is streamed into HBM with the nvme_test shape (32 MiB segments,
+6 in flight, chunk = min(B, 8 KiB); utils/nvme_test.c:40-41, 383-498):
+
+  GiBps        whole-window throughput (page cache evicted first)
+  iops         completed storage requests per second during that stream
+  p50/p99_us   QD1 latency of single B-byte reads into HBM (native loop)
+
+``python -m nvme_strom_amd.tools.sweep --out gpurun_out/sweep.json``
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def _mk(path: str, nbytes: int) -> None:
+    if os.path.exists(path) and os.path.getsize(path) == nbytes:
+        return
+    rng = np.random.default_rng(11)
+    with open(path, "wb") as f:
+        left = nbytes
+        while left:
+            n = min(64 << 20, left)
+            f.write(rng.integers(0, 1 << 63, size=n // 8, dtype=np.uint64).tobytes())
+            left -= n
+        os.fsync(f.fileno())
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--file-gib", type=float, default=2.0)
+    ap.add_argument("--dir", default="/tmp/strom_sweep")
+    ap.add_argument("--blocks", default="4K,8K,16K,32K,64K,128K,256K,512K,1M,2M,4M")
+    ap.add_argument("--max-gib", type=float, default=1.0, help="bytes streamed per block size (cap)")
+    ap.add_argument("--lat-samples", type=int, default=300)
+    ap.add_argument("--qd", type=int, default=0, help="engine queue depth override (0 = default)")
+    ap.add_argument("--device", default="cuda", help="cpu = emulated HBM (tests)")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    import nvme_strom_amd as S
+
+    def sync():
+        if a.device != "cpu":
+            torch.cuda.synchronize()
+    from nvme_strom_amd.models.ssd2gpu_stream import StreamLoader
+
+    def size(s: str) -> int:
+        m = {"K": 1 << 10, "M": 1 << 20, "G": 1 << 30}
+        return int(s[:-1]) * m[s[-1]] if s[-1] in m else int(s)
+
+    os.makedirs(a.dir, exist_ok=True)
+    path = os.path.join(a.dir, "sweep.bin")
+    F = int(a.file_gib * (1 << 30)) // (4 << 20) * (4 << 20)
+    _mk(path, F)
+    fd = os.open(path, os.O_RDONLY)
+    defaults = {k: S.config_get(k) for k in ("max_request", "queue_depth")}
+    rows = []
+    try:
+        for B in [size(x) for x in a.blocks.split(",")]:
+            kv = {"max_request": B}
+            if a.qd:
+                kv["queue_depth"] = a.qd
+            S.configure(**kv)
+            chunk = min(B, 8192)
+            nbytes = min(int(a.max_gib * (1 << 30)), B * 65536, F) // (32 << 20) * (32 << 20)
+            nbytes = max(nbytes, 32 << 20)
+            ld = StreamLoader(path, segment_sz=32 << 20, nr_segments=6, chunk_sz=chunk,
+                              device=a.device, depth=6)
+            S.evict_file(fd)
+            ld.run(0, 32 << 20)                      # warm the engine, not the cache
+            S.evict_file(fd)
+            sync()
+            st = ld.run(0, nbytes)
+            sync()
+            gibs = nbytes / st.seconds / (1 << 30)
+            iops = st.nr_submit / st.seconds
+            # QD1 latency of B-byte reads at random aligned offsets
+            S.evict_file(fd)
+            rng = np.random.default_rng(B)
+            offs = rng.integers(0, F // B, size=a.lat_samples + 20) * B
+            ns = S.pread_gpu_latency(ld.buf.handle, 0, fd, offs, B)[20:] / 1e3
+            row = dict(block=B, GiBps=round(gibs, 2), iops=round(iops), bytes=nbytes,
+                       avg_req_kib=round(0.5 * st.nr_blocks / st.nr_submit, 1) if st.nr_submit else 0,
+                       ram_chunks=st.nr_ram, p50_us=round(float(np.percentile(ns, 50)), 2),
+                       p99_us=round(float(np.percentile(ns, 99)), 2))
+            rows.append(row)
+            _log(json.dumps(row))
+            ld.close()
+    finally:
+        S.configure(**defaults)
+        os.close(fd)
+    out = dict(workers=int(S.config_get("workers")), queue_depth=a.qd or int(defaults["queue_depth"]),
+               backend=S.config_get("backend"), file_bytes=F, rows=rows)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+    print(json.dumps(out))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

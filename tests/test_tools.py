@@ -52,3 +52,20 @@ def test_strom_test_cli_verify(rand_file):
     pr = subprocess.run([_tool("strom_test"), "-p", path], capture_output=True, text=True,
                         timeout=120, env=_env())
     assert pr.returncode == 0 and "mapped region" in pr.stdout
+
+
+def test_block_sweep_cpu(strom, tmp_path):
+    """Block-size sweep tool end to end on emulated HBM (small sizes)."""
+    from nvme_strom_amd.tools import sweep
+    out = tmp_path / "sweep.json"
+    rc = sweep.main(["--file-gib", "0.125", "--dir", str(tmp_path), "--blocks", "4K,64K,1M",
+                     "--max-gib", "0.0625", "--lat-samples", "20", "--device", "cpu",
+                     "--out", str(out)])
+    assert rc == 0
+    import json
+    rows = json.load(open(out))["rows"]
+    assert [r["block"] for r in rows] == [4096, 65536, 1 << 20]
+    for r in rows:
+        assert r["GiBps"] > 0 and r["p50_us"] > 0
+        assert r["avg_req_kib"] <= r["block"] / 1024
+    assert strom.config_get("max_request") == str(1 << 20)   # restored
