@@ -8,7 +8,7 @@ OUT      := nvme_strom_amd/lib
 OBJ      := build/obj
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Icsrc/include -Icsrc/engine
 HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
-LDFLAGS  := -shared -fPIC -lpthread -L$(ROCM)/lib -lrocprofiler-sdk-roctx
+LDFLAGS  := -shared -fPIC -lpthread -L$(ROCM)/lib -lrocprofiler-sdk-roctx -lhsa-runtime64
 
 ENGINE_SRC := $(wildcard csrc/engine/*.cc)
 KERNEL_SRC := $(wildcard csrc/kernels/*.hip)
@@ -45,7 +45,7 @@ clean:
 # are not part of these builds.  GPU sanitizers are not used on this pool.
 SELFTEST_SRC := csrc/tests/engine_selftest.cc $(ENGINE_SRC)
 SELFTEST_FLAGS := -std=c++17 -g -O1 -Icsrc/include -Icsrc/engine -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
-SELFTEST_LIBS := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
+SELFTEST_LIBS := -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
 
 build/selftest: $(SELFTEST_SRC) csrc/engine/engine.h
 	@mkdir -p build

@@ -34,6 +34,8 @@ static thread_local bool tl_sync_call = false;
 struct Engine::OpenFile {
   dev_t dev = 0;
   ino_t ino = 0;
+  struct timespec ctim {};    // st_ctim when last validated
+  off_t vsize = -1;           // st_size when last validated
   int fd_direct = -1;
   int fd_buffered = -1;
   FileClass fc;
@@ -91,10 +93,18 @@ std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
   auto it = files_.find(key);
   if (it != files_.end()) {
     std::shared_ptr<OpenFile> f = it->second;
+    // Fast path: same ctime and size as when the entry was validated.  A
+    // recycled inode number (cached file deleted, new one created) comes
+    // with a new ctime, so only then is the cached descriptor re-checked.
+    if (f->vsize == st.st_size && f->ctim.tv_sec == st.st_ctim.tv_sec &&
+        f->ctim.tv_nsec == st.st_ctim.tv_nsec)
+      return f;
     struct stat cst;
     bool stale = fstat(f->fd_buffered, &cst) != 0 || cst.st_nlink == 0 ||
                  cst.st_ino != st.st_ino;
     if (!stale) {
+      f->ctim = st.st_ctim;
+      f->vsize = st.st_size;
       if ((off_t)f->fc.size != st.st_size) {
         std::lock_guard<std::mutex> fg(f->mu);
         f->fc.size = st.st_size;
@@ -133,6 +143,8 @@ std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
   }
   f->dev = st.st_dev;
   f->ino = st.st_ino;
+  f->ctim = st.st_ctim;
+  f->vsize = st.st_size;
   if (config().pgcache_probe && st.st_size > 0) {
     void *m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, f->fd_buffered, 0);
     if (m != MAP_FAILED) {
@@ -301,10 +313,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   // page-cache chunks overlap with the storage reads
   if (plan.nr_ram) {
     rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, ram_dest);
-    if (rc == 0 && !a->wb_buffer) {
-      _mm_sfence();
-      (void)*(volatile uint32_t *)ram_dest;  // flush posted BAR writes
-    }
+    if (rc == 0 && !a->wb_buffer) gmap->bar_flush((const uint8_t *)ram_dest);
   }
   t->frozen = true;
   uint64_t id = t->id;

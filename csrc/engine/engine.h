@@ -174,11 +174,17 @@ struct GpuMapping {
   uint8_t *bar = nullptr;
   uint64_t bar_va = 0;
   size_t bar_len = 0;
+  volatile uint32_t *hdp = nullptr;  // HDP_MEM_FLUSH_CNTL of the device, or null
   std::atomic<int> inflight{0};
   // CPU store of [src, src+len) into HBM at device VA dst through the BAR;
   // false when the range is not BAR-mapped.  Ends with a read-back that
   // flushes the posted writes, so the data is in HBM when this returns.
   bool bar_write(uint64_t dst, const void *src, size_t len) const;
+  // make CPU stores through the BAR (ending at `last`) visible to shaders:
+  // sfence, then an HDP flush (write + read back the flush register, as
+  // the runtime does for CPU-written kernargs in VRAM); without the
+  // register, a read-back of the last dword drains the posted writes
+  void bar_flush(const uint8_t *last) const;
   ~GpuMapping();
   bool detached = false;
   std::mutex mu;
@@ -352,6 +358,7 @@ void host_free_thp(void *p, size_t bytes);
 // CPU mapping of device memory [va, va+len) through its dma-buf export;
 // returns the mapping (and sets *map_va/*map_len to what it covers) or null.
 uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len);
+volatile uint32_t *hdp_flush_reg(int device);  // null when not exposed
 void bar_unmap(uint8_t *p, size_t len);
 int copy_dtoh(void *dst, uint64_t src, size_t len);   // synchronous, 0 / -EIO
 int copy_htod(uint64_t dst, const void *src, size_t len);

@@ -6,6 +6,8 @@
 // calling thread's NUMA policy (hipHostMallocNumaUser), which the I/O
 // workers set to the node of the GPU's PCIe root before allocating.
 #include <hip/hip_runtime_api.h>  // host API only: builds with g++ (sanitizers)
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <errno.h>
 #include <stdio.h>
 #include <string.h>
@@ -14,6 +16,7 @@
 #include <x86intrin.h>
 
 #include <cctype>
+#include <map>
 #include <mutex>
 #include <string>
 
@@ -160,6 +163,53 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
   *map_va = lo;
   *map_len = hi - lo;
   return (uint8_t *)p;
+}
+
+namespace {
+struct HdpFind {
+  uint32_t domain, bdf;
+  volatile uint32_t *reg;
+};
+hsa_status_t hdp_agent_cb(hsa_agent_t a, void *p) {
+  auto *f = (HdpFind *)p;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS ||
+      t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  (void)hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+  if (bdf != f->bdf || dom != f->domain) return HSA_STATUS_SUCCESS;
+  hsa_amd_hdp_flush_t h{};
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &h) == HSA_STATUS_SUCCESS)
+    f->reg = h.HDP_MEM_FLUSH_CNTL;
+  return HSA_STATUS_INFO_BREAK;
+}
+}  // namespace
+
+// The HSA agent of a HIP device is found by PCI location (HIP and HSA may
+// order devices differently); hsa_init is reference counted and HIP has
+// already initialised the runtime.
+volatile uint32_t *hdp_flush_reg(int device) {
+  static std::mutex mu;
+  static std::map<int, volatile uint32_t *> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  volatile uint32_t *reg = nullptr;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) == hipSuccess && hsa_init() == HSA_STATUS_SUCCESS) {
+    HdpFind f{(uint32_t)p.pciDomainID, ((uint32_t)p.pciBusID << 8) | ((uint32_t)p.pciDeviceID << 3),
+              nullptr};
+    (void)hsa_iterate_agents(hdp_agent_cb, &f);
+    reg = f.reg;
+  } else {
+    (void)hipGetLastError();
+  }
+  STROM_LOG(1, "device %d: HDP flush register %p", device, (void *)reg);
+  cache[device] = reg;
+  return reg;
 }
 
 void bar_unmap(uint8_t *p, size_t len) {

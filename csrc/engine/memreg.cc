@@ -47,10 +47,19 @@ bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len) const {
   if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
   uint8_t *p = bar + (dst - bar_va);
   memcpy(p, src, len);
-  _mm_sfence();
-  // a read from the device cannot pass the posted writes before it
-  (void)*(volatile uint32_t *)(p + ((len - 1) & ~(size_t)3));
+  bar_flush(p + ((len - 1) & ~(size_t)3));
   return true;
+}
+
+void GpuMapping::bar_flush(const uint8_t *last) const {
+  _mm_sfence();
+  if (hdp) {
+    *hdp = 1u;
+    (void)*hdp;
+  } else {
+    // a read from the device cannot pass the posted writes before it
+    (void)*(const volatile uint32_t *)last;
+  }
 }
 
 int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memory *out) {
@@ -78,6 +87,7 @@ int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memor
   if (npages > 0xffffffffull) return -E2BIG;
   if (device >= 0 && config().bar_map) {
     m->bar = hip::bar_map(va, len, &m->bar_va, &m->bar_len);
+    if (m->bar) m->hdp = hip::hdp_flush_reg(device);
     STROM_LOG(1, "bar map of %#lx: %s", (unsigned long)va, m->bar ? "yes" : "no");
   }
   {

@@ -13,7 +13,7 @@ for cfg in "4 2048 512" "4 1024 256" "4 2048 256" "2 1024 256" "2 512 256" "8 20
     -DSTROM_DECOMP_GL=${1}u -DSTROM_DECOMP_RING=${2}u -DSTROM_DECOMP_INW=${3}u \
     -c csrc/kernels/decompress.hip -o /tmp/decompress.o || exit 1
   objs=$(ls build/obj/engine/*.o build/obj/kernels/*.o | grep -v decompress.o)
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o nvme_strom_amd/lib/libstrom.so $objs /tmp/decompress.o -lpthread -L/opt/rocm/lib -lrocprofiler-sdk-roctx || exit 1
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o nvme_strom_amd/lib/libstrom.so $objs /tmp/decompress.o -lpthread -L/opt/rocm/lib -lrocprofiler-sdk-roctx -lhsa-runtime64 || exit 1
   echo "gl=$1 ring=$2 inw=$3"
   timeout -k 10 200 python -m nvme_strom_amd.tools.kbench --gib 1 --only lz4,snappy 2>&1 | grep decompress
   rc=$?; [ $rc -eq 0 ] || { echo "kbench rc=$rc"; cp /tmp/libstrom.default.so nvme_strom_amd/lib/libstrom.so; exit $rc; }
