@@ -43,6 +43,11 @@ Config Config::from_env() {
     for (const char *p = k; *p; ++p) env += (char)toupper(*p);
     if (const char *v = getenv(env.c_str())) c.set(k, v);
   }
+  // ranks of one node share its storage: past ~4 reader threads in all the
+  // pool box loses throughput (8 ranks x 4 workers 12.7 GiB/s, 8 x 1 21.7,
+  // profiles/r1k), so under torchrun the default pool shrinks per rank
+  const char *lw = getenv("LOCAL_WORLD_SIZE");
+  if (!getenv("STROM_WORKERS") && lw && atoi(lw) > 1) c.workers = std::max(1, c.workers / atoi(lw));
   return c;
 }
 

@@ -299,7 +299,12 @@ struct IoEngine::Worker {
       finish_request(r, status);
       return;
     }
-    if (r.len <= cfg.bar_max && r.gmap && r.gmap->bar_write(r.gpu_dst, c.dst, r.len)) {
+    // worker requests take the BAR only up to 64 KiB: past that the workers'
+    // CPU stores fall behind SDMA (256 KiB: 14.2 vs 17.8 GiB/s, 512 KiB: 23.7
+    // vs 26.5, profiles/r1j/sweep_barmax_*); synchronous reads keep bar_max
+    constexpr uint32_t kWorkerBarMax = 64u << 10;
+    if (r.len <= std::min(cfg.bar_max, kWorkerBarMax) && r.gmap &&
+        r.gmap->bar_write(r.gpu_dst, c.dst, r.len)) {
       // small request: CPU stores through the large BAR beat an SDMA round trip
       stats().copy_ns.add(mono_ns() - now);
       free_slots.push_back(c.slot);

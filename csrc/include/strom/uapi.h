@@ -114,8 +114,9 @@ struct strom_map_gpu_dmabuf {
 	strom_u32     gpu_npages;  /* out */
 	int           dmabuf_fd;   /* in */
 	int           device_id;   /* in:  HIP ordinal (informational) */
-	strom_u64     vaddress;    /* in:  device VA the dma-buf covers */
+	strom_u64     vaddress;    /* in:  device VA of the mapped range */
 	size_t        length;      /* in */
+	strom_u64     dmabuf_offset; /* in: byte offset of vaddress inside the dma-buf */
 };
 
 /* ---- MEMCPY_SSD2GPU ------------------------------------------------- */

@@ -34,9 +34,15 @@ static const struct dma_buf_attach_ops strom_importer_ops = {
 	.move_notify = strom_move_notify,
 };
 
-static void gpumap_release(struct kref *ref)
+static struct workqueue_struct *gpumap_wq;
+
+/* The last reference can drop in an NVMe completion (IRQ context, through
+ * the task), but unpin/detach take the reservation lock and sleep: the
+ * teardown runs on a workqueue.  Module exit destroys the queue, which
+ * waits for a teardown still running. */
+static void gpumap_free_work(struct work_struct *w)
 {
-	struct strom_gpumap *m = container_of(ref, struct strom_gpumap, ref);
+	struct strom_gpumap *m = container_of(w, struct strom_gpumap, free_work);
 	int i;
 
 	for (i = 0; i < m->natt; i++) {
@@ -51,6 +57,13 @@ static void gpumap_release(struct kref *ref)
 	dma_buf_put(m->dmabuf);
 	kfree(m);
 	module_put(THIS_MODULE);
+}
+
+static void gpumap_release(struct kref *ref)
+{
+	struct strom_gpumap *m = container_of(ref, struct strom_gpumap, ref);
+
+	queue_work(gpumap_wq, &m->free_work);
 }
 
 struct strom_gpumap *strom_gpumap_get(unsigned long handle)
@@ -84,7 +97,10 @@ int strom_map_dmabuf(struct strom_map_gpu_dmabuf *arg)
 	db = dma_buf_get(arg->dmabuf_fd);
 	if (IS_ERR(db))
 		return PTR_ERR(db);
-	if (arg->length > db->size) {
+	/* userspace exports the whole allocation that holds the range (a
+	 * tensor is usually a sub-allocation): the range starts dmabuf_offset
+	 * bytes into it */
+	if (arg->dmabuf_offset > db->size || arg->length > db->size - arg->dmabuf_offset) {
 		dma_buf_put(db);
 		return -ERANGE;
 	}
@@ -95,6 +111,8 @@ int strom_map_dmabuf(struct strom_map_gpu_dmabuf *arg)
 	}
 	m->dmabuf = db;
 	m->vaddress = arg->vaddress;
+	m->dmabuf_off = arg->dmabuf_offset;
+	INIT_WORK(&m->free_work, gpumap_free_work);
 	m->length = arg->length;
 	m->owner = current_euid();
 	mutex_init(&m->att_lock);
@@ -186,6 +204,7 @@ int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
 
 	if (!a)
 		return -EOPNOTSUPP;
+	off += m->dmabuf_off;
 	for_each_sgtable_dma_sg(a->sgt, sg, i) {
 		size_t len = sg_dma_len(sg);
 
@@ -202,28 +221,35 @@ int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
 int strom_list_gpu(struct strom_list_gpu_memory __user *uarg)
 {
 	struct strom_gpumap *m;
-	u32 nrooms, n = 0;
-	int bkt;
+	unsigned long *h = NULL;
+	u32 nrooms, cap, n = 0;
+	int bkt, rc = 0;
 
 	if (get_user(nrooms, &uarg->nrooms))
 		return -EFAULT;
+	/* copying out may fault and sleep, and a record may be unmapped and
+	 * freed once the lock is dropped: snapshot the handles first */
+	cap = min_t(u32, nrooms, 4096);
+	if (cap) {
+		h = kmalloc_array(cap, sizeof(*h), GFP_KERNEL);
+		if (!h)
+			return -ENOMEM;
+	}
 	spin_lock(&gpumap_lock);
 	hash_for_each(gpumap_slots, bkt, m, node) {
 		if (!uid_eq(m->owner, current_euid()))
 			continue;
-		if (n < nrooms) {
-			/* put_user may fault: collect under the lock into a copy */
-			unsigned long h = m->handle;
-
-			spin_unlock(&gpumap_lock);
-			if (put_user(h, &uarg->handles[n]))
-				return -EFAULT;
-			spin_lock(&gpumap_lock);
-		}
+		if (n < cap)
+			h[n] = m->handle;
 		n++;
 	}
 	spin_unlock(&gpumap_lock);
-	return put_user(n, &uarg->nitems);
+	if (cap && copy_to_user(uarg->handles, h, min(n, cap) * sizeof(*h)))
+		rc = -EFAULT;
+	kfree(h);
+	if (!rc && put_user(n, &uarg->nitems))
+		rc = -EFAULT;
+	return rc;
 }
 
 int strom_info_gpu(struct strom_info_gpu_memory __user *uarg)
@@ -242,7 +268,7 @@ int strom_info_gpu(struct strom_info_gpu_memory __user *uarg)
 	k.version = 1;
 	k.gpu_page_sz = STROM_GPU_BOUND_SIZE;
 	k.owner = from_kuid(current_user_ns(), m->owner);
-	k.map_offset = 0;
+	k.map_offset = m->vaddress & (STROM_GPU_BOUND_SIZE - 1);
 	k.map_length = m->length;
 	for (i = 0; i < npages && i < k.nrooms; i++) {
 		/* bus address as seen by the first attached controller, if any */
@@ -264,12 +290,16 @@ int strom_info_gpu(struct strom_info_gpu_memory __user *uarg)
 	return copy_to_user(uarg, &k, offsetof(struct strom_info_gpu_memory, paddrs)) ? -EFAULT : 0;
 }
 
-void strom_gpumap_init(void)
+int strom_gpumap_init(void)
 {
 	hash_init(gpumap_slots);
+	gpumap_wq = alloc_workqueue("strom_gpumap", WQ_UNBOUND, 0);
+	return gpumap_wq ? 0 : -ENOMEM;
 }
 
 void strom_gpumap_exit(void)
 {
-	/* module refs held by live mappings prevent unload; nothing to do */
+	/* live mappings hold module references, so only teardowns queued by
+	 * the last puts can remain: destroying the queue drains them */
+	destroy_workqueue(gpumap_wq);
 }

@@ -34,6 +34,38 @@
 #define NVME_PRP_ENTRIES (NVME_CTRL_PAGE_SIZE / sizeof(__le64))
 
 /* ------------------------------------------------------------ file check */
+/*
+ * With native NVMe multipath (the default on current distributions) the
+ * visible nvmeXnY is a bio-based head disk whose private_data is a struct
+ * nvme_ns_head, not a namespace; its paths are blk-mq disks.  A blk-mq disk
+ * has no ->submit_bio, which tells the two apart.  For a head the first path
+ * on its list is used (nvme_find_path() is not exported).  The path is not
+ * pinned: one removed while requests are being built fails them, as hot
+ * removal fails any I/O in flight.
+ */
+static struct nvme_ns *disk_nvme_ns(struct gendisk *disk, int *err)
+{
+	if (!disk->fops->submit_bio)
+		return disk->private_data;
+#ifdef CONFIG_NVME_MULTIPATH
+	{
+		struct nvme_ns_head *head = disk->private_data;
+		struct nvme_ns *ns;
+		int idx = srcu_read_lock(&head->srcu);
+
+		ns = list_first_or_null_rcu(&head->list, struct nvme_ns, siblings);
+		srcu_read_unlock(&head->srcu, idx);
+		if (ns)
+			return ns;
+		*err = -ENODEV;
+		return NULL;
+	}
+#else
+	*err = -EOPNOTSUPP;
+	return NULL;
+#endif
+}
+
 static struct nvme_ns *file_nvme_ns(struct file *filp, int *err)
 {
 	struct inode *inode = file_inode(filp);
@@ -51,7 +83,7 @@ static struct nvme_ns *file_nvme_ns(struct file *filp, int *err)
 	if (!bdev || strncmp(bdev->bd_disk->disk_name, "nvme", 4))
 		return NULL;   /* md raid0 / others: userspace engine */
 	*err = 0;
-	return bdev->bd_disk->private_data;
+	return disk_nvme_ns(bdev->bd_disk, err);
 }
 
 int strom_check_file(struct strom_check_file *arg)
@@ -539,6 +571,9 @@ int strom_memcpy_ssd2ram(struct strom_session *s, struct strom_memcpy_ssd2ram __
 		rc = -ENOMEM;
 		goto out;
 	}
+	/* the buffer's pages must outlive the DMA even if userspace unmaps
+	 * and closes it meanwhile (the reference refcounted its buffers) */
+	x.t->dbuf_filp = get_file(vma->vm_file);
 	x.inode = file_inode(filp);
 	x.vma = vma;
 	x.uaddr_base = (unsigned long)k.dest_uaddr;

@@ -12,7 +12,8 @@
  * kallsyms lookups (unexported since 5.7): file extents come from bmap(),
  * NVMe commands are passthrough requests on the namespace queue.
  *
- * Status: written against Linux 6.6 APIs; compile-untested in this repo's
+ * Status: written against Linux 6.8+ APIs (ns_id / lba_shift live in
+ * struct nvme_ns_head since 6.8); compile-untested in this repo's
  * environment (no kernel headers, no root on the GPU pool).  Build with
  * KSRC pointing at a configured kernel tree (drivers/nvme/host/nvme.h is
  * needed for struct nvme_ns and nvme_init_request()).
@@ -30,6 +31,7 @@
 #include <linux/spinlock.h>
 #include <linux/types.h>
 #include <linux/wait.h>
+#include <linux/workqueue.h>
 
 #include "../csrc/include/strom/uapi.h"
 
@@ -64,6 +66,10 @@ extern int strom_stat_level;
 struct strom_session {
 	struct list_head failed;         /* strom_task records nobody waited */
 	spinlock_t lock;
+	struct file *filp;               /* the /dev or /proc file: every task
+	                                    pins it, so release() (and kfree of
+	                                    the session) follows the last
+	                                    completion */
 };
 
 /* ---- HBM mapping: imported dma-buf ------------------------------------ */
@@ -78,7 +84,8 @@ struct strom_gpumap {
 	unsigned long handle;
 	kuid_t owner;
 	struct dma_buf *dmabuf;
-	u64 vaddress;                    /* user VA the buffer covers */
+	u64 vaddress;                    /* user VA of the mapped range */
+	u64 dmabuf_off;                  /* byte offset of vaddress in the dma-buf */
 	size_t length;
 	struct strom_attach att[4];      /* lazily per target controller */
 	int natt;
@@ -86,6 +93,7 @@ struct strom_gpumap {
 	atomic_t inflight;               /* requests targeting the range */
 	wait_queue_head_t drain;
 	struct kref ref;
+	struct work_struct free_work;    /* teardown sleeps: never in IRQ */
 };
 
 int strom_map_dmabuf(struct strom_map_gpu_dmabuf *arg);
@@ -98,7 +106,7 @@ void strom_gpumap_put(struct strom_gpumap *m);
  * contiguous bytes follow it */
 int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
 		     dma_addr_t *addr, size_t *contig);
-void strom_gpumap_init(void);
+int strom_gpumap_init(void);
 void strom_gpumap_exit(void);
 
 /* ---- DMA task table ---------------------------------------------------- */
@@ -112,6 +120,7 @@ struct strom_task {
 	bool frozen;
 	struct strom_gpumap *gmap;       /* SSD2GPU target (ref held) */
 	struct file *filp;               /* source (ref held) */
+	struct file *dbuf_filp;          /* SSD2RAM destination buffer (ref held) */
 	u64 t_start;
 };
 

@@ -36,6 +36,7 @@ static int strom_open(struct inode *inode, struct file *filp)
 		return -ENOMEM;
 	INIT_LIST_HEAD(&s->failed);
 	spin_lock_init(&s->lock);
+	s->filp = filp;
 	filp->private_data = s;
 	return 0;
 }
@@ -162,7 +163,9 @@ static int __init nvme_strom_init(void)
 	int rc;
 
 	strom_task_init();
-	strom_gpumap_init();
+	rc = strom_gpumap_init();
+	if (rc)
+		return rc;
 	rc = misc_register(&strom_misc);
 	if (rc)
 		goto out_map;

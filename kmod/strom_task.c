@@ -52,6 +52,7 @@ struct strom_task *strom_task_create(struct strom_session *s, struct file *filp,
 		return NULL;
 	t->id = atomic64_inc_return(&next_id);
 	t->sess = s;
+	get_file(s->filp);      /* the session outlives its tasks */
 	atomic_set(&t->refcnt, 1);
 	t->gmap = gmap;
 	t->filp = filp;
@@ -75,6 +76,7 @@ void strom_task_get(struct strom_task *t)
 void strom_task_put(struct strom_task *t, long status)
 {
 	unsigned int k = slot_of(t->id);
+	struct file *sfilp;
 	unsigned long flags;
 
 	if (status)
@@ -90,14 +92,21 @@ void strom_task_put(struct strom_task *t, long status)
 	}
 	spin_unlock_irqrestore(&slots[k].lock, flags);
 	wake_up_all(&slots[k].wq);
+	sfilp = t->sess->filp;
 	if (t->gmap)
-		strom_gpumap_put(t->gmap);
+		strom_gpumap_put(t->gmap);   /* teardown runs on a workqueue */
 	if (t->filp)
 		fput(t->filp);
+	if (t->dbuf_filp)
+		fput(t->dbuf_filp);
 	t->gmap = NULL;
 	t->filp = NULL;
+	t->dbuf_filp = NULL;
 	if (!t->status)
 		kfree(t);
+	/* last: a failed record stays on the session's list until WAIT or
+	 * release(), which this reference holds off */
+	fput(sfilp);
 }
 
 static bool task_running(unsigned long id)

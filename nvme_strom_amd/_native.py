@@ -53,7 +53,7 @@ class MapGpuMemory(C.Structure):
 class MapGpuDmabuf(C.Structure):
     _fields_ = [("handle", C.c_ulong), ("gpu_page_sz", C.c_uint32), ("gpu_npages", C.c_uint32),
                 ("dmabuf_fd", C.c_int), ("device_id", C.c_int), ("vaddress", C.c_uint64),
-                ("length", C.c_size_t)]
+                ("length", C.c_size_t), ("dmabuf_offset", C.c_uint64)]
 
 
 class UnmapGpuMemory(C.Structure):
