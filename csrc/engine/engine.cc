@@ -496,6 +496,33 @@ static int kernel_fd() {
   return g_kernel_fd = fd;
 }
 
+// Kernel provider: MAP_GPU_MEMORY carries only a VA, which the kernel
+// cannot resolve to an amdgpu buffer object (the reference asked
+// nvidia_p2p_get_pages, kmod/pmemmap.c:250).  Export the allocation that
+// holds the range as a dma-buf and register it with MAP_GPU_DMABUF; the
+// kernel keeps its own reference to the dma-buf.
+static int kernel_map_gpu(int kfd, strom_map_gpu_memory *a) {
+  if (!hip::available()) return -ENODEV;
+  int dfd = -1, dev = -1;
+  uint64_t off = 0;
+  int rc = hip::export_dmabuf(a->vaddress, a->length, &dfd, &off, &dev);
+  if (rc) return rc;
+  strom_map_gpu_dmabuf m{};
+  m.dmabuf_fd = dfd;
+  m.device_id = dev;
+  m.vaddress = a->vaddress;
+  m.length = a->length;
+  m.dmabuf_offset = off;
+  int r = ioctl(kfd, STROM_IOCTL__MAP_GPU_DMABUF, &m);
+  int e = errno;
+  close(dfd);
+  if (r < 0) return -e;
+  a->handle = m.handle;
+  a->gpu_page_sz = m.gpu_page_sz;
+  a->gpu_npages = m.gpu_npages;
+  return 0;
+}
+
 extern "C" {
 
 const char *strom_version(void) { return "strom-mi355x 0.1.0 (abi nvme-strom 0.6)"; }
@@ -524,6 +551,7 @@ int strom_ioctl(int session, unsigned long cmd, void *arg) {
     kfd = kernel_fd();
   }
   if (kfd >= 0) {
+    if (cmd == STROM_IOCTL__MAP_GPU_MEMORY) return kernel_map_gpu(kfd, (strom_map_gpu_memory *)arg);
     int r = ioctl(kfd, cmd, arg);
     return r < 0 ? -errno : r;
   }
@@ -638,6 +666,12 @@ int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd
     if (r < 0) return (int)r;
   }
   return 0;
+}
+
+int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset) {
+  if (!hip::available()) return -ENODEV;
+  int dev = -1;
+  return hip::export_dmabuf(va, len, fd, offset, &dev);
 }
 
 int strom_config_set(const char *key, const char *value) {

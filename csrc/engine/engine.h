@@ -360,6 +360,9 @@ void host_free_thp(void *p, size_t bytes);
 uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len);
 volatile uint32_t *hdp_flush_reg(int device);  // null when not exposed
 void bar_unmap(uint8_t *p, size_t len);
+// dma-buf fd of the whole allocation holding [va, va+len) (PCIe mapping
+// type, for peer-to-peer importers) and va's byte offset inside it
+int export_dmabuf(uint64_t va, size_t len, int *fd, uint64_t *offset, int *device);
 int copy_dtoh(void *dst, uint64_t src, size_t len);   // synchronous, 0 / -EIO
 int copy_htod(uint64_t dst, const void *src, size_t len);
 int numa_node_of_device(int device);

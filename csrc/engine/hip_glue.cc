@@ -216,6 +216,29 @@ void bar_unmap(uint8_t *p, size_t len) {
   if (p) munmap(p, len);
 }
 
+int export_dmabuf(uint64_t va, size_t len, int *fd, uint64_t *offset, int *device) {
+  uint64_t base = 0;
+  size_t size = 0;
+  *device = pointer_device(va, &base, &size);
+  if (*device < 0 || size == 0) return -EINVAL;
+  if (va + len > base + size) return -ERANGE;
+  *fd = -1;
+  if (hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd,
+                                     hipMemRangeFlagDmaBufMappingTypePcie) != hipSuccess ||
+      *fd < 0) {
+    (void)hipGetLastError();
+    *fd = -1;
+    if (hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size,
+                                       hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess ||
+        *fd < 0) {
+      (void)hipGetLastError();
+      return -EOPNOTSUPP;
+    }
+  }
+  *offset = va - base;
+  return 0;
+}
+
 int copy_dtoh(void *dst, uint64_t src, size_t len) {
   return hipMemcpy(dst, (const void *)src, len, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -EIO;
 }

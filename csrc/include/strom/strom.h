@@ -43,6 +43,11 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
 int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd,
                         const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out);
 
+/* dma-buf fd of the HIP allocation holding [va, va+len) and va's byte
+ * offset inside it: what MAP_GPU_MEMORY registers with the kernel provider
+ * (MAP_GPU_DMABUF).  The caller closes the fd. */
+int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset);
+
 /* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
 int strom_config_set(const char *key, const char *value);
 int strom_config_get(const char *key, char *buf, size_t buflen);

@@ -177,3 +177,29 @@ def test_latency_4k(S, tmp_path):
             got = hb.tensor[:4096].cpu().numpy()
             assert np.array_equal(got, data[cid * 4096:(cid + 1) * 4096])
         assert np.median(lat) < 0.01
+
+
+def test_export_dmabuf_offsets(S):
+    """MAP_GPU_MEMORY under the kernel provider registers the dma-buf of the
+    whole allocation plus the range's offset in it (tensors are usually
+    sub-allocations of a caching-allocator block)."""
+    import ctypes as C
+    from nvme_strom_amd import _native as N
+    t = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+    lib = N.lib()
+    fds, offs = [], []
+    try:
+        for delta in (0, (1 << 20) + 4096):
+            fd, off = C.c_int(-1), C.c_uint64(0)
+            assert lib.strom_export_dmabuf(t.data_ptr() + delta, 4096, C.byref(fd), C.byref(off)) == 0
+            assert fd.value >= 0
+            fds.append(fd.value)
+            offs.append(off.value)
+        assert offs[1] - offs[0] == (1 << 20) + 4096
+        # a dma-buf reports its size through lseek(SEEK_END)
+        assert os.lseek(fds[0], 0, os.SEEK_END) >= offs[0] + (8 << 20)
+        h = np.zeros(4096, dtype=np.uint8)
+        assert lib.strom_export_dmabuf(h.ctypes.data, 4096, C.byref(C.c_int()), C.byref(C.c_uint64())) < 0
+    finally:
+        for fd in fds:
+            os.close(fd)
