@@ -195,6 +195,15 @@ def main() -> int:
         lat_py = np.array(py)
     p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
     p50_py = float(np.percentile(lat_py, 50))
+    # where the 4 KiB latency goes (native phase stamps, this rank's medians)
+    # and its floor: a bare O_DIRECT pread of the same offsets into host RAM
+    phases, raw_p50 = {}, float("nan")
+    if a.lat_samples:
+        S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
+        phases = S.phase_breakdown(S.pread_gpu_phases(buf.handle, 0, fd, offs)[50:])
+        S.evict_file(fd)
+        raw_p50 = float(np.percentile(S.pread_raw_latency(fd, offs)[50:], 50)) / 1e3
 
     # VFS control: pread -> pinned -> HtoD, same window
     S.evict_file(fd)
@@ -224,6 +233,8 @@ def main() -> int:
         "p99_4k_lat_us": round(p99, 2),
         "p50_4k_lat_python_us": round(p50_py, 2),
         "engine_io_p50_us": round(S.hist_percentile(hist["io_ns"], 50) / 1e3, 2),
+        "raw_odirect_4k_p50_us": round(raw_p50, 2),
+        "p50_4k_phases_us": phases,
         "verified_crc32c": bool(ver == 1.0),
         "avg_request_kib": round(0.5 * agg["nr_blocks"] / agg["nr_submit"], 1) if agg["nr_submit"] else 0,
         "ram_chunks": agg["nr_ram"],

@@ -12,6 +12,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <sys/ioctl.h>
 #include <sys/mman.h>
@@ -29,6 +30,7 @@ namespace strom {
 // set while strom_pread_gpu runs: a synchronous caller gains nothing from a
 // worker hand-off, so its single request runs inline at any size
 static thread_local bool tl_sync_call = false;
+thread_local uint64_t *tl_phase = nullptr;
 
 
 struct Engine::OpenFile {
@@ -279,12 +281,14 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   pp.file_size = (uint64_t)f->fc.size;
   pp.max_request = config().max_request;
   pp.reorder = true;
+  phase_mark(0);
   std::vector<unsigned char> resv;
   uint64_t res_lo = 0;
   if (config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
   ChunkPlan plan;
   int rc = plan_chunks(pp, &plan);
   if (rc) return rc;
+  phase_mark(1);
   // MI355X extension: wb_buffer == NULL asks the engine to put page-cache
   // chunks straight into HBM (buffered reads into the large-BAR mapping);
   // they still land at the tail and are reported as nr_ram2gpu.
@@ -302,6 +306,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   std::vector<IoReq> reqs;
   build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, gmap.get(),
                  gmap->va + a->offset, host_dest, &reqs);
+  phase_mark(2);
   uint64_t t0 = tsc_now();
   if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
     io_->run_inline(reqs[0]);
@@ -666,6 +671,48 @@ int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd
     if (r < 0) return (int)r;
   }
   return 0;
+}
+
+int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int fd,
+                           const uint64_t *file_offs, uint32_t n, uint64_t len,
+                           uint64_t *phase_ns) {
+  uint64_t st[STROM_NPHASE];
+  for (uint32_t i = 0; i < n; ++i) {
+    memset(st, 0, sizeof st);
+    strom::tl_phase = st;
+    const uint64_t t0 = mono_ns();
+    const long r = strom_pread_gpu(session, handle, offset, fd, file_offs[i], len);
+    st[STROM_NPHASE - 1] = mono_ns();
+    strom::tl_phase = nullptr;
+    if (r < 0) return (int)r;
+    for (int k = 0; k < STROM_NPHASE; ++k)
+      phase_ns[(size_t)i * STROM_NPHASE + k] = st[k] ? st[k] - t0 : 0;
+  }
+  return 0;
+}
+
+int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t len,
+                        uint64_t *ns_out) {
+  if (len == 0 || (len & 4095)) return -EINVAL;
+  char path[64];
+  snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+  int d = open(path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+  if (d < 0) return -errno;
+  void *buf = nullptr;
+  if (posix_memalign(&buf, 4096, len) != 0) {
+    close(d);
+    return -ENOMEM;
+  }
+  int rc = 0;
+  for (uint32_t i = 0; i < n && rc == 0; ++i) {
+    const uint64_t t0 = mono_ns();
+    const ssize_t got = pread(d, buf, len, (off_t)file_offs[i]);
+    ns_out[i] = mono_ns() - t0;
+    if (got < 0) rc = -errno;
+  }
+  free(buf);
+  close(d);
+  return rc;
 }
 
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset) {

@@ -394,6 +394,14 @@ class Engine {
 Engine &engine();
 void engine_reset();
 
+// Phase probe of the synchronous small-read path (strom_pread_gpu_phases):
+// while a caller thread has tl_phase set, the path stamps mono_ns() at the
+// end of each phase (STROM_NPHASE points, strom.h).
+extern thread_local uint64_t *tl_phase;
+inline void phase_mark(int k) {
+  if (__builtin_expect(tl_phase != nullptr, 0)) tl_phase[k] = mono_ns();
+}
+
 #define STROM_LOG(lvl, ...)                                   \
   do {                                                        \
     if (::strom::config().verbose >= (lvl)) {                 \

@@ -528,7 +528,9 @@ void IoEngine::run_inline(IoReq &r) {
   if (r.host_dst) {
     long got = frc ? frc : pread_full(r.fd, r.host_dst, len, r.off);
     stats().io_ns.add(mono_ns() - t0);
+    phase_mark(3);
     finish_request(r, finalize_read(r, r.host_dst, len, got));
+    phase_mark(6);
     return;
   }
   if (c.cap < r.len) {
@@ -544,6 +546,7 @@ void IoEngine::run_inline(IoReq &r) {
   }
   long got = frc ? frc : pread_full(r.fd, c.buf, len, r.off);
   uint64_t t1 = mono_ns();
+  if (tl_phase) tl_phase[3] = t1;
   stats().io_ns.add(t1 - t0);
   long status = finalize_read(r, c.buf, len, got);
   if (status == 0 && r.len <= config().bar_max && r.gmap &&
@@ -559,11 +562,13 @@ void IoEngine::run_inline(IoReq &r) {
     }
     hipError_t e = hipMemcpyAsync((void *)r.gpu_dst, c.buf, r.len, hipMemcpyHostToDevice, c.st);
     if (e == hipSuccess) e = hipStreamSynchronize(c.st);
+    phase_mark(4);
     if (e != hipSuccess) status = -EIO;
     stats().copy_ns.add(mono_ns() - t1);
     stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
   }
   finish_request(r, status);
+  phase_mark(6);
 }
 
 void IoEngine::submit(std::vector<IoReq> &reqs) {

@@ -47,7 +47,9 @@ bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len) const {
   if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
   uint8_t *p = bar + (dst - bar_va);
   memcpy(p, src, len);
+  phase_mark(4);
   bar_flush(p + ((len - 1) & ~(size_t)3));
+  phase_mark(5);
   return true;
 }
 

@@ -42,6 +42,19 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
  * Returns 0 or the first failure's -errno. */
 int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd,
                         const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out);
+/* The same probe split into phases: phase_ns[i*STROM_NPHASE + k] is the time
+ * from the start of read i to the end of phase k, 0 when k was not reached:
+ *   0 file lookup   1 chunk plan (residency probe + merge)   2 task + requests
+ *   3 storage read   4 stores into HBM (BAR) or the SDMA copy   5 HDP flush
+ *   6 request completion   7 WAIT returned (the total). */
+#define STROM_NPHASE 8
+int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int fd,
+                           const uint64_t *file_offs, uint32_t n, uint64_t len,
+                           uint64_t *phase_ns);
+/* The floor under those reads: O_DIRECT pread of len bytes at each offset
+ * into aligned host memory (no engine, no HBM), ns per read. */
+int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t len,
+                        uint64_t *ns_out);
 
 /* dma-buf fd of the HIP allocation holding [va, va+len) and va's byte
  * offset inside it: what MAP_GPU_MEMORY registers with the kernel provider

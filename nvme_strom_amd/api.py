@@ -308,6 +308,45 @@ def pread_gpu_latency(handle: int, offset: int, fd: int, file_offs, length: int 
     return out
 
 
+PHASES = ("lookup", "plan", "setup", "storage", "hbm_store", "hdp_flush", "complete", "wait")
+
+
+def pread_gpu_phases(handle: int, offset: int, fd: int, file_offs, length: int = 4096,
+                     sess: Optional[Session] = None) -> np.ndarray:
+    """Phase-stamped QD1 probe: (n, len(PHASES)) ns from each read's start to
+    the end of each phase (0 where a phase was not reached; last = total)."""
+    s = sess or session()
+    offs = np.ascontiguousarray(file_offs, dtype=np.uint64)
+    out = np.zeros((len(offs), len(PHASES)), dtype=np.uint64)
+    _check(s.lib.strom_pread_gpu_phases(s.sid, handle, offset, fd, offs.ctypes.data, len(offs),
+                                        length, out.ctypes.data), "pread_gpu_phases")
+    return out
+
+
+def phase_breakdown(stamps: np.ndarray) -> dict:
+    """Median duration (us) of each phase of pread_gpu_phases() stamps: a phase
+    lasts from the previous reached stamp to its own; None if never reached."""
+    st = stamps.astype(np.float64)
+    prev = np.zeros(len(st))
+    out = {}
+    for k, name in enumerate(PHASES):
+        col = st[:, k]
+        hit = col > 0
+        out[name] = round(float(np.median((col - prev)[hit])) / 1e3, 2) if hit.any() else None
+        prev = np.where(hit, col, prev)
+    return out
+
+
+def pread_raw_latency(fd: int, file_offs, length: int = 4096) -> np.ndarray:
+    """The floor under pread_gpu: O_DIRECT pread into aligned host memory,
+    ns per read (no engine, no HBM)."""
+    offs = np.ascontiguousarray(file_offs, dtype=np.uint64)
+    out = np.zeros(len(offs), dtype=np.uint64)
+    _check(N.lib().strom_pread_raw_lat(fd, offs.ctypes.data, len(offs), length, out.ctypes.data),
+           "pread_raw_lat")
+    return out
+
+
 def memcpy_wait(task_id: int, timeout: Optional[float] = None,
                 sess: Optional[Session] = None) -> None:
     """Block until the task finishes; raises StromError(EIO, status=...) on a

@@ -361,3 +361,28 @@ def test_concurrent_tasks_from_threads(strom, rand_file):
             assert np.array_equal(buf.array[:128 * CH], data)
     finally:
         os.close(fd)
+
+
+def test_pread_gpu_phase_probe(strom, rand_file):
+    """Phase stamps of the synchronous path rise monotonically to the total,
+    the data lands, and the raw O_DIRECT floor is measured alongside."""
+    path, data = rand_file(64 * 4096)
+    fd = _open(path)
+    try:
+        keep, hbm = _host_target(16 * 4096)
+        with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+            offs = np.array([3, 9, 27, 50, 1], dtype=np.uint64) * 4096
+            st = strom.pread_gpu_phases(m.handle, 0, fd, offs)
+            assert st.shape == (5, len(strom.PHASES))
+            for row in st:
+                hit = row[row > 0].astype(np.int64)
+                assert len(hit) >= 4 and (np.diff(hit) >= 0).all()
+                assert row[-1] == hit.max()
+            assert (st[:, strom.PHASES.index("storage")] > 0).all()
+            assert np.array_equal(hbm[:4096], data[4096:8192])
+            bd = strom.phase_breakdown(st)
+            assert list(bd) == list(strom.PHASES) and bd["wait"] is not None
+            raw = strom.pread_raw_latency(fd, offs)
+            assert raw.shape == (5,) and (raw > 0).all()
+    finally:
+        os.close(fd)
