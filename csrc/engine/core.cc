@@ -34,7 +34,7 @@ Config Config::from_env() {
   Config c;
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
-                               "bar_map", "bar_max", "trace",
+                               "bar_map", "bar_max", "coalesce", "trace",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind",
                                "stat_info", "verbose"};
@@ -83,6 +83,7 @@ int Config::set(const std::string &k, const std::string &v) {
   }
   if (k == "spin_us") { if (n < 0 || n > 10000) return -EINVAL; spin_us = (uint32_t)n; return 0; }
   if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
+  if (k == "coalesce") { coalesce = parse_bool(v); return 0; }
   if (k == "trace") { trace = parse_bool(v); return 0; }
   if (k == "bar_max") {
     if (n < 0 || n > (64l << 20)) return -EINVAL;
@@ -114,6 +115,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "spin_us") v = spin_us;
   else if (k == "inline_max") v = inline_max;
   else if (k == "bar_map") v = bar_map;
+  else if (k == "coalesce") v = coalesce;
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;

@@ -56,6 +56,7 @@ struct Config {
                                  // sleeping on a futex (hand-off latency)
   uint32_t inline_max = 64u << 10;  // single requests up to this run inline
   bool bar_map = true;           // CPU-map HBM through the large BAR (dma-buf)
+  bool coalesce = true;          // workers merge adjacent staged HBM copies
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks

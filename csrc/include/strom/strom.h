@@ -56,6 +56,13 @@ int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int
 int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t len,
                         uint64_t *ns_out);
 
+/* Storage ceiling for a block size, no engine: `threads` io_uring rings,
+ * each `qd` deep, O_DIRECT reads of `block` bytes at random aligned
+ * offsets (or in file order from a shared cursor when `sequential`) into
+ * host memory until `nreq` reads are done. */
+int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads, uint32_t qd,
+                        int sequential, double *iops, double *gibps);
+
 /* dma-buf fd of the HIP allocation holding [va, va+len) and va's byte
  * offset inside it: what MAP_GPU_MEMORY registers with the kernel provider
  * (MAP_GPU_DMABUF).  The caller closes the fd. */

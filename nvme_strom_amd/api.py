@@ -347,6 +347,18 @@ def pread_raw_latency(fd: int, file_offs, length: int = 4096) -> np.ndarray:
     return out
 
 
+def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
+                  sequential: bool = False) -> tuple:
+    """Storage ceiling for one block size with no engine in the way:
+    ``threads`` io_uring rings ``qd`` deep, O_DIRECT reads into host memory
+    at random aligned offsets (or in file order through a shared cursor).
+    Returns (IOPS, GiB/s)."""
+    iops, gibps = C.c_double(), C.c_double()
+    _check(N.lib().strom_raw_read_rate(fd, block, nreq, threads, qd, int(sequential),
+                                       C.byref(iops), C.byref(gibps)), "raw_read_rate")
+    return iops.value, gibps.value
+
+
 def memcpy_wait(task_id: int, timeout: Optional[float] = None,
                 sess: Optional[Session] = None) -> None:
     """Block until the task finishes; raises StromError(EIO, status=...) on a

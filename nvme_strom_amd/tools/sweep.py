@@ -8,6 +8,10 @@ and the file is streamed into HBM with the nvme_test shape (32 MiB segments,
   GiBps        whole-window throughput (page cache evicted first)
   iops         completed storage requests per second during that stream
   p50/p99_us   QD1 latency of single B-byte reads into HBM (native loop)
+  raw_*        the storage ceiling for B: the same number of io_uring rings,
+               as deep, reading B-byte O_DIRECT blocks into host RAM in file
+               order (no engine, no HBM) — the engine's target at that size
+               (raw_random_GiBps: the same at random aligned offsets)
 
 ``python -m nvme_strom_amd.tools.sweep --out gpurun_out/sweep.json``
 """
@@ -47,6 +51,8 @@ def main(argv=None) -> int:
     ap.add_argument("--lat-samples", type=int, default=300)
     ap.add_argument("--qd", type=int, default=0, help="engine queue depth override (0 = default)")
     ap.add_argument("--device", default="cuda", help="cpu = emulated HBM (tests)")
+    ap.add_argument("--no-raw", dest="raw", action="store_false",
+                    help="skip the raw io_uring ceiling per block size")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -98,6 +104,16 @@ def main(argv=None) -> int:
                        avg_req_kib=round(0.5 * st.nr_blocks / st.nr_submit, 1) if st.nr_submit else 0,
                        ram_chunks=st.nr_ram, p50_us=round(float(np.percentile(ns, 50)), 2),
                        p99_us=round(float(np.percentile(ns, 99)), 2))
+            if a.raw:
+                nraw = max(2000, min(nbytes // B, 200000))
+                kw = dict(threads=int(S.config_get("workers")), qd=int(S.config_get("queue_depth")))
+                S.evict_file(fd)
+                riops, rgib = S.raw_read_rate(fd, B, nraw, sequential=True, **kw)
+                S.evict_file(fd)
+                _, rgib_rand = S.raw_read_rate(fd, B, nraw, **kw)
+                row.update(raw_iops=round(riops), raw_GiBps=round(rgib, 2),
+                           raw_random_GiBps=round(rgib_rand, 2),
+                           of_raw=round(gibs / rgib, 3) if rgib else None)
             rows.append(row)
             _log(json.dumps(row))
             ld.close()

@@ -386,3 +386,14 @@ def test_pread_gpu_phase_probe(strom, rand_file):
             assert raw.shape == (5,) and (raw > 0).all()
     finally:
         os.close(fd)
+
+
+def test_coalesce_knob(strom):
+    """Worker copy coalescing is a config key (default on), parsed as a bool."""
+    assert strom.config_get("coalesce") == "1"
+    strom.configure(coalesce=0)
+    try:
+        assert strom.config_get("coalesce") == "0"
+    finally:
+        strom.configure(coalesce=1)
+    assert strom.config_get("coalesce") == "1"

@@ -96,6 +96,20 @@ def test_load_file_end_to_end(S, tmp_path, backend):
     S.configure(backend="uring")
 
 
+@pytest.mark.parametrize("coalesce", [0, 1])
+def test_worker_copy_coalescing(S, tmp_path, coalesce):
+    """128 KiB requests through the SDMA path (past the 64 KiB BAR cut) land
+    byte-exact whether adjacent staged copies are merged or not."""
+    from nvme_strom_amd.tensor import load_file
+    S.configure(max_request=128 << 10, coalesce=coalesce)
+    try:
+        p, data = _mkfile(tmp_path, (24 << 20) + 8192, seed=9)
+        t = load_file(p, device="cuda", chunk_sz=1 << 16, window=8 << 20)
+        assert torch.equal(t.cpu(), torch.from_numpy(data))
+    finally:
+        S.configure(max_request=1 << 20, coalesce=1)
+
+
 def test_read_chunks_hybrid_reorder(S, tmp_path):
     """Page-cache chunks land at the tail via the write-back buffer; the
     reader scatters everything back into the requested order on the GPU."""

@@ -68,4 +68,23 @@ def test_block_sweep_cpu(strom, tmp_path):
     for r in rows:
         assert r["GiBps"] > 0 and r["p50_us"] > 0
         assert r["avg_req_kib"] <= r["block"] / 1024
+        assert r["raw_iops"] > 0 and r["raw_GiBps"] > 0
     assert strom.config_get("max_request") == str(1 << 20)   # restored
+
+
+def test_raw_read_rate(strom, tmp_path):
+    """The storage-ceiling probe reads the requested count and rejects bad shapes."""
+    import os
+    path = tmp_path / "raw.bin"
+    path.write_bytes(os.urandom(4 << 20))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        for seq in (False, True):
+            iops, gib = strom.raw_read_rate(fd, 65536, 300, threads=3, qd=4, sequential=seq)
+            assert iops > 0 and abs(gib - iops * 65536 / (1 << 30)) < 1e-6 * max(gib, 1)
+        for bad in [dict(block=1000, nreq=10), dict(block=4096, nreq=0),
+                    dict(block=8 << 20, nreq=10)]:
+            with pytest.raises(strom.StromError):
+                strom.raw_read_rate(fd, bad["block"], bad["nreq"])
+    finally:
+        os.close(fd)
