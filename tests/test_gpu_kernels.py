@@ -150,3 +150,17 @@ def test_column_filter(dev, dtype):
     assert np.array_equal(got, ref)
     idx = bitmap_to_indices(bm, n, cnt)
     assert np.array_equal(idx.cpu().numpy(), np.nonzero(ref)[0].astype(np.int32))
+
+
+@pytest.mark.parametrize("density", [0.0, 0.003, 0.5, 1.0])
+def test_bitmap_to_indices_many_tiles(dev, density):
+    """Single-pass look-back compaction over ~1200 tiles vs numpy.nonzero."""
+    from nvme_strom_amd.ops.colfilter import bitmap_to_indices
+    n = 20_000_037
+    bits = np.random.default_rng(7).random(n) < density
+    packed = np.packbits(bits, bitorder="little")
+    packed = np.concatenate([packed, np.full((-len(packed)) % 8 + 8, 0xFF, np.uint8)])  # junk past n
+    bm = torch.from_numpy(packed.view(np.uint64).copy()).to(dev)
+    ref = np.nonzero(bits)[0]
+    idx = bitmap_to_indices(bm, n, int(bits.sum()))
+    assert np.array_equal(idx.cpu().numpy().astype(np.int64), ref)
