@@ -9,6 +9,9 @@ Reference map (pgsql/nvme_strom.c):
   * tablespace capability cache (:192-295)        -> :class:`TablespaceCache`
   * parallel block cursor in DSM (:90-104, :1181-1233) -> :class:`ParallelCursor`
   * chunk ring + load + tuple iteration (:852-1123) -> :class:`HeapRelationScan`
+  * ExecReScanNVMEStrom cursor reset (:1168-1176)  -> :meth:`ParallelCursor.rescan`;
+    the reference persists no scan state, :class:`ResumableScan` adds
+    block-range checkpoints so an interrupted scan resumes where it stopped
 
 The ring lives in HBM: each chunk of blocks is read with MEMCPY_SSD2GPU
 (``relseg_sz`` = RELSEG_SIZE maps block numbers to 1 GiB segment files) and
@@ -21,6 +24,7 @@ buffer + host tuple walk) used as the parity baseline.
 """
 from __future__ import annotations
 
+import json
 import os
 import threading
 import time
@@ -106,9 +110,10 @@ class TablespaceCache:
 class ParallelCursor:
     """Shared block cursor (pg_atomic_fetch_add_u64 on nsp_cblock)."""
 
-    def __init__(self, nblocks: int):
-        self.nblocks = nblocks
-        self._next = 0
+    def __init__(self, nblocks: int, start: int = 0):
+        self.nblocks = nblocks       # end of the claimable range
+        self.start = start
+        self._next = start
         self._lock = threading.Lock()
 
     def claim(self, n: int, boundary: int = 0) -> Tuple[int, int]:
@@ -123,7 +128,7 @@ class ParallelCursor:
 
     def rescan(self) -> None:
         with self._lock:
-            self._next = 0
+            self._next = self.start
 
 
 class Relation:
@@ -223,8 +228,10 @@ class HeapRelationScan:
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.pred = dict(attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi)
 
-    def run(self, workers: int = 1) -> ScanResult:
-        cursor = ParallelCursor(self.rel.nblocks)
+    def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None) -> ScanResult:
+        """Scan all blocks, or the block range ``[b0, b1)`` given as ``blocks``."""
+        b0, b1 = _block_range(blocks, self.rel.nblocks)
+        cursor = ParallelCursor(b1, start=b0)
         results: List[ScanResult] = []
         errors: List[BaseException] = []
         t0 = time.perf_counter()
@@ -302,10 +309,21 @@ class HeapRelationScan:
         st.add_io(res)
 
 
+def _block_range(blocks: Optional[Tuple[int, int]], nblocks: int) -> Tuple[int, int]:
+    if blocks is None:
+        return 0, nblocks
+    b0, b1 = int(blocks[0]), min(int(blocks[1]), nblocks)
+    if b0 < 0 or b0 > b1:
+        raise ValueError(f"bad block range {blocks} for {nblocks} blocks")
+    return b0, b1
+
+
 def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1,
-             attr_width: int = 8, lo: int = -(1 << 63), hi: int = (1 << 63) - 1) -> ScanResult:
+             attr_width: int = 8, lo: int = -(1 << 63), hi: int = (1 << 63) - 1,
+             blocks: Optional[Tuple[int, int]] = None) -> ScanResult:
     """Reference-shaped path: SSD2RAM into a NUMA DMA buffer, host tuple walk."""
     cfg = cfg or ScanConfig()
+    b0, b1 = _block_range(blocks, rel.nblocks)
     per_chunk = cfg.chunk_size // BLCKSZ
     t0 = time.perf_counter()
     items: List[int] = []
@@ -316,7 +334,9 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
             try:
                 nblk = os.fstat(fd).st_size // BLCKSZ
                 base = seg * rel.relseg_size
-                for c0 in range(0, nblk, per_chunk):
+                first = max(0, b0 - base)
+                nblk = min(nblk, b1 - base)
+                for c0 in range(first, nblk, per_chunk):
                     n = min(per_chunk, nblk - c0)
                     ids = np.arange(base + c0, base + c0 + n, dtype=np.uint32)
                     r = api.memcpy_ssd2ram(buf.address, fd, ids, BLCKSZ, rel.relseg_size)
@@ -333,3 +353,83 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
     st.items = np.array(sorted(items), dtype=np.uint64)
     st.seconds = time.perf_counter() - t0
     return st
+
+
+class ResumableScan:
+    """Checkpointed scan: the relation is scanned in block ranges of
+    ``step_blocks``; after each range the qualifying items and the per-scan
+    counters are written atomically (tmp file + rename) to ``path`` (an .npz
+    holding only arrays; loaded with ``allow_pickle=False``).  A new instance
+    over the same checkpoint continues at the first unscanned block, so each
+    block's tuples are reported exactly once across interruptions.
+
+    ``scan`` is any ``(b0, b1) -> ScanResult`` — e.g.
+    ``lambda b0, b1: HeapRelationScan(...).run(4, blocks=(b0, b1))`` or the
+    ``cpu_scan`` path.  ``key`` identifies the relation + predicate; resuming
+    a checkpoint written under a different key raises ``ValueError``.
+    """
+
+    _COUNTERS = ("pages", "bad_pages", "nr_ram", "nr_ssd", "nr_dma_submit", "nr_dma_blocks",
+                 "chunks")
+
+    def __init__(self, scan, nblocks: int, path: str, step_blocks: int, key: str = ""):
+        if step_blocks <= 0:
+            raise ValueError("step_blocks must be positive")
+        self.scan, self.nblocks, self.path, self.step, self.key = scan, nblocks, path, step_blocks, key
+        self.next_block = 0
+        self.items: List[np.ndarray] = []
+        self.counters = dict.fromkeys(self._COUNTERS, 0)
+        self.seconds = 0.0
+        if os.path.exists(path):
+            self._load()
+
+    def _load(self) -> None:
+        with np.load(self.path, allow_pickle=False) as z:
+            meta = json.loads(bytes(z["meta"]).decode())
+            items = z["items"].astype(np.uint64)
+        if meta["key"] != self.key or meta["nblocks"] != self.nblocks:
+            raise ValueError(f"checkpoint {self.path} is for {meta['key']!r}/{meta['nblocks']} blocks, "
+                             f"not {self.key!r}/{self.nblocks}")
+        self.next_block = int(meta["next_block"])
+        self.counters.update({k: int(meta[k]) for k in self._COUNTERS})
+        self.seconds = float(meta["seconds"])
+        self.items = [items]
+
+    def _save(self) -> None:
+        meta = dict(self.counters, key=self.key, nblocks=self.nblocks, next_block=self.next_block,
+                    seconds=self.seconds)
+        items = np.concatenate(self.items) if self.items else np.zeros(0, np.uint64)
+        tmp = self.path + ".tmp"
+        with open(tmp, "wb") as f:
+            np.savez(f, items=items, meta=np.frombuffer(json.dumps(meta).encode(), np.uint8))
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self.path)
+        self.items = [items]
+
+    @property
+    def done(self) -> bool:
+        return self.next_block >= self.nblocks
+
+    def run(self, max_steps: Optional[int] = None) -> Optional[ScanResult]:
+        """Scan up to ``max_steps`` ranges (all if None); returns the merged
+        result once the whole relation is done, else None."""
+        steps = 0
+        while not self.done and (max_steps is None or steps < max_steps):
+            b0 = self.next_block
+            b1 = min(self.nblocks, b0 + self.step)
+            r = self.scan(b0, b1)
+            self.items.append(np.asarray(r.items, np.uint64))
+            for k in self._COUNTERS:
+                self.counters[k] += int(getattr(r, k))
+            self.seconds += r.seconds
+            self.next_block = b1
+            self._save()
+            steps += 1
+        if not self.done:
+            return None
+        items = np.sort(np.concatenate(self.items)) if self.items else np.zeros(0, np.uint64)
+        out = ScanResult(items, seconds=self.seconds)
+        for k, v in self.counters.items():
+            setattr(out, k, v)
+        return out

@@ -40,6 +40,26 @@ def test_pg_relation_scan_gpu_vs_cpu(S, tmp_path):
         assert g.bad_pages == 0 and g.pages == rel.nblocks
 
 
+def test_pg_relation_scan_resumable_gpu(S, tmp_path):
+    """GPU block-range scans under ResumableScan, interrupted and resumed,
+    equal one full CPU scan."""
+    from nvme_strom_amd.models import pg_scan
+    from nvme_strom_amd.utils import pgpage
+    vals = np.random.default_rng(5).integers(-5000, 5000, 24000).astype(np.int64)
+    data = pgpage.build_table(vals, per_page=150, width=8, invisible_every=7)   # 160 pages
+    rel = pg_scan.Relation.write(str(tmp_path / "24577"), data, relseg_size=64)
+    cfg = pg_scan.ScanConfig(chunk_size=16 * 8192, buffer_size=64 * 8192, verify_checksum=True)
+    pred = dict(attr_off=0, attr_width=8, lo=-1000, hi=3000)
+    full = pg_scan.cpu_scan(rel, cfg, **pred)
+    g = pg_scan.HeapRelationScan(rel, cfg, "cuda", **pred)
+    ck = str(tmp_path / "gpu.ckpt.npz")
+    scan = lambda b0, b1: g.run(2, blocks=(b0, b1))
+    a = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577")
+    assert a.run(max_steps=1) is None and a.next_block == 50
+    r = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577").run()
+    assert np.array_equal(r.items, full.items) and r.pages == rel.nblocks and r.bad_pages == 0
+
+
 def test_arrow_scan_lz4(S, tmp_path):
     pa = pytest.importorskip("pyarrow")
     import pyarrow.ipc as ipc

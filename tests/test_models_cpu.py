@@ -114,3 +114,36 @@ def test_arrow_ipc_metadata(tmp_path):
                 ref = b.columns[1].data
                 vals = raw[ref.offset:ref.offset + 2500 * 8].view(np.int64)
                 assert np.array_equal(vals, a[k * 2500:(k + 1) * 2500])
+
+
+def test_cpu_scan_block_range_and_resumable(strom, tmp_path):
+    """Block-range scans + checkpoint/resume: an interrupted ResumableScan
+    continues at the first unscanned block and equals one full scan."""
+    vals = np.arange(2000, dtype=np.int64)
+    data = pgpage.build_table(vals, per_page=100, width=8, invisible_every=10)   # 20 pages
+    rel = pg_scan.Relation.write(str(tmp_path / "16385"), data, relseg_size=8)
+    cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192, verify_checksum=True)
+    pred = dict(attr_off=0, attr_width=8, lo=50, hi=1749)
+    full = pg_scan.cpu_scan(rel, cfg, **pred)
+    part = pg_scan.cpu_scan(rel, cfg, blocks=(5, 13), **pred)     # crosses a segment boundary
+    blocks = set((part.items >> np.uint64(16)).astype(int).tolist())
+    assert blocks == set(range(5, 13)) and part.pages == 8
+    sel = (full.items >> np.uint64(16) >= 5) & (full.items >> np.uint64(16) < 13)
+    assert np.array_equal(part.items, full.items[sel])
+    with pytest.raises(ValueError):
+        pg_scan.cpu_scan(rel, cfg, blocks=(7, 3), **pred)
+
+    ck = str(tmp_path / "scan.ckpt.npz")
+    scan = lambda b0, b1: pg_scan.cpu_scan(rel, cfg, blocks=(b0, b1), **pred)
+    a = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=3, key="16385:50-1749")
+    assert a.run(max_steps=2) is None and a.next_block == 6       # "interrupted"
+    b = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=3, key="16385:50-1749")
+    assert b.next_block == 6 and b.counters["pages"] == 6
+    r = b.run()
+    assert r is not None and np.array_equal(r.items, full.items)
+    assert r.pages == 20 and r.nr_ram + r.nr_ssd == 20 and r.bad_pages == 0
+    # a finished checkpoint reloads as done; a different key is refused
+    c = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=3, key="16385:50-1749")
+    assert c.done and np.array_equal(c.run().items, full.items)
+    with pytest.raises(ValueError):
+        pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=3, key="other")
