@@ -35,6 +35,7 @@ Config Config::from_env() {
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
                                "bar_map", "bar_max", "coalesce", "trace",
+                               "ingest", "ingest_grid", "ingest_piece", "hdp_sync",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind",
                                "stat_info", "verbose"};
@@ -84,6 +85,14 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "spin_us") { if (n < 0 || n > 10000) return -EINVAL; spin_us = (uint32_t)n; return 0; }
   if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
   if (k == "coalesce") { coalesce = parse_bool(v); return 0; }
+  if (k == "ingest") { ingest = parse_bool(v); return 0; }
+  if (k == "hdp_sync") { hdp_sync = parse_bool(v); return 0; }
+  if (k == "ingest_grid") { if (n < 1 || n > 256) return -EINVAL; ingest_grid = (int)n; return 0; }
+  if (k == "ingest_piece") {
+    if (n < 4096 || n > (16l << 20) || (n & 4095)) return -EINVAL;
+    ingest_piece = (uint32_t)n;
+    return 0;
+  }
   if (k == "trace") { trace = parse_bool(v); return 0; }
   if (k == "bar_max") {
     if (n < 0 || n > (64l << 20)) return -EINVAL;
@@ -116,6 +125,10 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "inline_max") v = inline_max;
   else if (k == "bar_map") v = bar_map;
   else if (k == "coalesce") v = coalesce;
+  else if (k == "ingest") v = ingest;
+  else if (k == "ingest_grid") v = ingest_grid;
+  else if (k == "ingest_piece") v = ingest_piece;
+  else if (k == "hdp_sync") v = hdp_sync;
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;

@@ -57,6 +57,12 @@ struct Config {
   uint32_t inline_max = 64u << 10;  // single requests up to this run inline
   bool bar_map = true;           // CPU-map HBM through the large BAR (dma-buf)
   bool coalesce = true;          // workers merge adjacent staged HBM copies
+  bool ingest = true;            // staged reads reach HBM through the GPU ingest
+                                 // grid (ingest.hip) instead of SDMA copies
+  int ingest_grid = 16;          // workgroups of the ingest grid (CUs it holds)
+  uint32_t ingest_piece = 256u << 10;  // bytes per ingest descriptor
+  bool hdp_sync = false;         // wait for each HDP flush to complete (read
+                                 // back) instead of posting it
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks
@@ -180,7 +186,7 @@ struct GpuMapping {
   // CPU store of [src, src+len) into HBM at device VA dst through the BAR;
   // false when the range is not BAR-mapped.  Ends with a read-back that
   // flushes the posted writes, so the data is in HBM when this returns.
-  bool bar_write(uint64_t dst, const void *src, size_t len) const;
+  bool bar_write(uint64_t dst, const void *src, size_t len, bool flush = true) const;
   // make CPU stores through the BAR (ending at `last`) visible to shaders:
   // sfence, then an HDP flush (write + read back the flush register, as
   // the runtime does for CPU-written kernargs in VRAM); without the
@@ -345,6 +351,45 @@ struct FaultInjector {
 };
 FaultInjector &faults();
 
+// ------------------------------------------------------------- HBM ingest
+// Host side of the persistent GPU pull grid (ingest.cc / ingest.hip): staged
+// bytes in pinned host memory are posted as descriptors and copied into HBM
+// by the GPU; completion is a host-memory word per descriptor.
+class Ingest {
+ public:
+  static Ingest *get(int device);   // null when disabled or unavailable
+  // Post [src, src+len) -> device VA dst as ceil(len / piece) descriptors with
+  // consecutive sequence numbers *first .. *first + *n - 1.  false: not
+  // postable (alignment, grid failure) — the caller falls back to SDMA.
+  bool post(const void *src, uint64_t dst, uint32_t len, uint64_t *seq);
+  bool post_many(const void *src, uint64_t dst, uint32_t len, uint32_t piece, uint64_t *first,
+                 uint32_t *n);
+  bool is_done(uint64_t seq) const;
+  void retired(uint32_t n);         // the poster observed n descriptors done
+  void idle();                      // stop the grid when nothing is outstanding
+  void shutdown();
+  void info(uint64_t *out);         // {available, launches, posted, outstanding}
+
+ private:
+  explicit Ingest(int device);
+  bool init();
+  int launch_grid();
+  int start_locked();
+  void stop_locked();
+  bool post_locked(const void *src, uint64_t dst, uint32_t len, uint64_t *seq);
+
+  int device_;
+  uint32_t nslots_ = 0, grid_ = 0;
+  void *host_ = nullptr, *ring_ = nullptr, *next_ = nullptr;
+  volatile uint64_t *done_ = nullptr, *stop_ = nullptr;
+  void *stream_ = nullptr, *end_ev_ = nullptr;
+  std::mutex mu_;
+  uint64_t post_seq_ = 0;
+  bool running_ = false, launched_ = false, dead_ = false;
+  std::atomic<long> outstanding_{0};
+  uint64_t nr_launch_ = 0;
+};
+
 // ------------------------------------------------------------- HIP glue
 namespace hip {
 bool available();
@@ -352,9 +397,11 @@ int device_count();
 // device ordinal of a device pointer, -1 when not device memory; sets
 // *alloc_base/*alloc_size to the enclosing allocation when known.
 int pointer_device(uint64_t va, uint64_t *alloc_base, size_t *alloc_size);
-void *host_alloc(size_t bytes);            // pinned, portable
+void *host_alloc(size_t bytes, bool coherent = false);  // pinned, portable
 void host_free(void *p);
-void *host_alloc_thp(size_t bytes);        // THP-backed, hipHostRegister'ed
+// THP-backed, hipHostRegister'ed; `uncached`: GPU reads bypass its caches
+// (staging the ingest grid pulls from)
+void *host_alloc_thp(size_t bytes, bool uncached = false);
 void host_free_thp(void *p, size_t bytes);
 // CPU mapping of device memory [va, va+len) through its dma-buf export;
 // returns the mapping (and sets *map_va/*map_len to what it covers) or null.

@@ -63,11 +63,14 @@ int pointer_device(uint64_t va, uint64_t *alloc_base, size_t *alloc_size) {
   return attr.device;
 }
 
-void *host_alloc(size_t bytes) {
+// `coherent`: fine-grained, so that GPU reads (the ingest grid) never hit
+// stale cached lines when the CPU refills the buffer
+void *host_alloc(size_t bytes, bool coherent) {
   void *p = nullptr;
-  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocNumaUser) != hipSuccess) {
+  const unsigned cf = coherent ? hipHostMallocCoherent : 0u;
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocNumaUser | cf) != hipSuccess) {
     (void)hipGetLastError();
-    if (hipHostMalloc(&p, bytes, hipHostMallocPortable) != hipSuccess) {
+    if (hipHostMalloc(&p, bytes, hipHostMallocPortable | cf) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
     }
@@ -84,7 +87,7 @@ void host_free(void *p) {
 // O_DIRECT into 2 MiB pages costs the kernel far less page pinning than
 // into hipHostMalloc's 4 KiB pages (single-thread 19-20 vs 14 GiB/s), and
 // SDMA reads it at the same ~50 GiB/s.
-void *host_alloc_thp(size_t bytes) {
+void *host_alloc_thp(size_t bytes, bool uncached) {
   const size_t huge = 2u << 20;
   size_t len = (bytes + huge - 1) / huge * huge;
   void *raw = mmap(nullptr, len + huge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
@@ -96,7 +99,10 @@ void *host_alloc_thp(size_t bytes) {
   void *p = (void *)a;
   madvise(p, len, MADV_HUGEPAGE);
   memset(p, 0, len);  // fault in (under the caller's NUMA policy)
-  if (hipHostRegister(p, len, hipHostRegisterPortable) != hipSuccess) {
+  // uncached for the GPU: the ingest grid reads each slot again after the
+  // CPU refilled it, and must not be served a stale L2 copy
+  const unsigned fl = hipHostRegisterPortable | (uncached ? hipExtHostRegisterUncached : 0u);
+  if (hipHostRegister(p, len, fl) != hipSuccess) {
     (void)hipGetLastError();
     munmap(p, len);
     return nullptr;

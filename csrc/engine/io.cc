@@ -6,10 +6,13 @@
 //   caller thread ── submit() ──► per-worker queue (batched, one lock)
 //   worker k:  io_uring READs (O_DIRECT) up to queue_depth in flight
 //              ├─ host destination (SSD2RAM): done on CQE
-//              └─ HBM destination: CQE ► hipMemcpyAsync(slot → HBM) on the
-//                 worker's own non-blocking stream (its own SDMA queue),
-//                 hipEventRecord; the worker retires events in FIFO order,
-//                 returning the pinned slot and putting the task.
+//              └─ HBM destination: CQE ► descriptor(s) posted to the device's
+//                 ingest grid (ingest.cc: the GPU pulls the staged bytes into
+//                 HBM; no HIP call on this thread); the worker polls the
+//                 done words, returns the pinned slot and puts the task.
+//                 Without the grid (ingest=0, host-only builds): small
+//                 requests are CPU-stored through the large BAR, larger ones
+//                 go out as coalesced hipMemcpyAsync SDMA copies + events.
 //
 // Each worker owns its ring, its staging slots and its stream, so the hot
 // path takes no shared lock.  Workers are pinned to the CPUs of the GPU's
@@ -179,6 +182,9 @@ struct IoEngine::Worker {
     IoReq req;
     uint64_t t_copy_ns = 0;
     int ev_slot = -1;    // slot whose event covers this slot's copy
+    Ingest *ing = nullptr;   // ingest descriptors seq_first .. + nseq - 1
+    uint64_t seq_first = 0;
+    uint32_t nseq = 0;
   };
   struct Ctx {           // one in-flight storage read
     IoReq req;
@@ -204,6 +210,8 @@ struct IoEngine::Worker {
   std::deque<int> free_slots;     // FIFO: consecutive requests get adjacent slots
   std::deque<int> copying;        // FIFO of slots with copies in flight
   std::vector<int> staged;        // reads done, HBM copy not yet issued
+  std::vector<int> ingesting;     // slots whose bytes the ingest grid is pulling
+  std::vector<std::pair<int, Ingest *>> ings;  // device -> ingest grid (or null)
   std::vector<hipStream_t> streams;
   int cur_dev = -2;
   Uring ring;
@@ -253,9 +261,9 @@ struct IoEngine::Worker {
     if (!slots.empty()) return true;
     const int ns = nslots();
     size_t bytes = (size_t)ns * cfg.max_request;
-    staging = (uint8_t *)hip::host_alloc_thp(bytes);
+    staging = (uint8_t *)hip::host_alloc_thp(bytes, cfg.ingest);
     staging_thp = staging != nullptr;
-    if (!staging) staging = (uint8_t *)hip::host_alloc(bytes);
+    if (!staging) staging = (uint8_t *)hip::host_alloc(bytes, cfg.ingest);
     if (!staging) {
       STROM_LOG(0, "worker %d: pinned staging allocation failed", idx);
       return false;
@@ -286,6 +294,39 @@ struct IoEngine::Worker {
     return streams[dev];
   }
 
+  Ingest *ingest_for(int dev) {
+    for (auto &p : ings)
+      if (p.first == dev) return p.second;
+    Ingest *ing = cfg.ingest ? Ingest::get(dev) : nullptr;
+    ings.emplace_back(dev, ing);
+    return ing;
+  }
+
+  // retire slots whose ingest descriptors are all done
+  bool retire_ingest() {
+    bool any = false;
+    for (size_t i = 0; i < ingesting.size();) {
+      const int si = ingesting[i];
+      Slot &s = slots[si];
+      bool all = true;
+      for (uint32_t k = 0; k < s.nseq && all; ++k) all = s.ing->is_done(s.seq_first + k);
+      if (!all) {
+        ++i;
+        continue;
+      }
+      const uint64_t dt = mono_ns() - s.t_copy_ns;
+      stats().copy_ns.add(dt);
+      stats().clk_debug[0].fetch_add(dt, std::memory_order_relaxed);
+      s.ing->retired(s.nseq);
+      ingesting[i] = ingesting.back();
+      ingesting.pop_back();
+      free_slots.push_back(si);
+      finish_request(s.req, 0);
+      any = true;
+    }
+    return any;
+  }
+
   // storage read finished for ctx c with `got` bytes or -errno
   void on_read_done(Ctx &c, long got) {
     IoReq &r = c.req;
@@ -301,6 +342,20 @@ struct IoEngine::Worker {
       free_slots.push_back(c.slot);
       finish_request(r, status);
       return;
+    }
+    if (Ingest *ing = r.gmap ? ingest_for(r.device) : nullptr) {
+      uint64_t first = 0;
+      uint32_t n = 0;
+      if (ing->post_many(c.dst, r.gpu_dst, r.len, cfg.ingest_piece, &first, &n)) {
+        s.req = r;
+        s.t_copy_ns = now;
+        s.ing = ing;
+        s.seq_first = first;
+        s.nseq = n;
+        ingesting.push_back(c.slot);
+        stats().nr_debug[0].fetch_add(n, std::memory_order_relaxed);
+        return;
+      }
     }
     // worker requests take the BAR only up to 64 KiB: past that the workers'
     // CPU stores fall behind SDMA (256 KiB: 14.2 vs 17.8 GiB/s, 512 KiB: 23.7
@@ -477,15 +532,22 @@ struct IoEngine::Worker {
     std::deque<IoReq> local;
     for (;;) {
       if (local.empty()) {
-        if (spin_ns && reads_inflight == 0 && copying.empty() && !pending.load(std::memory_order_acquire)) {
+        const bool quiet = reads_inflight == 0 && copying.empty() && ingesting.empty();
+        if (spin_ns && quiet && !pending.load(std::memory_order_acquire)) {
           // idle: poll briefly before sleeping, so back-to-back work skips
           // the futex wake-up (bounded, so stop is still seen promptly)
           const uint64_t end = mono_ns() + spin_ns;
           while (!pending.load(std::memory_order_acquire) && mono_ns() < end)
             for (int i = 0; i < 32; ++i) _mm_pause();
         }
+        if (quiet && !pending.load(std::memory_order_acquire)) {
+          // about to sleep: let the ingest grids stop if nobody has work
+          // in them (a device-wide synchronize must not wait on them)
+          for (auto &p : ings)
+            if (p.second) p.second->idle();
+        }
         std::unique_lock<std::mutex> g(mu);
-        if (q.empty() && reads_inflight == 0 && copying.empty()) {
+        if (q.empty() && quiet) {
           if (stop) break;
           sleeping = true;
           cv.wait(g, [&] { return stop || !q.empty(); });
@@ -505,20 +567,33 @@ struct IoEngine::Worker {
       }
       if (use_ring && ring.pending()) ring.enter(0);
       retire(false);
+      retire_ingest();
       if (use_ring) reap();
       if (!local.empty() && !blocked && reads_inflight < qd) continue;
       // nothing more can start: wait for a read, a copy, or new work
-      if (reads_inflight > 0 && copying.empty()) {
+      const bool hbm_busy = !copying.empty() || !ingesting.empty();
+      if (reads_inflight > 0 && !hbm_busy) {
         ring.enter(1);
         reap();
-      } else if (reads_inflight == 0 && !copying.empty()) {
+      } else if (reads_inflight == 0 && hbm_busy) {
         if (local.empty()) {
           std::lock_guard<std::mutex> g(mu);
           if (!q.empty()) continue;
         }
-        retire(true);
+        if (!ingesting.empty()) {
+          // the grid's completions land in host memory within microseconds:
+          // poll them (and any SDMA events) instead of sleeping
+          const uint64_t end = mono_ns() + 200000;
+          while (!retire_ingest() && mono_ns() < end) {
+            for (int i = 0; i < 16; ++i) _mm_pause();
+            if (pending.load(std::memory_order_acquire)) break;
+          }
+          retire(false);
+        } else {
+          retire(true);
+        }
       } else if (reads_inflight > 0) {
-        sched_yield();  // both pipes busy
+        if (!retire_ingest()) sched_yield();  // both pipes busy
       }
     }
     for (auto &s : slots)

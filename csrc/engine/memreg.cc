@@ -43,23 +43,33 @@ namespace strom {
 // ------------------------------------------------------- GPU registry
 GpuMapping::~GpuMapping() { hip::bar_unmap(bar, bar_len); }
 
-bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len) const {
+bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len, bool flush) const {
   if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
   uint8_t *p = bar + (dst - bar_va);
   memcpy(p, src, len);
   phase_mark(4);
-  bar_flush(p + ((len - 1) & ~(size_t)3));
+  if (flush) bar_flush(p + ((len - 1) & ~(size_t)3));
   phase_mark(5);
   return true;
 }
 
+// The HDP flush is POSTED by default: the register write travels behind the
+// data writes (PCIe posted writes stay in order), and anything that can
+// consume the bytes afterwards — a kernel launch, an SDMA copy — is started
+// by a later doorbell write, itself posted behind the flush.  Reading the
+// register back (hdp_sync=1, what the runtime does for kernargs) waits for
+// the flush to finish: +1.4 us per call on MI355X (round 1 p50 phases).
+// tests/test_gpu_core.py::test_pread_gpu_visible_to_next_kernel checks the
+// posted form on 1000 distinct offsets, each read by a kernel launched right
+// after pread_gpu returns.
 void GpuMapping::bar_flush(const uint8_t *last) const {
   _mm_sfence();
   if (hdp) {
     *hdp = 1u;
-    (void)*hdp;
+    if (config().hdp_sync) (void)*hdp;
   } else {
-    // a read from the device cannot pass the posted writes before it
+    // no flush register: a read from the device cannot pass the posted
+    // writes before it
     (void)*(const volatile uint32_t *)last;
   }
 }

@@ -68,6 +68,11 @@ int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
  * (MAP_GPU_DMABUF).  The caller closes the fd. */
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset);
 
+/* HBM ingest grid of a device (the persistent GPU pull kernel that moves
+ * staged reads into HBM): out[4] = {available, grid launches, descriptors
+ * posted, descriptors outstanding}.  -ENODEV when it cannot run there. */
+int strom_ingest_info(int device, uint64_t *out);
+
 /* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
 int strom_config_set(const char *key, const char *value);
 int strom_config_get(const char *key, char *buf, size_t buflen);

@@ -3,21 +3,27 @@
 // The reference's PostgreSQL CustomScan loads heap blocks into a DMA buffer
 // and then walks line pointers on the CPU (pgsql/nvme_strom.c:1054-1092:
 // nvmestrom_next_tuple), with visibility handled per tuple for blocks that
-// came through the buffer manager (:896-940).  On MI355X the loaded pages sit
-// in HBM and one wavefront per page does all of it:
+// came through the buffer manager (:896-940) and all-visible blocks taken as
+// they are (:870-891).  On MI355X the loaded pages sit in HBM and one
+// wavefront per page does all of it, from an LDS copy of the page:
+//   0. the page is staged into LDS with coalesced 16-B loads (one 1 KiB
+//      wave-instruction per 1 KiB of page); the NEXT page's loads are issued
+//      before the current page is parsed, so HBM latency hides under the
+//      parse (every later access — header, checksum columns, line pointers,
+//      tuple headers, column values — is an LDS access);
 //   1. page header sanity (pd_lower/pd_upper/pd_special bounds, flag bits,
 //      page size) — PageIsVerified-style;
 //   2. optional data checksum (pg_checksum_page: 32 interleaved FNV-1a
-//      sums = 32 lanes, one column of uint32 words each);
+//      sums = 32 lanes, one column of uint32 words each, conflict-free
+//      ds_read_b32 across the lanes of a row);
 //   3. line pointers 64 at a time (one per lane): LP_NORMAL items, optional
-//      hint-bit visibility (xmin committed, xmax invalid or lock-only), and
-//      an optional range predicate on a fixed-offset int4/int8 column; the
-//      per-64 ballot masks are parked in LDS;
+//      visibility (PD_ALL_VISIBLE page: every tuple; else xmin known
+//      committed — frozen xmin included — and xmax invalid or lock-only),
+//      and an optional range predicate on a fixed-offset int4/int8 column;
+//      the per-64 ballot masks are parked in LDS;
 //   4. output reservation once per WORKGROUP (4 pages): the waves' counts
 //      are summed in LDS and thread 0 does a single atomicAdd, then each
 //      wave replays its masks to write (page << 16 | lineno) item ids.
-//      A same-address atomic per 64 items capped v1 at ~234 GB/s on scans
-//      where most tuples qualify (~88 same-word atomics/us on MI355X).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -35,108 +41,160 @@ __constant__ uint32_t g_pg_base[32] = {
     0x9FBF8C76, 0x15CA20BE, 0xF2CA9FFF, 0x3ED50F2B};
 
 constexpr uint32_t kSizeOfPageHeader = 24;
-constexpr uint16_t kLpNormal = 1;
-constexpr uint16_t kHeapHasNull = 0x0001;
-constexpr uint16_t kXmaxLockOnly = 0x0080;
-constexpr uint16_t kXminCommitted = 0x0100;
-constexpr uint16_t kXminInvalid = 0x0200;
-constexpr uint16_t kXmaxInvalid = 0x0800;
-constexpr uint32_t kMaxChunks = 128;  // 32 KiB pages: <= 8186 line pointers
+constexpr uint32_t kLpNormal = 1;
+constexpr uint32_t kHeapHasNull = 0x0001;
+constexpr uint32_t kXmaxLockOnly = 0x0080;
+constexpr uint32_t kXminCommitted = 0x0100;   // also set in a frozen xmin (0x0300)
+constexpr uint32_t kXmaxInvalid = 0x0800;
+constexpr uint32_t kPdAllVisible = 0x0004;
+constexpr int kWaves = 4;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t fnv_mix(uint32_t s, uint32_t v) {
   uint32_t t = s ^ v;
   return t * 16777619u ^ (t >> 17);
 }
 
-__device__ __forceinline__ uint16_t ld16(const uint8_t *p) {
-  return (uint16_t)(p[0] | (p[1] << 8));
+// little-endian reads from the LDS page image.  Tuple offsets are MAXALIGNed
+// but user columns need not be 4-aligned, so wide reads are assembled from
+// the two aligned words around them.
+__device__ __forceinline__ uint32_t lds_u32a(const uint8_t *pg, uint32_t off) {
+  return *(const uint32_t *)(pg + off);  // off % 4 == 0
+}
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *pg, uint32_t off) {
+  const uint32_t sh = (off & 3) * 8;
+  const uint32_t lo = lds_u32a(pg, off & ~3u);
+  if (!sh) return lo;
+  const uint32_t hi = lds_u32a(pg, (off & ~3u) + 4);
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
 }
 
-__device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+struct PageHdr {
+  uint32_t checksum, flags, lower, upper, special, psv;
+};
+
+__device__ __forceinline__ PageHdr read_hdr(const uint8_t *pg) {
+  PageHdr h;
+  const uint32_t w2 = lds_u32a(pg, 8), w3 = lds_u32a(pg, 12), w4 = lds_u32a(pg, 16);
+  h.checksum = w2 & 0xffff;
+  h.flags = w2 >> 16;
+  h.lower = w3 & 0xffff;
+  h.upper = w3 >> 16;
+  h.special = w4 & 0xffff;
+  h.psv = w4 >> 16;
+  return h;
 }
 
 // page header check + optional checksum; returns STROM_PAGE_* bits
-__device__ uint32_t page_status(const strom_heap_scan_args &a, const uint8_t *page, uint32_t pg,
-                                uint32_t lane) {
-  const uint32_t *w = (const uint32_t *)page;
-  const uint16_t pd_checksum = ld16(page + 8);
-  const uint16_t pd_flags = ld16(page + 10);
-  const uint16_t pd_lower = ld16(page + 12);
-  const uint16_t pd_upper = ld16(page + 14);
-  const uint16_t pd_special = ld16(page + 16);
-  const uint16_t pd_psv = ld16(page + 18);
-  if (pd_upper == 0) return STROM_PAGE_EMPTY;
-  if (pd_lower < kSizeOfPageHeader || pd_lower > pd_upper || pd_upper > pd_special ||
-      pd_special > a.page_sz || (pd_special & 7) || (pd_flags & ~0x7u) ||
-      (pd_psv & 0xFF00u) != (a.page_sz & 0xFF00u))
+__device__ uint32_t page_status(const strom_heap_scan_args &a, const uint8_t *pg,
+                                const PageHdr &h, uint32_t page_no, uint32_t lane) {
+  if (h.upper == 0) return STROM_PAGE_EMPTY;
+  if (h.lower < kSizeOfPageHeader || h.lower > h.upper || h.upper > h.special ||
+      h.special > a.page_sz || (h.special & 7) || (h.flags & ~0x7u) ||
+      (h.psv & 0xFF00u) != (a.page_sz & 0xFF00u))
     return STROM_PAGE_BAD_HEADER;
   if (!(a.flags & STROM_HEAP_VERIFY_CHECKSUM)) return 0;
-  // lanes 0..31 own one FNV sum each; lanes 32..63 duplicate (ignored)
+  // lanes 0..31 own one FNV sum each (lanes 32..63 duplicate and are
+  // ignored); lane j reads column j of each 128-B row: 32 consecutive words
   const uint32_t j = lane & 31;
+  const uint32_t *w = (const uint32_t *)pg;
   uint32_t s = g_pg_base[j];
   const uint32_t rows = a.page_sz / 128;
-  for (uint32_t r = 0; r < rows; ++r) {
-    uint32_t v = w[r * 32 + j];
-    if (r == 0 && j == 2) v &= 0xffff0000u;  // pd_checksum reads as zero
+  {
+    uint32_t v = w[j];
+    if (j == 2) v &= 0xffff0000u;  // pd_checksum reads as zero
     s = fnv_mix(s, v);
   }
+  for (uint32_t r = 1; r < rows; ++r) s = fnv_mix(s, w[r * 32 + j]);
   s = fnv_mix(s, 0);
   s = fnv_mix(s, 0);
 #pragma unroll
   for (int o = 16; o > 0; o >>= 1) s ^= __shfl_xor(s, o, 64);
-  const uint32_t blkno = a.blknos ? a.blknos[pg] : a.blkno_base + pg;
+  const uint32_t blkno = a.blknos ? a.blknos[page_no] : a.blkno_base + page_no;
   const uint32_t c = ((s ^ blkno) % 65535u) + 1u;
-  return (uint16_t)c != pd_checksum ? STROM_PAGE_BAD_CHECKSUM : 0u;
+  return (c & 0xffffu) != h.checksum ? STROM_PAGE_BAD_CHECKSUM : 0u;
 }
 
-__device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const uint8_t *page,
-                                           uint32_t lp) {
+__device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const uint8_t *pg,
+                                           uint32_t lp, bool all_visible) {
   const uint32_t off = lp & 0x7fff, flags = (lp >> 15) & 3, len = lp >> 17;
-  if (flags != kLpNormal || len < 23 || off < kSizeOfPageHeader || off + len > a.page_sz)
+  if (flags != kLpNormal || len < 23 || off < kSizeOfPageHeader || off + len > a.page_sz ||
+      (off & 1))
     return false;
-  const uint8_t *tup = page + off;
-  const uint16_t infomask = ld16(tup + 20);
-  if (a.flags & STROM_HEAP_SKIP_INVISIBLE) {
-    bool xmin_ok = (infomask & kXminCommitted) && !(infomask & kXminInvalid);
-    bool xmax_ok = (infomask & kXmaxInvalid) || (infomask & kXmaxLockOnly);
-    if (!(xmin_ok && xmax_ok)) return false;
+  const uint32_t w20 = lds_u32(pg, off + 20);  // t_infomask (16) | t_hoff (8) | bits
+  const uint32_t infomask = w20 & 0xffff, hoff = (w20 >> 16) & 0xff;
+  if ((a.flags & STROM_HEAP_SKIP_INVISIBLE) && !all_visible) {
+    // no clog here: only hint bits that prove visibility count
+    if (!(infomask & kXminCommitted)) return false;
+    if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return false;
   }
   if (a.attr_off < 0) return true;
-  const uint32_t at = tup[22] + (uint32_t)a.attr_off;
+  const uint32_t at = hoff + (uint32_t)a.attr_off;
   if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return false;
   int64_t v;
   if (a.attr_width == 8) {
-    uint64_t lo = ld32u(tup + at), hi = ld32u(tup + at + 4);
+    const uint64_t lo = lds_u32(pg, off + at), hi = lds_u32(pg, off + at + 4);
     v = (int64_t)(lo | (hi << 32));
   } else {
-    v = (int32_t)ld32u(tup + at);
+    v = (int32_t)lds_u32(pg, off + at);
   }
   return v >= a.lo && v <= a.hi;
 }
 
-__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a) {
-  __shared__ uint64_t masks[4][kMaxChunks];
-  __shared__ uint32_t wcount[4];
-  __shared__ uint32_t wbase[4];
+// PAGE = page size known at compile time (0: a.page_sz at run time).  Each
+// lane moves NV 16-byte pieces of its wave's page per iteration.
+template <int PAGE>
+__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, uint32_t maxchunks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t page_sz = PAGE ? (uint32_t)PAGE : a.page_sz;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t *mypage = smem + (size_t)wid * page_sz;
+  uint64_t *masks = (uint64_t *)(smem + (size_t)kWaves * page_sz) + (size_t)wid * maxchunks;
+  uint32_t *wcount = (uint32_t *)((uint64_t *)(smem + (size_t)kWaves * page_sz) + kWaves * maxchunks);
+  uint32_t *wbase = wcount + kWaves;
+
+  constexpr int NV = PAGE ? PAGE / (64 * 16) : 32;   // 32 = up to 32 KiB pages
+  const uint32_t nv = page_sz / (64 * 16);
+  v4u buf[NV];
+
+#define STROM_HS_ISSUE(page_no)                                                           \
+  do {                                                                                    \
+    const v4u *src_ = (const v4u *)((const uint8_t *)a.pages + (uint64_t)(page_no) * page_sz); \
+    _Pragma("unroll") for (int k = 0; k < NV; ++k)                                        \
+      if (PAGE || (uint32_t)k < nv) buf[k] = __builtin_nontemporal_load(src_ + k * 64 + lane); \
+  } while (0)
+
+  const uint32_t stride = gridDim.x * kWaves;
+  uint32_t pg = blockIdx.x * kWaves + wid;
+  if (pg < a.npages) STROM_HS_ISSUE(pg);
   // every wave of a workgroup runs the same trip count (barriers inside)
-  for (uint32_t base = blockIdx.x * 4; base < a.npages; base += gridDim.x * 4) {
-    const uint32_t pg = base + wid;
+  for (uint32_t base = blockIdx.x * kWaves; base < a.npages; base += stride, pg += stride) {
+    const bool have = pg < a.npages;
+    if (have) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        if (PAGE || (uint32_t)k < nv) ((v4u *)mypage)[k * 64 + lane] = buf[k];
+    }
+    __syncthreads();
+    // next page's loads are in flight while this one is parsed from LDS
+    if (pg + stride < a.npages) STROM_HS_ISSUE(pg + stride);
+
     uint32_t count = 0, nchunks = 0;
-    const uint8_t *page = (const uint8_t *)a.pages + (uint64_t)pg * a.page_sz;
-    if (pg < a.npages) {
-      const uint32_t status = page_status(a, page, pg, lane);
+    if (have) {
+      const PageHdr h = read_hdr(mypage);
+      const uint32_t status = page_status(a, mypage, h, pg, lane);
       if (lane == 0 && a.page_status) a.page_status[pg] = status;
       if (status == 0) {
-        const uint32_t *w = (const uint32_t *)page;
-        const uint32_t nitems = (ld16(page + 12) - kSizeOfPageHeader) / 4;
+        const bool all_visible = (h.flags & kPdAllVisible) != 0;
+        const uint32_t nitems = (h.lower - kSizeOfPageHeader) / 4;
         nchunks = (nitems + 63) / 64;
         for (uint32_t c = 0; c < nchunks; ++c) {
           const uint32_t i = c * 64 + lane;
-          const bool keep = i < nitems && tuple_keep(a, page, w[6 + i]);
+          const bool keep =
+              i < nitems && tuple_keep(a, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i),
+                                       all_visible);
           const uint64_t m = __ballot(keep);
-          if (lane == 0) masks[wid][c] = m;
+          if (lane == 0) masks[c] = m;
           count += __popcll(m);
         }
       }
@@ -144,9 +202,10 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a) 
     if (lane == 0) wcount[wid] = count;
     __syncthreads();
     if (threadIdx.x == 0) {
-      const uint32_t total = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+      uint32_t total = 0;
+      for (int k = 0; k < kWaves; ++k) total += wcount[k];
       uint32_t start = total ? atomicAdd(a.out_count, total) : 0u;
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kWaves; ++k) {
         wbase[k] = start;
         start += wcount[k];
       }
@@ -156,7 +215,7 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a) 
       uint32_t run = wbase[wid];
       const uint64_t below = (1ull << lane) - 1;
       for (uint32_t c = 0; c < nchunks; ++c) {
-        const uint64_t m = masks[wid][c];
+        const uint64_t m = masks[c];
         if ((m >> lane) & 1) {
           const uint32_t slot = run + __popcll(m & below);
           if (slot < a.out_cap) a.out_items[slot] = (pg << 16) | (c * 64 + lane + 1);  // 1-based
@@ -164,22 +223,32 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a) 
         run += __popcll(m);
       }
     }
-    __syncthreads();  // masks/wcount are reused by the next iteration
+    __syncthreads();  // page image, masks and wcount are reused next iteration
   }
+#undef STROM_HS_ISSUE
 }
 
 }  // namespace
 
 extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   if (!a || !a->pages || !a->out_count) return -22;
-  if (a->page_sz < 1024 || (a->page_sz & 127) || a->page_sz > 32768) return -22;
+  if (a->page_sz < 1024 || (a->page_sz & 1023) || a->page_sz > 32768) return -22;
   if (a->attr_off >= 0 && a->attr_width != 4 && a->attr_width != 8) return -22;
   // (page << 16 | lineno) item ids address at most 65535 pages per call
   if (a->out_items && a->npages > 0xffffu) return -34;
   if (a->npages == 0) return 0;
-  (void)hipMemsetAsync(a->out_count, 0, sizeof(uint32_t), (hipStream_t)stream);
-  uint32_t grid = (a->npages + 3) / 4;
-  if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(heap_scan_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(a->out_count, 0, sizeof(uint32_t), st);
+  const uint32_t maxchunks = ((a->page_sz - 24) / 4 + 63) / 64;
+  const size_t lds = (size_t)kWaves * a->page_sz + (size_t)kWaves * maxchunks * 8 + 2 * kWaves * 4;
+  // enough workgroups to fill 256 CUs at the occupancy LDS allows, then stride
+  const uint32_t per_cu = (uint32_t)(160u * 1024u / ((lds + 1023) & ~(size_t)1023));
+  uint32_t grid = (a->npages + kWaves - 1) / kWaves;
+  const uint32_t cap = 256u * (per_cu ? per_cu : 1u) * 2u;
+  if (grid > cap) grid = cap;
+  if (a->page_sz == 8192)
+    hipLaunchKernelGGL(heap_scan_kernel<8192>, dim3(grid), dim3(256), lds, st, *a, maxchunks);
+  else
+    hipLaunchKernelGGL(heap_scan_kernel<0>, dim3(grid), dim3(256), lds, st, *a, maxchunks);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

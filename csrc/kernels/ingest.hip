@@ -1,0 +1,133 @@
+// ingest.hip — the device side of the HBM ingest engine (csrc/engine/ingest.cc).
+//
+// The reference never copied anything on the GPU: its NVMe READs wrote
+// straight into BAR pages (kmod/nvme_strom.c:1408-1482).  An unprivileged
+// process reads into pinned host staging instead, and every staged request
+// then has to reach HBM.  Round 1 issued one hipMemcpyAsync + hipEventRecord
+// per (coalesced) request: 14-23 us of host CPU per call (profiles/r1s), which
+// capped 4-128 KiB streams at 65-75% of the storage rate.  Here the copy is
+// PULLED by the GPU: a small persistent grid polls a descriptor ring in
+// fine-grained host memory, copies each staged range over PCIe with 16-byte
+// loads (32 KiB in flight per workgroup), and publishes completion into a
+// host-memory done[] word.  Posting a request costs the host one 32-byte
+// store sequence; no HIP API call, no syscall.
+//
+// Protocol (host side: ingest.cc):
+//   ring[s % nslots] = {src, dst, len, seq = s + 1}   host stores seq last
+//   done[s % nslots] = s + 1                          device, after the bytes
+//                                                     are written through to HBM
+//   *stop != 0                                        every waiting workgroup exits
+// A workgroup claims the next sequence number from a device counter, waits
+// for the host to post it (or for stop), copies, and publishes.  Payload
+// stores are write-through (sc1: the line leaves this XCD's L2), every wave
+// drains its stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
+// then one lane stores done[] at system scope: the valid hand-off form of
+// MI355X_MICROARCH.md §visibility without an L2 write-back of the whole XCD
+// (other kernels' dirty lines are not ours to flush).
+//
+// Termination: the host sets *stop whenever the engine goes idle (no request
+// outstanding) and before it exits; every spin in here re-reads *stop, so the
+// grid always drains.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u gv4u;   // global, not flat
+
+struct IngestDesc {          // 32 bytes, ingest.cc writes the same layout
+  uint64_t src;              // pinned host VA (fine-grained, GPU-mapped)
+  uint64_t dst;              // device VA
+  uint64_t len_tag;          // low 32 bits: byte count (multiple of 16)
+  uint64_t seq;              // s + 1 once posted
+};
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 8;   // 16-B loads in flight per lane
+constexpr int kAuxSc1 = 16;  // buffer store cache policy: sc1 (write-through)
+
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kThreads) void ingest_kernel(const IngestDesc *ring, uint64_t *done,
+                                                          const uint64_t *stop, uint32_t *next,
+                                                          uint32_t nslots, uint64_t base) {
+  __shared__ uint64_t s_src, s_dst, s_seq;
+  __shared__ uint32_t s_len;
+  __shared__ int s_ok;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t s = base + atomicAdd(next, 1u);
+      const IngestDesc *d = ring + (s % nslots);
+      int ok = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_sys(&d->seq) == s + 1) {
+          ok = 1;
+          break;
+        }
+        if (ld_sys(stop)) break;
+        if (spin < 256) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(16);
+      }
+      // the field loads below are issued after the seq load returned
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ok) {
+        s_src = ld_sys(&d->src);
+        s_dst = ld_sys(&d->dst);
+        s_len = (uint32_t)ld_sys(&d->len_tag);
+      }
+      s_seq = s;
+      s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;  // uniform: stop requested
+    gv4u *src = (gv4u *)s_src;
+    const uint32_t n16 = s_len >> 4;
+    // wave-uniform descriptor for the destination (SGPRs: no waterfall loop)
+    const uint64_t dst = s_dst;
+    const uint32_t dlo = __builtin_amdgcn_readfirstlane((uint32_t)dst);
+    const uint32_t dhi = __builtin_amdgcn_readfirstlane((uint32_t)(dst >> 32));
+    const uint32_t nbytes = __builtin_amdgcn_readfirstlane(s_len);
+    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)dhi << 32) | dlo), (short)0, (int)nbytes, 0x00020000);
+    for (uint32_t i = threadIdx.x; i < n16; i += kThreads * kUnroll) {
+      v4u r[kUnroll];
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) {
+        const uint32_t idx = i + k * kThreads;
+        if (idx < n16) r[k] = __builtin_nontemporal_load(src + idx);
+      }
+#pragma unroll
+      for (int k = 0; k < kUnroll; ++k) {
+        const uint32_t idx = i + k * kThreads;
+        if (idx < n16) __builtin_amdgcn_raw_buffer_store_b128(r[k], rsrc, (int)(idx * 16), 0, kAuxSc1);
+      }
+    }
+    // every storing wave drains its write-through stores, then one lane publishes
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t s = s_seq;
+      __hip_atomic_store(done + (s % nslots), s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();  // s_* are rewritten by the next claim
+  }
+}
+
+}  // namespace
+
+// Launch `grid` workgroups of the ingest grid on `stream`.  `next` is a
+// device u32 the caller zeroed on the same stream; sequence numbers handed out
+// start at `base`.  Returns 0 or -EIO.
+extern "C" int strom_ingest_kernel_launch(const void *ring, void *done, const void *stop,
+                                          void *next, uint32_t nslots, uint64_t base,
+                                          uint32_t grid, void *stream) {
+  if (!ring || !done || !stop || !next || nslots == 0 || grid == 0 || grid > 1024) return -22;
+  hipLaunchKernelGGL(ingest_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream,
+                     (const IngestDesc *)ring, (uint64_t *)done, (const uint64_t *)stop,
+                     (uint32_t *)next, nslots, base);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}

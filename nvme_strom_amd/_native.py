@@ -158,6 +158,7 @@ _SIGS = {
                                       C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "strom_export_dmabuf": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_int),
                                       C.POINTER(C.c_uint64)]),
+    "strom_ingest_info": (C.c_int, [C.c_int, C.c_void_p]),
     "strom_config_set": (C.c_int, [C.c_char_p, C.c_char_p]),
     "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "strom_engine_reset": (C.c_int, []),

@@ -115,6 +115,16 @@ def fault_inject(fail_at: int = 0, err: int = _errno.EIO, short_at: int = 0,
     N.lib().strom_fault_inject(fail_at, err, short_at, short_bytes, delay_us)
 
 
+def ingest_info(device: int = 0) -> Optional[dict]:
+    """Counters of the device's HBM ingest grid (the persistent GPU kernel that
+    pulls staged reads into HBM), or None when it cannot run there."""
+    out = np.zeros(4, dtype=np.uint64)
+    if N.lib().strom_ingest_info(device, out.ctypes.data) < 0:
+        return None
+    return dict(available=bool(out[0]), launches=int(out[1]), posted=int(out[2]),
+                outstanding=int(out[3]))
+
+
 def resident_bytes(fd: int, offset: int = 0, length: int = 1 << 62) -> int:
     return _check(N.lib().strom_resident_bytes(fd, offset, length), "resident_bytes")
 

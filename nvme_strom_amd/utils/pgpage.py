@@ -24,6 +24,8 @@ HEAP_XMAX_LOCK_ONLY = 0x0080
 HEAP_XMIN_COMMITTED = 0x0100
 HEAP_XMIN_INVALID = 0x0200
 HEAP_XMAX_INVALID = 0x0800
+HEAP_XMIN_FROZEN = HEAP_XMIN_COMMITTED | HEAP_XMIN_INVALID   # VACUUM FREEZE / COPY FREEZE
+PD_ALL_VISIBLE = 0x0004
 LP_UNUSED, LP_NORMAL, LP_REDIRECT, LP_DEAD = 0, 1, 2, 3
 VISIBLE = HEAP_XMIN_COMMITTED | HEAP_XMAX_INVALID
 
@@ -46,8 +48,11 @@ def checksum(page: bytes, blkno: int) -> int:
 
 
 def build_page(tuples: Sequence[bytes], blkno: int = 0, page_sz: int = 8192,
-               with_checksum: bool = True, lp_flags: Optional[Sequence[int]] = None) -> bytes:
-    """Heap page with the given tuples (each a full tuple incl. header)."""
+               with_checksum: bool = True, lp_flags: Optional[Sequence[int]] = None,
+               all_visible: bool = False) -> bytes:
+    """Heap page with the given tuples (each a full tuple incl. header).
+    ``all_visible`` sets PD_ALL_VISIBLE in pd_flags (every tuple visible to
+    every snapshot, hint bits or not)."""
     page = bytearray(page_sz)
     upper = page_sz
     lps = []
@@ -62,35 +67,73 @@ def build_page(tuples: Sequence[bytes], blkno: int = 0, page_sz: int = 8192,
     for i, lp in enumerate(lps):
         struct.pack_into("<I", page, SIZE_OF_PAGE_HEADER + 4 * i, lp)
     # pd_lsn, pd_checksum, pd_flags, pd_lower, pd_upper, pd_special, pd_psv, pd_prune_xid
-    struct.pack_into("<QHHHHHHI", page, 0, 1, 0, 0, lower, upper, page_sz, page_sz | 4, 0)
+    flags = PD_ALL_VISIBLE if all_visible else 0
+    struct.pack_into("<QHHHHHHI", page, 0, 1, 0, flags, lower, upper, page_sz, page_sz | 4, 0)
     if with_checksum:
         struct.pack_into("<H", page, 8, checksum(bytes(page), blkno))
     return bytes(page)
 
 
 def int_tuples(values: Iterable[int], width: int = 8, invisible: Iterable[int] = (),
-               pad: int = 0) -> List[bytes]:
-    """One fixed-width int column (+ ``pad`` filler bytes) per tuple."""
-    inv = set(invisible)
+               pad: int = 0, frozen: Iterable[int] = (), nohint: Iterable[int] = ()) -> List[bytes]:
+    """One fixed-width int column (+ ``pad`` filler bytes) per tuple.
+
+    Row i carries: xmin aborted (``invisible``), xmin frozen + xmax invalid
+    (``frozen``), no hint bits at all (``nohint``: visible only on an
+    all-visible page), else xmin committed + xmax invalid."""
+    inv, frz, noh = set(invisible), set(frozen), set(nohint)
     fmt = "<q" if width == 8 else "<i"
     out = []
     for i, v in enumerate(values):
-        mask = (HEAP_XMIN_INVALID | HEAP_XMAX_INVALID) if i in inv else VISIBLE
+        if i in inv:
+            mask = HEAP_XMIN_INVALID | HEAP_XMAX_INVALID
+        elif i in frz:
+            mask = HEAP_XMIN_FROZEN | HEAP_XMAX_INVALID
+        elif i in noh:
+            mask = 0
+        else:
+            mask = VISIBLE
         out.append(tuple_bytes(struct.pack(fmt, v) + b"\xAB" * pad, infomask=mask))
     return out
 
 
 def build_table(values: np.ndarray, per_page: int, width: int = 8, page_sz: int = 8192,
                 with_checksum: bool = True, invisible_every: int = 0,
-                blkno_base: int = 0) -> bytes:
-    """A relation of pages, ``per_page`` int tuples each."""
+                blkno_base: int = 0, frozen_every: int = 0,
+                all_visible_every: int = 0) -> bytes:
+    """A relation of pages, ``per_page`` int tuples each.
+
+    ``frozen_every``: every k-th row is frozen (both xmin hint bits).
+    ``all_visible_every``: every k-th page has PD_ALL_VISIBLE set and its
+    rows carry no hint bits (VACUUM set the flag, nobody hinted the rows)."""
     pages = []
     for p, i0 in enumerate(range(0, len(values), per_page)):
         chunk = values[i0:i0 + per_page]
-        inv = [j for j in range(len(chunk)) if invisible_every and (i0 + j) % invisible_every == 0]
-        pages.append(build_page(int_tuples(chunk.tolist(), width, inv), blkno_base + p, page_sz,
-                                with_checksum))
+        allvis = bool(all_visible_every) and p % all_visible_every == 0
+        rows = range(len(chunk))
+        if allvis:
+            inv, frz, noh = [], [], list(rows)
+        else:
+            inv = [j for j in rows if invisible_every and (i0 + j) % invisible_every == 0]
+            frz = [j for j in rows if frozen_every and (i0 + j) % frozen_every == 1 % frozen_every
+                   and j not in inv]
+            noh = []
+        pages.append(build_page(int_tuples(chunk.tolist(), width, inv, frozen=frz, nohint=noh),
+                                blkno_base + p, page_sz, with_checksum, all_visible=allvis))
     return b"".join(pages)
+
+
+def tuple_visible(infomask: int, pd_flags: int) -> bool:
+    """Hint-bit visibility as the GPU scanner applies it (no clog access):
+    every tuple of a PD_ALL_VISIBLE page is visible (reference
+    pgsql/nvme_strom.c:870-891 sends such pages to DMA unchecked); else
+    xmin must be known committed (HEAP_XMIN_COMMITTED, which a frozen xmin
+    also carries) and xmax invalid or lock-only."""
+    if pd_flags & PD_ALL_VISIBLE:
+        return True
+    if not infomask & HEAP_XMIN_COMMITTED:
+        return False
+    return bool(infomask & (HEAP_XMAX_INVALID | HEAP_XMAX_LOCK_ONLY))
 
 
 def host_scan(data: bytes, page_sz: int = 8192, skip_invisible: bool = False,
@@ -121,11 +164,8 @@ def host_scan(data: bytes, page_sz: int = 8192, skip_invisible: bool = False,
                 continue
             infomask, = struct.unpack_from("<H", page, off + 20)
             hoff = page[off + 22]
-            if skip_invisible:
-                if not ((infomask & HEAP_XMIN_COMMITTED) and not (infomask & HEAP_XMIN_INVALID)):
-                    continue
-                if not ((infomask & HEAP_XMAX_INVALID) or (infomask & HEAP_XMAX_LOCK_ONLY)):
-                    continue
+            if skip_invisible and not tuple_visible(infomask, flags):
+                continue
             if attr_off >= 0:
                 at = hoff + attr_off
                 if infomask & HEAP_HASNULL or at + attr_width > ln:

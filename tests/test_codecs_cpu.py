@@ -79,3 +79,41 @@ def test_pg_page_builder_and_checksum():
     # filter on the int8 column
     items, _ = pgpage.host_scan(data, attr_off=0, attr_width=8, lo=10, hi=19)
     assert len(items) == 10
+
+
+def test_pg_visibility_frozen_and_all_visible():
+    """Frozen rows (xmin COMMITTED|INVALID = 0x0300) are visible; rows with no
+    hint bits are visible only on a PD_ALL_VISIBLE page (reference
+    pgsql/nvme_strom.c:870-891 takes such pages without per-tuple checks)."""
+    vals = np.arange(300, dtype=np.int64)
+    # 3 pages of 100; page 0 all-visible (rows unhinted), rows 1,4,7.. frozen
+    data = pgpage.build_table(vals, per_page=100, width=8, frozen_every=3,
+                              all_visible_every=3, invisible_every=10)
+    flags = [int.from_bytes(data[p * 8192 + 10:p * 8192 + 12], "little") for p in range(3)]
+    assert flags == [pgpage.PD_ALL_VISIBLE, 0, 0]
+    items, status = pgpage.host_scan(data, skip_invisible=True, verify_checksum=True)
+    assert status == [0, 0, 0]
+    rows = {(it >> 16) * 100 + (it & 0xffff) - 1 for it in items}
+    # page 0: every row although none carries a hint bit
+    assert all(r in rows for r in range(100))
+    # pages 1-2: invisible rows (every 10th) dropped, frozen rows kept
+    for r in range(100, 300):
+        assert (r in rows) == (r % 10 != 0), r
+    frozen = [r for r in range(100, 300) if r % 3 == 1 and r % 10 != 0]
+    assert frozen and all(r in rows for r in frozen)
+    # the same page without PD_ALL_VISIBLE: unhinted rows are not provably visible
+    noflag = bytearray(data)
+    noflag[10:12] = b"\0\0"
+    items2, _ = pgpage.host_scan(bytes(noflag), skip_invisible=True)
+    assert not any((it >> 16) == 0 for it in items2)
+
+
+def test_pg_tuple_visible_rules():
+    V = pgpage.tuple_visible
+    assert V(pgpage.HEAP_XMIN_COMMITTED | pgpage.HEAP_XMAX_INVALID, 0)
+    assert V(pgpage.HEAP_XMIN_FROZEN | pgpage.HEAP_XMAX_INVALID, 0)
+    assert V(pgpage.HEAP_XMIN_COMMITTED | pgpage.HEAP_XMAX_LOCK_ONLY, 0)
+    assert not V(pgpage.HEAP_XMIN_INVALID | pgpage.HEAP_XMAX_INVALID, 0)   # aborted
+    assert not V(pgpage.HEAP_XMAX_INVALID, 0)                               # xmin unknown
+    assert not V(pgpage.HEAP_XMIN_COMMITTED, 0)                             # deleted / unknown xmax
+    assert V(0, pgpage.PD_ALL_VISIBLE)

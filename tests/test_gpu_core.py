@@ -98,16 +98,78 @@ def test_load_file_end_to_end(S, tmp_path, backend):
 
 @pytest.mark.parametrize("coalesce", [0, 1])
 def test_worker_copy_coalescing(S, tmp_path, coalesce):
-    """128 KiB requests through the SDMA path (past the 64 KiB BAR cut) land
-    byte-exact whether adjacent staged copies are merged or not."""
+    """128 KiB requests through the SDMA path (ingest grid off, past the
+    64 KiB BAR cut) land byte-exact whether adjacent staged copies are merged
+    or not."""
     from nvme_strom_amd.tensor import load_file
-    S.configure(max_request=128 << 10, coalesce=coalesce)
+    S.configure(max_request=128 << 10, coalesce=coalesce, ingest=0)
     try:
         p, data = _mkfile(tmp_path, (24 << 20) + 8192, seed=9)
         t = load_file(p, device="cuda", chunk_sz=1 << 16, window=8 << 20)
         assert torch.equal(t.cpu(), torch.from_numpy(data))
     finally:
-        S.configure(max_request=1 << 20, coalesce=1)
+        S.configure(max_request=1 << 20, coalesce=1, ingest=1)
+
+
+@pytest.mark.parametrize("req", [4096, 16384, 65536, 262144, 1 << 20, 4 << 20])
+def test_ingest_grid_request_sizes(S, tmp_path, req):
+    """The GPU ingest grid pulls staged reads into HBM byte-exact at every
+    request size (pieces of ingest_piece bytes).  Two files with different
+    bytes go through the same pinned staging slots one after the other, so a
+    stale GPU-cached copy of a refilled slot would show as a mismatch."""
+    from nvme_strom_amd.ops import verify as V
+    from nvme_strom_amd.tensor import load_file
+    S.configure(max_request=req, ingest=1, workers=4)
+    before = S.ingest_info(0)
+    assert before and before["available"]
+    try:
+        for seed in (21, 22):
+            p, data = _mkfile(tmp_path, (12 << 20) + 4096, seed=seed)
+            t = load_file(p, device="cuda", chunk_sz=min(req, 1 << 16), window=4 << 20)
+            assert torch.equal(t.cpu(), torch.from_numpy(data)), seed
+            assert V.crc32c(t) == S.crc32c_host(data.tobytes())
+        after = S.ingest_info(0)
+        assert after["posted"] >= before["posted"] + (24 << 20) // max(req, 256 << 10) // 2
+        assert after["outstanding"] == 0
+    finally:
+        S.configure(max_request=1 << 20, ingest=1)
+
+
+def test_ingest_grid_stops_when_idle(S, tmp_path):
+    """A device-wide synchronize returns once the engine is idle: the ingest
+    grid is a persistent kernel, so the workers stop it before sleeping."""
+    import time
+    from nvme_strom_amd.tensor import load_file
+    S.configure(ingest=1)
+    p, data = _mkfile(tmp_path, 8 << 20, seed=23)
+    t = load_file(p, device="cuda", chunk_sz=1 << 16, window=2 << 20)
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 5.0
+    assert torch.equal(t.cpu(), torch.from_numpy(data))
+
+
+def test_pread_gpu_visible_to_next_kernel(S, tmp_path):
+    """Posted HDP flush (hdp_sync=0): bytes stored through the BAR by
+    pread_gpu are seen by a kernel launched right after it returns — 1000
+    distinct 4 KiB offsets, each checked by its own CRC kernel."""
+    from nvme_strom_amd.ops import verify as V
+    from nvme_strom_amd.tensor import HbmBuffer
+    S.configure(hdp_sync=0, bar_map=1)
+    n = 1000
+    p, data = _mkfile(tmp_path, 16 << 20, seed=31)
+    fd = os.open(p, os.O_RDONLY)
+    offs = np.random.default_rng(3).choice((16 << 20) // 4096, n, replace=False) * 4096
+    crcs = []
+    with HbmBuffer(n * 4096, "cuda") as hb:
+        for i, off in enumerate(offs.tolist()):
+            assert S.pread_gpu(hb.handle, i * 4096, fd, off, 4096) == 4096
+            crcs.append(V.crc32c_chunks(hb.tensor[i * 4096:(i + 1) * 4096], 4096))
+        got = [int(V.u32(c)[0]) for c in crcs]
+    os.close(fd)
+    ref = [S.crc32c_host(data[o:o + 4096].tobytes()) for o in offs.tolist()]
+    bad = [i for i in range(n) if got[i] != ref[i]]
+    assert not bad, f"{len(bad)} stale reads, first at {bad[:5]}"
 
 
 def test_read_chunks_hybrid_reorder(S, tmp_path):

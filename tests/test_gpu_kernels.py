@@ -39,6 +39,42 @@ def test_heap_scan_matches_host(dev):
     assert npages > 6
 
 
+def test_heap_scan_frozen_and_all_visible(dev):
+    """Frozen rows and PD_ALL_VISIBLE pages (rows without hint bits) are kept
+    by skip_invisible, like the host reference (frozen rows were
+    dropped)."""
+    from nvme_strom_amd.ops.heapscan import heap_scan
+    from nvme_strom_amd.utils import pgpage
+    vals = np.arange(6000, dtype=np.int64)
+    data = pgpage.build_table(vals, per_page=150, width=8, frozen_every=4, all_visible_every=5,
+                              invisible_every=11)
+    t = _t(data, dev)
+    for kw in [dict(skip_invisible=True), dict(skip_invisible=True, verify_checksum=True,
+                                               attr_off=0, attr_width=8, lo=100, hi=4000)]:
+        r = heap_scan(t, **kw)
+        ref_items, ref_status = pgpage.host_scan(data, **kw)
+        assert list(r.sorted_items()) == ref_items, kw
+        assert list(r.page_status.cpu().numpy()) == ref_status, kw
+    r = heap_scan(t, skip_invisible=True)
+    assert r.count == 6000 - len([i for i in range(6000) if i % 11 == 0 and (i // 150) % 5])
+
+
+@pytest.mark.parametrize("page_sz", [4096, 16384, 32768])
+def test_heap_scan_other_page_sizes(dev, page_sz):
+    from nvme_strom_amd.ops.heapscan import heap_scan
+    from nvme_strom_amd.utils import pgpage
+    vals = np.arange(20000, dtype=np.int64) - 7000
+    per = page_sz // 48
+    data = pgpage.build_table(vals, per_page=per, width=8, page_sz=page_sz, invisible_every=13,
+                              frozen_every=6)
+    kw = dict(page_sz=page_sz, skip_invisible=True, verify_checksum=True, attr_off=0,
+              attr_width=8, lo=-50, hi=9000)
+    r = heap_scan(_t(data, dev), **kw)
+    ref_items, ref_status = pgpage.host_scan(data, **kw)
+    assert list(r.sorted_items()) == ref_items
+    assert list(r.page_status.cpu().numpy()) == ref_status
+
+
 def test_heap_scan_int4_column(dev):
     from nvme_strom_amd.ops.heapscan import heap_scan
     from nvme_strom_amd.utils import pgpage
