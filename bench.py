@@ -236,6 +236,16 @@ def main() -> int:
         S.evict_file(fd)
         raw_p50 = float(np.percentile(S.pread_raw_latency(fd, offs)[50:], 50)) / 1e3
 
+    # the same QD1 reads through the v0.6 ioctl pair (SSD2GPU + WAIT: task
+    # table, residency probe, planner), and the host primitive costs below both
+    ioctl_p50 = float("nan")
+    costs = {}
+    if a.lat_samples:
+        S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
+        ioctl_p50 = float(np.percentile(S.ioctl_latency(buf.handle, 0, fd, offs)[50:], 50)) / 1e3
+        costs = S.host_costs(fd)
+
     # VFS control: pread -> pinned -> HtoD, same window
     S.evict_file(fd)
     vt = vfs_control(path, 0, W, buf.tensor, segment_sz=a.segment_mib << 20, nr_segments=a.depth)
@@ -265,6 +275,8 @@ def main() -> int:
         "p50_4k_lat_us": round(p50, 2),
         "p99_4k_lat_us": round(p99, 2),
         "p50_4k_lat_python_us": round(p50_py, 2),
+        "p50_4k_lat_ioctl_us": round(ioctl_p50, 2),
+        "host_costs_ns": costs,
         "engine_io_p50_us": round(S.hist_percentile(hist["io_ns"], 50) / 1e3, 2),
         "raw_odirect_4k_p50_us": round(raw_p50, 2),
         "storage_4k_p50_us": round(raw_p50, 2),

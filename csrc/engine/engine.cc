@@ -337,6 +337,42 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   return 0;
 }
 
+long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off,
+                        uint64_t len) {
+  if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
+  auto gmap = gpu_registry().get(handle);
+  if (!gmap) return -ENOENT;
+  if (gmap->map_offset + offset + len > gmap->map_length) return -ERANGE;
+  int err = 0;
+  auto f = open_file(fd, &err);
+  if (!f) return err;
+  phase_mark(0);
+  const uint64_t size = (uint64_t)f->fc.size;
+  if (file_off >= size) return -ERANGE;
+  phase_mark(1);
+  long status = 0;
+  IoReq r;
+  r.fd = f->fd_direct;
+  r.fd_buffered = f->fd_buffered;
+  r.off = file_off;
+  r.len = (uint32_t)len;
+  r.valid = (uint32_t)std::min<uint64_t>(len, size - file_off);
+  if (gmap->device < 0) r.host_dst = (uint8_t *)(gmap->va + offset);  // emulated HBM
+  else r.gpu_dst = gmap->va + offset;
+  r.device = gmap->device;
+  r.gmap = gmap.get();
+  r.status_out = &status;
+  r.t_submit_ns = mono_ns();
+  r.t_submit_tsc = tsc_now();
+  gmap->inflight.fetch_add(1);
+  stats().inflight_inc();
+  stats().nr_setup_prps.fetch_add(1, std::memory_order_relaxed);
+  phase_mark(2);
+  io_->run_inline(r);
+  if (status) return status;
+  return (long)len;
+}
+
 int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   a->nr_ram2ram = a->nr_ssd2ram = a->nr_dma_submit = a->nr_dma_blocks = 0;
   a->dma_task_id = 0;
@@ -578,6 +614,18 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
                      uint64_t file_off, uint64_t len) {
   if ((file_off | len) & 4095) return -EINVAL;
   if (len == 0) return 0;
+  {
+    int kfd;
+    {
+      std::lock_guard<std::mutex> g(g_sess_mu);
+      kfd = kernel_fd();
+    }
+    if (kfd < 0) {
+      // userspace provider: task-less synchronous path
+      const long r = engine().pread_sync(handle, offset, fd, file_off, len);
+      if (r != -EAGAIN) return r;
+    }
+  }
   // one chunk per request-sized piece when aligned, else 4 KiB chunks
   uint32_t chunk = 4096;
   for (uint32_t c = config().max_request; c > 4096; c >>= 1)
@@ -673,6 +721,34 @@ int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd
   return 0;
 }
 
+int strom_ioctl_lat(int session, unsigned long handle, size_t offset, int fd,
+                    const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out) {
+  if (len == 0 || (len & 4095) || len > (1u << 20)) return -EINVAL;
+  uint32_t ids[256];
+  const uint32_t chunk = 4096, nch = (uint32_t)(len / chunk);
+  std::vector<char> wb(len);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t t0 = mono_ns();
+    for (uint32_t k = 0; k < nch; ++k) ids[k] = (uint32_t)(file_offs[i] / chunk + k);
+    strom_memcpy_ssd2gpu a{};
+    a.handle = handle;
+    a.offset = offset;
+    a.file_desc = fd;
+    a.nr_chunks = nch;
+    a.chunk_sz = chunk;
+    a.chunk_ids = ids;
+    a.wb_buffer = wb.data();
+    int rc = strom_ioctl(session, STROM_IOCTL__MEMCPY_SSD2GPU, &a);
+    if (rc) return rc;
+    strom_memcpy_wait w{};
+    w.dma_task_id = a.dma_task_id;
+    rc = strom_ioctl(session, STROM_IOCTL__MEMCPY_WAIT, &w);
+    ns_out[i] = mono_ns() - t0;
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int fd,
                            const uint64_t *file_offs, uint32_t n, uint64_t len,
                            uint64_t *phase_ns) {
@@ -713,6 +789,35 @@ int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t 
   free(buf);
   close(d);
   return rc;
+}
+
+// Host primitive costs on this machine (ns per call, mean of n): what the
+// 4 KiB latency path is made of below the engine's own logic.
+//   0 clock_gettime(MONOTONIC)  1 rdtsc  2 fstat  3 mincore(1 page)
+//   4 getppid (bare syscall)  5 mutex lock+unlock  6 condvar notify (no waiter)
+int strom_host_costs(int fd, uint64_t *out, int n) {
+  if (n <= 0 || fd < 0) return -EINVAL;
+  auto bench = [&](auto &&fn) {
+    const uint64_t t0 = mono_ns();
+    for (int i = 0; i < n; ++i) fn();
+    return (mono_ns() - t0) / (uint64_t)n;
+  };
+  volatile uint64_t sink = 0;
+  timespec ts;
+  out[0] = bench([&] { clock_gettime(CLOCK_MONOTONIC, &ts); sink += ts.tv_nsec; });
+  out[1] = bench([&] { sink += __rdtsc(); });
+  struct stat st;
+  out[2] = bench([&] { fstat(fd, &st); sink += st.st_size; });
+  void *m = mmap(nullptr, 4096, PROT_READ, MAP_SHARED, fd, 0);
+  unsigned char v = 0;
+  out[3] = m == MAP_FAILED ? 0 : bench([&] { mincore(m, 4096, &v); sink += v; });
+  if (m != MAP_FAILED) munmap(m, 4096);
+  out[4] = bench([&] { sink += (uint64_t)getppid(); });
+  std::mutex mu;
+  out[5] = bench([&] { std::lock_guard<std::mutex> g(mu); sink += 1; });
+  std::condition_variable cv;
+  out[6] = bench([&] { cv.notify_all(); });
+  return 0;
 }
 
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset) {

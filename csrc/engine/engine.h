@@ -194,6 +194,7 @@ struct GpuMapping {
   void bar_flush(const uint8_t *last) const;
   ~GpuMapping();
   bool detached = false;
+  std::atomic<bool> draining{false};  // an UNMAP waits for inflight == 0
   std::mutex mu;
   std::condition_variable cv;
 };
@@ -317,6 +318,7 @@ struct IoReq {
   uint64_t t_submit_ns = 0;
   uint64_t t_submit_tsc = 0;
   GpuMapping *gmap = nullptr; // inflight counter owner
+  long *status_out = nullptr; // task-less synchronous request: status lands here
 };
 
 class IoEngine {
@@ -422,6 +424,11 @@ class Engine {
   Engine();
   ~Engine();
   int ioctl(int session, unsigned long cmd, void *arg);
+  // Synchronous read of [file_off, file_off+len) into a mapped GPU range on
+  // the caller's thread: no task, no residency probe (O_DIRECT reads see
+  // dirty page-cache data: the kernel writes the range back first).  The
+  // 4 KiB latency path of strom_pread_gpu.  -EAGAIN: use the task path.
+  long pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off, uint64_t len);
   IoEngine &io() { return *io_; }
   struct OpenFile;
 

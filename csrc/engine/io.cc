@@ -137,12 +137,13 @@ void finish_request(IoReq &r, long status) {
   st.clk_ssd2gpu.fetch_add(tsc_now() - r.t_submit_tsc, std::memory_order_relaxed);
   st.inflight_dec();
   if (r.gmap) {
-    if (r.gmap->inflight.fetch_sub(1) == 1) {
+    if (r.gmap->inflight.fetch_sub(1) == 1 && r.gmap->draining.load()) {
       std::lock_guard<std::mutex> g(r.gmap->mu);
       r.gmap->cv.notify_all();
     }
   }
-  tasks().put(r.task, status);
+  if (r.task) tasks().put(r.task, status);
+  else if (r.status_out) *r.status_out = status;
 }
 
 // read [off, off+len) fully; returns bytes read or -errno.
@@ -655,10 +656,11 @@ void IoEngine::run_inline(IoReq &r) {
     phase_mark(6);
     return;
   }
+  const bool ing_ok = config().ingest;
   if (c.cap < r.len) {
     size_t cap = std::max<size_t>(r.len, 64u << 10);
-    uint8_t *b = (uint8_t *)hip::host_alloc_thp(cap);
-    if (!b) b = (uint8_t *)hip::host_alloc(cap);
+    uint8_t *b = (uint8_t *)hip::host_alloc_thp(cap, ing_ok);
+    if (!b) b = (uint8_t *)hip::host_alloc(cap, ing_ok);
     if (!b) {
       finish_request(r, -ENOMEM);
       return;
@@ -671,10 +673,22 @@ void IoEngine::run_inline(IoReq &r) {
   if (tl_phase) tl_phase[3] = t1;
   stats().io_ns.add(t1 - t0);
   long status = finalize_read(r, c.buf, len, got);
+  Ingest *ing = nullptr;
+  uint64_t first = 0;
+  uint32_t nseq = 0;
   if (status == 0 && r.len <= config().bar_max && r.gmap &&
       r.gmap->bar_write(r.gpu_dst, c.buf, r.len)) {
     stats().copy_ns.add(mono_ns() - t1);
     stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+  } else if (status == 0 && ing_ok && r.gmap && (ing = Ingest::get(r.device)) &&
+             ing->post_many(c.buf, r.gpu_dst, r.len, config().ingest_piece, &first, &nseq)) {
+    // past the BAR cut: the ingest grid pulls the bytes (no HIP call here)
+    for (uint32_t k = 0; k < nseq; ++k)
+      while (!ing->is_done(first + k)) _mm_pause();
+    ing->retired(nseq);
+    phase_mark(4);
+    stats().copy_ns.add(mono_ns() - t1);
+    stats().nr_debug[0].fetch_add(nseq, std::memory_order_relaxed);
   } else if (status == 0) {
     if (c.dev != r.device) {
       (void)hipSetDevice(r.device);

@@ -132,8 +132,10 @@ int GpuRegistry::unmap(unsigned long handle) {
     m = it->second;
     maps_.erase(it);
   }
-  // wait for in-flight DMA targeting the range (free-callback semantics)
+  // wait for in-flight DMA targeting the range (free-callback semantics);
+  // completions notify only while someone drains
   std::unique_lock<std::mutex> g(m->mu);
+  m->draining.store(true);  // seq_cst: pairs with the completion's inflight RMW + load
   m->cv.wait(g, [&] { return m->inflight.load() == 0; });
   m->detached = true;
   return 0;

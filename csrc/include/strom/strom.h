@@ -42,6 +42,11 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
  * Returns 0 or the first failure's -errno. */
 int strom_pread_gpu_lat(int session, unsigned long handle, size_t offset, int fd,
                         const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out);
+/* The same QD1 probe through the ioctl pair a v0.6 client issues
+ * (MEMCPY_SSD2GPU of len/4096 chunks + MEMCPY_WAIT per read): task table,
+ * residency probe and planner included.  len <= 1 MiB. */
+int strom_ioctl_lat(int session, unsigned long handle, size_t offset, int fd,
+                    const uint64_t *file_offs, uint32_t n, uint64_t len, uint64_t *ns_out);
 /* The same probe split into phases: phase_ns[i*STROM_NPHASE + k] is the time
  * from the start of read i to the end of phase k, 0 when k was not reached:
  *   0 file lookup   1 chunk plan (residency probe + merge)   2 task + requests
@@ -55,6 +60,11 @@ int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int
  * into aligned host memory (no engine, no HBM), ns per read. */
 int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t len,
                         uint64_t *ns_out);
+
+/* Host primitive costs (ns per call, mean of n) on this machine, for the
+ * latency breakdown: {clock_gettime, rdtsc, fstat(fd), mincore 1 page of fd,
+ * bare syscall, mutex lock+unlock, condvar notify} -> out[7]. */
+int strom_host_costs(int fd, uint64_t *out, int n);
 
 /* Storage ceiling for a block size, no engine: `threads` io_uring rings,
  * each `qd` deep, O_DIRECT reads of `block` bytes at random aligned

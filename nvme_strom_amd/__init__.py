@@ -19,7 +19,7 @@ from .api import (  # noqa: F401
     check_file, config_get, config_set, configure, crc32c_host, engine_reset, evict_file,
     fault_inject, hist_percentile, info_gpu_memory, list_gpu_memory, map_gpu_memory,
     memcpy_ssd2gpu, memcpy_ssd2ram, memcpy_wait, pread_gpu, pread_gpu_latency, provider,
-    PHASES, ingest_info, phase_breakdown, pread_gpu_phases, pread_raw_latency, raw_read_rate,
+    PHASES, host_costs, ingest_info, ioctl_latency, phase_breakdown, pread_gpu_phases, pread_raw_latency, raw_read_rate,
     resident_bytes, session,
     stat_hist, stat_info, unmap_gpu_memory, version,
 )

@@ -151,6 +151,8 @@ _SIGS = {
                                    C.c_uint64]),
     "strom_pread_gpu_lat": (C.c_int, [C.c_int, C.c_ulong, C.c_size_t, C.c_int, C.c_void_p,
                                       C.c_uint32, C.c_uint64, C.c_void_p]),
+    "strom_ioctl_lat": (C.c_int, [C.c_int, C.c_ulong, C.c_size_t, C.c_int, C.c_void_p,
+                                  C.c_uint32, C.c_uint64, C.c_void_p]),
     "strom_pread_gpu_phases": (C.c_int, [C.c_int, C.c_ulong, C.c_size_t, C.c_int, C.c_void_p,
                                          C.c_uint32, C.c_uint64, C.c_void_p]),
     "strom_pread_raw_lat": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p]),
@@ -159,6 +161,7 @@ _SIGS = {
     "strom_export_dmabuf": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_int),
                                       C.POINTER(C.c_uint64)]),
     "strom_ingest_info": (C.c_int, [C.c_int, C.c_void_p]),
+    "strom_host_costs": (C.c_int, [C.c_int, C.c_void_p, C.c_int]),
     "strom_config_set": (C.c_int, [C.c_char_p, C.c_char_p]),
     "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "strom_engine_reset": (C.c_int, []),

@@ -125,6 +125,16 @@ def ingest_info(device: int = 0) -> Optional[dict]:
                 outstanding=int(out[3]))
 
 
+HOST_COSTS = ("clock_gettime", "rdtsc", "fstat", "mincore", "syscall", "mutex", "cv_notify")
+
+
+def host_costs(fd: int, n: int = 20000) -> dict:
+    """ns per call of the host primitives under the 4 KiB latency path."""
+    out = np.zeros(len(HOST_COSTS), dtype=np.uint64)
+    _check(N.lib().strom_host_costs(fd, out.ctypes.data, n), "host_costs")
+    return {k: int(v) for k, v in zip(HOST_COSTS, out)}
+
+
 def resident_bytes(fd: int, offset: int = 0, length: int = 1 << 62) -> int:
     return _check(N.lib().strom_resident_bytes(fd, offset, length), "resident_bytes")
 
@@ -315,6 +325,18 @@ def pread_gpu_latency(handle: int, offset: int, fd: int, file_offs, length: int 
     out = np.zeros(len(offs), dtype=np.uint64)
     _check(s.lib.strom_pread_gpu_lat(s.sid, handle, offset, fd, offs.ctypes.data, len(offs),
                                      length, out.ctypes.data), "pread_gpu_lat")
+    return out
+
+
+def ioctl_latency(handle: int, offset: int, fd: int, file_offs, length: int = 4096,
+                  sess: Optional[Session] = None) -> np.ndarray:
+    """QD1 probe through MEMCPY_SSD2GPU + MEMCPY_WAIT per read (the v0.6
+    client's call pair), native loop.  -> ns per read."""
+    s = sess or session()
+    offs = np.ascontiguousarray(file_offs, dtype=np.uint64)
+    out = np.zeros(len(offs), dtype=np.uint64)
+    _check(s.lib.strom_ioctl_lat(s.sid, handle, offset, fd, offs.ctypes.data, len(offs),
+                                 length, out.ctypes.data), "ioctl_lat")
     return out
 
 

@@ -355,29 +355,64 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
     return st
 
 
+def _atomic_write(path: str, write) -> None:
+    """Crash-safe replace of ``path``: unique temp file in the same directory
+    (two writers never share it), fsync, rename, then fsync the directory so
+    the rename itself survives a crash."""
+    import tempfile
+    d = os.path.dirname(os.path.abspath(path))
+    fd, tmp = tempfile.mkstemp(prefix=os.path.basename(path) + ".", suffix=".tmp", dir=d)
+    try:
+        with os.fdopen(fd, "wb") as f:
+            write(f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, path)
+    except BaseException:
+        try:
+            os.unlink(tmp)
+        except OSError:
+            pass
+        raise
+    dfd = os.open(d, os.O_RDONLY)
+    try:
+        os.fsync(dfd)
+    finally:
+        os.close(dfd)
+
+
 class ResumableScan:
     """Checkpointed scan: the relation is scanned in block ranges of
-    ``step_blocks``; after each range the qualifying items and the per-scan
-    counters are written atomically (tmp file + rename) to ``path`` (an .npz
-    holding only arrays; loaded with ``allow_pickle=False``).  A new instance
-    over the same checkpoint continues at the first unscanned block, so each
-    block's tuples are reported exactly once across interruptions.
+    ``step_blocks``; after each range its qualifying items go to a file of
+    their own (``<path>.r<b0>-<b1>.npy``) and then the checkpoint ``path`` (an
+    .npz holding only arrays, loaded with ``allow_pickle=False``) is replaced
+    with the new cursor, counters and range list.  Every write is a unique
+    temp file + fsync + rename + directory fsync, so checkpoint I/O per range
+    is O(range) — not O(everything so far) — and a crash leaves either the
+    old or the new checkpoint.  A new instance over the same checkpoint
+    continues at the first unscanned block, so each block's tuples are
+    reported exactly once across interruptions.
 
     ``scan`` is any ``(b0, b1) -> ScanResult`` — e.g.
     ``lambda b0, b1: HeapRelationScan(...).run(4, blocks=(b0, b1))`` or the
-    ``cpu_scan`` path.  ``key`` identifies the relation + predicate; resuming
-    a checkpoint written under a different key raises ``ValueError``.
+    ``cpu_scan`` path.  ``key`` (required, non-empty) identifies the relation,
+    predicate and scan options — :func:`scan_key` builds one; resuming a
+    checkpoint written under a different key, block count or step raises
+    ``ValueError``.
     """
 
     _COUNTERS = ("pages", "bad_pages", "nr_ram", "nr_ssd", "nr_dma_submit", "nr_dma_blocks",
                  "chunks")
 
-    def __init__(self, scan, nblocks: int, path: str, step_blocks: int, key: str = ""):
+    def __init__(self, scan, nblocks: int, path: str, step_blocks: int, key: str):
         if step_blocks <= 0:
             raise ValueError("step_blocks must be positive")
+        if not key:
+            raise ValueError("a non-empty key (relation + predicate + options) is required: "
+                             "see scan_key()")
         self.scan, self.nblocks, self.path, self.step, self.key = scan, nblocks, path, step_blocks, key
         self.next_block = 0
-        self.items: List[np.ndarray] = []
+        self.ranges: List[str] = []          # item files of the finished ranges, in order
         self.counters = dict.fromkeys(self._COUNTERS, 0)
         self.seconds = 0.0
         if os.path.exists(path):
@@ -386,26 +421,37 @@ class ResumableScan:
     def _load(self) -> None:
         with np.load(self.path, allow_pickle=False) as z:
             meta = json.loads(bytes(z["meta"]).decode())
-            items = z["items"].astype(np.uint64)
-        if meta["key"] != self.key or meta["nblocks"] != self.nblocks:
-            raise ValueError(f"checkpoint {self.path} is for {meta['key']!r}/{meta['nblocks']} blocks, "
-                             f"not {self.key!r}/{self.nblocks}")
+        if (meta["key"] != self.key or meta["nblocks"] != self.nblocks
+                or meta.get("step_blocks") != self.step):
+            raise ValueError(f"checkpoint {self.path} is for {meta['key']!r}/{meta['nblocks']} blocks/"
+                             f"step {meta.get('step_blocks')}, not {self.key!r}/{self.nblocks}/{self.step}")
         self.next_block = int(meta["next_block"])
         self.counters.update({k: int(meta[k]) for k in self._COUNTERS})
         self.seconds = float(meta["seconds"])
-        self.items = [items]
+        self.ranges = list(meta["ranges"])
+        d = os.path.dirname(os.path.abspath(self.path))
+        for name in self.ranges:
+            if not os.path.exists(os.path.join(d, name)):
+                raise ValueError(f"checkpoint {self.path}: range file {name} is missing")
 
-    def _save(self) -> None:
-        meta = dict(self.counters, key=self.key, nblocks=self.nblocks, next_block=self.next_block,
-                    seconds=self.seconds)
-        items = np.concatenate(self.items) if self.items else np.zeros(0, np.uint64)
-        tmp = self.path + ".tmp"
-        with open(tmp, "wb") as f:
-            np.savez(f, items=items, meta=np.frombuffer(json.dumps(meta).encode(), np.uint8))
-            f.flush()
-            os.fsync(f.fileno())
-        os.replace(tmp, self.path)
-        self.items = [items]
+    def _range_path(self, name: str) -> str:
+        return os.path.join(os.path.dirname(os.path.abspath(self.path)), name)
+
+    def _save_range(self, b0: int, b1: int, items: np.ndarray) -> str:
+        name = f"{os.path.basename(self.path)}.r{b0}-{b1}.npy"
+        _atomic_write(self._range_path(name), lambda f: np.save(f, items, allow_pickle=False))
+        return name
+
+    def _save_meta(self) -> None:
+        meta = dict(self.counters, key=self.key, nblocks=self.nblocks, step_blocks=self.step,
+                    next_block=self.next_block, seconds=self.seconds, ranges=self.ranges)
+        blob = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+        _atomic_write(self.path, lambda f: np.savez(f, meta=blob))
+
+    def items(self) -> np.ndarray:
+        parts = [np.load(self._range_path(n), allow_pickle=False).astype(np.uint64)
+                 for n in self.ranges]
+        return np.sort(np.concatenate(parts)) if parts else np.zeros(0, np.uint64)
 
     @property
     def done(self) -> bool:
@@ -419,17 +465,42 @@ class ResumableScan:
             b0 = self.next_block
             b1 = min(self.nblocks, b0 + self.step)
             r = self.scan(b0, b1)
-            self.items.append(np.asarray(r.items, np.uint64))
+            self.ranges.append(self._save_range(b0, b1, np.asarray(r.items, np.uint64)))
             for k in self._COUNTERS:
                 self.counters[k] += int(getattr(r, k))
             self.seconds += r.seconds
             self.next_block = b1
-            self._save()
+            self._save_meta()      # the range counts only once the checkpoint names it
             steps += 1
         if not self.done:
             return None
-        items = np.sort(np.concatenate(self.items)) if self.items else np.zeros(0, np.uint64)
-        out = ScanResult(items, seconds=self.seconds)
+        out = ScanResult(self.items(), seconds=self.seconds)
         for k, v in self.counters.items():
             setattr(out, k, v)
         return out
+
+    def remove(self) -> None:
+        """Delete the checkpoint and its range files (after a finished scan)."""
+        for n in self.ranges:
+            try:
+                os.unlink(self._range_path(n))
+            except FileNotFoundError:
+                pass
+        try:
+            os.unlink(self.path)
+        except FileNotFoundError:
+            pass
+
+
+def scan_key(rel: "Relation", cfg: Optional[ScanConfig] = None, attr_off: int = -1,
+             attr_width: int = 8, lo: int = -(1 << 63), hi: int = (1 << 63) - 1) -> str:
+    """Checkpoint key for :class:`ResumableScan`: relation files (path, inode,
+    size, mtime), predicate and the options that change the result."""
+    cfg = cfg or ScanConfig()
+    files = []
+    for p in rel.segments:
+        st = os.stat(p)
+        files.append(f"{os.path.abspath(p)}:{st.st_ino}:{st.st_size}:{st.st_mtime_ns}")
+    return json.dumps(dict(files=files, attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi,
+                           skip_invisible=cfg.skip_invisible,
+                           verify_checksum=cfg.verify_checksum), sort_keys=True)

@@ -147,3 +147,23 @@ def test_cpu_scan_block_range_and_resumable(strom, tmp_path):
     assert c.done and np.array_equal(c.run().items, full.items)
     with pytest.raises(ValueError):
         pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=3, key="other")
+    # a different step size, or no key at all, is refused too
+    with pytest.raises(ValueError):
+        pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=4, key="16385:50-1749")
+    with pytest.raises(ValueError):
+        pg_scan.ResumableScan(scan, rel.nblocks, str(tmp_path / "x.npz"), step_blocks=3, key="")
+    # per-range item files: each holds only its own range's rows
+    names = sorted(c.ranges)
+    assert len(names) == 7 and all(os.path.exists(tmp_path / n) for n in names)
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".tmp")]
+    c.remove()
+    assert not os.path.exists(ck) and not any(os.path.exists(tmp_path / n) for n in names)
+
+
+def test_scan_key_tracks_relation_and_predicate(strom, tmp_path):
+    data = pgpage.build_table(np.arange(300, dtype=np.int64), per_page=100, width=8)
+    rel = pg_scan.Relation.write(str(tmp_path / "16390"), data)
+    k1 = pg_scan.scan_key(rel, attr_off=0, lo=1, hi=5)
+    assert k1 == pg_scan.scan_key(rel, attr_off=0, lo=1, hi=5)
+    assert k1 != pg_scan.scan_key(rel, attr_off=0, lo=1, hi=6)
+    assert k1 != pg_scan.scan_key(rel, pg_scan.ScanConfig(verify_checksum=True), attr_off=0, lo=1, hi=5)
