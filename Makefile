@@ -12,6 +12,9 @@ LDFLAGS  := -shared -fPIC -lpthread -L$(ROCM)/lib -lrocprofiler-sdk-roctx -lhsa-
 
 ENGINE_SRC := $(wildcard csrc/engine/*.cc)
 KERNEL_SRC := $(wildcard csrc/kernels/*.hip)
+# the kernel-free core shared with the kernel module (planner, raid0, PRPs)
+CORE_SRC   := kmod/strom_core.c
+CORE_OBJ   := $(OBJ)/core/strom_core.o
 ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
@@ -20,7 +23,11 @@ all: $(OUT)/libstrom.so tools
 
 tools: $(TOOLS)
 
-$(OBJ)/engine/%.o: csrc/engine/%.cc csrc/engine/engine.h csrc/include/strom/uapi.h csrc/include/strom/strom.h
+$(CORE_OBJ): $(CORE_SRC) kmod/strom_core.h
+	@mkdir -p $(dir $@)
+	gcc -O2 -std=gnu11 -fPIC -Wall -Wextra -Wno-unused-parameter -c $< -o $@
+
+$(OBJ)/engine/%.o: csrc/engine/%.cc csrc/engine/engine.h csrc/include/strom/uapi.h csrc/include/strom/strom.h kmod/strom_core.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(CXXFLAGS) -D__HIP_PLATFORM_AMD__ -c $< -o $@
 
@@ -28,7 +35,7 @@ $(OBJ)/kernels/%.o: csrc/kernels/%.hip csrc/include/strom/strom.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ)
+$(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ) $(CORE_OBJ)
 	@mkdir -p $(OUT)
 	$(HIPCC) $(LDFLAGS) --offload-arch=$(ARCH) -o $@ $^
 
@@ -43,7 +50,7 @@ clean:
 # ---- host-only engine self-test, plain and under sanitizers ---------------
 # The engine's host code builds with g++ (HIP host API only); device kernels
 # are not part of these builds.  GPU sanitizers are not used on this pool.
-SELFTEST_SRC := csrc/tests/engine_selftest.cc $(ENGINE_SRC)
+SELFTEST_SRC := csrc/tests/engine_selftest.cc $(ENGINE_SRC) $(CORE_SRC)
 SELFTEST_FLAGS := -std=c++17 -g -O1 -Icsrc/include -Icsrc/engine -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 SELFTEST_LIBS := -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx -lpthread -Wl,-rpath,$(ROCM)/lib
 

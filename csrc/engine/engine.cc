@@ -514,6 +514,10 @@ int Engine::ioctl(int session, unsigned long cmd, void *arg) {
       return stats().fill((strom_stat_info *)arg);
     case STROM_IOCTL__STAT_HIST:
       return stats().fill_hist((strom_stat_hist *)arg);
+    case STROM_IOCTL__SET_ROUTE:
+      // kernel provider only: this engine reaches md / multipath members
+      // through the block layer (O_DIRECT on the volume)
+      return -EOPNOTSUPP;
     default:
       return -EINVAL;
   }
@@ -887,18 +891,25 @@ int strom_raid0_map(const uint64_t *zone_end, const uint64_t *zone_dev_start,
                     const int *zone_nb_dev, int nzones, uint32_t chunk_sects,
                     const uint64_t *data_offset, int raid_disks, uint64_t sector,
                     uint32_t nr_sects, int *member, uint64_t *member_sector) {
-  Raid0Geometry g;
+  if (nzones <= 0 || nzones > STROM_RAID0_MAX_ZONES || raid_disks <= 0 ||
+      raid_disks > STROM_RAID0_MAX_DISKS)
+    return -EINVAL;
+  strom_raid0 g;
+  memset(&g, 0, sizeof g);
   g.chunk_sects = chunk_sects;
+  g.nzones = (uint32_t)nzones;
+  g.ndisks = (uint32_t)raid_disks;
   for (int z = 0; z < nzones; ++z) {
-    g.zone_end.push_back(zone_end[z]);
-    g.zone_dev_start.push_back(zone_dev_start[z]);
+    g.zone_end[z] = zone_end[z];
+    g.zone_dev_start[z] = zone_dev_start[z];
     // zone z holds the last nb_dev members (smaller members drop out)
-    std::vector<int> devs;
-    for (int d = raid_disks - zone_nb_dev[z]; d < raid_disks; ++d) devs.push_back(d);
-    g.zone_devs.push_back(devs);
+    if (zone_nb_dev[z] <= 0 || zone_nb_dev[z] > raid_disks) return -EINVAL;
+    g.zone_nb_dev[z] = (uint32_t)zone_nb_dev[z];
+    for (int k = 0; k < zone_nb_dev[z]; ++k)
+      g.zone_devs[z][k] = (uint8_t)(raid_disks - zone_nb_dev[z] + k);
   }
-  for (int d = 0; d < raid_disks; ++d) g.data_offset.push_back(data_offset ? data_offset[d] : 0);
-  return g.map(sector, nr_sects, member, member_sector);
+  for (int d = 0; d < raid_disks; ++d) g.data_offset[d] = data_offset ? data_offset[d] : 0;
+  return strom_core_raid0_map(&g, sector, nr_sects, member, member_sector);
 }
 
 }  // extern "C"

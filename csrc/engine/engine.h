@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "strom/strom.h"
+#include "../../kmod/strom_core.h"
 
 namespace strom {
 
@@ -242,15 +243,9 @@ class DmaBufRegistry {
 DmaBufRegistry &dmabuf_registry();
 
 // ------------------------------------------------------- file classifier
-struct Raid0Geometry {
-  uint32_t chunk_sects = 0;                 // 512-B sectors per chunk
-  std::vector<uint64_t> zone_end;           // md sector (exclusive)
-  std::vector<uint64_t> zone_dev_start;     // member sector of zone start
-  std::vector<std::vector<int>> zone_devs;  // member index per zone slot
-  std::vector<uint64_t> data_offset;        // per member
-  // -ESPIPE when [sector, sector+nr) crosses a chunk; -ERANGE past the end.
-  int map(uint64_t sector, uint32_t nr, int *member, uint64_t *msector) const;
-};
+// md raid0 geometry: the C struct of the shared core (kmod/strom_core.h)
+// that both providers remap with.
+using Raid0Geometry = strom_raid0;
 
 struct FileClass {
   dev_t dev = 0;
@@ -265,7 +260,7 @@ struct FileClass {
   int numa_node = -1;
   bool dma64 = true;
   uint64_t part_start_sect = 0;
-  Raid0Geometry raid0;
+  Raid0Geometry raid0{};
   std::vector<std::string> members;
 };
 
@@ -296,8 +291,12 @@ struct PlanParams {
   uint32_t max_request = 1u << 20;
   uint64_t dest_segment = 0;         // 0 = no segment boundary rule
   bool reorder = true;               // SSD2GPU: SSD head / RAM tail
-  const Raid0Geometry *raid0 = nullptr;
+  const Raid0Geometry *raid0 = nullptr;   // split requests at stripe chunks
   uint64_t part_start_sect = 0;
+  // file 4 KiB page -> volume block (4 KiB units); null = identity (the
+  // engine reads by file offset, so merging never needs the device layout)
+  int (*bmap)(void *ctx, uint64_t fblk, uint64_t *dblk) = nullptr;
+  void *bmap_ctx = nullptr;
   // resident pages of [fpos, fpos+len) or -1 unknown; null = never cached
   std::function<long(uint64_t, uint32_t)> resident;
 };

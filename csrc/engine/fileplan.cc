@@ -82,7 +82,8 @@ static const char *fs_name_of(uint64_t magic) {
 }
 
 // Build raid0 zones from sysfs: members sorted by size give the zones
-// (drivers/md/raid0.c create_strip_zones semantics, re-derived).
+// (drivers/md/raid0.c create_strip_zones semantics, re-derived), in the
+// shared core's geometry struct.
 static int load_raid0(const std::string &md, FileClass *fc) {
   std::string base = "/sys/block/" + md + "/md/";
   std::string level;
@@ -91,7 +92,9 @@ static int load_raid0(const std::string &md, FileClass *fc) {
   if (layout != 0 && layout != 1 && layout != 2) return -ENOTSUP;
   long chunk_bytes = read_long(base + "chunk_size", 0);
   if (chunk_bytes < 4096 || (chunk_bytes % 4096)) return -ENOTSUP;
-  fc->raid0.chunk_sects = (uint32_t)(chunk_bytes >> 9);
+  Raid0Geometry &g = fc->raid0;
+  memset(&g, 0, sizeof g);
+  g.chunk_sects = (uint32_t)(chunk_bytes >> 9);
   struct Mem { std::string name; uint64_t sectors; uint64_t off; int slot; };
   std::vector<Mem> mem;
   DIR *d = opendir(base.c_str());
@@ -99,61 +102,41 @@ static int load_raid0(const std::string &md, FileClass *fc) {
   while (dirent *e = readdir(d)) {
     if (strncmp(e->d_name, "dev-", 4) != 0) continue;
     std::string dd = base + e->d_name + "/";
-    std::string blk;
     char link[PATH_MAX];
     ssize_t n = readlink((dd + "block").c_str(), link, sizeof link - 1);
     if (n <= 0) continue;
     link[n] = 0;
-    blk = strrchr(link, '/') ? strrchr(link, '/') + 1 : link;
     Mem m;
-    m.name = blk;
+    m.name = strrchr(link, '/') ? strrchr(link, '/') + 1 : link;
     m.slot = (int)read_long(dd + "slot", (long)mem.size());
     m.off = (uint64_t)read_long(dd + "offset", 0);
     m.sectors = (uint64_t)read_long(dd + "size", 0) * 2;  // KiB -> sectors
     mem.push_back(m);
   }
   closedir(d);
-  if (mem.empty()) return -ENOTSUP;
+  if (mem.empty() || mem.size() > STROM_RAID0_MAX_DISKS) return -ENOTSUP;
   std::sort(mem.begin(), mem.end(), [](const Mem &a, const Mem &b) { return a.slot < b.slot; });
-  fc->raid0.data_offset.clear();
-  for (auto &m : mem) {
-    fc->members.push_back(m.name);
-    fc->raid0.data_offset.push_back(m.off);
+  g.ndisks = (uint32_t)mem.size();
+  for (size_t i = 0; i < mem.size(); ++i) {
+    fc->members.push_back(mem[i].name);
+    g.data_offset[i] = mem[i].off;
   }
-  // zones: distinct member sizes rounded to the chunk
   std::set<uint64_t> sizes;
-  for (auto &m : mem) sizes.insert(m.sectors / fc->raid0.chunk_sects * fc->raid0.chunk_sects);
+  for (auto &m : mem) sizes.insert(m.sectors / g.chunk_sects * g.chunk_sects);
   uint64_t prev = 0, md_end = 0;
   for (uint64_t sz : sizes) {
-    std::vector<int> devs;
-    for (size_t i = 0; i < mem.size(); ++i)
-      if (mem[i].sectors / fc->raid0.chunk_sects * fc->raid0.chunk_sects >= sz) devs.push_back((int)i);
     if (sz == prev) continue;
-    md_end += (sz - prev) * devs.size();
-    fc->raid0.zone_end.push_back(md_end);
-    fc->raid0.zone_dev_start.push_back(prev);
-    fc->raid0.zone_devs.push_back(devs);
+    if (g.nzones == STROM_RAID0_MAX_ZONES) return -ENOTSUP;
+    const uint32_t z = g.nzones++;
+    for (size_t i = 0; i < mem.size(); ++i)
+      if (mem[i].sectors / g.chunk_sects * g.chunk_sects >= sz)
+        g.zone_devs[z][g.zone_nb_dev[z]++] = (uint8_t)i;
+    md_end += (sz - prev) * g.zone_nb_dev[z];
+    g.zone_end[z] = md_end;
+    g.zone_dev_start[z] = prev;
     prev = sz;
   }
-  return 0;
-}
-
-int Raid0Geometry::map(uint64_t sector, uint32_t nr, int *member, uint64_t *msector) const {
-  if (chunk_sects == 0 || zone_end.empty()) return -EINVAL;
-  size_t z = 0;
-  while (z < zone_end.size() && sector >= zone_end[z]) ++z;
-  if (z == zone_end.size()) return -ERANGE;
-  uint64_t zstart = z ? zone_end[z - 1] : 0;
-  uint64_t in_chunk = sector % chunk_sects;
-  if (in_chunk + nr > chunk_sects) return -ESPIPE;  // request straddles a stripe
-  const std::vector<int> &devs = zone_devs[z];
-  uint64_t off = sector - zstart;
-  uint64_t chunk_no = off / chunk_sects;             // chunk index inside the zone
-  uint64_t row = chunk_no / devs.size();
-  int dev = devs[chunk_no % devs.size()];
-  *member = dev;
-  *msector = zone_dev_start[z] + row * chunk_sects + in_chunk + data_offset[dev];
-  return 0;
+  return strom_core_raid0_check(&g) ? -ENOTSUP : 0;
 }
 
 int classify_file(int fd, FileClass *fc, bool strict) {
@@ -221,6 +204,20 @@ int classify_file(int fd, FileClass *fc, bool strict) {
 }
 
 // ------------------------------------------------------------- planning
+namespace {
+int plan_submit(void *ctx, const strom_extent *e) {
+  auto *out = (ChunkPlan *)ctx;
+  out->ssd.push_back(IoRange{e->file_off, e->dest, e->len, e->member});
+  return 0;
+}
+int ident_bmap(void *, uint64_t fblk, uint64_t *dblk) {
+  *dblk = fblk;
+  return 0;
+}
+}  // namespace
+
+// Placement, residency routing and merging come from the shared core
+// (kmod/strom_core.c): the kernel provider plans with the same code.
 int plan_chunks(const PlanParams &p, ChunkPlan *out) {
   const uint32_t cs = p.chunk_sz;
   if (cs < 4096 || (cs & 4095) || cs > std::max(p.max_request, STROM_LEGACY_MAX_REQUEST))
@@ -230,101 +227,51 @@ int plan_chunks(const PlanParams &p, ChunkPlan *out) {
   out->ram_fpos.clear();
   out->ram_dest.clear();
   out->nr_ram = out->nr_ssd = out->nr_submit = out->nr_blocks = 0;
-  const uint32_t npages = cs >> 12;
-  const long threshold = npages / 2;
-  const uint32_t max_req = std::max<uint32_t>(p.max_request, cs);
+  const uint32_t threshold = strom_core_cache_threshold(cs >> 12);
 
-  IoRange cur{0, 0, 0, -1};
-  auto flush = [&]() {
-    if (cur.len) {
-      out->ssd.push_back(cur);
-      out->nr_submit++;
-      out->nr_blocks += cur.len >> 9;
-      cur.len = 0;
-    }
-  };
-  uint64_t ssd_dest = 0;
+  strom_landing land{p.nr_chunks, 0, 0, p.reorder};
+  strom_planner pl;
+  memset(&pl, 0, sizeof pl);
+  pl.max_req = std::max<uint32_t>(p.max_request, cs);
+  pl.file_contig = true;      // reads go by file offset
+  pl.dest_segment = p.dest_segment;
+  pl.blkbits = 12;
+  // raid0 splits need volume sectors: only with a real block map
+  pl.raid0 = p.bmap ? p.raid0 : nullptr;
+  pl.part_start_sect = p.bmap ? p.part_start_sect : 0;
+  pl.bmap = p.bmap ? p.bmap : ident_bmap;
+  pl.bmap_ctx = p.bmap_ctx;
+  pl.submit = plan_submit;
+  pl.submit_ctx = out;
+  strom_core_planner_init(&pl);
+
   for (uint32_t i = 0; i < p.nr_chunks; ++i) {
-    uint64_t cid = p.ids[i];
-    uint64_t fpos = (p.relseg_sz ? cid % p.relseg_sz : cid) * (uint64_t)cs;
-    if (fpos >= p.file_size) return -ERANGE;
-    long score = 0;
+    const uint32_t cid = p.ids[i];
+    uint64_t fpos = 0;
+    if (strom_core_chunk_fpos(cid, cs, p.relseg_sz, p.file_size, &fpos)) return -ERANGE;
+    bool cached = false;
     if (p.resident) {
-      long r = p.resident(fpos, cs);
-      if (r > 0) score = r;
+      // mincore cannot see dirty pages; O_DIRECT writes them back first
+      const long r = p.resident(fpos, cs);
+      cached = r > 0 && strom_core_cache_wins((uint32_t)r, threshold);
     }
-    if (score > threshold) {
-      uint64_t dest;
-      if (p.reorder) {
-        out->nr_ram++;
-        uint32_t pos = p.nr_chunks - out->nr_ram;
-        out->ids_out[pos] = (uint32_t)cid;
-        dest = (uint64_t)pos * cs;
-      } else {
-        out->nr_ram++;
-        out->ids_out[i] = (uint32_t)cid;
-        dest = (uint64_t)i * cs;
-      }
+    const uint32_t slot = strom_core_land(&land, i, cached);
+    out->ids_out[slot] = cid;
+    const uint64_t dest = (uint64_t)slot * cs;
+    if (cached) {
       out->ram_fpos.push_back(fpos);
       out->ram_dest.push_back(dest);
       continue;
     }
-    uint64_t dest = p.reorder ? ssd_dest : (uint64_t)i * cs;
-    if (p.reorder) {
-      out->ids_out[out->nr_ssd] = (uint32_t)cid;
-      ssd_dest += cs;
-    } else {
-      out->ids_out[i] = (uint32_t)cid;
-    }
-    out->nr_ssd++;
-    // walk the chunk in 4 KiB pages (raid0 may split it), merging as we go
-    for (uint32_t pg = 0; pg < npages;) {
-      uint64_t f = fpos + (uint64_t)pg * 4096;
-      uint64_t d = dest + (uint64_t)pg * 4096;
-      uint32_t run = npages - pg;  // pages we may take in one piece
-      int member = -1;
-      if (p.raid0) {
-        // pages to the end of the current stripe chunk
-        uint64_t sect = (f >> 9) + p.part_start_sect;
-        uint64_t in_chunk = sect % p.raid0->chunk_sects;
-        uint32_t left = (uint32_t)((p.raid0->chunk_sects - in_chunk) >> 3);
-        if (left == 0) left = 1;
-        run = std::min(run, left);
-        uint64_t msect;
-        int rc = p.raid0->map(sect, run * 8, &member, &msect);
-        if (rc) return rc;
-      }
-      uint32_t bytes = run * 4096;
-      bool seg_ok = true;
-      if (p.dest_segment) {
-        // the merged request may not cross a destination segment
-        seg_ok = (cur.dest_off / p.dest_segment) == ((d + bytes - 1) / p.dest_segment);
-      }
-      if (cur.len && cur.member == member && cur.file_off + cur.len == f &&
-          cur.dest_off + cur.len == d && seg_ok && cur.len + bytes <= max_req) {
-        cur.len += bytes;
-      } else if (cur.len && cur.member == member && cur.file_off + cur.len == f &&
-                 cur.dest_off + cur.len == d && seg_ok && cur.len < max_req) {
-        // fill the current request up to max_req, continue with the rest
-        uint32_t take = max_req - cur.len;
-        cur.len += take;
-        flush();
-        pg += take / 4096;
-        continue;
-      } else {
-        flush();
-        if (p.dest_segment) {
-          // never start a request that crosses a segment: trim the run
-          uint64_t seg_end = (d / p.dest_segment + 1) * p.dest_segment;
-          if (d + bytes > seg_end) bytes = (uint32_t)(seg_end - d);
-        }
-        if (bytes > max_req) bytes = max_req;
-        cur = IoRange{f, d, bytes, member};
-      }
-      pg += bytes / 4096;
-    }
+    int rc = strom_core_plan_range(&pl, fpos, cs, dest);
+    if (rc) return rc;
   }
-  flush();
+  int rc = strom_core_plan_flush(&pl);
+  if (rc) return rc;
+  out->nr_ram = land.nr_ram;
+  out->nr_ssd = land.nr_ssd;
+  out->nr_submit = pl.nr_submit;
+  out->nr_blocks = (uint32_t)pl.nr_sectors;
   return 0;
 }
 

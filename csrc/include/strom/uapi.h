@@ -55,6 +55,7 @@ typedef uint64_t strom_u64;
 #define STROM_IOCTL__MAP_GPU_DMABUF     _IO(STROM_IOC_MAGIC, 0x86)
 #define STROM_IOCTL__MEMCPY_WAIT_TIMED  _IO(STROM_IOC_MAGIC, 0x93)
 #define STROM_IOCTL__STAT_HIST          _IO(STROM_IOC_MAGIC, 0x9a)
+#define STROM_IOCTL__SET_ROUTE          _IO(STROM_IOC_MAGIC, 0x87)
 
 /* Kernel provider entry points.  /proc keeps v0.6 compatibility; /dev is
  * what the MI355X kmod registers as a misc device. */
@@ -207,6 +208,37 @@ struct strom_stat_hist {
 	strom_u64 task_ns[STROM_HIST_BUCKETS];  /* ioctl entry -> task done */
 };
 
+/* ---- SET_ROUTE (MI355X, kernel provider, CAP_SYS_ADMIN) --------------
+ * How the kernel provider reaches the NVMe namespaces behind a volume it
+ * cannot decode without md/nvme private structures: an md raid0 array
+ * (geometry + members, reference kmod/nvme_strom.c:755-820) or a native
+ * multipath head (one member: the path namespace to submit on).  Userspace
+ * derives it from sysfs (nvme_strom_amd/utils/route.py); the module checks
+ * the geometry (strom_core_raid0_check), the members' sizes against it and
+ * that every member is an NVMe namespace with a blk-mq queue.  nmembers == 0
+ * removes the volume's route. */
+#define STROM_ROUTE_MAX_ZONES  16
+#define STROM_ROUTE_MAX_DISKS  32
+struct strom_set_route {
+	strom_u32 volume_major;     /* in: md array / nvme head block device */
+	strom_u32 volume_minor;
+	strom_u32 nmembers;         /* in: 0 = drop the route */
+	strom_u32 chunk_sects;      /* in: raid0 stripe chunk (sectors); 0 = single path */
+	strom_u32 nzones;
+	strom_u32 reserved;
+	strom_u64 zone_end[STROM_ROUTE_MAX_ZONES];        /* md sector, exclusive */
+	strom_u64 zone_dev_start[STROM_ROUTE_MAX_ZONES];  /* member sector of zone start */
+	strom_u32 zone_nb_dev[STROM_ROUTE_MAX_ZONES];
+	unsigned char zone_devs[STROM_ROUTE_MAX_ZONES][STROM_ROUTE_MAX_DISKS];
+	strom_u32 member_major[STROM_ROUTE_MAX_DISKS];
+	strom_u32 member_minor[STROM_ROUTE_MAX_DISKS];
+	strom_u64 data_offset[STROM_ROUTE_MAX_DISKS];     /* sectors */
+	/* a member with major 0 is named instead, "<pci>/<ctrl>/<disk>", e.g.
+	 * "0000:41:00.0/nvme0/nvme0c0n1": the hidden path disk of a multipath
+	 * namespace, which has no openable dev_t */
+	char member_name[STROM_ROUTE_MAX_DISKS][40];
+};
+
 /* ---- v0.6 source-compatible names ----------------------------------- */
 typedef struct strom_check_file        StromCmd__CheckFile;
 typedef struct strom_map_gpu_memory    StromCmd__MapGpuMemory;
@@ -250,6 +282,8 @@ STROM_ASSERT(sizeof(struct strom_alloc_dma_buffer) == 16, "AllocDMABuffer");
 STROM_ASSERT(sizeof(struct strom_stat_info) == 168, "StatInfo");
 STROM_ASSERT(offsetof(struct strom_stat_info, tsc) == 8, "Stat.tsc");
 STROM_ASSERT(offsetof(struct strom_stat_info, nr_debug1) == 104, "Stat.dbg1");
+STROM_ASSERT(sizeof(struct strom_set_route) == 2648, "SetRoute");
+STROM_ASSERT(offsetof(struct strom_set_route, zone_devs) == 344, "Route.devs");
 STROM_ASSERT(STROM_IOCTL__CHECK_FILE == 0x5380, "code");
 STROM_ASSERT(STROM_IOCTL__MEMCPY_SSD2GPU == 0x5390, "code");
 STROM_ASSERT(STROM_IOCTL__STAT_INFO == 0x5399, "code");

@@ -53,6 +53,7 @@ static void gpumap_free_work(struct work_struct *w)
 		dma_buf_unpin(a->att);
 		dma_resv_unlock(m->dmabuf->resv);
 		dma_buf_detach(m->dmabuf, a->att);
+		kvfree(a->seg_addr);
 	}
 	dma_buf_put(m->dmabuf);
 	kfree(m);
@@ -131,22 +132,60 @@ int strom_map_dmabuf(struct strom_map_gpu_dmabuf *arg)
 	return 0;
 }
 
+/* Only the caller that takes the record out of the table owns the table's
+ * reference: a second, concurrent UNMAP of the same handle finds nothing and
+ * returns -ENOENT (two callers could both pass a lookup and drop
+ * four references against three). */
 int strom_unmap_gpu(unsigned long handle)
 {
-	struct strom_gpumap *m = strom_gpumap_get(handle);
+	struct strom_gpumap *m = NULL, *it;
 
+	spin_lock(&gpumap_lock);
+	hash_for_each_possible(gpumap_slots, it, node, handle) {
+		if (it->handle == handle && uid_eq(it->owner, current_euid())) {
+			hash_del(&it->node);
+			m = it;
+			break;
+		}
+	}
+	spin_unlock(&gpumap_lock);
 	if (!m)
 		return -ENOENT;
-	spin_lock(&gpumap_lock);
-	hash_del(&m->node);
-	spin_unlock(&gpumap_lock);
+	/* reference v0.6 never waited (defect #7): drain in-flight DMA first */
 	wait_event(m->drain, atomic_read(&m->inflight) == 0);
-	strom_gpumap_put(m);   /* lookup reference */
-	strom_gpumap_put(m);   /* table reference */
+	strom_gpumap_put(m);   /* the table's reference, now ours */
 	return 0;
 }
 
-/* attach + pin + map for `dev` once; caller holds a reference on m */
+/* the sg table flattened into start/len/bus-address arrays once: every
+ * later lookup is a binary search (or O(1) for the next page), where v1
+ * walked the list from its head for each 4 KiB page */
+static int flatten_sgt(struct strom_attach *a)
+{
+	struct scatterlist *sg;
+	u32 n = 0, i = 0;
+	u64 off = 0;
+	int k;
+
+	for_each_sgtable_dma_sg(a->sgt, sg, k)
+		n++;
+	a->seg_addr = kvmalloc_array(n, 3 * sizeof(u64), GFP_KERNEL);
+	if (!a->seg_addr)
+		return -ENOMEM;
+	a->seg_len = a->seg_addr + n;
+	a->seg_start = a->seg_len + n;
+	for_each_sgtable_dma_sg(a->sgt, sg, k) {
+		a->seg_addr[i] = sg_dma_address(sg);
+		a->seg_len[i] = sg_dma_len(sg);
+		a->seg_start[i] = off;
+		off += sg_dma_len(sg);
+		i++;
+	}
+	a->nsegs = n;
+	return 0;
+}
+
+/* attach + pin + map + flatten for `dev` once; caller holds a reference on m */
 static struct strom_attach *gpumap_attach(struct strom_gpumap *m, struct device *dev)
 {
 	struct strom_attach *a = NULL;
@@ -179,43 +218,44 @@ static struct strom_attach *gpumap_attach(struct strom_gpumap *m, struct device 
 	}
 	sgt = dma_buf_map_attachment(att, DMA_BIDIRECTIONAL);
 	dma_resv_unlock(m->dmabuf->resv);
-	if (IS_ERR(sgt)) {
-		dma_resv_lock(m->dmabuf->resv, NULL);
-		dma_buf_unpin(att);
-		dma_resv_unlock(m->dmabuf->resv);
-		dma_buf_detach(m->dmabuf, att);
-		goto out;
-	}
-	a = &m->att[m->natt++];
+	if (IS_ERR(sgt))
+		goto unpin;
+	a = &m->att[m->natt];
 	a->dev = dev;
 	a->att = att;
 	a->sgt = sgt;
+	if (flatten_sgt(a)) {
+		dma_resv_lock(m->dmabuf->resv, NULL);
+		dma_buf_unmap_attachment(att, sgt, DMA_BIDIRECTIONAL);
+		dma_resv_unlock(m->dmabuf->resv);
+		memset(a, 0, sizeof(*a));
+		a = NULL;
+		goto unpin;
+	}
+	m->natt++;
+	goto out;
+unpin:
+	dma_resv_lock(m->dmabuf->resv, NULL);
+	dma_buf_unpin(att);
+	dma_resv_unlock(m->dmabuf->resv);
+	dma_buf_detach(m->dmabuf, att);
 out:
 	mutex_unlock(&m->att_lock);
 	return a;
 }
 
-int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
-		     dma_addr_t *addr, size_t *contig)
+int strom_gpumap_sgmap(struct strom_gpumap *m, struct device *dev, struct strom_sgmap *sg)
 {
 	struct strom_attach *a = gpumap_attach(m, dev);
-	struct scatterlist *sg;
-	int i;
 
 	if (!a)
 		return -EOPNOTSUPP;
-	off += m->dmabuf_off;
-	for_each_sgtable_dma_sg(a->sgt, sg, i) {
-		size_t len = sg_dma_len(sg);
-
-		if (off < len) {
-			*addr = sg_dma_address(sg) + off;
-			*contig = len - off;
-			return 0;
-		}
-		off -= len;
-	}
-	return -ERANGE;
+	sg->nsegs = a->nsegs;
+	sg->addr = a->seg_addr;
+	sg->len = a->seg_len;
+	sg->start = a->seg_start;
+	sg->hint = 0;          /* per caller: lookups never share a hint */
+	return 0;
 }
 
 int strom_list_gpu(struct strom_list_gpu_memory __user *uarg)
@@ -271,14 +311,16 @@ int strom_info_gpu(struct strom_info_gpu_memory __user *uarg)
 	k.map_offset = m->vaddress & (STROM_GPU_BOUND_SIZE - 1);
 	k.map_length = m->length;
 	for (i = 0; i < npages && i < k.nrooms; i++) {
-		/* bus address as seen by the first attached controller, if any */
+		/* bus address as seen by the first attached controller, if any
+		 * (natt only grows, and att[0] never changes once set) */
 		u64 pa = 0;
 
 		if (m->natt) {
-			dma_addr_t a;
-			size_t c;
+			struct strom_sgmap sg;
+			u64 a, c;
 
-			if (!strom_gpumap_dma(m, m->att[0].dev, (size_t)i * STROM_GPU_BOUND_SIZE, &a, &c))
+			if (!strom_gpumap_sgmap(m, m->att[0].dev, &sg) &&
+			    !strom_core_sg_lookup(&sg, m->dmabuf_off + (u64)i * STROM_GPU_BOUND_SIZE, &a, &c))
 				pa = a;
 		}
 		if (put_user(pa, &uarg->paddrs[i])) {

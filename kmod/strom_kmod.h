@@ -10,35 +10,67 @@
  * those addresses go straight into NVMe READ PRP lists.  No
  * nvidia_p2p_get_pages, no raw physical addresses (reference defect #8), no
  * kallsyms lookups (unexported since 5.7): file extents come from bmap(),
- * NVMe commands are passthrough requests on the namespace queue.
+ * NVMe commands are passthrough requests on the namespace's blk-mq queue.
  *
- * Status: written against Linux 6.8+ APIs (ns_id / lba_shift live in
- * struct nvme_ns_head since 6.8); compile-untested in this repo's
- * environment (no kernel headers, no root on the GPU pool).  Build with
- * KSRC pointing at a configured kernel tree (drivers/nvme/host/nvme.h is
- * needed for struct nvme_ns and nvme_init_request()).
+ * Kernel interface: Linux >= 6.8, EXPORTED interfaces only — no private
+ * drivers/nvme or drivers/md headers (the reference vendored RHEL7 copies of
+ * nvme.h / md.h / raid0.h, kmod/514.6.2.el7/).  What those headers gave the
+ * reference is obtained here as follows:
+ *   namespace id       the disk's own NVME_IOCTL_ID ioctl (as the reference's
+ *                      CHECK_FILE ping did)
+ *   LBA size           queue_logical_block_size()
+ *   DMA device         the nearest PCI ancestor of the disk's struct device
+ *   command setup      nvme_init_request() — EXPORT_SYMBOL_GPL of nvme-core;
+ *                      its prototype is declared below (checked against a
+ *                      kernel tree by kmod/kernel-check.sh)
+ *   multipath paths    a hidden path disk (nvmeXcYnZ) is found by name under
+ *                      its controller with device_find_child_by_name()
+ *   md raid0 geometry  registered by userspace (STROM_IOCTL__SET_ROUTE,
+ *                      CAP_SYS_ADMIN) from sysfs and checked here
+ * The one piece of NVMe state read from a completed request is the
+ * blk_status_t handed to end_io (nvme_end_req translates the NVMe status).
+ *
+ * Version gates (LINUX_VERSION_CODE) exist only where an API moved inside
+ * [6.8, 6.18]: MODULE_IMPORT_NS takes a string literal from 6.13, block
+ * devices are opened with bdev_file_open_by_dev() from 6.9 (bdev_open_by_dev()
+ * handles in 6.8), and struct fd is read through fd_file() from 6.12.
  */
 #ifndef STROM_KMOD_H
 #define STROM_KMOD_H
 
 #include <linux/atomic.h>
+#include <linux/blk-mq.h>
 #include <linux/blkdev.h>
 #include <linux/dma-buf.h>
 #include <linux/fs.h>
 #include <linux/kref.h>
 #include <linux/list.h>
 #include <linux/mutex.h>
+#include <linux/nvme.h>
 #include <linux/spinlock.h>
 #include <linux/types.h>
+#include <linux/version.h>
 #include <linux/wait.h>
 #include <linux/workqueue.h>
 
-#include "../csrc/include/strom/uapi.h"
+#include "strom/uapi.h"       /* -I$(src)/include (DKMS) or ../csrc/include (tree) */
+#include "strom_core.h"
+
+#if LINUX_VERSION_CODE < KERNEL_VERSION(6, 8, 0)
+#error "nvme-strom (MI355X) needs Linux >= 6.8"
+#endif
+#if LINUX_VERSION_CODE < KERNEL_VERSION(6, 12, 0)
+#define fd_file(f) ((f).file)          /* accessor introduced in 6.12 */
+#endif
 
 #define STROM_NAME "nvme-strom"
-#define STROM_MAX_REQ (1U << 20)         /* merge limit, clamped by MDTS */
 #define STROM_NR_TASK_SLOTS 512
 #define STROM_NR_MAP_SLOTS 64
+#define STROM_MAX_ATTACH 8               /* NVMe controllers per HBM mapping */
+
+/* nvme-core, EXPORT_SYMBOL_GPL (drivers/nvme/host/core.c); declared in the
+ * private drivers/nvme/host/nvme.h, so declared here */
+void nvme_init_request(struct request *req, struct nvme_command *cmd);
 
 extern int strom_verbose;
 extern int strom_stat_level;
@@ -72,11 +104,47 @@ struct strom_session {
 	                                    completion */
 };
 
+/* ---- NVMe namespaces behind a volume ------------------------------------ */
+struct strom_member {
+	struct device *disk_dev;         /* held (get_device) */
+	struct gendisk *disk;            /* blk-mq namespace (path) disk */
+	struct request_queue *q;
+	struct device *dma_dev;          /* the controller's PCI function */
+	u32 nsid;
+	u32 lba_shift;
+	u32 max_bytes;                   /* queue_max_hw_sectors, bytes */
+	sector_t nr_sects;               /* capacity */
+	struct dma_pool *prp_pool;
+};
+
+struct strom_volume {
+	struct kref ref;
+	struct work_struct free_work;    /* members are released in process context */
+	struct list_head node;           /* route table (registered volumes) */
+	dev_t devt;                      /* md array / nvme head / plain namespace */
+	bool registered;
+	bool raid0;
+	struct strom_raid0 geo;
+	int nmembers;
+	struct strom_member m[STROM_ROUTE_MAX_DISKS];
+};
+
+/* The volume under a file: its route when registered, else the file's own
+ * disk when that is a blk-mq NVMe namespace.  Reference held. */
+struct strom_volume *strom_volume_of_file(struct file *filp, int *err);
+void strom_volume_put(struct strom_volume *v);
+int strom_set_route(const struct strom_set_route *r);
+int strom_route_init(void);
+void strom_route_exit(void);
+
 /* ---- HBM mapping: imported dma-buf ------------------------------------ */
 struct strom_attach {                    /* one per NVMe controller device */
 	struct device *dev;
 	struct dma_buf_attachment *att;
 	struct sg_table *sgt;
+	/* the sg table flattened once (strom_core_sg_lookup searches it) */
+	u32 nsegs;
+	u64 *seg_addr, *seg_len, *seg_start;
 };
 
 struct strom_gpumap {
@@ -87,7 +155,7 @@ struct strom_gpumap {
 	u64 vaddress;                    /* user VA of the mapped range */
 	u64 dmabuf_off;                  /* byte offset of vaddress in the dma-buf */
 	size_t length;
-	struct strom_attach att[4];      /* lazily per target controller */
+	struct strom_attach att[STROM_MAX_ATTACH];   /* lazily per controller */
 	int natt;
 	struct mutex att_lock;
 	atomic_t inflight;               /* requests targeting the range */
@@ -102,10 +170,10 @@ int strom_list_gpu(struct strom_list_gpu_memory __user *uarg);
 int strom_info_gpu(struct strom_info_gpu_memory __user *uarg);
 struct strom_gpumap *strom_gpumap_get(unsigned long handle);
 void strom_gpumap_put(struct strom_gpumap *m);
-/* bus address of byte `off` of the mapping as seen by `dev`, and how many
- * contiguous bytes follow it */
-int strom_gpumap_dma(struct strom_gpumap *m, struct device *dev, size_t off,
-		     dma_addr_t *addr, size_t *contig);
+/* bus addresses of the dma-buf as seen by `dev` (attach + pin + map once per
+ * controller): *sg maps byte offsets of the WHOLE dma-buf, so a destination
+ * offset inside the mapped range is looked up at dmabuf_off + offset */
+int strom_gpumap_sgmap(struct strom_gpumap *m, struct device *dev, struct strom_sgmap *sg);
 int strom_gpumap_init(void);
 void strom_gpumap_exit(void);
 
@@ -121,6 +189,7 @@ struct strom_task {
 	struct strom_gpumap *gmap;       /* SSD2GPU target (ref held) */
 	struct file *filp;               /* source (ref held) */
 	struct file *dbuf_filp;          /* SSD2RAM destination buffer (ref held) */
+	struct strom_volume *vol;        /* namespaces the requests go to (ref held) */
 	u64 t_start;
 };
 

@@ -6,7 +6,9 @@
  * and init/exit (:2159-2217) with modern registration: a misc device
  * (/dev/nvme-strom, mode 0444) plus the legacy /proc entry for old binaries.
  * read() returns the version signature; release() reclaims failed tasks the
- * opener never waited for.  MAP_GPU_MEMORY (VA only) is answered -EOPNOTSUPP:
+ * opener never waited for.  SET_ROUTE (admin) registers the namespaces behind
+ * an md raid0 array or an NVMe multipath head.  MAP_GPU_MEMORY (VA only) is
+ * answered -EOPNOTSUPP:
  * the kernel cannot resolve an amdgpu VA to its buffer object, so libstrom
  * exports the range as a dma-buf and calls MAP_GPU_DMABUF instead.
  */
@@ -14,6 +16,7 @@
 #include <linux/module.h>
 #include <linux/proc_fs.h>
 #include <linux/slab.h>
+#include <linux/string.h>
 #include <linux/uaccess.h>
 
 #include "strom_kmod.h"
@@ -121,6 +124,15 @@ static long strom_ioctl(struct file *filp, unsigned int cmd, unsigned long arg)
 			rc = -EFAULT;
 		return rc;
 	}
+	case STROM_IOCTL__SET_ROUTE: {
+		struct strom_set_route *r = memdup_user(uarg, sizeof(*r));
+
+		if (IS_ERR(r))
+			return PTR_ERR(r);
+		rc = strom_set_route(r);
+		kfree(r);
+		return rc;
+	}
 	case STROM_IOCTL__STAT_INFO: {
 		COPY_IN(struct strom_stat_info);
 		rc = strom_stat_info(&karg);
@@ -166,9 +178,12 @@ static int __init nvme_strom_init(void)
 	rc = strom_gpumap_init();
 	if (rc)
 		return rc;
-	rc = misc_register(&strom_misc);
+	rc = strom_route_init();
 	if (rc)
 		goto out_map;
+	rc = misc_register(&strom_misc);
+	if (rc)
+		goto out_route;
 	strom_proc = proc_create(STROM_NAME, 0444, NULL, &strom_proc_ops);
 	if (!strom_proc) {
 		rc = -ENOMEM;
@@ -179,6 +194,8 @@ static int __init nvme_strom_init(void)
 	return 0;
 out_misc:
 	misc_deregister(&strom_misc);
+out_route:
+	strom_route_exit();
 out_map:
 	strom_gpumap_exit();
 	return rc;
@@ -188,6 +205,7 @@ static void __exit nvme_strom_exit(void)
 {
 	proc_remove(strom_proc);
 	misc_deregister(&strom_misc);
+	strom_route_exit();
 	strom_gpumap_exit();
 	pr_info("nvme-strom: unloaded\n");
 }
@@ -198,4 +216,8 @@ MODULE_AUTHOR("strom-mi355x");
 MODULE_DESCRIPTION("SSD-to-GPU direct DMA for AMD Instinct MI355X (dma-buf P2P)");
 MODULE_VERSION("0.1.0");
 MODULE_LICENSE("GPL v2");
+#if LINUX_VERSION_CODE >= KERNEL_VERSION(6, 13, 0)
+MODULE_IMPORT_NS("DMA_BUF");        /* namespaces are string literals since 6.13 */
+#else
 MODULE_IMPORT_NS(DMA_BUF);
+#endif

@@ -99,9 +99,11 @@ void strom_task_put(struct strom_task *t, long status)
 		fput(t->filp);
 	if (t->dbuf_filp)
 		fput(t->dbuf_filp);
+	strom_volume_put(t->vol);           /* frees on a workqueue if last */
 	t->gmap = NULL;
 	t->filp = NULL;
 	t->dbuf_filp = NULL;
+	t->vol = NULL;
 	if (!t->status)
 		kfree(t);
 	/* last: a failed record stays on the session's list until WAIT or
