@@ -21,11 +21,12 @@
 //      committed — frozen xmin included — and xmax invalid or lock-only),
 //      and an optional range predicate on a fixed-offset int4/int8 column;
 //      the per-64 ballot masks are parked in LDS;
-//   4. output reservation once per WORKGROUP (4 pages): the waves' counts
-//      are summed in LDS and thread 0 does a single atomicAdd, then each
-//      wave replays its masks to write (page << 16 | lineno) item ids.
+//   4. output reservation once per WORKGROUP (4 waves x 8 pages): the waves'
+//      counts are summed in LDS and thread 0 does a single atomicAdd, then
+//      each wave replays its masks to write (page << 16 | lineno) item ids.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "strom/strom.h"
@@ -142,16 +143,27 @@ __device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const 
 }
 
 // PAGE = page size known at compile time (0: a.page_sz at run time).  Each
-// lane moves NV 16-byte pieces of its wave's page per iteration.
+// lane moves NV 16-byte pieces of its wave's page per page.  A workgroup
+// handles kWaves x kPerWave pages per output reservation: one same-address
+// atomicAdd per 32 pages (round 1: per 4 pages, which capped scans where
+// every page has qualifying rows at ~88 atomics/us, MI355X_MICROARCH.md
+// row "dequeue" — 2.1 TB/s).
+constexpr int kPerWave = 8;
+
 template <int PAGE>
-__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, uint32_t maxchunks) {
+__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, uint32_t maxchunks,
+                                                        uint32_t ppw) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t page_sz = PAGE ? (uint32_t)PAGE : a.page_sz;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t *mypage = smem + (size_t)wid * page_sz;
-  uint64_t *masks = (uint64_t *)(smem + (size_t)kWaves * page_sz) + (size_t)wid * maxchunks;
-  uint32_t *wcount = (uint32_t *)((uint64_t *)(smem + (size_t)kWaves * page_sz) + kWaves * maxchunks);
+  // masks[wid][j][chunk] for the wave's kPerWave pages
+  uint64_t *masks =
+      (uint64_t *)(smem + (size_t)kWaves * page_sz) + (size_t)wid * ppw * maxchunks;
+  uint32_t *wcount =
+      (uint32_t *)((uint64_t *)(smem + (size_t)kWaves * page_sz) + kWaves * ppw * maxchunks);
   uint32_t *wbase = wcount + kWaves;
+  uint32_t *nch = wbase + kWaves + wid * ppw;        // chunks per page of this wave
 
   constexpr int NV = PAGE ? PAGE / (64 * 16) : 32;   // 32 = up to 32 KiB pages
   const uint32_t nv = page_sz / (64 * 16);
@@ -164,40 +176,48 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
       if (PAGE || (uint32_t)k < nv) buf[k] = __builtin_nontemporal_load(src_ + k * 64 + lane); \
   } while (0)
 
-  const uint32_t stride = gridDim.x * kWaves;
-  uint32_t pg = blockIdx.x * kWaves + wid;
-  if (pg < a.npages) STROM_HS_ISSUE(pg);
-  // every wave of a workgroup runs the same trip count (barriers inside)
-  for (uint32_t base = blockIdx.x * kWaves; base < a.npages; base += stride, pg += stride) {
-    const bool have = pg < a.npages;
-    if (have) {
+  const uint32_t kPerWg = kWaves * ppw;
+  const uint32_t stride = gridDim.x * kPerWg;
+  // wave wid owns pages [base + wid*ppw, +ppw) of each group
+  uint32_t first = blockIdx.x * kPerWg + wid * ppw;
+  if (first < a.npages) STROM_HS_ISSUE(first);
+  // every wave of a workgroup runs the same trip counts (barriers inside)
+  for (uint32_t base = blockIdx.x * kPerWg; base < a.npages; base += stride, first += stride) {
+    uint32_t count = 0;
+    for (uint32_t j = 0; j < ppw; ++j) {
+      const uint32_t pg = first + j;
+      const bool have = pg < a.npages;
+      if (have) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k)
-        if (PAGE || (uint32_t)k < nv) ((v4u *)mypage)[k * 64 + lane] = buf[k];
-    }
-    __syncthreads();
-    // next page's loads are in flight while this one is parsed from LDS
-    if (pg + stride < a.npages) STROM_HS_ISSUE(pg + stride);
-
-    uint32_t count = 0, nchunks = 0;
-    if (have) {
-      const PageHdr h = read_hdr(mypage);
-      const uint32_t status = page_status(a, mypage, h, pg, lane);
-      if (lane == 0 && a.page_status) a.page_status[pg] = status;
-      if (status == 0) {
-        const bool all_visible = (h.flags & kPdAllVisible) != 0;
-        const uint32_t nitems = (h.lower - kSizeOfPageHeader) / 4;
-        nchunks = (nitems + 63) / 64;
-        for (uint32_t c = 0; c < nchunks; ++c) {
-          const uint32_t i = c * 64 + lane;
-          const bool keep =
-              i < nitems && tuple_keep(a, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i),
-                                       all_visible);
-          const uint64_t m = __ballot(keep);
-          if (lane == 0) masks[c] = m;
-          count += __popcll(m);
+        for (int k = 0; k < NV; ++k)
+          if (PAGE || (uint32_t)k < nv) ((v4u *)mypage)[k * 64 + lane] = buf[k];
+      }
+      __syncthreads();
+      // the next page's loads are in flight while this one is parsed
+      const uint32_t nxt = j + 1 < ppw ? pg + 1 : first + stride;
+      if (nxt < a.npages && (j + 1 < ppw ? have : true)) STROM_HS_ISSUE(nxt);
+      uint32_t nchunks = 0;
+      if (have) {
+        const PageHdr h = read_hdr(mypage);
+        const uint32_t status = page_status(a, mypage, h, pg, lane);
+        if (lane == 0 && a.page_status) a.page_status[pg] = status;
+        if (status == 0) {
+          const bool all_visible = (h.flags & kPdAllVisible) != 0;
+          const uint32_t nitems = (h.lower - kSizeOfPageHeader) / 4;
+          nchunks = (nitems + 63) / 64;
+          for (uint32_t c = 0; c < nchunks; ++c) {
+            const uint32_t i = c * 64 + lane;
+            const bool keep =
+                i < nitems && tuple_keep(a, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i),
+                                         all_visible);
+            const uint64_t m = __ballot(keep);
+            if (lane == 0) masks[j * maxchunks + c] = m;
+            count += __popcll(m);
+          }
         }
       }
+      if (lane == 0) nch[j] = nchunks;
+      __syncthreads();   // the page image is overwritten next
     }
     if (lane == 0) wcount[wid] = count;
     __syncthreads();
@@ -214,16 +234,19 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
     if (count && a.out_items) {
       uint32_t run = wbase[wid];
       const uint64_t below = (1ull << lane) - 1;
-      for (uint32_t c = 0; c < nchunks; ++c) {
-        const uint64_t m = masks[c];
-        if ((m >> lane) & 1) {
-          const uint32_t slot = run + __popcll(m & below);
-          if (slot < a.out_cap) a.out_items[slot] = (pg << 16) | (c * 64 + lane + 1);  // 1-based
+      for (uint32_t j = 0; j < ppw; ++j) {
+        const uint32_t pg = first + j;
+        for (uint32_t c = 0; c < nch[j]; ++c) {
+          const uint64_t m = masks[j * maxchunks + c];
+          if ((m >> lane) & 1) {
+            const uint32_t slot = run + __popcll(m & below);
+            if (slot < a.out_cap) a.out_items[slot] = (pg << 16) | (c * 64 + lane + 1);  // 1-based
+          }
+          run += __popcll(m);
         }
-        run += __popcll(m);
       }
     }
-    __syncthreads();  // page image, masks and wcount are reused next iteration
+    __syncthreads();  // masks, counts and wcount are reused next iteration
   }
 #undef STROM_HS_ISSUE
 }
@@ -240,15 +263,21 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   (void)hipMemsetAsync(a->out_count, 0, sizeof(uint32_t), st);
   const uint32_t maxchunks = ((a->page_sz - 24) / 4 + 63) / 64;
-  const size_t lds = (size_t)kWaves * a->page_sz + (size_t)kWaves * maxchunks * 8 + 2 * kWaves * 4;
+  // pages per wave per output reservation: kPerWave, fewer when the page
+  // images leave too little LDS for the masks (32 KiB pages)
+  const size_t budget = 160u * 1024u - (size_t)kWaves * a->page_sz - (3 * kWaves + kWaves * kPerWave) * 4;
+  uint32_t ppw = (uint32_t)std::min<size_t>(kPerWave, budget / ((size_t)kWaves * maxchunks * 8));
+  if (ppw < 1) return -22;
+  const size_t lds = (size_t)kWaves * a->page_sz + (size_t)kWaves * ppw * maxchunks * 8 +
+                     (2 * kWaves + kWaves * ppw) * 4;
   // enough workgroups to fill 256 CUs at the occupancy LDS allows, then stride
   const uint32_t per_cu = (uint32_t)(160u * 1024u / ((lds + 1023) & ~(size_t)1023));
-  uint32_t grid = (a->npages + kWaves - 1) / kWaves;
+  uint32_t grid = (a->npages + kWaves * ppw - 1) / (kWaves * ppw);
   const uint32_t cap = 256u * (per_cu ? per_cu : 1u) * 2u;
   if (grid > cap) grid = cap;
   if (a->page_sz == 8192)
-    hipLaunchKernelGGL(heap_scan_kernel<8192>, dim3(grid), dim3(256), lds, st, *a, maxchunks);
+    hipLaunchKernelGGL(heap_scan_kernel<8192>, dim3(grid), dim3(256), lds, st, *a, maxchunks, ppw);
   else
-    hipLaunchKernelGGL(heap_scan_kernel<0>, dim3(grid), dim3(256), lds, st, *a, maxchunks);
+    hipLaunchKernelGGL(heap_scan_kernel<0>, dim3(grid), dim3(256), lds, st, *a, maxchunks, ppw);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
