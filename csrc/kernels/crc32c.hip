@@ -7,15 +7,24 @@
 //
 // Layout of the work (one wavefront per chunk, 64-wide, grid-stride):
 //   the chunk is viewed as rows of 1 KiB = 64 lanes x 16 B (one
-//   global_load_dwordx4 per lane per row, fully coalesced).  Lane l keeps a
-//   running raw CRC A_l of its column: A_l <- shift1K(A_l) ^ R(piece), where
-//   R() is zero-init CRC of a 16-byte piece by slicing-by-16 lookups and
-//   shift1K() is the linear "append 1024 zero bytes" map, both as byte
-//   tables staged in LDS (20 KiB).  Columns are then aligned with one GF(2)
-//   multiply by x^(8*16*(63-l)) mod P and folded with a 6-step xor
-//   butterfly — no cross-lane ordering, no serial dependency across lanes.
-//   CRC linearity also turns the 0xFFFFFFFF initial value into an xor of
-//   the first data word, so no pow(x, 8n) is needed for the init term.
+//   global_load_dwordx4 per lane per row, fully coalesced, 8 rows in flight
+//   per lane).  Lane l keeps a running raw CRC A_l of its column:
+//   A_l <- shift1K(A_l) ^ R(piece), where
+//     R()      = zero-init CRC of a 16-byte piece, slicing-by-4 (4 word steps
+//                of 4 table lookups, tables T0..T3);
+//     shift1K  = "append 1024 zero bytes", 4 lookups (tables X0..X3).
+//   The 8 tables sit in LDS as 16 lane-indexed copies (entry b of copy c at
+//   word b*16 + c): lanes l and l+16 share a copy and collide only when
+//   their entries have the same parity, so a ds_read_b32 takes at most two
+//   passes whatever the data, where round 1's single copy of 20 tables
+//   (slicing-by-16) took ~4 on random bytes (14x more bank-conflict cycles
+//   than LDS instructions on its worst input, profiles/r1i).  (A VALU-only
+//   shift1K — 32 masked xors — measured slower: 2.8 vs 3.7 TB/s, r2.)
+//   128 KiB of LDS, one workgroup of up to 16 waves per CU.
+//   Columns are then aligned with one GF(2) multiply by x^(8*16*(63-l)) mod
+//   P and folded with a 6-step xor butterfly — no cross-lane ordering, no
+//   serial dependency across lanes.  CRC linearity also turns the 0xFFFFFFFF
+//   initial value into an xor of the first data word.
 // A second kernel folds per-chunk CRCs into the CRC of the whole buffer
 // (zlib crc32_combine algebra: crc(A|B) = shift(crc(A), |B|) ^ crc(B)).
 #include <hip/hip_runtime.h>
@@ -94,107 +103,149 @@ __device__ __forceinline__ uint32_t xpow8n(uint64_t n) {
   return p;
 }
 
-struct Lds {
-  uint32_t T[16][256];
-  uint32_t X[4][256];
-};
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int kCopies = 16;                    // lanes l and l+16 share a copy
+constexpr int kTables = 8;                     // T0..T3 (slicing-by-4), X0..X3 (shift1K)
+constexpr int kLdsWords = kTables * 256 * kCopies;   // 128 KiB
 
-__device__ __forceinline__ uint32_t r16(const Lds &s, uint4 w) {
-  uint32_t r = 0;
-  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    r ^= s.T[15 - 4 * i][v[i] & 0xff];
-    r ^= s.T[14 - 4 * i][(v[i] >> 8) & 0xff];
-    r ^= s.T[13 - 4 * i][(v[i] >> 16) & 0xff];
-    r ^= s.T[12 - 4 * i][v[i] >> 24];
-  }
-  return r;
+// table k (0..3 = T, 4..7 = X), entry b, from this lane's copy
+__device__ __forceinline__ uint32_t tab(const uint32_t *lds, uint32_t k, uint32_t b, uint32_t cp) {
+  return lds[((k << 8) + b) * kCopies + cp];
 }
 
-__device__ __forceinline__ uint32_t shift1k(const Lds &s, uint32_t a) {
-  return s.X[0][a & 0xff] ^ s.X[1][(a >> 8) & 0xff] ^ s.X[2][(a >> 16) & 0xff] ^ s.X[3][a >> 24];
+// zero-init CRC of a 16-byte piece (words in memory order)
+__device__ __forceinline__ uint32_t r16(const uint32_t *lds, uint32_t cp, uint4 w) {
+  const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = c ^ v[i];
+    c = tab(lds, 3, x & 0xff, cp) ^ tab(lds, 2, (x >> 8) & 0xff, cp) ^
+        tab(lds, 1, (x >> 16) & 0xff, cp) ^ tab(lds, 0, x >> 24, cp);
+  }
+  return c;
+}
+
+// append 1024 zero bytes
+__device__ __forceinline__ uint32_t shift1k(const uint32_t *lds, uint32_t cp, uint32_t a) {
+  return tab(lds, 4, a & 0xff, cp) ^ tab(lds, 5, (a >> 8) & 0xff, cp) ^
+         tab(lds, 6, (a >> 16) & 0xff, cp) ^ tab(lds, 7, a >> 24, cp);
 }
 
 // append b (< 16) zero bytes
-__device__ __forceinline__ uint32_t zshift(const Lds &s, uint32_t a, uint32_t b) {
-  for (uint32_t j = 0; j < b; ++j) a = (a >> 8) ^ s.T[0][a & 0xff];
+__device__ __forceinline__ uint32_t zshift(const uint32_t *lds, uint32_t cp, uint32_t a, uint32_t b) {
+  for (uint32_t j = 0; j < b; ++j) a = (a >> 8) ^ tab(lds, 0, a & 0xff, cp);
   return a;
 }
 
-__global__ __launch_bounds__(256) void crc32c_chunks_kernel(const uint8_t *__restrict__ in,
-                                                            uint64_t n, uint32_t chunk,
-                                                            uint32_t nchunks,
-                                                            uint32_t *__restrict__ out) {
-  __shared__ Lds s;
-  {
-    const uint32_t *srcT = &g_crc.T[0][0];
-    uint32_t *dstT = &s.T[0][0];
-    for (int i = threadIdx.x; i < 16 * 256; i += 256) dstT[i] = srcT[i];
-    const uint32_t *srcX = &g_crc.X[0][0];
-    uint32_t *dstX = &s.X[0][0];
-    for (int i = threadIdx.x; i < 4 * 256; i += 256) dstX[i] = srcX[i];
+constexpr int kWaves = 16;                  // 1024-thread workgroups
+constexpr int kRows = 8;                    // rows in flight per lane
+
+// CRC register state after the bytes p[0, L) (init = ~0 when `first`, else
+// 0 — the caller combines parts with crc(A|B) = shift(crc(A), |B|) ^ crc(B))
+// computed by one wave; every lane returns the same value.
+__device__ uint32_t wave_crc(const uint32_t *lds, uint32_t lane, uint32_t cp, const uint8_t *p,
+                             uint32_t L, bool first) {
+  if (L < 4) {
+    uint32_t st = first ? 0xffffffffu : 0u;
+    for (uint32_t j = 0; j < L; ++j) st = (st >> 8) ^ tab(lds, 0, (st ^ p[j]) & 0xff, cp);
+    return st;
+  }
+  const uint32_t nfull = L >> 10;
+  uint32_t a = 0;
+  uint32_t r = 0;
+  for (; r + kRows <= nfull; r += kRows) {
+    uint4 w[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const v4u x = __builtin_nontemporal_load((const v4u *)(p + (uint64_t)(r + k) * 1024 + lane * 16));
+      w[k] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (first && r == 0 && lane == 0) w[0].x ^= 0xffffffffu;
+    uint32_t rr[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) rr[k] = r16(lds, cp, w[k]);
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) a = shift1k(lds, cp, a) ^ rr[k];
+  }
+  for (; r < nfull; ++r) {
+    uint4 w = *(const uint4 *)(p + (uint64_t)r * 1024 + lane * 16);
+    if (first && r == 0 && lane == 0) w.x ^= 0xffffffffu;
+    a = shift1k(lds, cp, a) ^ r16(lds, cp, w);
+  }
+  const uint32_t full = nfull ? wave_xor(multmodp(g_crc.sh16[63 - lane], a)) : 0u;
+  const uint32_t rest = L - nfull * 1024;
+  if (!rest) return full;
+  const uint32_t q = rest >> 4, b = rest & 15;
+  const uint8_t *rp = p + (uint64_t)nfull * 1024;
+  const bool head = first && nfull == 0;
+  uint32_t contrib = 0;
+  if (lane < q) {
+    uint4 w = *(const uint4 *)(rp + lane * 16);
+    if (head && lane == 0) w.x ^= 0xffffffffu;
+    contrib = zshift(lds, cp, multmodp(g_crc.sh16[q - 1 - lane], r16(lds, cp, w)), b);
+  } else if (lane == q && b) {
+    uint32_t st = 0;
+    for (uint32_t j = 0; j < b; ++j) {
+      uint32_t byte = rp[lane * 16 + j];
+      if (head && q == 0 && j < 4) byte ^= 0xffu;
+      st = (st >> 8) ^ tab(lds, 0, (st ^ byte) & 0xff, cp);
+    }
+    contrib = st;
+  }
+  contrib = wave_xor(contrib);
+  return zshift(lds, cp, multmodp(g_crc.sh16[q], full), b) ^ contrib;
+}
+
+// Two schedules over the same per-wave body:
+//   split = 0: one wave per chunk, grid-stride over chunks (many chunks);
+//   split = 1: one workgroup per chunk, each wave CRCs a contiguous 1-KiB-
+//              aligned part and the parts are folded in LDS (few, large
+//              chunks: 1 MiB chunks over 1 GiB are only 4 waves per CU in
+//              wave mode).
+__global__ __launch_bounds__(1024) void crc32c_chunks_kernel(const uint8_t *__restrict__ in,
+                                                             uint64_t n, uint32_t chunk,
+                                                             uint32_t nchunks, int split,
+                                                             uint32_t *__restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint32_t parts[kWaves];
+  // fill: table word e = k*256 + b is loaded once and stored as its 16
+  // contiguous copies (4 x ds_write_b128)
+  for (uint32_t e = threadIdx.x; e < kTables * 256; e += blockDim.x) {
+    const uint32_t v = e < 1024 ? g_crc.T[e >> 8][e & 255] : g_crc.X[(e >> 8) - 4][e & 255];
+    const uint4 q = make_uint4(v, v, v, v);
+    uint4 *dst = (uint4 *)(lds + e * kCopies);
+#pragma unroll
+    for (int j = 0; j < kCopies / 4; ++j) dst[j] = q;
   }
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * 4;
-  for (uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6); c < nchunks; c += nwaves) {
+  const uint32_t lane = threadIdx.x & 63, cp = lane & 15, wv = threadIdx.x >> 6;
+  const uint32_t wpb = blockDim.x >> 6;
+  if (!split) {
+    const uint32_t nwaves = gridDim.x * wpb;
+    for (uint32_t c = blockIdx.x * wpb + wv; c < nchunks; c += nwaves) {
+      const uint64_t base = (uint64_t)c * chunk;
+      const uint32_t L = (uint32_t)min<uint64_t>(chunk, n - base);
+      const uint32_t crc = ~wave_crc(lds, lane, cp, in + base, L, true);
+      if (lane == 0) out[c] = crc;
+    }
+    return;
+  }
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {   // uniform per workgroup
     const uint64_t base = (uint64_t)c * chunk;
     const uint32_t L = (uint32_t)min<uint64_t>(chunk, n - base);
-    const uint8_t *p = in + base;
-    uint32_t crc;
-    if (L < 4) {
-      uint32_t st = 0xffffffffu;
-      for (uint32_t j = 0; j < L; ++j) st = (st >> 8) ^ s.T[0][(st ^ p[j]) & 0xff];
-      crc = ~st;
-    } else {
-      const uint32_t nfull = L >> 10;
-      uint32_t a = 0;
+    const uint32_t plen = (((L + wpb - 1) / wpb) + 1023u) & ~1023u;
+    const uint32_t lo = min(L, wv * plen), hi = min(L, lo + plen);
+    uint32_t v = hi > lo ? wave_crc(lds, lane, cp, in + base + lo, hi - lo, wv == 0) : 0u;
+    if (hi > lo && hi < L) v = multmodp(xpow8n(L - hi), v);
+    if (lane == 0) parts[wv] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
       uint32_t r = 0;
-      // 4 rows in flight per lane
-      for (; r + 4 <= nfull; r += 4) {
-        uint4 w0 = *(const uint4 *)(p + (uint64_t)(r + 0) * 1024 + lane * 16);
-        uint4 w1 = *(const uint4 *)(p + (uint64_t)(r + 1) * 1024 + lane * 16);
-        uint4 w2 = *(const uint4 *)(p + (uint64_t)(r + 2) * 1024 + lane * 16);
-        uint4 w3 = *(const uint4 *)(p + (uint64_t)(r + 3) * 1024 + lane * 16);
-        if (r == 0 && lane == 0) w0.x ^= 0xffffffffu;
-        a = shift1k(s, a) ^ r16(s, w0);
-        a = shift1k(s, a) ^ r16(s, w1);
-        a = shift1k(s, a) ^ r16(s, w2);
-        a = shift1k(s, a) ^ r16(s, w3);
-      }
-      for (; r < nfull; ++r) {
-        uint4 w = *(const uint4 *)(p + (uint64_t)r * 1024 + lane * 16);
-        if (r == 0 && lane == 0) w.x ^= 0xffffffffu;
-        a = shift1k(s, a) ^ r16(s, w);
-      }
-      uint32_t full = nfull ? wave_xor(multmodp(g_crc.sh16[63 - lane], a)) : 0u;
-      const uint32_t rest = L - nfull * 1024;
-      uint32_t res = full;
-      if (rest) {
-        const uint32_t q = rest >> 4, b = rest & 15;
-        const uint8_t *rp = p + (uint64_t)nfull * 1024;
-        const bool first = nfull == 0;
-        uint32_t contrib = 0;
-        if (lane < q) {
-          uint4 w = *(const uint4 *)(rp + lane * 16);
-          if (first && lane == 0) w.x ^= 0xffffffffu;
-          contrib = zshift(s, multmodp(g_crc.sh16[q - 1 - lane], r16(s, w)), b);
-        } else if (lane == q && b) {
-          uint32_t st = 0;
-          for (uint32_t j = 0; j < b; ++j) {
-            uint32_t byte = rp[lane * 16 + j];
-            if (first && q == 0 && j < 4) byte ^= 0xffu;
-            st = (st >> 8) ^ s.T[0][(st ^ byte) & 0xff];
-          }
-          contrib = st;
-        }
-        contrib = wave_xor(contrib);
-        res = zshift(s, multmodp(g_crc.sh16[q], full), b) ^ contrib;
-      }
-      crc = ~res;
+      for (uint32_t k = 0; k < wpb; ++k) r ^= parts[k];
+      out[c] = ~r;
     }
-    if (lane == 0) out[c] = crc;
+    __syncthreads();
   }
 }
 
@@ -249,11 +300,30 @@ extern "C" int strom_crc32c_chunks(const void *d_in, uint64_t nbytes, uint32_t c
   if (nbytes == 0) return 0;
   uint64_t nch = (nbytes + chunk - 1) / chunk;
   if (nch > 0xffffffffull) return -22;
-  uint32_t waves_needed = (uint32_t)nch;
-  uint32_t grid = (waves_needed + 3) / 4;
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                     (const uint8_t *)d_in, nbytes, chunk, (uint32_t)nch, d_out);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void *)crc32c_chunks_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLdsWords * 4);
+    attr_set = true;
+  }
+  // one workgroup per CU holds the 128 KiB tables.  Enough chunks for 8+
+  // waves per CU: one wave per chunk, up to 16 waves per workgroup; fewer,
+  // larger chunks: a 16-wave workgroup per chunk.
+  const bool split = nch < 256ull * 8 && chunk >= 16384;
+  uint32_t wpb, grid;
+  if (split) {
+    wpb = kWaves;
+    grid = (uint32_t)(nch < 256 ? nch : 256);
+  } else {
+    wpb = (uint32_t)((nch + 255) / 256);
+    if (wpb > kWaves) wpb = kWaves;
+    if (wpb < 1) wpb = 1;
+    grid = (uint32_t)((nch + wpb - 1) / wpb);
+    if (grid > 256) grid = 256;
+  }
+  hipLaunchKernelGGL(crc32c_chunks_kernel, dim3(grid), dim3(64 * wpb), kLdsWords * 4,
+                     (hipStream_t)stream, (const uint8_t *)d_in, nbytes, chunk, (uint32_t)nch,
+                     (int)split, d_out);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 

@@ -25,7 +25,11 @@ def _dev(a):
 
 @pytest.mark.parametrize("n,chunk", [(1, 16), (3, 16), (4, 16), (17, 16), (1000, 1024),
                                      (8192 * 5 + 77, 8192), (1 << 20, 1 << 20),
-                                     ((3 << 20) + 4096 + 5, 1 << 16), (100000, 4096)])
+                                     ((3 << 20) + 4096 + 5, 1 << 16), (100000, 4096),
+                                     # workgroup-per-chunk schedule: parts of 1-KiB rows,
+                                     # a 2-byte last part, a 3-byte tail chunk
+                                     ((5 << 20) + 16386, 1 << 20), ((1 << 20) + 3, 1 << 20),
+                                     (3 * 20000 + 7, 20000)])
 def test_crc32c_chunks_vs_host(S, n, chunk):
     from nvme_strom_amd.ops import verify as V
     data = np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8)

@@ -1,0 +1,47 @@
+#!/bin/bash
+# GPU-box passes, run through gpurun from the repo root:
+#   gpurun -- bash tools/gpu.sh TAG PHASE [PHASE...]
+# Phases (each under its own time limit; the first failure ends the call):
+#   tests      pytest -m gpu (one process)
+#   ktests     GPU kernel numerics only (crc/heap/decoder/filter tests)
+#   smoke      __graft_entry__.smoke()
+#   bench      python bench.py (default flagship config)
+#   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
+#   ktrace     rocprofv3 kernel trace + stats of a short kbench
+#   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
+#   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
+#   arrow      config-5 Arrow scan bench (tools.arrow_bench)
+# Output lands in gpurun_out/TAG/.
+set -o pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
+ROOT=$PWD
+step() {
+  local name=$1 limit=$2; shift 2
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.log"; exit $rc; fi
+}
+for phase in "$@"; do
+  case $phase in
+    tests) step tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    ktests) step ktests 300 python -u -m pytest tests/test_gpu_core.py tests/test_gpu_kernels.py -m gpu -x -q \
+              --timeout 120 --timeout-method thread -k "crc or heap or lz4 or snappy or malformed or filter or compact" ;;
+    smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
+    kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
+    ktrace) (cd /tmp && step ktrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o trace \
+              -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5) ;;
+    kpmc) (cd /tmp && step kpmc 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
+              SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$ROOT/$OUT/pmc" -o pmc \
+              -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only crc,heap,lz4) ;;
+    sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
+    arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
+    *) echo "unknown phase $phase"; exit 2 ;;
+  esac
+done
+echo done
