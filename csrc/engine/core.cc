@@ -37,7 +37,7 @@ Config Config::from_env() {
                                "bar_map", "bar_max", "coalesce", "trace",
                                "ingest", "ingest_grid", "ingest_piece", "hdp_sync",
                                "strict", "direct_io",
-                               "pgcache_probe", "gpu_emulation", "numa_bind",
+                               "pgcache_probe", "gpu_emulation", "numa_bind", "check_freed",
                                "stat_info", "verbose"};
   for (const char *k : keys) {
     std::string env = "STROM_";
@@ -68,6 +68,7 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "pgcache_probe") { pgcache_probe = parse_bool(v); return 0; }
   if (k == "gpu_emulation") { gpu_emulation = parse_bool(v); return 0; }
   if (k == "numa_bind") { numa_bind = parse_bool(v); return 0; }
+  if (k == "check_freed") { check_freed = parse_bool(v); return 0; }
   if (!num_ok) return -EINVAL;
   if (k == "workers") { if (n < 1 || n > 256) return -EINVAL; workers = (int)n; return 0; }
   if (k == "queue_depth") { if (n < 1 || n > 4096) return -EINVAL; queue_depth = (int)n; return 0; }
@@ -136,6 +137,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "pgcache_probe") v = pgcache_probe;
   else if (k == "gpu_emulation") v = gpu_emulation;
   else if (k == "numa_bind") v = numa_bind;
+  else if (k == "check_freed") v = check_freed;
   else if (k == "stat_info") v = stat_info;
   else if (k == "verbose") v = verbose;
   else return -ENOENT;

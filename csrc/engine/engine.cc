@@ -267,6 +267,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   if (!a->chunk_ids) return -EFAULT;
   auto gmap = gpu_registry().get(a->handle);
   if (!gmap) return -ENOENT;
+  if (int v = gpu_registry().validate(gmap)) return v;
   uint64_t bytes = (uint64_t)a->nr_chunks * a->chunk_sz;
   if (gmap->map_offset + a->offset + bytes > gmap->map_length) return -ERANGE;
   int err = 0;
@@ -342,6 +343,7 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
   auto gmap = gpu_registry().get(handle);
   if (!gmap) return -ENOENT;
+  if (int v = gpu_registry().validate(gmap)) return v;
   if (gmap->map_offset + offset + len > gmap->map_length) return -ERANGE;
   int err = 0;
   auto f = open_file(fd, &err);
@@ -823,6 +825,32 @@ int strom_host_costs(int fd, uint64_t *out, int n) {
   out[6] = bench([&] { cv.notify_all(); });
   return 0;
 }
+
+// SSD2RAM destinations: mmap a DMA-buffer fd through the engine so the
+// range sits in the registry's address index (no VMA query per request).
+// Kernel provider: a plain mmap of the kernel's buffer fd.
+void *strom_dmabuf_mmap(int fd, size_t length) {
+  void *p = nullptr;
+  if (kernel_fd() >= 0) {
+    p = mmap(nullptr, length, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    return p == MAP_FAILED ? nullptr : p;
+  }
+  int rc = dmabuf_registry().map(fd, length, &p);
+  if (rc) {
+    errno = -rc;
+    return nullptr;
+  }
+  return p;
+}
+
+int strom_dmabuf_munmap(void *addr, size_t length) {
+  if (kernel_fd() >= 0) return munmap(addr, length) == 0 ? 0 : -errno;
+  return dmabuf_registry().unmap(addr, length);
+}
+
+int strom_dmabuf_gc(void) { return dmabuf_registry().gc(); }
+
+long strom_gpu_detached(void) { return (long)gpu_registry().detached_count(); }
 
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset) {
   if (!hip::available()) return -ENODEV;

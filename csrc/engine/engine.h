@@ -70,6 +70,8 @@ struct Config {
   bool pgcache_probe = true;     // residency scoring (mincore)
   bool gpu_emulation = false;    // accept host memory as "GPU" (CPU tests)
   bool numa_bind = true;         // pin workers near the GPU / SSD
+  bool check_freed = true;       // re-check a mapping's allocation identity per
+                                 // SSD2GPU (freed / recycled range -> -ENOENT)
   int stat_info = 1;             // 0 off, 1 on, 2 +debug fields
   int verbose = 0;
   bool trace = false;            // roctx ranges around engine calls
@@ -177,6 +179,10 @@ struct GpuMapping {
   uid_t owner = 0;
   int dmabuf_fd = -1;
   uint32_t version = 1;
+  // identity of the allocation behind the range, taken at MAP time and
+  // re-checked per request (GpuRegistry::validate): the HIP buffer id of a
+  // device allocation, or the covering VMA of emulated (host) memory
+  uint64_t ident = 0;
   // Large-BAR CPU mapping of the range (dma-buf export + mmap), or null.
   // bar_va is the device VA that bar[0] aliases.
   uint8_t *bar = nullptr;
@@ -207,37 +213,66 @@ class GpuRegistry {
   int list(strom_list_gpu_memory *out);
   int info(strom_info_gpu_memory *out);
   std::shared_ptr<GpuMapping> get(unsigned long handle);
+  // 0 while the allocation that was mapped still backs the range; else the
+  // mapping is detached (like the reference's free callback,
+  // kmod/pmemmap.c:150-208) and -ENOENT returned
+  int validate(const std::shared_ptr<GpuMapping> &m);
+  uint64_t detached_count() const { return detached_.load(); }
 
  private:
   std::mutex mu_;
   std::map<unsigned long, std::shared_ptr<GpuMapping>> maps_;
   unsigned long next_ = 0x5350000000000000ul;  // 'S','P' tag + counter
+  std::atomic<uint64_t> detached_{0};
 };
 
 GpuRegistry &gpu_registry();
 
 // ----------------------------------------------------- DMA buffer registry
 struct DmaBuffer {
-  int fd = -1;                // our own reference (user gets a dup)
   dev_t dev = 0;
   ino_t ino = 0;
   size_t length = 0;
   int node = -1;
-  void *self_map = nullptr;   // engine-side mapping (keeps pages alive)
-  ~DmaBuffer();
 };
+
+// Which VMA covers an address (PROCMAP_QUERY on /proc/self/maps, Linux
+// >= 6.11, else a text scan): the userspace find_vma().
+struct VmaInfo {
+  uint64_t start = 0, end = 0, pgoff = 0, ino = 0;
+  dev_t dev = 0;
+  bool dmabuf = false;   // a mapping of one of our "strom-dmabuf" memfds
+};
+// 0 and *out filled; -ENOENT nothing mapped at addr; other -errno on failure
+int vma_query(uint64_t addr, VmaInfo *out);
 
 class DmaBufRegistry {
  public:
   int alloc(size_t length, int node, int *user_fd);
   // Resolve a user VA range to (buffer, byte offset).  -EINVAL when the
   // range is not inside an ALLOC_DMA_BUFFER mapping (find_vma analogue).
+  // Mappings made through map() are found in an address index without a
+  // syscall; others (a caller's own mmap of the fd) by one VMA query.
   int resolve(const void *uaddr, size_t len, std::shared_ptr<DmaBuffer> *buf,
               size_t *offset);
+  // mmap a DMA-buffer fd (MAP_SHARED) and index the range / drop it again
+  int map(int fd, size_t len, void **addr);
+  int unmap(void *addr, size_t len);
+  // Drop buffers no fd and no mapping of this process refers to any more
+  // (the fd-close analogue of the reference's anon-inode release); returns
+  // the number still registered
+  int gc();
+  size_t count();
 
  private:
+  struct Range {
+    uint64_t end;
+    size_t pgoff;
+    std::shared_ptr<DmaBuffer> buf;
+  };
   std::mutex mu_;
   std::map<std::pair<dev_t, ino_t>, std::shared_ptr<DmaBuffer>> bufs_;
+  std::map<uint64_t, Range> ranges_;   // start -> engine-made mapping
 };
 
 DmaBufRegistry &dmabuf_registry();
@@ -415,6 +450,8 @@ int export_dmabuf(uint64_t va, size_t len, int *fd, uint64_t *offset, int *devic
 int copy_dtoh(void *dst, uint64_t src, size_t len);   // synchronous, 0 / -EIO
 int copy_htod(uint64_t dst, const void *src, size_t len);
 int numa_node_of_device(int device);
+// unique id of the live allocation holding va (HIP buffer id), 0 if none
+uint64_t buffer_id(uint64_t va);
 }  // namespace hip
 
 // -------------------------------------------------------------- engine

@@ -118,6 +118,49 @@ void host_free_thp(void *p, size_t bytes) {
   munmap(p, len);
 }
 
+// The CPU alias of HBM through a dma-buf mmap needs a large BAR (or the
+// driver falls back to something the GPU does not see).  Checked ONCE per
+// device on a private 64 KiB allocation — never by storing into a user's
+// live tensor, which kernels on other streams may be using.
+static bool bar_alias_ok(int device) {
+  static std::mutex mu;
+  static std::map<int, bool> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  bool ok = false;
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  void *probe = nullptr;
+  const size_t len = 64u << 10;
+  if (hipSetDevice(device) == hipSuccess && hipMalloc(&probe, len) == hipSuccess) {
+    int fd = -1;
+    if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)probe, len,
+                                       hipMemRangeHandleTypeDmaBufFd, 0) == hipSuccess &&
+        fd >= 0) {
+      void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+      if (p != MAP_FAILED) {
+        const uint64_t canary = 0x5354524f4d424152ull ^ (uint64_t)probe;
+        uint64_t back = 0;
+        volatile uint64_t *q = (volatile uint64_t *)((uint8_t *)p + 4096);
+        *q = canary;
+        _mm_sfence();
+        (void)*q;  // drains the posted write
+        ok = hipMemcpy(&back, (uint8_t *)probe + 4096, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+             back == canary;
+        munmap(p, len);
+      }
+    }
+    (void)hipFree(probe);
+  }
+  (void)hipGetLastError();
+  if (cur >= 0) (void)hipSetDevice(cur);
+  STROM_LOG(1, "device %d: BAR alias of HBM %s", device, ok ? "verified" : "unusable");
+  cache[device] = ok;
+  return ok;
+}
+
 uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
   // Export the WHOLE allocation (caching allocators sub-allocate tensors
   // inside larger hipMalloc blocks) and map the page-aligned cover of the
@@ -129,6 +172,13 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
     (void)hipGetLastError();
     return nullptr;
   }
+  hipPointerAttribute_t attr;
+  memset(&attr, 0, sizeof attr);
+  if (hipPointerGetAttributes(&attr, (void *)va) != hipSuccess || attr.type != hipMemoryTypeDevice) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (!bar_alias_ok(attr.device)) return nullptr;
   uint64_t base = (uint64_t)abase;
   uint64_t lo = va & ~(page - 1);
   uint64_t hi = (va + len + page - 1) & ~(page - 1);
@@ -145,30 +195,21 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
   void *p = mmap(nullptr, hi - lo, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)(lo - base));
   close(fd);  // the mapping keeps the dma-buf alive
   if (p == MAP_FAILED) return nullptr;
-  const uint64_t t2 = mono_ns();
-  // Self-check with a canary: the CPU alias must be the bytes the GPU sees.
-  uint8_t *q = (uint8_t *)p + (va - lo);
-  uint64_t orig = 0, canary = 0x5354524f4d424152ull ^ va, back = 0;
-  bool ok = hipMemcpy(&orig, (void *)va, 8, hipMemcpyDeviceToHost) == hipSuccess;
-  if (ok) {
-    memcpy(q, &canary, 8);
-    _mm_sfence();
-    (void)*(volatile uint32_t *)q;
-    ok = hipMemcpy(&back, (void *)va, 8, hipMemcpyDeviceToHost) == hipSuccess && back == canary;
-    memcpy(q, &orig, 8);
-    _mm_sfence();
-    (void)*(volatile uint32_t *)q;
-  }
-  if (!ok) {
-    (void)hipGetLastError();
-    munmap(p, hi - lo);
-    return nullptr;
-  }
-  STROM_LOG(1, "bar_map %zu MiB: export %.2f ms, mmap %.2f ms, canary %.2f ms", asize >> 20,
-            (t1 - t0) / 1e6, (t2 - t1) / 1e6, (mono_ns() - t2) / 1e6);
+  STROM_LOG(1, "bar_map %zu MiB: export %.2f ms, mmap %.2f ms", asize >> 20, (t1 - t0) / 1e6,
+            (mono_ns() - t1) / 1e6);
   *map_va = lo;
   *map_len = hi - lo;
   return (uint8_t *)p;
+}
+
+uint64_t buffer_id(uint64_t va) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)va) !=
+      hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)id;
 }
 
 namespace {

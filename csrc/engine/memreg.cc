@@ -10,14 +10,30 @@
 // INFO returns per-page device addresses; the kmod fills bus addresses
 // from the imported dma-buf sg_table instead.
 //
+// A freed allocation is detected per request: MAP records the identity of
+// the allocation (HIP buffer id), SSD2GPU re-reads it, and a mismatch (the
+// range was hipFree'd, or freed and re-allocated at the same VA) detaches
+// the mapping with -ENOENT instead of writing into whatever now lives there
+// (reference: nvidia's free callback, kmod/pmemmap.c:150-208).  Ranges a
+// caching allocator recycles INSIDE one live hipMalloc block keep their
+// identity — exactly what the reference's callback saw too.
+//
 // DmaBufRegistry replaces the anon-inode DMA buffer (pmemmap.c:497-717):
 // a memfd named "strom-dmabuf<node>:<size>", whose shared NUMA policy is
 // bound to the requested node and whose pages are pre-faulted there.  The
-// SSD2RAM destination check is the find_vma()/f_op test re-done against
-// /proc/self/maps: the address range must lie inside a mapping of one of
-// our memfds, and the byte offset is vm_pgoff + (uaddr - vm_start).
+// SSD2RAM destination check is the find_vma()/f_op test: mappings made
+// through DmaBufRegistry::map sit in an address index (no syscall); any
+// other address is looked up with one PROCMAP_QUERY ioctl on
+// /proc/self/maps (Linux >= 6.11; a text scan before that).  The range must
+// lie inside a mapping of one of our memfds, and the byte offset is
+// vm_pgoff + (uaddr - vm_start).  Buffers nothing refers to any more are
+// dropped by gc() (run on every ALLOC_DMA_BUFFER).
+#include <dirent.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <linux/ioctl.h>
+#include <sys/ioctl.h>
+#include <sys/sysmacros.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -26,8 +42,7 @@
 #include <unistd.h>
 #include <x86intrin.h>
 
-#include <fstream>
-#include <sstream>
+#include <set>
 
 #include "engine.h"
 
@@ -95,6 +110,9 @@ int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memor
   m->device = device;
   m->owner = geteuid();
   m->dmabuf_fd = dmabuf_fd;
+  // identity: the HIP buffer id; emulated (host) memory has none that
+  // survives VMA merges, so there it is "both ends still mapped"
+  m->ident = device >= 0 ? hip::buffer_id(va) : 1;
   uint64_t npages = (m->map_length + STROM_GPU_BOUND_SIZE - 1) >> STROM_GPU_BOUND_SHIFT;
   if (npages > 0xffffffffull) return -E2BIG;
   if (device >= 0 && config().bar_map) {
@@ -120,6 +138,30 @@ std::shared_ptr<GpuMapping> GpuRegistry::get(unsigned long handle) {
   auto it = maps_.find(handle);
   if (it == maps_.end() || it->second->owner != geteuid()) return nullptr;
   return it->second;
+}
+
+int GpuRegistry::validate(const std::shared_ptr<GpuMapping> &m) {
+  if (!config().check_freed || m->ident == 0) return 0;
+  uint64_t now = 0;
+  if (m->device >= 0) {
+    now = hip::buffer_id(m->va);
+    // the range must still end inside the allocation (a smaller one at the
+    // same VA has a new id anyway)
+  } else {
+    VmaInfo v;
+    if (vma_query(m->va, &v) == 0 && vma_query(m->va + m->length - 1, &v) == 0) now = 1;
+  }
+  if (now == m->ident) return 0;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = maps_.find(m->handle);
+    if (it != maps_.end() && it->second == m) maps_.erase(it);
+  }
+  m->detached = true;
+  detached_.fetch_add(1);
+  STROM_LOG(0, "mapping %#lx (va %#lx): allocation freed or replaced, detached", m->handle,
+            (unsigned long)m->va);
+  return -ENOENT;
 }
 
 int GpuRegistry::unmap(unsigned long handle) {
@@ -176,16 +218,91 @@ GpuRegistry &gpu_registry() {
 }
 
 // ---------------------------------------------------------- DMA buffers
-DmaBuffer::~DmaBuffer() {
-  if (self_map) munmap(self_map, length);
-  if (fd >= 0) close(fd);
+namespace {
+constexpr const char kDmaBufName[] = "strom-dmabuf";
+
+// struct procmap_query / PROCMAP_QUERY of <linux/fs.h> (Linux 6.11+), kept
+// here so the build does not depend on the installed headers
+struct ProcmapQuery {
+  uint64_t size, query_flags, query_addr;
+  uint64_t vma_start, vma_end, vma_flags, vma_page_size, vma_offset, inode;
+  uint32_t dev_major, dev_minor, vma_name_size, build_id_size;
+  uint64_t vma_name_addr, build_id_addr;
+};
+static_assert(sizeof(ProcmapQuery) == 104, "procmap_query layout");
+constexpr unsigned long kProcmapQuery = _IOWR('f', 17, ProcmapQuery);
+
+std::atomic<int> g_maps_fd{-2};  // -2 not opened, -1 no PROCMAP_QUERY
+
+int vma_query_scan(uint64_t a, VmaInfo *out) {
+  FILE *f = fopen("/proc/self/maps", "r");
+  if (!f) return -errno;
+  char line[4096];
+  int rc = -ENOENT;
+  while (fgets(line, sizeof line, f)) {
+    unsigned long lo, hi, off, ino;
+    unsigned dmaj, dmin;
+    char perms[8];
+    int pos = 0;
+    if (sscanf(line, "%lx-%lx %7s %lx %x:%x %lu %n", &lo, &hi, perms, &off, &dmaj, &dmin, &ino,
+               &pos) < 7)
+      continue;
+    if (a < lo || a >= hi) continue;
+    out->start = lo;
+    out->end = hi;
+    out->pgoff = off;
+    out->ino = ino;
+    out->dev = makedev(dmaj, dmin);
+    out->dmabuf = strstr(line + pos, kDmaBufName) != nullptr;
+    rc = 0;
+    break;
+  }
+  fclose(f);
+  return rc;
+}
+}  // namespace
+
+int vma_query(uint64_t addr, VmaInfo *out) {
+  int fd = g_maps_fd.load(std::memory_order_acquire);
+  if (fd == -2) {
+    int nfd = open("/proc/self/maps", O_RDONLY | O_CLOEXEC);
+    int expect = -2;
+    if (!g_maps_fd.compare_exchange_strong(expect, nfd < 0 ? -1 : nfd)) {
+      if (nfd >= 0) close(nfd);
+    }
+    fd = g_maps_fd.load();
+  }
+  if (fd >= 0) {
+    char name[256];
+    ProcmapQuery q{};
+    q.size = sizeof q;
+    q.query_addr = addr;
+    q.vma_name_addr = (uint64_t)name;
+    q.vma_name_size = sizeof name;
+    if (ioctl(fd, kProcmapQuery, &q) == 0) {
+      out->start = q.vma_start;
+      out->end = q.vma_end;
+      out->pgoff = q.vma_offset;
+      out->ino = q.inode;
+      out->dev = makedev(q.dev_major, q.dev_minor);
+      out->dmabuf = q.vma_name_size > 0 && strstr(name, kDmaBufName) != nullptr;
+      return 0;
+    }
+    if (errno == ENOENT) return -ENOENT;
+    if (errno != ENOTTY && errno != EINVAL && errno != EOPNOTSUPP) return -errno;
+    // kernel without PROCMAP_QUERY: scan from now on
+    int expect = fd;
+    if (g_maps_fd.compare_exchange_strong(expect, -1)) close(fd);
+  }
+  return vma_query_scan(addr, out);
 }
 
 int DmaBufRegistry::alloc(size_t length, int node, int *user_fd) {
   if (length == 0) return -EINVAL;
   size_t len = (length + STROM_DMABUF_SEGMENT - 1) / STROM_DMABUF_SEGMENT * STROM_DMABUF_SEGMENT;
+  (void)gc();
   char name[64];
-  snprintf(name, sizeof name, "strom-dmabuf%d:%zu", node, len);
+  snprintf(name, sizeof name, "%s%d:%zu", kDmaBufName, node, len);
   int fd = (int)syscall(SYS_memfd_create, name, 0u);
   if (fd < 0) return -errno;
   if (ftruncate(fd, (off_t)len) != 0) {
@@ -219,48 +336,118 @@ int DmaBufRegistry::alloc(size_t length, int node, int *user_fd) {
   b->ino = st.st_ino;
   b->length = len;
   b->node = node;
-  int ufd = fd;
   {
     std::lock_guard<std::mutex> g(mu_);
     bufs_[{b->dev, b->ino}] = b;
   }
-  *user_fd = ufd;
+  *user_fd = fd;
   return 0;
 }
 
 int DmaBufRegistry::resolve(const void *uaddr, size_t len, std::shared_ptr<DmaBuffer> *buf,
                             size_t *offset) {
-  uint64_t a = (uint64_t)uaddr;
-  FILE *f = fopen("/proc/self/maps", "r");
-  if (!f) return -errno;
-  char line[4096];
-  int rc = -EINVAL;
-  while (fgets(line, sizeof line, f)) {
-    unsigned long lo, hi, off, ino;
-    unsigned dmaj, dmin;
-    char perms[8];
-    int pos = 0;
-    if (sscanf(line, "%lx-%lx %7s %lx %x:%x %lu %n", &lo, &hi, perms, &off, &dmaj, &dmin, &ino,
-               &pos) < 7)
-      continue;
-    if (a < lo || a >= hi) continue;
-    const char *path = line + pos;
-    if (!strstr(path, "strom-dmabuf")) break;        // wrong kind of mapping
-    if (a + len > hi) break;                         // crosses the VMA end
+  const uint64_t a = (uint64_t)uaddr;
+  if (a + len < a) return -EINVAL;
+  {
     std::lock_guard<std::mutex> g(mu_);
-    for (auto &kv : bufs_) {
-      if (kv.first.second != (ino_t)ino) continue;
-      size_t o = off + (a - lo);
-      if (o + len > kv.second->length) break;
-      *buf = kv.second;
-      *offset = o;
-      rc = 0;
-      break;
+    auto it = ranges_.upper_bound(a);
+    if (it != ranges_.begin()) {
+      --it;
+      if (a < it->second.end) {
+        if (a + len > it->second.end) return -EINVAL;  // crosses the mapping end
+        const size_t o = it->second.pgoff + (a - it->first);
+        if (o + len > it->second.buf->length) return -EINVAL;
+        *buf = it->second.buf;
+        *offset = o;
+        return 0;
+      }
     }
-    break;
   }
-  fclose(f);
-  return rc;
+  VmaInfo v;
+  int rc = vma_query(a, &v);
+  if (rc) return rc == -ENOENT ? -EINVAL : rc;
+  if (!v.dmabuf || a + len > v.end) return -EINVAL;  // wrong kind of mapping / crosses its end
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = bufs_.find({v.dev, (ino_t)v.ino});
+  if (it == bufs_.end()) return -EINVAL;
+  const size_t o = v.pgoff + (a - v.start);
+  if (o + len > it->second->length) return -EINVAL;
+  *buf = it->second;
+  *offset = o;
+  return 0;
+}
+
+int DmaBufRegistry::map(int fd, size_t len, void **addr) {
+  struct stat st;
+  if (fstat(fd, &st) != 0) return -errno;
+  std::shared_ptr<DmaBuffer> b;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = bufs_.find({st.st_dev, st.st_ino});
+    if (it == bufs_.end()) return -EINVAL;  // not one of ours
+    b = it->second;
+  }
+  if (len == 0 || len > b->length) return -EINVAL;
+  void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (p == MAP_FAILED) return -errno;
+  std::lock_guard<std::mutex> g(mu_);
+  ranges_[(uint64_t)p] = Range{(uint64_t)p + len, 0, b};
+  *addr = p;
+  return 0;
+}
+
+int DmaBufRegistry::unmap(void *addr, size_t len) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = ranges_.find((uint64_t)addr);
+    if (it == ranges_.end() || it->second.end - it->first != len) return -EINVAL;
+    ranges_.erase(it);
+  }
+  return munmap(addr, len) == 0 ? 0 : -errno;
+}
+
+int DmaBufRegistry::gc() {
+  // inodes this process still holds: open fds, then mappings
+  std::set<std::pair<dev_t, ino_t>> live;
+  if (DIR *d = opendir("/proc/self/fd")) {
+    while (struct dirent *e = readdir(d)) {
+      if (e->d_name[0] == '.') continue;
+      char path[64], tgt[256];
+      snprintf(path, sizeof path, "/proc/self/fd/%s", e->d_name);
+      ssize_t n = readlink(path, tgt, sizeof tgt - 1);
+      if (n <= 0) continue;
+      tgt[n] = 0;
+      struct stat st;
+      if (strstr(tgt, kDmaBufName) && stat(path, &st) == 0) live.insert({st.st_dev, st.st_ino});
+    }
+    closedir(d);
+  } else {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int)bufs_.size();  // cannot tell: keep everything
+  }
+  if (FILE *f = fopen("/proc/self/maps", "r")) {
+    char line[4096];
+    while (fgets(line, sizeof line, f)) {
+      if (!strstr(line, kDmaBufName)) continue;
+      unsigned long lo, hi, off, ino;
+      unsigned dmaj, dmin;
+      char perms[8];
+      if (sscanf(line, "%lx-%lx %7s %lx %x:%x %lu", &lo, &hi, perms, &off, &dmaj, &dmin, &ino) == 7)
+        live.insert({makedev(dmaj, dmin), (ino_t)ino});
+    }
+    fclose(f);
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = bufs_.begin(); it != bufs_.end();) {
+    if (live.count(it->first)) ++it;
+    else it = bufs_.erase(it);   // in-flight SSD2RAM tasks keep their shared_ptr
+  }
+  return (int)bufs_.size();
+}
+
+size_t DmaBufRegistry::count() {
+  std::lock_guard<std::mutex> g(mu_);
+  return bufs_.size();
 }
 
 DmaBufRegistry &dmabuf_registry() {

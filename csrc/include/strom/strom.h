@@ -78,6 +78,19 @@ int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
  * (MAP_GPU_DMABUF).  The caller closes the fd. */
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset);
 
+/* SSD2RAM destinations: mmap (MAP_SHARED, read/write) `length` bytes of an
+ * ALLOC_DMA_BUFFER fd through the engine, so the range is found in the
+ * registry's address index; NULL + errno on failure.  Unmap with
+ * strom_dmabuf_munmap.  A caller's own mmap of the fd works too (looked up
+ * by one PROCMAP_QUERY per request). */
+void *strom_dmabuf_mmap(int fd, size_t length);
+int strom_dmabuf_munmap(void *addr, size_t length);
+/* Drop DMA buffers no fd and no mapping of the process refers to any more;
+ * returns how many stay registered. */
+int strom_dmabuf_gc(void);
+/* Mappings detached because their allocation was freed or replaced. */
+long strom_gpu_detached(void);
+
 /* HBM ingest grid of a device (the persistent GPU pull kernel that moves
  * staged reads into HBM): out[4] = {available, grid launches, descriptors
  * posted, descriptors outstanding}.  -ENODEV when it cannot run there. */

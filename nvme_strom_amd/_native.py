@@ -161,6 +161,10 @@ _SIGS = {
     "strom_export_dmabuf": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_int),
                                       C.POINTER(C.c_uint64)]),
     "strom_ingest_info": (C.c_int, [C.c_int, C.c_void_p]),
+    "strom_dmabuf_mmap": (C.c_void_p, [C.c_int, C.c_size_t]),
+    "strom_dmabuf_munmap": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "strom_dmabuf_gc": (C.c_int, []),
+    "strom_gpu_detached": (C.c_long, []),
     "strom_host_costs": (C.c_int, [C.c_int, C.c_void_p, C.c_int]),
     "strom_config_set": (C.c_int, [C.c_char_p, C.c_char_p]),
     "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
@@ -216,7 +220,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise NativeMissing(
                 f"{LIB_PATH} not built: run `make -j16` or `python -m nvme_strom_amd.build`")
-        handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        handle = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL, use_errno=True)
         for name, (res, args) in _SIGS.items():
             fn = getattr(handle, name, None)
             if fn is None:

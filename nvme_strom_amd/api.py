@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import ctypes as C
 import errno as _errno
-import mmap
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -226,7 +225,10 @@ class DmaBuffer:
     """NUMA-local host buffer usable as an SSD2RAM destination.
 
     ``array`` is a writable numpy uint8 view of the mapping; ``address`` is
-    the mapping's VA (what MEMCPY_SSD2RAM takes as ``dest_uaddr``).
+    the mapping's VA (what MEMCPY_SSD2RAM takes as ``dest_uaddr``).  The
+    mapping is made by the engine (``strom_dmabuf_mmap``), so SSD2RAM finds
+    it in the registry's address index; ``array`` must not be used after
+    :meth:`close`.
     """
 
     def __init__(self, length: int, node: int = -1, sess: Optional[Session] = None):
@@ -235,18 +237,20 @@ class DmaBuffer:
         self.fd = a.dmabuf_fdesc
         self.length = os.fstat(self.fd).st_size
         self.node = node
-        self.mm = mmap.mmap(self.fd, self.length, flags=mmap.MAP_SHARED,
-                            prot=mmap.PROT_READ | mmap.PROT_WRITE)
-        self.array = np.frombuffer(self.mm, dtype=np.uint8)
-        self.address = self.array.ctypes.data
+        self._lib = N.lib()
+        addr = self._lib.strom_dmabuf_mmap(self.fd, self.length)
+        if not addr:
+            err = C.get_errno() or _errno.EINVAL
+            os.close(self.fd)
+            self.fd = -1
+            raise StromError(err, "strom_dmabuf_mmap")
+        self.address = int(addr)
+        self.array = np.ctypeslib.as_array((C.c_uint8 * self.length).from_address(self.address))
 
     def close(self) -> None:
         if self.fd >= 0:
             self.array = None
-            try:
-                self.mm.close()
-            except BufferError:
-                pass
+            self._lib.strom_dmabuf_munmap(self.address, self.length)
             os.close(self.fd)
             self.fd = -1
 
@@ -255,6 +259,16 @@ class DmaBuffer:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def dmabuf_gc() -> int:
+    """Drop DMA buffers nothing refers to any more; returns how many remain."""
+    return N.lib().strom_dmabuf_gc()
+
+
+def gpu_detached() -> int:
+    """Mappings detached because their allocation was freed or replaced."""
+    return N.lib().strom_gpu_detached()
 
 
 def alloc_dma_buffer(length: int, node: int = -1, sess: Optional[Session] = None) -> DmaBuffer:

@@ -283,3 +283,31 @@ def test_export_dmabuf_offsets(S):
     finally:
         for fd in fds:
             os.close(fd)
+
+
+def test_freed_allocation_detaches_mapping(S, tmp_path):
+    """hipFree of a mapped range (torch: del + empty_cache) is caught at the
+    next SSD2GPU: -ENOENT, handle gone (reference free callback,
+    kmod/pmemmap.c:150-208) — nothing is written into recycled memory."""
+    import errno
+    path = str(tmp_path / "f.bin")
+    with open(path, "wb") as f:
+        f.write(os.urandom(1 << 20))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        t = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
+        m = S.map_gpu_memory(t.data_ptr(), t.numel())
+        r = S.memcpy_ssd2gpu(m.handle, 0, fd, np.arange(4, dtype=np.uint32), 65536)
+        S.memcpy_wait(r.dma_task_id)
+        before = S.gpu_detached()
+        del t
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        with pytest.raises(S.StromError) as e:
+            S.memcpy_ssd2gpu(m.handle, 0, fd, np.arange(4, dtype=np.uint32), 65536)
+        assert e.value.errno == errno.ENOENT
+        assert S.gpu_detached() == before + 1
+        assert m.handle not in S.list_gpu_memory()
+        m.handle = 0
+    finally:
+        os.close(fd)
