@@ -115,9 +115,11 @@ int main(int argc, char **argv) {
     perror("ALLOC_DMA_BUFFER");
     return 1;
   }
-  char *buf = (char *)mmap(nullptr, ab.length, PROT_READ | PROT_WRITE, MAP_SHARED, ab.dmabuf_fdesc, 0);
-  if (buf == MAP_FAILED) {
-    perror("mmap");
+  // mapped through the engine: SSD2RAM then finds the destination in the
+  // registry's address index instead of querying the VMA per call
+  char *buf = (char *)strom_dmabuf_mmap(ab.dmabuf_fdesc, ab.length);
+  if (!buf) {
+    perror("strom_dmabuf_mmap");
     return 1;
   }
   std::atomic<size_t> cursor{0};

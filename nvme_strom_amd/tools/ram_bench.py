@@ -1,0 +1,79 @@
+"""SSD2RAM throughput against the raw storage ceiling (ssd2ram_test shape).
+
+The reference's ssd2ram_test streams a file in 1 MiB units of 8 KiB chunks
+into a NUMA-local DMA buffer from N threads (utils/ssd2ram_test.c:149-236).
+This runs the native ``ssd2ram_test`` (csrc/tools/ssd2ram_test.cc) over a
+fresh file and, on the same file, the engine-free ceiling: the same number
+of io_uring rings, as deep, reading 1 MiB O_DIRECT blocks in file order into
+host memory.  ``of_raw`` = SSD2RAM GiB/s / raw GiB/s.
+
+``python -m nvme_strom_amd.tools.ram_bench --out gpurun_out/ram.json``
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+
+from .sweep import _mk
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--file-gib", type=float, default=2.0)
+    ap.add_argument("--dir", default="/tmp/strom_ram")
+    ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--unit-kib", type=int, default=1024)
+    ap.add_argument("--buffer-mib", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    import nvme_strom_amd as S
+
+    os.makedirs(a.dir, exist_ok=True)
+    path = os.path.join(a.dir, "ram.bin")
+    F = int(a.file_gib * (1 << 30)) // (4 << 20) * (4 << 20)
+    _mk(path, F)
+    fd = os.open(path, os.O_RDONLY)
+    unit = a.unit_kib << 10
+    slots = max(1, (a.buffer_mib << 20) // a.threads // unit)
+    res = dict(file_bytes=F, threads=a.threads, unit_kib=a.unit_kib, slots_per_thread=slots,
+               engine_workers=int(S.config_get("workers")),
+               engine_queue_depth=int(S.config_get("queue_depth")), runs=[], raw=[])
+    try:
+        for _ in range(a.reps):
+            S.evict_file(fd)
+            out = subprocess.run([os.path.join(LIB, "ssd2ram_test"), "-n", str(a.threads),
+                                  "-u", str(a.unit_kib), "-s", str(a.buffer_mib), path],
+                                 capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(out.stdout, out.stderr, file=sys.stderr)
+                return out.returncode
+            m = re.search(r"\(([\d.]+) GiB/s\)", out.stdout)
+            res["runs"].append(float(m.group(1)))
+            S.evict_file(fd)
+            _, gib = S.raw_read_rate(fd, unit, F // unit, sequential=True, threads=a.threads,
+                                     qd=slots)
+            res["raw"].append(round(gib, 2))
+            print(f"ssd2ram {res['runs'][-1]:.2f} GiB/s  raw {gib:.2f} GiB/s", file=sys.stderr,
+                  flush=True)
+    finally:
+        os.close(fd)
+    best, raw = max(res["runs"]), max(res["raw"])
+    res.update(ssd2ram_GiBps=best, raw_GiBps=raw, of_raw=round(best / raw, 3) if raw else None,
+               last_stdout=out.stdout.strip().splitlines())
+    js = json.dumps(res)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

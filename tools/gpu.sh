@@ -10,11 +10,12 @@
 #   ktrace     rocprofv3 kernel trace + stats of a short kbench
 #   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
 #   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
+#   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   arrow      config-5 Arrow scan bench (tools.arrow_bench)
 # Output lands in gpurun_out/TAG/.
 set -o pipefail
 TAG=${1:?tag}; shift
-OUT=gpurun_out/$TAG
+OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export PYTHONPATH=$PWD${PYTHONPATH:+:$PYTHONPATH}
@@ -34,12 +35,13 @@ for phase in "$@"; do
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
-    ktrace) (cd /tmp && step ktrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o trace \
+    ktrace) (cd /tmp && step ktrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace \
               -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5) ;;
     kpmc) (cd /tmp && step kpmc 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
-              SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$ROOT/$OUT/pmc" -o pmc \
+              SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc" -o pmc \
               -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only crc,heap,lz4) ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
+    ram) step ram 400 python -u -m nvme_strom_amd.tools.ram_bench --out "$OUT/ram.json" ;;
     arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
