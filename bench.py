@@ -108,6 +108,11 @@ def main() -> int:
     path = os.path.join(a.dir, f"shard_r{rank}.bin")
     t0 = time.time()
     make_shard(path, F, 1234 + rank)
+    # reader pool per rank: split only among ranks that share this shard's
+    # backing device (placement.plan_io all-gathers the device identities)
+    from nvme_strom_amd.parallel.placement import plan_io
+    placement = plan_io(path, device=local)
+    _log(rank, f"placement {placement}")
     fd = os.open(path, os.O_RDONLY)
     S.evict_file(fd)
     _log(rank, f"shard {F >> 20} MiB ready in {time.time() - t0:.1f}s, resident="
@@ -314,6 +319,7 @@ def main() -> int:
             "file_bytes_per_rank": F,
             "backend": S.config_get("backend"),
             "workers": int(S.config_get("workers")),
+            "placement": placement,
             "max_request": int(S.config_get("max_request")),
         },
     }

@@ -44,11 +44,9 @@ Config Config::from_env() {
     for (const char *p = k; *p; ++p) env += (char)toupper(*p);
     if (const char *v = getenv(env.c_str())) c.set(k, v);
   }
-  // ranks of one node share its storage: past ~4 reader threads in all the
-  // pool box loses throughput (8 ranks x 4 workers 12.7 GiB/s, 8 x 1 21.7,
-  // profiles/r1k), so under torchrun the default pool shrinks per rank
-  const char *lw = getenv("LOCAL_WORLD_SIZE");
-  if (!getenv("STROM_WORKERS") && lw && atoi(lw) > 1) c.workers = std::max(1, c.workers / atoi(lw));
+  // Ranks sharing one backing device split the pool: the parallel layer
+  // counts them per device (nvme_strom_amd/parallel/placement.py) and sets
+  // `workers`; one SSD per GPU keeps the full pool.
   return c;
 }
 

@@ -17,6 +17,7 @@
 #include <sys/ioctl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/sysmacros.h>
 #include <unistd.h>
 #include <x86intrin.h>
 
@@ -850,7 +851,42 @@ int strom_dmabuf_munmap(void *addr, size_t length) {
 
 int strom_dmabuf_gc(void) { return dmabuf_registry().gc(); }
 
+int strom_file_topology(int fd, strom_file_topo *out) {
+  if (!out) return -EFAULT;
+  FileClass fc;
+  int rc = classify_file(fd, &fc, false);
+  if (rc) return rc;
+  memset(out, 0, sizeof *out);
+  out->dev_major = major(fc.dev);
+  out->dev_minor = minor(fc.dev);
+  out->numa_node = fc.numa_node;
+  snprintf(out->fs_name, sizeof out->fs_name, "%s", fc.fs_name.c_str());
+  snprintf(out->disk, sizeof out->disk, "%s", fc.disk.c_str());
+  std::vector<std::string> members;
+  if (fc.md_raid0) members = fc.members;
+  else if (!fc.disk.empty()) members.push_back(fc.disk);
+  for (auto &m : members) {
+    if (out->nmembers >= STROM_TOPO_MAX_MEMBERS) break;
+    std::string disk = m;
+    size_t pp = disk.rfind('p');                 // partition member: its disk
+    if (pp != std::string::npos && disk.compare(0, 4, "nvme") == 0 &&
+        disk.find('n', 4) != std::string::npos && disk.find('n', 4) < pp)
+      disk = disk.substr(0, pp);
+    snprintf(out->member_disk[out->nmembers], 32, "%s", m.c_str());
+    snprintf(out->member_pci[out->nmembers], 16, "%s", nvme_controller_bdf(disk).c_str());
+    ++out->nmembers;
+  }
+  return 0;
+}
+
+
 long strom_gpu_detached(void) { return (long)gpu_registry().detached_count(); }
+
+long strom_gpu_bar_bytes(unsigned long handle) {
+  auto m = gpu_registry().get(handle);
+  if (!m) return -ENOENT;
+  return (long)(m->bar ? m->bar_len : 0);
+}
 
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset) {
   if (!hip::available()) return -ENODEV;

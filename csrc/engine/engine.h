@@ -300,6 +300,9 @@ struct FileClass {
 };
 
 int classify_file(int fd, FileClass *out, bool strict);
+// PCI function "dddd:bb:dd.f" of the NVMe controller of a namespace disk
+// (first path of a multipath head), "" when not found
+std::string nvme_controller_bdf(const std::string &disk);
 
 // ------------------------------------------------------------ chunk plan
 struct IoRange {

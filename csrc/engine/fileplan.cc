@@ -203,6 +203,53 @@ int classify_file(int fd, FileClass *fc, bool strict) {
   return 0;
 }
 
+// PCI function (domain:bus:dev.fn) of the NVMe controller behind a
+// namespace disk: /sys/block/<disk>/device resolves to .../<bdf>/nvme/nvmeX
+// for a plain controller; a multipath head resolves to its nvme-subsystem,
+// whose first controller link is used.
+static bool is_bdf(const std::string &c) {
+  unsigned d, b, v, f;
+  char tail;
+  return c.size() == 12 && sscanf(c.c_str(), "%4x:%2x:%2x.%1x%c", &d, &b, &v, &f, &tail) == 4;
+}
+
+static std::string bdf_in_path(const std::string &p) {
+  std::string last;
+  size_t i = 0;
+  while (i < p.size()) {
+    size_t j = p.find('/', i);
+    if (j == std::string::npos) j = p.size();
+    std::string c = p.substr(i, j - i);
+    if (is_bdf(c)) last = c;
+    i = j + 1;
+  }
+  return last;
+}
+
+std::string nvme_controller_bdf(const std::string &disk) {
+  char real[PATH_MAX];
+  std::string dev = "/sys/block/" + disk + "/device";
+  if (!realpath(dev.c_str(), real)) return "";
+  std::string p = real;
+  if (p.find("nvme-subsystem") != std::string::npos) {
+    if (DIR *d = opendir(p.c_str())) {
+      std::string found;
+      while (struct dirent *e = readdir(d)) {
+        unsigned c;
+        char tail;
+        if (sscanf(e->d_name, "nvme%u%c", &c, &tail) != 1) continue;
+        std::string q = p + "/" + e->d_name;
+        if (realpath(q.c_str(), real)) found = bdf_in_path(real);
+        if (!found.empty()) break;
+      }
+      closedir(d);
+      return found;
+    }
+    return "";
+  }
+  return bdf_in_path(p);
+}
+
 // ------------------------------------------------------------- planning
 namespace {
 int plan_submit(void *ctx, const strom_extent *e) {

@@ -314,3 +314,16 @@ int numa_node_of_device(int device) {
 }  // namespace strom
 
 extern "C" int strom_gpu_count(void) { return strom::hip::device_count(); }
+
+extern "C" int strom_gpu_pci_bdf(int device, char *buf, size_t len) {
+  if (!strom::hip::available()) return -ENODEV;
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -ENODEV;
+  }
+  for (char *c = bus; *c; ++c) *c = (char)tolower(*c);
+  snprintf(buf, len, "%s", bus);
+  return 0;
+}
+

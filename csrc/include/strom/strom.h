@@ -90,6 +90,28 @@ int strom_dmabuf_munmap(void *addr, size_t length);
 int strom_dmabuf_gc(void);
 /* Mappings detached because their allocation was freed or replaced. */
 long strom_gpu_detached(void);
+/* Bytes of a mapping the CPU can store into through the large BAR (0: none;
+ * small reads then go staging -> SDMA / ingest grid instead). */
+long strom_gpu_bar_bytes(unsigned long handle);
+
+/* Placement facts of a file for GPU<->SSD affinity (CHECK_FILE tells
+ * only the NUMA node): the backing disk, its members (md raid0) and the
+ * PCI function of each member's controller (NVMe, or whatever PCI device
+ * the disk hangs off; "" when unknown).  nmembers = 0 for a virtual filesystem (overlay, tmpfs). */
+#define STROM_TOPO_MAX_MEMBERS 16
+typedef struct strom_file_topo {
+  uint32_t dev_major, dev_minor; /* st_dev of the file */
+  int32_t numa_node;
+  uint32_t nmembers;
+  char fs_name[16];
+  char disk[32];
+  char member_disk[STROM_TOPO_MAX_MEMBERS][32];
+  char member_pci[STROM_TOPO_MAX_MEMBERS][16];
+} strom_file_topo;
+int strom_file_topology(int fd, strom_file_topo *out);
+/* PCI function "dddd:bb:dd.f" of a HIP device (no GPU init past the
+ * runtime's own); -ENODEV without one. */
+int strom_gpu_pci_bdf(int device, char *buf, size_t len);
 
 /* HBM ingest grid of a device (the persistent GPU pull kernel that moves
  * staged reads into HBM): out[4] = {available, grid launches, descriptors

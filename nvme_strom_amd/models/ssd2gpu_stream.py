@@ -81,17 +81,27 @@ class StreamLoader:
         total_chunks = (nbytes + self.chunk_sz - 1) // self.chunk_sz
         inflight: List[tuple] = []
         t0 = time.perf_counter()
-        for seg, c0 in enumerate(range(0, total_chunks, self.per_seg)):
-            if len(inflight) == self.depth:
+        try:
+            for seg, c0 in enumerate(range(0, total_chunks, self.per_seg)):
+                if len(inflight) == self.depth:
+                    self._retire(inflight.pop(0), st, verify, dst)
+                n = min(self.per_seg, total_chunks - c0)
+                ids = np.arange(first_chunk + c0, first_chunk + c0 + n, dtype=np.uint32)
+                slot = seg % nseg_buf
+                res, landed = self.reader.submit(dst, slot * self.segment_sz, ids,
+                                                 wb=self.wbs[seg % self.depth])
+                inflight.append((res, slot, ids, landed))
+            while inflight:
                 self._retire(inflight.pop(0), st, verify, dst)
-            n = min(self.per_seg, total_chunks - c0)
-            ids = np.arange(first_chunk + c0, first_chunk + c0 + n, dtype=np.uint32)
-            slot = seg % nseg_buf
-            res, landed = self.reader.submit(dst, slot * self.segment_sz, ids,
-                                             wb=self.wbs[seg % self.depth])
-            inflight.append((res, slot, ids, landed))
-        while inflight:
-            self._retire(inflight.pop(0), st, verify, dst)
+        except BaseException:
+            # a failed segment: drain the others before the buffers (and the
+            # caller's retry) can be reused, and claim their task records
+            for res, *_ in inflight:
+                try:
+                    self.reader.finish(res)
+                except (api.StromError, OSError):
+                    pass
+            raise
         st.seconds = time.perf_counter() - t0
         st.bytes = nbytes
         self.stats.bytes += st.bytes

@@ -1,2 +1,4 @@
 """Multi-GPU: one process per GPU, shard loading + RCCL fan-out over xGMI."""
-from .fanout import FanoutStats, ShardedLoader, init_distributed, shard_range  # noqa: F401
+from .fanout import (FanoutStats, ShardedLoader, ShardLoadError, init_distributed,  # noqa: F401
+                     shard_range)
+from .placement import device_identity, plan_io  # noqa: F401

@@ -65,6 +65,18 @@ def shard_range(total: int, world: int, rank: int, align: int = 1 << 20) -> tupl
     return lo, min(total, lo + per) - lo
 
 
+class ShardLoadError(RuntimeError):
+    """A rank's window load failed; raised on EVERY rank of the group (the
+    others would otherwise block in the next collective forever)."""
+
+    def __init__(self, step: int, failed: List[int], cause: Optional[BaseException] = None):
+        super().__init__(f"step {step}: window load failed on rank(s) {failed}"
+                         + (f": {cause}" if cause else ""))
+        self.step = step
+        self.failed = failed
+        self.cause = cause
+
+
 @dataclass
 class FanoutStats:
     steps: int = 0
@@ -139,8 +151,13 @@ class ShardedLoader:
         buf = self.bufs[i % 2]
         off = self.file_offset + (i % self.nwin) * self.window
         t0 = time.perf_counter()
-        st = self.loader.run(off, self.window, buf=buf)
+        err = None
+        try:
+            st = self.loader.run(off, self.window, buf=buf)
+        except (api.StromError, OSError) as e:
+            err = e
         self.stats.load_s += time.perf_counter() - t0
+        self._agree(i, err)
         self.stats.bytes_loaded += st.bytes
         h = self._fan(buf.tensor)
         # the fan-out of step i-1 overlapped this load; retire it before the
@@ -150,6 +167,23 @@ class ShardedLoader:
         self.stats.steps += 1
         if self.world > 1:
             self.stats.bytes_gathered += self.out.numel()
+
+    def _agree(self, i: int, err: Optional[BaseException]) -> None:
+        """Failure consensus before the collective: one 4-byte all-gather of
+        per-rank status (RCCL on the GPU), so a read error on one rank
+        surfaces as ShardLoadError on all of them instead of a hang."""
+        if self.world == 1:
+            if err is not None:
+                raise ShardLoadError(i, [self.rank], err)
+            return
+        mine = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=self.device)
+        every = torch.empty(self.world, dtype=torch.int32, device=self.device)
+        dist.all_gather_into_tensor(every, mine, group=self.group)
+        failed = [r for r, v in enumerate(every.tolist()) if v]
+        if failed:
+            self._finish(self._pending)
+            self._pending = None
+            raise ShardLoadError(i, failed, err)
 
     def run(self, steps: int, start: int = 0) -> FanoutStats:
         t0 = time.perf_counter()

@@ -294,9 +294,12 @@ def test_freed_allocation_detaches_mapping(S, tmp_path):
     with open(path, "wb") as f:
         f.write(os.urandom(1 << 20))
     fd = os.open(path, os.O_RDONLY)
+    S.evict_file(fd)
     try:
         t = torch.empty(8 << 20, dtype=torch.uint8, device="cuda")
         m = S.map_gpu_memory(t.data_ptr(), t.numel())
+        # the large-BAR alias is set up (probe on a private allocation)
+        assert S.session().lib.strom_gpu_bar_bytes(m.handle) >= t.numel()
         r = S.memcpy_ssd2gpu(m.handle, 0, fd, np.arange(4, dtype=np.uint32), 65536)
         S.memcpy_wait(r.dma_task_id)
         before = S.gpu_detached()
