@@ -118,53 +118,11 @@ void host_free_thp(void *p, size_t bytes) {
   munmap(p, len);
 }
 
-// The CPU alias of HBM through a dma-buf mmap needs a large BAR (or the
-// driver falls back to something the GPU does not see).  Checked ONCE per
-// device on a private 64 KiB allocation — never by storing into a user's
-// live tensor, which kernels on other streams may be using.
-static bool bar_alias_ok(int device) {
-  static std::mutex mu;
-  static std::map<int, bool> cache;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = cache.find(device);
-  if (it != cache.end()) return it->second;
-  bool ok = false;
-  int cur = -1;
-  (void)hipGetDevice(&cur);
-  void *probe = nullptr;
-  const size_t len = 64u << 10;
-  if (hipSetDevice(device) == hipSuccess && hipMalloc(&probe, len) == hipSuccess) {
-    int fd = -1;
-    if (hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)probe, len,
-                                       hipMemRangeHandleTypeDmaBufFd, 0) == hipSuccess &&
-        fd >= 0) {
-      void *p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-      close(fd);
-      if (p != MAP_FAILED) {
-        const uint64_t canary = 0x5354524f4d424152ull ^ (uint64_t)probe;
-        uint64_t back = 0;
-        volatile uint64_t *q = (volatile uint64_t *)((uint8_t *)p + 4096);
-        *q = canary;
-        _mm_sfence();
-        (void)*q;  // drains the posted write
-        ok = hipMemcpy(&back, (uint8_t *)probe + 4096, 8, hipMemcpyDeviceToHost) == hipSuccess &&
-             back == canary;
-        munmap(p, len);
-      }
-    }
-    (void)hipFree(probe);
-  }
-  (void)hipGetLastError();
-  if (cur >= 0) (void)hipSetDevice(cur);
-  STROM_LOG(1, "device %d: BAR alias of HBM %s", device, ok ? "verified" : "unusable");
-  cache[device] = ok;
-  return ok;
-}
-
-uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
-  // Export the WHOLE allocation (caching allocators sub-allocate tensors
-  // inside larger hipMalloc blocks) and map the page-aligned cover of the
-  // range at its offset inside the export.
+// CPU mapping of the page-aligned cover of [va, va+len): the WHOLE
+// allocation holding it is exported (allocators sub-allocate inside larger
+// blocks) and the cover is mapped at its offset inside the export.
+static uint8_t *map_cover(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len,
+                          double *export_ms, double *mmap_ms) {
   const uint64_t page = 4096;
   hipDeviceptr_t abase = nullptr;
   size_t asize = 0;
@@ -172,16 +130,9 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
     (void)hipGetLastError();
     return nullptr;
   }
-  hipPointerAttribute_t attr;
-  memset(&attr, 0, sizeof attr);
-  if (hipPointerGetAttributes(&attr, (void *)va) != hipSuccess || attr.type != hipMemoryTypeDevice) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  if (!bar_alias_ok(attr.device)) return nullptr;
-  uint64_t base = (uint64_t)abase;
-  uint64_t lo = va & ~(page - 1);
-  uint64_t hi = (va + len + page - 1) & ~(page - 1);
+  const uint64_t base = (uint64_t)abase;
+  const uint64_t lo = va & ~(page - 1);
+  const uint64_t hi = (va + len + page - 1) & ~(page - 1);
   if (lo < base || hi > base + ((asize + page - 1) & ~(page - 1))) return nullptr;
   int fd = -1;
   const uint64_t t0 = mono_ns();
@@ -195,11 +146,63 @@ uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
   void *p = mmap(nullptr, hi - lo, PROT_READ | PROT_WRITE, MAP_SHARED, fd, (off_t)(lo - base));
   close(fd);  // the mapping keeps the dma-buf alive
   if (p == MAP_FAILED) return nullptr;
-  STROM_LOG(1, "bar_map %zu MiB: export %.2f ms, mmap %.2f ms", asize >> 20, (t1 - t0) / 1e6,
-            (mono_ns() - t1) / 1e6);
+  if (export_ms) *export_ms = (t1 - t0) / 1e6;
+  if (mmap_ms) *mmap_ms = (mono_ns() - t1) / 1e6;
   *map_va = lo;
   *map_len = hi - lo;
   return (uint8_t *)p;
+}
+
+// The CPU alias of HBM through a dma-buf mmap needs a large BAR (or the
+// driver falls back to something the GPU does not see).  Checked ONCE per
+// device on a private allocation — never by storing into a user's live
+// tensor, which kernels on other streams may be using.
+static bool bar_alias_ok(int device) {
+  static std::mutex mu;
+  static std::map<int, bool> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(device);
+  if (it != cache.end()) return it->second;
+  bool ok = false;
+  int cur = -1;
+  (void)hipGetDevice(&cur);
+  void *probe = nullptr;
+  const size_t len = 2u << 20;
+  if (hipSetDevice(device) == hipSuccess && hipMalloc(&probe, len) == hipSuccess) {
+    uint64_t mva = 0;
+    size_t mlen = 0;
+    const uint64_t at = (uint64_t)probe + 4096;
+    if (uint8_t *p = map_cover(at, 8, &mva, &mlen, nullptr, nullptr)) {
+      const uint64_t canary = 0x5354524f4d424152ull ^ at;
+      uint64_t back = 0;
+      volatile uint64_t *q = (volatile uint64_t *)(p + (at - mva));
+      *q = canary;
+      _mm_sfence();
+      (void)*q;  // drains the posted write
+      ok = hipMemcpy(&back, (void *)at, 8, hipMemcpyDeviceToHost) == hipSuccess && back == canary;
+      munmap(p, mlen);
+    }
+    (void)hipFree(probe);
+  }
+  (void)hipGetLastError();
+  if (cur >= 0) (void)hipSetDevice(cur);
+  STROM_LOG(ok ? 1 : 0, "device %d: BAR alias of HBM %s", device, ok ? "verified" : "unusable");
+  cache[device] = ok;
+  return ok;
+}
+
+uint8_t *bar_map(uint64_t va, size_t len, uint64_t *map_va, size_t *map_len) {
+  hipPointerAttribute_t attr;
+  memset(&attr, 0, sizeof attr);
+  if (hipPointerGetAttributes(&attr, (void *)va) != hipSuccess || attr.type != hipMemoryTypeDevice) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (!bar_alias_ok(attr.device)) return nullptr;
+  double ex = 0, mm = 0;
+  uint8_t *p = map_cover(va, len, map_va, map_len, &ex, &mm);
+  if (p) STROM_LOG(1, "bar_map %zu KiB: export %.2f ms, mmap %.2f ms", *map_len >> 10, ex, mm);
+  return p;
 }
 
 uint64_t buffer_id(uint64_t va) {

@@ -215,6 +215,7 @@ struct strom_decomp_desc {
 #define STROM_CODEC_COPY   3   /* stored block */
 #define STROM_CODEC_LZ4_FRAME     4  /* LZ4 frame data blocks (after header) */
 #define STROM_CODEC_LZ4_FRAME_BCS 5  /*   ... with 4-byte block checksums */
+#define STROM_CODEC_ARROW_LZ4     6  /* Arrow IPC buffer: i64 length (-1 = raw) + LZ4 frame */
 /* status[i] = decoded bytes, or -1 malformed / -2 overflow / -3 distance */
 int strom_decompress(int codec, const void *d_src, void *d_dst,
                      const struct strom_decomp_desc *d_desc, uint32_t nblocks,
@@ -231,6 +232,29 @@ int strom_column_filter(int type, const void *d_values, const uint8_t *d_valid,
 /* Compact selected row indices from a bitmap (stable order). */
 int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n,
                             uint32_t *d_out, uint64_t *d_count, void *stream);
+
+/* Batched scan over many record batches in ONE launch each, counts kept on
+ * the device (no host sync per batch).  Batch b's rows occupy bitmap words
+ * [word_base, word_base + ceil(nrows/64)) (every batch starts on a fresh
+ * word); values / valid are device addresses (valid = 0: no nulls; Arrow
+ * LSB-first bits, readable as whole 64-bit words). */
+struct strom_filter_batch {
+	uint64_t values;
+	uint64_t valid;
+	uint64_t nrows;
+	uint64_t word_base;
+	uint64_t row_base;     /* global row id of the batch's first row */
+};
+/* *d_count += selected rows (the caller zeroes it once per scan). */
+int strom_column_filter_batched(int type, const struct strom_filter_batch *d_batches,
+                                uint32_t nbatches, uint64_t nwords, double lo, double hi,
+                                uint64_t *d_bitmap, uint64_t *d_count, void *stream);
+/* Append the global row ids (int64, batch row_base + local row) of the set
+ * bits to d_out at the device-side cursor *d_total, which advances by the
+ * number appended: scans of successive groups fill one output in order. */
+int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
+                         const struct strom_filter_batch *d_batches, uint32_t nbatches,
+                         int64_t *d_out, uint64_t *d_total, void *stream);
 
 #ifdef __cplusplus
 }

@@ -116,6 +116,127 @@ __global__ __launch_bounds__(256) void emit_indices_kernel(const uint64_t *__res
   }
 }
 
+// ---------------------------------------------------------------- batched
+// batch of bitmap word w: the last b with word_base <= w (uniform per wave)
+__device__ __forceinline__ uint32_t batch_of(const strom_filter_batch *b, uint32_t nb, uint64_t w) {
+  uint32_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (b[mid].word_base <= w) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void filter_batched_kernel(const strom_filter_batch *__restrict__ bt,
+                                                             uint32_t nb, uint64_t nwords, T lo,
+                                                             T hi, uint64_t *__restrict__ bitmap,
+                                                             unsigned long long *__restrict__ count) {
+  __shared__ uint32_t wave_cnt[4];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t local = 0;
+  for (uint64_t w = (uint64_t)blockIdx.x * 4 + wid; w < nwords; w += (uint64_t)gridDim.x * 4) {
+    const strom_filter_batch b = bt[batch_of(bt, nb, w)];
+    const uint64_t k = w - b.word_base;           // word within the batch
+    const uint64_t i = k * 64 + lane;
+    bool ok = false;
+    if (i < b.nrows) {
+      const T x = ((const T *)b.values)[i];
+      ok = x >= lo && x <= hi;
+    }
+    uint64_t word = __ballot(ok);
+    if (b.valid && k * 64 < b.nrows) word &= ((const uint64_t *)b.valid)[k];
+    if (lane == 0) bitmap[w] = word;
+    local += __popcll(word);
+  }
+  if (lane == 0) wave_cnt[wid] = local;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicAdd(count, (unsigned long long)(wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3]));
+}
+
+// like scan_blocks_kernel, offset by the running output cursor, which it
+// then advances (one workgroup: every thread reads the cursor before the
+// first barrier, thread 1023 writes it after the last)
+__global__ __launch_bounds__(1024) void scan_blocks_cursor_kernel(uint64_t *__restrict__ cnt,
+                                                                  uint32_t nb,
+                                                                  unsigned long long *__restrict__ cursor) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t base = *cursor;
+  const uint32_t per = (nb + 1023) / 1024;
+  const uint32_t lo = min(nb, t * per), hi = min(nb, lo + per);
+  uint64_t s = 0;
+  for (uint32_t i = lo; i < hi; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1) {
+    uint64_t add = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += add;
+    __syncthreads();
+  }
+  uint64_t run = base + (t ? part[t - 1] : 0);
+  for (uint32_t i = lo; i < hi; ++i) {
+    const uint64_t c = cnt[i];
+    cnt[i] = run;
+    run += c;
+  }
+  if (t == 1023) *cursor = base + part[1023];
+}
+
+__global__ __launch_bounds__(256) void block_popc64_kernel(const uint64_t *__restrict__ bm,
+                                                           uint64_t nwords,
+                                                           uint64_t *__restrict__ block_cnt) {
+  __shared__ uint32_t s[4];
+  uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint32_t c = w < nwords ? __popcll(bm[w]) : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+__global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restrict__ bm,
+                                                        uint64_t nwords,
+                                                        const strom_filter_batch *__restrict__ bt,
+                                                        uint32_t nb,
+                                                        const uint64_t *__restrict__ base,
+                                                        int64_t *__restrict__ out) {
+  __shared__ uint32_t s[256];
+  const uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint64_t word = w < nwords ? bm[w] : 0;
+  const uint32_t c = __popcll(word);
+  s[threadIdx.x] = c;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    uint32_t add = threadIdx.x >= off ? s[threadIdx.x - off] : 0;
+    __syncthreads();
+    s[threadIdx.x] += add;
+    __syncthreads();
+  }
+  if (!word) return;
+  uint64_t pos = base[blockIdx.x] + s[threadIdx.x] - c;
+  const strom_filter_batch b = bt[batch_of(bt, nb, w)];
+  const int64_t row0 = (int64_t)(b.row_base + (w - b.word_base) * 64);
+  while (word) {
+    const uint32_t bit = __ffsll((unsigned long long)word) - 1;
+    out[pos++] = row0 + bit;
+    word &= word - 1;
+  }
+}
+
+template <typename T>
+int launch_filter_batched(const strom_filter_batch *bt, uint32_t nb, uint64_t nwords, double lo,
+                          double hi, uint64_t *bm, uint64_t *cnt, hipStream_t st) {
+  uint64_t g = (nwords + 3) / 4;
+  uint32_t grid = (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
+  hipLaunchKernelGGL(filter_batched_kernel<T>, dim3(grid), dim3(256), 0, st, bt, nb, nwords, (T)lo,
+                     (T)hi, bm, (unsigned long long *)cnt);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 template <typename T>
 int launch_filter(const void *v, const uint8_t *valid, uint64_t n, double lo, double hi,
                   uint64_t *bm, uint64_t *cnt, hipStream_t st) {
@@ -161,6 +282,42 @@ extern "C" int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n, uin
   hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
                      (unsigned long long *)d_count);
   hipLaunchKernelGGL(emit_indices_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, words, n, cnt, d_out);
+  (void)hipFreeAsync(cnt, st);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int strom_column_filter_batched(int type, const strom_filter_batch *d_batches,
+                                           uint32_t nbatches, uint64_t nwords, double lo,
+                                           double hi, uint64_t *d_bitmap, uint64_t *d_count,
+                                           void *stream) {
+  if (!nbatches || !nwords) return 0;
+  if (!d_batches || !d_bitmap || !d_count || ((uintptr_t)d_bitmap & 7)) return -22;
+  hipStream_t st = (hipStream_t)stream;
+  switch (type) {
+    case STROM_COL_I32: return launch_filter_batched<int32_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_I64: return launch_filter_batched<int64_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_F32: return launch_filter_batched<float>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_F64: return launch_filter_batched<double>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
+    default: return -22;
+  }
+}
+
+extern "C" int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
+                                    const strom_filter_batch *d_batches, uint32_t nbatches,
+                                    int64_t *d_out, uint64_t *d_total, void *stream) {
+  if (!nwords || !nbatches) return 0;
+  if (!d_bitmap || !d_batches || !d_out || !d_total) return -22;
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
+  if (nb64 > 0xffffffffull) return -75;
+  const uint32_t nb = (uint32_t)nb64;
+  uint64_t *cnt = nullptr;
+  if (hipMallocAsync((void **)&cnt, sizeof(uint64_t) * nb, st) != hipSuccess) return -12;
+  hipLaunchKernelGGL(block_popc64_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, cnt);
+  hipLaunchKernelGGL(scan_blocks_cursor_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
+                     (unsigned long long *)d_total);
+  hipLaunchKernelGGL(emit_rows_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                     nbatches, cnt, d_out);
   (void)hipFreeAsync(cnt, st);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

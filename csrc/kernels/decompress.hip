@@ -29,38 +29,24 @@
 // which on CDNA also counts the wave's in-flight byte stores.
 //
 // Codecs: raw LZ4 block, LZ4 frame block sequence (linked or independent
-// blocks, optional per-block checksums skipped, stored blocks), raw snappy,
-// stored copy.  All positions are 32-bit (streams < 4 GiB).
+// blocks, optional per-block checksums skipped, stored blocks), a whole
+// Arrow IPC compressed buffer (length prefix + frame header parsed on the
+// device, so the host never reads the file), raw snappy, stored copy.  All positions are 32-bit (streams < 4 GiB).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "strom/strom.h"
 
-#ifndef STROM_DECOMP_GL
-#define STROM_DECOMP_GL 4u
-#endif
-#ifndef STROM_DECOMP_RING
-#define STROM_DECOMP_RING (2u << 10)
-#endif
-#ifndef STROM_DECOMP_INW
-#define STROM_DECOMP_INW 512u
-#endif
-
 namespace {
 
-constexpr uint32_t GL = STROM_DECOMP_GL;     // lanes per stream
-constexpr uint32_t G = 64 / GL;              // streams per wave
+// Geometry, chosen per launch from the number of streams (strom_decompress):
+//   GL  lanes per stream (G = 64 / GL streams per wave),
+//   RING history ring and INW input window bytes per stream in LDS.
+// Many streams: small groups, many streams per wave; few streams: whole
+// waves per stream (wider copy passes, more waves resident per CU).
 constexpr uint32_t BPL = 4;                  // bytes per lane per pass
-constexpr uint32_t W = GL * BPL;             // bytes per pass per stream
-constexpr uint32_t kRing = STROM_DECOMP_RING;
-constexpr uint32_t kMask = kRing - 1;
-constexpr uint32_t kInW = STROM_DECOMP_INW;
-constexpr uint32_t kSlot = kRing + kInW;     // LDS bytes per stream
-static_assert(64 % GL == 0 && (kRing & kMask) == 0, "geometry");
-static_assert(kRing >= 4 * W && kInW >= 4 * W && kInW % 4 == 0, "window sizes");
-static_assert(G * kSlot <= 64 * 1024, "LDS per wave");
-static_assert(kRing / 2 + 3 * W + 16 <= kRing, "flush pacing vs ring / far matches");
 
 enum : int32_t { kErrFormat = -1, kErrOverflow = -2 };
 enum : uint32_t { kHdr = 0, kLz4 = 1, kSnappy = 2, kDone = 3 };
@@ -74,7 +60,22 @@ __device__ __forceinline__ uint32_t ld_bypass_byte(const uint8_t *p) {
 }
 
 // Group-uniform stream state (every lane of a group holds the same values).
+template <uint32_t GL_, uint32_t RING_, uint32_t INW_>
 struct Stream {
+  static constexpr uint32_t GL = GL_;
+  static constexpr uint32_t G = 64 / GL;     // streams per wave
+  static constexpr uint32_t W = GL * BPL;    // bytes per pass per stream
+  static constexpr uint32_t kRing = RING_;
+  static constexpr uint32_t kMask = kRing - 1;
+  static constexpr uint32_t kInW = INW_;
+  static constexpr uint32_t kSlot = kRing + kInW;   // LDS bytes per stream
+  // waves per SIMD the LDS footprint allows (160 KiB per CU, 4 SIMDs)
+  static constexpr uint32_t kMinWaves = (160u * 1024 / (G * kSlot)) / 4 >= 4 ? 4 : 1;
+  static_assert(64 % GL == 0 && (kRing & kMask) == 0, "geometry");
+  static_assert(kRing >= 4 * W && kInW >= 4 * W && kInW % 4 == 0, "window sizes");
+  static_assert(G * kSlot <= 64 * 1024, "LDS per wave");
+  static_assert(kRing / 2 + 3 * W + 16 <= kRing, "flush pacing vs ring / far matches");
+
   const uint8_t *ina;  // 4-aligned input base (= stream start - mis)
   uint8_t *out;
   uint8_t *ring;       // this group's LDS history ring
@@ -91,6 +92,8 @@ struct Stream {
   uint32_t omis;       // out & 15: ring index = (pos + omis) & kMask, so
                        // 16-B ring chunks are 16-B aligned in HBM too
   uint32_t olen;       // snappy: declared length
+  uint32_t bcs;        // LZ4 frame blocks carry 4-byte checksums
+  uint32_t fhdr;       // Arrow buffer: length prefix + frame header pending
   uint32_t mode;
   int32_t err;
 
@@ -349,6 +352,29 @@ struct Stream {
       literal(ip, n);
       ip = iend;
       mode = kDone;
+    } else if (fhdr) {
+      // Arrow IPC compressed buffer (BodyCompression LZ4_FRAME): int64
+      // uncompressed length (-1: the rest is stored raw), then one LZ4 frame
+      fhdr = 0;
+      if (iend - ip < 8) { err = kErrFormat; return; }
+      const uint32_t lo = rd4(ip, nullptr), hi = rd4(ip + 4, nullptr);
+      ip += 8;
+      if (lo == 0xffffffffu && hi == 0xffffffffu) {
+        const uint32_t n = iend - ip;
+        if (n > ocap) { err = kErrOverflow; return; }
+        literal(ip, n);
+        ip = iend;
+        mode = kDone;
+        return;
+      }
+      if (hi != 0 || lo > ocap) { err = kErrOverflow; return; }
+      if (iend - ip < 7 || rd4(ip, nullptr) != 0x184D2204u) { err = kErrFormat; return; }
+      const uint32_t flg = rd1(ip + 4);
+      if ((flg >> 6) != 1) { err = kErrFormat; return; }
+      const uint32_t hl = 7 + ((flg & 0x08) ? 8 : 0) + ((flg & 0x01) ? 4 : 0);
+      if (iend - ip < hl) { err = kErrFormat; return; }
+      bcs = (flg & 0x10) ? 1 : 0;
+      ip += hl;
     } else {
       // LZ4 frame data blocks: [u32 size|stored flag][data][u32 bcs?]... [u32 0]
       if (iend - ip < 4) { err = kErrFormat; return; }
@@ -362,7 +388,7 @@ struct Stream {
         if (bs > ocap - op) { err = kErrOverflow; return; }
         literal(ip, bs);
         ip += bs;
-        if (codec == STROM_CODEC_LZ4_FRAME_BCS) ip += 4;
+        if (bcs) ip += 4;
       } else {
         bend = ip + bs;
         mode = kLz4;
@@ -379,7 +405,7 @@ struct Stream {
         if (codec == STROM_CODEC_LZ4) {
           mode = kDone;
         } else {
-          ip = bend + (codec == STROM_CODEC_LZ4_FRAME_BCS ? 4 : 0);
+          ip = bend + (bcs ? 4 : 0);
           mode = kHdr;
         }
       } else {
@@ -397,18 +423,22 @@ struct Stream {
   }
 };
 
-__global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t *__restrict__ src,
+// 64 threads, >= 4 waves per SIMD (<= 128 VGPRs): the decoder is latency
+// bound per wave (round 2 trace: 256 or 1024 waves took the same ~9 ms),
+// so throughput comes from waves resident per CU
+template <class S>
+__global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec, const uint8_t *__restrict__ src,
                                                         uint8_t *__restrict__ dst,
                                                         const strom_decomp_desc *__restrict__ desc,
                                                         uint32_t nblocks, int32_t *status) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[G * kSlot];
-  const uint32_t lane = threadIdx.x, g = lane / GL;
-  const uint32_t stride = gridDim.x * G;
-  Stream st;
-  st.t = lane % GL;
-  st.ring = lds + g * kSlot;
-  st.inw = st.ring + kRing;
-  uint32_t b = blockIdx.x * G + g;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[S::G * S::kSlot];
+  const uint32_t lane = threadIdx.x, g = lane / S::GL;
+  const uint32_t stride = gridDim.x * S::G;
+  S st;
+  st.t = lane % S::GL;
+  st.ring = lds + g * S::kSlot;
+  st.inw = st.ring + S::kRing;
+  uint32_t b = blockIdx.x * S::G + g;
   bool live = false;
   for (;;) {
     if (!live && b < nblocks) {
@@ -427,6 +457,8 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
       st.flushed = 0;
       st.omis = (uint32_t)((uintptr_t)st.out & 15);
       st.olen = 0;
+      st.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
+      st.fhdr = codec == STROM_CODEC_ARROW_LZ4;
       st.mode = kHdr;
       st.err = 0;
       live = true;
@@ -441,16 +473,37 @@ __global__ __launch_bounds__(64) void decompress_kernel(int codec, const uint8_t
   }
 }
 
+using S16 = Stream<4, 2048, 512>;     // 16 streams per wave, 40 KiB LDS per wave
+using S4 = Stream<16, 2048, 512>;     // 4 streams per wave, 10 KiB
+using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
+
+template <class S>
+int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d_desc,
+           uint32_t nblocks, int32_t *d_status, hipStream_t st) {
+  const uint32_t waves = (nblocks + S::G - 1) / S::G;
+  const uint32_t grid = waves < 16384 ? waves : 16384;
+  hipLaunchKernelGGL(decompress_kernel<S>, dim3(grid), dim3(64), 0, st, codec,
+                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 }  // namespace
 
+// Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
+// when there are enough streams, else give each stream more lanes.
+// STROM_DECOMP_G (1, 4, 16) forces a geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
-  if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_LZ4_FRAME_BCS) return -22;
+  if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_ARROW_LZ4) return -22;
   if (!nblocks) return 0;
-  const uint32_t waves = (nblocks + G - 1) / G;
-  const uint32_t grid = waves < 8192 ? waves : 8192;
-  hipLaunchKernelGGL(decompress_kernel, dim3(grid), dim3(64), 0, (hipStream_t)stream, codec,
-                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
-  return hipGetLastError() == hipSuccess ? 0 : -5;
+  const char *e = getenv("STROM_DECOMP_G");
+  uint32_t g = e ? (uint32_t)atoi(e) : 0u;
+  // waves per CU at 256 CUs: S16 holds 3 (LDS), S4 ~16, S1 ~16 (VGPRs)
+  if (g != 1 && g != 4 && g != 16)
+    g = nblocks >= 256u * 16 * 16 ? 16 : nblocks >= 256u * 4 * 4 ? 4 : 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  if (g == 4) return launch<S4>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  return launch<S1>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
 }

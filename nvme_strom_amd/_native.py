@@ -203,6 +203,13 @@ _SIGS = {
                                       C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "strom_bitmap_to_indices": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                           C.c_void_p]),
+    "strom_column_filter_batched": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint64,
+                                              C.c_double, C.c_double, C.c_void_p, C.c_void_p,
+                                              C.c_void_p]),
+    "strom_bitmap_to_rows": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]),
+    "strom_file_topology": (C.c_int, [C.c_int, C.c_void_p]),
+    "strom_gpu_pci_bdf": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t]),
 }
 
 

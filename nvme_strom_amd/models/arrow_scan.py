@@ -1,33 +1,45 @@
 """PG-Strom-style SSD→GPU direct scan of an Apache Arrow IPC file
-(BASELINE config 5): file → HBM through the engine → LZ4 decode on the GPU
-→ range filter → selected row ids, with no host-side data touch.
+(BASELINE config 5): only the scanned column's buffers travel storage → HBM
+through the engine, are LZ4-decoded and filtered on the GPU, and the
+selected row ids are appended on the device — one host sync per scan.
 
-Steps
-  1. metadata: footer + record-batch headers only (utils/arrow_ipc.py);
-  2. load: the whole file (or any byte window) into a resident HBM tensor via
-     MEMCPY_SSD2GPU (tensor.load_file);
-  3. column: per batch, the data/validity buffers are either zero-copy views
-     of the loaded file (uncompressed) or LZ4-frame streams decoded by one
-     launch of the GPU decoder into a contiguous column tensor (Arrow's
-     BodyCompression: 8-byte uncompressed length prefix, -1 = stored raw);
-  4. filter: column_filter per batch (validity ANDed in), bitmap compaction to
-     global row ids.
+Pipeline (a ring of ``nslots`` HBM slots, groups of record batches):
+
+    host:   plan groups from the footer / batch headers (utils/arrow_ipc.py):
+            per batch the column's data (+ validity when it has nulls)
+            buffer ranges -> the file chunks that cover them
+    group g:  MEMCPY_SSD2GPU(chunk ids of g) -> slot g % nslots      (engine)
+              WAIT(g) ; then on the compute stream, no host sync:
+                decode  one launch over every compressed buffer of g
+                        (Arrow BodyCompression LZ4_FRAME: the length prefix and
+                        frame header are parsed on the device);
+                        status vs expected sizes -> device error counter
+                filter  one launch over every batch of g (validity ANDed in,
+                        each batch on fresh bitmap words), count on device
+                emit    global row ids appended at a device-side cursor
+              event(g) ; the slot is refilled only after event(g)
+    while group g computes, group g+1 is already being read.
+
+Unreferenced columns are never read; files larger than HBM stream through
+the ring.  The reference has no columnar path (new MI355X
+work); its chunk-list I/O (MEMCPY_SSD2GPU with arbitrary chunk ids,
+kmod/nvme_strom.c:1488-1604) is what fetches the scattered buffers.
 """
 from __future__ import annotations
 
 import os
-import struct
 import time
-from dataclasses import dataclass
-from typing import Dict, List, Optional, Tuple
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
 
 from ..ops import decompress as D
-from ..ops.colfilter import bitmap_to_indices, column_filter
-from ..tensor import load_file
-from ..utils.arrow_ipc import ArrowFile, BufferRef, read_metadata
+from ..ops.colfilter import BATCH_FIELDS, bitmap_to_rows, filter_batched
+from ..ops.reorder import chunk_scatter, landing_positions
+from ..tensor import FileReader, HbmBuffer, host_buffer
+from ..utils.arrow_ipc import ArrowFile, read_metadata
 
 _TORCH = {"i4": torch.int32, "i8": torch.int64, "f4": torch.float32, "f8": torch.float64}
 
@@ -38,117 +50,265 @@ class ScanOut:
     selected: int
     indices: torch.Tensor
     seconds: Dict[str, float]
+    bytes_read: int = 0           # file bytes moved storage -> HBM
+    column_bytes: int = 0         # decoded bytes of the scanned column
+    groups: int = 0
+
+
+@dataclass
+class _Buf:
+    off: int          # file offset of the stored buffer
+    length: int       # stored bytes (prefix + frame when compressed)
+    need: int         # bytes the scan reads from the decoded buffer
+    cap: int          # decode capacity (need rounded up to 64)
+    compressed: bool
+
+
+@dataclass
+class _Batch:
+    rows: int
+    row_base: int
+    data: _Buf
+    valid: Optional[_Buf]
+
+
+@dataclass
+class _Group:
+    batches: List[_Batch]
+    ids: np.ndarray                       # sorted file chunk ids
+    dec_bytes: int = 0
+    words: int = 0
+
+
+@dataclass
+class _Slot:
+    hbm: HbmBuffer
+    dec: torch.Tensor
+    bitmap: torch.Tensor
+    event: Optional[torch.cuda.Event] = None
+    pending: object = None                # (CopyResult, landed ids, group)
+    keep: List[torch.Tensor] = field(default_factory=list)
+
+
+def _up64(n: int) -> int:
+    return (n + 63) // 64 * 64
 
 
 class ArrowScan:
-    def __init__(self, path: str, device=None, chunk_sz: int = 1 << 20):
+    def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
+                 slot_bytes: int = 256 << 20, nslots: int = 3):
         self.path = path
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.meta: ArrowFile = read_metadata(path)
         self.chunk_sz = chunk_sz
-        self.file: Optional[torch.Tensor] = None
-        self._hdr_fd = os.open(path, os.O_RDONLY)
-        self.timings: Dict[str, float] = {}
+        self.slot_bytes = slot_bytes
+        self.nslots = max(2, nslots)
+        self.reader: Optional[FileReader] = None
+        self._slots: List[_Slot] = []
+        self._scratch: Optional[torch.Tensor] = None
 
-    def load(self) -> torch.Tensor:
-        t0 = time.perf_counter()
-        self.file = load_file(self.path, self.device, chunk_sz=self.chunk_sz)
-        self.timings["load_s"] = time.perf_counter() - t0
-        return self.file
-
-    # ----------------------------------------------------------- buffers
-    def _buffer_plan(self, ref: BufferRef, codec: Optional[str]) -> Tuple[str, int, int, int, int]:
-        """-> (kind, src_off, src_len, out_len, lz4 codec id)"""
-        if ref.length == 0:
-            return "empty", 0, 0, 0, 0
-        if codec is None:
-            return "raw", ref.offset, ref.length, ref.length, 0
-        if codec != "lz4_frame":
-            raise NotImplementedError(f"body compression {codec} (GPU decoder: LZ4 frame)")
-        head = os.pread(self._hdr_fd, 32, ref.offset)
-        ulen, = struct.unpack_from("<q", head, 0)
-        if ulen == -1:
-            return "raw", ref.offset + 8, ref.length - 8, ref.length - 8, 0
-        info = D.parse_lz4_frame_header(head, 8)
-        codec_id = D.LZ4_FRAME_BCS if info.block_checksum else D.LZ4_FRAME
-        so = ref.offset + 8 + info.data_offset
-        return "lz4", so, ref.length - 8 - info.data_offset, ulen, codec_id
-
-    def _gather(self, refs: List[BufferRef], codecs: List[Optional[str]], sizes: List[int],
-                pad_to: int) -> Tuple[torch.Tensor, List[int]]:
-        """Materialise buffers back to back (each padded to ``pad_to``)."""
-        offs, total = [], 0
-        for s in sizes:
-            offs.append(total)
-            total += (s + pad_to - 1) // pad_to * pad_to
-        out = torch.zeros(max(total, 8), dtype=torch.uint8, device=self.device)
-        groups: Dict[int, list] = {}
-        for ref, codec, o, s in zip(refs, codecs, offs, sizes):
-            kind, so, sl, ol, cid = self._buffer_plan(ref, codec)
-            if kind == "empty":
-                continue
-            if kind == "raw":
-                n = min(sl, s)
-                out[o:o + n].copy_(self.file[so:so + n])
-            else:
-                groups.setdefault(cid, []).append((so, sl, o, min(ol, s)))
-        for cid, items in groups.items():
-            st = D.decompress(cid, self.file, out, D.make_descs(items))
-            bad = [i for i, (x, it) in enumerate(zip(st, items)) if x != it[3]]
-            if bad:
-                raise RuntimeError(f"LZ4 decode failed for {len(bad)} buffer(s): {st[bad[:4]]}")
-        return out, offs
-
-    def column(self, name: str) -> Tuple[torch.Tensor, Optional[torch.Tensor], List[int]]:
-        """(values, validity bytes or None, per-batch row offsets)."""
-        if self.file is None:
-            self.load()
+    # ------------------------------------------------------------- plan
+    def _plan(self, name: str) -> tuple:
         ci = self.meta.column_index(name)
         col = self.meta.schema[ci]
-        if not col.supported:
-            raise NotImplementedError(f"column {name} is not a fixed-width primitive")
+        if not col.supported or col.numpy_dtype not in _TORCH:
+            raise NotImplementedError(f"column {name}: the GPU filter takes int32/64, float32/64")
         width = col.bit_width // 8
-        t0 = time.perf_counter()
-        bs = self.meta.batches
-        rows = [b.columns[ci].length for b in bs]
-        codecs = [b.codec for b in bs]
-        # values: back to back, each batch padded to 64 B so views stay aligned
-        vals, voffs = self._gather([b.columns[ci].data for b in bs], codecs,
-                                   [r * width for r in rows], 64)
-        has_nulls = any(b.columns[ci].null_count for b in bs)
-        valid = None
-        if has_nulls:
-            valid, _ = self._gather([b.columns[ci].validity for b in bs], codecs,
-                                    [(r + 7) // 8 for r in rows], 64)
-        torch.cuda.synchronize() if self.device.type == "cuda" else None
-        self.timings["decode_s"] = time.perf_counter() - t0
-        self._layout = (voffs, rows, width, col.numpy_dtype)
-        return vals, valid, voffs
+        out, base = [], 0
+        for b in self.meta.batches:
+            if b.codec not in (None, "lz4_frame"):
+                raise NotImplementedError(f"body compression {b.codec} (GPU decoder: LZ4 frame)")
+            cc = b.columns[ci]
+            comp = b.codec is not None
+            need = cc.length * width
+            data = _Buf(cc.data.offset, cc.data.length, need, _up64(need), comp)
+            valid = None
+            if cc.null_count and cc.validity.length:
+                vn = (cc.length + 7) // 8
+                valid = _Buf(cc.validity.offset, cc.validity.length, vn, _up64(vn) + 64, comp)
+            out.append(_Batch(cc.length, base, data, valid))
+            base += cc.length
+        return out, _TORCH[col.numpy_dtype], base
 
-    def filter(self, name: str, lo, hi) -> ScanOut:
-        vals, valid, voffs = self.column(name)
-        _, rows, width, dt = self._layout
+    def _chunks(self, b: _Batch) -> np.ndarray:
+        c = self.chunk_sz
+        parts = []
+        for buf in (b.data, b.valid):
+            if buf is not None and buf.length:
+                parts.append(np.arange(buf.off // c, (buf.off + buf.length + c - 1) // c))
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+
+    def _groups(self, batches: List[_Batch]) -> List[_Group]:
+        groups: List[_Group] = []
+        cur: List[_Batch] = []
+        ids = np.zeros(0, dtype=np.int64)
+        limit = self.slot_bytes // self.chunk_sz
+        for b in batches:
+            mine = self._chunks(b)
+            merged = np.union1d(ids, mine)
+            if cur and len(merged) > limit:
+                groups.append(_Group(cur, ids))
+                cur, merged = [], np.unique(mine)
+            cur.append(b)
+            ids = merged
+        if cur:
+            groups.append(_Group(cur, ids))
+        for g in groups:
+            g.dec_bytes = sum((b.data.cap if b.data.compressed else 0) +
+                              (b.valid.cap if b.valid is not None and b.valid.compressed else 0)
+                              for b in g.batches)
+            g.words = sum((b.rows + 63) // 64 for b in g.batches)
+        return groups
+
+    # --------------------------------------------------------- pipeline
+    def _ensure_slots(self, groups: List[_Group]) -> None:
+        nbytes = max(len(g.ids) for g in groups) * self.chunk_sz
+        dec = max(max(g.dec_bytes for g in groups), 64)
+        words = max(max(g.words for g in groups), 1)
+        if self._slots and (self._slots[0].hbm.nbytes >= nbytes and
+                            self._slots[0].dec.numel() >= dec and
+                            self._slots[0].bitmap.numel() >= words):
+            return
+        self._free_slots()
+        for _ in range(self.nslots):
+            self._slots.append(_Slot(HbmBuffer(nbytes, self.device),
+                                     torch.empty(dec, dtype=torch.uint8, device=self.device),
+                                     torch.empty(words, dtype=torch.int64, device=self.device)))
+        if self.reader is None:
+            self.reader = FileReader(self.path, chunk_sz=self.chunk_sz,
+                                     max_chunks=nbytes // self.chunk_sz)
+        self._wbs = [host_buffer(nbytes) for _ in range(self.nslots)]
+
+    def _submit(self, k: int, g: _Group) -> None:
+        s = self._slots[k % self.nslots]
+        if s.event is not None:
+            s.event.synchronize()            # the slot's previous group is consumed
+            s.event = None
+        s.keep = []
+        res, landed = self.reader.submit(s.hbm, 0, g.ids.astype(np.uint32),
+                                         wb=self._wbs[k % self.nslots])
+        s.pending = (res, landed, g)
+
+    def _compute(self, k: int, dtype, lo, hi, state) -> None:
+        s = self._slots[k % self.nslots]
+        res, landed, g = s.pending
+        s.pending = None
         t0 = time.perf_counter()
-        idx, total, base = [], 0, 0
-        voff_valid = 0
-        for r, vo in zip(rows, voffs):
-            v = vals[vo:vo + r * width].view(_TORCH[dt])
-            vb = None
-            if valid is not None:
-                vb = valid[voff_valid:voff_valid + ((r + 7) // 8 + 63) // 64 * 64]
-                voff_valid += ((r + 7) // 8 + 63) // 64 * 64
-            bm, cnt = column_filter(v, lo, hi, vb)
-            if cnt:
-                idx.append(bitmap_to_indices(bm, r, cnt).to(torch.int64) + base)
-            total += cnt
-            base += r
-        out = torch.cat(idx) if idx else torch.zeros(0, dtype=torch.int64, device=self.device)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
-        self.timings["filter_s"] = time.perf_counter() - t0
-        return ScanOut(base, total, out, dict(self.timings))
+        self.reader.finish(res)
+        state["wait_s"] += time.perf_counter() - t0
+        region = s.hbm.tensor[:len(g.ids) * self.chunk_sz]
+        # write-back copies of page-cache chunks (FileReader.submit without a
+        # BAR) were queued on the current stream
+        self.cs.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.cs):
+            if res.nr_ram and not np.array_equal(landed, g.ids.astype(np.uint32)):
+                # page-cache chunks landed at the tail: restore chunk order
+                if self._scratch is None or self._scratch.numel() < region.numel():
+                    self._scratch = torch.empty(s.hbm.nbytes, dtype=torch.uint8,
+                                                device=self.device)
+                tmp = self._scratch[:region.numel()]
+                tmp.copy_(region)
+                chunk_scatter(tmp, region, landing_positions(g.ids.astype(np.uint32), landed,
+                                                             res.nr_ssd), self.chunk_sz)
+            base = region.data_ptr()
+            dec_base = s.dec.data_ptr()
+            c = self.chunk_sz
+
+            def slot_off(off: int) -> int:
+                return int(np.searchsorted(g.ids, off // c)) * c + off % c
+
+            descs, need = [], []
+            table = np.zeros((len(g.batches), BATCH_FIELDS), dtype=np.int64)
+            dcur, wcur = 0, 0
+            for i, b in enumerate(g.batches):
+                ptrs = []
+                for buf in (b.data, b.valid):
+                    if buf is None:
+                        ptrs.append(0)
+                    elif buf.length == 0:
+                        ptrs.append(dec_base)        # empty batch: nothing is read
+                    elif buf.compressed:
+                        descs.append((slot_off(buf.off), buf.length, dcur, buf.cap))
+                        need.append(buf.need)
+                        ptrs.append(dec_base + dcur)
+                        dcur += buf.cap
+                    else:
+                        ptrs.append(base + slot_off(buf.off))
+                table[i] = (ptrs[0], ptrs[1], b.rows, wcur, b.row_base)
+                wcur += (b.rows + 63) // 64
+            if descs:
+                d = D.make_descs(descs)
+                d_desc = torch.from_numpy(d.view(np.uint8).copy()).pin_memory().to(
+                    self.device, non_blocking=True)
+                d_need = torch.from_numpy(np.array(need, dtype=np.int32)).pin_memory().to(
+                    self.device, non_blocking=True)
+                status = torch.empty(len(descs), dtype=torch.int32, device=self.device)
+                D.decompress_async(D.ARROW_LZ4, region, s.dec, d_desc, status, stream=self.cs)
+                # status = decoded bytes; short or failed -> error count
+                state["err"] += ((status < d_need) | (status < 0)).sum()
+                s.keep += [d_desc, d_need, status]
+            d_table = torch.from_numpy(table).pin_memory().to(self.device, non_blocking=True)
+            filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap, state["count"],
+                           stream=self.cs)
+            bitmap_to_rows(s.bitmap, g.words, d_table, state["out"], state["cursor"],
+                           stream=self.cs)
+            s.keep.append(d_table)
+            s.event = torch.cuda.Event()
+            s.event.record(self.cs)
+        state["bytes_read"] += len(g.ids) * self.chunk_sz
+        state["column_bytes"] += sum(b.data.need for b in g.batches)
+
+    def scan(self, name: str, lo, hi) -> ScanOut:
+        """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never
+        qualify)."""
+        t0 = time.perf_counter()
+        batches, dtype, nrows = self._plan(name)
+        groups = self._groups(batches)
+        out = torch.empty(max(nrows, 1), dtype=torch.int64, device=self.device)
+        if not groups or nrows == 0:
+            return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0})
+        self._ensure_slots(groups)
+        self.cs = torch.cuda.Stream(device=self.device)
+        z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
+        state = dict(out=out, cursor=z(), count=z(), err=z(), wait_s=0.0, bytes_read=0,
+                     column_bytes=0)
+        t_plan = time.perf_counter()
+        # depth nslots - 1 of reads ahead of the group being computed
+        ahead = self.nslots - 1
+        for k in range(min(ahead, len(groups))):
+            self._submit(k, groups[k])
+        for k in range(len(groups)):
+            if k + ahead < len(groups):
+                self._compute(k, dtype, lo, hi, state)
+                self._submit(k + ahead, groups[k + ahead])
+            else:
+                self._compute(k, dtype, lo, hi, state)
+        self.cs.synchronize()
+        cursor, count, err = torch.cat([state["cursor"], state["count"], state["err"]]).tolist()
+        t_end = time.perf_counter()
+        if err:
+            raise RuntimeError(f"LZ4 decode failed for {err} buffer(s) of column {name}")
+        if cursor != count:
+            raise RuntimeError(f"row emit mismatch: {cursor} ids for {count} selected")
+        for s in self._slots:
+            s.keep = []
+            s.event = None
+        return ScanOut(nrows, int(count), out[:count],
+                       {"plan_s": t_plan - t0, "wait_s": state["wait_s"], "total_s": t_end - t0},
+                       bytes_read=state["bytes_read"], column_bytes=state["column_bytes"],
+                       groups=len(groups))
+
+    # the pre-pipeline name
+    filter = scan
+
+    def _free_slots(self) -> None:
+        for s in self._slots:
+            s.hbm.close()
+        self._slots = []
 
     def close(self) -> None:
-        if self._hdr_fd >= 0:
-            os.close(self._hdr_fd)
-            self._hdr_fd = -1
+        self._free_slots()
+        self._scratch = None
+        if self.reader is not None:
+            self.reader.close()
+            self.reader = None

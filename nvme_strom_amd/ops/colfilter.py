@@ -55,3 +55,39 @@ def _popcount(bitmap: torch.Tensor, n: int) -> int:
     b = bitmap.cpu().numpy().view(np.uint8)
     bits = np.unpackbits(b, bitorder="little")[:n]
     return int(bits.sum())
+
+
+# ----------------------------------------------------------- batched scan
+# struct strom_filter_batch (strom.h): values, valid, nrows, word_base,
+# row_base as five u64 — a (nbatches, 5) int64 tensor on the device
+BATCH_FIELDS = 5
+
+
+def filter_batched(dtype: torch.dtype, batches: torch.Tensor, nwords: int, lo, hi,
+                   bitmap: torch.Tensor, count: torch.Tensor, stream=None) -> None:
+    """One launch over many record batches; ``count`` (int64[1] on the
+    device) accumulates the selected rows — nothing is read back."""
+    if dtype not in _TYPES:
+        raise ValueError(f"unsupported dtype {dtype}")
+    require_cuda(batches, "batches")
+    nb = batches.shape[0]
+    if batches.dtype != torch.int64 or batches.shape[1] != BATCH_FIELDS:
+        raise ValueError("batches: int64 (n, 5)")
+    if bitmap.numel() < nwords:
+        raise ValueError("bitmap too small")
+    check(lib().strom_column_filter_batched(_TYPES[dtype], ptr(batches), nb, nwords, float(lo),
+                                            float(hi), ptr(bitmap), ptr(count),
+                                            stream_handle(stream)), "column_filter_batched")
+
+
+def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out: torch.Tensor,
+                   cursor: torch.Tensor, stream=None) -> None:
+    """Append global row ids (int64) of the set bits at ``out[cursor]``;
+    ``cursor`` (int64[1], device) advances — successive groups of one scan
+    fill ``out`` in order without a host round trip."""
+    require_cuda(bitmap, "bitmap")
+    if out.dtype != torch.int64:
+        raise ValueError("out must be int64")
+    check(lib().strom_bitmap_to_rows(ptr(bitmap), nwords, ptr(batches), batches.shape[0],
+                                     ptr(out), ptr(cursor), stream_handle(stream)),
+          "bitmap_to_rows")

@@ -26,6 +26,7 @@ SNAPPY = 2
 COPY = 3
 LZ4_FRAME = 4
 LZ4_FRAME_BCS = 5
+ARROW_LZ4 = 6          # Arrow IPC buffer: i64 length prefix (-1 = raw) + LZ4 frame
 
 DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_len", "<u4"),
                        ("dst_len", "<u4")])
@@ -119,6 +120,18 @@ def make_descs(items: Sequence[tuple]) -> np.ndarray:
     for i, (so, sl, do, dl) in enumerate(items):
         d[i] = (so, do, sl, dl)
     return d
+
+
+def decompress_async(codec: int, src: torch.Tensor, dst: torch.Tensor, d_desc: torch.Tensor,
+                     status: torch.Tensor, stream=None) -> None:
+    """Device-side descriptors (uint8 view of DESC_DTYPE records) and status:
+    no host sync; the caller checks ``status`` on the device.  Bounds are
+    the caller's contract (checked by :func:`decompress`)."""
+    n = d_desc.numel() // DESC_DTYPE.itemsize
+    if n == 0:
+        return
+    check(lib().strom_decompress(codec, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status),
+                                 stream_handle(stream)), "decompress")
 
 
 def decompress(codec: int, src: torch.Tensor, dst: torch.Tensor, descs: np.ndarray,

@@ -1,0 +1,155 @@
+"""Config-5 benchmark: SSD -> HBM -> LZ4 decode -> filter of one column of
+an Arrow IPC file (models/arrow_scan.py), against pyarrow on the CPU.
+
+The file is written by pyarrow (LZ4_FRAME body compression, linked 64 KiB
+blocks as pyarrow writes them) with three columns — ``id`` (int64,
+sequential), ``val`` (int64, uniform in [0, 1e6)) and ``x`` (float64, 5 %
+nulls) — in record batches of ``--batch-rows``.  Each timed run starts with
+the file evicted from the page cache.  Reported per scanned column:
+
+  column_GBps   decoded column bytes / wall time of ArrowScan.scan
+  file_GBps     file bytes moved storage -> HBM / wall time
+  cpu_GBps      the same scan with pyarrow on the host (memory-mapped file,
+                LZ4 decode + compute.and of two comparisons + indices)
+  verified      GPU row ids == numpy row ids of the regenerated column
+
+``python -m nvme_strom_amd.tools.arrow_bench --out gpurun_out/arrow.json``
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_file(path: str, rows: int, batch_rows: int, seed: int = 7) -> None:
+    import pyarrow as pa
+    import pyarrow.ipc as ipc
+    if os.path.exists(path):
+        return
+    schema = pa.schema([("id", pa.int64()), ("val", pa.int64()), ("x", pa.float64())])
+    rng = np.random.default_rng(seed)
+    tmp = path + ".tmp"
+    with ipc.new_file(tmp, schema, options=ipc.IpcWriteOptions(compression="lz4")) as w:
+        for b0 in range(0, rows, batch_rows):
+            n = min(batch_rows, rows - b0)
+            ids = np.arange(b0, b0 + n, dtype=np.int64)
+            val = rng.integers(0, 1_000_000, n, dtype=np.int64)
+            x = rng.random(n)
+            mask = rng.random(n) < 0.05
+            w.write_batch(pa.record_batch([pa.array(ids), pa.array(val),
+                                           pa.array(x, mask=mask)], schema=schema))
+    os.replace(tmp, path)
+
+
+def column_np(path: str, name: str):
+    import pyarrow as pa
+    import pyarrow.ipc as ipc
+    with pa.memory_map(path) as src:
+        t = ipc.open_file(src).read_all()
+    c = t.column(name).combine_chunks()
+    vals = c.to_numpy(zero_copy_only=False)
+    valid = ~np.asarray(c.is_null()) if c.null_count else None
+    return vals, valid
+
+
+def cpu_scan(path: str, name: str, lo, hi) -> tuple:
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import pyarrow.ipc as ipc
+    t0 = time.perf_counter()
+    with pa.memory_map(path) as src:
+        r = ipc.open_file(src)
+        sel, base = [], 0
+        for i in range(r.num_record_batches):
+            col = r.get_batch(i).column(name)
+            m = pc.and_(pc.greater_equal(col, lo), pc.less_equal(col, hi))
+            idx = np.flatnonzero(np.asarray(m.fill_null(False)))
+            sel.append(idx + base)
+            base += len(col)
+    n = int(sum(len(s) for s in sel))
+    return time.perf_counter() - t0, n
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1 << 27)
+    ap.add_argument("--batch-rows", type=int, default=1 << 16)
+    ap.add_argument("--dir", default="/tmp/strom_arrow")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--slot-mib", type=int, default=256)
+    ap.add_argument("--columns", default="val,x")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    import torch
+
+    import nvme_strom_amd as S
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+
+    os.makedirs(a.dir, exist_ok=True)
+    path = os.path.join(a.dir, f"t_{a.rows}_{a.batch_rows}.arrow")
+    t0 = time.time()
+    make_file(path, a.rows, a.batch_rows)
+    fsize = os.path.getsize(path)
+    _log(f"file {fsize / 2**30:.2f} GiB ({a.rows} rows, {a.batch_rows}/batch) in "
+         f"{time.time() - t0:.1f}s")
+    preds = {"val": (100_000, 199_999), "x": (0.25, 0.5), "id": (1000, 5_000_000)}
+    res = dict(file_bytes=fsize, rows=a.rows, batch_rows=a.batch_rows, codec="lz4_frame (pyarrow)",
+               slot_mib=a.slot_mib, columns={})
+    fd = os.open(path, os.O_RDONLY)
+    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20)
+    try:
+        for name in a.columns.split(","):
+            lo, hi = preds[name]
+            runs = []
+            for _ in range(a.reps):
+                S.evict_file(fd)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                out = sc.scan(name, lo, hi)
+                dt = time.perf_counter() - t1
+                runs.append(dt)
+                _log(f"{name}: {out.selected} rows, {dt * 1e3:.1f} ms, groups {out.groups}, "
+                     f"{out.column_bytes / dt / 1e9:.1f} GB/s column, "
+                     f"{out.bytes_read / dt / 1e9:.1f} GB/s file, {out.seconds}")
+            vals, valid = column_np(path, name)
+            m = (vals >= lo) & (vals <= hi)
+            if valid is not None:
+                m &= valid
+            ref = np.flatnonzero(m)
+            got = out.indices.cpu().numpy()
+            ok = bool(len(got) == len(ref) and np.array_equal(got, ref))
+            cpu_s, cpu_n = cpu_scan(path, name, lo, hi)
+            best = min(runs)
+            res["columns"][name] = dict(
+                selected=out.selected, verified=ok, cpu_selected=cpu_n,
+                column_bytes=out.column_bytes, bytes_read=out.bytes_read, groups=out.groups,
+                ms=[round(r * 1e3, 2) for r in runs],
+                column_GBps=round(out.column_bytes / best / 1e9, 2),
+                file_GBps=round(out.bytes_read / best / 1e9, 2),
+                cpu_ms=round(cpu_s * 1e3, 1),
+                cpu_GBps=round(out.column_bytes / cpu_s / 1e9, 2))
+            _log(json.dumps(res["columns"][name]))
+    finally:
+        sc.close()
+        os.close(fd)
+    res["arrow_scan_GBps"] = min(c["column_GBps"] for c in res["columns"].values())
+    res["verified"] = all(c["verified"] for c in res["columns"].values())
+    js = json.dumps(res)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+    return 0 if res["verified"] else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

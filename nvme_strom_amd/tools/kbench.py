@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 
 import numpy as np
@@ -101,6 +102,17 @@ def main(argv=None):
             tag = "64k" if dname == "words" else f"{dname}_64k"
             log(f"decompress_{codec}_{tag}_ratio{len(blk) / len(comp):.1f}",
                 timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
+            if codec == "lz4" and dname == "words":
+                # the same streams under each geometry (streams per wave), and
+                # a few-streams launch (an Arrow scan group: ~1k buffers)
+                for g in (16, 4, 1):
+                    os.environ["STROM_DECOMP_G"] = str(g)
+                    log(f"decompress_lz4_64k_g{g}",
+                        timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
+                os.environ.pop("STROM_DECOMP_G", None)
+                few = min(nblk, 1024)
+                log(f"decompress_lz4_64k_{few}streams",
+                    timed(lambda: D.decompress(cid, src, dst, descs[:few]), 3), few * len(blk))
             del src, dst
     if "filter" in only:
         nv = n // 8
