@@ -19,7 +19,7 @@ ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
-all: $(OUT)/libstrom.so tools
+all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so
 
 tools: $(TOOLS)
 
@@ -39,11 +39,16 @@ $(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ) $(CORE_OBJ)
 	@mkdir -p $(OUT)
 	$(HIPCC) $(LDFLAGS) --offload-arch=$(ARCH) -o $@ $^
 
+# the LZ4/snappy decoder with its cycle profile compiled in (tools/decomp_prof.py)
+$(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/include/strom/strom.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ $<
+
 $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
-	rm -rf build $(OUT)/libstrom.so $(TOOLS)
+	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(TOOLS)
 
 .PHONY: all tools clean
 

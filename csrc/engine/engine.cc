@@ -913,6 +913,14 @@ int strom_engine_reset(void) {
   return 0;
 }
 
+int strom_fake_backend(uint64_t seed, uint64_t *completions, uint64_t *reordered) {
+  FaultInjector &f = faults();
+  if (seed) f.fake_seed = seed;
+  if (completions) *completions = f.fake_completions.load();
+  if (reordered) *reordered = f.fake_reordered.load();
+  return 0;
+}
+
 int strom_fault_inject(long fail_at, int err, long short_at, int short_bytes, int delay_us) {
   FaultInjector &f = faults();
   f.counter = 0;

@@ -387,6 +387,9 @@ struct FaultInjector {
   std::atomic<int> delay_us{0};
   // returns 0 or -errno; may shrink *len
   int on_request(uint32_t *len);
+  // fake backend: completions delivered in a seeded random order
+  std::atomic<uint64_t> fake_seed{0x5eed};
+  std::atomic<uint64_t> fake_completions{0}, fake_reordered{0};
 };
 FaultInjector &faults();
 

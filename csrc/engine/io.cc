@@ -193,7 +193,39 @@ struct IoEngine::Worker {
     uint8_t *dst = nullptr;
     uint32_t len = 0;
     uint64_t t0 = 0;
+    long got = 0;        // fake backend: the read's result, delivered later
+    uint64_t seq = 0;    // fake backend: submission order
   };
+
+  // Fake namespace (backend=fake, CPU tests): reads are served from the
+  // file at submission, but their completions are held in a device queue
+  // and delivered in a seeded random order once the queue is full or the
+  // worker runs dry — what an NVMe controller may do, and what the task
+  // refcounts, landing order and staging-slot recycling must survive.
+  std::vector<Ctx> fake_cq;
+  uint64_t fake_rng = 0, fake_seq = 0, fake_next = 0;
+
+  uint64_t fake_rand() {
+    fake_rng ^= fake_rng << 13;
+    fake_rng ^= fake_rng >> 7;
+    fake_rng ^= fake_rng << 17;
+    return fake_rng;
+  }
+
+  void reap_fake() {
+    while (!fake_cq.empty()) {
+      const size_t i = (size_t)(fake_rand() % fake_cq.size());
+      Ctx c = fake_cq[i];
+      fake_cq[i] = fake_cq.back();
+      fake_cq.pop_back();
+      --reads_inflight;
+      faults().fake_completions.fetch_add(1, std::memory_order_relaxed);
+      if (c.seq != fake_next) faults().fake_reordered.fetch_add(1, std::memory_order_relaxed);
+      fake_next = c.seq + 1;
+      on_read_done(c, c.got);
+    }
+    flush_staged();
+  }
 
   int idx = 0;
   Config cfg;
@@ -251,11 +283,16 @@ struct IoEngine::Worker {
     }
   }
 
-  // staging slots: at least staging_slots, else as many max_request-sized
-  // slots as staging_bytes holds (small requests keep many in flight)
+  // staging slots (each max_request bytes): at least staging_slots; small
+  // requests get up to queue_depth slots within the same in-flight byte
+  // budget (staging_slots x 1 MiB), so a 16-128 KiB stream keeps the queue
+  // as deep as the raw ceiling's (round 2 sweep: 4 slots capped 64 KiB
+  // reads at 0.72 of raw); staging_bytes opts into more
   int nslots() const {
-    const size_t by_bytes = cfg.staging_bytes / cfg.max_request;
-    return (int)std::max<size_t>(cfg.staging_slots, std::min<size_t>(by_bytes, 256));
+    const size_t budget = (size_t)cfg.staging_slots << 20;
+    const size_t small = std::min<size_t>((size_t)cfg.queue_depth, budget / cfg.max_request);
+    const size_t by_bytes = std::min<size_t>(cfg.staging_bytes / cfg.max_request, 256);
+    return (int)std::max<size_t>(cfg.staging_slots, std::max(small, by_bytes));
   }
 
   bool ensure_slots() {
@@ -470,9 +507,16 @@ struct IoEngine::Worker {
     c.dst = dst;
     c.len = len;
     c.t0 = mono_ns();
-    if (frc) {
+    if (frc && cfg.backend != BackendKind::kFake) {
       on_read_done(c, frc);
       flush_staged();
+      return true;
+    }
+    if (cfg.backend == BackendKind::kFake) {
+      c.got = frc ? frc : pread_full(r.fd, dst, len, r.off);
+      c.seq = fake_seq++;
+      fake_cq.push_back(c);
+      ++reads_inflight;
       return true;
     }
     if (use_ring) {
@@ -525,10 +569,12 @@ struct IoEngine::Worker {
 
   void run() {
     bind_numa();
+    const bool fake = cfg.backend == BackendKind::kFake;
     bool use_ring = cfg.backend == BackendKind::kUring;
     const int qd_cfg = std::max(cfg.queue_depth, nslots());
     if (use_ring && ring.init((unsigned)std::max(8, qd_cfg * 2)) != 0) use_ring = false;
-    int qd = use_ring ? qd_cfg : 1;
+    int qd = use_ring || fake ? qd_cfg : 1;
+    fake_rng = faults().fake_seed.load() * 2654435761u + (uint64_t)idx * 0x9E3779B97F4A7C15ull + 1;
     const uint64_t spin_ns = (uint64_t)cfg.spin_us * 1000;
     std::deque<IoReq> local;
     for (;;) {
@@ -567,6 +613,7 @@ struct IoEngine::Worker {
         local.pop_front();
       }
       if (use_ring && ring.pending()) ring.enter(0);
+      if (fake && (local.empty() || blocked || reads_inflight >= qd)) reap_fake();
       retire(false);
       retire_ingest();
       if (use_ring) reap();
@@ -574,8 +621,12 @@ struct IoEngine::Worker {
       // nothing more can start: wait for a read, a copy, or new work
       const bool hbm_busy = !copying.empty() || !ingesting.empty();
       if (reads_inflight > 0 && !hbm_busy) {
-        ring.enter(1);
-        reap();
+        if (fake) {
+          reap_fake();
+        } else {
+          ring.enter(1);
+          reap();
+        }
       } else if (reads_inflight == 0 && hbm_busy) {
         if (local.empty()) {
           std::lock_guard<std::mutex> g(mu);

@@ -131,6 +131,11 @@ int strom_engine_reset(void);
 int strom_fault_inject(long fail_at, int err, long short_at, int short_bytes,
                        int delay_us);
 
+/* Fake namespace backend (backend=fake): completions come back in a seeded
+ * random order.  Sets the seed (0 keeps it; takes effect at the next
+ * engine reset) and reads the completion / out-of-order counters. */
+int strom_fake_backend(uint64_t seed, uint64_t *completions, uint64_t *reordered);
+
 /* ---- host helpers ------------------------------------------------------ */
 /* Bytes of a file range resident in the page cache (mincore). */
 long strom_resident_bytes(int fd, uint64_t offset, uint64_t length);

@@ -48,6 +48,22 @@ namespace {
 // waves per stream (wider copy passes, more waves resident per CU).
 constexpr uint32_t BPL = 4;                  // bytes per lane per pass
 
+// Optional cycle profile (-DSTROM_DECOMP_PROF, the libstrom_decprof.so
+// build used by tools/decomp_prof.py): s_memtime spans per code path,
+// summed by lane 0 of each group, plus event counts.
+enum : int { kPSeq, kPLit, kPNear, kPShort, kPFar, kPRefill, kPFlush, kPHdr, kPFarFence,
+             kPNSeq, kPNFar, kPNRefill, kPNFlush, kPNLitPass, kPNMatchPass, kPSteps, kPN };
+#ifdef STROM_DECOMP_PROF
+__device__ unsigned long long g_prof[kPN];
+#define PROF_T0() const uint64_t _t0 = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(k) (prof[k] += __builtin_amdgcn_s_memtime() - _t0)
+#define PROF_CNT(k, n) (prof[k] += (n))
+#else
+#define PROF_T0() (void)0
+#define PROF_ADD(k) (void)0
+#define PROF_CNT(k, n) (void)0
+#endif
+
 enum : int32_t { kErrFormat = -1, kErrOverflow = -2 };
 enum : uint32_t { kHdr = 0, kLz4 = 1, kSnappy = 2, kDone = 3 };
 
@@ -96,8 +112,13 @@ struct Stream {
   uint32_t fhdr;       // Arrow buffer: length prefix + frame header pending
   uint32_t mode;
   int32_t err;
+#ifdef STROM_DECOMP_PROF
+  uint64_t prof[kPN];
+#endif
 
   __device__ void refill(uint32_t p) {
+    PROF_T0();
+    PROF_CNT(kPNRefill, 1);
     const uint32_t at = p & ~3u;
     const uint32_t n = iend - at < kInW ? iend - at : kInW;
     const uint8_t *src = ina + at;
@@ -113,6 +134,7 @@ struct Stream {
     for (; k + 4 <= n; k += GL * 4) *(uint32_t *)(inw + k) = *(const uint32_t *)(src + k);
     for (uint32_t kb = (n & ~3u) + t; kb < n; kb += GL) inw[kb] = src[kb];  // <= 3 tail bytes
     win = at;
+    PROF_ADD(kPRefill);
   }
   // window holds [p, p + need) (bytes past iend are never used)
   __device__ __forceinline__ void ensure(uint32_t p, uint32_t need) {
@@ -137,6 +159,8 @@ struct Stream {
   // (stream head/tail) byte by byte.  exact=false leaves a partial last
   // chunk for later.
   __device__ void flush(uint32_t upto, bool exact) {
+    PROF_T0();
+    PROF_CNT(kPNFlush, 1);
     const uint32_t rb = flushed + omis, re = upto + omis;
     const uint32_t cb = rb >> 4, ce = exact ? (re + 15) >> 4 : re >> 4;
     for (uint32_t c = cb + t; c < ce; c += GL) {
@@ -155,6 +179,7 @@ struct Stream {
     }
     const uint32_t nf = exact ? upto : (ce << 4) - omis;
     if (ce > cb && nf > flushed) flushed = nf;
+    PROF_ADD(kPFlush);
   }
   // bound the unflushed span so the ring never overwrites it (and far
   // matches only read flushed output): called after every pass
@@ -164,6 +189,8 @@ struct Stream {
 
   // literal bytes [p, p+len) of the input -> output
   __device__ void literal(uint32_t p, uint32_t len) {
+    PROF_T0();
+    PROF_CNT(kPNLitPass, (len + W - 1) / W);
     const uint32_t k = t * BPL;
     for (uint32_t done = 0; done < len; done += W) {
       const uint32_t n = len - done < W ? len - done : W;
@@ -180,9 +207,12 @@ struct Stream {
       pace(op + done + n);
     }
     op += len;
+    PROF_ADD(kPLit);
   }
 
   __device__ void match(uint32_t off, uint32_t len) {
+    PROF_T0();
+    PROF_CNT(kPNMatchPass, (len + W - 1) / W);
     if (off == 0 || off > op) {
       err = kErrFormat;
       return;
@@ -207,6 +237,7 @@ struct Stream {
           }
           pace(op + done + n);
         }
+        PROF_ADD(kPNear);
       } else {
         // short period: byte k of a pass starting at s repeats s-off+(k mod off)
         uint32_t r[BPL];
@@ -227,17 +258,21 @@ struct Stream {
             if (k + j < n) put(s + k + j, v[j]);
           pace(s + n);
         }
+        PROF_ADD(kPShort);
       }
     } else {
+      PROF_CNT(kPNFar, 1);
       // far (off > kRing - W >= 3W): sources are this wave's stored output
       for (uint32_t done = 0; done < len; done += W) {
         const uint32_t n = len - done < W ? len - done : W;
         const uint32_t s = op + done;
         if (s - off + n > vis) {
           // pace() keeps these sources flushed already; stay safe anyway
+          PROF_T0();
           if (s - off + n > flushed) flush(s, true);
           __threadfence();
           vis = flushed;
+          PROF_ADD(kPFarFence);
         }
         if (k < n) {
 #pragma unroll
@@ -246,12 +281,15 @@ struct Stream {
         }
         pace(s + n);
       }
+      PROF_ADD(kPFar);
     }
     op += len;
   }
 
   // ---- one LZ4 sequence of the block ending at bend
   __device__ void lz4_seq() {
+    PROF_T0();
+    PROF_CNT(kPNSeq, 1);
     const uint32_t w = rd4(ip, nullptr);
     uint32_t lit = (w >> 4) & 15, ml = w & 15;
     uint32_t p = ip + 1;
@@ -284,6 +322,7 @@ struct Stream {
     if (ml > ocap - op) { err = kErrOverflow; return; }
     match(off, ml);
     ip = p;
+    PROF_ADD(kPSeq);
   }
 
   // ---- one snappy element (literal run or copy)
@@ -435,6 +474,9 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
   const uint32_t lane = threadIdx.x, g = lane / S::GL;
   const uint32_t stride = gridDim.x * S::G;
   S st;
+#ifdef STROM_DECOMP_PROF
+  for (int i = 0; i < kPN; ++i) st.prof[i] = 0;
+#endif
   st.t = lane % S::GL;
   st.ring = lds + g * S::kSlot;
   st.inw = st.ring + S::kRing;
@@ -464,6 +506,9 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
       live = true;
     }
     if (!__any(live)) break;
+#ifdef STROM_DECOMP_PROF
+    if (live) st.prof[kPSteps] += 1;
+#endif
     if (live && !st.step(codec)) {
       if (!st.err) st.flush(st.op, true);
       if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
@@ -471,6 +516,10 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
       b += stride;
     }
   }
+#ifdef STROM_DECOMP_PROF
+  if (st.t == 0)
+    for (int i = 0; i < kPN; ++i) atomicAdd(&g_prof[i], (unsigned long long)st.prof[i]);
+#endif
 }
 
 using S16 = Stream<4, 2048, 512>;     // 16 streams per wave, 40 KiB LDS per wave
@@ -499,11 +548,24 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   if (!nblocks) return 0;
   const char *e = getenv("STROM_DECOMP_G");
   uint32_t g = e ? (uint32_t)atoi(e) : 0u;
-  // waves per CU at 256 CUs: S16 holds 3 (LDS), S4 ~16, S1 ~16 (VGPRs)
-  if (g != 1 && g != 4 && g != 16)
-    g = nblocks >= 256u * 16 * 16 ? 16 : nblocks >= 256u * 4 * 4 ? 4 : 1;
+  // 16 streams per wave won at 16k streams (107 vs 76 vs 21 GB/s for
+  // 16 / 4 / 1, round 2 kbench); fewer streams spread over more waves
+  if (g != 1 && g != 4 && g != 16) g = nblocks >= 4096 ? 16 : nblocks >= 1024 ? 4 : 1;
   hipStream_t st = (hipStream_t)stream;
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 4) return launch<S4>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   return launch<S1>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
 }
+
+#ifdef STROM_DECOMP_PROF
+// read (and zero) the profile counters: out[kPN]
+extern "C" int strom_decomp_prof(uint64_t *out) {
+  unsigned long long h[kPN] = {0};
+  if (hipDeviceSynchronize() != hipSuccess) return -5;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof h) != hipSuccess) return -5;
+  unsigned long long z[kPN] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+  for (int i = 0; i < kPN; ++i) out[i] = h[i];
+  return kPN;
+}
+#endif

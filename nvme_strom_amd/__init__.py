@@ -18,7 +18,7 @@ from .api import (  # noqa: F401
     CopyResult, DmaBuffer, FileInfo, GpuMapping, Session, StromError, alloc_dma_buffer,
     check_file, config_get, config_set, configure, crc32c_host, dmabuf_gc, engine_reset, evict_file,
     gpu_detached,
-    fault_inject, hist_percentile, info_gpu_memory, list_gpu_memory, map_gpu_memory,
+    fake_backend, fault_inject, hist_percentile, info_gpu_memory, list_gpu_memory, map_gpu_memory,
     memcpy_ssd2gpu, memcpy_ssd2ram, memcpy_wait, pread_gpu, pread_gpu_latency, provider,
     PHASES, host_costs, ingest_info, ioctl_latency, phase_breakdown, pread_gpu_phases, pread_raw_latency, raw_read_rate,
     resident_bytes, session,

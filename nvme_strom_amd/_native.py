@@ -171,6 +171,7 @@ _SIGS = {
     "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "strom_engine_reset": (C.c_int, []),
     "strom_fault_inject": (C.c_int, [C.c_long, C.c_int, C.c_long, C.c_int, C.c_int]),
+    "strom_fake_backend": (C.c_int, [C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "strom_resident_bytes": (C.c_long, [C.c_int, C.c_uint64, C.c_uint64]),
     "strom_evict_file": (C.c_int, [C.c_int]),
     "strom_crc32c_host": (C.c_uint32, [C.c_uint32, C.c_void_p, C.c_size_t]),

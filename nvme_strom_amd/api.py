@@ -114,6 +114,14 @@ def fault_inject(fail_at: int = 0, err: int = _errno.EIO, short_at: int = 0,
     N.lib().strom_fault_inject(fail_at, err, short_at, short_bytes, delay_us)
 
 
+def fake_backend(seed: int = 0) -> tuple:
+    """Fake namespace backend counters: (completions, out-of-order
+    completions); ``seed`` != 0 reseeds the completion order (next reset)."""
+    c, r = C.c_uint64(), C.c_uint64()
+    N.lib().strom_fake_backend(seed, C.byref(c), C.byref(r))
+    return c.value, r.value
+
+
 def ingest_info(device: int = 0) -> Optional[dict]:
     """Counters of the device's HBM ingest grid (the persistent GPU kernel that
     pulls staged reads into HBM), or None when it cannot run there."""

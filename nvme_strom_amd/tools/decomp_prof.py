@@ -1,0 +1,94 @@
+"""Where the LZ4/snappy decoder's time goes (csrc/kernels/decompress.hip
+built with -DSTROM_DECOMP_PROF into lib/libstrom_decprof.so).
+
+Runs the kbench corpora through the profiling build under each geometry
+(streams per wave 16 / 4 / 1) and reports, per decoded sequence, the shader
+cycles a stream spent in each code path (s_memtime spans summed over
+streams) and how often the expensive events happen.
+
+``python -m nvme_strom_amd.tools.decomp_prof --out gpurun_out/decprof.json``
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+NAMES = ["seq", "literal", "match_near", "match_short", "match_far", "refill", "flush", "header",
+         "far_fence", "n_seq", "n_far", "n_refill", "n_flush", "n_lit_pass", "n_match_pass",
+         "steps"]
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=16384)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    from nvme_strom_amd.ops import decompress as D
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+                              "libstrom_decprof.so"))
+    lib.strom_decompress.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.c_void_p, C.c_void_p]
+    lib.strom_decomp_prof.argtypes = [C.c_void_p]
+    rng = np.random.default_rng(1)
+    words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+    corpora = {
+        "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
+        "ints": np.cumsum(rng.integers(0, 5, 8192)).astype(np.int64).tobytes(),
+        "rand3": np.random.default_rng(2).integers(0, 1_000_000, 8192).astype(np.int64).tobytes(),
+    }
+    res = {}
+    dev = torch.device("cuda")
+    for cname, blk in corpora.items():
+        comp = D.lz4_compress(blk)
+        for nblk in sorted({a.blocks, 1024}):
+            src = torch.from_numpy(np.frombuffer(comp * nblk, dtype=np.uint8).copy()).to(dev)
+            dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
+            descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk))
+                                  for i in range(nblk)])
+            d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+            status = torch.empty(nblk, dtype=torch.int32, device=dev)
+            for g in (16, 4, 1):
+                os.environ["STROM_DECOMP_G"] = str(g)
+                out = np.zeros(len(NAMES), dtype=np.uint64)
+                lib.strom_decompress(D.LZ4, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),
+                                     nblk, status.data_ptr(), None)
+                torch.cuda.synchronize()
+                lib.strom_decomp_prof(out.ctypes.data)       # discard the warm-up
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                lib.strom_decompress(D.LZ4, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),
+                                     nblk, status.data_ptr(), None)
+                e.record()
+                torch.cuda.synchronize()
+                ms = s.elapsed_time(e)
+                lib.strom_decomp_prof(out.ctypes.data)
+                ok = bool((status.cpu().numpy() == len(blk)).all()) and \
+                    bytes(dst[:len(blk)].cpu().numpy()) == blk
+                nseq = max(int(out[9]), 1)
+                row = dict(ms=round(ms, 3), GBps=round(nblk * len(blk) / ms / 1e6, 1), ok=ok,
+                           ratio=round(len(blk) / len(comp), 2),
+                           seq_per_block=round(nseq / nblk, 1),
+                           cycles_per_seq={NAMES[i]: round(int(out[i]) / nseq, 1) for i in range(9)},
+                           events_per_seq={NAMES[i]: round(int(out[i]) / nseq, 3)
+                                           for i in range(10, 16)})
+                key = f"{cname}_{nblk}_g{g}"
+                res[key] = row
+                print(key, json.dumps(row), file=sys.stderr, flush=True)
+            os.environ.pop("STROM_DECOMP_G", None)
+            del src, dst
+    js = json.dumps(res)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -11,6 +11,7 @@
 #   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
 #   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
+#   decprof    decoder cycle profile per code path (libstrom_decprof.so)
 #   arrow      config-5 Arrow scan bench (tools.arrow_bench)
 # Output lands in gpurun_out/TAG/.
 set -o pipefail
@@ -42,6 +43,7 @@ for phase in "$@"; do
               -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only crc,heap,lz4) ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
     ram) step ram 400 python -u -m nvme_strom_amd.tools.ram_bench --out "$OUT/ram.json" ;;
+    decprof) step decprof 300 python -u -m nvme_strom_amd.tools.decomp_prof --out "$OUT/decprof.json" ;;
     arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
