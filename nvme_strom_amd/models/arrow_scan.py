@@ -9,14 +9,16 @@ Pipeline (a ring of ``nslots`` HBM slots, groups of record batches):
             per batch the column's data (+ validity when it has nulls)
             buffer ranges -> the file chunks that cover them
     group g:  MEMCPY_SSD2GPU(chunk ids of g) -> slot g % nslots      (engine)
-              WAIT(g) ; then on the compute stream, no host sync:
+              WAIT(g) ; then on the slot's stream, no host sync:
                 decode  one launch over every compressed buffer of g
                         (Arrow BodyCompression LZ4_FRAME: the length prefix and
                         frame header are parsed on the device);
                         status vs expected sizes -> device error counter
                 filter  one launch over every batch of g (validity ANDed in,
                         each batch on fresh bitmap words), count on device
-                emit    global row ids appended at a device-side cursor
+                emit    global row ids appended at a device-side cursor, on one
+                        emit stream in group order (decode/filter of several
+                        groups run concurrently on their slots' streams)
               event(g) ; the slot is refilled only after event(g)
     while group g computes, group g+1 is already being read.
 
@@ -86,6 +88,10 @@ class _Slot:
     dec: torch.Tensor
     bitmap: torch.Tensor
     event: Optional[torch.cuda.Event] = None
+    stream: Optional[torch.cuda.Stream] = None
+    count: Optional[torch.Tensor] = None   # selected rows of the slot's group
+    err: Optional[torch.Tensor] = None     # failed decodes of the slot's group
+    scratch: Optional[torch.Tensor] = None # chunk-order restore (page-cache hits)
     pending: object = None                # (CopyResult, landed ids, group)
     keep: List[torch.Tensor] = field(default_factory=list)
 
@@ -105,7 +111,6 @@ class ArrowScan:
         self.nslots = max(2, nslots)
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
-        self._scratch: Optional[torch.Tensor] = None
 
     # ------------------------------------------------------------- plan
     def _plan(self, name: str) -> tuple:
@@ -171,9 +176,13 @@ class ArrowScan:
             return
         self._free_slots()
         for _ in range(self.nslots):
-            self._slots.append(_Slot(HbmBuffer(nbytes, self.device),
-                                     torch.empty(dec, dtype=torch.uint8, device=self.device),
-                                     torch.empty(words, dtype=torch.int64, device=self.device)))
+            sl = _Slot(HbmBuffer(nbytes, self.device),
+                       torch.empty(dec, dtype=torch.uint8, device=self.device),
+                       torch.empty(words, dtype=torch.int64, device=self.device))
+            sl.stream = torch.cuda.Stream(device=self.device)
+            sl.count = torch.zeros(1, dtype=torch.int64, device=self.device)
+            sl.err = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._slots.append(sl)
         if self.reader is None:
             self.reader = FileReader(self.path, chunk_sz=self.chunk_sz,
                                      max_chunks=nbytes // self.chunk_sz)
@@ -199,14 +208,14 @@ class ArrowScan:
         region = s.hbm.tensor[:len(g.ids) * self.chunk_sz]
         # write-back copies of page-cache chunks (FileReader.submit without a
         # BAR) were queued on the current stream
-        self.cs.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.cs):
+        cs = s.stream
+        cs.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(cs):
             if res.nr_ram and not np.array_equal(landed, g.ids.astype(np.uint32)):
                 # page-cache chunks landed at the tail: restore chunk order
-                if self._scratch is None or self._scratch.numel() < region.numel():
-                    self._scratch = torch.empty(s.hbm.nbytes, dtype=torch.uint8,
-                                                device=self.device)
-                tmp = self._scratch[:region.numel()]
+                if s.scratch is None:
+                    s.scratch = torch.empty(s.hbm.nbytes, dtype=torch.uint8, device=self.device)
+                tmp = s.scratch[:region.numel()]
                 tmp.copy_(region)
                 chunk_scatter(tmp, region, landing_positions(g.ids.astype(np.uint32), landed,
                                                              res.nr_ssd), self.chunk_sz)
@@ -243,18 +252,30 @@ class ArrowScan:
                 d_need = torch.from_numpy(np.array(need, dtype=np.int32)).pin_memory().to(
                     self.device, non_blocking=True)
                 status = torch.empty(len(descs), dtype=torch.int32, device=self.device)
-                D.decompress_async(D.ARROW_LZ4, region, s.dec, d_desc, status, stream=self.cs)
+                D.decompress_async(D.ARROW_LZ4, region, s.dec, d_desc, status, stream=cs)
                 # status = decoded bytes; short or failed -> error count
-                state["err"] += ((status < d_need) | (status < 0)).sum()
+                s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]
             d_table = torch.from_numpy(table).pin_memory().to(self.device, non_blocking=True)
-            filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap, state["count"],
-                           stream=self.cs)
-            bitmap_to_rows(s.bitmap, g.words, d_table, state["out"], state["cursor"],
-                           stream=self.cs)
+            filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap, s.count, stream=cs)
             s.keep.append(d_table)
+        # decode + filter of successive groups overlap on their slots'
+        # streams; the row-id emit runs in group order on one stream (the
+        # output cursor is shared), and frees the slot
+        ready = torch.cuda.Event()
+        ready.record(cs)
+        es = self.emit_stream
+        es.wait_event(ready)
+        with torch.cuda.stream(es):
+            bitmap_to_rows(s.bitmap, g.words, s.keep[-1], state["out"], state["cursor"],
+                           stream=es)
+            state["count"] += s.count
+            s.count.zero_()
+            if descs:
+                state["err"] += s.err
+                s.err.zero_()
             s.event = torch.cuda.Event()
-            s.event.record(self.cs)
+            s.event.record(es)
         state["bytes_read"] += len(g.ids) * self.chunk_sz
         state["column_bytes"] += sum(b.data.need for b in g.batches)
 
@@ -268,7 +289,7 @@ class ArrowScan:
         if not groups or nrows == 0:
             return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0})
         self._ensure_slots(groups)
-        self.cs = torch.cuda.Stream(device=self.device)
+        self.emit_stream = torch.cuda.Stream(device=self.device)
         z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
         state = dict(out=out, cursor=z(), count=z(), err=z(), wait_s=0.0, bytes_read=0,
                      column_bytes=0)
@@ -283,7 +304,7 @@ class ArrowScan:
                 self._submit(k + ahead, groups[k + ahead])
             else:
                 self._compute(k, dtype, lo, hi, state)
-        self.cs.synchronize()
+        torch.cuda.synchronize(self.device)
         cursor, count, err = torch.cat([state["cursor"], state["count"], state["err"]]).tolist()
         t_end = time.perf_counter()
         if err:
@@ -308,7 +329,6 @@ class ArrowScan:
 
     def close(self) -> None:
         self._free_slots()
-        self._scratch = None
         if self.reader is not None:
             self.reader.close()
             self.reader = None
