@@ -24,6 +24,7 @@
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
+#include <set>
 
 #include "engine.h"
 
@@ -66,6 +67,27 @@ struct Engine::OpenFile {
     return res;
   }
 };
+
+// A logical file striped over member files: stripe s (unit bytes) lives
+// in member s % n at member offset (s / n) * unit.  The remap is the shared
+// core's raid0 map (one zone, every member), so requests split at stripe
+// boundaries exactly as they do for md raid0.
+struct Engine::StripeSet {
+  std::vector<std::shared_ptr<OpenFile>> m;
+  uint32_t unit = 0;
+  uint64_t size = 0;
+  Raid0Geometry geo{};
+  int numa = -1;
+};
+
+static std::mutex g_stripes_mu;
+static std::map<int, std::shared_ptr<Engine::StripeSet>> g_stripes;
+static int g_next_stripe = 0;
+
+static int stripe_ident_bmap(void *, uint64_t fblk, uint64_t *dblk) {
+  *dblk = fblk;
+  return 0;
+}
 
 static std::mutex g_engine_mu;
 static Engine *g_engine = nullptr;
@@ -195,7 +217,68 @@ static void attach_residency(Engine::OpenFile *fp, PlanParams *pp,
   pp->resident = [fp](uint64_t off, uint32_t len) { return fp->resident(off, len); };
 }
 
+int Engine::stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size) {
+  if (!fds || n == 0 || n > STROM_RAID0_MAX_DISKS) return -EINVAL;
+  if (unit < 4096 || (unit & 4095) || size == 0) return -EINVAL;
+  auto ss = std::make_shared<StripeSet>();
+  ss->unit = unit;
+  ss->size = size;
+  const uint64_t nstripes = (size + unit - 1) / unit;
+  std::set<int> nodes;
+  for (uint32_t k = 0; k < n; ++k) {
+    int err = 0;
+    auto f = open_file(fds[k], &err);
+    if (!f) return err;
+    // member k holds stripes k, k+n, ...: the last of them may be partial
+    const uint64_t mine = nstripes > k ? (nstripes - k + n - 1) / n : 0;
+    uint64_t need = mine * (uint64_t)unit;
+    if (mine && (nstripes - 1) % n == k) need -= (uint64_t)unit * nstripes - size;
+    if ((uint64_t)f->fc.size < need) return -ERANGE;
+    nodes.insert(f->fc.numa_node);
+    ss->m.push_back(f);
+  }
+  ss->numa = nodes.size() == 1 ? *nodes.begin() : -1;
+  Raid0Geometry &g = ss->geo;
+  g.chunk_sects = unit >> 9;
+  g.nzones = 1;
+  g.ndisks = n;
+  // the zone spans whole stripe rows, so the tail row maps like the rest
+  const uint64_t rows = (nstripes + n - 1) / n;
+  g.zone_end[0] = rows * n * (uint64_t)(unit >> 9);
+  g.zone_dev_start[0] = 0;
+  g.zone_nb_dev[0] = n;
+  for (uint32_t k = 0; k < n; ++k) g.zone_devs[0][k] = (uint8_t)k;
+  if (strom_core_raid0_check(&g)) return -EINVAL;
+  std::lock_guard<std::mutex> l(g_stripes_mu);
+  if (g_stripes.size() >= 4096) return -EMFILE;
+  int fd;
+  do {
+    fd = kStripeFdBase + (g_next_stripe++ & 0xffffff);
+  } while (g_stripes.count(fd));
+  g_stripes[fd] = ss;
+  return fd;
+}
+
+int Engine::stripe_close(int sfd) {
+  std::lock_guard<std::mutex> l(g_stripes_mu);
+  return g_stripes.erase(sfd) ? 0 : -EBADF;
+}
+
+std::shared_ptr<Engine::StripeSet> Engine::stripe(int fd) {
+  if (fd < kStripeFdBase) return nullptr;
+  std::lock_guard<std::mutex> l(g_stripes_mu);
+  auto it = g_stripes.find(fd);
+  return it == g_stripes.end() ? nullptr : it->second;
+}
+
 int Engine::check_file(strom_check_file *a) {
+  if (a->fdesc >= kStripeFdBase) {
+    auto ss = stripe(a->fdesc);
+    if (!ss) return -EBADF;
+    a->numa_node_id = ss->numa;
+    a->support_dma64 = 1;
+    return 0;
+  }
   FileClass fc;
   int rc = classify_file(a->fdesc, &fc, config().strict);
   if (rc) return rc;
@@ -231,7 +314,8 @@ static int copy_ram_chunks(int fd, const ChunkPlan &plan, uint32_t chunk_sz, uin
 
 static void build_requests(Task *t, const ChunkPlan &plan, int fd_direct, int fd_buffered,
                            uint64_t file_size, GpuMapping *gmap, uint64_t dest_base,
-                           bool dest_is_host, std::vector<IoReq> *out) {
+                           bool dest_is_host, std::vector<IoReq> *out,
+                           const Engine::StripeSet *ss = nullptr) {
   uint64_t t0 = tsc_now();
   out->reserve(plan.ssd.size());
   uint64_t now_ns = mono_ns();
@@ -243,6 +327,14 @@ static void build_requests(Task *t, const ChunkPlan &plan, int fd_direct, int fd
     q.off = r.file_off;
     q.len = r.len;
     q.valid = (uint32_t)std::min<uint64_t>(r.len, file_size > r.file_off ? file_size - r.file_off : 0);
+    if (ss && r.member >= 0) {
+      // stripe-set member: its own descriptors and byte offset; the bytes
+      // past the logical end are zero-filled like a file's tail
+      const auto &mf = ss->m[(size_t)r.member];
+      q.fd = mf->fd_direct;
+      q.fd_buffered = mf->fd_buffered;
+      q.off = r.msect << 9;
+    }
     if (dest_is_host) {
       q.host_dst = (uint8_t *)(dest_base + r.dest_off);
     } else {
@@ -272,21 +364,30 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   uint64_t bytes = (uint64_t)a->nr_chunks * a->chunk_sz;
   if (gmap->map_offset + a->offset + bytes > gmap->map_length) return -ERANGE;
   int err = 0;
-  auto f = open_file(a->file_desc, &err);
-  if (!f) return err;
+  auto ss = stripe(a->file_desc);
+  std::shared_ptr<OpenFile> f;
+  if (!ss) {
+    if (a->file_desc >= kStripeFdBase) return -EBADF;
+    f = open_file(a->file_desc, &err);
+    if (!f) return err;
+  }
 
   PlanParams pp;
   pp.ids = a->chunk_ids;
   pp.nr_chunks = a->nr_chunks;
   pp.chunk_sz = a->chunk_sz;
   pp.relseg_sz = a->relseg_sz;
-  pp.file_size = (uint64_t)f->fc.size;
+  pp.file_size = ss ? ss->size : (uint64_t)f->fc.size;
   pp.max_request = config().max_request;
   pp.reorder = true;
+  if (ss) {
+    pp.raid0 = &ss->geo;
+    pp.bmap = stripe_ident_bmap;
+  }
   phase_mark(0);
   std::vector<unsigned char> resv;
   uint64_t res_lo = 0;
-  if (config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
+  if (f && config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
   ChunkPlan plan;
   int rc = plan_chunks(pp, &plan);
   if (rc) return rc;
@@ -306,8 +407,8 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   t->gmap = gmap;
   bool host_dest = gmap->device < 0;  // emulated GPU memory (CPU tests)
   std::vector<IoReq> reqs;
-  build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, gmap.get(),
-                 gmap->va + a->offset, host_dest, &reqs);
+  build_requests(t, plan, f ? f->fd_direct : -1, f ? f->fd_buffered : -1, pp.file_size,
+                 gmap.get(), gmap->va + a->offset, host_dest, &reqs, ss.get());
   phase_mark(2);
   uint64_t t0 = tsc_now();
   if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
@@ -317,8 +418,9 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
   stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
 
-  // page-cache chunks overlap with the storage reads
-  if (plan.nr_ram) {
+  // page-cache chunks overlap with the storage reads (none for stripe sets:
+  // their members are read with O_DIRECT, coherent with dirty pages)
+  if (plan.nr_ram && f) {
     rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, ram_dest);
     if (rc == 0 && !a->wb_buffer) gmap->bar_flush((const uint8_t *)ram_dest);
   }
@@ -342,6 +444,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
 long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off,
                         uint64_t len) {
   if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
+  if (fd >= kStripeFdBase) return -EAGAIN;  // stripe sets: the planner routes members
   auto gmap = gpu_registry().get(handle);
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
@@ -387,20 +490,29 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   int rc = dmabuf_registry().resolve(a->dest_uaddr, bytes, &dbuf, &dest_off);
   if (rc) return rc;
   int err = 0;
-  auto f = open_file(a->file_desc, &err);
-  if (!f) return err;
+  auto ss = stripe(a->file_desc);
+  std::shared_ptr<OpenFile> f;
+  if (!ss) {
+    if (a->file_desc >= kStripeFdBase) return -EBADF;
+    f = open_file(a->file_desc, &err);
+    if (!f) return err;
+  }
 
   PlanParams pp;
   pp.ids = a->chunk_ids;
   pp.nr_chunks = a->nr_chunks;
   pp.chunk_sz = a->chunk_sz;
   pp.relseg_sz = a->relseg_sz;
-  pp.file_size = (uint64_t)f->fc.size;
+  pp.file_size = ss ? ss->size : (uint64_t)f->fc.size;
   pp.max_request = config().max_request;
   pp.reorder = false;
+  if (ss) {
+    pp.raid0 = &ss->geo;
+    pp.bmap = stripe_ident_bmap;
+  }
   std::vector<unsigned char> resv;
   uint64_t res_lo = 0;
-  if (config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
+  if (f && config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
   ChunkPlan plan;
   rc = plan_chunks(pp, &plan);
   if (rc) return rc;
@@ -408,8 +520,8 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   Task *t = tasks().create(session);
   t->dbuf = dbuf;
   std::vector<IoReq> reqs;
-  build_requests(t, plan, f->fd_direct, f->fd_buffered, pp.file_size, nullptr,
-                 (uint64_t)a->dest_uaddr, true, &reqs);
+  build_requests(t, plan, f ? f->fd_direct : -1, f ? f->fd_buffered : -1, pp.file_size, nullptr,
+                 (uint64_t)a->dest_uaddr, true, &reqs, ss.get());
   uint64_t t0 = tsc_now();
   if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
     io_->run_inline(reqs[0]);
@@ -417,7 +529,7 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
     io_->submit(reqs);
   stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
   stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
-  if (plan.nr_ram)
+  if (plan.nr_ram && f)
     rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, (char *)a->dest_uaddr);
   t->frozen = true;
   uint64_t id = t->id;
@@ -850,6 +962,13 @@ int strom_dmabuf_munmap(void *addr, size_t length) {
 }
 
 int strom_dmabuf_gc(void) { return dmabuf_registry().gc(); }
+
+int strom_stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size) {
+  if (kernel_fd() >= 0) return -EOPNOTSUPP;  // kernel provider: md raid0 routes
+  return engine().stripe_open(fds, n, unit, size);
+}
+
+int strom_stripe_close(int sfd) { return engine().stripe_close(sfd); }
 
 int strom_file_topology(int fd, strom_file_topo *out) {
   if (!out) return -EFAULT;

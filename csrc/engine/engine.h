@@ -309,7 +309,8 @@ struct IoRange {
   uint64_t file_off;
   uint64_t dest_off;
   uint32_t len;
-  int member;                // raid0 member (-1 = whole device)
+  int member;                // raid0 / stripe-set member (-1 = whole device)
+  uint64_t msect = 0;        // member 512-B sector (member >= 0)
 };
 
 struct ChunkPlan {
@@ -473,6 +474,13 @@ class Engine {
   long pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off, uint64_t len);
   IoEngine &io() { return *io_; }
   struct OpenFile;
+  // Stripe sets (PAR2 without md): a logical file striped in `unit`-byte
+  // stripes over member files, usually one per SSD; the returned pseudo
+  // descriptor is accepted wherever a file descriptor is (CHECK_FILE,
+  // SSD2GPU, SSD2RAM).  Process-wide: survives engine resets.
+  int stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size);
+  int stripe_close(int sfd);
+  struct StripeSet;
 
  private:
   int check_file(strom_check_file *a);
@@ -483,10 +491,15 @@ class Engine {
 
   std::shared_ptr<OpenFile> open_file(int fd, int *err);
 
+  std::shared_ptr<StripeSet> stripe(int fd);
+
   std::unique_ptr<IoEngine> io_;
   std::mutex files_mu_;
   std::map<std::pair<dev_t, ino_t>, std::shared_ptr<OpenFile>> files_;
 };
+
+// pseudo descriptors of stripe sets: far above any real fd
+constexpr int kStripeFdBase = 0x7f000000;
 
 Engine &engine();
 void engine_reset();

@@ -254,7 +254,7 @@ std::string nvme_controller_bdf(const std::string &disk) {
 namespace {
 int plan_submit(void *ctx, const strom_extent *e) {
   auto *out = (ChunkPlan *)ctx;
-  out->ssd.push_back(IoRange{e->file_off, e->dest, e->len, e->member});
+  out->ssd.push_back(IoRange{e->file_off, e->dest, e->len, e->member, e->sect});
   return 0;
 }
 int ident_bmap(void *, uint64_t fblk, uint64_t *dblk) {

@@ -78,6 +78,15 @@ int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
  * (MAP_GPU_DMABUF).  The caller closes the fd. */
 int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset);
 
+/* Stripe set: a logical file of `size` bytes striped in `unit`-byte
+ * stripes (multiple of 4 KiB) over n member files (stripe s in member
+ * s % n at offset (s / n) * unit) — one member per SSD aggregates them
+ * without md.  Returns a pseudo descriptor usable as file_desc for
+ * CHECK_FILE / SSD2GPU / SSD2RAM / strom_pread_gpu until closed; -ERANGE
+ * when a member is too short.  Userspace provider only. */
+int strom_stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size);
+int strom_stripe_close(int sfd);
+
 /* SSD2RAM destinations: mmap (MAP_SHARED, read/write) `length` bytes of an
  * ALLOC_DMA_BUFFER fd through the engine, so the range is found in the
  * registry's address index; NULL + errno on failure.  Unmap with

@@ -67,13 +67,6 @@ __device__ unsigned long long g_prof[kPN];
 enum : int32_t { kErrFormat = -1, kErrOverflow = -2 };
 enum : uint32_t { kHdr = 0, kLz4 = 1, kSnappy = 2, kDone = 3 };
 
-__device__ __forceinline__ uint32_t ld_bypass_byte(const uint8_t *p) {
-  // dword-aligned agent-scope relaxed load: skips L1, sees this wave's
-  // fenced stores
-  const uint32_t *w = (const uint32_t *)((uintptr_t)p & ~(uintptr_t)3);
-  uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return (v >> (8 * ((uintptr_t)p & 3))) & 0xff;
-}
 
 // Group-uniform stream state (every lane of a group holds the same values).
 template <uint32_t GL_, uint32_t RING_, uint32_t INW_>
@@ -270,14 +263,22 @@ struct Stream {
           // pace() keeps these sources flushed already; stay safe anyway
           PROF_T0();
           if (s - off + n > flushed) flush(s, true);
-          __threadfence();
+          // our stores complete at L2 before the L1-bypassing loads below
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
           vis = flushed;
           PROF_ADD(kPFarFence);
         }
         if (k < n) {
+          // two L1-bypassing dword loads + alignbyte per lane (the second
+          // dword ends below s: off > 3W)
+          const uintptr_t q = (uintptr_t)(out + s + k - off);
+          const uint32_t *w = (const uint32_t *)(q & ~(uintptr_t)3);
+          const uint32_t d0 = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t d1 = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(q & 3));
 #pragma unroll
           for (uint32_t j = 0; j < BPL; ++j)
-            if (k + j < n) put(s + k + j, (uint8_t)ld_bypass_byte(out + s + k + j - off));
+            if (k + j < n) put(s + k + j, (uint8_t)(v >> (8 * j)));
         }
         pace(s + n);
       }
@@ -522,7 +523,11 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
 #endif
 }
 
-using S16 = Stream<4, 2048, 512>;     // 16 streams per wave, 40 KiB LDS per wave
+// 16 x 2496 B = 39 KiB (+ the runtime's 512 B) lets 4 waves share a CU's
+// 160 KiB: at 40.5 KiB only 3 fit (round 2 trace: LDS_Block_Size 41472)
+using S16 = Stream<4, 2048, 448>;     // 16 streams per wave
+// A/B variant: half the LDS (2 waves per SIMD), a 1 KiB history ring
+using S16s = Stream<4, 1024, 224>;    // 16 streams per wave, 19.5 KiB
 using S4 = Stream<16, 2048, 512>;     // 4 streams per wave, 10 KiB
 using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
 
@@ -540,7 +545,8 @@ int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d
 
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
-// STROM_DECOMP_G (1, 4, 16) forces a geometry (A/B runs).
+// STROM_DECOMP_G (1, 4, 16; 32 = 16 with the small ring) forces a
+// geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
@@ -548,11 +554,15 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   if (!nblocks) return 0;
   const char *e = getenv("STROM_DECOMP_G");
   uint32_t g = e ? (uint32_t)atoi(e) : 0u;
-  // 16 streams per wave won at 16k streams (107 vs 76 vs 21 GB/s for
-  // 16 / 4 / 1, round 2 kbench); fewer streams spread over more waves
-  if (g != 1 && g != 4 && g != 16) g = nblocks >= 4096 ? 16 : nblocks >= 1024 ? 4 : 1;
+  // 16 streams per wave wins at every stream count measured (round 2
+  // decprof: 16k streams 107 / 76 / 21 GB/s for 16 / 4 / 1 streams per
+  // wave, 1k streams 5.3 / 2.7 / 2.9): wide groups pay more per sequence
+  // (the short-period path covers every offset below the pass width) than
+  // they gain from more resident waves
+  if (g != 1 && g != 4 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  if (g == 32) return launch<S16s>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 4) return launch<S4>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   return launch<S1>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
 }

@@ -283,6 +283,71 @@ def alloc_dma_buffer(length: int, node: int = -1, sess: Optional[Session] = None
     return DmaBuffer(length, node, sess)
 
 
+# -------------------------------------------------------------- stripe sets
+class StripeSet:
+    """A logical file striped over member files, one per SSD (SURVEY §2.3
+    PAR2 without md): stripe ``s`` of ``unit`` bytes lives in member
+    ``s % n`` at offset ``(s // n) * unit``.  ``fd`` is a pseudo descriptor
+    the engine accepts wherever it takes a file descriptor (CHECK_FILE,
+    MEMCPY_SSD2GPU / SSD2RAM, pread_gpu, FileReader / StreamLoader).
+    Requests split at stripe boundaries and run on every member at once.
+    """
+
+    def __init__(self, members, unit: int = 1 << 20, size: Optional[int] = None):
+        self.unit = int(unit)
+        self._own = []
+        fds = []
+        for m in members:
+            if isinstance(m, int):
+                fds.append(m)
+            else:
+                fd = os.open(m, os.O_RDONLY)
+                self._own.append(fd)
+                fds.append(fd)
+        self.members = list(members)
+        self.size = int(size) if size is not None else sum(os.fstat(fd).st_size for fd in fds)
+        arr = (C.c_int * len(fds))(*fds)
+        rc = N.lib().strom_stripe_open(arr, len(fds), self.unit, self.size)
+        if rc < 0:
+            for fd in self._own:
+                os.close(fd)
+            raise StromError(-rc, "strom_stripe_open")
+        self.fd = rc
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            N.lib().strom_stripe_close(self.fd)
+            self.fd = -1
+            for fd in self._own:
+                os.close(fd)
+            self._own = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def write_striped(paths, data, unit: int = 1 << 20) -> int:
+    """Write ``data`` (bytes-like) as a stripe set over ``paths``; returns
+    the logical size (test and benchmark helper)."""
+    mv = memoryview(np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray)
+                    else data.view(np.uint8).reshape(-1))
+    n = len(paths)
+    files = [open(p, "wb") for p in paths]
+    try:
+        for s, off in enumerate(range(0, len(mv), unit)):
+            files[s % n].write(mv[off:off + unit])
+        for f in files:
+            f.flush()
+            os.fsync(f.fileno())
+    finally:
+        for f in files:
+            f.close()
+    return len(mv)
+
+
 # ---------------------------------------------------------------- MEMCPY_*
 @dataclass
 class CopyResult:

@@ -69,12 +69,18 @@ class HbmBuffer:
 class FileReader:
     """MEMCPY_SSD2GPU driver for one file."""
 
-    def __init__(self, path: str, chunk_sz: int = 8192, relseg_sz: int = 0,
+    def __init__(self, path, chunk_sz: int = 8192, relseg_sz: int = 0,
                  max_chunks: int = 4096, sess: Optional[api.Session] = None,
                  direct_ram: bool = True):
+        # a path, or an api.StripeSet (its pseudo descriptor and logical size)
         self.path = path
-        self.fd = os.open(path, os.O_RDONLY)
-        self.size = os.fstat(self.fd).st_size
+        self._own_fd = not isinstance(path, api.StripeSet)
+        if self._own_fd:
+            self.fd = os.open(path, os.O_RDONLY)
+            self.size = os.fstat(self.fd).st_size
+        else:
+            self.fd = path.fd
+            self.size = path.size
         self.chunk_sz = chunk_sz
         self.relseg_sz = relseg_sz
         self.sess = sess or api.session()
@@ -142,7 +148,8 @@ class FileReader:
 
     def close(self) -> None:
         if self.fd >= 0:
-            os.close(self.fd)
+            if self._own_fd:
+                os.close(self.fd)
             self.fd = -1
 
     def __enter__(self):
@@ -158,7 +165,7 @@ def load_file(path: str, device=None, chunk_sz: int = 1 << 20, window: int = 64 
 
     Windows of ``window`` bytes are issued ``inflight`` at a time so storage
     reads, SDMA copies and ioctl submission overlap."""
-    size = os.path.getsize(path)
+    size = path.size if isinstance(path, api.StripeSet) else os.path.getsize(path)
     padded = (size + chunk_sz - 1) // chunk_sz * chunk_sz
     own = buf is None
     if own:
