@@ -108,6 +108,82 @@ uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno, uint32_t page_
   return (uint16_t)((x % 65535u) + 1);
 }
 
+// ---- MVCC visibility of heap tuples (HeapTupleSatisfiesMVCC, simplified):
+// hint bits first, then the commit log (pg_xact layout: 2 bits per xid,
+// 0 in progress / 1 committed / 2 aborted / 3 sub-committed), then the
+// snapshot (visible: committed and xid < xmin, or xid < xmax and not in xip).
+namespace {
+constexpr uint16_t kXminCommitted = 0x0100, kXminInvalid = 0x0200, kXmaxCommitted = 0x0400,
+                   kXmaxInvalid = 0x0800, kXmaxLockOnly = 0x0080;
+struct Snap {
+  uint32_t xmin, xmax;
+  const uint32_t *xip;
+  uint32_t nxip;
+  const uint8_t *clog;
+  uint64_t nclog;      // xids covered by clog
+};
+int xid_status(const Snap &s, uint32_t xid) {
+  if (xid < 3) return xid == 0 ? 2 : 1;            // invalid / bootstrap, frozen
+  if (!s.clog || xid >= s.nclog) return 0;           // unknown: in progress
+  return (s.clog[xid >> 2] >> ((xid & 3) * 2)) & 3;
+}
+bool in_snapshot(const Snap &s, uint32_t xid) {
+  if (xid < 3 || xid < s.xmin) return true;
+  if (xid >= s.xmax) return false;
+  for (uint32_t i = 0; i < s.nxip; ++i)
+    if (s.xip[i] == xid) return false;
+  return true;
+}
+bool mvcc_visible(const Snap &s, const uint8_t *tup) {
+  const uint32_t xmin = rd32(tup), xmax = rd32(tup + 4);
+  const uint16_t mask = (uint16_t)(tup[20] | (tup[21] << 8));
+  const bool frozen = (mask & (kXminCommitted | kXminInvalid)) == (kXminCommitted | kXminInvalid);
+  if (!frozen) {
+    if (mask & kXminInvalid) return false;
+    const bool committed = (mask & kXminCommitted) || xid_status(s, xmin) == 1;
+    if (!committed || !in_snapshot(s, xmin)) return false;
+  }
+  if ((mask & kXmaxInvalid) || xmax == 0 || (mask & kXmaxLockOnly)) return true;
+  const bool deleted = (mask & kXmaxCommitted) || xid_status(s, xmax) == 1;
+  return !(deleted && in_snapshot(s, xmax));
+}
+}  // namespace
+
+long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
+                             const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
+                             uint64_t clog_xids) {
+  uint8_t *p = (uint8_t *)page;
+  const uint16_t lower = (uint16_t)(p[12] | (p[13] << 8)), flags = (uint16_t)(p[10] | (p[11] << 8));
+  if (lower < 24 || lower > page_sz) return -22;
+  if (flags & 0x0004) return 0;                      // PD_ALL_VISIBLE: nothing to check
+  const Snap s{snap_xmin, snap_xmax, xip, nxip, clog, clog_xids};
+  long removed = 0;
+  for (uint32_t i = 0; i < (uint32_t)(lower - 24) / 4; ++i) {
+    uint8_t *lpp = p + 24 + 4 * i;
+    uint32_t lp = rd32(lpp);
+    const uint32_t off = lp & 0x7fff, fl = (lp >> 15) & 3, len = lp >> 17;
+    if (fl != 1 || len < 23 || off < 24 || off + len > page_sz) continue;
+    if (mvcc_visible(s, p + off)) continue;
+    lp &= ~(3u << 15);                               // LP_UNUSED, as the reference marks them
+    memcpy(lpp, &lp, 4);
+    ++removed;
+  }
+  return removed;
+}
+
+uint64_t strom_atomic_fetch_add_u64(uint64_t *addr, uint64_t v) {
+  return __atomic_fetch_add(addr, v, __ATOMIC_SEQ_CST);
+}
+
+int strom_atomic_cas_u64(uint64_t *addr, uint64_t expect, uint64_t desired) {
+  return __atomic_compare_exchange_n(addr, &expect, desired, false, __ATOMIC_SEQ_CST,
+                                     __ATOMIC_SEQ_CST) ? 1 : 0;
+}
+
+uint64_t strom_atomic_load_u64(const uint64_t *addr) {
+  return __atomic_load_n(addr, __ATOMIC_SEQ_CST);
+}
+
 long strom_lz4_compress_host(const void *src, size_t n, void *dst, size_t cap) {
   const uint8_t *ip = (const uint8_t *)src, *base = ip, *iend = ip + n;
   const uint8_t *anchor = ip;

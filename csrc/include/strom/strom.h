@@ -216,6 +216,19 @@ struct strom_heap_scan_args {
 int strom_heap_scan(const struct strom_heap_scan_args *a, void *stream);
 uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
                                 uint32_t page_sz);
+/* Per-tuple MVCC check of a heap page against a snapshot (xmin, xmax,
+ * in-progress xids) and a commit log (pg_xact layout, 2 bits per xid):
+ * invisible LP_NORMAL tuples are marked LP_UNUSED in place, as the
+ * reference does before copying buffer-manager blocks into its chunk
+ * (pgsql/nvme_strom.c:896-940).  PD_ALL_VISIBLE pages are left alone.
+ * Returns the tuples removed. */
+long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
+                             const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
+                             uint64_t clog_xids);
+/* fetch-and-add on shared memory (cross-process scan cursors) */
+uint64_t strom_atomic_fetch_add_u64(uint64_t *addr, uint64_t v);
+int strom_atomic_cas_u64(uint64_t *addr, uint64_t expect, uint64_t desired);
+uint64_t strom_atomic_load_u64(const uint64_t *addr);
 
 /* LZ4 / snappy raw-block batch decode: one block per wavefront. */
 struct strom_decomp_desc {

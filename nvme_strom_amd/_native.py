@@ -186,6 +186,11 @@ _SIGS = {
     "strom_snappy_compress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
     "strom_snappy_decompress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
     "strom_pg_checksum_host": (C.c_uint16, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "strom_pg_apply_snapshot": (C.c_long, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
+    "strom_atomic_fetch_add_u64": (C.c_uint64, [C.c_void_p, C.c_uint64]),
+    "strom_atomic_cas_u64": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64]),
+    "strom_atomic_load_u64": (C.c_uint64, [C.c_void_p]),
     "strom_gpu_count": (C.c_int, []),
     "strom_crc32c_chunks": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     "strom_crc32c_combine": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64,

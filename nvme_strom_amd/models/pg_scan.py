@@ -8,7 +8,16 @@ Reference map (pgsql/nvme_strom.c):
     (:1258-1268) and cost (:398-467)              -> :func:`use_strom`, :func:`scan_cost`
   * tablespace capability cache (:192-295)        -> :class:`TablespaceCache`
   * parallel block cursor in DSM (:90-104, :1181-1233) -> :class:`ParallelCursor`
+    (threads of one process) and :class:`SharedCursor` (a shared-memory
+    segment + native atomics: participants in separate processes)
+  * planner hook set_rel_pathlist_hook -> add_path(CustomPath) with the
+    threshold and cost model (:502-580)             -> :func:`plan_scan`
   * chunk ring + load + tuple iteration (:852-1123) -> :class:`HeapRelationScan`
+  * visibility-map routing (:870-940): with a snapshot, all-visible blocks
+    go to DMA unchecked, the others are read through the host ("buffer
+    manager") and every tuple is checked against the snapshot + commit log,
+    invisible ones marked unused, before the chunk is scanned
+    (utils/pgmvcc.py, native strom_pg_apply_snapshot)
   * ExecReScanNVMEStrom cursor reset (:1168-1176)  -> :meth:`ParallelCursor.rescan`;
     the reference persists no scan state, :class:`ResumableScan` adds
     block-range checkpoints so an interrupted scan resumes where it stopped
@@ -37,7 +46,8 @@ import torch
 from .. import api
 from ..ops.heapscan import heap_scan
 from ..tensor import FileReader, HbmBuffer, host_buffer
-from ..utils import pgpage
+from ..utils import pgmvcc, pgpage
+from ..utils.pgmvcc import CommitLog, Snapshot
 
 BLCKSZ = 8192
 RELSEG_SIZE = 131072          # blocks per segment file (1 GiB)
@@ -52,6 +62,11 @@ class ScanConfig:
     debug_no_threshold: bool = False
     verify_checksum: bool = False
     skip_invisible: bool = True
+    # MVCC mode: with a snapshot, blocks route by the visibility map (all-
+    # visible -> DMA, unchecked; others -> host read + per-tuple snapshot
+    # check); without one, the GPU applies hint bits / PD_ALL_VISIBLE
+    snapshot: Optional[Snapshot] = None
+    clog: Optional[CommitLog] = None
 
     def validate(self) -> None:
         if self.chunk_size % BLCKSZ or self.buffer_size % self.chunk_size:
@@ -73,6 +88,42 @@ def scan_cost(pages: int, cfg: ScanConfig, parallel_workers: int = 0,
               cpu_tuple_cost: float = 0.01, tuples: int = 0) -> float:
     divisor = 1.0 + min(parallel_workers, 4) if parallel_workers else 1.0
     return (cfg.seq_page_cost * pages + cpu_tuple_cost * tuples) / divisor
+
+
+@dataclass
+class ScanPlan:
+    path: str                    # "nvme_strom" or "seqscan"
+    cost: float
+    workers: int
+    seqscan_cost: float
+    reason: str
+
+    def explain(self) -> str:
+        node = "Custom Scan (NVMEStrom)" if self.path == "nvme_strom" else "Seq Scan"
+        par = f" (parallel workers={self.workers})" if self.workers else ""
+        return f"{node}{par}  (cost=0.00..{self.cost:.2f})  -- {self.reason}"
+
+
+def plan_scan(rel_bytes: int, ntuples: int, ram_bytes: int, shared_buffers: int,
+              cfg: Optional[ScanConfig] = None, tablespace_ok: bool = True,
+              parallel_workers: int = 0, seq_page_cost: float = 1.0,
+              cpu_tuple_cost: float = 0.01) -> ScanPlan:
+    """The planner hook's decision (nvmestrom_add_scan_path,
+    pgsql/nvme_strom.c:502-543): offer the strom path only for relations
+    on an NVMe-capable tablespace above the threshold, cost it with
+    ``seq_page_cost`` (divided for parallel plans, :398-467) and keep it
+    when it beats the ordinary sequential scan."""
+    cfg = cfg or ScanConfig()
+    pages = (rel_bytes + BLCKSZ - 1) // BLCKSZ
+    seq = seq_page_cost * pages + cpu_tuple_cost * ntuples
+    if not use_strom(rel_bytes, ram_bytes, shared_buffers, cfg, tablespace_ok):
+        why = ("disabled" if not cfg.enabled else "tablespace not on NVMe" if not tablespace_ok
+               else f"below threshold {strom_threshold(ram_bytes, shared_buffers)} bytes")
+        return ScanPlan("seqscan", seq, 0, seq, why)
+    cost = scan_cost(pages, cfg, parallel_workers, cpu_tuple_cost, ntuples)
+    if cost < seq:
+        return ScanPlan("nvme_strom", cost, parallel_workers, seq, "cheaper than seqscan")
+    return ScanPlan("seqscan", seq, 0, seq, "seqscan is cheaper")
 
 
 class TablespaceCache:
@@ -131,8 +182,88 @@ class ParallelCursor:
             self._next = self.start
 
 
+class SharedCursor:
+    """Cross-process block cursor + scan counters in a shared-memory segment
+    (the reference's NVMEStromParallelDesc in DSM: nsp_cblock claimed with
+    pg_atomic_fetch_add_u64, per-scan counters; pgsql/nvme_strom.c:90-104,
+    :1181-1233).  The leader creates it; workers attach by name.  Claims use
+    a native compare-and-swap, so they never cross a ``boundary`` (segment
+    file) and no block is handed out twice across processes."""
+
+    MAGIC = 0x53545243555253  # "STRCURS"
+    FIELDS = ("magic", "nblocks", "start", "next") + ("pages", "bad_pages", "nr_ram", "nr_ssd",
+                                                       "nr_dma_submit", "nr_dma_blocks",
+                                                       "chunks", "tuples")
+
+    def __init__(self, name: str, nblocks: int = 0, start: int = 0, create: bool = False):
+        import mmap as _mmap
+        self.name = name
+        self.path = f"/dev/shm/nvme-strom-scan.{name}"
+        flags = os.O_RDWR | (os.O_CREAT | os.O_EXCL if create else 0)
+        fd = os.open(self.path, flags, 0o600)
+        try:
+            if create:
+                os.ftruncate(fd, 8 * len(self.FIELDS))
+            self._mm = _mmap.mmap(fd, 8 * len(self.FIELDS))
+        finally:
+            os.close(fd)
+        self._a = np.frombuffer(self._mm, dtype=np.uint64)
+        self._lib = api.N.lib()
+        if create:
+            self._a[:] = 0
+            self._a[1], self._a[2], self._a[3] = nblocks, start, start
+            self._a[0] = self.MAGIC
+        elif int(self._a[0]) != self.MAGIC:
+            raise ValueError(f"{self.path}: not a scan cursor")
+        self.owner = create
+
+    def _addr(self, i: int) -> int:
+        return self._a.ctypes.data + 8 * i
+
+    @property
+    def nblocks(self) -> int:
+        return int(self._a[1])
+
+    def claim(self, n: int, boundary: int = 0) -> Tuple[int, int]:
+        end = self.nblocks
+        while True:
+            lo = int(self._lib.strom_atomic_load_u64(self._addr(3)))
+            if lo >= end:
+                return lo, 0
+            hi = min(end, lo + n)
+            if boundary:
+                hi = min(hi, (lo // boundary + 1) * boundary)
+            if self._lib.strom_atomic_cas_u64(self._addr(3), lo, hi):
+                return lo, hi - lo
+
+    def rescan(self) -> None:
+        self._a[3] = self._a[2]
+
+    def add(self, r: "ScanResult") -> None:
+        for i, k in enumerate(self.FIELDS[4:], start=4):
+            v = r.ntuples if k == "tuples" else int(getattr(r, k))
+            if v:
+                self._lib.strom_atomic_fetch_add_u64(self._addr(i), v)
+
+    def counters(self) -> Dict[str, int]:
+        return {k: int(self._lib.strom_atomic_load_u64(self._addr(i)))
+                for i, k in enumerate(self.FIELDS[4:], start=4)}
+
+    def close(self, unlink: Optional[bool] = None) -> None:
+        if self._mm is not None:
+            self._a = None
+            self._mm.close()
+            self._mm = None
+        if self.owner if unlink is None else unlink:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
 class Relation:
-    """A heap relation stored as PostgreSQL segment files: path, path.1, ..."""
+    """A heap relation stored as PostgreSQL segment files: path, path.1, ...
+    plus its visibility-map fork ``path_vm`` when present."""
 
     def __init__(self, path: str, relseg_size: int = RELSEG_SIZE):
         self.path = path
@@ -149,9 +280,17 @@ class Relation:
             raise FileNotFoundError(path)
         sizes = [os.path.getsize(p) for p in self.segments]
         self.nblocks = sum(s // BLCKSZ for s in sizes)
+        self.vm = pgmvcc.read_vm(pgmvcc.vm_path(path), self.nblocks)
+
+    def all_visible(self, lo: int, n: int) -> np.ndarray:
+        """VM all-visible bits of blocks [lo, lo+n) (all False without a VM)."""
+        if self.vm is None:
+            return np.zeros(n, dtype=bool)
+        return (self.vm[lo:lo + n] & pgmvcc.VM_ALL_VISIBLE).astype(bool)
 
     @staticmethod
-    def write(path: str, data: bytes, relseg_size: int = RELSEG_SIZE) -> "Relation":
+    def write(path: str, data: bytes, relseg_size: int = RELSEG_SIZE,
+              all_visible: Optional[Sequence[bool]] = None) -> "Relation":
         seg = relseg_size * BLCKSZ
         for k, lo in enumerate(range(0, len(data), seg)):
             p = path if k == 0 else f"{path}.{k}"
@@ -159,6 +298,8 @@ class Relation:
                 f.write(data[lo:lo + seg])
                 f.flush()
                 os.fsync(f.fileno())
+        if all_visible is not None:
+            pgmvcc.write_vm(pgmvcc.vm_path(path), all_visible)
         return Relation(path, relseg_size)
 
 
@@ -177,6 +318,9 @@ class ScanResult:
     nr_dma_blocks: int = 0
     chunks: int = 0
     workers: int = 1
+    # MVCC mode: blocks that took the checked (host) path, tuples it removed
+    nr_checked: int = 0
+    removed: int = 0
 
     @property
     def ntuples(self) -> int:
@@ -198,6 +342,8 @@ class ScanResult:
             self.nr_dma_submit += p.nr_dma_submit
             self.nr_dma_blocks += p.nr_dma_blocks
             self.chunks += p.chunks
+            self.nr_checked += p.nr_checked
+            self.removed += p.removed
 
     def explain(self) -> str:
         """EXPLAIN ANALYZE-style summary of the scan's I/O split and rates."""
@@ -211,6 +357,7 @@ class ScanResult:
             + (f" ({100.0 * self.nr_ram / blocks:.1f}% page cache)" if blocks else ""),
             f"  DMA: submits={self.nr_dma_submit} sectors={self.nr_dma_blocks} avg={avg_kib:.1f} KiB chunks={self.chunks}",
             f"  Bad pages: {self.bad_pages}",
+            f"  Visibility: checked blocks={self.nr_checked} tuples removed={self.removed}",
             f"  Time: {self.seconds * 1e3:.2f} ms ({rate:.1f} MiB/s)",
         ]
         return "\n".join(lines)
@@ -228,10 +375,15 @@ class HeapRelationScan:
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.pred = dict(attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi)
 
-    def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None) -> ScanResult:
-        """Scan all blocks, or the block range ``[b0, b1)`` given as ``blocks``."""
+    def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None,
+            cursor=None) -> ScanResult:
+        """Scan all blocks, or the block range ``[b0, b1)`` given as ``blocks``,
+        with ``workers`` participant threads.  ``cursor`` (e.g. a
+        :class:`SharedCursor` other processes also claim from) replaces the
+        private one: this process then scans its share."""
         b0, b1 = _block_range(blocks, self.rel.nblocks)
-        cursor = ParallelCursor(b1, start=b0)
+        if cursor is None:
+            cursor = ParallelCursor(b1, start=b0)
         results: List[ScanResult] = []
         errors: List[BaseException] = []
         t0 = time.perf_counter()
@@ -252,14 +404,18 @@ class HeapRelationScan:
         out.merge(results)
         return out
 
-    def _participant(self, cursor: ParallelCursor) -> ScanResult:
+    def _participant(self, cursor) -> ScanResult:
         cfg = self.cfg
+        mvcc = cfg.snapshot is not None
         per_chunk = cfg.chunk_size // BLCKSZ
         nslots = cfg.buffer_size // cfg.chunk_size
         sess = api.Session()
         hb = HbmBuffer(cfg.buffer_size, self.device, sess=sess)
         readers = [FileReader(p, BLCKSZ, self.rel.relseg_size, per_chunk, sess) for p in self.rel.segments]
         wbs = [host_buffer(cfg.chunk_size) for _ in range(nslots)]
+        # checked-path pages (MVCC mode) are staged here, then copied to HBM
+        # right after the chunk's DMA blocks
+        cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if mvcc else []
         ring: List[Optional[tuple]] = [None] * nslots
         found: List[np.ndarray] = []
         st = ScanResult(np.zeros(0, np.uint64))
@@ -276,8 +432,21 @@ class HeapRelationScan:
                     break
                 seg = lo // self.rel.relseg_size
                 ids = np.arange(lo, lo + n, dtype=np.uint32)
-                res, landed = readers[seg].submit(hb, slot * cfg.chunk_size, ids, wb=wbs[slot])
-                ring[slot] = (res, landed, slot, seg)
+                cpu_ids = ids[:0]
+                if mvcc:
+                    av = self.rel.all_visible(lo, n)
+                    ids, cpu_ids = ids[av], ids[~av]
+                res, landed = None, ids[:0]
+                if len(ids):
+                    res, landed = readers[seg].submit(hb, slot * cfg.chunk_size, ids,
+                                                      wb=wbs[slot])
+                if len(cpu_ids):
+                    st.removed += self._checked_pages(readers[seg].fd, cpu_ids, cpu_bufs[slot])
+                    st.nr_checked += len(cpu_ids)
+                    at = slot * cfg.chunk_size + len(ids) * BLCKSZ
+                    nb = len(cpu_ids) * BLCKSZ
+                    hb.tensor[at:at + nb].copy_(cpu_bufs[slot][:nb], non_blocking=True)
+                ring[slot] = (res, landed, slot, seg, cpu_ids)
                 k += 1
             for item in ring:
                 if item is not None:
@@ -290,14 +459,33 @@ class HeapRelationScan:
         st.items = np.concatenate(found) if found else np.zeros(0, np.uint64)
         return st
 
+    def _checked_pages(self, fd: int, blocks: np.ndarray, stage: torch.Tensor) -> int:
+        """Buffer-manager path: read each block through the page cache and
+        mark the tuples the snapshot must not see as unused."""
+        arr = stage.numpy() if stage.device.type == "cpu" else stage.cpu().numpy()
+        removed = 0
+        for j, b in enumerate(blocks.tolist()):
+            page = arr[j * BLCKSZ:(j + 1) * BLCKSZ]
+            got = os.preadv(fd, [memoryview(page)], (b % self.rel.relseg_size) * BLCKSZ)
+            if got < BLCKSZ:
+                page[got:] = 0
+            removed += pgmvcc.apply_snapshot(page, self.cfg.snapshot, self.cfg.clog,
+                                             b if self.cfg.verify_checksum else None)
+        return removed
+
     def _consume(self, item, hb, readers, found, st: ScanResult) -> None:
-        res, landed, slot, seg = item
-        readers[seg].finish(res)
+        res, landed, slot, seg, cpu_ids = item
+        if res is not None:
+            readers[seg].finish(res)
+        landed = np.concatenate([landed, cpu_ids])
         n = len(landed)
         pages = hb.tensor[slot * self.cfg.chunk_size: slot * self.cfg.chunk_size + n * BLCKSZ]
         blk = torch.from_numpy(landed.astype(np.int64).astype(np.uint32).view(np.int32)).to(pages.device)
+        # MVCC mode: visibility is settled (all-visible blocks unchecked, the
+        # rest filtered against the snapshot): every LP_NORMAL tuple counts
+        skip = self.cfg.skip_invisible and self.cfg.snapshot is None
         r = heap_scan(pages, BLCKSZ, verify_checksum=self.cfg.verify_checksum,
-                      skip_invisible=self.cfg.skip_invisible, blknos=blk, **self.pred)
+                      skip_invisible=skip, blknos=blk, **self.pred)
         it = r.items[:r.count].cpu().numpy().view(np.uint32)
         page_idx = (it >> 16).astype(np.int64)
         lineno = (it & 0xFFFF).astype(np.uint64)
@@ -306,7 +494,8 @@ class HeapRelationScan:
         status = r.page_status.cpu().numpy()
         st.pages += n
         st.bad_pages += int(((status & 3) != 0).sum())
-        st.add_io(res)
+        if res is not None:
+            st.add_io(res)
 
 
 def _block_range(blocks: Optional[Tuple[int, int]], nblocks: int) -> Tuple[int, int]:
@@ -323,6 +512,7 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
              blocks: Optional[Tuple[int, int]] = None) -> ScanResult:
     """Reference-shaped path: SSD2RAM into a NUMA DMA buffer, host tuple walk."""
     cfg = cfg or ScanConfig()
+    mvcc = cfg.snapshot is not None
     b0, b1 = _block_range(blocks, rel.nblocks)
     per_chunk = cfg.chunk_size // BLCKSZ
     t0 = time.perf_counter()
@@ -339,15 +529,42 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                 for c0 in range(first, nblk, per_chunk):
                     n = min(per_chunk, nblk - c0)
                     ids = np.arange(base + c0, base + c0 + n, dtype=np.uint32)
-                    r = api.memcpy_ssd2ram(buf.address, fd, ids, BLCKSZ, rel.relseg_size)
-                    api.memcpy_wait(r.dma_task_id)
-                    its, status = pgpage.host_scan(bytes(buf.array[:n * BLCKSZ]), BLCKSZ,
-                                                   cfg.skip_invisible, attr_off, attr_width, lo, hi,
-                                                   cfg.verify_checksum, base + c0)
-                    items.extend(((base + c0 + (i >> 16)) << 16) | (i & 0xFFFF) for i in its)
+                    cpu_ids = ids[:0]
+                    if mvcc:
+                        av = rel.all_visible(base + c0, n)
+                        ids, cpu_ids = ids[av], ids[~av]
+                    if len(ids):
+                        r = api.memcpy_ssd2ram(buf.address, fd, ids, BLCKSZ, rel.relseg_size)
+                        api.memcpy_wait(r.dma_task_id)
+                        st.add_io(r)
+                    for j, b in enumerate(cpu_ids.tolist()):
+                        # buffer-manager path: page cache read + snapshot check
+                        page = buf.array[(len(ids) + j) * BLCKSZ:(len(ids) + j + 1) * BLCKSZ]
+                        got = os.preadv(fd, [memoryview(page)], (b % rel.relseg_size) * BLCKSZ)
+                        if got < BLCKSZ:
+                            page[got:] = 0
+                        st.removed += pgmvcc.apply_snapshot(page, cfg.snapshot, cfg.clog,
+                                                            b if cfg.verify_checksum else None)
+                    st.nr_checked += len(cpu_ids)
+                    blocks_here = np.concatenate([ids, cpu_ids]).astype(np.int64)
+                    # block numbers feed the checksum: scan page by page
+                    # when the order is not the plain file order
+                    skip = cfg.skip_invisible and not mvcc
+                    raw = bytes(buf.array[:n * BLCKSZ])
+                    if np.array_equal(blocks_here, np.arange(base + c0, base + c0 + n)):
+                        its, status = pgpage.host_scan(raw, BLCKSZ, skip, attr_off, attr_width,
+                                                       lo, hi, cfg.verify_checksum, base + c0)
+                        items.extend(((base + c0 + (i >> 16)) << 16) | (i & 0xFFFF) for i in its)
+                    else:
+                        status = []
+                        for j, b in enumerate(blocks_here.tolist()):
+                            its, stt = pgpage.host_scan(raw[j * BLCKSZ:(j + 1) * BLCKSZ], BLCKSZ,
+                                                        skip, attr_off, attr_width, lo, hi,
+                                                        cfg.verify_checksum, b)
+                            items.extend((b << 16) | (i & 0xFFFF) for i in its)
+                            status += stt
                     st.pages += n
                     st.bad_pages += sum(1 for s in status if s & 3)
-                    st.add_io(r)
             finally:
                 os.close(fd)
     st.items = np.array(sorted(items), dtype=np.uint64)

@@ -100,3 +100,21 @@ def test_sharded_loader_single_rank(S, tmp_path):
         exp = data[(i % 4) * (4 << 20):][:4 << 20]
         assert np.array_equal(ld.current(i).cpu().numpy(), exp)
     ld.close()
+
+
+def test_heap_scan_vm_routing_matches_cpu(S, tmp_path):
+    """MVCC mode on the GPU: all-visible blocks DMA'd unchecked, the others
+    snapshot-checked on the host and copied behind them in HBM; the rows
+    equal the reference-shaped CPU path's."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_pg_mvcc_cpu import _mvcc_relation
+    from nvme_strom_amd.models import pg_scan
+    rel, snap, clog, want, nchecked = _mvcc_relation(tmp_path, nblocks=40)
+    cfg = pg_scan.ScanConfig(chunk_size=6 * 8192, buffer_size=18 * 8192, snapshot=snap,
+                             clog=clog, verify_checksum=True)
+    g = pg_scan.HeapRelationScan(rel, cfg, "cuda").run(workers=2)
+    assert set(g.items.tolist()) == want
+    assert g.nr_checked == nchecked and g.bad_pages == 0
+    c = pg_scan.cpu_scan(rel, cfg)
+    assert np.array_equal(g.items, c.items)
