@@ -242,8 +242,10 @@ int Engine::stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size
   g.chunk_sects = unit >> 9;
   g.nzones = 1;
   g.ndisks = n;
-  // the zone spans whole stripe rows, so the tail row maps like the rest
-  const uint64_t rows = (nstripes + n - 1) / n;
+  // the zone spans whole stripe rows, plus room for a chunk (<= 64 MiB)
+  // that starts before the end and runs past it: its tail pages map to
+  // member offsets past EOF, read as zeros like a file's tail
+  const uint64_t rows = (nstripes + n - 1) / n + ((64ull << 20) / ((uint64_t)unit * n)) + 1;
   g.zone_end[0] = rows * n * (uint64_t)(unit >> 9);
   g.zone_dev_start[0] = 0;
   g.zone_nb_dev[0] = n;

@@ -97,6 +97,25 @@ def test_stripe_stream_loader(strom, tmp_path):
         ld.close()
 
 
+def test_stripe_chunk_past_logical_end(strom, tmp_path):
+    """A chunk that starts before the logical end and runs past it (and
+    past the last stripe row) reads the tail as zeros, as for a file."""
+    unit = 256 << 10
+    data = np.random.default_rng(4).integers(0, 256, (6 << 20) + 12345, dtype=np.uint8)
+    paths, size = _members(tmp_path, 3, data, unit)
+    big = 1 << 20
+    nch = (size + big - 1) // big
+    keep = np.zeros(nch * big + 65536, dtype=np.uint8)
+    off = (-keep.ctypes.data) % 65536
+    hbm = keep[off:off + nch * big]
+    hbm[:] = 0xEE
+    with strom.StripeSet(paths, unit) as ss, strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+        r = strom.memcpy_ssd2gpu(m.handle, 0, ss.fd, np.arange(nch, dtype=np.uint32), big)
+        strom.memcpy_wait(r.dma_task_id)
+        assert np.array_equal(hbm[:size], data)
+        assert not hbm[size:].any()
+
+
 def test_stripe_validation(strom, tmp_path):
     unit = 16 << 10
     data = np.random.default_rng(0).integers(0, 256, 10 * unit, dtype=np.uint8)
