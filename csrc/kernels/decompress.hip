@@ -146,6 +146,17 @@ struct Stream {
   __device__ __forceinline__ uint32_t rd1(uint32_t p) { return rd4(p, nullptr) & 0xff; }
 
   __device__ __forceinline__ void put(uint32_t pos, uint8_t v) { ring[(pos + omis) & kMask] = v; }
+  // the first min(m, 4) bytes of v at pos..pos+3: one uniform test, then
+  // unguarded byte stores for a full 4-byte span (no per-byte branch)
+  __device__ __forceinline__ void put4(uint32_t pos, uint32_t v, uint32_t m) {
+    const uint32_t a = pos + omis;
+    if (m >= 4) {
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) ring[(a + j) & kMask] = (uint8_t)(v >> (8 * j));
+    } else {
+      for (uint32_t j = 0; j < m; ++j) ring[(a + j) & kMask] = (uint8_t)(v >> (8 * j));
+    }
+  }
 
   // Store ring bytes [flushed, upto) to HBM: whole 16-B chunks as one
   // dwordx4 store each (GL chunks per group instruction); partial chunks
@@ -192,10 +203,7 @@ struct Stream {
         const uint32_t o = p + done + k - win;
         const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
         const uint32_t v = __builtin_amdgcn_alignbyte(d[1], d[0], o & 3);
-        const uint32_t s = op + done + k;
-#pragma unroll
-        for (uint32_t j = 0; j < BPL; ++j)
-          if (k + j < n) put(s + j, (uint8_t)(v >> (8 * j)));
+        put4(op + done + k, v, n - k);
       }
       pace(op + done + n);
     }
@@ -224,9 +232,7 @@ struct Stream {
             const uint32_t d0 = *(const uint32_t *)(ring + a0);
             const uint32_t d1 = *(const uint32_t *)(ring + ((a0 + 4) & kMask));
             const uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, q & 3);
-#pragma unroll
-            for (uint32_t j = 0; j < BPL; ++j)
-              if (k + j < n) put(s + j, (uint8_t)(v >> (8 * j)));
+            put4(s, v, n - k);
           }
           pace(op + done + n);
         }
@@ -234,7 +240,16 @@ struct Stream {
       } else {
         // short period: byte k of a pass starting at s repeats s-off+(k mod off)
         uint32_t r[BPL];
-        r[0] = k % off;
+        // k % off for k < 256, off < W: one float reciprocal instead of the
+        // ~30-instruction integer remainder (exact: the quotient error of
+        // the rcp is far below 1/256, corrected by one compare)
+        {
+          uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)off));
+          uint32_t rem = k - q * off;
+          if ((int32_t)rem < 0) rem += off;
+          else if (rem >= off) rem -= off;
+          r[0] = rem;
+        }
 #pragma unroll
         for (uint32_t j = 1; j < BPL; ++j) {
           r[j] = r[j - 1] + 1;

@@ -101,13 +101,20 @@ def _up64(n: int) -> int:
 
 
 class ArrowScan:
+    # the decoder runs one stream per compressed buffer at a roughly fixed
+    # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
+    # to fill the GPU, so compressed groups grow to hold that many buffers
+    TARGET_STREAMS = 8192
+
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
-                 slot_bytes: int = 256 << 20, nslots: int = 3):
+                 slot_bytes: int = 256 << 20, nslots: int = 3,
+                 max_slot_bytes: int = 4 << 30):
         self.path = path
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.meta: ArrowFile = read_metadata(path)
         self.chunk_sz = chunk_sz
         self.slot_bytes = slot_bytes
+        self.max_slot_bytes = max(slot_bytes, max_slot_bytes)
         self.nslots = max(2, nslots)
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
@@ -147,7 +154,14 @@ class ArrowScan:
         groups: List[_Group] = []
         cur: List[_Batch] = []
         ids = np.zeros(0, dtype=np.int64)
-        limit = self.slot_bytes // self.chunk_sz
+        slot = self.slot_bytes
+        # really compressed buffers (a stored-raw one is as long as its data)
+        comp = [b for b in batches
+                if b.data.compressed and 0 < b.data.length < 0.9 * b.data.need]
+        if comp:
+            avg = sum(b.data.length + (b.valid.length if b.valid else 0) for b in comp) / len(comp)
+            slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
+        limit = max(1, slot // self.chunk_sz)
         for b in batches:
             mine = self._chunks(b)
             merged = np.union1d(ids, mine)
