@@ -5,8 +5,9 @@
 // irqsave spinlocks, RCU and refcounts (kmod/nvme_strom.c:648-731,
 // 1148-1187): many threads issuing SSD2RAM tasks and waiting on them,
 // injected device errors racing with completions, session close reclaiming
-// failed tasks, emulated-GPU SSD2GPU with the page-cache hybrid, and engine
-// teardown while idle.
+// failed tasks, emulated-GPU SSD2GPU with the page-cache hybrid, the fake
+// backend's out-of-order completions over a stripe set, and engine teardown
+// while idle.
 #include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
@@ -167,6 +168,63 @@ int main() {
     CHECK(bad == 0);
     strom_unmap_gpu_memory um{m.handle};
     CHECK(nvme_strom_ioctl(STROM_IOCTL__UNMAP_GPU_MEMORY, &um) == 0);
+  }
+
+  // 5. fake namespace backend (completions in a seeded random order) under
+  //    concurrency, reading a stripe set over two member files: chunk ids
+  //    reversed per thread, each thread its own session and buffer slice
+  {
+    char m0[] = "/tmp/strom_selftest_m0.XXXXXX", m1[] = "/tmp/strom_selftest_m1.XXXXXX";
+    int f0 = mkstemp(m0), f1 = mkstemp(m1);
+    CHECK(f0 >= 0 && f1 >= 0);
+    const uint32_t unit = 4 * CH;
+    for (size_t s0 = 0, k = 0; s0 < fsz; s0 += unit, ++k)
+      CHECK(write(k % 2 ? f1 : f0, data.data() + s0, unit) == (ssize_t)unit);
+    fsync(f0);
+    fsync(f1);
+    strom_config_set("backend", "fake");
+    strom_config_set("max_request", "8192");
+    strom_fake_backend(77, nullptr, nullptr);
+    strom_engine_reset();
+    int mfd[2] = {f0, f1};
+    const int sfd = strom_stripe_open(mfd, 2, unit, fsz);
+    CHECK(sfd >= 0);
+    memset(buf, 0, fsz);
+    std::vector<std::thread> g;
+    for (int t = 0; t < 4; ++t) {
+      g.emplace_back([&, t] {
+        int s = strom_open();
+        const size_t per = nch / 4;
+        std::vector<uint32_t> ids(per);
+        for (size_t i = 0; i < per; ++i) ids[i] = (uint32_t)(t * per + per - 1 - i);
+        strom_memcpy_ssd2ram a{};
+        a.dest_uaddr = buf + t * per * CH;
+        a.file_desc = sfd;
+        a.nr_chunks = (unsigned)per;
+        a.chunk_sz = CH;
+        a.chunk_ids = ids.data();
+        if (strom_ioctl(s, STROM_IOCTL__MEMCPY_SSD2RAM, &a) != 0) { bad++; return; }
+        strom_memcpy_wait w{};
+        w.dma_task_id = a.dma_task_id;
+        if (strom_ioctl(s, STROM_IOCTL__MEMCPY_WAIT, &w) != 0) bad++;
+        for (size_t i = 0; i < per; ++i)
+          if (memcmp(buf + (t * per + i) * CH, data.data() + (size_t)ids[i] * CH, CH)) bad++;
+        strom_close(s);
+      });
+    }
+    for (auto &x : g) x.join();
+    CHECK(bad == 0);
+    uint64_t comps = 0, reord = 0;
+    strom_fake_backend(0, &comps, &reord);
+    CHECK(comps >= nch && reord > 0);
+    CHECK(strom_stripe_close(sfd) == 0);
+    close(f0);
+    close(f1);
+    unlink(m0);
+    unlink(m1);
+    strom_config_set("backend", "uring");
+    strom_config_set("max_request", "1048576");
+    strom_engine_reset();
   }
 
   strom_stat_info si{};
