@@ -9,6 +9,7 @@
 #   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
 #   ktrace     rocprofv3 kernel trace + stats of a short kbench
 #   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
+#   btrace     rocprofv3 kernel + memory-copy trace of a short bench run
 #   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   decprof    decoder cycle profile per code path (libstrom_decprof.so)
@@ -41,6 +42,8 @@ for phase in "$@"; do
     kpmc) (cd /tmp && step kpmc 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
               SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc" -o pmc \
               -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only crc,heap,lz4) ;;
+    btrace) (cd /tmp && step btrace 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/btrace" -o btrace \
+              -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --lat-samples 300) ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
     ram) step ram 400 python -u -m nvme_strom_amd.tools.ram_bench --out "$OUT/ram.json" ;;
     decprof) step decprof 300 python -u -m nvme_strom_amd.tools.decomp_prof --out "$OUT/decprof.json" ;;
