@@ -181,7 +181,8 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
   // wave wid owns pages [base + wid*ppw, +ppw) of each group
   uint32_t first = blockIdx.x * kPerWg + wid * ppw;
   if (first < a.npages) STROM_HS_ISSUE(first);
-  // every wave of a workgroup runs the same trip counts (barriers inside)
+  // every wave of a workgroup runs the same trip counts (the output
+  // reservation below has workgroup barriers)
   for (uint32_t base = blockIdx.x * kPerWg; base < a.npages; base += stride, first += stride) {
     uint32_t count = 0;
     for (uint32_t j = 0; j < ppw; ++j) {
@@ -192,7 +193,11 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
         for (int k = 0; k < NV; ++k)
           if (PAGE || (uint32_t)k < nv) ((v4u *)mypage)[k * 64 + lane] = buf[k];
       }
-      __syncthreads();
+      // the page image is this wave's alone: a wavefront-scope fence orders
+      // its LDS stores before the reads below (a workgroup barrier here
+      // held all four waves to the slowest page, twice per page)
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       // the next page's loads are in flight while this one is parsed
       const uint32_t nxt = j + 1 < ppw ? pg + 1 : first + stride;
       if (nxt < a.npages && (j + 1 < ppw ? have : true)) STROM_HS_ISSUE(nxt);
@@ -217,7 +222,9 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
         }
       }
       if (lane == 0) nch[j] = nchunks;
-      __syncthreads();   // the page image is overwritten next
+      // the wave's own page image is overwritten next
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
     }
     if (lane == 0) wcount[wid] = count;
     __syncthreads();
