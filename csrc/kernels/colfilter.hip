@@ -23,6 +23,11 @@
 
 namespace {
 
+// Each wave takes U consecutive 64-row words per trip and issues all their
+// loads before the first compare: U rows per lane in flight instead of one
+// (round 2 trace: 3.75 TB/s with one load in flight per wave).
+constexpr uint32_t kU = 4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void filter_kernel(const T *__restrict__ v,
                                                      const uint64_t *__restrict__ valid,
@@ -33,17 +38,24 @@ __global__ __launch_bounds__(256) void filter_kernel(const T *__restrict__ v,
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t nwords = (n + 63) / 64;
   uint32_t local = 0;
-  for (uint64_t w = (uint64_t)blockIdx.x * 4 + wid; w < nwords; w += (uint64_t)gridDim.x * 4) {
-    uint64_t i = w * 64 + lane;
-    bool ok = false;
-    if (i < n) {
-      T x = v[i];
-      ok = x >= lo && x <= hi;
+  const uint64_t step = (uint64_t)gridDim.x * 4 * kU;
+  for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wid) * kU; w0 < nwords; w0 += step) {
+    T x[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t i = (w0 + u) * 64 + lane;
+      x[u] = i < n ? __builtin_nontemporal_load(v + i) : (T)0;
     }
-    uint64_t word = __ballot(ok);
-    if (valid) word &= valid[w];
-    if (lane == 0) bitmap[w] = word;
-    local += __popcll(word);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t w = w0 + u;
+      if (w >= nwords) break;
+      const uint64_t i = w * 64 + lane;
+      uint64_t word = __ballot(i < n && x[u] >= lo && x[u] <= hi);
+      if (valid) word &= valid[w];
+      if (lane == 0) bitmap[w] = word;
+      local += __popcll(word);
+    }
   }
   if (lane == 0) wave_cnt[wid] = local;
   __syncthreads();
@@ -136,19 +148,35 @@ __global__ __launch_bounds__(256) void filter_batched_kernel(const strom_filter_
   __shared__ uint32_t wave_cnt[4];
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t local = 0;
-  for (uint64_t w = (uint64_t)blockIdx.x * 4 + wid; w < nwords; w += (uint64_t)gridDim.x * 4) {
-    const strom_filter_batch b = bt[batch_of(bt, nb, w)];
-    const uint64_t k = w - b.word_base;           // word within the batch
-    const uint64_t i = k * 64 + lane;
-    bool ok = false;
-    if (i < b.nrows) {
-      const T x = ((const T *)b.values)[i];
-      ok = x >= lo && x <= hi;
+  const uint64_t step = (uint64_t)gridDim.x * 4 * kU;
+  for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wid) * kU; w0 < nwords; w0 += step) {
+    // U words per trip, all loads issued first (as filter_kernel)
+    T x[kU];
+    uint32_t bi[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t w = w0 + u;
+      x[u] = (T)0;
+      bi[u] = 0;
+      if (w < nwords) {
+        bi[u] = batch_of(bt, nb, w);
+        const strom_filter_batch &b = bt[bi[u]];
+        const uint64_t i = (w - b.word_base) * 64 + lane;
+        if (i < b.nrows) x[u] = ((const T *)b.values)[i];
+      }
     }
-    uint64_t word = __ballot(ok);
-    if (b.valid && k * 64 < b.nrows) word &= ((const uint64_t *)b.valid)[k];
-    if (lane == 0) bitmap[w] = word;
-    local += __popcll(word);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint64_t w = w0 + u;
+      if (w >= nwords) break;
+      const strom_filter_batch b = bt[bi[u]];
+      const uint64_t k = w - b.word_base;           // word within the batch
+      const uint64_t i = k * 64 + lane;
+      uint64_t word = __ballot(i < b.nrows && x[u] >= lo && x[u] <= hi);
+      if (b.valid && k * 64 < b.nrows) word &= ((const uint64_t *)b.valid)[k];
+      if (lane == 0) bitmap[w] = word;
+      local += __popcll(word);
+    }
   }
   if (lane == 0) wave_cnt[wid] = local;
   __syncthreads();
@@ -230,7 +258,7 @@ __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restri
 template <typename T>
 int launch_filter_batched(const strom_filter_batch *bt, uint32_t nb, uint64_t nwords, double lo,
                           double hi, uint64_t *bm, uint64_t *cnt, hipStream_t st) {
-  uint64_t g = (nwords + 3) / 4;
+  uint64_t g = (nwords + 4 * kU - 1) / (4 * kU);
   uint32_t grid = (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
   hipLaunchKernelGGL(filter_batched_kernel<T>, dim3(grid), dim3(256), 0, st, bt, nb, nwords, (T)lo,
                      (T)hi, bm, (unsigned long long *)cnt);
@@ -241,7 +269,7 @@ template <typename T>
 int launch_filter(const void *v, const uint8_t *valid, uint64_t n, double lo, double hi,
                   uint64_t *bm, uint64_t *cnt, hipStream_t st) {
   uint64_t words = (n + 63) / 64;
-  uint64_t g = (words + 3) / 4;
+  uint64_t g = (words + 4 * kU - 1) / (4 * kU);
   uint32_t grid = (uint32_t)(g > 4096 ? 4096 : (g ? g : 1));
   (void)hipMemsetAsync(cnt, 0, sizeof(uint64_t), st);
   hipLaunchKernelGGL(filter_kernel<T>, dim3(grid), dim3(256), 0, st, (const T *)v,

@@ -170,9 +170,9 @@ def test_malformed_streams_report_errors(dev):
 
 # -------------------------------------------------------------- column filter
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64, torch.float32, torch.float64])
-def test_column_filter(dev, dtype):
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255 * 64 + 7, 1_000_003])
+def test_column_filter(dev, dtype, n):
     from nvme_strom_amd.ops.colfilter import bitmap_to_indices, column_filter
-    n = 1_000_003
     rng = np.random.default_rng(2)
     v = rng.integers(-1000, 1000, n)
     vt = torch.from_numpy(v).to(dtype).to(dev)
