@@ -77,7 +77,8 @@ struct Stream {
   static constexpr uint32_t kRing = RING_;
   static constexpr uint32_t kMask = kRing - 1;
   static constexpr uint32_t kInW = INW_;
-  static constexpr uint32_t kSlot = kRing + kInW;   // LDS bytes per stream
+  static constexpr uint32_t kDummy = 16;     // sink for masked-off fast-path stores
+  static constexpr uint32_t kSlot = kRing + kInW + kDummy;   // LDS bytes per stream
   // waves per SIMD the LDS footprint allows (160 KiB per CU, 4 SIMDs)
   static constexpr uint32_t kMinWaves = (160u * 1024 / (G * kSlot)) / 4 >= 4 ? 4 : 1;
   static_assert(64 % GL == 0 && (kRing & kMask) == 0, "geometry");
@@ -300,6 +301,66 @@ struct Stream {
       PROF_ADD(kPFar);
     }
     op += len;
+  }
+
+  // window bytes p..p+3 without the window check (caller guarantees it)
+  __device__ __forceinline__ uint32_t rd4u(uint32_t p) const {
+    const uint32_t o = p - win;
+    const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+    return __builtin_amdgcn_alignbyte(d[1], d[0], o & 3);
+  }
+
+  // ---- the common LZ4 sequence in one straight-line pass: short literal
+  // run and short near match (lit < 15, match < 19 without a length
+  // extension and <= W bytes, 1 <= off <=
+  // kRing - W), input window and output ring already in place.  Every lane
+  // stores its 4 literal and 4 match bytes unconditionally — bytes past the
+  // run go to a per-stream sink — so the step has no per-byte branches and
+  // no loops; the round 2 cycle profile put ~2k cycles per sequence in the
+  // general path, most of it control flow.  false: take the general path
+  // (nothing was changed).
+  __device__ __forceinline__ bool lz4_fast() {
+    if (win == 0xffffffffu || ip < win || ip + 24 > win + kInW || ip + 24 > bend) return false;
+    const uint32_t w = rd4u(ip);
+    const uint32_t lit = (w >> 4) & 15, mlen = (w & 15) + 4;
+    const uint32_t po = ip + 1 + lit;
+    const uint32_t off = rd4u(po) & 0xffff;
+    if (lit == 15 || (w & 15) == 15 || mlen > W || off == 0 || off > op + lit || off > kRing - W ||
+        lit + mlen > ocap - op)
+      return false;
+    uint8_t *sink = inw + kInW;
+    const uint32_t k = t * BPL;
+    {  // literal bytes [ip + 1, ip + 1 + lit): lane t moves bytes k..k+3
+      const uint32_t v = rd4u(ip + 1 + k);
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        uint8_t *d = k + j < lit ? ring + ((op + k + j + omis) & kMask) : sink + j;
+        *d = (uint8_t)(v >> (8 * j));
+      }
+    }
+    {  // match: byte i of the copy at s is out[s - off + (i mod off)]
+      const uint32_t s = op + lit;
+      const uint32_t base = s - off + omis;
+      uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)off));
+      uint32_t r = k - q * off;
+      if ((int32_t)r < 0) r += off;
+      else if (r >= off) r -= off;
+      uint8_t v[BPL];
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        v[j] = ring[(base + r) & kMask];
+        r = r + 1 == off ? 0 : r + 1;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        uint8_t *d = k + j < mlen ? ring + ((s + k + j + omis) & kMask) : sink + 4 + j;
+        *d = v[j];
+      }
+    }
+    ip = po + 2;
+    op += lit + mlen;
+    pace(op);
+    return true;
   }
 
   // ---- one LZ4 sequence of the block ending at bend
@@ -525,7 +586,10 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
 #ifdef STROM_DECOMP_PROF
     if (live) st.prof[kPSteps] += 1;
 #endif
-    if (live && !st.step(codec)) {
+    // the common short sequence goes through the straight-line step; the
+    // rest (long runs, far matches, block/frame edges, errors) through step()
+    const bool fast = live && st.mode == kLz4 && st.lz4_fast();
+    if (live && !fast && !st.step(codec)) {
       if (!st.err) st.flush(st.op, true);
       if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
       live = false;
@@ -543,6 +607,7 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
 using S16 = Stream<4, 2048, 448>;     // 16 streams per wave
 // A/B variant: half the LDS (2 waves per SIMD), a 1 KiB history ring
 using S16s = Stream<4, 1024, 224>;    // 16 streams per wave, 19.5 KiB
+using S8 = Stream<8, 2048, 448>;      // 8 streams per wave, 19.5 KiB (2 waves per SIMD)
 using S4 = Stream<16, 2048, 512>;     // 4 streams per wave, 10 KiB
 using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
 
@@ -560,7 +625,7 @@ int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d
 
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
-// STROM_DECOMP_G (1, 4, 16; 32 = 16 with the small ring) forces a
+// STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring) forces a
 // geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
@@ -574,10 +639,11 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // wave, 1k streams 5.3 / 2.7 / 2.9): wide groups pay more per sequence
   // (the short-period path covers every offset below the pass width) than
   // they gain from more resident waves
-  if (g != 1 && g != 4 && g != 16 && g != 32) g = 16;
+  if (g != 1 && g != 4 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 32) return launch<S16s>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  if (g == 8) return launch<S8>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 4) return launch<S4>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   return launch<S1>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
 }

@@ -53,7 +53,7 @@ def main(argv=None) -> int:
                                   for i in range(nblk)])
             d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
             status = torch.empty(nblk, dtype=torch.int32, device=dev)
-            for g in ((16, 32, 4, 1) if nblk <= 1024 else (16, 32)):
+            for g in ((16, 8, 4, 1) if nblk <= 1024 else (16, 8, 32)):
                 os.environ["STROM_DECOMP_G"] = str(g)
                 out = np.zeros(len(NAMES), dtype=np.uint64)
                 lib.strom_decompress(D.LZ4, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),

@@ -105,7 +105,7 @@ def main(argv=None):
             if codec == "lz4" and dname == "words":
                 # the same streams under each geometry (streams per wave), and
                 # a few-streams launch (an Arrow scan group: ~1k buffers)
-                for g in (16, 4, 1):
+                for g in (16, 8, 4, 1):
                     os.environ["STROM_DECOMP_G"] = str(g)
                     log(f"decompress_lz4_64k_g{g}",
                         timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))

@@ -127,6 +127,24 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
+@pytest.mark.parametrize("g", [1, 4, 8, 16, 32])
+@pytest.mark.parametrize("codec", ["lz4", "snappy"])
+def test_decoder_geometries(dev, monkeypatch, g, codec):
+    """Every streams-per-wave variant (STROM_DECOMP_G) decodes the same
+    payloads: the fast LZ4 step's pass width differs per geometry (a
+    length-15 match nibble must still take the extended-length path)."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd.ops import decompress as D
+    monkeypatch.setenv("STROM_DECOMP_G", str(g))
+    pays = _payloads()
+    name, cid = ("lz4_raw", D.LZ4) if codec == "lz4" else ("snappy", D.SNAPPY)
+    comp = [pa.compress(p, codec=name, asbytes=True) if p else
+            (D.lz4_compress(p) if codec == "lz4" else D.snappy_compress(p)) for p in pays]
+    st, outs = _run(cid, comp, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
 @pytest.mark.parametrize("which", ["ours", "pyarrow"])
 def test_snappy(dev, which):
     from nvme_strom_amd.ops import decompress as D
