@@ -319,8 +319,47 @@ struct Stream {
   // no loops; the round 2 cycle profile put ~2k cycles per sequence in the
   // general path, most of it control flow.  false: take the general path
   // (nothing was changed).
+  // lane t stores literal bytes k..k+3 of [src, src + lit) at op (bytes
+  // past the run go to the sink)
+  __device__ __forceinline__ void fast_lit(uint32_t src, uint32_t lit) {
+    uint8_t *sink = inw + kInW;
+    const uint32_t k = t * BPL;
+    const uint32_t v = rd4u(src + k);
+#pragma unroll
+    for (uint32_t j = 0; j < BPL; ++j) {
+      uint8_t *d = k + j < lit ? ring + ((op + k + j + omis) & kMask) : sink + j;
+      *d = (uint8_t)(v >> (8 * j));
+    }
+  }
+
+  // match at s: byte i of the copy is out[s - off + (i mod off)]
+  __device__ __forceinline__ void fast_copy(uint32_t s, uint32_t off, uint32_t mlen) {
+    uint8_t *sink = inw + kInW;
+    const uint32_t k = t * BPL;
+    const uint32_t base = s - off + omis;
+    uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)off));
+    uint32_t r = k - q * off;
+    if ((int32_t)r < 0) r += off;
+    else if (r >= off) r -= off;
+    uint8_t v[BPL];
+#pragma unroll
+    for (uint32_t j = 0; j < BPL; ++j) {
+      v[j] = ring[(base + r) & kMask];
+      r = r + 1 == off ? 0 : r + 1;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < BPL; ++j) {
+      uint8_t *d = k + j < mlen ? ring + ((s + k + j + omis) & kMask) : sink + 4 + j;
+      *d = v[j];
+    }
+  }
+
+  __device__ __forceinline__ bool fast_window(uint32_t end) const {
+    return win != 0xffffffffu && ip >= win && ip + 24 <= win + kInW && ip + 24 <= end;
+  }
+
   __device__ __forceinline__ bool lz4_fast() {
-    if (win == 0xffffffffu || ip < win || ip + 24 > win + kInW || ip + 24 > bend) return false;
+    if (!fast_window(bend)) return false;
     const uint32_t w = rd4u(ip);
     const uint32_t lit = (w >> 4) & 15, mlen = (w & 15) + 4;
     const uint32_t po = ip + 1 + lit;
@@ -328,37 +367,41 @@ struct Stream {
     if (lit == 15 || (w & 15) == 15 || mlen > W || off == 0 || off > op + lit || off > kRing - W ||
         lit + mlen > ocap - op)
       return false;
-    uint8_t *sink = inw + kInW;
-    const uint32_t k = t * BPL;
-    {  // literal bytes [ip + 1, ip + 1 + lit): lane t moves bytes k..k+3
-      const uint32_t v = rd4u(ip + 1 + k);
-#pragma unroll
-      for (uint32_t j = 0; j < BPL; ++j) {
-        uint8_t *d = k + j < lit ? ring + ((op + k + j + omis) & kMask) : sink + j;
-        *d = (uint8_t)(v >> (8 * j));
-      }
-    }
-    {  // match: byte i of the copy at s is out[s - off + (i mod off)]
-      const uint32_t s = op + lit;
-      const uint32_t base = s - off + omis;
-      uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)off));
-      uint32_t r = k - q * off;
-      if ((int32_t)r < 0) r += off;
-      else if (r >= off) r -= off;
-      uint8_t v[BPL];
-#pragma unroll
-      for (uint32_t j = 0; j < BPL; ++j) {
-        v[j] = ring[(base + r) & kMask];
-        r = r + 1 == off ? 0 : r + 1;
-      }
-#pragma unroll
-      for (uint32_t j = 0; j < BPL; ++j) {
-        uint8_t *d = k + j < mlen ? ring + ((s + k + j + omis) & kMask) : sink + 4 + j;
-        *d = v[j];
-      }
-    }
+    fast_lit(ip + 1, lit);
+    fast_copy(op + lit, off, mlen);
     ip = po + 2;
     op += lit + mlen;
+    pace(op);
+    return true;
+  }
+
+  // the same for one snappy element: a literal of <= W bytes (tag-encoded
+  // length) or a 1-/2-byte-offset copy of <= W bytes
+  __device__ __forceinline__ bool snappy_fast() {
+    if (!fast_window(iend)) return false;
+    const uint32_t w = rd4u(ip);
+    const uint32_t tag = w & 0xff, kind = tag & 3;
+    if (kind == 0) {
+      // tag lengths 61..64 announce 1..4 length bytes; the run must lie in
+      // the loaded window (24 bytes past ip are guaranteed, wide groups
+      // take longer runs)
+      const uint32_t len = (tag >> 2) + 1;
+      if (len > 60 || len > W || len > olen - op || ip + 1 + len > win + kInW ||
+          ip + 1 + len > iend)
+        return false;
+      fast_lit(ip + 1, len);
+      ip += 1 + len;
+      op += len;
+      pace(op);
+      return true;
+    }
+    if (kind == 3) return false;
+    const uint32_t len = kind == 1 ? 4 + ((tag >> 2) & 7) : (tag >> 2) + 1;
+    const uint32_t off = kind == 1 ? ((tag >> 5) << 8) | ((w >> 8) & 0xff) : (w >> 8) & 0xffff;
+    if (len > W || off == 0 || off > op || off > kRing - W || len > olen - op) return false;
+    fast_copy(op, off, len);
+    ip += 1 + kind;
+    op += len;
     pace(op);
     return true;
   }
@@ -445,7 +488,9 @@ struct Stream {
   }
 
   // ---- stream-level headers: frame block header, snappy preamble, copy
+  template <bool kSnap>
   __device__ void header(int codec) {
+    if (kSnap) codec = STROM_CODEC_SNAPPY;
     if (codec == STROM_CODEC_LZ4) {
       bend = iend;
       mode = kLz4;
@@ -513,10 +558,11 @@ struct Stream {
   }
 
   // one unit of work; false once the stream is finished (or failed)
+  template <bool kSnap>
   __device__ bool step(int codec) {
     if (mode == kHdr) {
-      header(codec);
-    } else if (mode == kLz4) {
+      header<kSnap>(codec);
+    } else if (!kSnap && mode == kLz4) {
       if (ip >= bend) {
         if (codec == STROM_CODEC_LZ4) {
           mode = kDone;
@@ -527,7 +573,7 @@ struct Stream {
       } else {
         lz4_seq();
       }
-    } else if (mode == kSnappy) {
+    } else if (kSnap && mode == kSnappy) {
       if (ip >= iend) {
         if (op != olen) err = kErrFormat;
         mode = kDone;
@@ -542,7 +588,9 @@ struct Stream {
 // 64 threads, >= 4 waves per SIMD (<= 128 VGPRs): the decoder is latency
 // bound per wave (round 2 trace: 256 or 1024 waves took the same ~9 ms),
 // so throughput comes from waves resident per CU
-template <class S>
+// kSnap: the snappy kernel, else the LZ4 family (raw, frame, Arrow) — one
+// fast step per kernel keeps the register budget of the 4-wave launch bound
+template <class S, bool kSnap>
 __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec, const uint8_t *__restrict__ src,
                                                         uint8_t *__restrict__ dst,
                                                         const strom_decomp_desc *__restrict__ desc,
@@ -588,8 +636,10 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
 #endif
     // the common short sequence goes through the straight-line step; the
     // rest (long runs, far matches, block/frame edges, errors) through step()
-    const bool fast = live && st.mode == kLz4 && st.lz4_fast();
-    if (live && !fast && !st.step(codec)) {
+    bool fast;
+    if constexpr (kSnap) fast = live && st.mode == kSnappy && st.snappy_fast();
+    else fast = live && st.mode == kLz4 && st.lz4_fast();
+    if (live && !fast && !st.template step<kSnap>(codec)) {
       if (!st.err) st.flush(st.op, true);
       if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
       live = false;
@@ -616,8 +666,12 @@ int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d
            uint32_t nblocks, int32_t *d_status, hipStream_t st) {
   const uint32_t waves = (nblocks + S::G - 1) / S::G;
   const uint32_t grid = waves < 16384 ? waves : 16384;
-  hipLaunchKernelGGL(decompress_kernel<S>, dim3(grid), dim3(64), 0, st, codec,
-                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
+  if (codec == STROM_CODEC_SNAPPY)
+    hipLaunchKernelGGL((decompress_kernel<S, true>), dim3(grid), dim3(64), 0, st, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
+  else
+    hipLaunchKernelGGL((decompress_kernel<S, false>), dim3(grid), dim3(64), 0, st, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
