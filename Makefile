@@ -44,13 +44,21 @@ $(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/include/strom/strom
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ $<
 
+# a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
+# make ab AB=name [SRC=path/to/decompress.hip]
+SRC ?= csrc/kernels/decompress.hip
+ab:
+	@mkdir -p $(OUT)/ab
+	$(HIPCC) $(HIPFLAGS) -Icsrc/include -shared -o $(OUT)/ab/$(AB).so $(SRC)
+	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DSTROM_DECOMP_PROF -shared -o $(OUT)/ab/$(AB)_prof.so $(SRC)
+
 $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
 	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(TOOLS)
 
-.PHONY: all tools clean
+.PHONY: all tools clean ab
 
 # ---- host-only engine self-test, plain and under sanitizers ---------------
 # The engine's host code builds with g++ (HIP host API only); device kernels

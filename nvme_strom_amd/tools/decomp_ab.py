@@ -1,0 +1,103 @@
+"""Same-box A/B of LZ4/snappy decoder builds.
+
+Kernel timings move by 10-20% between pool boxes, more than most decoder
+changes are worth, so variants are compared inside one process: each
+shared library passed on the command line is a standalone build of
+csrc/kernels/decompress.hip (``make ab AB=name`` builds the working tree
+into lib/ab/name.so); the corpora of kbench run through every library in
+alternating order, several rounds, and the median is reported.
+
+``python -m nvme_strom_amd.tools.decomp_ab lib/ab/base.so lib/ab/new.so``
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+
+def corpora():
+    rng = np.random.default_rng(1)
+    words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+    return {
+        "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
+        "ints": np.cumsum(rng.integers(0, 5, 8192)).astype(np.int64).tobytes(),
+    }
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--streams", type=int, default=16384)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--cases", default="", help="e.g. lz4_words,snappy_ints (default: all)")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    cases = set(a.cases.split(",")) if a.cases else None
+    from nvme_strom_amd.ops import decompress as D
+    libs = {}
+    for p in a.libs:
+        lib = C.CDLL(os.path.abspath(p))
+        lib.strom_decompress.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]
+        libs[os.path.basename(p).rsplit(".", 1)[0]] = lib
+    dev = torch.device("cuda")
+    res = {}
+    for codec in ("lz4", "snappy"):
+        cid = D.LZ4 if codec == "lz4" else D.SNAPPY
+        for dname, blk in corpora().items():
+            if cases is not None and f"{codec}_{dname}" not in cases:
+                continue
+            comp = D.lz4_compress(blk) if codec == "lz4" else D.snappy_compress(blk)
+            n = a.streams
+            src = torch.from_numpy(np.frombuffer(comp * n, dtype=np.uint8).copy()).to(dev)
+            dst = torch.empty(n * len(blk), dtype=torch.uint8, device=dev)
+            descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk))
+                                  for i in range(n)])
+            d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+            status = torch.empty(n, dtype=torch.int32, device=dev)
+            times = {k: [] for k in libs}
+
+            def run(lib):
+                rc = lib.strom_decompress(cid, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),
+                                          n, status.data_ptr(), None)
+                assert rc == 0, rc
+
+            for name, lib in libs.items():           # warm-up + correctness per build
+                dst.zero_()
+                run(lib)
+                torch.cuda.synchronize()
+                ok = bool((status == len(blk)).all().item()) and \
+                    bytes(dst[-len(blk):].cpu().numpy()) == blk
+                if not ok:
+                    raise SystemExit(f"{name}: wrong output on {codec}/{dname}")
+            for r in range(a.rounds):
+                order = list(libs.items())
+                if r % 2:
+                    order.reverse()
+                for name, lib in order:
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    run(lib)
+                    e.record()
+                    torch.cuda.synchronize()
+                    times[name].append(s.elapsed_time(e))
+            row = {k: round(n * len(blk) / float(np.median(v)) / 1e6, 1) for k, v in times.items()}
+            res[f"{codec}_{dname}"] = row
+            print(f"{codec}_{dname}", json.dumps(row), file=sys.stderr, flush=True)
+            del src, dst
+    js = json.dumps({"GBps": res, "streams": a.streams, "rounds": a.rounds})
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(js)
+    print(js)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

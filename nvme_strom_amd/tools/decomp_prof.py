@@ -28,9 +28,12 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=16384)
     ap.add_argument("--out", default="")
+    ap.add_argument("--lib", default="", help="a profiling build other than lib/libstrom_decprof.so")
+    ap.add_argument("--g", default="", help="comma-separated geometries (default: all)")
     a = ap.parse_args(argv)
     from nvme_strom_amd.ops import decompress as D
-    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
+    lib = C.CDLL(os.path.abspath(a.lib) if a.lib else
+                 os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib",
                               "libstrom_decprof.so"))
     lib.strom_decompress.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p, C.c_void_p]
@@ -53,7 +56,10 @@ def main(argv=None) -> int:
                                   for i in range(nblk)])
             d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
             status = torch.empty(nblk, dtype=torch.int32, device=dev)
-            for g in ((16, 8, 4, 1) if nblk <= 1024 else (16, 8, 32)):
+            gs = (16, 8, 4, 1) if nblk <= 1024 else (16, 8, 32)
+            if a.g:
+                gs = tuple(int(x) for x in a.g.split(","))
+            for g in gs:
                 os.environ["STROM_DECOMP_G"] = str(g)
                 out = np.zeros(len(NAMES), dtype=np.uint64)
                 lib.strom_decompress(D.LZ4, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),

@@ -13,6 +13,8 @@
 #   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   decprof    decoder cycle profile per code path (libstrom_decprof.so)
+#   decpmc     two PMC passes (issue / wait / LDS / memory instruction mix)
+#              over the LZ4 decoder build DECLIB (default lib/ab/base.so)
 #   arrow      config-5 Arrow scan bench (tools.arrow_bench)
 # Output lands in gpurun_out/TAG/.
 set -o pipefail
@@ -47,6 +49,13 @@ for phase in "$@"; do
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
     ram) step ram 400 python -u -m nvme_strom_amd.tools.ram_bench --out "$OUT/ram.json" ;;
     decprof) step decprof 300 python -u -m nvme_strom_amd.tools.decomp_prof --out "$OUT/decprof.json" ;;
+    decpmc) for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                        "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+              n=$((n + 1))
+              (cd /tmp && step decpmc$n 90 rocprofv3 --pmc $pass --output-format csv -d "$OUT/decpmc$n" -o pmc \
+                -- python3 -m nvme_strom_amd.tools.decomp_ab "$ROOT/${DECLIB:-nvme_strom_amd/lib/ab/base.so}" \
+                   --rounds 1 --cases "${DECCASES:-lz4_words,lz4_ints}") || exit 1
+            done ;;
     arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
