@@ -52,7 +52,11 @@ constexpr uint32_t BPL = 4;                  // bytes per lane per pass
 // build used by tools/decomp_prof.py): s_memtime spans per code path,
 // summed by lane 0 of each group, plus event counts.
 enum : int { kPSeq, kPLit, kPNear, kPShort, kPFar, kPRefill, kPFlush, kPHdr, kPFarFence,
-             kPNSeq, kPNFar, kPNRefill, kPNFlush, kPNLitPass, kPNMatchPass, kPSteps, kPN };
+             kPNSeq, kPNFar, kPNRefill, kPNFlush, kPNLitPass, kPNMatchPass, kPSteps,
+             // wave-level (lane 0 only): loop iterations, cycles in the fast
+             // step, cycles in the general step, cycles of whole iterations,
+             // iterations in which some group took the general step
+             kPWIter, kPWFast, kPWSlow, kPWLoop, kPWSlowIter, kPN };
 #ifdef STROM_DECOMP_PROF
 __device__ unsigned long long g_prof[kPN];
 #define PROF_T0() const uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -633,18 +637,33 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
     if (!__any(live)) break;
 #ifdef STROM_DECOMP_PROF
     if (live) st.prof[kPSteps] += 1;
+    const uint64_t _w0 = __builtin_amdgcn_s_memtime();
 #endif
     // the common short sequence goes through the straight-line step; the
     // rest (long runs, far matches, block/frame edges, errors) through step()
     bool fast;
     if constexpr (kSnap) fast = live && st.mode == kSnappy && st.snappy_fast();
     else fast = live && st.mode == kLz4 && st.lz4_fast();
+#ifdef STROM_DECOMP_PROF
+    const uint64_t _w1 = __builtin_amdgcn_s_memtime();
+    const bool _slow = __any(live && !fast);
+#endif
     if (live && !fast && !st.template step<kSnap>(codec)) {
       if (!st.err) st.flush(st.op, true);
       if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
       live = false;
       b += stride;
     }
+#ifdef STROM_DECOMP_PROF
+    const uint64_t _w2 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      st.prof[kPWIter] += 1;
+      st.prof[kPWFast] += _w1 - _w0;
+      st.prof[kPWSlow] += _w2 - _w1;
+      st.prof[kPWLoop] += _w2 - _w0;
+      st.prof[kPWSlowIter] += _slow ? 1 : 0;
+    }
+#endif
   }
 #ifdef STROM_DECOMP_PROF
   if (st.t == 0)

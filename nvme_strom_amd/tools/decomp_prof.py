@@ -21,7 +21,7 @@ import torch
 
 NAMES = ["seq", "literal", "match_near", "match_short", "match_far", "refill", "flush", "header",
          "far_fence", "n_seq", "n_far", "n_refill", "n_flush", "n_lit_pass", "n_match_pass",
-         "steps"]
+         "steps", "w_iter", "w_fast", "w_slow", "w_loop", "w_slow_iter"]
 
 
 def main(argv=None) -> int:
@@ -83,6 +83,12 @@ def main(argv=None) -> int:
                            cycles_per_seq={NAMES[i]: round(int(out[i]) / nseq, 1) for i in range(9)},
                            events_per_seq={NAMES[i]: round(int(out[i]) / nseq, 3)
                                            for i in range(10, 16)})
+                it = max(int(out[16]), 1)
+                row["wave"] = dict(iters=int(out[16]),
+                                   fast_cyc_per_iter=round(int(out[17]) / it, 1),
+                                   slow_cyc_per_iter=round(int(out[18]) / it, 1),
+                                   loop_cyc_per_iter=round(int(out[19]) / it, 1),
+                                   slow_iter_frac=round(int(out[20]) / it, 3))
                 key = f"{cname}_{nblk}_g{g}"
                 res[key] = row
                 print(key, json.dumps(row), file=sys.stderr, flush=True)
