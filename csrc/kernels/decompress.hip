@@ -336,7 +336,10 @@ struct Stream {
     }
   }
 
-  // match at s: byte i of the copy is out[s - off + (i mod off)]
+  // match at s, mlen <= 2W: byte i of the copy is out[s - off + (i mod off)].
+  // Relative to any pass start sp the same holds with sp for s (the output
+  // from s - off on is periodic), so both passes use the same residues;
+  // the second runs only for groups whose match needs it.
   __device__ __forceinline__ void fast_copy(uint32_t s, uint32_t off, uint32_t mlen) {
     uint8_t *sink = inw + kInW;
     const uint32_t k = t * BPL;
@@ -345,68 +348,112 @@ struct Stream {
     uint32_t r = k - q * off;
     if ((int32_t)r < 0) r += off;
     else if (r >= off) r -= off;
-    uint8_t v[BPL];
+    uint32_t rr[BPL];
 #pragma unroll
     for (uint32_t j = 0; j < BPL; ++j) {
-      v[j] = ring[(base + r) & kMask];
+      rr[j] = r;
       r = r + 1 == off ? 0 : r + 1;
     }
 #pragma unroll
-    for (uint32_t j = 0; j < BPL; ++j) {
-      uint8_t *d = k + j < mlen ? ring + ((s + k + j + omis) & kMask) : sink + 4 + j;
-      *d = v[j];
+    for (uint32_t c = 0; c < 2 * W; c += W) {
+      if (c && mlen <= W) break;
+      uint8_t v[BPL];
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) v[j] = ring[(base + c + rr[j]) & kMask];
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        uint8_t *d = c + k + j < mlen ? ring + ((s + c + k + j + omis) & kMask) : sink + 4 + j;
+        *d = v[j];
+      }
     }
+  }
+
+  // the fast step's only obstacle is the end of the loaded input window
+  __device__ __forceinline__ bool window_short(bool snap) const {
+    const uint32_t end = snap ? iend : bend;
+    return mode == (snap ? kSnappy : kLz4) && win != 0xffffffffu && ip >= win &&
+           ip + 24 > win + kInW && ip + 24 <= end;
   }
 
   __device__ __forceinline__ bool fast_window(uint32_t end) const {
     return win != 0xffffffffu && ip >= win && ip + 24 <= win + kInW && ip + 24 <= end;
   }
 
-  __device__ __forceinline__ bool lz4_fast() {
-    if (!fast_window(bend)) return false;
-    const uint32_t w = rd4u(ip);
-    const uint32_t lit = (w >> 4) & 15, mlen = (w & 15) + 4;
-    const uint32_t po = ip + 1 + lit;
-    const uint32_t off = rd4u(po) & 0xffff;
-    if (lit == 15 || (w & 15) == 15 || mlen > W || off == 0 || off > op + lit || off > kRing - W ||
-        lit + mlen > ocap - op)
-      return false;
-    fast_lit(ip + 1, lit);
+  // en: the group is live in LZ4 mode.  Every test is folded into one
+  // predicate (bitwise, no short circuit) behind one branch: each early
+  // return used to be a v_cmp -> s_and_saveexec -> s_cbranch chain waiting
+  // on the compare (round 2 stamps: ~1,150 cycles per step for ~150
+  // instructions).  Reads before the test use a clamped window offset, so
+  // they stay inside this stream's LDS slot whatever the state.
+  __device__ __forceinline__ bool lz4_fast(bool en) {
+    bool ok = en & (win != 0xffffffffu) & (ip >= win) & (ip + 24 <= win + kInW) & (ip + 24 <= bend);
+    const uint32_t o = ok ? ip - win : 0u;
+    const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+    const uint32_t w = __builtin_amdgcn_alignbyte(d[1], d[0], o & 3);
+    const uint32_t lit = (w >> 4) & 15, ml = w & 15;
+    const uint32_t oo = o + 1 + lit;
+    const uint32_t *e = (const uint32_t *)(inw + (oo & ~3u));
+    const uint32_t ox = __builtin_amdgcn_alignbyte(e[1], e[0], oo & 3);
+    const uint32_t off = ox & 0xffff, xb = (ox >> 16) & 0xff;   // xb: length extension byte
+    const uint32_t mlen = ml == 15 ? 19 + xb : ml + 4;
+    // this lane's 4 literal bytes, read with the offset (same round trip)
+    const uint32_t ol = o + 1 + t * BPL;
+    const uint32_t *f = (const uint32_t *)(inw + (ol & ~3u));
+    const uint32_t lv = __builtin_amdgcn_alignbyte(f[1], f[0], ol & 3);
+    ok = ok & (lit != 15) & ((ml != 15) | (xb != 255)) & (mlen <= 2 * W) & (off != 0) &
+         (off <= op + lit) & (off <= kRing - W) & (lit + mlen <= ocap - op);
+    if (!ok) return false;
+    {
+      uint8_t *sink = inw + kInW;
+      const uint32_t k = t * BPL;
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        uint8_t *dd = k + j < lit ? ring + ((op + k + j + omis) & kMask) : sink + j;
+        *dd = (uint8_t)(lv >> (8 * j));
+      }
+    }
     fast_copy(op + lit, off, mlen);
-    ip = po + 2;
+    ip += 3 + lit + (ml == 15);
     op += lit + mlen;
-    pace(op);
-    return true;
+    return true;                 // flush pacing: the kernel loop's exception test
   }
 
-  // the same for one snappy element: a literal of <= W bytes (tag-encoded
-  // length) or a 1-/2-byte-offset copy of <= W bytes
-  __device__ __forceinline__ bool snappy_fast() {
-    if (!fast_window(iend)) return false;
-    const uint32_t w = rd4u(ip);
+  // the same for one snappy element: a literal with its length in the tag
+  // or a copy with a 1- or 2-byte offset, <= W bytes either way.  Both
+  // halves always run (a literal is a copy of length 0 and a copy a
+  // literal of length 0, their stores going to the sink), so groups on
+  // different element kinds do not diverge.
+  __device__ __forceinline__ bool snappy_fast(bool en) {
+    bool ok = en & (win != 0xffffffffu) & (ip >= win) & (ip + 24 <= win + kInW) & (ip + 24 <= iend);
+    const uint32_t o = ok ? ip - win : 0u;
+    const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+    const uint32_t w = __builtin_amdgcn_alignbyte(d[1], d[0], o & 3);
+    const uint32_t ol = o + 1 + t * BPL;
+    const uint32_t *f = (const uint32_t *)(inw + (ol & ~3u));
+    const uint32_t lv = __builtin_amdgcn_alignbyte(f[1], f[0], ol & 3);
     const uint32_t tag = w & 0xff, kind = tag & 3;
-    if (kind == 0) {
-      // tag lengths 61..64 announce 1..4 length bytes; the run must lie in
-      // the loaded window (24 bytes past ip are guaranteed, wide groups
-      // take longer runs)
-      const uint32_t len = (tag >> 2) + 1;
-      if (len > 60 || len > W || len > olen - op || ip + 1 + len > win + kInW ||
-          ip + 1 + len > iend)
-        return false;
-      fast_lit(ip + 1, len);
-      ip += 1 + len;
-      op += len;
-      pace(op);
-      return true;
-    }
-    if (kind == 3) return false;
+    const bool islit = kind == 0;
     const uint32_t len = kind == 1 ? 4 + ((tag >> 2) & 7) : (tag >> 2) + 1;
-    const uint32_t off = kind == 1 ? ((tag >> 5) << 8) | ((w >> 8) & 0xff) : (w >> 8) & 0xffff;
-    if (len > W || off == 0 || off > op || off > kRing - W || len > olen - op) return false;
-    fast_copy(op, off, len);
-    ip += 1 + kind;
+    const uint32_t coff = kind == 1 ? ((tag >> 5) << 8) | ((w >> 8) & 0xff) : (w >> 8) & 0xffff;
+    const uint32_t lit = islit ? len : 0u, mlen = islit ? 0u : len, off = islit ? 1u : coff;
+    // literal tag lengths 61..64 announce length bytes; a literal longer
+    // than the 24 guaranteed bytes (wide groups) must lie in the window
+    ok = ok & (kind != 3) & (len <= W) & (len <= olen - op) &
+         (islit ? (len <= 60) & (ip + 1 + len <= win + kInW) & (ip + 1 + len <= iend)
+                : (off != 0) & (off <= op) & (off <= kRing - W));
+    if (!ok) return false;
+    {
+      uint8_t *sink = inw + kInW;
+      const uint32_t k = t * BPL;
+#pragma unroll
+      for (uint32_t j = 0; j < BPL; ++j) {
+        uint8_t *dd = k + j < lit ? ring + ((op + k + j + omis) & kMask) : sink + j;
+        *dd = (uint8_t)(lv >> (8 * j));
+      }
+    }
+    fast_copy(op, off, mlen);
+    ip += islit ? 1 + len : 1 + kind;
     op += len;
-    pace(op);
     return true;
   }
 
@@ -612,47 +659,59 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
   uint32_t b = blockIdx.x * S::G + g;
   bool live = false;
   for (;;) {
-    if (!live && b < nblocks) {
-      const strom_decomp_desc d = desc[b];
-      const uint8_t *in = src + d.src_off;
-      const uint32_t mis = (uint32_t)((uintptr_t)in & 3);
-      st.ina = in - mis;
-      st.out = dst + d.dst_off;
-      st.iend = d.src_len + mis;
-      st.ocap = d.dst_len;
-      st.ip = mis;
-      st.op = 0;
-      st.bend = 0;
-      st.win = 0xffffffffu;
-      st.vis = 0;
-      st.flushed = 0;
-      st.omis = (uint32_t)((uintptr_t)st.out & 15);
-      st.olen = 0;
-      st.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
-      st.fhdr = codec == STROM_CODEC_ARROW_LZ4;
-      st.mode = kHdr;
-      st.err = 0;
-      live = true;
-    }
-    if (!__any(live)) break;
 #ifdef STROM_DECOMP_PROF
     if (live) st.prof[kPSteps] += 1;
     const uint64_t _w0 = __builtin_amdgcn_s_memtime();
 #endif
-    // the common short sequence goes through the straight-line step; the
-    // rest (long runs, far matches, block/frame edges, errors) through step()
+    // The common short sequence goes through the straight-line step.  One
+    // rare, wave-uniform branch covers everything else: the general step
+    // (long runs, far matches, block/frame edges, errors), flush pacing,
+    // finishing a stream and taking the next one — every extra branch in
+    // the common path cost a compare-to-branch round trip per step.
     bool fast;
-    if constexpr (kSnap) fast = live && st.mode == kSnappy && st.snappy_fast();
-    else fast = live && st.mode == kLz4 && st.lz4_fast();
+    if constexpr (kSnap) fast = st.snappy_fast(live & (st.mode == kSnappy));
+    else fast = st.lz4_fast(live & (st.mode == kLz4));
+    const bool exc = !fast | (st.op - st.flushed >= S::kRing / 2);
 #ifdef STROM_DECOMP_PROF
     const uint64_t _w1 = __builtin_amdgcn_s_memtime();
     const bool _slow = __any(live && !fast);
 #endif
-    if (live && !fast && !st.template step<kSnap>(codec)) {
-      if (!st.err) st.flush(st.op, true);
-      if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
-      live = false;
-      b += stride;
+    if (__builtin_expect(__any(exc), 0)) {
+      if (fast) {
+        st.pace(st.op);
+      } else if (live && st.window_short(kSnap)) {
+        // only the input window ran short: slide it now rather than send
+        // the next few sequences through the general step one by one
+        st.refill(st.ip);
+      } else if (live && !st.template step<kSnap>(codec)) {
+        if (!st.err) st.flush(st.op, true);
+        if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
+        live = false;
+        b += stride;
+      }
+      if (!live && b < nblocks) {
+        const strom_decomp_desc d = desc[b];
+        const uint8_t *in = src + d.src_off;
+        const uint32_t mis = (uint32_t)((uintptr_t)in & 3);
+        st.ina = in - mis;
+        st.out = dst + d.dst_off;
+        st.iend = d.src_len + mis;
+        st.ocap = d.dst_len;
+        st.ip = mis;
+        st.op = 0;
+        st.bend = 0;
+        st.win = 0xffffffffu;
+        st.vis = 0;
+        st.flushed = 0;
+        st.omis = (uint32_t)((uintptr_t)st.out & 15);
+        st.olen = 0;
+        st.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
+        st.fhdr = codec == STROM_CODEC_ARROW_LZ4;
+        st.mode = kHdr;
+        st.err = 0;
+        live = true;
+      }
+      if (!__any(live)) break;
     }
 #ifdef STROM_DECOMP_PROF
     const uint64_t _w2 = __builtin_amdgcn_s_memtime();

@@ -21,8 +21,8 @@ import numpy as np
 import torch
 
 
-def corpora():
-    rng = np.random.default_rng(1)
+def corpora(seed=1):
+    rng = np.random.default_rng(seed)
     words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
     return {
         "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
@@ -35,6 +35,9 @@ def main(argv=None) -> int:
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--streams", type=int, default=16384)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--distinct", type=int, default=1,
+                    help="K different blocks, stream i decodes block i mod K (kbench: 1, all "
+                         "streams identical, so the groups of a wave never diverge)")
     ap.add_argument("--cases", default="", help="e.g. lz4_words,snappy_ints (default: all)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
@@ -50,15 +53,23 @@ def main(argv=None) -> int:
     res = {}
     for codec in ("lz4", "snappy"):
         cid = D.LZ4 if codec == "lz4" else D.SNAPPY
-        for dname, blk in corpora().items():
+        pools = [corpora(1 + k) for k in range(a.distinct)]
+        for dname in pools[0]:
             if cases is not None and f"{codec}_{dname}" not in cases:
                 continue
-            comp = D.lz4_compress(blk) if codec == "lz4" else D.snappy_compress(blk)
+            blks = [p[dname] for p in pools]
+            blk = blks[0]
+            assert all(len(b) == len(blk) for b in blks)
+            comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in blks]
             n = a.streams
-            src = torch.from_numpy(np.frombuffer(comp * n, dtype=np.uint8).copy()).to(dev)
+            K = len(comps)
+            offs = np.cumsum([0] + [len(c) for c in comps])
+            one = b"".join(comps)
+            reps = (n + K - 1) // K
+            src = torch.from_numpy(np.frombuffer(one * reps, dtype=np.uint8).copy()).to(dev)
             dst = torch.empty(n * len(blk), dtype=torch.uint8, device=dev)
-            descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk))
-                                  for i in range(n)])
+            descs = D.make_descs([((i // K) * len(one) + int(offs[i % K]), len(comps[i % K]),
+                                   i * len(blk), len(blk)) for i in range(n)])
             d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
             status = torch.empty(n, dtype=torch.int32, device=dev)
             times = {k: [] for k in libs}
@@ -73,7 +84,7 @@ def main(argv=None) -> int:
                 run(lib)
                 torch.cuda.synchronize()
                 ok = bool((status == len(blk)).all().item()) and \
-                    bytes(dst[-len(blk):].cpu().numpy()) == blk
+                    bytes(dst[(n - 1) * len(blk):].cpu().numpy()) == blks[(n - 1) % K]
                 if not ok:
                     raise SystemExit(f"{name}: wrong output on {codec}/{dname}")
             for r in range(a.rounds):
@@ -91,7 +102,7 @@ def main(argv=None) -> int:
             res[f"{codec}_{dname}"] = row
             print(f"{codec}_{dname}", json.dumps(row), file=sys.stderr, flush=True)
             del src, dst
-    js = json.dumps({"GBps": res, "streams": a.streams, "rounds": a.rounds})
+    js = json.dumps({"GBps": res, "streams": a.streams, "rounds": a.rounds, "distinct": a.distinct})
     if a.out:
         with open(a.out, "w") as f:
             f.write(js)

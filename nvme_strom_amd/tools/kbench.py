@@ -114,6 +114,25 @@ def main(argv=None):
                 log(f"decompress_lz4_64k_{few}streams",
                     timed(lambda: D.decompress(cid, src, dst, descs[:few]), 3), few * len(blk))
             del src, dst
+            # 61 different blocks (stream i decodes block i mod 61): the groups
+            # of a wave diverge as on real data; the rows above decode copies
+            # of one block, which keeps a wave's streams in lockstep
+            from nvme_strom_amd.tools.decomp_ab import corpora
+            blks = [corpora(1 + k)[dname] for k in range(61)]
+            comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in blks]
+            offs = np.cumsum([0] + [len(c) for c in comps])
+            one = b"".join(comps)
+            reps = (nblk + 60) // 61
+            src = torch.from_numpy(np.frombuffer(one * reps, dtype=np.uint8).copy()).to(dev)
+            dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
+            descs = D.make_descs([((i // 61) * len(one) + int(offs[i % 61]), len(comps[i % 61]),
+                                   i * len(blk), len(blk)) for i in range(nblk)])
+            st = D.decompress(cid, src, dst, descs)
+            assert (st == len(blk)).all(), st[:4]
+            assert bytes(dst[len(blk):2 * len(blk)].cpu().numpy()) == blks[1 % 61]
+            log(f"decompress_{codec}_{tag}_distinct61",
+                timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
+            del src, dst
     if "filter" in only:
         nv = n // 8
         v = torch.randint(-1000, 1000, (nv,), dtype=torch.int64, device=dev)
