@@ -15,8 +15,11 @@
 // group's lanes, BPL consecutive bytes per lane per pass.
 //
 // Per stream (LDS, per group):
-//   * an input window of kInW bytes, refilled with dword loads from 4-aligned
-//     addresses ("P space": positions offset by the stream's misalignment);
+//   * an input window of kInW bytes ("P space": positions offset by the
+//     stream's misalignment to 16 bytes).  The next window is prefetched
+//     into VGPRs as soon as one is installed, so a sequential refill is LDS
+//     stores only (VGPRs are free: LDS already limits residency to one wave
+//     per SIMD);
 //     token / length / offset bytes come from two dword reads + alignbyte;
 //   * a history ring of kRing bytes.  Match bytes are read from the ring
 //     with the period recurrence out[s+k] = out[s-off+(k mod off)], s = the
@@ -25,8 +28,8 @@
 //     LDS stream).  Matches farther than kRing - W read the wave's own HBM
 //     output instead (L1-bypassing loads after a fence; one fence covers all
 //     output before it).
-// The hot path issues no vector-memory loads, so it never waits on vmcnt,
-// which on CDNA also counts the wave's in-flight byte stores.
+// The hot path waits on vmcnt only when it installs a prefetched window
+// (on CDNA vmcnt also counts the wave's in-flight output stores).
 //
 // Codecs: raw LZ4 block, LZ4 frame block sequence (linked or independent
 // blocks, optional per-block checksums skipped, stored blocks), a whole
@@ -83,14 +86,20 @@ struct Stream {
   static constexpr uint32_t kInW = INW_;
   static constexpr uint32_t kDummy = 16;     // sink for masked-off fast-path stores
   static constexpr uint32_t kSlot = kRing + kInW + kDummy;   // LDS bytes per stream
+  // input prefetch: the next window, kPfN 16-byte loads per lane, starts
+  // kSlide bytes past the current one (the overlap covers reads that
+  // straddle the old window's end)
+  static constexpr uint32_t kPfN = kInW / (16 * GL);
+  static constexpr uint32_t kSlide = kInW - 64;
   // waves per SIMD the LDS footprint allows (160 KiB per CU, 4 SIMDs)
   static constexpr uint32_t kMinWaves = (160u * 1024 / (G * kSlot)) / 4 >= 4 ? 4 : 1;
   static_assert(64 % GL == 0 && (kRing & kMask) == 0, "geometry");
   static_assert(kRing >= 4 * W && kInW >= 4 * W && kInW % 4 == 0, "window sizes");
   static_assert(G * kSlot <= 64 * 1024, "LDS per wave");
+  static_assert(kInW % (16 * GL) == 0 && kSlot % 16 == 0, "prefetch tiles");
   static_assert(kRing / 2 + 3 * W + 16 <= kRing, "flush pacing vs ring / far matches");
 
-  const uint8_t *ina;  // 4-aligned input base (= stream start - mis)
+  const uint8_t *ina;  // 16-aligned input base (= stream start - mis)
   uint8_t *out;
   uint8_t *ring;       // this group's LDS history ring
   uint8_t *inw;        // this group's LDS input window
@@ -110,13 +119,39 @@ struct Stream {
   uint32_t fhdr;       // Arrow buffer: length prefix + frame header pending
   uint32_t mode;
   int32_t err;
+  uint32_t pf_at;      // P-space start of the prefetched window; ~0 = none
+  uint4 pf[kPfN];      // lane t: 16 bytes at pf_at + 16 (u GL + t)
 #ifdef STROM_DECOMP_PROF
   uint64_t prof[kPN];
 #endif
 
-  __device__ void refill(uint32_t p) {
+  // Window for [p, p + need).  Takes the prefetched next window when it
+  // covers the range (the sequential case: its loads were issued one window
+  // earlier, so no HBM latency here), else loads synchronously; then issues
+  // the prefetch of the window after.  With the streams of a wave out of
+  // step, each group's synchronous refill stalled all 16 (round 2 profile,
+  // 61 distinct blocks: ~4.5k cycles per refill, ~30 % of the wave).
+  __device__ void refill(uint32_t p, uint32_t need) {
     PROF_T0();
     PROF_CNT(kPNRefill, 1);
+    if (pf_at != 0xffffffffu && p >= pf_at && p + need <= pf_at + kInW) {
+#pragma unroll
+      for (uint32_t u = 0; u < kPfN; ++u) *(uint4 *)(inw + 16 * (u * GL + t)) = pf[u];
+      win = pf_at;
+    } else {
+      load_window(p);
+    }
+    const uint32_t nx = (win + kSlide) & ~15u;
+    if (nx + kInW <= iend) {
+#pragma unroll
+      for (uint32_t u = 0; u < kPfN; ++u) pf[u] = *(const uint4 *)(ina + nx + 16 * (u * GL + t));
+      pf_at = nx;
+    } else {
+      pf_at = 0xffffffffu;
+    }
+    PROF_ADD(kPRefill);
+  }
+  __device__ void load_window(uint32_t p) {
     const uint32_t at = p & ~3u;
     const uint32_t n = iend - at < kInW ? iend - at : kInW;
     const uint8_t *src = ina + at;
@@ -132,11 +167,10 @@ struct Stream {
     for (; k + 4 <= n; k += GL * 4) *(uint32_t *)(inw + k) = *(const uint32_t *)(src + k);
     for (uint32_t kb = (n & ~3u) + t; kb < n; kb += GL) inw[kb] = src[kb];  // <= 3 tail bytes
     win = at;
-    PROF_ADD(kPRefill);
   }
   // window holds [p, p + need) (bytes past iend are never used)
   __device__ __forceinline__ void ensure(uint32_t p, uint32_t need) {
-    if (p < win || p + need > win + kInW) refill(p);
+    if (p < win || p + need > win + kInW) refill(p, need);
   }
   // bytes p..p+3 (little endian) and, in *b4, byte p+4
   __device__ __forceinline__ uint32_t rd4(uint32_t p, uint32_t *b4) {
@@ -172,7 +206,18 @@ struct Stream {
     PROF_CNT(kPNFlush, 1);
     const uint32_t rb = flushed + omis, re = upto + omis;
     const uint32_t cb = rb >> 4, ce = exact ? (re + 15) >> 4 : re >> 4;
-    for (uint32_t c = cb + t; c < ce; c += GL) {
+    uint32_t c = cb + t;
+    // whole chunks four at a time: the four LDS reads in flight together
+    // instead of one read-then-store round trip per chunk
+    const uint32_t cfull = re >> 4;
+    for (; c + 3 * GL < cfull && (c << 4) >= rb; c += 4 * GL) {
+      uint4 v[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) v[u] = *(const uint4 *)(ring + (((c + u * GL) << 4) & kMask));
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u) *(uint4 *)(out + (((c + u * GL) << 4) - omis)) = v[u];
+    }
+    for (; c < ce; c += GL) {
       const uint32_t r0 = c << 4;
       const uint32_t lo = r0 < rb ? rb : r0, hi = r0 + 16 > re ? re : r0 + 16;
       const uint4 v = *(const uint4 *)(ring + (r0 & kMask));
@@ -682,7 +727,7 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
       } else if (live && st.window_short(kSnap)) {
         // only the input window ran short: slide it now rather than send
         // the next few sequences through the general step one by one
-        st.refill(st.ip);
+        st.refill(st.ip, 24);
       } else if (live && !st.template step<kSnap>(codec)) {
         if (!st.err) st.flush(st.op, true);
         if (st.t == 0) status[b] = st.err ? st.err : (int32_t)st.op;
@@ -692,7 +737,7 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
       if (!live && b < nblocks) {
         const strom_decomp_desc d = desc[b];
         const uint8_t *in = src + d.src_off;
-        const uint32_t mis = (uint32_t)((uintptr_t)in & 3);
+        const uint32_t mis = (uint32_t)((uintptr_t)in & 15);
         st.ina = in - mis;
         st.out = dst + d.dst_off;
         st.iend = d.src_len + mis;
@@ -701,6 +746,7 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
         st.op = 0;
         st.bend = 0;
         st.win = 0xffffffffu;
+        st.pf_at = 0xffffffffu;
         st.vis = 0;
         st.flushed = 0;
         st.omis = (uint32_t)((uintptr_t)st.out & 15);
@@ -734,8 +780,8 @@ __global__ __launch_bounds__(64, S::kMinWaves) void decompress_kernel(int codec,
 // 160 KiB: at 40.5 KiB only 3 fit (round 2 trace: LDS_Block_Size 41472)
 using S16 = Stream<4, 2048, 448>;     // 16 streams per wave
 // A/B variant: half the LDS (2 waves per SIMD), a 1 KiB history ring
-using S16s = Stream<4, 1024, 224>;    // 16 streams per wave, 19.5 KiB
-using S8 = Stream<8, 2048, 448>;      // 8 streams per wave, 19.5 KiB (2 waves per SIMD)
+using S16s = Stream<4, 1024, 256>;    // 16 streams per wave, 19.5 KiB
+using S8 = Stream<8, 2048, 512>;      // 8 streams per wave, 19.5 KiB (2 waves per SIMD)
 using S4 = Stream<16, 2048, 512>;     // 4 streams per wave, 10 KiB
 using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
 

@@ -30,6 +30,8 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="", help="a profiling build other than lib/libstrom_decprof.so")
     ap.add_argument("--g", default="", help="comma-separated geometries (default: all)")
+    ap.add_argument("--distinct", type=int, default=1,
+                    help="K different blocks per corpus (stream i decodes block i mod K)")
     a = ap.parse_args(argv)
     from nvme_strom_amd.ops import decompress as D
     lib = C.CDLL(os.path.abspath(a.lib) if a.lib else
@@ -38,22 +40,32 @@ def main(argv=None) -> int:
     lib.strom_decompress.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.c_void_p, C.c_void_p]
     lib.strom_decomp_prof.argtypes = [C.c_void_p]
-    rng = np.random.default_rng(1)
-    words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
-    corpora = {
-        "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
-        "ints": np.cumsum(rng.integers(0, 5, 8192)).astype(np.int64).tobytes(),
-        "rand3": np.random.default_rng(2).integers(0, 1_000_000, 8192).astype(np.int64).tobytes(),
-    }
+    def corpora(seed):
+        rng = np.random.default_rng(seed)
+        words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+        return {
+            "words": b" ".join(words[i] for i in rng.integers(0, len(words), 16000))[:64 << 10],
+            "ints": np.cumsum(rng.integers(0, 5, 8192)).astype(np.int64).tobytes(),
+            "rand3": np.random.default_rng(seed + 1).integers(0, 1_000_000, 8192)
+            .astype(np.int64).tobytes(),
+        }
+    pools = [corpora(1 + k) for k in range(a.distinct)]
+    K = a.distinct
     res = {}
     dev = torch.device("cuda")
-    for cname, blk in corpora.items():
-        comp = D.lz4_compress(blk)
+    for cname in pools[0]:
+        blks = [p[cname] for p in pools]
+        blk = blks[0]
+        comps = [D.lz4_compress(b) for b in blks]
+        offs = np.cumsum([0] + [len(c) for c in comps])
+        one = b"".join(comps)
+        comp = comps[0]
         for nblk in sorted({a.blocks, 1024}):
-            src = torch.from_numpy(np.frombuffer(comp * nblk, dtype=np.uint8).copy()).to(dev)
+            reps = (nblk + K - 1) // K
+            src = torch.from_numpy(np.frombuffer(one * reps, dtype=np.uint8).copy()).to(dev)
             dst = torch.empty(nblk * len(blk), dtype=torch.uint8, device=dev)
-            descs = D.make_descs([(i * len(comp), len(comp), i * len(blk), len(blk))
-                                  for i in range(nblk)])
+            descs = D.make_descs([((i // K) * len(one) + int(offs[i % K]), len(comps[i % K]),
+                                   i * len(blk), len(blk)) for i in range(nblk)])
             d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
             status = torch.empty(nblk, dtype=torch.int32, device=dev)
             gs = (16, 8, 4, 1) if nblk <= 1024 else (16, 8, 32)
