@@ -64,8 +64,17 @@ def main(argv=None) -> int:
                   flush=True)
     finally:
         os.close(fd)
+    import statistics
     best, raw = max(res["runs"]), max(res["raw"])
+    med, rmed = statistics.median(res["runs"]), statistics.median(res["raw"])
+    # runs alternate engine / raw on the same file, so the pairwise ratio
+    # cancels the box's drift between reps (the raw rate alone moved 18-25
+    # GiB/s between 2 GiB reps on the pool's overlay storage)
+    pair = [r / w for r, w in zip(res["runs"], res["raw"]) if w]
     res.update(ssd2ram_GiBps=best, raw_GiBps=raw, of_raw=round(best / raw, 3) if raw else None,
+               ssd2ram_median_GiBps=med, raw_median_GiBps=rmed,
+               of_raw_median=round(med / rmed, 3) if rmed else None,
+               of_raw_pairwise_median=round(statistics.median(pair), 3) if pair else None,
                last_stdout=out.stdout.strip().splitlines())
     js = json.dumps(res)
     if a.out:

@@ -47,7 +47,7 @@ for phase in "$@"; do
     btrace) (cd /tmp && step btrace 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/btrace" -o btrace \
               -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --lat-samples 300) ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
-    ram) step ram 400 python -u -m nvme_strom_amd.tools.ram_bench --out "$OUT/ram.json" ;;
+    ram) step ram 500 python -u -m nvme_strom_amd.tools.ram_bench --file-gib ${RAM_GIB:-8} --reps ${RAM_REPS:-7} --out "$OUT/ram.json" ;;
     decprof) step decprof 300 python -u -m nvme_strom_amd.tools.decomp_prof --out "$OUT/decprof.json" ;;
     decpmc) for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
                         "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
