@@ -80,6 +80,15 @@ class _Group:
     ids: np.ndarray                       # sorted file chunk ids
     dec_bytes: int = 0
     words: int = 0
+    # slot-relative launch tables, built once per plan (_prepare): decoder
+    # descriptors, and per batch the data/validity pointers as (kind, offset)
+    # with kind 0 none, 1 slot region, 2 decode buffer
+    descs: Optional[np.ndarray] = None
+    need: Optional[np.ndarray] = None
+    ptr_kind: Optional[np.ndarray] = None
+    ptr_rel: Optional[np.ndarray] = None
+    table: Optional[np.ndarray] = None    # (n, BATCH_FIELDS) with pointer columns 0
+    column_bytes: int = 0
 
 
 @dataclass
@@ -118,6 +127,7 @@ class ArrowScan:
         self.nslots = max(2, nslots)
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
+        self._plans: Dict[str, tuple] = {}     # column -> (dtype, rows, groups)
 
     # ------------------------------------------------------------- plan
     def _plan(self, name: str) -> tuple:
@@ -162,22 +172,67 @@ class ArrowScan:
             avg = sum(b.data.length + (b.valid.length if b.valid else 0) for b in comp) / len(comp)
             slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
         limit = max(1, slot // self.chunk_sz)
-        for b in batches:
-            mine = self._chunks(b)
-            merged = np.union1d(ids, mine)
-            if cur and len(merged) > limit:
-                groups.append(_Group(cur, ids))
-                cur, merged = [], np.unique(mine)
+        seen: set = set()            # the current group's chunk ids (linear time;
+        for b in batches:            # a running np.union1d was quadratic in batches)
+            mine = self._chunks(b).tolist()
+            fresh = [c for c in mine if c not in seen]
+            if cur and len(seen) + len(fresh) > limit:
+                groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
+                cur, seen, fresh = [], set(), mine
             cur.append(b)
-            ids = merged
+            seen.update(fresh)
         if cur:
-            groups.append(_Group(cur, ids))
+            groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
         for g in groups:
             g.dec_bytes = sum((b.data.cap if b.data.compressed else 0) +
                               (b.valid.cap if b.valid is not None and b.valid.compressed else 0)
                               for b in g.batches)
             g.words = sum((b.rows + 63) // 64 for b in g.batches)
+            self._prepare(g)
         return groups
+
+    def _prepare(self, g: _Group) -> None:
+        c = self.chunk_sz
+        n = len(g.batches)
+        kind = np.zeros((n, 2), dtype=np.int8)
+        rel = np.zeros((n, 2), dtype=np.int64)
+        so, sl, do, dl, need = [], [], [], [], []
+        dcur = 0
+        for i, b in enumerate(g.batches):
+            for j, buf in enumerate((b.data, b.valid)):
+                if buf is None:
+                    continue
+                if buf.length == 0:
+                    kind[i, j] = 2                    # empty batch: nothing is read
+                elif buf.compressed:
+                    so.append(buf.off)
+                    sl.append(buf.length)
+                    do.append(dcur)
+                    dl.append(buf.cap)
+                    need.append(buf.need)
+                    kind[i, j], rel[i, j] = 2, dcur
+                    dcur += buf.cap
+                else:
+                    kind[i, j], rel[i, j] = 1, buf.off
+        # file offsets -> offsets in the slot (chunks land in id order)
+        def slot_off(off):
+            off = np.asarray(off, dtype=np.int64)
+            return np.searchsorted(g.ids, off // c) * c + off % c
+        reg = kind == 1
+        rel[reg] = slot_off(rel[reg])
+        if so:
+            g.descs = D.make_descs_arrays(slot_off(so), np.asarray(sl), np.asarray(do),
+                                          np.asarray(dl))
+            g.need = np.asarray(need, dtype=np.int32)
+        g.ptr_kind, g.ptr_rel = kind, rel
+        rows = np.array([b.rows for b in g.batches], dtype=np.int64)
+        words = (rows + 63) // 64
+        table = np.zeros((n, BATCH_FIELDS), dtype=np.int64)
+        table[:, 2] = rows
+        table[:, 3] = np.concatenate([[0], np.cumsum(words)[:-1]]) if n else 0
+        table[:, 4] = [b.row_base for b in g.batches]
+        g.table = table
+        g.column_bytes = sum(b.data.need for b in g.batches)
 
     # --------------------------------------------------------- pipeline
     def _ensure_slots(self, groups: List[_Group]) -> None:
@@ -235,36 +290,14 @@ class ArrowScan:
                                                              res.nr_ssd), self.chunk_sz)
             base = region.data_ptr()
             dec_base = s.dec.data_ptr()
-            c = self.chunk_sz
-
-            def slot_off(off: int) -> int:
-                return int(np.searchsorted(g.ids, off // c)) * c + off % c
-
-            descs, need = [], []
-            table = np.zeros((len(g.batches), BATCH_FIELDS), dtype=np.int64)
-            dcur, wcur = 0, 0
-            for i, b in enumerate(g.batches):
-                ptrs = []
-                for buf in (b.data, b.valid):
-                    if buf is None:
-                        ptrs.append(0)
-                    elif buf.length == 0:
-                        ptrs.append(dec_base)        # empty batch: nothing is read
-                    elif buf.compressed:
-                        descs.append((slot_off(buf.off), buf.length, dcur, buf.cap))
-                        need.append(buf.need)
-                        ptrs.append(dec_base + dcur)
-                        dcur += buf.cap
-                    else:
-                        ptrs.append(base + slot_off(buf.off))
-                table[i] = (ptrs[0], ptrs[1], b.rows, wcur, b.row_base)
-                wcur += (b.rows + 63) // 64
-            if descs:
-                d = D.make_descs(descs)
-                d_desc = torch.from_numpy(d.view(np.uint8).copy()).pin_memory().to(
+            table = g.table.copy()
+            table[:, :2] = np.where(g.ptr_kind == 1, base + g.ptr_rel,
+                                    np.where(g.ptr_kind == 2, dec_base + g.ptr_rel, 0))
+            descs = g.descs
+            if descs is not None:
+                d_desc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(
                     self.device, non_blocking=True)
-                d_need = torch.from_numpy(np.array(need, dtype=np.int32)).pin_memory().to(
-                    self.device, non_blocking=True)
+                d_need = torch.from_numpy(g.need).pin_memory().to(self.device, non_blocking=True)
                 status = torch.empty(len(descs), dtype=torch.int32, device=self.device)
                 D.decompress_async(D.ARROW_LZ4, region, s.dec, d_desc, status, stream=cs)
                 # status = decoded bytes; short or failed -> error count
@@ -285,20 +318,22 @@ class ArrowScan:
                            stream=es)
             state["count"] += s.count
             s.count.zero_()
-            if descs:
+            if descs is not None:
                 state["err"] += s.err
                 s.err.zero_()
             s.event = torch.cuda.Event()
             s.event.record(es)
         state["bytes_read"] += len(g.ids) * self.chunk_sz
-        state["column_bytes"] += sum(b.data.need for b in g.batches)
+        state["column_bytes"] += g.column_bytes
 
     def scan(self, name: str, lo, hi) -> ScanOut:
         """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never
         qualify)."""
         t0 = time.perf_counter()
-        batches, dtype, nrows = self._plan(name)
-        groups = self._groups(batches)
+        if name not in self._plans:               # the file's layout is fixed once opened
+            batches, dtype, nrows = self._plan(name)
+            self._plans[name] = (dtype, nrows, self._groups(batches))
+        dtype, nrows, groups = self._plans[name]
         out = torch.empty(max(nrows, 1), dtype=torch.int64, device=self.device)
         if not groups or nrows == 0:
             return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0})

@@ -116,9 +116,19 @@ def _xxh32(data: bytes, seed: int = 0) -> int:
 # ------------------------------------------------------------ GPU decode
 def make_descs(items: Sequence[tuple]) -> np.ndarray:
     """items: (src_off, src_len, dst_off, dst_len) per stream."""
-    d = np.zeros(len(items), dtype=DESC_DTYPE)
-    for i, (so, sl, do, dl) in enumerate(items):
-        d[i] = (so, do, sl, dl)
+    if len(items) == 0:
+        return np.zeros(0, dtype=DESC_DTYPE)
+    a = np.asarray(items, dtype=np.int64).reshape(-1, 4)
+    return make_descs_arrays(a[:, 0], a[:, 1], a[:, 2], a[:, 3])
+
+
+def make_descs_arrays(src_off, src_len, dst_off, dst_len) -> np.ndarray:
+    """The same from four equal-length integer arrays (no per-stream Python)."""
+    d = np.zeros(len(src_off), dtype=DESC_DTYPE)
+    d[DESC_DTYPE.names[0]] = src_off
+    d[DESC_DTYPE.names[1]] = dst_off
+    d[DESC_DTYPE.names[2]] = src_len
+    d[DESC_DTYPE.names[3]] = dst_len
     return d
 
 
