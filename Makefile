@@ -19,7 +19,7 @@ ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
-all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so
+all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_waveprof.so
 
 tools: $(TOOLS)
 
@@ -44,6 +44,11 @@ $(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/include/strom/strom
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ $<
 
+# the wave-per-stream decoder with its phase profile (tools/wave_prof.py)
+$(OUT)/libstrom_waveprof.so: csrc/kernels/decompress_wave.hip csrc/include/strom/strom.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -DSTROM_WAVE_PROF -shared -o $@ $<
+
 # a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
 # make ab AB=name [SRC=path/to/decompress.hip]
 SRC ?= csrc/kernels/decompress.hip
@@ -56,7 +61,7 @@ $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
-	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(TOOLS)
+	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_waveprof.so $(TOOLS)
 
 .PHONY: all tools clean ab
 

@@ -801,6 +801,11 @@ int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d
 
 }  // namespace
 
+// decompress_wave.hip: one wave per stream (few, long streams)
+extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
+                                     const strom_decomp_desc *d_desc, uint32_t nblocks,
+                                     int32_t *d_status, void *stream);
+
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
 // STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring) forces a
@@ -817,6 +822,11 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // wave, 1k streams 5.3 / 2.7 / 2.9): wide groups pay more per sequence
   // (the short-period path covers every offset below the pass width) than
   // they gain from more resident waves
+  // wave per stream: forced (64), or snappy with few streams, where it
+  // measured 1.1-1.9x the lane groups (round 2 wave rows: 1,024 / 2,048
+  // distinct streams; the LZ4 lane-group step is the leaner one there too)
+  if (g == 64 || (!e && codec == STROM_CODEC_SNAPPY && nblocks <= 2048))
+    return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   if (g != 1 && g != 4 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);

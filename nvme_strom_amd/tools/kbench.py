@@ -133,6 +133,8 @@ def main(argv=None):
             log(f"decompress_{codec}_{tag}_distinct61",
                 timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
             del src, dst
+    if "wave" in only:
+        _wave_rows(D, dev, log)
     if "filter" in only:
         nv = n // 8
         v = torch.randint(-1000, 1000, (nv,), dtype=torch.int64, device=dev)
@@ -144,6 +146,57 @@ def main(argv=None):
         with open(a.out, "w") as f:
             f.write(js)
     print(js)
+
+
+def _wave_rows(D, dev, log):
+    """Lane-group (g16) vs wave-per-stream (g64) decoder by stream count:
+    61 distinct 64 KiB blocks per codec/corpus, and config-5-shaped streams
+    (pyarrow LZ4 frames of 512 KiB, eight linked 64 KiB blocks each)."""
+    from nvme_strom_amd.tools.decomp_ab import corpora
+
+    def run(tag, cid, comps, sizes, counts):
+        offs = np.cumsum([0] + [len(c) for c in comps])
+        one = b"".join(comps)
+        osz = np.cumsum([0] + list(sizes))
+        k = len(comps)
+        for cnt in counts:
+            reps = (cnt + k - 1) // k
+            src = torch.from_numpy(np.frombuffer(one * reps, dtype=np.uint8).copy()).to(dev)
+            dst = torch.empty(int(osz[-1]) * reps, dtype=torch.uint8, device=dev)
+            descs = D.make_descs([((i // k) * len(one) + int(offs[i % k]), len(comps[i % k]),
+                                   (i // k) * int(osz[-1]) + int(osz[i % k]), sizes[i % k])
+                                  for i in range(cnt)])
+            total = sum(sizes[i % k] for i in range(cnt))
+            for g in ("16", "64"):
+                os.environ["STROM_DECOMP_G"] = g
+                st = D.decompress(cid, src, dst, descs)
+                assert (st == np.array([sizes[i % k] for i in range(cnt)])).all(), (g, st[:4])
+                j = cnt - 1
+                lo = (j // k) * int(osz[-1]) + int(osz[j % k])
+                assert bytes(dst[lo:lo + 4096].cpu().numpy()) == corpus_out[j % k][:4096]
+                log(f"wave_{tag}_{cnt}streams_g{g}",
+                    timed(lambda: D.decompress(cid, src, dst, descs), 3), total)
+            os.environ.pop("STROM_DECOMP_G", None)
+            del src, dst
+
+    for codec in ("lz4", "snappy"):
+        for dname in ("words", "ints"):
+            corpus_out = [corpora(1 + k)[dname] for k in range(61)]
+            comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in corpus_out]
+            run(f"{codec}_{dname}", D.LZ4 if codec == "lz4" else D.SNAPPY, comps,
+                [len(b) for b in corpus_out], (1024, 2048, 4096, 16384))
+    try:
+        import pyarrow as pa
+    except Exception:
+        return
+    rng = np.random.default_rng(3)
+    corpus_out = [np.cumsum(rng.integers(0, 1 << 12, 65536)).astype(np.int64).tobytes()
+                  for _ in range(8)]
+    frames = [pa.compress(b, codec="lz4", asbytes=True) for b in corpus_out]
+    info = D.parse_lz4_frame_header(frames[0])
+    comps = [f[info.data_offset:] for f in frames]
+    cid = D.LZ4_FRAME_BCS if info.block_checksum else D.LZ4_FRAME
+    run("frame512k_ints", cid, comps, [len(b) for b in corpus_out], (512, 2048))
 
 
 if __name__ == "__main__":

@@ -127,12 +127,13 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 4, 8, 16, 32])
+@pytest.mark.parametrize("g", [1, 4, 8, 16, 32, 64])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant (STROM_DECOMP_G) decodes the same
     payloads: the fast LZ4 step's pass width differs per geometry (a
-    length-15 match nibble must still take the extended-length path)."""
+    length-15 match nibble must still take the extended-length path);
+    64 = the wave-per-stream batched decoder (decompress_wave.hip)."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
     monkeypatch.setenv("STROM_DECOMP_G", str(g))
@@ -159,10 +160,13 @@ def test_snappy(dev, which):
     assert outs == pays
 
 
-def test_lz4_frame_linked_blocks_from_pyarrow(dev):
+@pytest.mark.parametrize("g", ["auto", "64"])
+def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     """pyarrow's 'lz4' codec = LZ4 frame with linked 64 KiB blocks: matches
     may reach into the previous block, which the LDS history ring covers."""
     pa = pytest.importorskip("pyarrow")
+    if g != "auto":
+        monkeypatch.setenv("STROM_DECOMP_G", g)
     from nvme_strom_amd.ops import decompress as D
     pays = [p for p in _payloads() if p]
     frames = [pa.compress(p, codec="lz4", asbytes=True) for p in pays]
@@ -174,8 +178,11 @@ def test_lz4_frame_linked_blocks_from_pyarrow(dev):
     assert outs == pays
 
 
-def test_malformed_streams_report_errors(dev):
+@pytest.mark.parametrize("g", ["auto", "64"])
+def test_malformed_streams_report_errors(dev, monkeypatch, g):
     from nvme_strom_amd.ops import decompress as D
+    if g != "auto":
+        monkeypatch.setenv("STROM_DECOMP_G", g)
     rng = np.random.default_rng(5)
     junk = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (10, 1000, 5000)]
     good = D.lz4_compress(b"hello world " * 1000)
