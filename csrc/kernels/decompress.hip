@@ -328,8 +328,12 @@ struct Stream {
           // pace() keeps these sources flushed already; stay safe anyway
           PROF_T0();
           if (s - off + n > flushed) flush(s, true);
-          // our stores complete at L2 before the L1-bypassing loads below
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          // our stores complete at L2 before the L1-bypassing loads below.
+          // Workgroup scope = s_waitcnt vmcnt(0): the reader is this wave,
+          // whose traffic all goes to its own XCD's L2, so no L2 write-back
+          // (the agent-scope form adds buffer_wbl2: ~4.9k cycles per far
+          // match on the config-5 column, where 24 % of matches are far)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           vis = flushed;
           PROF_ADD(kPFarFence);
         }
@@ -385,9 +389,29 @@ struct Stream {
   // Relative to any pass start sp the same holds with sp for s (the output
   // from s - off on is periodic), so both passes use the same residues;
   // the second runs only for groups whose match needs it.
-  __device__ __forceinline__ void fast_copy(uint32_t s, uint32_t off, uint32_t mlen) {
+  // far (off > kRing - W, sources below vis: stored and fenced) reads the
+  // wave's HBM output instead of the ring: off > 2W >= mlen, so the 4 bytes
+  // of a lane are consecutive (two L1-bypassing dword loads + alignbyte)
+  __device__ __forceinline__ void fast_copy(uint32_t s, uint32_t off, uint32_t mlen, bool far) {
     uint8_t *sink = inw + kInW;
     const uint32_t k = t * BPL;
+    if (far) {
+#pragma unroll
+      for (uint32_t c = 0; c < 2 * W; c += W) {
+        if (c && mlen <= W) break;
+        const uintptr_t q = (uintptr_t)(out + s - off + c + k);
+        const uint32_t *w = (const uint32_t *)(q & ~(uintptr_t)3);
+        const uint32_t d0 = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t d1 = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)(q & 3));
+#pragma unroll
+        for (uint32_t j = 0; j < BPL; ++j) {
+          uint8_t *d = c + k + j < mlen ? ring + ((s + c + k + j + omis) & kMask) : sink + 4 + j;
+          *d = (uint8_t)(v >> (8 * j));
+        }
+      }
+      return;
+    }
     const uint32_t base = s - off + omis;
     uint32_t q = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)off));
     uint32_t r = k - q * off;
@@ -445,8 +469,11 @@ struct Stream {
     const uint32_t ol = o + 1 + t * BPL;
     const uint32_t *f = (const uint32_t *)(inw + (ol & ~3u));
     const uint32_t lv = __builtin_amdgcn_alignbyte(f[1], f[0], ol & 3);
+    // a far match (past the ring) stays in the fast step when its source
+    // lies below vis (already stored and fenced: read back from HBM)
+    const bool far = off > kRing - W;
     ok = ok & (lit != 15) & ((ml != 15) | (xb != 255)) & (mlen <= 2 * W) & (off != 0) &
-         (off <= op + lit) & (off <= kRing - W) & (lit + mlen <= ocap - op);
+         (off <= op + lit) & (!far | (op + lit + mlen <= vis + off)) & (lit + mlen <= ocap - op);
     if (!ok) return false;
     {
       uint8_t *sink = inw + kInW;
@@ -457,7 +484,7 @@ struct Stream {
         *dd = (uint8_t)(lv >> (8 * j));
       }
     }
-    fast_copy(op + lit, off, mlen);
+    fast_copy(op + lit, off, mlen, far);
     ip += 3 + lit + (ml == 15);
     op += lit + mlen;
     return true;                 // flush pacing: the kernel loop's exception test
@@ -496,7 +523,7 @@ struct Stream {
         *dd = (uint8_t)(lv >> (8 * j));
       }
     }
-    fast_copy(op, off, mlen);
+    fast_copy(op, off, mlen, false);
     ip += islit ? 1 + len : 1 + kind;
     op += len;
     return true;
@@ -784,6 +811,12 @@ using S16s = Stream<4, 1024, 256>;    // 16 streams per wave, 19.5 KiB
 using S8 = Stream<8, 2048, 512>;      // 8 streams per wave, 19.5 KiB (2 waves per SIMD)
 using S4 = Stream<16, 2048, 512>;     // 4 streams per wave, 10 KiB
 using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
+// few streams (<= 2,048: a launch leaves most SIMDs idle anyway): large
+// history rings, so far matches (sources past the ring, read back from HBM)
+// stay rare — on the config-5 column 24 % of LZ4 matches reach past 2 KiB,
+// 5 % past 16 KiB
+using S2L = Stream<32, 16384, 512>;   // 2 streams per wave, 33 KiB
+using S4L = Stream<16, 8192, 512>;    // 4 streams per wave, 35 KiB
 
 template <class S>
 int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d_desc,
@@ -808,7 +841,8 @@ extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
 
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
-// STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring) forces a
+// STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring; 2 / 6 = 2 / 4
+// streams per wave with 16 / 8 KiB rings; 64 = wave per stream) forces a
 // geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
@@ -817,18 +851,21 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   if (!nblocks) return 0;
   const char *e = getenv("STROM_DECOMP_G");
   uint32_t g = e ? (uint32_t)atoi(e) : 0u;
-  // 16 streams per wave wins at every stream count measured (round 2
-  // decprof: 16k streams 107 / 76 / 21 GB/s for 16 / 4 / 1 streams per
-  // wave, 1k streams 5.3 / 2.7 / 2.9): wide groups pay more per sequence
-  // (the short-period path covers every offset below the pass width) than
-  // they gain from more resident waves
-  // wave per stream: forced (64), or snappy with few streams, where it
-  // measured 1.1-1.9x the lane groups (round 2 wave rows: 1,024 / 2,048
-  // distinct streams; the LZ4 lane-group step is the leaner one there too)
-  if (g == 64 || (!e && codec == STROM_CODEC_SNAPPY && nblocks <= 2048))
-    return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
-  if (g != 1 && g != 4 && g != 8 && g != 16 && g != 32) g = 16;
+  // Default geometry by stream count (round 2 same-box A/B over 61 distinct
+  // blocks + config-5 frames, profiles/r2/dec/geometry_ab.json): few
+  // streams leave SIMDs idle whatever the geometry, so they get fewer
+  // streams per wave and larger history rings (far matches — HBM reads —
+  // stay rare); from ~16k streams 16 per wave wins (VALU per stream).
+  //   <= 2,048: 2 per wave, 16 KiB rings (config-5 frames 14.6 -> 27.5 GB/s)
+  //   <= 4,096: 4 per wave, 8 KiB rings;  <= 8,192: 4 per wave, 2 KiB rings
+  if (!e) g = nblocks <= 2048 ? 2 : nblocks <= 4096 ? 6 : nblocks <= 8192 ? 4 : 16;
+  // wave per stream (decompress_wave.hip): forced only; the large-ring lane
+  // groups measured as fast or faster at every count
+  if (g == 64) return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+  if (g != 1 && g != 2 && g != 4 && g != 6 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
+  if (g == 2) return launch<S2L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  if (g == 6) return launch<S4L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 32) return launch<S16s>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 8) return launch<S8>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);

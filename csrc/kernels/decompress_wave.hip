@@ -193,7 +193,9 @@ struct WaveStream {
     if (end > flushed) flush(end, true);
     if (end > fenced) {
       WP_CNT(kNFence, 1);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      // this wave's stores done at its XCD's L2 (s_waitcnt vmcnt(0)); the
+      // readers are this wave's own L1-bypassing loads, so no L2 write-back
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       fenced = flushed;
     }
   }

@@ -39,6 +39,12 @@ def main(argv=None) -> int:
                     help="K different blocks, stream i decodes block i mod K (kbench: 1, all "
                          "streams identical, so the groups of a wave never diverge)")
     ap.add_argument("--cases", default="", help="e.g. lz4_words,snappy_ints (default: all)")
+    ap.add_argument("--arrow", type=int, default=0,
+                    help="also N config-5 streams: pyarrow LZ4 frames of 65,536 int64 uniform in "
+                         "[0, 1e6) (arrow_bench's val column; 24 %% of matches past 2 KiB)")
+    ap.add_argument("--g", default="",
+                    help="comma-separated STROM_DECOMP_G values: every build runs under each "
+                         "(variants named build@g)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     cases = set(a.cases.split(",")) if a.cases else None
@@ -48,20 +54,33 @@ def main(argv=None) -> int:
         lib = C.CDLL(os.path.abspath(p))
         lib.strom_decompress.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                          C.c_void_p, C.c_void_p]
-        libs[os.path.basename(p).rsplit(".", 1)[0]] = lib
+        name = os.path.basename(p).rsplit(".", 1)[0]
+        for g in (a.g.split(",") if a.g else [""]):
+            libs[f"{name}@{g}" if g else name] = (lib, g)
     dev = torch.device("cuda")
     res = {}
+    todo = []
     for codec in ("lz4", "snappy"):
-        cid = D.LZ4 if codec == "lz4" else D.SNAPPY
         pools = [corpora(1 + k) for k in range(a.distinct)]
         for dname in pools[0]:
             if cases is not None and f"{codec}_{dname}" not in cases:
                 continue
             blks = [p[dname] for p in pools]
+            comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in blks]
+            todo.append((codec, dname, D.LZ4 if codec == "lz4" else D.SNAPPY, blks, comps, a.streams))
+    if a.arrow:
+        import pyarrow as pa
+        rng = np.random.default_rng(7)
+        blks = [rng.integers(0, 1_000_000, 65536, dtype=np.int64).tobytes()
+                for _ in range(max(1, a.distinct))]
+        frames = [pa.compress(b, codec="lz4", asbytes=True) for b in blks]
+        info = D.parse_lz4_frame_header(frames[0])
+        comps = [f[info.data_offset:] for f in frames]
+        todo.append(("lz4f", "val", D.LZ4_FRAME_BCS if info.block_checksum else D.LZ4_FRAME,
+                     blks, comps, a.arrow))
+    for codec, dname, cid, blks, comps, n in todo:
             blk = blks[0]
             assert all(len(b) == len(blk) for b in blks)
-            comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in blks]
-            n = a.streams
             K = len(comps)
             offs = np.cumsum([0] + [len(c) for c in comps])
             one = b"".join(comps)
@@ -74,7 +93,12 @@ def main(argv=None) -> int:
             status = torch.empty(n, dtype=torch.int32, device=dev)
             times = {k: [] for k in libs}
 
-            def run(lib):
+            def run(lg):
+                lib, g = lg
+                if g:
+                    os.environ["STROM_DECOMP_G"] = g
+                else:
+                    os.environ.pop("STROM_DECOMP_G", None)
                 rc = lib.strom_decompress(cid, src.data_ptr(), dst.data_ptr(), d_desc.data_ptr(),
                                           n, status.data_ptr(), None)
                 assert rc == 0, rc
@@ -102,7 +126,8 @@ def main(argv=None) -> int:
             res[f"{codec}_{dname}"] = row
             print(f"{codec}_{dname}", json.dumps(row), file=sys.stderr, flush=True)
             del src, dst
-    js = json.dumps({"GBps": res, "streams": a.streams, "rounds": a.rounds, "distinct": a.distinct})
+    js = json.dumps({"GBps": res, "streams": a.streams, "rounds": a.rounds, "distinct": a.distinct,
+                     "arrow_streams": a.arrow})
     if a.out:
         with open(a.out, "w") as f:
             f.write(js)

@@ -98,7 +98,10 @@ def _payloads():
     far = r1 + r2 + r1[:5000] + r2[3000:9000] + r1
     r3 = rng.integers(0, 256, 9000, dtype=np.uint8).tobytes()
     far_overlap = r3 * 5
-    return [text, runs, rand, ints, b"x", b"", bytes(200000), far, far_overlap]
+    # the config-5 column: int64 uniform in [0, 1e6) — short matches, a
+    # quarter of them past 2 KiB (far matches taken in the fast step)
+    uni = rng.integers(0, 1_000_000, 40000).astype(np.int64).tobytes()
+    return [text, runs, rand, ints, b"x", b"", bytes(200000), far, far_overlap, uni]
 
 
 def _run(codec, streams, sizes, dev):
@@ -127,13 +130,14 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("g", [1, 2, 4, 6, 8, 16, 32, 64])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant (STROM_DECOMP_G) decodes the same
     payloads: the fast LZ4 step's pass width differs per geometry (a
     length-15 match nibble must still take the extended-length path);
-    64 = the wave-per-stream batched decoder (decompress_wave.hip)."""
+    2 / 6 = the large-ring few-stream geometries; 64 = the wave-per-stream
+    batched decoder (decompress_wave.hip)."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
     monkeypatch.setenv("STROM_DECOMP_G", str(g))
