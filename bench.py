@@ -106,6 +106,19 @@ def main() -> int:
     F = int(a.file_gib * (1 << 30)) // W * W
     F = max(F, W)
     path = os.path.join(a.dir, f"shard_r{rank}.bin")
+    # every rank of the node writes its shard to the same directory: size the
+    # shards to 80 % of the free space (same size on every rank: MIN over
+    # ranks, taken before anyone writes), never below one window
+    import shutil
+    have = os.path.getsize(path) if os.path.exists(path) else 0
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    cap = int((shutil.disk_usage(a.dir).free + have) * 0.8) // max(1, local_world) // W * W
+    if world > 1:
+        t = torch.tensor([min(F, max(cap, W))], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        F = int(t.item())
+    else:
+        F = min(F, max(cap, W))
     t0 = time.time()
     make_shard(path, F, 1234 + rank)
     # reader pool per rank: split only among ranks that share this shard's

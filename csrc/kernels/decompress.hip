@@ -85,6 +85,9 @@ struct Stream {
   static constexpr uint32_t kMask = kRing - 1;
   static constexpr uint32_t kInW = INW_;
   static constexpr uint32_t kDummy = 16;     // sink for masked-off fast-path stores
+  // far matches in the fast step: on for the few-stream geometries (config-5
+  // frames 2x); with 16 streams per wave the extra predicate cost text -5 %
+  static constexpr bool kFarFast = G <= 4;
   static constexpr uint32_t kSlot = kRing + kInW + kDummy;   // LDS bytes per stream
   // input prefetch: the next window, kPfN 16-byte loads per lane, starts
   // kSlide bytes past the current one (the overlap covers reads that
@@ -473,7 +476,8 @@ struct Stream {
     // lies below vis (already stored and fenced: read back from HBM)
     const bool far = off > kRing - W;
     ok = ok & (lit != 15) & ((ml != 15) | (xb != 255)) & (mlen <= 2 * W) & (off != 0) &
-         (off <= op + lit) & (!far | (op + lit + mlen <= vis + off)) & (lit + mlen <= ocap - op);
+         (off <= op + lit) & (!far | (kFarFast & (op + lit + mlen <= vis + off))) &
+         (lit + mlen <= ocap - op);
     if (!ok) return false;
     {
       uint8_t *sink = inw + kInW;
@@ -484,7 +488,7 @@ struct Stream {
         *dd = (uint8_t)(lv >> (8 * j));
       }
     }
-    fast_copy(op + lit, off, mlen, far);
+    fast_copy(op + lit, off, mlen, kFarFast && far);
     ip += 3 + lit + (ml == 15);
     op += lit + mlen;
     return true;                 // flush pacing: the kernel loop's exception test
