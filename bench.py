@@ -82,6 +82,9 @@ def main() -> int:
     ap.add_argument("--fanout", choices=["allgather", "none"], default="allgather")
     ap.add_argument("--dir", default=os.environ.get("STROM_BENCH_DIR", "/tmp/strom_bench"))
     ap.add_argument("--keep", action="store_true", help="keep shard files")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group backend (nccl = RCCL; gloo only to rehearse the "
+                         "multi-rank path with several ranks on one GPU, --fanout none)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -91,10 +94,16 @@ def main() -> int:
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # ranks beyond the visible GPUs share them (multi-rank rehearsal on a
+    # one-GPU box; device_count() does not initialise the GPU)
+    local_dev = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     import nvme_strom_amd as S
     from nvme_strom_amd.models.ssd2gpu_stream import StreamLoader, vfs_control
@@ -124,7 +133,7 @@ def main() -> int:
     # reader pool per rank: split only among ranks that share this shard's
     # backing device (placement.plan_io all-gathers the device identities)
     from nvme_strom_amd.parallel.placement import plan_io
-    placement = plan_io(path, device=local)
+    placement = plan_io(path, device=local_dev)
     _log(rank, f"placement {placement}")
     fd = os.open(path, os.O_RDONLY)
     S.evict_file(fd)
@@ -275,7 +284,7 @@ def main() -> int:
     p50, p99, p50_py, vfs_avg, ver = vals.tolist()
     vfs_total = vfs_avg * world
     hist = S.stat_hist()
-    ing = S.ingest_info(local)
+    ing = S.ingest_info(local_dev)
     steps_bytes = (a.warmup + a.steps) * W
     out = {
         "metric": METRIC,
