@@ -250,8 +250,12 @@ __global__ __launch_bounds__(1024) void crc32c_chunks_kernel(const uint8_t *__re
 }
 
 // Fold per-chunk CRCs: one workgroup of 1024 threads; each thread folds a
-// contiguous run (Horner with a fixed shift), then a log-depth tree with
-// length-dependent shifts.
+// contiguous run (Horner with a fixed shift), then a log-depth tree.  A
+// right subtree at level s holds s*per full chunks except the one with the
+// buffer's tail, so its shift x^(8*chunk*per*s) is the previous level's
+// squared (one GF(2) multiply per level, every thread alike); only the node
+// whose right side holds the tail pays xpow8n (was: xpow8n at every node
+// and level, ~40 % of crc32c() on 1 GiB).
 __global__ __launch_bounds__(1024) void crc32c_combine_kernel(const uint32_t *__restrict__ crcs,
                                                               uint32_t nchunks, uint32_t chunk,
                                                               uint64_t nbytes,
@@ -273,15 +277,19 @@ __global__ __launch_bounds__(1024) void crc32c_combine_kernel(const uint32_t *__
   sc[t] = acc;
   sl[t] = len;
   __syncthreads();
+  const uint64_t full1 = (uint64_t)per * chunk;    // bytes of a full level-1 right side
+  uint32_t ks = xpow8n(full1);                     // x^(8 * full1 * s) at level s
   for (uint32_t stride = 1; stride < 1024; stride <<= 1) {
     uint32_t c2 = 0;
     uint64_t l2 = 0;
     bool active = (t % (2 * stride)) == 0 && t + stride < 1024;
     if (active) {
       uint64_t lr = sl[t + stride];
-      c2 = (lr ? multmodp(xpow8n(lr), sc[t]) : sc[t]) ^ sc[t + stride];
+      const uint32_t k = lr == full1 * stride ? ks : xpow8n(lr);
+      c2 = (lr ? multmodp(k, sc[t]) : sc[t]) ^ sc[t + stride];
       l2 = sl[t] + lr;
     }
+    ks = multmodp(ks, ks);
     __syncthreads();
     if (active) {
       sc[t] = c2;
