@@ -249,55 +249,56 @@ __global__ __launch_bounds__(1024) void crc32c_chunks_kernel(const uint8_t *__re
   }
 }
 
-// Fold per-chunk CRCs: one workgroup of 1024 threads; each thread folds a
-// contiguous run (Horner with a fixed shift), then a log-depth tree.  A
-// right subtree at level s holds s*per full chunks except the one with the
-// buffer's tail, so its shift x^(8*chunk*per*s) is the previous level's
-// squared (one GF(2) multiply per level, every thread alike); only the node
-// whose right side holds the tail pays xpow8n (was: xpow8n at every node
-// and level, ~40 % of crc32c() on 1 GiB).
+// Fold per-chunk CRCs: one workgroup of 1024 threads.  Each thread folds a
+// contiguous run of chunks (Horner; the fixed per-chunk shift as 4 byte
+// lookups, one table entry built per thread), then shifts its run's CRC
+// past every byte after the run, x^(8 * bytes after) — independent per
+// thread, no serial tree of shifts — and the runs are xor-reduced
+// (crc(A|B) = shift(crc(A), |B|) ^ crc(B), zlib's crc32_combine algebra).
 __global__ __launch_bounds__(1024) void crc32c_combine_kernel(const uint32_t *__restrict__ crcs,
                                                               uint32_t nchunks, uint32_t chunk,
                                                               uint64_t nbytes,
                                                               uint32_t *__restrict__ out) {
-  __shared__ uint32_t sc[1024];
-  __shared__ uint64_t sl[1024];
+  __shared__ uint32_t xk[4][256];      // xk[j][v] = (v << 8j) * x^(8 chunk) mod P
+  __shared__ uint32_t part[16];
   const uint32_t t = threadIdx.x;
   const uint32_t per = (nchunks + 1023) / 1024;
   const uint32_t lo = min(nchunks, t * per), hi = min(nchunks, lo + per);
-  const uint32_t kchunk = xpow8n(chunk);
-  uint32_t acc = 0;
-  uint64_t len = 0;
-  for (uint32_t i = lo; i < hi; ++i) {
-    uint64_t li = min<uint64_t>(chunk, nbytes - (uint64_t)i * chunk);
-    uint32_t k = li == chunk ? kchunk : xpow8n(li);
-    acc = (len ? multmodp(k, acc) : 0u) ^ crcs[i];
-    len += li;
-  }
-  sc[t] = acc;
-  sl[t] = len;
+  xk[t >> 8][t & 255] = multmodp(xpow8n(chunk), (t & 255) << (8 * (t >> 8)));
   __syncthreads();
-  const uint64_t full1 = (uint64_t)per * chunk;    // bytes of a full level-1 right side
-  uint32_t ks = xpow8n(full1);                     // x^(8 * full1 * s) at level s
-  for (uint32_t stride = 1; stride < 1024; stride <<= 1) {
-    uint32_t c2 = 0;
-    uint64_t l2 = 0;
-    bool active = (t % (2 * stride)) == 0 && t + stride < 1024;
-    if (active) {
-      uint64_t lr = sl[t + stride];
-      const uint32_t k = lr == full1 * stride ? ks : xpow8n(lr);
-      c2 = (lr ? multmodp(k, sc[t]) : sc[t]) ^ sc[t + stride];
-      l2 = sl[t] + lr;
-    }
-    ks = multmodp(ks, ks);
-    __syncthreads();
-    if (active) {
-      sc[t] = c2;
-      sl[t] = l2;
-    }
-    __syncthreads();
+  uint32_t acc = 0;
+  // full chunks 8 at a time with their CRC loads in flight together (one
+  // dependent load per chunk was most of this kernel's time)
+  const uint32_t full_hi = min<uint64_t>(hi, nbytes / chunk);   // chunks before a partial tail
+  uint32_t i = lo;
+  for (; i + 8 <= full_hi; i += 8) {
+    uint32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = crcs[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      acc = (xk[0][acc & 255] ^ xk[1][(acc >> 8) & 255] ^ xk[2][(acc >> 16) & 255] ^
+             xk[3][acc >> 24]) ^ c[k];
   }
-  if (t == 0) out[0] = sc[0];
+  for (; i < hi; ++i) {
+    const uint64_t li = min<uint64_t>(chunk, nbytes - (uint64_t)i * chunk);
+    const uint32_t sh = li == chunk ? xk[0][acc & 255] ^ xk[1][(acc >> 8) & 255] ^
+                                          xk[2][(acc >> 16) & 255] ^ xk[3][acc >> 24]
+                                    : multmodp(xpow8n(li), acc);
+    acc = sh ^ crcs[i];
+  }
+  if (hi > lo) {
+    const uint64_t after = nbytes - min<uint64_t>(nbytes, (uint64_t)hi * chunk);
+    if (after) acc = multmodp(xpow8n(after), acc);
+  }
+  acc = wave_xor(acc);
+  if ((t & 63) == 0) part[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < (blockDim.x >> 6); ++k) r ^= part[k];
+    out[0] = r;
+  }
 }
 
 }  // namespace
