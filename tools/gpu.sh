@@ -19,6 +19,7 @@
 #   decpmc     two PMC passes (issue / wait / LDS / memory instruction mix)
 #              over the LZ4 decoder build DECLIB (default lib/ab/base.so)
 #   arrow      config-5 Arrow scan bench (tools.arrow_bench)
+#   stripe     config-3 proxy: 4-member stripe set vs one file (tools.stripe_bench)
 # Output lands in gpurun_out/TAG/.
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -63,6 +64,7 @@ for phase in "$@"; do
                 -- python3 -m nvme_strom_amd.tools.decomp_ab "$ROOT/${DECLIB:-nvme_strom_amd/lib/ab/base.so}" \
                    --rounds 1 --cases "${DECCASES:-lz4_words,lz4_ints}") || exit 1
             done ;;
+    stripe) step stripe 400 python -u -m nvme_strom_amd.tools.stripe_bench --out "$OUT/stripe.json" ;;
     arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
