@@ -1,0 +1,31 @@
+"""CPU tests of the measurement tools' pure parts (no GPU)."""
+import csv
+
+from nvme_strom_amd.tools import ktrace_summary as K
+
+
+def test_ktrace_summary_groups_and_rates(tmp_path, capsys):
+    path = tmp_path / "tr_kernel_trace.csv"
+    rows = [
+        ("void (anonymous namespace)::decompress_kernel<(anonymous namespace)::Stream<4u, 2048u, 448u>,"
+         " false>(int, unsigned char const*)", 0, 2000),
+        ("void (anonymous namespace)::decompress_kernel<(anonymous namespace)::Stream<4u, 2048u, 448u>,"
+         " false>(int, unsigned char const*)", 5000, 9000),
+        ("(anonymous namespace)::crc32c_chunks_kernel(unsigned char const*, unsigned long)", 0, 250000),
+        ("(anonymous namespace)::crc32c_chunks_kernel(unsigned char const*, unsigned long)", 0, 200000),
+        ("(anonymous namespace)::crc32c_chunks_kernel(unsigned char const*, unsigned long)", 0, 300000),
+    ]
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        for r in rows:
+            w.writerow(r)
+    md = tmp_path / "out.md"
+    assert K.main([str(path), "--bytes", "crc32c_chunks=1000000000", "--md", str(md)]) == 0
+    text = md.read_text()
+    # template arguments kept, parameter lists and namespaces dropped
+    assert "`decompress_kernel<Stream<4u, 2048u, 448u>, false>` | 2 | 3.0 | 2.0 |" in text
+    # median 250 us over 1 GB -> 4.00 TB/s
+    assert "`crc32c_chunks_kernel` | 3 | 250.0 | 200.0 | 4.00 |" in text
+    # the heavier kernel (total time) is listed first
+    assert text.index("crc32c_chunks_kernel") < text.index("decompress_kernel")
