@@ -58,6 +58,7 @@ int Config::set(const std::string &k, const std::string &v) {
     if (v == "psync") backend = BackendKind::kPsync;
     else if (v == "uring") backend = BackendKind::kUring;
     else if (v == "fake") backend = BackendKind::kFake;
+    else if (v == "cache") backend = BackendKind::kCache;
     else return -EINVAL;
     return 0;
   }
@@ -111,7 +112,10 @@ int Config::set(const std::string &k, const std::string &v) {
 int Config::get(const std::string &k, std::string *out) const {
   char buf[64];
   if (k == "backend") {
-    *out = backend == BackendKind::kPsync ? "psync" : backend == BackendKind::kUring ? "uring" : "fake";
+    *out = backend == BackendKind::kPsync   ? "psync"
+           : backend == BackendKind::kUring ? "uring"
+           : backend == BackendKind::kCache ? "cache"
+                                            : "fake";
     return 0;
   }
   long v;

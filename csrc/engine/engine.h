@@ -39,7 +39,9 @@
 namespace strom {
 
 // ------------------------------------------------------------------ config
-enum class BackendKind { kPsync, kUring, kFake };
+// kCache: the uring path on the buffered descriptor (page-cache reads):
+// the engine + HBM ingest ceiling with the storage taken out (tools.ceiling)
+enum class BackendKind { kPsync, kUring, kFake, kCache };
 
 struct Config {
   // defaults from the MI355X-host sweep (nvme_strom_amd/tools/tune.py)

@@ -535,7 +535,7 @@ struct IoEngine::Worker {
         sqe = ring.next_sqe();
       }
       sqe->opcode = IORING_OP_READ;
-      sqe->fd = r.fd;
+      sqe->fd = read_fd(r);
       sqe->addr = (uint64_t)dst;
       sqe->len = len;
       sqe->off = r.off;
@@ -543,10 +543,13 @@ struct IoEngine::Worker {
       ++reads_inflight;
       return true;
     }
-    long got = pread_full(r.fd, dst, len, r.off);
+    long got = pread_full(read_fd(r), dst, len, r.off);
     on_read_done(c, got);
     flush_staged();
     return true;
+  }
+  int read_fd(const IoReq &r) const {
+    return cfg.backend == BackendKind::kCache && r.fd_buffered >= 0 ? r.fd_buffered : r.fd;
   }
 
   void reap() {
@@ -559,7 +562,7 @@ struct IoEngine::Worker {
       long got = cqe.res;
       if (got >= 0 && (uint32_t)got < c.len) {
         // partial completion: finish the remainder synchronously
-        long more = pread_full(c.req.fd, c.dst + got, c.len - (uint32_t)got, c.req.off + got);
+        long more = pread_full(read_fd(c.req), c.dst + got, c.len - (uint32_t)got, c.req.off + got);
         got = more < 0 ? more : got + more;
       }
       on_read_done(c, got);
@@ -570,7 +573,7 @@ struct IoEngine::Worker {
   void run() {
     bind_numa();
     const bool fake = cfg.backend == BackendKind::kFake;
-    bool use_ring = cfg.backend == BackendKind::kUring;
+    bool use_ring = cfg.backend == BackendKind::kUring || cfg.backend == BackendKind::kCache;
     const int qd_cfg = std::max(cfg.queue_depth, nslots());
     if (use_ring && ring.init((unsigned)std::max(8, qd_cfg * 2)) != 0) use_ring = false;
     int qd = use_ring || fake ? qd_cfg : 1;
@@ -719,7 +722,8 @@ void IoEngine::run_inline(IoReq &r) {
     c.buf = b;  // the old buffer (if any) is leaked on purpose: it is small
     c.cap = cap;
   }
-  long got = frc ? frc : pread_full(r.fd, c.buf, len, r.off);
+  const int rfd = config().backend == BackendKind::kCache && r.fd_buffered >= 0 ? r.fd_buffered : r.fd;
+  long got = frc ? frc : pread_full(rfd, c.buf, len, r.off);
   uint64_t t1 = mono_ns();
   if (tl_phase) tl_phase[3] = t1;
   stats().io_ns.add(t1 - t0);

@@ -34,9 +34,12 @@ def _chunks(data, ids, chunk=CH, relseg=0):
     return np.concatenate(out)
 
 
-@pytest.mark.parametrize("backend", ["uring", "psync"])
+@pytest.mark.parametrize("backend", ["uring", "psync", "cache"])
 def test_ssd2ram_identity_and_permutation(strom, rand_file, backend):
-    strom.configure(backend=backend)
+    # cache: worker reads through the buffered descriptor (the engine-ceiling
+    # mode of tools/ceiling_bench.py), the page-cache probe off
+    strom.configure(backend=backend, pgcache_probe=int(backend != "cache"))
+    assert strom.config_get("backend") == backend
     path, data = rand_file(64 * CH)
     fd = _open(path)
     try:
