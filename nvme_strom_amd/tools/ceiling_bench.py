@@ -91,6 +91,14 @@ def main(argv=None) -> int:
                 while f.read(64 << 20):
                     pass
             res["runs"][f"cache_w{w}"] = stream("cache")
+        # QD1 4 KiB reads into HBM with the storage taken out: the engine's
+        # own latency (lookup, staging, BAR store + flush, completion)
+        S.configure(backend="cache", pgcache_probe=0, workers=4)
+        offs = np.random.default_rng(1).integers(0, F // 4096, size=1050) * 4096
+        lat = S.pread_gpu_latency(buf.handle, 0, fd, offs)[50:] / 1e3
+        res["p50_4k_lat_cache_us"] = round(float(np.percentile(lat, 50)), 2)
+        res["p99_4k_lat_cache_us"] = round(float(np.percentile(lat, 99)), 2)
+        _log("4 KiB QD1 from the page cache: p50 %.2f us" % res["p50_4k_lat_cache_us"])
         S.configure(backend="uring", pgcache_probe=1, workers=4)
         res["runs"]["odirect_w4"] = stream("odirect")
     finally:
