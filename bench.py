@@ -51,6 +51,14 @@ def make_shard(path: str, nbytes: int, seed: int) -> None:
     os.replace(path + ".tmp", path)
 
 
+def shard_bytes(want: int, window: int, free: int, have: int, local_world: int) -> int:
+    """Shard size per rank: ``want`` capped at 80 % of the directory's free
+    space (plus this rank's existing shard) split over the node's ranks, in
+    whole windows, never below one window."""
+    cap = int((free + have) * 0.8) // max(1, local_world) // window * window
+    return min(want, max(cap, window))
+
+
 def fs_type(path: str) -> str:
     """Filesystem type of the mount holding ``path`` (longest mountinfo prefix)."""
     best, typ = "", "unknown"
@@ -121,13 +129,11 @@ def main() -> int:
     import shutil
     have = os.path.getsize(path) if os.path.exists(path) else 0
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
-    cap = int((shutil.disk_usage(a.dir).free + have) * 0.8) // max(1, local_world) // W * W
+    F = shard_bytes(F, W, shutil.disk_usage(a.dir).free, have, local_world)
     if world > 1:
-        t = torch.tensor([min(F, max(cap, W))], dtype=torch.int64, device=dev)
+        t = torch.tensor([F], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         F = int(t.item())
-    else:
-        F = min(F, max(cap, W))
     t0 = time.time()
     make_shard(path, F, 1234 + rank)
     # reader pool per rank: split only among ranks that share this shard's

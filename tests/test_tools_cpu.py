@@ -29,3 +29,18 @@ def test_ktrace_summary_groups_and_rates(tmp_path, capsys):
     assert "`crc32c_chunks_kernel` | 3 | 250.0 | 200.0 | 4.00 |" in text
     # the heavier kernel (total time) is listed first
     assert text.index("crc32c_chunks_kernel") < text.index("decompress_kernel")
+
+
+def test_bench_shard_sizing():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_mod", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    G = 1 << 30
+    assert b.shard_bytes(4 * G, G, 100 * G, 0, 1) == 4 * G          # plenty of room
+    assert b.shard_bytes(4 * G, G, 20 * G, 0, 8) == 2 * G           # 16 GiB over 8 ranks
+    assert b.shard_bytes(4 * G, G, 20 * G, 4 * G, 8) == 2 * G       # own old shard counts
+    assert b.shard_bytes(4 * G, G, 1 * G, 0, 8) == G                # never below a window
+    assert b.shard_bytes(4 * G, G, int(9.9 * G), 0, 2) == 3 * G     # whole windows
