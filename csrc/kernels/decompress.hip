@@ -821,6 +821,7 @@ using S1 = Stream<64, 2048, 1024>;    // 1 stream per wave, 3 KiB
 // 5 % past 16 KiB
 using S2L = Stream<32, 16384, 512>;   // 2 streams per wave, 33 KiB
 using S4L = Stream<16, 8192, 512>;    // 4 streams per wave, 35 KiB
+using S1L = Stream<64, 16384, 1024>;  // 1 stream per wave, 17 KiB (2 waves per SIMD)
 
 template <class S>
 int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d_desc,
@@ -845,9 +846,9 @@ extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
 
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
-// STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring; 2 / 6 = 2 / 4
-// streams per wave with 16 / 8 KiB rings; 64 = wave per stream) forces a
-// geometry (A/B runs).
+// STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring; 3 / 2 / 6 = 1 /
+// 2 / 4 streams per wave with 16 / 16 / 8 KiB rings; 64 = wave per stream)
+// forces a geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
@@ -860,16 +861,19 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // streams leave SIMDs idle whatever the geometry, so they get fewer
   // streams per wave and larger history rings (far matches — HBM reads —
   // stay rare); from ~16k streams 16 per wave wins (VALU per stream).
+  //   <= 1,024: 1 per wave, 16 KiB ring (every SIMD busy: +7-12 % over 2/wave)
   //   <= 2,048: 2 per wave, 16 KiB rings (config-5 frames 14.6 -> 27.5 GB/s)
   //   <= 4,096: 4 per wave, 8 KiB rings;  <= 8,192: 4 per wave, 2 KiB rings
-  if (!e) g = nblocks <= 2048 ? 2 : nblocks <= 4096 ? 6 : nblocks <= 8192 ? 4 : 16;
+  if (!e)
+    g = nblocks <= 1024 ? 3 : nblocks <= 2048 ? 2 : nblocks <= 4096 ? 6 : nblocks <= 8192 ? 4 : 16;
   // wave per stream (decompress_wave.hip): forced only; the large-ring lane
   // groups measured as fast or faster at every count
   if (g == 64) return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
-  if (g != 1 && g != 2 && g != 4 && g != 6 && g != 8 && g != 16 && g != 32) g = 16;
+  if (g != 1 && g != 2 && g != 3 && g != 4 && g != 6 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 2) return launch<S2L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 6) return launch<S4L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
+  if (g == 3) return launch<S1L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 16) return launch<S16>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 32) return launch<S16s>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
   if (g == 8) return launch<S8>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);

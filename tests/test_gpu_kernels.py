@@ -130,13 +130,13 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 2, 4, 6, 8, 16, 32, 64])
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, 64])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant (STROM_DECOMP_G) decodes the same
     payloads: the fast LZ4 step's pass width differs per geometry (a
     length-15 match nibble must still take the extended-length path);
-    2 / 6 = the large-ring few-stream geometries; 64 = the wave-per-stream
+    3 / 2 / 6 = the large-ring few-stream geometries; 64 = the wave-per-stream
     batched decoder (decompress_wave.hip)."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
