@@ -868,7 +868,8 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
     g = nblocks <= 1024 ? 3 : nblocks <= 2048 ? 2 : nblocks <= 4096 ? 6 : nblocks <= 8192 ? 4 : 16;
   // wave per stream (decompress_wave.hip): forced only; the large-ring lane
   // groups measured as fast or faster at every count
-  if (g == 64) return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+  if (g == 64 || g == 65)
+    return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   if (g != 1 && g != 2 && g != 3 && g != 4 && g != 6 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 2) return launch<S2L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "strom/strom.h"
 
@@ -83,6 +84,7 @@ struct WaveStream {
   uint8_t *ring;
   uint8_t *inw;
   uint8_t *sink;       // per-lane target of masked-off byte stores
+  uint32_t *pv;        // resolve batches: per output byte a value or a source
   uint32_t lane;
   uint32_t iend, ocap, ip, op, bend, win, flushed, fenced, omis, olen, bcs, fhdr, mode;
   int32_t err;
@@ -529,6 +531,122 @@ struct WaveStream {
     return true;
   }
 
+  // ---- resolve batch (LZ4, STROM_DECOMP_G=65): a lean scalar parse of up
+  // to 64 sequences, then every output byte of the batch is resolved at once
+  // — literal bytes carry their value, match byte x points at x - off — by
+  // pointer doubling (pv[x] = pv[pv[x]], lane-parallel) until each entry is
+  // a value or history before the batch (ring, or HBM past the ring).  No
+  // match is copied sequence by sequence.
+  static constexpr uint32_t kRB = 1024;         // output bytes per resolve batch
+  // pv entry: bits 31:30 = 01 a byte value, 00 a source inside the batch,
+  // 11 a (negative) source before it; sources stay within +-2^29
+  static constexpr uint32_t kVal = 0x40000000u;
+  __device__ bool batch_res() {
+    if (!in_window(ip, kInW / 2)) refill(ip);
+    uint32_t A = 0, B = 0, C = 0;
+    uint32_t nb = 0, bout = 0, maxshort = 0;
+    uint64_t longmask = 0;
+    uint32_t p = ip;
+    while (nb < kNB && p < bend && in_window(p, 24)) {
+      const uint32_t o = p - win;
+      const uint32_t *d = (const uint32_t *)(inw + (o & ~3u));
+      const uint32_t x0 = rfl(d[0]), x1 = rfl(d[1]), x2 = rfl(d[2]), x3 = rfl(d[3]), x4 = rfl(d[4]);
+      const uint32_t sh = 8 * (o & 3);
+      const uint32_t w0 = (uint32_t)((((uint64_t)x1 << 32) | x0) >> sh);
+      const uint32_t w1 = (uint32_t)((((uint64_t)x2 << 32) | x1) >> sh);
+      const uint32_t w2 = (uint32_t)((((uint64_t)x3 << 32) | x2) >> sh);
+      const uint32_t w3 = (uint32_t)((((uint64_t)x4 << 32) | x3) >> sh);
+      const uint32_t lit = (w0 >> 4) & 15, ml = w0 & 15;
+      const uint32_t e = p + 1 + lit;
+      const uint32_t r = 1 + lit, sel = r >> 2;
+      const uint32_t lo = sel == 0 ? w0 : sel == 1 ? w1 : sel == 2 ? w2 : w3;
+      const uint32_t hi = sel == 0 ? w1 : sel == 1 ? w2 : w3;
+      const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (r & 3)));
+      const uint32_t off = v & 0xffff, xb = (v >> 16) & 0xff;
+      const bool last = e == bend;
+      const uint32_t m = last ? 0u : (ml == 15 ? 19 + xb : ml + 4);
+      const uint32_t oa = op + bout;
+      const bool ok = (lit <= 12) & (e <= bend) & (last | (bend - e >= 3)) &
+                      (last | (ml != 15) | (xb != 255)) &
+                      (last | ((off != 0) & (off <= oa + lit))) & (lit + m <= ocap - oa) &
+                      (lit + m <= kRB - bout);
+      if (!ok) break;
+      A = wrl(p + 1, nb, A, lane);
+      B = wrl(bout | lit << 16, nb, B, lane);
+      C = wrl(off | m << 16, nb, C, lane);
+      const uint32_t n = lit + m;
+      if (n > 32) longmask |= 1ull << nb;
+      else if (n > maxshort) maxshort = n;
+      bout += n;
+      ++nb;
+      p = last ? e : e + 2 + (ml == 15);
+      if (last) break;
+    }
+    if (nb == 0) return false;
+    const uint32_t rel = B & 0xffff, lit = B >> 16, off = C & 0xffff, m = C >> 16;
+    const uint32_t n = lane < nb ? lit + m : 0u;
+    // (1) fill: lane j writes record j (<= 32 bytes); longer records by the wave
+    {
+      const uint32_t my = n <= 32 ? n : 0u;
+      for (uint32_t k = 0; k < maxshort; ++k) {
+        if (k < my) {
+          uint32_t val;
+          if (k < lit) val = kVal | inw[A + k - win];
+          else val = (uint32_t)((int32_t)(rel + k) - (int32_t)off);
+          pv[rel + k] = val;
+        }
+      }
+      for (uint64_t mk = longmask; mk; mk &= mk - 1) {
+        const uint32_t j = __builtin_ctzll(mk);
+        const uint32_t ja = rdl(A, j), jb = rdl(B, j), jc = rdl(C, j);
+        const uint32_t jr = jb & 0xffff, jl = jb >> 16, jo = jc & 0xffff, jn = jl + (jc >> 16);
+        for (uint32_t k = lane; k < jn; k += 64)
+          pv[jr + k] = k < jl ? kVal | inw[ja + k - win] : (uint32_t)((int32_t)(jr + k) - (int32_t)jo);
+      }
+    }
+    // (2) pointer doubling until every entry is a value or history (< 0)
+    for (;;) {
+      bool ch = false;
+      for (uint32_t x = lane; x < bout; x += 64) {
+        const uint32_t q = pv[x];
+        if ((q >> 30) == 0) {
+          pv[x] = pv[q];
+          ch = true;
+        }
+      }
+      if (!__any(ch)) break;
+    }
+    // (3) bytes into the ring; history from the ring, or HBM past it (a
+    // resolved chain can end farther back than any single offset)
+    bool need = false;
+    for (uint32_t x = lane; x < bout; x += 64) {
+      const uint32_t q = pv[x];
+      need |= (q >> 30) == 3 && (uint32_t)(-(int32_t)q) > kNear;
+    }
+    if (__any(need)) far_ready(op);
+    for (uint32_t x = lane; x < bout; x += 64) {
+      const uint32_t q = pv[x];
+      uint32_t byte;
+      if ((q >> 30) == 1) {
+        byte = q & 0xff;
+      } else {
+        const uint32_t h = op + (int32_t)q;     // absolute output position < op
+        if (op - h <= kNear) {
+          byte = ring[(h + omis) & kRMask];
+        } else {
+          const uintptr_t a = (uintptr_t)(out + h);
+          const uint32_t w = __hip_atomic_load((const uint32_t *)(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          byte = (w >> (8 * (a & 3))) & 0xff;
+        }
+      }
+      ring[(op + x + omis) & kRMask] = (uint8_t)byte;
+    }
+    op += bout;
+    ip = p;
+    return true;
+  }
+
   // one unit alone, window and ring paced (long runs, window edges, errors)
   template <bool kSnap>
   __device__ void single() {
@@ -619,7 +737,7 @@ struct WaveStream {
     }
   }
 
-  template <bool kSnap>
+  template <bool kSnap, bool kRes>
   __device__ void run(int codec) {
     while (!err && mode != kDone) {
       if (mode == kHdr) {
@@ -635,7 +753,7 @@ struct WaveStream {
         if (op != olen) err = kErrFormat;
         mode = kDone;
       } else {
-        if (!batch<kSnap>()) single<kSnap>();
+        if (!((kRes && !kSnap) ? batch_res() : batch<kSnap>())) single<kSnap>();
         flush(op, false);
       }
     }
@@ -644,17 +762,19 @@ struct WaveStream {
 };
 
 // one wave per workgroup; LDS (18.3 KiB) keeps 8 waves per CU
-template <bool kSnap>
+template <bool kSnap, bool kRes>
 __global__ __launch_bounds__(64) void decompress_wave_kernel(int codec, const uint8_t *__restrict__ src,
                                                              uint8_t *__restrict__ dst,
                                                              const strom_decomp_desc *__restrict__ desc,
                                                              uint32_t nblocks, int32_t *status) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRing + kInW + 16 + 256];
+  __shared__ __attribute__((aligned(16)))
+  uint8_t lds[kRing + kInW + 16 + 256 + (kRes ? 4 * WaveStream::kRB : 0)];
   WaveStream s;
   s.lane = threadIdx.x;
   s.ring = lds;
   s.inw = lds + kRing;
   s.sink = lds + kRing + kInW + 16;
+  s.pv = (uint32_t *)(lds + kRing + kInW + 16 + 256);
 #ifdef STROM_WAVE_PROF
   for (int i = 0; i < kWN; ++i) s.prof[i] = 0;
   const uint64_t t_all = __builtin_amdgcn_s_memtime();
@@ -679,7 +799,7 @@ __global__ __launch_bounds__(64) void decompress_wave_kernel(int codec, const ui
     s.fhdr = codec == STROM_CODEC_ARROW_LZ4;
     s.mode = kHdr;
     s.err = 0;
-    s.run<kSnap>(codec);
+    s.run<kSnap, kRes>(codec);
     if (s.lane == 0) status[b] = s.err ? s.err : (int32_t)s.op;
   }
 #ifdef STROM_WAVE_PROF
@@ -700,11 +820,16 @@ extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
   if (!nblocks) return 0;
   const uint32_t grid = nblocks < 65535 ? nblocks : 65535;
   hipStream_t st = (hipStream_t)stream;
+  const char *e = getenv("STROM_DECOMP_G");
+  const bool res = e && atoi(e) == 65;     // resolve batches (LZ4 family)
   if (codec == STROM_CODEC_SNAPPY)
-    hipLaunchKernelGGL(decompress_wave_kernel<true>, dim3(grid), dim3(64), 0, st, codec,
+    hipLaunchKernelGGL((decompress_wave_kernel<true, false>), dim3(grid), dim3(64), 0, st, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
+  else if (res)
+    hipLaunchKernelGGL((decompress_wave_kernel<false, true>), dim3(grid), dim3(64), 0, st, codec,
                        (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
   else
-    hipLaunchKernelGGL(decompress_wave_kernel<false>, dim3(grid), dim3(64), 0, st, codec,
+    hipLaunchKernelGGL((decompress_wave_kernel<false, false>), dim3(grid), dim3(64), 0, st, codec,
                        (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nblocks, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -130,14 +130,15 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, 64])
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, 64, 65])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant (STROM_DECOMP_G) decodes the same
     payloads: the fast LZ4 step's pass width differs per geometry (a
     length-15 match nibble must still take the extended-length path);
     3 / 2 / 6 = the large-ring few-stream geometries; 64 = the wave-per-stream
-    batched decoder (decompress_wave.hip)."""
+    batched decoder (decompress_wave.hip), 65 = the same with LZ4 matches
+    resolved by pointer doubling."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
     monkeypatch.setenv("STROM_DECOMP_G", str(g))
@@ -164,7 +165,7 @@ def test_snappy(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["auto", "64"])
+@pytest.mark.parametrize("g", ["auto", "64", "65"])
 def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     """pyarrow's 'lz4' codec = LZ4 frame with linked 64 KiB blocks: matches
     may reach into the previous block, which the LDS history ring covers."""
@@ -182,7 +183,7 @@ def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["auto", "64"])
+@pytest.mark.parametrize("g", ["auto", "64", "65"])
 def test_malformed_streams_report_errors(dev, monkeypatch, g):
     from nvme_strom_amd.ops import decompress as D
     if g != "auto":
