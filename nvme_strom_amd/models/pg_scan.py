@@ -318,6 +318,9 @@ class ScanResult:
     nr_dma_blocks: int = 0
     chunks: int = 0
     workers: int = 1
+    # per participant: (first block, item pointers) of every chunk, merged
+    # in block order by HeapRelationScan.run
+    chunk_items: list = field(default_factory=list, repr=False)
     # MVCC mode: blocks that took the checked (host) path, tuples it removed
     nr_checked: int = 0
     removed: int = 0
@@ -374,6 +377,42 @@ class HeapRelationScan:
         self.cfg.validate()
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.pred = dict(attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi)
+        # idle participant resources (session, HBM ring, readers, pinned
+        # write-back buffers), reused by later runs: allocating and pinning
+        # them per run cost more than the scan of a GiB-sized relation
+        self._pool: List[tuple] = []
+        self._pool_lock = threading.Lock()
+
+    def _acquire(self) -> tuple:
+        with self._pool_lock:
+            if self._pool:
+                return self._pool.pop()
+        cfg = self.cfg
+        per_chunk = cfg.chunk_size // BLCKSZ
+        nslots = cfg.buffer_size // cfg.chunk_size
+        sess = api.Session()
+        hb = HbmBuffer(cfg.buffer_size, self.device, sess=sess)
+        readers = [FileReader(p, BLCKSZ, self.rel.relseg_size, per_chunk, sess) for p in self.rel.segments]
+        wbs = [host_buffer(cfg.chunk_size) for _ in range(nslots)]
+        # checked-path pages (MVCC mode) are staged here, then copied to HBM
+        # right after the chunk's DMA blocks
+        cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if cfg.snapshot is not None else []
+        return sess, hb, readers, wbs, cpu_bufs
+
+    @staticmethod
+    def _free(rs: tuple) -> None:
+        sess, hb, readers, _, _ = rs
+        for r in readers:
+            r.close()
+        hb.close()
+        sess.close()
+
+    def close(self) -> None:
+        """Release the pooled participant resources."""
+        with self._pool_lock:
+            pool, self._pool = self._pool, []
+        for rs in pool:
+            self._free(rs)
 
     def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None,
             cursor=None) -> ScanResult:
@@ -399,7 +438,11 @@ class HeapRelationScan:
         [t.join() for t in ths]
         if errors:
             raise errors[0]
-        items = np.sort(np.concatenate([r.items for r in results])) if results else np.zeros(0, np.uint64)
+        # each chunk is a contiguous block range with its items in order:
+        # ordering the chunks by first block orders every item (no sort of
+        # the items themselves: that was most of a GiB-scale scan's host time)
+        chunks = sorted((c for r in results for c in r.chunk_items), key=lambda c: c[0])
+        items = np.concatenate([c[1] for c in chunks]) if chunks else np.zeros(0, np.uint64)
         out = ScanResult(items, seconds=time.perf_counter() - t0, workers=workers)
         out.merge(results)
         return out
@@ -409,15 +452,10 @@ class HeapRelationScan:
         mvcc = cfg.snapshot is not None
         per_chunk = cfg.chunk_size // BLCKSZ
         nslots = cfg.buffer_size // cfg.chunk_size
-        sess = api.Session()
-        hb = HbmBuffer(cfg.buffer_size, self.device, sess=sess)
-        readers = [FileReader(p, BLCKSZ, self.rel.relseg_size, per_chunk, sess) for p in self.rel.segments]
-        wbs = [host_buffer(cfg.chunk_size) for _ in range(nslots)]
-        # checked-path pages (MVCC mode) are staged here, then copied to HBM
-        # right after the chunk's DMA blocks
-        cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if mvcc else []
+        rs = self._acquire()
+        sess, hb, readers, wbs, cpu_bufs = rs
         ring: List[Optional[tuple]] = [None] * nslots
-        found: List[np.ndarray] = []
+        found: List[Tuple[int, np.ndarray]] = []    # (first block, item pointers)
         st = ScanResult(np.zeros(0, np.uint64))
         k = 0
         try:
@@ -451,12 +489,12 @@ class HeapRelationScan:
             for item in ring:
                 if item is not None:
                     self._consume(item, hb, readers, found, st)
-        finally:
-            for r in readers:
-                r.close()
-            hb.close()
-            sess.close()
-        st.items = np.concatenate(found) if found else np.zeros(0, np.uint64)
+        except BaseException:
+            self._free(rs)          # a failed participant's reads may still be in flight
+            raise
+        with self._pool_lock:
+            self._pool.append(rs)
+        st.chunk_items = found
         return st
 
     def _checked_pages(self, fd: int, blocks: np.ndarray, stage: torch.Tensor) -> int:
@@ -486,11 +524,17 @@ class HeapRelationScan:
         skip = self.cfg.skip_invisible and self.cfg.snapshot is None
         r = heap_scan(pages, BLCKSZ, verify_checksum=self.cfg.verify_checksum,
                       skip_invisible=skip, blknos=blk, **self.pred)
-        it = r.items[:r.count].cpu().numpy().view(np.uint32)
+        # the kernel reserves output per workgroup (arbitrary order across
+        # workgroups): sort the chunk's items on the GPU (page order) before
+        # the copy, so chunks only need ordering by their first block
+        it = torch.sort(r.items[:r.count].to(torch.int64) & 0xFFFFFFFF).values.cpu().numpy().astype(np.uint32)
         page_idx = (it >> 16).astype(np.int64)
         lineno = (it & 0xFFFF).astype(np.uint64)
         blocks = landed.astype(np.uint64)[page_idx]
-        found.append((blocks << np.uint64(16)) | lineno)
+        ptrs = (blocks << np.uint64(16)) | lineno
+        if n > 1 and bool((landed[1:] < landed[:-1]).any()):
+            ptrs = np.sort(ptrs)        # page-cache chunks landed at the tail
+        found.append((int(landed.min()) if n else 0, ptrs))
         status = r.page_status.cpu().numpy()
         st.pages += n
         st.bad_pages += int(((status & 3) != 0).sum())

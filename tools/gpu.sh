@@ -20,6 +20,7 @@
 #              over the LZ4 decoder build DECLIB (default lib/ab/base.so)
 #   arrow      config-5 Arrow scan bench (tools.arrow_bench)
 #   ceiling    engine + ingest ceiling: page-cache reads (backend=cache) vs O_DIRECT
+#   pg         end-to-end PostgreSQL heap scan (GPU ring vs the reference-shaped CPU scan)
 #   stripe     config-3 proxy: 4-member stripe set vs one file (tools.stripe_bench)
 # Output lands in gpurun_out/TAG/.
 set -o pipefail
@@ -65,6 +66,7 @@ for phase in "$@"; do
                 -- python3 -m nvme_strom_amd.tools.decomp_ab "$ROOT/${DECLIB:-nvme_strom_amd/lib/ab/base.so}" \
                    --rounds 1 --cases "${DECCASES:-lz4_words,lz4_ints}") || exit 1
             done ;;
+    pg) step pg 400 python -u -m nvme_strom_amd.tools.pg_bench --out "$OUT/pg.json" ;;
     stripe) step stripe 400 python -u -m nvme_strom_amd.tools.stripe_bench --out "$OUT/stripe.json" ;;
     ceiling) step ceiling 400 python -u -m nvme_strom_amd.tools.ceiling_bench --out "$OUT/ceiling.json" ;;
     arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
