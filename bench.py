@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """Headline benchmark: SSD→GPU read GiB/s + p50 4 KiB IOP latency.
 
-One process per GPU (torchrun for N>1, RCCL over xGMI).  Each rank owns a
+One process per GPU (torchrun for N>1, RCCL over xGMI; ``--gpus N`` run
+outside torchrun starts a child torchrun with N ranks and relays rank 0's
+line, so ``n_gpus`` is always the number of ranks that ran).  Each rank owns a
 synthetic random-byte shard file; a *step* loads a ``--window-mib`` window of
 its shard into a resident HBM buffer through the engine (MEMCPY_SSD2GPU,
 nvme_test methodology: 32 MiB segments of 8 KiB chunks, 6 segments in
 flight — reference utils/nvme_test.c:40-41, 301-302, 383-498).  With N>1 the
 previous step's shard is all-gathered over RCCL on a side stream while the
-next window loads.  ``value`` = total bytes loaded by all ranks / max-rank
+next window loads (parallel/fanout.ShardedLoader: status word + data
+collective per step, failure consensus, per-slice CRC check of the last
+fan-out).  ``value`` = total bytes loaded by all ranks / max-rank
 wall time (GiB/s, weak scaling).  Also reported: p50/p99 latency of single
 4 KiB reads into HBM (QD1), the VFS control (pread → pinned → HtoD, the
 reference's ``nvme_test -f``) and a CRC32C check of the last window on the
@@ -76,6 +80,44 @@ def fs_type(path: str) -> str:
     return typ
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """``--gpus N`` outside torchrun: run N ranks as a CHILD torchrun (never
+    exec: this process has not touched the GPU and stays the parent), relay
+    its output, and fail unless rank 0 printed a result line for N ranks."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    print("[bench] launching", " ".join(cmd[1:]), file=sys.stderr, flush=True)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    result = None
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.startswith("{"):
+            try:
+                result = json.loads(line)
+            except ValueError:
+                pass
+    rc = p.wait()
+    if rc != 0:
+        return rc
+    if result is None or result.get("n_gpus") != n:
+        print(f"[bench] child run printed no result for {n} ranks", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,24 +129,33 @@ def main() -> int:
     ap.add_argument("--depth", type=int, default=6, help="segments in flight")
     ap.add_argument("--chunk", type=int, default=8192)
     ap.add_argument("--lat-samples", type=int, default=2000)
-    ap.add_argument("--fanout", choices=["allgather", "none"], default="allgather")
+    ap.add_argument("--fanout", choices=["allgather", "broadcast", "none"], default="allgather")
     ap.add_argument("--dir", default=os.environ.get("STROM_BENCH_DIR", "/tmp/strom_bench"))
     ap.add_argument("--keep", action="store_true", help="keep shard files")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process group backend (nccl = RCCL; gloo only to rehearse the "
-                         "multi-rank path with several ranks on one GPU, --fanout none)")
+                    help="process group backend (nccl = RCCL; gloo rehearses the multi-rank "
+                         "path with several ranks on one GPU, collectives staged via the host)")
     a = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a.gpus, sys.argv[1:])
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {a.gpus}")
 
     import torch
     import torch.distributed as dist
 
-    # ranks beyond the visible GPUs share them (multi-rank rehearsal on a
-    # one-GPU box; device_count() does not initialise the GPU)
-    local_dev = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    if a.backend == "nccl" and local_world > ndev:
+        raise SystemExit(f"bench: {local_world} ranks on this node but {ndev} GPUs visible "
+                         "(RCCL needs one GPU per rank; --backend gloo rehearses on one GPU)")
+    # gloo rehearsal: ranks beyond the visible GPUs share them
+    local_dev = local % max(1, ndev)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     if world > 1:
@@ -112,11 +163,19 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        assert dist.get_world_size() == a.gpus
+    # small control-plane collectives: device tensors under RCCL, host under gloo
+    cdev = dev if a.backend == "nccl" else torch.device("cpu")
+
+    def allreduce(vals, op):
+        t = torch.tensor(vals, dtype=torch.float64, device=cdev)
+        if world > 1:
+            dist.all_reduce(t, op=op)
+        return t.tolist()
 
     import nvme_strom_amd as S
-    from nvme_strom_amd.models.ssd2gpu_stream import StreamLoader, vfs_control
-    from nvme_strom_amd.ops import verify as V
-    from nvme_strom_amd.tensor import FileReader, HbmBuffer
+    from nvme_strom_amd.models.ssd2gpu_stream import vfs_control
+    from nvme_strom_amd.parallel.fanout import ShardedLoader
 
     os.makedirs(a.dir, exist_ok=True)
     W = a.window_mib << 20
@@ -128,12 +187,8 @@ def main() -> int:
     # ranks, taken before anyone writes), never below one window
     import shutil
     have = os.path.getsize(path) if os.path.exists(path) else 0
-    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
     F = shard_bytes(F, W, shutil.disk_usage(a.dir).free, have, local_world)
-    if world > 1:
-        t = torch.tensor([F], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        F = int(t.item())
+    F = int(allreduce([F], dist.ReduceOp.MIN if world > 1 else None)[0])
     t0 = time.time()
     make_shard(path, F, 1234 + rank)
     # reader pool per rank: split only among ranks that share this shard's
@@ -147,95 +202,46 @@ def main() -> int:
                f"{S.resident_bytes(fd) >> 20} MiB, engine={S.version()} provider={S.provider()}")
 
     fstype = fs_type(a.dir)
-    fan = world > 1 and a.fanout == "allgather"
-    # two resident windows when fanning out: step i loads one while the
-    # all-gather of step i-1 reads the other
-    bufs = [HbmBuffer(W, dev) for _ in range(2 if fan else 1)]
-    loader = StreamLoader(path, segment_sz=a.segment_mib << 20, chunk_sz=a.chunk, buf=bufs[0],
-                          depth=a.depth)
-    gather_out = torch.empty(world * W, dtype=torch.uint8, device=dev) if fan else None
-    side = torch.cuda.Stream(device=dev) if fan else None
-    nwin = F // W
-
-    def step(i: int):
-        off = (i % nwin) * W
-        b = bufs[i % len(bufs)]
-        st = loader.run(off, W, buf=b)
-        work = None
-        if fan:
-            ev = torch.cuda.Event()
-            ev.record()
-            with torch.cuda.stream(side):
-                side.wait_event(ev)
-                h = dist.all_gather_into_tensor(gather_out, b.tensor, async_op=True)
-                h.wait()                     # side stream waits for RCCL
-                work = torch.cuda.Event()
-                work.record(side)
-        return st, work
+    mode = a.fanout if world > 1 else "none"
+    fan = mode != "none"
+    # the loader: window i of this rank's shard into HBM buffer i % 2 while
+    # the side stream fans out window i-1 (status word + RCCL all-gather)
+    ld = ShardedLoader(path, W, dev, mode=mode, segment_sz=a.segment_mib << 20,
+                       chunk_sz=a.chunk, depth=a.depth)
+    nwin = ld.nwin
 
     for i in range(a.warmup):
-        _, w = step(i)
-        if w is not None:
-            w.synchronize()
+        ld.step(i)
+    ld.flush()
+    ld.stats = type(ld.stats)()
+    ld.gather_seconds()
+    ld.gather_s = 0.0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    agg = dict(nr_ram=0, nr_ssd=0, nr_submit=0, nr_blocks=0)
-    pend = None
     for i in range(a.steps):
-        st, w = step(a.warmup + i)
-        # the previous all-gather overlapped this step's load; its window is
-        # reloaded by the next step, so the host waits for it here
-        if pend is not None:
-            pend.synchronize()
-        pend = w
-        for k in agg:
-            agg[k] += getattr(st, k)
-    if pend is not None:
-        pend.synchronize()
-    if side is not None:
-        side.synchronize()
+        ld.step(a.warmup + i)
+    ld.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
 
     # max over ranks
-    times = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(times, op=dist.ReduceOp.MAX)
-    tmax = float(times.item())
+    tmax = allreduce([dt], dist.ReduceOp.MAX if world > 1 else None)[0]
     total_bytes = world * W * a.steps
     value = total_bytes / tmax / (1 << 30)
+    per_rank = ld.report(wall_s=dt)
+    st = ld.stats
+    agg = dict(nr_ram=st.nr_ram, nr_ssd=st.nr_ssd, nr_submit=st.nr_submit, nr_blocks=st.nr_blocks)
 
-    # integrity of the last loaded window (not timed)
+    # integrity of the last loaded window, and of every slice of the last
+    # fan-out (collective CRC check, not timed)
     last = a.warmup + a.steps - 1
-    last_off = (last % nwin) * W
-    buf = bufs[last % len(bufs)]
-    dev_crc = V.crc32c(buf.tensor)
-    with open(path, "rb") as f:
-        f.seek(last_off)
-        host_crc = 0
-        left = W
-        while left:
-            blk = f.read(min(64 << 20, left))
-            host_crc = S.crc32c_host(blk, host_crc)
-            left -= len(blk)
-    verified = dev_crc == host_crc
-
-    # RCCL all-gather integrity: slice r of the last gathered tensor is rank
-    # r's last window; compare its GPU CRC with the host CRC rank r computed
-    gather_ok = None
-    if fan:
-        crcs = torch.tensor([host_crc], dtype=torch.int64, device=dev)
-        allc = [torch.zeros_like(crcs) for _ in range(world)]
-        dist.all_gather(allc, crcs)
-        want = [int(c.item()) for c in allc]
-        got = [V.crc32c(gather_out[r * W:(r + 1) * W]) for r in range(world)]
-        ok = torch.tensor([float(got == want)], dtype=torch.float64, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        gather_ok = bool(ok.item() == 1.0)
+    verified = ld.verify(last)
+    gather_ok = verified if fan else None
+    buf = ld.bufs[last % len(ld.bufs)]
 
     # p50/p99 latency of single 4 KiB reads into HBM (QD1, O_DIRECT path),
     # timed in the engine's native loop (the reference's C-tool vantage);
@@ -283,12 +289,13 @@ def main() -> int:
     S.evict_file(fd)
     vt = vfs_control(path, 0, W, buf.tensor, segment_sz=a.segment_mib << 20, nr_segments=a.depth)
     vfs = W / vt / (1 << 30)
-    vals = torch.tensor([p50, p99, p50_py, vfs, float(verified)], dtype=torch.float64, device=dev)
+    # worst rank for latencies, sum of ranks for the control's throughput
     if world > 1:
-        dist.all_reduce(vals, op=dist.ReduceOp.SUM)
-        vals /= world
-    p50, p99, p50_py, vfs_avg, ver = vals.tolist()
-    vfs_total = vfs_avg * world
+        p50, p99, p50_py, ioctl_p50 = allreduce([p50, p99, p50_py, ioctl_p50], dist.ReduceOp.MAX)
+        vfs_total = allreduce([vfs], dist.ReduceOp.SUM)[0]
+    else:
+        vfs_total = vfs
+    ver = 1.0 if verified else 0.0
     hist = S.stat_hist()
     ing = S.ingest_info(local_dev)
     steps_bytes = (a.warmup + a.steps) * W
@@ -328,8 +335,12 @@ def main() -> int:
             "reread_note": "O_DIRECT: a re-read window is read from the backing store again "
                            "(no page cache in the path)",
         },
-        "rccl": {"world_size": world, "backend": dist.get_backend() if world > 1 else None,
+        "rccl": {"world_size": dist.get_world_size() if world > 1 else 1,
+                 "backend": dist.get_backend() if world > 1 else None,
+                 "collective": mode, "staged_via_host": ld.staged,
                  "allgather_verified": gather_ok},
+        "per_rank": per_rank,
+        "latency_reduction": "max over ranks (worst rank)",
         "ingest_grid": ing,
         "p50_4k_phases_us": phases,
         "verified_crc32c": bool(ver == 1.0),
@@ -342,7 +353,7 @@ def main() -> int:
             "model": f"ssd2gpu_stream(segment={a.segment_mib}MiB x depth {a.depth}, chunk={a.chunk}B)",
             "global_batch": world * W,
             "seq_len": a.chunk,
-            "parallelism": f"dp{world}" + ("+allgather" if fan else ""),
+            "parallelism": f"dp{world}" + (f"+{mode}" if fan else ""),
             "window_bytes_per_rank": W,
             "file_bytes_per_rank": F,
             "backend": S.config_get("backend"),
@@ -353,9 +364,7 @@ def main() -> int:
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    loader.close()
-    for b in bufs:
-        b.close()
+    ld.close()
     os.close(fd)
     if not a.keep:
         try:

@@ -364,7 +364,9 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
   uint64_t bytes = (uint64_t)a->nr_chunks * a->chunk_sz;
-  if (gmap->map_offset + a->offset + bytes > gmap->map_length) return -ERANGE;
+  // overflow-safe, shared with the kernel provider (strom_core_check_range)
+  if (strom_core_check_range(gmap->map_length - gmap->map_offset, a->offset, bytes))
+    return -ERANGE;
   int err = 0;
   auto ss = stripe(a->file_desc);
   std::shared_ptr<OpenFile> f;
@@ -450,7 +452,7 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   auto gmap = gpu_registry().get(handle);
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
-  if (gmap->map_offset + offset + len > gmap->map_length) return -ERANGE;
+  if (strom_core_check_range(gmap->map_length - gmap->map_offset, offset, len)) return -ERANGE;
   int err = 0;
   auto f = open_file(fd, &err);
   if (!f) return err;

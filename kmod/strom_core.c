@@ -274,9 +274,17 @@ int strom_core_nvme_rw(sc_u64 sect, sc_u32 len, sc_u32 lba_shift, sc_u64 *slba, 
 	return 0;
 }
 
+int strom_core_check_range(sc_u64 length, sc_u64 offset, sc_u64 bytes)
+{
+	/* offset + bytes <= length, without the sum (it can wrap) */
+	if (offset > length || bytes > length - offset)
+		return -ERANGE;
+	return 0;
+}
+
 int strom_core_check_dest(sc_u64 length, sc_u64 base_off, sc_u64 offset, sc_u64 bytes)
 {
-	if (offset > length || bytes > length - offset)
+	if (strom_core_check_range(length, offset, bytes))
 		return -ERANGE;
 	if ((base_off + offset) & (STROM_CORE_PAGE - 1))
 		return -EINVAL;

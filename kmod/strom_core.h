@@ -191,6 +191,7 @@ int strom_core_nvme_rw(sc_u64 sect, sc_u32 len, sc_u32 lba_shift, sc_u64 *slba,
 /* Destination window check for SSD2GPU against a registered range:
  * -ERANGE when [offset, offset + bytes) leaves [0, length) (overflow-safe),
  * -EINVAL when base_off + offset is not 4 KiB aligned (PRP rule above). */
+int strom_core_check_range(sc_u64 length, sc_u64 offset, sc_u64 bytes);
 int strom_core_check_dest(sc_u64 length, sc_u64 base_off, sc_u64 offset, sc_u64 bytes);
 
 #ifdef __cplusplus

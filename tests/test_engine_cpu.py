@@ -207,6 +207,26 @@ def test_ssd2gpu_range_and_handle_checks(strom, rand_file):
         os.close(fd)
 
 
+def test_destination_offset_wrap_is_erange(strom, rand_file):
+    """offset + bytes must not wrap past the mapping:
+    both providers use the overflow-safe strom_core_check_range."""
+    path, _ = rand_file(16 * CH)
+    fd = _open(path)
+    try:
+        keep, hbm = _host_target(8 * CH)
+        with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+            huge = (1 << 64) - 4096
+            with pytest.raises(strom.StromError) as e:
+                strom.memcpy_ssd2gpu(m.handle, huge, fd, np.arange(2, dtype=np.uint32), CH)
+            assert e.value.errno == errno.ERANGE
+            with pytest.raises(strom.StromError) as e:
+                strom.pread_gpu(m.handle, huge, fd, 0, 8192)
+            assert e.value.errno == errno.ERANGE
+            assert strom.pread_gpu(m.handle, 7 * CH, fd, 0, CH) == CH    # last slot fits
+    finally:
+        os.close(fd)
+
+
 def test_gpu_registry_list_info_unmap(strom):
     keep, hbm = _host_target(300 * 1024)
     addr = hbm.ctypes.data + 4096                       # not 64 KiB aligned

@@ -127,8 +127,12 @@ def _worker(rank, world, port, path, window, q):
             S.evict_file(fd)                        # storage reads, not page-cache copies
             os.close(fd)
             S.fault_inject(fail_at=1)               # first storage request of step 1
+        # no per-step host sync: the failure surfaces at the next check
+        # (every K steps or flush), on every rank, with the failed step
         try:
             ld.step(1)
+            out["raised_in_step"] = True
+            ld.flush()
             out["raised"] = None
         except ShardLoadError as e:
             out["raised"] = (e.step, e.failed, e.cause is not None)
@@ -168,4 +172,5 @@ def test_four_rank_placement_and_failure_consensus(tmp_path):
         assert got[r]["split"] == (2, 2, 2)
         # rank 2's read error reaches every rank, with its cause only there
         assert got[r]["raised"] == (1, [2], r == 2)
+        assert got[r]["raised_in_step"]             # step itself did not block/raise
         assert got[r]["after_ok"]
