@@ -92,3 +92,42 @@ selftest: build/selftest build/selftest-asan build/selftest-tsan
 	STROM_STAT_SHM=0 ./build/selftest && STROM_STAT_SHM=0 ./build/selftest-asan && STROM_STAT_SHM=0 TSAN_OPTIONS=report_signal_unsafe=0 ./build/selftest-tsan
 
 .PHONY: selftest
+
+# ---- kernel provider executed on the CPU ----------------------------------
+# The real kmod/strom_*.c linked against the behavioural kernel model
+# (kmod/testshim/kshim_rt.c) and driven by kmod/testshim/kmod_exec.c, plain,
+# ASAN+UBSAN and TSAN (tests/test_kmod_exec_cpu.py).
+KMOD_SRC  := $(wildcard kmod/strom_*.c) kmod/testshim/kshim_rt.c
+KMOD_HDR  := $(wildcard kmod/*.h) $(wildcard kmod/testshim/*.h) csrc/include/strom/uapi.h
+KSIM_KFLAGS := -std=gnu11 -g -D__KERNEL__ -Ikmod/testshim -Ikmod -Icsrc/include -Wall \
+               -Wno-unused-function -Wno-address-of-packed-member
+KSIM_UFLAGS := -std=gnu11 -g -Ikmod/testshim -Icsrc/include -Wall
+KSIM_DRV  := kmod/testshim/kmod_exec.c
+
+define ksim_build
+	@mkdir -p build/ksim$(2)
+	for f in $(KMOD_SRC); do $(1) $(KSIM_KFLAGS) $(3) -c $$f -o build/ksim$(2)/$$(basename $$f .c).o || exit 1; done
+	$(1) $(KSIM_UFLAGS) $(3) -c $(KSIM_DRV) -o build/ksim$(2)/kmod_exec.o
+	$(1) $(3) -o $@ build/ksim$(2)/*.o -lpthread
+endef
+
+build/kmod_exec: $(KMOD_SRC) $(KMOD_HDR) $(KSIM_DRV)
+	$(call ksim_build,gcc,,-O1)
+
+build/kmod_exec-asan: $(KMOD_SRC) $(KMOD_HDR) $(KSIM_DRV)
+	$(call ksim_build,gcc,-asan,-O1 -fsanitize=address$(comma)undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined)
+
+build/kmod_exec-tsan: $(KMOD_SRC) $(KMOD_HDR) $(KSIM_DRV)
+	$(call ksim_build,$(ROCM)/llvm/bin/clang,-tsan,-O1 -fsanitize=thread)
+
+comma := ,
+# the same, as a library for the ctypes differential test against libstrom
+build/libkmodsim.so: $(KMOD_SRC) $(KMOD_HDR)
+	@mkdir -p build/ksim-so
+	for f in $(KMOD_SRC); do gcc $(KSIM_KFLAGS) -O1 -fPIC -c $$f -o build/ksim-so/$$(basename $$f .c).o || exit 1; done
+	gcc -shared -o $@ build/ksim-so/*.o -lpthread
+
+kmod-exec: build/kmod_exec build/kmod_exec-asan build/kmod_exec-tsan
+	./build/kmod_exec && ./build/kmod_exec-asan && TSAN_OPTIONS=halt_on_error=1 ./build/kmod_exec-tsan
+
+.PHONY: kmod-exec

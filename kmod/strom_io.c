@@ -98,23 +98,23 @@ struct strom_req {
 	__le64 *prp_list;
 	dma_addr_t prp_dma;
 	u64 t0;
-	/* /proc/diskstats accounting so P2P reads show in iostat, as the
-	 * reference's part_stat_* calls did (kmod/nvme_strom.c:1012-1034) */
-	unsigned long acct_start;
+	/* /proc/diskstats accounting so P2P reads show in iostat, on the
+	 * member namespace AND on the volume the file lives on (md raid0 /
+	 * multipath head), as the reference's part_stat_* calls did
+	 * (kmod/nvme_strom.c:1012-1034) */
+	struct block_device *vol_part;   /* NULL: the file is on the namespace */
+	unsigned long acct_start, vol_acct_start;
 	unsigned int acct_sectors;
-	/* SSD2RAM: pages mapped for the device, unmapped on completion */
-	int nram;
-	dma_addr_t ram_dma[];
+	/* SSD2RAM: the DMA buffer range written (one segment: merges never
+	 * cross one), handed back to the CPU on completion */
+	dma_addr_t ram_dma;
+	u32 ram_len;
 };
 
 static void req_release_dma(struct strom_req *r)
 {
 	if (r->prp_list)
 		dma_pool_free(r->mbr->prp_pool, r->prp_list, r->prp_dma);
-	while (r->nram > 0) {
-		r->nram--;
-		dma_unmap_page(r->mbr->dma_dev, r->ram_dma[r->nram], PAGE_SIZE, DMA_FROM_DEVICE);
-	}
 }
 
 static enum rq_end_io_ret strom_end_io(struct request *rq, blk_status_t err)
@@ -127,6 +127,10 @@ static enum rq_end_io_ret strom_end_io(struct request *rq, blk_status_t err)
 	atomic64_add(strom_tsc() - r->t0, &strom_stats.clk_ssd2gpu);
 	atomic64_dec(&strom_stats.cur_dma_count);
 	bdev_end_io_acct(r->mbr->disk->part0, REQ_OP_READ, r->acct_sectors, r->acct_start);
+	if (r->vol_part)
+		bdev_end_io_acct(r->vol_part, REQ_OP_READ, r->acct_sectors, r->vol_acct_start);
+	if (r->ram_len)
+		dma_sync_single_for_cpu(r->mbr->dma_dev, r->ram_dma, r->ram_len, DMA_FROM_DEVICE);
 	req_release_dma(r);
 	if (r->gmap && atomic_dec_and_test(&r->gmap->inflight))
 		wake_up_all(&r->gmap->drain);
@@ -143,29 +147,28 @@ struct copy_ctx {
 	u64 gpu_base;                    /* dma-buf byte offset of destination 0 */
 	struct vm_area_struct *vma;      /* SSD2RAM */
 	unsigned long uaddr_base;
+	u64 ram_base;                    /* SSD2RAM: buffer offset of dest_uaddr; the
+					    planner works in buffer offsets so that
+					    dest_segment matches the real segments */
 	struct strom_planner pl;
 };
 
 struct ram_addr_ctx {
-	struct strom_req *r;
-	struct vm_area_struct *vma;
-	unsigned long uaddr;
+	struct device *dev;
+	struct file *dbuf;
+	u64 base;                        /* buffer offset of the request */
 };
 
+/* the buffer's segments are mapped once per controller (strom_dmabuffer.c) */
 static int ram_page_addr(void *p, u64 off, u32 need, u64 *a)
 {
 	struct ram_addr_ctx *x = p;
-	struct page *pg = strom_dma_buffer_page(x->vma, x->uaddr + off - x->vma->vm_start);
-	dma_addr_t d;
+	u64 contig;
+	int rc = strom_dma_buffer_dma(x->dbuf, x->dev, x->base + off, a, &contig);
 
-	if (!pg)
-		return -EFAULT;
-	d = dma_map_page(x->r->mbr->dma_dev, pg, 0, PAGE_SIZE, DMA_FROM_DEVICE);
-	if (dma_mapping_error(x->r->mbr->dma_dev, d))
-		return -EIO;
-	x->r->ram_dma[x->r->nram++] = d;
-	*a = d;
-	return 0;
+	if (!rc && contig < need)
+		rc = -EINVAL;          /* a merge never crosses a segment */
+	return rc;
 }
 
 /* submit one merged READ (the planner's flush callback) */
@@ -185,7 +188,7 @@ static int submit_extent(void *p, const struct strom_extent *e)
 	rc = strom_core_nvme_rw(e->sect, e->len, mbr->lba_shift, &slba, &nlb0);
 	if (rc)
 		return rc;
-	r = kzalloc(struct_size(r, ram_dma, x->vma ? npages : 0), GFP_KERNEL);
+	r = kzalloc(sizeof(*r), GFP_KERNEL);
 	if (!r)
 		return -ENOMEM;
 	r->task = x->t;
@@ -206,10 +209,14 @@ static int submit_extent(void *p, const struct strom_extent *e)
 						   e->len, (u64 *)r->prp_list, STROM_CORE_PRP_LIST_MAX,
 						   r->prp_dma, &prps);
 	} else {
-		struct ram_addr_ctx rx = { r, x->vma, x->uaddr_base + e->dest };
+		struct ram_addr_ctx rx = { mbr->dma_dev, x->t->dbuf_filp, e->dest };
 
 		rc = strom_core_build_prps(ram_page_addr, &rx, 0, e->len, (u64 *)r->prp_list,
 					   STROM_CORE_PRP_LIST_MAX, r->prp_dma, &prps);
+		if (!rc) {
+			r->ram_dma = prps.prp1;
+			r->ram_len = e->len;
+		}
 	}
 	atomic64_inc(&strom_stats.nr_setup_prps);
 	atomic64_add(strom_tsc() - t0, &strom_stats.clk_setup_prps);
@@ -238,10 +245,16 @@ static int submit_extent(void *p, const struct strom_extent *e)
 	strom_stat_inflight_inc();
 	r->acct_sectors = e->len >> SECTOR_SHIFT;
 	r->acct_start = bdev_start_io_acct(mbr->disk->part0, REQ_OP_READ, jiffies);
-	r->t0 = strom_tsc();
+	if (x->vol->registered) {
+		r->vol_part = x->inode->i_sb->s_bdev;   /* partition: the disk is accounted too */
+		r->vol_acct_start = bdev_start_io_acct(r->vol_part, REQ_OP_READ, jiffies);
+	}
+	t0 = r->t0 = strom_tsc();
 	blk_execute_rq_nowait(rq, false);
+	/* r belongs to the completion now (it may already be freed): no r->
+	 * past this point (TSAN, kernel-model harness) */
 	atomic64_inc(&strom_stats.nr_submit_dma);
-	atomic64_add(strom_tsc() - r->t0, &strom_stats.clk_submit_dma);
+	atomic64_add(strom_tsc() - t0, &strom_stats.clk_submit_dma);
 	return 0;
 fail:
 	req_release_dma(r);
@@ -356,6 +369,32 @@ static int copy_pgcache_to_ram(struct file *filp, loff_t fpos, u32 len,
 	return 0;
 }
 
+/* The part of a chunk that has blocks: whole pages up to EOF.  Pages wholly
+ * past EOF are never read (they map to no block); SSD2RAM zero-fills them
+ * in the buffer, SSD2GPU leaves them untouched in HBM (libstrom clears the
+ * file's tail itself), like the userspace provider's short read. */
+static u32 chunk_extent(u64 fpos, u32 chunk_sz, loff_t isize)
+{
+	return (u32)min_t(u64, chunk_sz, round_up((u64)isize - fpos, PAGE_SIZE));
+}
+
+static int zero_ram(struct vm_area_struct *vma, unsigned long uaddr, u32 len)
+{
+	u32 off;
+
+	for (off = 0; off < len; off += PAGE_SIZE) {
+		struct page *pg = strom_dma_buffer_page(vma, uaddr + off - vma->vm_start);
+		void *k;
+
+		if (!pg)
+			return -EFAULT;
+		k = kmap_local_page(pg);
+		memset(k, 0, PAGE_SIZE);
+		kunmap_local(k);
+	}
+	return 0;
+}
+
 /* resolve file + volume; the task owns the references on success */
 static int open_source(int fd, struct file **filp, struct strom_volume **vol)
 {
@@ -453,7 +492,8 @@ int strom_memcpy_ssd2gpu(struct strom_session *s, struct strom_memcpy_ssd2gpu __
 				rc = filemap_write_and_wait_range(filp->f_mapping, fpos,
 								  fpos + k.chunk_sz - 1);
 			if (!rc)
-				rc = strom_core_plan_range(&x.pl, fpos, k.chunk_sz, dest);
+				rc = strom_core_plan_range(&x.pl, fpos,
+							   chunk_extent(fpos, k.chunk_sz, isize), dest);
 		}
 	}
 	if (!rc)
@@ -534,6 +574,7 @@ int strom_memcpy_ssd2ram(struct strom_session *s, struct strom_memcpy_ssd2ram __
 	x.t->dbuf_filp = get_file(vma->vm_file);
 	x.vma = vma;
 	x.uaddr_base = (unsigned long)k.dest_uaddr;
+	x.ram_base = ((unsigned long)k.dest_uaddr - vma->vm_start) + (vma->vm_pgoff << PAGE_SHIFT);
 	ctx_init(&x, filp);
 	/* a merged request never crosses a 4 MiB segment of the buffer
 	 * (reference dest_segment_sz), where physical contiguity ends */
@@ -552,10 +593,15 @@ int strom_memcpy_ssd2ram(struct strom_session *s, struct strom_memcpy_ssd2ram __
 			break;
 		cached = chunk_is_cached(filp->f_mapping, fpos >> PAGE_SHIFT, k.chunk_sz >> PAGE_SHIFT);
 		dest = (size_t)strom_core_land(&land, i, cached) * k.chunk_sz;
-		if (cached)
+		if (cached) {
 			rc = copy_pgcache_to_ram(filp, fpos, k.chunk_sz, vma, x.uaddr_base + dest);
-		else
-			rc = strom_core_plan_range(&x.pl, fpos, k.chunk_sz, dest);
+		} else {
+			u32 n = chunk_extent(fpos, k.chunk_sz, isize);
+
+			rc = strom_core_plan_range(&x.pl, fpos, n, x.ram_base + dest);
+			if (!rc && n < k.chunk_sz)
+				rc = zero_ram(vma, x.uaddr_base + dest + n, k.chunk_sz - n);
+		}
 	}
 	if (!rc)
 		rc = strom_core_plan_flush(&x.pl);

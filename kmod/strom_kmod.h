@@ -109,7 +109,7 @@ struct strom_member {
 	struct device *disk_dev;         /* held (get_device) */
 	struct gendisk *disk;            /* blk-mq namespace (path) disk */
 	struct request_queue *q;
-	struct device *dma_dev;          /* the controller's PCI function */
+	struct device *dma_dev;          /* the controller's PCI function (held) */
 	u32 nsid;
 	u32 lba_shift;
 	u32 max_bytes;                   /* queue_max_hw_sectors, bytes */
@@ -122,6 +122,7 @@ struct strom_volume {
 	struct work_struct free_work;    /* members are released in process context */
 	struct list_head node;           /* route table (registered volumes) */
 	dev_t devt;                      /* md array / nvme head / plain namespace */
+	u64 diskseq;                     /* unregistered: the disk instance cached */
 	bool registered;
 	bool raid0;
 	struct strom_raid0 geo;
@@ -215,6 +216,7 @@ int strom_memcpy_ssd2ram(struct strom_session *s,
 int strom_alloc_dma_buffer(struct strom_alloc_dma_buffer *arg);
 bool strom_is_dma_buffer(struct vm_area_struct *vma);
 struct page *strom_dma_buffer_page(struct vm_area_struct *vma, unsigned long off);
+int strom_dma_buffer_dma(struct file *filp, struct device *dev, u64 off, u64 *addr, u64 *contig);
 
 /* ---- statistics ---------------------------------------------------------- */
 struct strom_stats {

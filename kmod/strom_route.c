@@ -14,11 +14,19 @@
  *     or, for hidden path disks, by "<pci>/<ctrl>/<disk>" name.  Every member
  *     must be a blk-mq NVMe namespace, and the geometry must be consistent
  *     (strom_core_raid0_check) and fit the members' capacity and the
- *     volume's size — a route can redirect reads only into the members the
- *     volume is made of, on a volume the admin named.
- * Members are held by their struct device (get_device); a member removed
- * while a route exists fails the requests sent to it, like any I/O to a
- * vanished disk.
+ *     volume's size.  A single-path alias must answer NVME_IOCTL_ID with the
+ *     head's nsid and have exactly the head's capacity.  That md members
+ *     really are the array's slaves is NOT verifiable through exported
+ *     interfaces (md's rdev list and the holder links are private): it is
+ *     asserted by the administrator who registers the route
+ *     (CAP_SYS_ADMIN), and a wrong route reads wrong sectors — the same
+ *     trust as writing to the member block devices directly.
+ * Members are held by their struct device (get_device), and so is each
+ * member's PCI function; a member removed while a route exists fails the
+ * requests sent to it, like any I/O to a vanished disk.  Unregistered
+ * (plain namespace) entries are a cache and are revalidated on every
+ * lookup: a disk that went away, or a new disk instance reusing the dev_t
+ * (diskseq), drops the stale entry.
  */
 #include <linux/blkdev.h>
 #include <linux/capability.h>
@@ -58,6 +66,7 @@ static int member_from_disk(struct strom_member *m, struct device *disk_dev)
 	m->dma_dev = pci_ancestor(disk_dev);
 	if (!m->dma_dev)
 		return -EOPNOTSUPP;
+	get_device(m->dma_dev);
 	m->disk_dev = get_device(disk_dev);
 	m->disk = disk;
 	m->q = q;
@@ -68,7 +77,9 @@ static int member_from_disk(struct strom_member *m, struct device *disk_dev)
 	m->prp_pool = dma_pool_create("strom_prp", m->dma_dev, STROM_CORE_PAGE, STROM_CORE_PAGE, 0);
 	if (!m->prp_pool) {
 		put_device(m->disk_dev);
+		put_device(m->dma_dev);
 		m->disk_dev = NULL;
+		m->dma_dev = NULL;
 		return -ENOMEM;
 	}
 	return 0;
@@ -80,8 +91,11 @@ static void member_release(struct strom_member *m)
 		dma_pool_destroy(m->prp_pool);
 	if (m->disk_dev)
 		put_device(m->disk_dev);
+	if (m->dma_dev)
+		put_device(m->dma_dev);
 	m->prp_pool = NULL;
 	m->disk_dev = NULL;
+	m->dma_dev = NULL;
 }
 
 /* "<pci>/<ctrl>/<disk>": PCI function -> controller device -> path disk */
@@ -179,63 +193,89 @@ void strom_volume_put(struct strom_volume *v)
 		kref_put(&v->ref, volume_free);
 }
 
+/* an unregistered entry describes the disk instance it was built from */
+static bool volume_stale(const struct strom_volume *v, struct gendisk *disk)
+{
+	return !v->registered &&
+	       (v->m[0].disk != disk || v->diskseq != disk->diskseq || !disk_live(disk));
+}
+
+/* under routes_lock: the entry for devt, a stale cached one unlinked into *stale */
+static struct strom_volume *route_lookup(dev_t devt, struct gendisk *disk,
+					 struct strom_volume **stale)
+{
+	struct strom_volume *v;
+
+	list_for_each_entry(v, &routes, node) {
+		if (v->devt != devt)
+			continue;
+		if (volume_stale(v, disk)) {
+			list_del(&v->node);
+			*stale = v;          /* the list's reference, dropped by the caller */
+			return NULL;
+		}
+		kref_get(&v->ref);
+		return v;
+	}
+	return NULL;
+}
+
 struct strom_volume *strom_volume_of_file(struct file *filp, int *err)
 {
 	struct inode *inode = file_inode(filp);
 	struct super_block *sb = inode->i_sb;
 	struct block_device *bdev = sb->s_bdev;
-	struct strom_volume *v;
+	struct strom_volume *v, *stale = NULL, *o;
+	struct gendisk *disk;
 	dev_t devt;
 	int rc;
 
 	*err = -EOPNOTSUPP;
 	if (!bdev)
 		return NULL;
-	devt = disk_devt(bdev->bd_disk);
+	disk = bdev->bd_disk;
+	devt = disk_devt(disk);
 	mutex_lock(&routes_lock);
-	list_for_each_entry(v, &routes, node) {
-		if (v->devt == devt) {
-			kref_get(&v->ref);
-			mutex_unlock(&routes_lock);
-			*err = 0;
-			return v;
-		}
-	}
+	v = route_lookup(devt, disk, &stale);
 	mutex_unlock(&routes_lock);
+	strom_volume_put(stale);                      /* in-flight tasks hold their own */
+	if (v) {
+		*err = 0;
+		return v;
+	}
 	/* unregistered: only a plain blk-mq namespace can be served */
 	v = volume_alloc(devt);
 	if (!v) {
 		*err = -ENOMEM;
 		return NULL;
 	}
-	rc = member_from_disk(&v->m[0], disk_to_dev(bdev->bd_disk));
+	rc = member_from_disk(&v->m[0], disk_to_dev(disk));
 	if (rc) {
 		kfree(v);
-		if (!queue_is_mq(bdev->bd_disk->queue))
+		if (!queue_is_mq(disk->queue))
 			prDebug("%s: bio-based volume (md / nvme multipath head): register a route",
-				bdev->bd_disk->disk_name);
+				disk->disk_name);
 		*err = rc;
 		return NULL;
 	}
 	v->nmembers = 1;
-	/* cache it (unregistered entries live until a route replaces them or
-	 * the module unloads): the next lookup of this volume is a list walk */
+	v->diskseq = disk->diskseq;
+	/* cache it (unregistered entries live until a route replaces them, the
+	 * disk goes away, or the module unloads) */
+	stale = NULL;
 	mutex_lock(&routes_lock);
-	{
-		struct strom_volume *o;
-
-		list_for_each_entry(o, &routes, node)
-			if (o->devt == devt) {            /* lost a race: use theirs */
-				kref_get(&o->ref);
-				mutex_unlock(&routes_lock);
-				strom_volume_put(v);
-				*err = 0;
-				return o;
-			}
+	o = route_lookup(devt, disk, &stale);
+	if (o) {                                      /* lost a race: use theirs */
+		mutex_unlock(&routes_lock);
+		strom_volume_put(stale);
+		strom_volume_put(v);
+		*err = 0;
+		return o;
 	}
 	kref_get(&v->ref);                            /* the list's reference */
 	list_add_tail(&v->node, &routes);
 	mutex_unlock(&routes_lock);
+	strom_volume_put(stale);
 	*err = 0;
 	return v;
 }
@@ -327,10 +367,24 @@ int strom_set_route(const struct strom_set_route *r)
 					goto fail;
 			}
 		}
-	} else if (r->nmembers != 1 || v->m[0].nr_sects < vol_sects) {
-		/* a path alias: one member, at least the volume's size */
+	} else {
+		/* a path alias of a multipath head: one member with the head's
+		 * nsid and exactly its capacity */
+		int head_nsid = -1;
+
 		rc = -EINVAL;
-		goto fail;
+		if (r->nmembers != 1 || v->m[0].nr_sects != vol_sects)
+			goto fail;
+		vd = find_disk_by_devt(vdev);
+		if (vd) {
+			struct gendisk *hd = dev_to_disk(vd);
+
+			if (hd->fops && hd->fops->ioctl)
+				head_nsid = hd->fops->ioctl(hd->part0, BLK_OPEN_READ, NVME_IOCTL_ID, 0);
+			put_device(vd);
+		}
+		if (head_nsid <= 0 || (u32)head_nsid != v->m[0].nsid)
+			goto fail;
 	}
 	mutex_lock(&routes_lock);
 	list_for_each_entry(old, &routes, node)

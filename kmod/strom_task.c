@@ -76,38 +76,51 @@ void strom_task_get(struct strom_task *t)
 void strom_task_put(struct strom_task *t, long status)
 {
 	unsigned int k = slot_of(t->id);
-	struct file *sfilp;
+	struct strom_gpumap *gmap;
+	struct strom_volume *vol;
+	struct file *filp, *dbuf, *sfilp;
 	unsigned long flags;
+	bool failed;
 
 	if (status)
 		cmpxchg(&t->status, 0, status);
 	if (!atomic_dec_and_test(&t->refcnt))
 		return;
+	/* The last reference.  Everything the record holds is taken out BEFORE
+	 * it becomes visible on the failed list: from that moment a WAIT on
+	 * another CPU may consume and kfree it (found by the TSAN run of the
+	 * kernel-model harness, kmod/testshim/kmod_exec.c). */
+	gmap = t->gmap;
+	filp = t->filp;
+	dbuf = t->dbuf_filp;
+	vol = t->vol;
+	sfilp = t->sess->filp;
+	t->gmap = NULL;
+	t->filp = NULL;
+	t->dbuf_filp = NULL;
+	t->vol = NULL;
+	failed = t->status != 0;
 	spin_lock_irqsave(&slots[k].lock, flags);
 	hlist_del(&t->node);
-	if (t->status) {
+	if (failed) {
 		spin_lock(&t->sess->lock);
 		list_add_tail(&t->failed_node, &t->sess->failed);
 		spin_unlock(&t->sess->lock);
 	}
 	spin_unlock_irqrestore(&slots[k].lock, flags);
 	wake_up_all(&slots[k].wq);
-	sfilp = t->sess->filp;
-	if (t->gmap)
-		strom_gpumap_put(t->gmap);   /* teardown runs on a workqueue */
-	if (t->filp)
-		fput(t->filp);
-	if (t->dbuf_filp)
-		fput(t->dbuf_filp);
-	strom_volume_put(t->vol);           /* frees on a workqueue if last */
-	t->gmap = NULL;
-	t->filp = NULL;
-	t->dbuf_filp = NULL;
-	t->vol = NULL;
-	if (!t->status)
+	if (!failed)
 		kfree(t);
-	/* last: a failed record stays on the session's list until WAIT or
-	 * release(), which this reference holds off */
+	/* t may be gone now */
+	if (gmap)
+		strom_gpumap_put(gmap);      /* teardown runs on a workqueue */
+	if (filp)
+		fput(filp);
+	if (dbuf)
+		fput(dbuf);
+	strom_volume_put(vol);              /* frees on a workqueue if last */
+	/* last: the session (and a failed record on its list) lives until WAIT
+	 * or release(), which this reference holds off */
 	fput(sfilp);
 }
 

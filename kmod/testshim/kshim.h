@@ -1,19 +1,35 @@
-/* kshim.h — a MODEL of the Linux (6.8 .. 6.18) kernel API surface the
- * nvme-strom module uses, so that `gcc -fsyntax-only` can type-check the
- * module sources on a machine without kernel headers
- * (tests/test_kmod_core_cpu.py::test_kmod_sources_typecheck_against_api_model).
+/* kshim.h — a behavioural MODEL of the Linux (6.8 .. 6.18) kernel API surface
+ * the nvme-strom module uses.
  *
- * Every declaration is written from the kernel's public headers as they stand
- * in that range (include/linux/{blkdev,blk-mq,dma-buf,fs,device,...}.h); it is
- * NOT a kernel and proves nothing about ABI or runtime behaviour — it catches
- * undeclared identifiers, wrong argument counts and type slips in code that
- * cannot be built here.  kmod/kernel-check.sh checks the real tree.
+ * Two uses:
+ *  1. `gcc -fsyntax-only` type-checks the module sources against it on a
+ *     machine without kernel headers, on each side of the version gates
+ *     (tests/test_kmod_core_cpu.py::test_kmod_sources_typecheck_against_api_model);
+ *  2. kshim_rt.c IMPLEMENTS it in userspace — blk-mq queues completing on
+ *     other threads ("IRQ context"), a fake NVMe controller that validates
+ *     every READ against the spec, per-device IOMMU domains, a dma-buf
+ *     exporter with reservation-lock rules, a page cache with clean and dirty
+ *     pages, ext4-like block maps, md raid0 volumes, workqueues, file
+ *     refcounts with deferred release — so the REAL kmod/strom_*.c files are
+ *     linked and executed through their ioctl entry points
+ *     (kmod/testshim/kmod_exec.c, tests/test_kmod_exec_cpu.py), plain and
+ *     under ASAN+UBSAN and TSAN.
+ *
+ * Every declaration follows the kernel's public headers in that range
+ * (include/linux/{blkdev,blk-mq,dma-buf,fs,device,...}.h).  Struct members
+ * marked "model" do not exist in the kernel: the runtime's bookkeeping.  It
+ * is not a kernel and proves nothing about ABI; kmod/kernel-check.sh checks
+ * the real tree.  What it does check at run time: the module's use of the
+ * API contracts it models (sleeping in IRQ context or under a spinlock,
+ * dma-buf pin/map without the reservation lock, DMA to addresses not mapped
+ * for the issuing device, PRP rules, leaked mappings/pages/references).
  */
 #ifndef KSHIM_H
 #define KSHIM_H
 #include <stddef.h>
 #include <stdbool.h>
 #include <stdint.h>
+#include <limits.h>
 
 #define KERNEL_VERSION(a, b, c) (((a) << 16) + ((b) << 8) + (c))
 #ifndef KSHIM_VERSION                 /* -DKSHIM_VERSION=... checks the other gates */
@@ -39,10 +55,10 @@ typedef u32 __le32;
 typedef u64 __le64;
 typedef u32 __u32;
 typedef u64 __u64;
-typedef long long loff_t;
+typedef long loff_t;                 /* glibc's width: the runtime includes both */
 typedef long ssize_t;
 typedef u64 sector_t;
-typedef u32 dev_t;
+typedef unsigned long dev_t;
 typedef u64 dma_addr_t;
 typedef unsigned int gfp_t;
 typedef unsigned int blk_mode_t;
@@ -52,7 +68,7 @@ typedef unsigned long pgoff_t;
 typedef struct { int counter; } atomic_t;
 typedef struct { s64 counter; } atomic64_t;
 typedef struct { unsigned int val; } kuid_t;
-typedef struct { int x; } spinlock_t;
+typedef struct { int locked; } spinlock_t;           /* model: test-and-set word */
 typedef struct { int x; } wait_queue_head_t;
 typedef unsigned int fmode_t;
 
@@ -74,16 +90,19 @@ typedef unsigned int fmode_t;
 #define ETIME 62
 #define EOPNOTSUPP 95
 #define ERESTARTSYS 512
+#define ENOIOCTLCMD 515
 
 #define GFP_KERNEL 0u
+#define GFP_ATOMIC 2u
 #define __GFP_ZERO 1u
 #define PAGE_SHIFT 12
 #define PAGE_SIZE (1UL << PAGE_SHIFT)
 #define SECTOR_SHIFT 9
 #define HZ 250
-#define MAX_SCHEDULE_TIMEOUT 0x7fffffffL
+#define MAX_SCHEDULE_TIMEOUT LONG_MAX
 #define NUMA_NO_NODE (-1)
 #define DMA_BIT_MASK(n) (((n) == 64) ? ~0ULL : ((1ULL << (n)) - 1))
+#define DMA_MAPPING_ERROR (~(dma_addr_t)0)
 #define FMODE_READ 1u
 #define BLK_OPEN_READ 1u
 #define S_ISREG(m) (((m) & 0170000) == 0100000)
@@ -101,6 +120,7 @@ typedef unsigned int fmode_t;
 
 #define ARRAY_SIZE(a) (sizeof(a) / sizeof((a)[0]))
 #define DIV_ROUND_UP(n, d) (((n) + (d) - 1) / (d))
+#define round_up(x, y) ((((x) - 1) | ((__typeof__(x))((y) - 1))) + 1)
 #define min(a, b) ((a) < (b) ? (a) : (b))
 #define max(a, b) ((a) > (b) ? (a) : (b))
 #define min_t(t, a, b) ((t)(a) < (t)(b) ? (t)(a) : (t)(b))
@@ -109,11 +129,16 @@ typedef unsigned int fmode_t;
 #define IS_ERR(p) ((unsigned long)(p) > (unsigned long)-4096)
 #define IS_ERR_OR_NULL(p) (!(p) || IS_ERR(p))
 #define PTR_ERR(p) ((long)(p))
-#define BUG_ON(c) do { if (c) __builtin_trap(); } while (0)
-#define WARN_ON_ONCE(c) ((void)(c))
-#define might_sleep() do { } while (0)
-#define pr_info(...) ((void)0)
-#define pr_notice(...) ((void)0)
+#define ERR_PTR(e) ((void *)(long)(e))
+void kshim_bug(const char *what, const char *file, int line);
+#define BUG_ON(c) do { if (c) kshim_bug(#c, __FILE__, __LINE__); } while (0)
+void kshim_warn(const char *what, const char *file, int line);
+#define WARN_ON_ONCE(c) ({ int __w = !!(c); if (__w) kshim_warn(#c, __FILE__, __LINE__); __w; })
+void kshim_might_sleep(const char *file, int line);
+#define might_sleep() kshim_might_sleep(__FILE__, __LINE__)
+void kshim_printk(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+#define pr_info(...) kshim_printk(__VA_ARGS__)
+#define pr_notice(...) kshim_printk(__VA_ARGS__)
 #define cmpxchg(p, o, n) __sync_val_compare_and_swap(p, o, n)
 #define uid_eq(a, b) ((a).val == (b).val)
 #define MKDEV(ma, mi) (((ma) << 20) | (mi))
@@ -121,11 +146,14 @@ typedef unsigned int fmode_t;
 #define cpu_to_le32(x) ((__le32)(x))
 #define cpu_to_le64(x) ((__le64)(x))
 #define ilog2(n) (63 - __builtin_clzll(n))
-#define put_user(x, p) ((void)(p), (void)(x), 0)
-#define get_user(x, p) ((void)(p), (x) = 0, 0)
+/* user pointers are host pointers in the model; kshim_uaccess_ok() knows
+ * the "unmapped" ones (NULL page, harness-poisoned ranges) */
+bool kshim_uaccess_ok(const void *p, size_t n);
+#define put_user(x, p) (kshim_uaccess_ok((p), sizeof(*(p))) ? (*(p) = (x), 0) : -EFAULT)
+#define get_user(x, p) (kshim_uaccess_ok((p), sizeof(*(p))) ? ((x) = *(p), 0) : -EFAULT)
 #define dev_is_pci(d) ((d)->bus == &pci_bus_type)
-#define DEFINE_SPINLOCK(x) spinlock_t x
-#define DEFINE_MUTEX(x) struct mutex x
+#define DEFINE_SPINLOCK(x) spinlock_t x = { 0 }
+#define DEFINE_MUTEX(x) struct mutex x = { 0 }
 #define LIST_HEAD(x) struct list_head x = { &(x), &(x) }
 #define DEFINE_HASHTABLE(n, bits) struct hlist_head n[1 << (bits)]
 #define ATOMIC64_INIT(i) { (i) }
@@ -137,8 +165,8 @@ typedef unsigned int fmode_t;
 #define MODULE_IMPORT_NS(x)
 #define MODULE_PARM_DESC(a, b)
 #define module_param_named(a, b, t, p)
-#define module_init(f) int init_module(void) { return f(); }
-#define module_exit(f) void cleanup_module(void) { f(); }
+#define module_init(f) int kshim_module_init(void) { return f(); }  /* not init_module: libc has one */
+#define module_exit(f) void kshim_module_exit(void) { f(); }
 #define THIS_MODULE ((struct module *)0)
 #define __stringify(x) #x
 
@@ -146,22 +174,49 @@ struct module;
 struct list_head { struct list_head *next, *prev; };
 struct hlist_node { struct hlist_node *next, **pprev; };
 struct hlist_head { struct hlist_node *first; };
-struct mutex { int x; };
+struct mutex { int locked; };                        /* model: sleeping lock word */
 struct kref { atomic_t refcount; };
-struct work_struct { int x; };
+struct work_struct {
+	void (*func)(struct work_struct *);
+	struct work_struct *next;                     /* model: queue link */
+	int pending;                                  /* model */
+};
 struct workqueue_struct;
 struct srcu_struct;
 struct rcu_head { void *p; };
 struct bus_type { const char *name; };
 struct class { const char *name; };
-struct device { struct device *parent; const struct bus_type *bus; const struct class *class; };
-struct page { unsigned long flags; };
+struct kshim_iommu;
+struct device {
+	struct device *parent;
+	const struct bus_type *bus;
+	const struct class *class;
+	/* model */
+	char kname[40];
+	int krefs;
+	int numa_node;
+	u64 dma_mask;
+	struct kshim_iommu *iommu;
+};
+struct page {
+	unsigned long flags;
+	/* model */
+	void *kaddr;
+	int refcount;
+	struct kshim_pblock *blk;
+};
 struct folio { unsigned long flags; };
 struct address_space;
 struct super_block;
 struct file_system_type { const char *name; };
 struct block_device;
-struct inode { unsigned int i_mode; unsigned char i_blkbits; struct super_block *i_sb; };
+struct inode {
+	unsigned int i_mode;
+	unsigned char i_blkbits;
+	struct super_block *i_sb;
+	loff_t i_size;                                /* model: i_size_read() */
+	struct address_space *i_mapping;
+};
 struct super_block { unsigned long s_blocksize; struct file_system_type *s_type; struct block_device *s_bdev; };
 struct file { fmode_t f_mode; struct address_space *f_mapping; void *private_data; const struct file_operations *f_op; };
 struct fd { struct file *file; };
@@ -204,14 +259,32 @@ struct gendisk {
 	const struct block_device_operations *fops;
 	struct request_queue *queue;
 	struct block_device *part0;
+	u64 diskseq;
 };
-struct block_device { struct gendisk *bd_disk; sector_t bd_start_sect; struct device bd_device; };
+struct block_device {
+	struct gendisk *bd_disk;
+	sector_t bd_start_sect;
+	struct device bd_device;
+	/* model: /proc/diskstats of this block device */
+	unsigned long kios, ksectors;
+	long kinflight;
+};
 struct bdev_handle { struct block_device *bdev; };
 enum req_op { REQ_OP_READ = 0, REQ_OP_DRV_IN = 34 };
 enum rq_end_io_ret { RQ_END_IO_NONE, RQ_END_IO_FREE };
 struct request;
 typedef enum rq_end_io_ret (rq_end_io_fn)(struct request *, blk_status_t);
-struct request { unsigned int timeout; rq_end_io_fn *end_io; void *end_io_data; };
+struct nvme_command;
+struct request {
+	unsigned int timeout;
+	rq_end_io_fn *end_io;
+	void *end_io_data;
+	/* model */
+	struct request_queue *q;
+	struct nvme_command *cmd;                     /* nvme_init_request() */
+	unsigned int opf;
+	struct request *knext;
+};
 struct request *blk_mq_alloc_request(struct request_queue *q, unsigned int opf, unsigned int flags);
 void blk_execute_rq_nowait(struct request *rq, bool at_head);
 int blk_status_to_errno(blk_status_t status);
@@ -221,6 +294,7 @@ unsigned int queue_max_hw_sectors(const struct request_queue *q);
 sector_t get_capacity(struct gendisk *disk);
 sector_t get_start_sect(struct block_device *bdev);
 dev_t disk_devt(struct gendisk *disk);
+bool disk_live(struct gendisk *disk);
 #define disk_to_dev(disk) (&((disk)->part0->bd_device))
 #define dev_to_bdev(d) container_of(d, struct block_device, bd_device)
 #define dev_to_disk(d) (dev_to_bdev(d)->bd_disk)
@@ -275,6 +349,7 @@ void *dma_pool_alloc(struct dma_pool *, gfp_t, dma_addr_t *);
 void dma_pool_free(struct dma_pool *, void *, dma_addr_t);
 dma_addr_t dma_map_page(struct device *, struct page *, size_t off, size_t sz, enum dma_data_direction);
 void dma_unmap_page(struct device *, dma_addr_t, size_t, enum dma_data_direction);
+void dma_sync_single_for_cpu(struct device *, dma_addr_t, size_t, enum dma_data_direction);
 int dma_mapping_error(struct device *, dma_addr_t);
 u64 dma_get_mask(struct device *);
 int dev_to_node(struct device *);
@@ -320,6 +395,8 @@ void free_page(unsigned long);
 void *kmap_local_page(struct page *);
 void kunmap_local(const void *);
 int numa_node_id(void);
+extern unsigned int nr_node_ids;
+bool node_online(int nid);
 
 /* memory + strings */
 void *kzalloc(size_t, gfp_t);
@@ -339,7 +416,9 @@ unsigned long copy_from_user(void *to, const void __user *from, unsigned long n)
 unsigned long copy_to_user(void __user *to, const void *from, unsigned long n);
 unsigned long clear_user(void __user *to, unsigned long n);
 
-/* sync */
+/* sync: spinlocks spin (and mark the thread atomic), mutexes and waits
+ * sleep — the runtime checks that nothing sleeps in IRQ context or under a
+ * spinlock */
 void spin_lock_init(spinlock_t *);
 void spin_lock(spinlock_t *);
 void spin_unlock(spinlock_t *);
@@ -352,8 +431,41 @@ void mutex_lock(struct mutex *);
 void mutex_unlock(struct mutex *);
 void init_waitqueue_head(wait_queue_head_t *);
 void wake_up_all(wait_queue_head_t *);
-#define wait_event(wq, cond) do { (void)(wq); while (!(cond)) { } } while (0)
-#define wait_event_interruptible_timeout(wq, cond, t) ((void)(wq), (cond) ? (long)(t) : 0L)
+/* one sleep slice on a wait queue (bounded, so a wakeup racing the
+ * condition check costs at most a slice); asserts a sleepable context */
+void kshim_wait_slice(wait_queue_head_t *wq, const char *file, int line);
+u64 kshim_now_ns(void);
+bool kshim_signal_pending(void);
+#define wait_event(wq, cond)                                                   \
+	do {                                                                   \
+		while (!(cond))                                                \
+			kshim_wait_slice(&(wq), __FILE__, __LINE__);            \
+	} while (0)
+#define wait_event_interruptible_timeout(wq, cond, timeout)                    \
+	({                                                                     \
+		long __to = (timeout), __ret;                                  \
+		u64 __dl = __to == MAX_SCHEDULE_TIMEOUT ? UINT64_MAX :         \
+			   kshim_now_ns() + (u64)__to * (1000000000ull / HZ);  \
+		for (;;) {                                                     \
+			u64 __now;                                             \
+			if (cond) {                                            \
+				__now = kshim_now_ns();                        \
+				__ret = __dl == UINT64_MAX ? __to :            \
+					max(1L, (long)((__dl > __now ? __dl - __now : 0) / (1000000000ull / HZ))); \
+				break;                                         \
+			}                                                      \
+			if (kshim_signal_pending()) {                          \
+				__ret = -ERESTARTSYS;                          \
+				break;                                         \
+			}                                                      \
+			if (kshim_now_ns() >= __dl) {                          \
+				__ret = (cond) ? 1 : 0;                        \
+				break;                                         \
+			}                                                      \
+			kshim_wait_slice(&(wq), __FILE__, __LINE__);            \
+		}                                                              \
+		__ret;                                                         \
+	})
 void kref_init(struct kref *);
 void kref_get(struct kref *);
 int kref_put(struct kref *, void (*release)(struct kref *));
@@ -368,7 +480,7 @@ void atomic64_add(s64, atomic64_t *);
 s64 atomic64_inc_return(atomic64_t *);
 s64 atomic64_cmpxchg(atomic64_t *, s64, s64);
 s64 atomic64_xchg(atomic64_t *, s64);
-#define INIT_WORK(w, f) ((void)(w), (void)(f))
+#define INIT_WORK(w, f) ((w)->func = (f), (w)->next = NULL, (w)->pending = 0)
 struct workqueue_struct *alloc_workqueue(const char *fmt, unsigned int flags, int max_active, ...);
 bool queue_work(struct workqueue_struct *, struct work_struct *);
 void destroy_workqueue(struct workqueue_struct *);
@@ -400,10 +512,11 @@ void hlist_del(struct hlist_node *n);
 #define hlist_for_each_entry(pos, head, member) \
 	for (pos = hlist_entry_safe((head)->first, __typeof__(*(pos)), member); pos; \
 	     pos = hlist_entry_safe((pos)->member.next, __typeof__(*(pos)), member))
-#define hash_init(t) ((void)(t))
-#define hash_add(t, n, key) hlist_add_head(n, &(t)[0])
+#define hash_init(t) do { for (size_t __i = 0; __i < ARRAY_SIZE(t); __i++) INIT_HLIST_HEAD(&(t)[__i]); } while (0)
+#define hash_add(t, n, key) hlist_add_head(n, &(t)[hash_long((unsigned long)(key), ilog2(ARRAY_SIZE(t)))])
 #define hash_del(n) hlist_del(n)
-#define hash_for_each_possible(t, obj, member, key) hlist_for_each_entry(obj, &(t)[0], member)
+#define hash_for_each_possible(t, obj, member, key) \
+	hlist_for_each_entry(obj, &(t)[hash_long((unsigned long)(key), ilog2(ARRAY_SIZE(t)))], member)
 #define hash_for_each(t, bkt, obj, member) \
 	for ((bkt) = 0; (bkt) < (int)ARRAY_SIZE(t); (bkt)++) hlist_for_each_entry(obj, &(t)[bkt], member)
 #endif
