@@ -236,6 +236,7 @@ struct DmaBuffer {
   ino_t ino = 0;
   size_t length = 0;
   int node = -1;
+  uint64_t gen = 0;                 // registration order (gc only drops older ones)
 };
 
 // Which VMA covers an address (PROCMAP_QUERY on /proc/self/maps, Linux
@@ -273,6 +274,7 @@ class DmaBufRegistry {
     std::shared_ptr<DmaBuffer> buf;
   };
   std::mutex mu_;
+  uint64_t next_gen_ = 1;              // under mu_
   std::map<std::pair<dev_t, ino_t>, std::shared_ptr<DmaBuffer>> bufs_;
   std::map<uint64_t, Range> ranges_;   // start -> engine-made mapping
 };

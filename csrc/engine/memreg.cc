@@ -338,6 +338,7 @@ int DmaBufRegistry::alloc(size_t length, int node, int *user_fd) {
   b->node = node;
   {
     std::lock_guard<std::mutex> g(mu_);
+    b->gen = next_gen_++;
     bufs_[{b->dev, b->ino}] = b;
   }
   *user_fd = fd;
@@ -407,6 +408,14 @@ int DmaBufRegistry::unmap(void *addr, size_t len) {
 }
 
 int DmaBufRegistry::gc() {
+  // Only buffers registered before the /proc snapshot below may be judged
+  // by it: one another thread registers while we scan is live but absent
+  // from the snapshot (gc erased a buffer allocated concurrently).
+  uint64_t before;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    before = next_gen_;
+  }
   // inodes this process still holds: open fds, then mappings
   std::set<std::pair<dev_t, ino_t>> live;
   if (DIR *d = opendir("/proc/self/fd")) {
@@ -439,7 +448,7 @@ int DmaBufRegistry::gc() {
   }
   std::lock_guard<std::mutex> g(mu_);
   for (auto it = bufs_.begin(); it != bufs_.end();) {
-    if (live.count(it->first)) ++it;
+    if (live.count(it->first) || it->second->gen >= before) ++it;
     else it = bufs_.erase(it);   // in-flight SSD2RAM tasks keep their shared_ptr
   }
   return (int)bufs_.size();

@@ -227,6 +227,31 @@ int main() {
     strom_engine_reset();
   }
 
+  // concurrent ALLOC_DMA_BUFFER: each alloc's gc snapshot must not drop a
+  // buffer another thread registered meanwhile (memreg.cc gc)
+  {
+    std::atomic<int> bad{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < 6; t++)
+      th.emplace_back([&bad] {
+        for (int i = 0; i < 25; i++) {
+          strom_alloc_dma_buffer a{};
+          a.length = 4096;
+          a.node_id = -1;
+          if (nvme_strom_ioctl(STROM_IOCTL__ALLOC_DMA_BUFFER, &a) != 0) {
+            bad++;
+            continue;
+          }
+          void *m = strom_dmabuf_mmap(a.dmabuf_fdesc, 4096);
+          if (!m) bad++;
+          else strom_dmabuf_munmap(m, 4096);
+          close(a.dmabuf_fdesc);
+        }
+      });
+    for (auto &t : th) t.join();
+    CHECK(bad.load() == 0);
+  }
+
   strom_stat_info si{};
   si.version = 1;
   CHECK(nvme_strom_ioctl(STROM_IOCTL__STAT_INFO, &si) == 0);

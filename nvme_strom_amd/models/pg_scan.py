@@ -37,6 +37,7 @@ import json
 import os
 import threading
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -379,14 +380,35 @@ class HeapRelationScan:
         self.pred = dict(attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi)
         # idle participant resources (session, HBM ring, readers, pinned
         # write-back buffers), reused by later runs: allocating and pinning
-        # them per run cost more than the scan of a GiB-sized relation
+        # them per run cost more than the scan of a GiB-sized relation.
+        # Entries are keyed by the configuration they were sized for, and
+        # released by close() / the context manager / garbage collection
+        # (weakref.finalize: a scan object that is simply dropped leaks
+        # nothing).
         self._pool: List[tuple] = []
         self._pool_lock = threading.Lock()
+        self._finalizer = weakref.finalize(self, HeapRelationScan._drain, self._pool,
+                                           self._pool_lock)
+
+    def _pool_key(self) -> tuple:
+        c = self.cfg
+        return (c.buffer_size, c.chunk_size, c.snapshot is not None, str(self.device))
 
     def _acquire(self) -> tuple:
+        key = self._pool_key()
+        stale = []
         with self._pool_lock:
-            if self._pool:
-                return self._pool.pop()
+            while self._pool:
+                k, rs = self._pool.pop()
+                if k == key:
+                    break
+                stale.append(rs)
+            else:
+                rs = None
+        for old in stale:                     # sized for another configuration
+            self._free(old)
+        if rs is not None:
+            return rs
         cfg = self.cfg
         per_chunk = cfg.chunk_size // BLCKSZ
         nslots = cfg.buffer_size // cfg.chunk_size
@@ -399,6 +421,10 @@ class HeapRelationScan:
         cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if cfg.snapshot is not None else []
         return sess, hb, readers, wbs, cpu_bufs
 
+    def _release(self, rs: tuple) -> None:
+        with self._pool_lock:
+            self._pool.append((self._pool_key(), rs))
+
     @staticmethod
     def _free(rs: tuple) -> None:
         sess, hb, readers, _, _ = rs
@@ -407,12 +433,23 @@ class HeapRelationScan:
         hb.close()
         sess.close()
 
+    @staticmethod
+    def _drain(pool: list, lock) -> None:
+        with lock:
+            items = list(pool)
+            pool.clear()
+        for _, rs in items:
+            HeapRelationScan._free(rs)
+
     def close(self) -> None:
         """Release the pooled participant resources."""
-        with self._pool_lock:
-            pool, self._pool = self._pool, []
-        for rs in pool:
-            self._free(rs)
+        self._drain(self._pool, self._pool_lock)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None,
             cursor=None) -> ScanResult:
@@ -492,8 +529,7 @@ class HeapRelationScan:
         except BaseException:
             self._free(rs)          # a failed participant's reads may still be in flight
             raise
-        with self._pool_lock:
-            self._pool.append(rs)
+        self._release(rs)
         st.chunk_items = found
         return st
 
@@ -654,9 +690,13 @@ class ResumableScan:
     continues at the first unscanned block, so each block's tuples are
     reported exactly once across interruptions.
 
-    ``scan`` is any ``(b0, b1) -> ScanResult`` — e.g.
-    ``lambda b0, b1: HeapRelationScan(...).run(4, blocks=(b0, b1))`` or the
-    ``cpu_scan`` path.  ``key`` (required, non-empty) identifies the relation,
+    ``scan`` is any ``(b0, b1) -> ScanResult`` — e.g. one scan object reused
+    for every range (its participant resources are pooled across runs)::
+
+        with HeapRelationScan(rel, cfg) as hs:
+            ResumableScan(lambda b0, b1: hs.run(4, blocks=(b0, b1)), ...).run()
+
+    or the ``cpu_scan`` path.  ``key`` (required, non-empty) identifies the relation,
     predicate and scan options — :func:`scan_key` builds one; resuming a
     checkpoint written under a different key, block count or step raises
     ``ValueError``.

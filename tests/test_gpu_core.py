@@ -176,6 +176,28 @@ def test_pread_gpu_visible_to_next_kernel(S, tmp_path):
     assert not bad, f"{len(bad)} stale reads, first at {bad[:5]}"
 
 
+def test_pread_gpu_visible_to_sdma_readback(S, tmp_path):
+    """the posted HDP flush is also enough for a copy-engine
+    consumer — each 4 KiB pread_gpu is read back with a D2H copy started
+    right after it returns (no kernel launch in between), 500 offsets."""
+    from nvme_strom_amd.tensor import HbmBuffer
+    S.configure(hdp_sync=0, bar_map=1)
+    n = 500
+    p, data = _mkfile(tmp_path, 8 << 20, seed=37)
+    fd = os.open(p, os.O_RDONLY)
+    offs = np.random.default_rng(4).choice((8 << 20) // 4096, n, replace=False) * 4096
+    host = torch.empty(4096, dtype=torch.uint8, pin_memory=True)
+    bad = []
+    with HbmBuffer(n * 4096, "cuda") as hb:
+        for i, off in enumerate(offs.tolist()):
+            assert S.pread_gpu(hb.handle, i * 4096, fd, off, 4096) == 4096
+            host.copy_(hb.tensor[i * 4096:(i + 1) * 4096])      # hipMemcpy D2H
+            if not np.array_equal(host.numpy(), data[off:off + 4096]):
+                bad.append(i)
+    os.close(fd)
+    assert not bad, f"{len(bad)} stale D2H reads, first at {bad[:5]}"
+
+
 def test_read_chunks_hybrid_reorder(S, tmp_path):
     """Page-cache chunks land at the tail via the write-back buffer; the
     reader scatters everything back into the requested order on the GPU."""

@@ -33,8 +33,9 @@ def test_pg_relation_scan_gpu_vs_cpu(S, tmp_path):
     os.close(fd)
     cfg = pg_scan.ScanConfig(chunk_size=16 * 8192, buffer_size=64 * 8192, verify_checksum=True)
     for workers in (1, 3):
-        g = pg_scan.HeapRelationScan(rel, cfg, "cuda", attr_off=0, attr_width=8, lo=-100,
-                                     hi=2500).run(workers)
+        with pg_scan.HeapRelationScan(rel, cfg, "cuda", attr_off=0, attr_width=8, lo=-100,
+                                      hi=2500) as hs:
+            g = hs.run(workers)
         c = pg_scan.cpu_scan(rel, cfg, attr_off=0, attr_width=8, lo=-100, hi=2500)
         assert np.array_equal(g.items, c.items)
         assert g.bad_pages == 0 and g.pages == rel.nblocks
@@ -51,12 +52,12 @@ def test_pg_relation_scan_resumable_gpu(S, tmp_path):
     cfg = pg_scan.ScanConfig(chunk_size=16 * 8192, buffer_size=64 * 8192, verify_checksum=True)
     pred = dict(attr_off=0, attr_width=8, lo=-1000, hi=3000)
     full = pg_scan.cpu_scan(rel, cfg, **pred)
-    g = pg_scan.HeapRelationScan(rel, cfg, "cuda", **pred)
-    ck = str(tmp_path / "gpu.ckpt.npz")
-    scan = lambda b0, b1: g.run(2, blocks=(b0, b1))
-    a = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577")
-    assert a.run(max_steps=1) is None and a.next_block == 50
-    r = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577").run()
+    with pg_scan.HeapRelationScan(rel, cfg, "cuda", **pred) as g:
+        ck = str(tmp_path / "gpu.ckpt.npz")
+        scan = lambda b0, b1: g.run(2, blocks=(b0, b1))
+        a = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577")
+        assert a.run(max_steps=1) is None and a.next_block == 50
+        r = pg_scan.ResumableScan(scan, rel.nblocks, ck, step_blocks=50, key="24577").run()
     assert np.array_equal(r.items, full.items) and r.pages == rel.nblocks and r.bad_pages == 0
 
 
@@ -113,7 +114,8 @@ def test_heap_scan_vm_routing_matches_cpu(S, tmp_path):
     rel, snap, clog, want, nchecked = _mvcc_relation(tmp_path, nblocks=40)
     cfg = pg_scan.ScanConfig(chunk_size=6 * 8192, buffer_size=18 * 8192, snapshot=snap,
                              clog=clog, verify_checksum=True)
-    g = pg_scan.HeapRelationScan(rel, cfg, "cuda").run(workers=2)
+    with pg_scan.HeapRelationScan(rel, cfg, "cuda") as hs:
+        g = hs.run(workers=2)
     assert set(g.items.tolist()) == want
     assert g.nr_checked == nchecked and g.bad_pages == 0
     c = pg_scan.cpu_scan(rel, cfg)

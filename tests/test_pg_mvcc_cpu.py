@@ -191,3 +191,34 @@ def test_plan_scan_decisions():
     assert pg_scan.plan_scan(100 * gib, 10, 64 * gib, 8 * gib, off).reason == "disabled"
     forced = pg_scan.ScanConfig(debug_no_threshold=True)
     assert pg_scan.plan_scan(1 << 20, 10, 64 * gib, 8 * gib, forced).path == "nvme_strom"
+
+
+def test_heap_scan_pool_keyed_and_released(tmp_path, monkeypatch):
+    """pooled participant resources are keyed by the configuration
+    they were sized for, and released by close(), the context manager, or
+    garbage collection of an unclosed scan object."""
+    import gc
+    from nvme_strom_amd.models import pg_scan
+    from nvme_strom_amd.utils import pgpage
+    data = pgpage.build_table(np.arange(300, dtype=np.int64), per_page=150, width=8)
+    rel = pg_scan.Relation.write(str(tmp_path / "16384"), data, relseg_size=64)
+    freed = []
+    monkeypatch.setattr(pg_scan.HeapRelationScan, "_free", staticmethod(lambda rs: freed.append(rs)))
+    cfg = pg_scan.ScanConfig(chunk_size=2 * 8192, buffer_size=8 * 8192)
+    hs = pg_scan.HeapRelationScan(rel, cfg, "cpu")
+    hs._release("A")
+    assert hs._acquire() == "A" and freed == []          # same configuration: reused
+    hs._release("A")
+    hs.cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192)
+    monkeypatch.setattr(pg_scan, "HbmBuffer", lambda *a, **k: (_ for _ in ()).throw(RuntimeError("x")))
+    with pytest.raises(RuntimeError):
+        hs._acquire()                                     # mismatched entry freed first
+    assert freed == ["A"]
+    with pg_scan.HeapRelationScan(rel, cfg, "cpu") as h2:
+        h2._release("B")
+    assert freed == ["A", "B"]
+    h3 = pg_scan.HeapRelationScan(rel, cfg, "cpu")
+    h3._release("C")
+    del h3
+    gc.collect()
+    assert freed == ["A", "B", "C"]
