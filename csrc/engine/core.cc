@@ -35,7 +35,7 @@ Config Config::from_env() {
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
                                "bar_map", "bar_max", "coalesce", "trace",
-                               "ingest", "ingest_grid", "ingest_piece", "hdp_sync",
+                               "ingest", "ingest_grid", "ingest_piece", "hdp_sync", "fixed_bufs",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind", "check_freed",
                                "stat_info", "verbose"};
@@ -87,6 +87,7 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "coalesce") { coalesce = parse_bool(v); return 0; }
   if (k == "ingest") { ingest = parse_bool(v); return 0; }
   if (k == "hdp_sync") { hdp_sync = parse_bool(v); return 0; }
+  if (k == "fixed_bufs") { fixed_bufs = parse_bool(v); return 0; }
   if (k == "ingest_grid") { if (n < 1 || n > 256) return -EINVAL; ingest_grid = (int)n; return 0; }
   if (k == "ingest_piece") {
     if (n < 4096 || n > (16l << 20) || (n & 4095)) return -EINVAL;
@@ -132,6 +133,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "ingest_grid") v = ingest_grid;
   else if (k == "ingest_piece") v = ingest_piece;
   else if (k == "hdp_sync") v = hdp_sync;
+  else if (k == "fixed_bufs") v = fixed_bufs;
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;

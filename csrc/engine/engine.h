@@ -66,6 +66,11 @@ struct Config {
   uint32_t ingest_piece = 256u << 10;  // bytes per ingest descriptor
   bool hdp_sync = false;         // wait for each HDP flush to complete (read
                                  // back) instead of posting it
+  bool fixed_bufs = true;        // register each worker's pinned staging with its
+                                 // io_uring (IORING_REGISTER_BUFFERS) and read
+                                 // into it with READ_FIXED (no per-I/O page
+                                 // pinning); falls back to READ when the
+                                 // kernel or RLIMIT_MEMLOCK refuses
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks

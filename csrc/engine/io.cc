@@ -27,6 +27,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
+#include <sys/uio.h>
 #include <unistd.h>
 #include <x86intrin.h>
 
@@ -104,6 +105,15 @@ class Uring {
   }
   unsigned pending() const { return pending_; }
   bool ok() const { return fd_ >= 0; }
+  void unregister_buffers() {
+    (void)syscall(__NR_io_uring_register, fd_, IORING_UNREGISTER_BUFFERS, nullptr, 0u);
+  }
+  // one fixed buffer (index 0) covering [p, p+len); -errno when refused
+  int register_buffer(void *p, size_t len) {
+    iovec iov{p, len};
+    int r = (int)syscall(__NR_io_uring_register, fd_, IORING_REGISTER_BUFFERS, &iov, 1u);
+    return r < 0 ? -errno : 0;
+  }
 
  private:
   int fail() {
@@ -240,6 +250,7 @@ struct IoEngine::Worker {
   uint8_t *staging = nullptr;     // one registered region, cut into slots
   size_t staging_bytes = 0;
   bool staging_thp = false;
+  bool fixed = false;             // staging registered with the ring (READ_FIXED)
   std::deque<int> free_slots;     // FIFO: consecutive requests get adjacent slots
   std::deque<int> copying;        // FIFO of slots with copies in flight
   std::vector<int> staged;        // reads done, HBM copy not yet issued
@@ -312,11 +323,22 @@ struct IoEngine::Worker {
       slots[i].buf = staging + (size_t)i * cfg.max_request;
       free_slots.push_back(i);
     }
+    // the staging is pinned already (hipHostMalloc); registering it lets
+    // READ_FIXED skip the per-I/O get_user_pages of the O_DIRECT path
+    fixed = false;
+    if (cfg.fixed_bufs && ring.ok()) {
+      int rc = ring.register_buffer(staging, bytes);
+      fixed = rc == 0;
+      if (rc) STROM_LOG(1, "worker %d: io_uring buffer registration refused (%d)", idx, rc);
+    }
+    stats().nr_debug[3].fetch_add(fixed ? 1 : 0, std::memory_order_relaxed);
     return true;
   }
 
   void free_staging() {
     if (!staging) return;
+    if (fixed) ring.unregister_buffers();
+    fixed = false;
     if (staging_thp) hip::host_free_thp(staging, staging_bytes);
     else hip::host_free(staging);
     staging = nullptr;
@@ -534,7 +556,12 @@ struct IoEngine::Worker {
         ring.enter(0);
         sqe = ring.next_sqe();
       }
-      sqe->opcode = IORING_OP_READ;
+      if (fixed && slot >= 0) {
+        sqe->opcode = IORING_OP_READ_FIXED;
+        sqe->buf_index = 0;
+      } else {
+        sqe->opcode = IORING_OP_READ;
+      }
       sqe->fd = read_fd(r);
       sqe->addr = (uint64_t)dst;
       sqe->len = len;
@@ -791,9 +818,11 @@ void IoEngine::submit(std::vector<IoReq> &reqs) {
 // reads of `block` bytes at random aligned offsets into host memory (or,
 // with `sequential`, the next block of a shared cursor: the order the
 // engine streams a window in).  The sweep prints it next to the engine's
-// SSD→HBM numbers.
+// SSD→HBM numbers.  `mode` bit 0: sequential; bit 1: buffered reads (the
+// page-cache ceiling the engine-only sweep compares against).
 extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
-                                   uint32_t qd, int sequential, double *iops, double *gibps) {
+                                   uint32_t qd, int mode, double *iops, double *gibps) {
+  const bool sequential = mode & 1;
   using namespace strom;
   if (block == 0 || (block & 4095) || nreq == 0 || threads == 0 || qd == 0 || qd > 256)
     return -EINVAL;
@@ -803,7 +832,7 @@ extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32
   if (nblk == 0) return -ERANGE;
   char path[64];
   snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
-  int d = open(path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+  int d = open(path, O_RDONLY | ((mode & 2) ? 0 : O_DIRECT) | O_CLOEXEC);
   if (d < 0) return -errno;
   std::atomic<int> err{0};
   std::atomic<uint32_t> issued{0};

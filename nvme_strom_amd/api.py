@@ -467,13 +467,14 @@ def pread_raw_latency(fd: int, file_offs, length: int = 4096) -> np.ndarray:
 
 
 def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
-                  sequential: bool = False) -> tuple:
+                  sequential: bool = False, buffered: bool = False) -> tuple:
     """Storage ceiling for one block size with no engine in the way:
     ``threads`` io_uring rings ``qd`` deep, O_DIRECT reads into host memory
-    at random aligned offsets (or in file order through a shared cursor).
-    Returns (IOPS, GiB/s)."""
+    at random aligned offsets (or in file order through a shared cursor);
+    ``buffered`` reads through the page cache instead.  Returns (IOPS, GiB/s)."""
     iops, gibps = C.c_double(), C.c_double()
-    _check(N.lib().strom_raw_read_rate(fd, block, nreq, threads, qd, int(sequential),
+    _check(N.lib().strom_raw_read_rate(fd, block, nreq, threads, qd,
+                                       int(sequential) | (2 if buffered else 0),
                                        C.byref(iops), C.byref(gibps)), "raw_read_rate")
     return iops.value, gibps.value
 

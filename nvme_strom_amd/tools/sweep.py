@@ -13,6 +13,16 @@ and the file is streamed into HBM with the nvme_test shape (32 MiB segments,
                order (no engine, no HBM) — the engine's target at that size
                (raw_random_GiBps: the same at random aligned offsets)
 
+``--engine-only``: the same sweep with the storage taken out
+(``backend=cache``: the workers read a file held in the page cache through
+its buffered descriptor, residency probe off so every chunk still takes the
+worker + staging + HBM-ingest path).  Each size then has a real engine
+ceiling — GiB/s, IOPS and QD1 p50/p99 of the engine alone — and ``raw_*`` is
+the same rings reading the cached file into host RAM.
+
+``--ab KEY`` runs every size twice, KEY=0 and KEY=1 interleaved (e.g.
+``--ab fixed_bufs``: io_uring registered staging + READ_FIXED vs plain READ).
+
 ``python -m nvme_strom_amd.tools.sweep --out gpurun_out/sweep.json``
 """
 from __future__ import annotations
@@ -53,6 +63,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="cuda", help="cpu = emulated HBM (tests)")
     ap.add_argument("--no-raw", dest="raw", action="store_false",
                     help="skip the raw io_uring ceiling per block size")
+    ap.add_argument("--engine-only", action="store_true",
+                    help="backend=cache: page-cache reads through the full engine path")
+    ap.add_argument("--ab", default="", help="config key to A/B (0 vs 1) at every size")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -74,42 +87,56 @@ def main(argv=None) -> int:
     F = int(a.file_gib * (1 << 30)) // (4 << 20) * (4 << 20)
     _mk(path, F)
     fd = os.open(path, os.O_RDONLY)
-    defaults = {k: S.config_get(k) for k in ("max_request", "queue_depth")}
+    keys = ["max_request", "queue_depth", "backend", "pgcache_probe"] + ([a.ab] if a.ab else [])
+    defaults = {k: S.config_get(k) for k in keys}
+    evict = (lambda f: None) if a.engine_only else S.evict_file
+    if a.engine_only:
+        S.configure(backend="cache", pgcache_probe=0)
+        with open(path, "rb") as f:                 # hold the file in the page cache
+            while f.read(64 << 20):
+                pass
     rows = []
+    sizes = [size(x) for x in a.blocks.split(",")]
+    runs = [(B, v) for B in sizes for v in ((0, 1) if a.ab else (None,))]
     try:
-        for B in [size(x) for x in a.blocks.split(",")]:
+        for B, abv in runs:
             kv = {"max_request": B}
             if a.qd:
                 kv["queue_depth"] = a.qd
+            if a.ab:
+                kv[a.ab] = abv
             S.configure(**kv)
             chunk = min(B, 8192)
             nbytes = min(int(a.max_gib * (1 << 30)), B * 65536, F) // (32 << 20) * (32 << 20)
             nbytes = max(nbytes, 32 << 20)
             ld = StreamLoader(path, segment_sz=32 << 20, nr_segments=6, chunk_sz=chunk,
                               device=a.device, depth=6)
-            S.evict_file(fd)
+            evict(fd)
             ld.run(0, 32 << 20)                      # warm the engine, not the cache
-            S.evict_file(fd)
+            evict(fd)
             sync()
             st = ld.run(0, nbytes)
             sync()
             gibs = nbytes / st.seconds / (1 << 30)
             iops = st.nr_submit / st.seconds
             # QD1 latency of B-byte reads at random aligned offsets
-            S.evict_file(fd)
+            evict(fd)
             rng = np.random.default_rng(B)
             offs = rng.integers(0, F // B, size=a.lat_samples + 20) * B
             ns = S.pread_gpu_latency(ld.buf.handle, 0, fd, offs, B)[20:] / 1e3
             row = dict(block=B, GiBps=round(gibs, 2), iops=round(iops), bytes=nbytes,
+                       **({a.ab: abv} if a.ab else {}),
                        avg_req_kib=round(0.5 * st.nr_blocks / st.nr_submit, 1) if st.nr_submit else 0,
                        ram_chunks=st.nr_ram, p50_us=round(float(np.percentile(ns, 50)), 2),
                        p99_us=round(float(np.percentile(ns, 99)), 2))
             if a.raw:
                 nraw = max(2000, min(nbytes // B, 200000))
                 kw = dict(threads=int(S.config_get("workers")), qd=int(S.config_get("queue_depth")))
-                S.evict_file(fd)
+                # engine-only: the same rings read the cached file (buffered)
+                kw["buffered"] = a.engine_only
+                evict(fd)
                 riops, rgib = S.raw_read_rate(fd, B, nraw, sequential=True, **kw)
-                S.evict_file(fd)
+                evict(fd)
                 _, rgib_rand = S.raw_read_rate(fd, B, nraw, **kw)
                 row.update(raw_iops=round(riops), raw_GiBps=round(rgib, 2),
                            raw_random_GiBps=round(rgib_rand, 2),
@@ -121,7 +148,9 @@ def main(argv=None) -> int:
         S.configure(**defaults)
         os.close(fd)
     out = dict(workers=int(S.config_get("workers")), queue_depth=a.qd or int(defaults["queue_depth"]),
-               backend=S.config_get("backend"), file_bytes=F, rows=rows)
+               backend="cache (engine only: storage removed)" if a.engine_only
+               else S.config_get("backend"), file_bytes=F, ab=a.ab or None,
+               fixed_bufs_workers=S.stat_info().get("nr_debug4"), rows=rows)
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)

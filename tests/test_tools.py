@@ -72,6 +72,24 @@ def test_block_sweep_cpu(strom, tmp_path):
     assert strom.config_get("max_request") == str(1 << 20)   # restored
 
 
+def test_block_sweep_engine_only_ab_cpu(strom, tmp_path):
+    """--engine-only (backend=cache, storage removed) with an interleaved
+    A/B of a config key: both arms per size, config restored after."""
+    from nvme_strom_amd.tools import sweep
+    out = tmp_path / "sweep_cache.json"
+    rc = sweep.main(["--file-gib", "0.0625", "--dir", str(tmp_path), "--blocks", "4K,64K",
+                     "--max-gib", "0.03125", "--lat-samples", "10", "--device", "cpu",
+                     "--engine-only", "--ab", "fixed_bufs", "--out", str(out)])
+    assert rc == 0
+    import json
+    res = json.load(open(out))
+    assert res["backend"].startswith("cache") and res["ab"] == "fixed_bufs"
+    assert [(r["block"], r["fixed_bufs"]) for r in res["rows"]] == [(4096, 0), (4096, 1),
+                                                                     (65536, 0), (65536, 1)]
+    assert all(r["GiBps"] > 0 and r["raw_GiBps"] > 0 for r in res["rows"])
+    assert strom.config_get("backend") == "uring" and strom.config_get("fixed_bufs") == "1"
+
+
 def test_raw_read_rate(strom, tmp_path):
     """The storage-ceiling probe reads the requested count and rejects bad shapes."""
     import os
