@@ -140,6 +140,9 @@ class Uring {
   unsigned sq_mask_ = 0, cq_mask_ = 0, entries_ = 0, pending_ = 0;
 };
 
+// worker-level I/O facts for tools (strom_io_info)
+static std::atomic<uint64_t> g_fixed_workers{0}, g_fixed_refused{0}, g_fixed_errno{0};
+
 // ------------------------------------------------------------- completion
 void finish_request(IoReq &r, long status) {
   Stats &st = stats();
@@ -329,15 +332,23 @@ struct IoEngine::Worker {
     if (cfg.fixed_bufs && ring.ok()) {
       int rc = ring.register_buffer(staging, bytes);
       fixed = rc == 0;
-      if (rc) STROM_LOG(1, "worker %d: io_uring buffer registration refused (%d)", idx, rc);
+      if (rc) {
+        STROM_LOG(1, "worker %d: io_uring buffer registration refused (%d)", idx, rc);
+        g_fixed_refused.fetch_add(1);
+        g_fixed_errno.store((uint64_t)-rc);
+      } else {
+        g_fixed_workers.fetch_add(1);
+      }
     }
-    stats().nr_debug[3].fetch_add(fixed ? 1 : 0, std::memory_order_relaxed);
     return true;
   }
 
   void free_staging() {
     if (!staging) return;
-    if (fixed) ring.unregister_buffers();
+    if (fixed) {
+      ring.unregister_buffers();
+      g_fixed_workers.fetch_sub(1);
+    }
     fixed = false;
     if (staging_thp) hip::host_free_thp(staging, staging_bytes);
     else hip::host_free(staging);
@@ -811,6 +822,14 @@ void IoEngine::submit(std::vector<IoReq> &reqs) {
 }
 
 }  // namespace strom
+
+// workers whose staging is registered (READ_FIXED), refusals, last errno
+extern "C" int strom_io_info(uint64_t *out) {
+  out[0] = strom::g_fixed_workers.load();
+  out[1] = strom::g_fixed_refused.load();
+  out[2] = strom::g_fixed_errno.load();
+  return 0;
+}
 
 // ----------------------------------------------------- raw storage ceiling
 // The device's own limit for a block size, with no engine in the way:

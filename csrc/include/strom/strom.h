@@ -282,6 +282,19 @@ int strom_column_filter_batched(int type, const struct strom_filter_batch *d_bat
 int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
                          const struct strom_filter_batch *d_batches, uint32_t nbatches,
                          int64_t *d_out, uint64_t *d_total, void *stream);
+/* Qualifier lists: combine != 0 ANDs the predicate into the existing
+ * bitmap words (count = rows left selected). */
+int strom_column_filter_batched2(int type, const struct strom_filter_batch *d_batches,
+                                 uint32_t nbatches, uint64_t nwords, double lo, double hi,
+                                 uint64_t *d_bitmap, uint64_t *d_count, int combine, void *stream);
+/* bitmap_to_rows + projection: d_proj (same batches, another column's
+ * values/valid pointers) non-NULL gathers each selected row's value (width 4
+ * or 8 bytes) into d_pout[pos] and, when d_pvalid, its validity (0/1). */
+int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwords,
+                              const struct strom_filter_batch *d_batches, uint32_t nbatches,
+                              int64_t *d_out, uint64_t *d_total,
+                              const struct strom_filter_batch *d_proj, uint32_t width,
+                              void *d_pout, uint8_t *d_pvalid, void *stream);
 
 #ifdef __cplusplus
 }

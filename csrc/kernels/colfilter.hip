@@ -140,11 +140,15 @@ __device__ __forceinline__ uint32_t batch_of(const strom_filter_batch *b, uint32
   return lo;
 }
 
+// combine: AND the predicate into the existing bitmap (a qualifier list:
+// the first column writes the words, later ones narrow them); the count is
+// of the combined words, so the last qualifier's count is the selection's
 template <typename T>
 __global__ __launch_bounds__(256) void filter_batched_kernel(const strom_filter_batch *__restrict__ bt,
                                                              uint32_t nb, uint64_t nwords, T lo,
                                                              T hi, uint64_t *__restrict__ bitmap,
-                                                             unsigned long long *__restrict__ count) {
+                                                             unsigned long long *__restrict__ count,
+                                                             int combine) {
   __shared__ uint32_t wave_cnt[4];
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t local = 0;
@@ -174,6 +178,7 @@ __global__ __launch_bounds__(256) void filter_batched_kernel(const strom_filter_
       const uint64_t i = k * 64 + lane;
       uint64_t word = __ballot(i < b.nrows && x[u] >= lo && x[u] <= hi);
       if (b.valid && k * 64 < b.nrows) word &= ((const uint64_t *)b.valid)[k];
+      if (combine) word &= bitmap[w];                 // uniform load, one per wave
       if (lane == 0) bitmap[w] = word;
       local += __popcll(word);
     }
@@ -226,12 +231,21 @@ __global__ __launch_bounds__(256) void block_popc64_kernel(const uint64_t *__res
   if (threadIdx.x == 0) block_cnt[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
 }
 
+// W: bytes per projected value (0: no projection).  With a projection the
+// selected rows' values of another column (its own per-batch pointers in
+// `pt`, same batches) are gathered next to the row ids, plus a 0/1 validity
+// byte when that column has nulls: PG-Strom's projection of the qualifying
+// tuples, done while the ids are written.
+template <uint32_t W>
 __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restrict__ bm,
                                                         uint64_t nwords,
                                                         const strom_filter_batch *__restrict__ bt,
                                                         uint32_t nb,
                                                         const uint64_t *__restrict__ base,
-                                                        int64_t *__restrict__ out) {
+                                                        int64_t *__restrict__ out,
+                                                        const strom_filter_batch *__restrict__ pt,
+                                                        void *__restrict__ pout,
+                                                        uint8_t *__restrict__ pvalid) {
   __shared__ uint32_t s[256];
   const uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
   uint64_t word = w < nwords ? bm[w] : 0;
@@ -246,22 +260,36 @@ __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restri
   }
   if (!word) return;
   uint64_t pos = base[blockIdx.x] + s[threadIdx.x] - c;
-  const strom_filter_batch b = bt[batch_of(bt, nb, w)];
-  const int64_t row0 = (int64_t)(b.row_base + (w - b.word_base) * 64);
+  const uint32_t bi = batch_of(bt, nb, w);
+  const strom_filter_batch b = bt[bi];
+  const uint64_t local0 = (w - b.word_base) * 64;
+  const int64_t row0 = (int64_t)(b.row_base + local0);
+  const uint8_t *pv = nullptr, *pval = nullptr;
+  if (W) {
+    pv = (const uint8_t *)pt[bi].values;
+    pval = (const uint8_t *)pt[bi].valid;
+  }
   while (word) {
     const uint32_t bit = __ffsll((unsigned long long)word) - 1;
-    out[pos++] = row0 + bit;
+    out[pos] = row0 + bit;
+    if (W) {
+      const uint64_t r = local0 + bit;
+      if (W == 8) ((uint64_t *)pout)[pos] = ((const uint64_t *)pv)[r];
+      else ((uint32_t *)pout)[pos] = ((const uint32_t *)pv)[r];
+      if (pvalid) pvalid[pos] = pval ? (pval[r >> 3] >> (r & 7)) & 1 : 1;
+    }
+    ++pos;
     word &= word - 1;
   }
 }
 
 template <typename T>
 int launch_filter_batched(const strom_filter_batch *bt, uint32_t nb, uint64_t nwords, double lo,
-                          double hi, uint64_t *bm, uint64_t *cnt, hipStream_t st) {
+                          double hi, uint64_t *bm, uint64_t *cnt, int combine, hipStream_t st) {
   uint64_t g = (nwords + 4 * kU - 1) / (4 * kU);
   uint32_t grid = (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
   hipLaunchKernelGGL(filter_batched_kernel<T>, dim3(grid), dim3(256), 0, st, bt, nb, nwords, (T)lo,
-                     (T)hi, bm, (unsigned long long *)cnt);
+                     (T)hi, bm, (unsigned long long *)cnt, combine);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -314,27 +342,38 @@ extern "C" int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n, uin
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-extern "C" int strom_column_filter_batched(int type, const strom_filter_batch *d_batches,
-                                           uint32_t nbatches, uint64_t nwords, double lo,
-                                           double hi, uint64_t *d_bitmap, uint64_t *d_count,
-                                           void *stream) {
+extern "C" int strom_column_filter_batched2(int type, const strom_filter_batch *d_batches,
+                                            uint32_t nbatches, uint64_t nwords, double lo,
+                                            double hi, uint64_t *d_bitmap, uint64_t *d_count,
+                                            int combine, void *stream) {
   if (!nbatches || !nwords) return 0;
   if (!d_batches || !d_bitmap || !d_count || ((uintptr_t)d_bitmap & 7)) return -22;
   hipStream_t st = (hipStream_t)stream;
   switch (type) {
-    case STROM_COL_I32: return launch_filter_batched<int32_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
-    case STROM_COL_I64: return launch_filter_batched<int64_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
-    case STROM_COL_F32: return launch_filter_batched<float>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
-    case STROM_COL_F64: return launch_filter_batched<double>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, st);
+    case STROM_COL_I32: return launch_filter_batched<int32_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, combine, st);
+    case STROM_COL_I64: return launch_filter_batched<int64_t>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, combine, st);
+    case STROM_COL_F32: return launch_filter_batched<float>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, combine, st);
+    case STROM_COL_F64: return launch_filter_batched<double>(d_batches, nbatches, nwords, lo, hi, d_bitmap, d_count, combine, st);
     default: return -22;
   }
 }
 
-extern "C" int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
-                                    const strom_filter_batch *d_batches, uint32_t nbatches,
-                                    int64_t *d_out, uint64_t *d_total, void *stream) {
+extern "C" int strom_column_filter_batched(int type, const strom_filter_batch *d_batches,
+                                           uint32_t nbatches, uint64_t nwords, double lo,
+                                           double hi, uint64_t *d_bitmap, uint64_t *d_count,
+                                           void *stream) {
+  return strom_column_filter_batched2(type, d_batches, nbatches, nwords, lo, hi, d_bitmap,
+                                      d_count, 0, stream);
+}
+
+extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwords,
+                                         const strom_filter_batch *d_batches, uint32_t nbatches,
+                                         int64_t *d_out, uint64_t *d_total,
+                                         const strom_filter_batch *d_proj, uint32_t width,
+                                         void *d_pout, uint8_t *d_pvalid, void *stream) {
   if (!nwords || !nbatches) return 0;
   if (!d_bitmap || !d_batches || !d_out || !d_total) return -22;
+  if (d_proj && ((width != 4 && width != 8) || !d_pout)) return -22;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
   if (nb64 > 0xffffffffull) return -75;
@@ -344,8 +383,22 @@ extern "C" int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
   hipLaunchKernelGGL(block_popc64_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, cnt);
   hipLaunchKernelGGL(scan_blocks_cursor_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
                      (unsigned long long *)d_total);
-  hipLaunchKernelGGL(emit_rows_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
-                     nbatches, cnt, d_out);
+  if (!d_proj)
+    hipLaunchKernelGGL(emit_rows_kernel<0>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, nullptr, nullptr, nullptr);
+  else if (width == 8)
+    hipLaunchKernelGGL(emit_rows_kernel<8>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
+  else
+    hipLaunchKernelGGL(emit_rows_kernel<4>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
   (void)hipFreeAsync(cnt, st);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
+                                    const strom_filter_batch *d_batches, uint32_t nbatches,
+                                    int64_t *d_out, uint64_t *d_total, void *stream) {
+  return strom_bitmap_to_rows_proj(d_bitmap, nwords, d_batches, nbatches, d_out, d_total, nullptr,
+                                   0, nullptr, nullptr, stream);
 }

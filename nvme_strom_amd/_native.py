@@ -216,6 +216,13 @@ _SIGS = {
                                               C.c_void_p]),
     "strom_bitmap_to_rows": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
                                        C.c_void_p, C.c_void_p, C.c_void_p]),
+    "strom_column_filter_batched2": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint64,
+                                               C.c_double, C.c_double, C.c_void_p, C.c_void_p,
+                                               C.c_int, C.c_void_p]),
+    "strom_bitmap_to_rows_proj": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]),
+    "strom_io_info": (C.c_int, [C.c_void_p]),
     "strom_file_topology": (C.c_int, [C.c_int, C.c_void_p]),
     "strom_gpu_pci_bdf": (C.c_int, [C.c_int, C.c_char_p, C.c_size_t]),
 }

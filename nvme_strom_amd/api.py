@@ -132,6 +132,14 @@ def ingest_info(device: int = 0) -> Optional[dict]:
                 outstanding=int(out[3]))
 
 
+def io_info() -> dict:
+    """Worker I/O facts: workers reading into io_uring-registered staging
+    (READ_FIXED), registrations refused, and the last refusal's errno."""
+    out = np.zeros(3, dtype=np.uint64)
+    _check(N.lib().strom_io_info(out.ctypes.data), "io_info")
+    return dict(fixed_workers=int(out[0]), fixed_refused=int(out[1]), fixed_errno=int(out[2]))
+
+
 HOST_COSTS = ("clock_gettime", "rdtsc", "fstat", "mincore", "syscall", "mutex", "cv_notify")
 
 

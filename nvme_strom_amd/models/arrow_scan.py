@@ -32,7 +32,7 @@ from __future__ import annotations
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -53,8 +53,10 @@ class ScanOut:
     indices: torch.Tensor
     seconds: Dict[str, float]
     bytes_read: int = 0           # file bytes moved storage -> HBM
-    column_bytes: int = 0         # decoded bytes of the scanned column
+    column_bytes: int = 0         # decoded bytes of the scanned columns
     groups: int = 0
+    values: Optional[torch.Tensor] = None   # projected column, one value per selected row
+    valid: Optional[torch.Tensor] = None    # its validity (uint8 0/1) when it has nulls
 
 
 @dataclass
@@ -70,8 +72,7 @@ class _Buf:
 class _Batch:
     rows: int
     row_base: int
-    data: _Buf
-    valid: Optional[_Buf]
+    cols: List[Tuple[_Buf, Optional[_Buf]]]   # per scanned column: (data, validity)
 
 
 @dataclass
@@ -81,13 +82,13 @@ class _Group:
     dec_bytes: int = 0
     words: int = 0
     # slot-relative launch tables, built once per plan (_prepare): decoder
-    # descriptors, and per batch the data/validity pointers as (kind, offset)
-    # with kind 0 none, 1 slot region, 2 decode buffer
+    # descriptors, and per batch and column the data/validity pointers as
+    # (kind, offset) with kind 0 none, 1 slot region, 2 decode buffer
     descs: Optional[np.ndarray] = None
     need: Optional[np.ndarray] = None
-    ptr_kind: Optional[np.ndarray] = None
-    ptr_rel: Optional[np.ndarray] = None
-    table: Optional[np.ndarray] = None    # (n, BATCH_FIELDS) with pointer columns 0
+    ptr_kind: Optional[np.ndarray] = None   # (n, ncols, 2)
+    ptr_rel: Optional[np.ndarray] = None    # (n, ncols, 2)
+    table: Optional[np.ndarray] = None      # (n, BATCH_FIELDS) with pointer columns 0
     column_bytes: int = 0
 
 
@@ -99,6 +100,7 @@ class _Slot:
     event: Optional[torch.cuda.Event] = None
     stream: Optional[torch.cuda.Stream] = None
     count: Optional[torch.Tensor] = None   # selected rows of the slot's group
+    junk: Optional[torch.Tensor] = None    # counts of non-final qualifiers
     err: Optional[torch.Tensor] = None     # failed decodes of the slot's group
     scratch: Optional[torch.Tensor] = None # chunk-order restore (page-cache hits)
     pending: object = None                # (CopyResult, landed ids, group)
@@ -127,49 +129,59 @@ class ArrowScan:
         self.nslots = max(2, nslots)
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
-        self._plans: Dict[str, tuple] = {}     # column -> (dtype, rows, groups)
+        self._wbs: List[Optional[torch.Tensor]] = []
+        # column tuple -> (dtypes, rows, groups)
+        self._plans: Dict[tuple, tuple] = {}
 
     # ------------------------------------------------------------- plan
-    def _plan(self, name: str) -> tuple:
-        ci = self.meta.column_index(name)
-        col = self.meta.schema[ci]
-        if not col.supported or col.numpy_dtype not in _TORCH:
-            raise NotImplementedError(f"column {name}: the GPU filter takes int32/64, float32/64")
-        width = col.bit_width // 8
+    def _plan(self, names: Sequence[str]) -> tuple:
+        cis, dtypes, widths = [], [], []
+        for name in names:
+            ci = self.meta.column_index(name)
+            col = self.meta.schema[ci]
+            if not col.supported or col.numpy_dtype not in _TORCH:
+                raise NotImplementedError(f"column {name}: the GPU filter takes int32/64, float32/64")
+            cis.append(ci)
+            dtypes.append(_TORCH[col.numpy_dtype])
+            widths.append(col.bit_width // 8)
         out, base = [], 0
         for b in self.meta.batches:
             if b.codec not in (None, "lz4_frame"):
                 raise NotImplementedError(f"body compression {b.codec} (GPU decoder: LZ4 frame)")
-            cc = b.columns[ci]
             comp = b.codec is not None
-            need = cc.length * width
-            data = _Buf(cc.data.offset, cc.data.length, need, _up64(need), comp)
-            valid = None
-            if cc.null_count and cc.validity.length:
-                vn = (cc.length + 7) // 8
-                valid = _Buf(cc.validity.offset, cc.validity.length, vn, _up64(vn) + 64, comp)
-            out.append(_Batch(cc.length, base, data, valid))
-            base += cc.length
-        return out, _TORCH[col.numpy_dtype], base
+            cols = []
+            for ci, width in zip(cis, widths):
+                cc = b.columns[ci]
+                need = cc.length * width
+                data = _Buf(cc.data.offset, cc.data.length, need, _up64(need), comp)
+                valid = None
+                if cc.null_count and cc.validity.length:
+                    vn = (cc.length + 7) // 8
+                    valid = _Buf(cc.validity.offset, cc.validity.length, vn, _up64(vn) + 64, comp)
+                cols.append((data, valid))
+            n = b.columns[cis[0]].length
+            out.append(_Batch(n, base, cols))
+            base += n
+        return out, dtypes, base
 
     def _chunks(self, b: _Batch) -> np.ndarray:
         c = self.chunk_sz
         parts = []
-        for buf in (b.data, b.valid):
-            if buf is not None and buf.length:
-                parts.append(np.arange(buf.off // c, (buf.off + buf.length + c - 1) // c))
-        return np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64)
+        for data, valid in b.cols:
+            for buf in (data, valid):
+                if buf is not None and buf.length:
+                    parts.append(np.arange(buf.off // c, (buf.off + buf.length + c - 1) // c))
+        return np.unique(np.concatenate(parts)) if parts else np.zeros(0, dtype=np.int64)
 
     def _groups(self, batches: List[_Batch]) -> List[_Group]:
         groups: List[_Group] = []
         cur: List[_Batch] = []
-        ids = np.zeros(0, dtype=np.int64)
         slot = self.slot_bytes
         # really compressed buffers (a stored-raw one is as long as its data)
-        comp = [b for b in batches
-                if b.data.compressed and 0 < b.data.length < 0.9 * b.data.need]
+        comp = [(d, v) for b in batches for d, v in b.cols
+                if d.compressed and 0 < d.length < 0.9 * d.need]
         if comp:
-            avg = sum(b.data.length + (b.valid.length if b.valid else 0) for b in comp) / len(comp)
+            avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
             slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
         limit = max(1, slot // self.chunk_sz)
         seen: set = set()            # the current group's chunk ids (linear time;
@@ -184,9 +196,8 @@ class ArrowScan:
         if cur:
             groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
         for g in groups:
-            g.dec_bytes = sum((b.data.cap if b.data.compressed else 0) +
-                              (b.valid.cap if b.valid is not None and b.valid.compressed else 0)
-                              for b in g.batches)
+            g.dec_bytes = sum(buf.cap for b in g.batches for pair in b.cols for buf in pair
+                              if buf is not None and buf.compressed)
             g.words = sum((b.rows + 63) // 64 for b in g.batches)
             self._prepare(g)
         return groups
@@ -194,26 +205,28 @@ class ArrowScan:
     def _prepare(self, g: _Group) -> None:
         c = self.chunk_sz
         n = len(g.batches)
-        kind = np.zeros((n, 2), dtype=np.int8)
-        rel = np.zeros((n, 2), dtype=np.int64)
+        ncols = len(g.batches[0].cols) if n else 0
+        kind = np.zeros((n, ncols, 2), dtype=np.int8)
+        rel = np.zeros((n, ncols, 2), dtype=np.int64)
         so, sl, do, dl, need = [], [], [], [], []
         dcur = 0
         for i, b in enumerate(g.batches):
-            for j, buf in enumerate((b.data, b.valid)):
-                if buf is None:
-                    continue
-                if buf.length == 0:
-                    kind[i, j] = 2                    # empty batch: nothing is read
-                elif buf.compressed:
-                    so.append(buf.off)
-                    sl.append(buf.length)
-                    do.append(dcur)
-                    dl.append(buf.cap)
-                    need.append(buf.need)
-                    kind[i, j], rel[i, j] = 2, dcur
-                    dcur += buf.cap
-                else:
-                    kind[i, j], rel[i, j] = 1, buf.off
+            for k, pair in enumerate(b.cols):
+                for j, buf in enumerate(pair):
+                    if buf is None:
+                        continue
+                    if buf.length == 0:
+                        kind[i, k, j] = 2             # empty batch: nothing is read
+                    elif buf.compressed:
+                        so.append(buf.off)
+                        sl.append(buf.length)
+                        do.append(dcur)
+                        dl.append(buf.cap)
+                        need.append(buf.need)
+                        kind[i, k, j], rel[i, k, j] = 2, dcur
+                        dcur += buf.cap
+                    else:
+                        kind[i, k, j], rel[i, k, j] = 1, buf.off
         # file offsets -> offsets in the slot (chunks land in id order)
         def slot_off(off):
             off = np.asarray(off, dtype=np.int64)
@@ -232,7 +245,7 @@ class ArrowScan:
         table[:, 3] = np.concatenate([[0], np.cumsum(words)[:-1]]) if n else 0
         table[:, 4] = [b.row_base for b in g.batches]
         g.table = table
-        g.column_bytes = sum(b.data.need for b in g.batches)
+        g.column_bytes = sum(d.need for b in g.batches for d, _ in b.cols)
 
     # --------------------------------------------------------- pipeline
     def _ensure_slots(self, groups: List[_Group]) -> None:
@@ -250,12 +263,16 @@ class ArrowScan:
                        torch.empty(words, dtype=torch.int64, device=self.device))
             sl.stream = torch.cuda.Stream(device=self.device)
             sl.count = torch.zeros(1, dtype=torch.int64, device=self.device)
+            sl.junk = torch.zeros(1, dtype=torch.int64, device=self.device)
             sl.err = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._slots.append(sl)
         if self.reader is None:
             self.reader = FileReader(self.path, chunk_sz=self.chunk_sz,
                                      max_chunks=nbytes // self.chunk_sz)
-        self._wbs = [host_buffer(nbytes) for _ in range(self.nslots)]
+        # pinned write-back buffers only once the BAR path is refused (a
+        # cold-scan cost otherwise: GiBs of pinned host memory per scan)
+        self._wbs = [None] * self.nslots
+        self._wb_bytes = nbytes
 
     def _submit(self, k: int, g: _Group) -> None:
         s = self._slots[k % self.nslots]
@@ -263,11 +280,22 @@ class ArrowScan:
             s.event.synchronize()            # the slot's previous group is consumed
             s.event = None
         s.keep = []
-        res, landed = self.reader.submit(s.hbm, 0, g.ids.astype(np.uint32),
-                                         wb=self._wbs[k % self.nslots])
+        wb = None
+        if self.reader._direct_ram is False:  # page-cache chunks go through host memory
+            if self._wbs[k % self.nslots] is None:
+                self._wbs[k % self.nslots] = host_buffer(self._wb_bytes)
+            wb = self._wbs[k % self.nslots]
+        res, landed = self.reader.submit(s.hbm, 0, g.ids.astype(np.uint32), wb=wb)
         s.pending = (res, landed, g)
 
-    def _compute(self, k: int, dtype, lo, hi, state) -> None:
+    @staticmethod
+    def _pointers(g: _Group, col: int, base: int, dec_base: int) -> np.ndarray:
+        t = g.table.copy()
+        kind, rel = g.ptr_kind[:, col, :], g.ptr_rel[:, col, :]
+        t[:, :2] = np.where(kind == 1, base + rel, np.where(kind == 2, dec_base + rel, 0))
+        return t
+
+    def _compute(self, k: int, quals, proj, state) -> None:
         s = self._slots[k % self.nslots]
         res, landed, g = s.pending
         s.pending = None
@@ -290,11 +318,9 @@ class ArrowScan:
                                                              res.nr_ssd), self.chunk_sz)
             base = region.data_ptr()
             dec_base = s.dec.data_ptr()
-            table = g.table.copy()
-            table[:, :2] = np.where(g.ptr_kind == 1, base + g.ptr_rel,
-                                    np.where(g.ptr_kind == 2, dec_base + g.ptr_rel, 0))
             descs = g.descs
             if descs is not None:
+                # every compressed buffer of every scanned column: one launch
                 d_desc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(
                     self.device, non_blocking=True)
                 d_need = torch.from_numpy(g.need).pin_memory().to(self.device, non_blocking=True)
@@ -303,19 +329,31 @@ class ArrowScan:
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]
-            d_table = torch.from_numpy(table).pin_memory().to(self.device, non_blocking=True)
-            filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap, s.count, stream=cs)
-            s.keep.append(d_table)
+            # the qualifier list: the first writes the bitmap, each later one
+            # ANDs into it; the last one's count is the selection's
+            for q, (col, dtype, lo, hi) in enumerate(quals):
+                tab = self._pointers(g, col, base, dec_base)
+                d_table = torch.from_numpy(tab).pin_memory().to(self.device, non_blocking=True)
+                last = q == len(quals) - 1
+                filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap,
+                               s.count if last else s.junk, stream=cs, combine=q > 0)
+                s.keep.append(d_table)
+            d_proj = None
+            if proj is not None:
+                tab = self._pointers(g, proj, base, dec_base)
+                d_proj = torch.from_numpy(tab).pin_memory().to(self.device, non_blocking=True)
+                s.keep.append(d_proj)
         # decode + filter of successive groups overlap on their slots'
-        # streams; the row-id emit runs in group order on one stream (the
-        # output cursor is shared), and frees the slot
+        # streams; the row-id emit (+ projection gather) runs in group order
+        # on one stream (the output cursor is shared), and frees the slot
         ready = torch.cuda.Event()
         ready.record(cs)
         es = self.emit_stream
         es.wait_event(ready)
         with torch.cuda.stream(es):
-            bitmap_to_rows(s.bitmap, g.words, s.keep[-1], state["out"], state["cursor"],
-                           stream=es)
+            bitmap_to_rows(s.bitmap, g.words, s.keep[-1] if d_proj is None else s.keep[-2],
+                           state["out"], state["cursor"], stream=es, proj=d_proj,
+                           proj_out=state.get("pout"), proj_valid=state.get("pvalid"))
             state["count"] += s.count
             s.count.zero_()
             if descs is not None:
@@ -326,47 +364,74 @@ class ArrowScan:
         state["bytes_read"] += len(g.ids) * self.chunk_sz
         state["column_bytes"] += g.column_bytes
 
-    def scan(self, name: str, lo, hi) -> ScanOut:
-        """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never
-        qualify)."""
+    def scan_where(self, quals: Sequence[Tuple[str, object, object]],
+                   project: Optional[str] = None) -> ScanOut:
+        """Row ids (int64, file order) where every ``lo <= column <= hi`` of
+        ``quals`` holds (nulls never qualify) — a PG-Strom qualifier list.
+        Each referenced column is read from storage and decoded once per
+        group; the per-column bitmaps are ANDed on the device.  ``project``
+        names a column whose values (and validity, when it has nulls) are
+        gathered for the selected rows while their ids are written."""
+        if not quals:
+            raise ValueError("at least one qualifier")
         t0 = time.perf_counter()
-        if name not in self._plans:               # the file's layout is fixed once opened
-            batches, dtype, nrows = self._plan(name)
-            self._plans[name] = (dtype, nrows, self._groups(batches))
-        dtype, nrows, groups = self._plans[name]
+        names: List[str] = []
+        for n in [q[0] for q in quals] + ([project] if project else []):
+            if n not in names:
+                names.append(n)
+        key = tuple(names)
+        if key not in self._plans:                # the file's layout is fixed once opened
+            batches, dtypes, nrows = self._plan(names)
+            self._plans[key] = (dtypes, nrows, self._groups(batches))
+        dtypes, nrows, groups = self._plans[key]
+        spec = [(names.index(n), dtypes[names.index(n)], lo, hi) for n, lo, hi in quals]
+        t_plan = time.perf_counter()
         out = torch.empty(max(nrows, 1), dtype=torch.int64, device=self.device)
+        pcol = names.index(project) if project else None
+        pout = pvalid = None
+        if project:
+            pout = torch.empty(max(nrows, 1), dtype=dtypes[pcol], device=self.device)
+            if any(b.cols[pcol][1] is not None for g in groups for b in g.batches):
+                pvalid = torch.empty(max(nrows, 1), dtype=torch.uint8, device=self.device)
         if not groups or nrows == 0:
-            return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0})
+            return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0},
+                           values=pout[:0] if pout is not None else None)
         self._ensure_slots(groups)
         self.emit_stream = torch.cuda.Stream(device=self.device)
         z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
         state = dict(out=out, cursor=z(), count=z(), err=z(), wait_s=0.0, bytes_read=0,
-                     column_bytes=0)
-        t_plan = time.perf_counter()
+                     column_bytes=0, pout=pout, pvalid=pvalid)
+        t_alloc = time.perf_counter()
         # depth nslots - 1 of reads ahead of the group being computed
         ahead = self.nslots - 1
         for k in range(min(ahead, len(groups))):
             self._submit(k, groups[k])
         for k in range(len(groups)):
+            self._compute(k, spec, pcol, state)
             if k + ahead < len(groups):
-                self._compute(k, dtype, lo, hi, state)
                 self._submit(k + ahead, groups[k + ahead])
-            else:
-                self._compute(k, dtype, lo, hi, state)
         torch.cuda.synchronize(self.device)
         cursor, count, err = torch.cat([state["cursor"], state["count"], state["err"]]).tolist()
         t_end = time.perf_counter()
         if err:
-            raise RuntimeError(f"LZ4 decode failed for {err} buffer(s) of column {name}")
+            raise RuntimeError(f"LZ4 decode failed for {err} buffer(s) of columns {names}")
         if cursor != count:
             raise RuntimeError(f"row emit mismatch: {cursor} ids for {count} selected")
         for s in self._slots:
             s.keep = []
             s.event = None
         return ScanOut(nrows, int(count), out[:count],
-                       {"plan_s": t_plan - t0, "wait_s": state["wait_s"], "total_s": t_end - t0},
+                       {"plan_s": t_plan - t0, "alloc_s": t_alloc - t_plan,
+                        "wait_s": state["wait_s"], "total_s": t_end - t0},
                        bytes_read=state["bytes_read"], column_bytes=state["column_bytes"],
-                       groups=len(groups))
+                       groups=len(groups),
+                       values=pout[:count] if pout is not None else None,
+                       valid=pvalid[:count] if pvalid is not None else None)
+
+    def scan(self, name: str, lo, hi) -> ScanOut:
+        """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never
+        qualify)."""
+        return self.scan_where([(name, lo, hi)])
 
     # the pre-pipeline name
     filter = scan

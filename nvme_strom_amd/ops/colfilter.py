@@ -64,9 +64,12 @@ BATCH_FIELDS = 5
 
 
 def filter_batched(dtype: torch.dtype, batches: torch.Tensor, nwords: int, lo, hi,
-                   bitmap: torch.Tensor, count: torch.Tensor, stream=None) -> None:
+                   bitmap: torch.Tensor, count: torch.Tensor, stream=None,
+                   combine: bool = False) -> None:
     """One launch over many record batches; ``count`` (int64[1] on the
-    device) accumulates the selected rows — nothing is read back."""
+    device) accumulates the selected rows — nothing is read back.
+    ``combine`` ANDs the predicate into the bitmap already there (the next
+    qualifier of a conjunction; ``count`` then counts the combined rows)."""
     if dtype not in _TYPES:
         raise ValueError(f"unsupported dtype {dtype}")
     require_cuda(batches, "batches")
@@ -75,19 +78,34 @@ def filter_batched(dtype: torch.dtype, batches: torch.Tensor, nwords: int, lo, h
         raise ValueError("batches: int64 (n, 5)")
     if bitmap.numel() < nwords:
         raise ValueError("bitmap too small")
-    check(lib().strom_column_filter_batched(_TYPES[dtype], ptr(batches), nb, nwords, float(lo),
-                                            float(hi), ptr(bitmap), ptr(count),
-                                            stream_handle(stream)), "column_filter_batched")
+    check(lib().strom_column_filter_batched2(_TYPES[dtype], ptr(batches), nb, nwords, float(lo),
+                                             float(hi), ptr(bitmap), ptr(count), int(combine),
+                                             stream_handle(stream)), "column_filter_batched")
 
 
 def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out: torch.Tensor,
-                   cursor: torch.Tensor, stream=None) -> None:
+                   cursor: torch.Tensor, stream=None, proj: Optional[torch.Tensor] = None,
+                   proj_out: Optional[torch.Tensor] = None,
+                   proj_valid: Optional[torch.Tensor] = None) -> None:
     """Append global row ids (int64) of the set bits at ``out[cursor]``;
     ``cursor`` (int64[1], device) advances — successive groups of one scan
-    fill ``out`` in order without a host round trip."""
+    fill ``out`` in order without a host round trip.  ``proj`` (a batch
+    table of another column, same batches) gathers that column's value of
+    each selected row into ``proj_out[cursor]`` (4- or 8-byte elements),
+    and its validity (0/1) into ``proj_valid`` when given."""
     require_cuda(bitmap, "bitmap")
     if out.dtype != torch.int64:
         raise ValueError("out must be int64")
-    check(lib().strom_bitmap_to_rows(ptr(bitmap), nwords, ptr(batches), batches.shape[0],
-                                     ptr(out), ptr(cursor), stream_handle(stream)),
-          "bitmap_to_rows")
+    width, pptr, vptr = 0, 0, 0
+    if proj is not None:
+        if proj_out is None or proj.shape != batches.shape:
+            raise ValueError("projection needs proj_out and a table of the same batches")
+        width = proj_out.element_size()
+        if width not in (4, 8):
+            raise ValueError("projected values are 4 or 8 bytes")
+        pptr = ptr(proj_out)
+        vptr = ptr(proj_valid) if proj_valid is not None else 0
+    check(lib().strom_bitmap_to_rows_proj(ptr(bitmap), nwords, ptr(batches), batches.shape[0],
+                                          ptr(out), ptr(cursor),
+                                          ptr(proj) if proj is not None else 0, width, pptr,
+                                          vptr, stream_handle(stream)), "bitmap_to_rows")

@@ -85,11 +85,18 @@ class FileReader:
         self.relseg_sz = relseg_sz
         self.sess = sess or api.session()
         self.info = api.check_file(self.fd, self.sess)
-        # pinned write-back buffer for page-cache chunks (one per reader);
-        # unused while the engine can write them into HBM itself (BAR)
-        self._wb = host_buffer(max_chunks * chunk_sz)
+        # pinned write-back buffer for page-cache chunks (one per reader),
+        # allocated on first use: unused while the engine can write them
+        # into HBM itself (BAR), and pinning it is a large part of a cold scan
+        self._wb_t: Optional[torch.Tensor] = None
         self.max_chunks = max_chunks
         self._direct_ram = None if direct_ram else False
+
+    @property
+    def _wb(self) -> torch.Tensor:
+        if self._wb_t is None:
+            self._wb_t = host_buffer(self.max_chunks * self.chunk_sz)
+        return self._wb_t
 
     @property
     def nchunks(self) -> int:

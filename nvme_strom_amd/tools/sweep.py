@@ -52,6 +52,20 @@ def _mk(path: str, nbytes: int) -> None:
         os.fsync(f.fileno())
 
 
+def _summary(rows, ab):
+    """Median GiB/s, IOPS and p50 per (block, arm) over the repetitions."""
+    out = {}
+    for r in rows:
+        out.setdefault((r["block"], r.get(ab) if ab else None), []).append(r)
+    res = []
+    for (b, v), rs in sorted(out.items(), key=lambda kv: (kv[0][0], kv[0][1] or 0)):
+        med = lambda k: float(np.median([x[k] for x in rs]))
+        res.append(dict(block=b, arm=v, n=len(rs), GiBps=round(med("GiBps"), 2),
+                        iops=round(med("iops")), p50_us=round(med("p50_us"), 2),
+                        p99_us=round(med("p99_us"), 2)))
+    return res
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--file-gib", type=float, default=2.0)
@@ -66,6 +80,7 @@ def main(argv=None) -> int:
     ap.add_argument("--engine-only", action="store_true",
                     help="backend=cache: page-cache reads through the full engine path")
     ap.add_argument("--ab", default="", help="config key to A/B (0 vs 1) at every size")
+    ap.add_argument("--reps", type=int, default=1, help="repetitions of every (size, arm)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
 
@@ -97,7 +112,9 @@ def main(argv=None) -> int:
                 pass
     rows = []
     sizes = [size(x) for x in a.blocks.split(",")]
-    runs = [(B, v) for B in sizes for v in ((0, 1) if a.ab else (None,))]
+    # interleaved arms, --reps times each (the box's storage drifts)
+    runs = [(B, v) for B in sizes for _ in range(a.reps)
+            for v in ((0, 1) if a.ab else (None,))]
     try:
         for B, abv in runs:
             kv = {"max_request": B}
@@ -141,6 +158,8 @@ def main(argv=None) -> int:
                 row.update(raw_iops=round(riops), raw_GiBps=round(rgib, 2),
                            raw_random_GiBps=round(rgib_rand, 2),
                            of_raw=round(gibs / rgib, 3) if rgib else None)
+            if a.ab:
+                row["io"] = S.io_info()
             rows.append(row)
             _log(json.dumps(row))
             ld.close()
@@ -150,7 +169,7 @@ def main(argv=None) -> int:
     out = dict(workers=int(S.config_get("workers")), queue_depth=a.qd or int(defaults["queue_depth"]),
                backend="cache (engine only: storage removed)" if a.engine_only
                else S.config_get("backend"), file_bytes=F, ab=a.ab or None,
-               fixed_bufs_workers=S.stat_info().get("nr_debug4"), rows=rows)
+               io=S.io_info(), rows=rows, summary=_summary(rows, a.ab))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(out, f, indent=1)

@@ -86,6 +86,21 @@ def test_arrow_scan_lz4(S, tmp_path):
         out = sc.filter("b", 0.25, 0.5)
         ref = np.nonzero((b >= 0.25) & (b <= 0.5) & ~mask)[0]
         assert np.array_equal(out.indices.cpu().numpy(), ref)
+        # a qualifier list over two columns (each read and decoded once,
+        # bitmaps ANDed on the device) + a projected third column
+        sel = (a >= -500_000) & (a <= 200_000) & (b >= 0.1) & (b <= 0.6) & ~mask
+        ref = np.nonzero(sel)[0]
+        out = sc.scan_where([("a", -500_000, 200_000), ("b", 0.1, 0.6)], project="a")
+        assert out.selected == len(ref)
+        assert np.array_equal(out.indices.cpu().numpy(), ref)
+        assert np.array_equal(out.values.cpu().numpy(), a[ref])
+        # projecting a column with nulls returns its validity too
+        out = sc.scan_where([("a", -500_000, 200_000)], project="b")
+        ref = np.nonzero((a >= -500_000) & (a <= 200_000))[0]
+        assert np.array_equal(out.indices.cpu().numpy(), ref)
+        v = out.valid.cpu().numpy().astype(bool)
+        assert np.array_equal(v, ~mask[ref])
+        assert np.array_equal(out.values.cpu().numpy()[v], b[ref][v])
         sc.close()
 
 
