@@ -58,6 +58,8 @@ def make_file(path: str, rows: int, batch_rows: int, seed: int = 7) -> None:
             mask = rng.random(n) < 0.05
             w.write_batch(pa.record_batch([pa.array(ids), pa.array(val),
                                            pa.array(x, mask=mask)], schema=schema))
+            if (b0 // batch_rows) % 256 == 255:
+                _log(f"writing {b0 + n}/{rows} rows")
     os.replace(tmp, path)
 
 
