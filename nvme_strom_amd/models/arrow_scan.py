@@ -94,7 +94,8 @@ class _Group:
 
 @dataclass
 class _Slot:
-    hbm: HbmBuffer
+    off: int                               # byte offset of the slot in the ring buffer
+    cap: int                               # slot bytes
     dec: torch.Tensor
     bitmap: torch.Tensor
     event: Optional[torch.cuda.Event] = None
@@ -116,6 +117,7 @@ class ArrowScan:
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
     # to fill the GPU, so compressed groups grow to hold that many buffers
     TARGET_STREAMS = 8192
+    MIN_STREAMS = 512              # per group, before splitting for overlap
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -175,24 +177,47 @@ class ArrowScan:
 
     def _groups(self, batches: List[_Batch]) -> List[_Group]:
         groups: List[_Group] = []
-        cur: List[_Batch] = []
         slot = self.slot_bytes
         # really compressed buffers (a stored-raw one is as long as its data)
         comp = [(d, v) for b in batches for d, v in b.cols
                 if d.compressed and 0 < d.length < 0.9 * d.need]
         if comp:
+            # the decoder runs one stream per buffer: a group needs thousands
+            # of them to fill the GPU, but the column is also cut into at
+            # least nslots groups when that still leaves ~1,000 streams each,
+            # so group g's decode overlaps the reads of g+1.. and the decodes
+            # of successive groups run concurrently on their slot streams
             avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
-            slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
+            total = sum(d.length + (v.length if v else 0) for d, v in comp)
+            want = avg * self.TARGET_STREAMS
+            if len(comp) >= self.nslots * self.MIN_STREAMS:
+                want = min(want, total / self.nslots)
+            slot = int(min(self.max_slot_bytes, max(slot, want)))
         limit = max(1, slot // self.chunk_sz)
-        seen: set = set()            # the current group's chunk ids (linear time;
-        for b in batches:            # a running np.union1d was quadratic in batches)
-            mine = self._chunks(b).tolist()
-            fresh = [c for c in mine if c not in seen]
+        # chunk ranges of every batch at once (vectorised: the qualifier-list
+        # plans touch several buffers per batch)
+        c = self.chunk_sz
+        spans = []                     # (batch index, first chunk, end chunk)
+        for i, b in enumerate(batches):
+            for data, valid in b.cols:
+                for buf in (data, valid):
+                    if buf is not None and buf.length:
+                        spans.append((i, buf.off // c, (buf.off + buf.length + c - 1) // c))
+        cur: List[_Batch] = []
+        seen: set = set()              # the current group's chunk ids
+        sp = np.array(spans, dtype=np.int64).reshape(-1, 3)
+        bounds = np.searchsorted(sp[:, 0], np.arange(len(batches) + 1)) if len(sp) else None
+        for i, b in enumerate(batches):
+            mine: set = set()
+            if bounds is not None:
+                for _, lo, hi in sp[bounds[i]:bounds[i + 1]]:
+                    mine.update(range(int(lo), int(hi)))
+            fresh = mine - seen
             if cur and len(seen) + len(fresh) > limit:
                 groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
                 cur, seen, fresh = [], set(), mine
             cur.append(b)
-            seen.update(fresh)
+            seen |= fresh
         if cur:
             groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
         for g in groups:
@@ -252,13 +277,16 @@ class ArrowScan:
         nbytes = max(len(g.ids) for g in groups) * self.chunk_sz
         dec = max(max(g.dec_bytes for g in groups), 64)
         words = max(max(g.words for g in groups), 1)
-        if self._slots and (self._slots[0].hbm.nbytes >= nbytes and
+        if self._slots and (self._slots[0].cap >= nbytes and
                             self._slots[0].dec.numel() >= dec and
                             self._slots[0].bitmap.numel() >= words):
             return
         self._free_slots()
-        for _ in range(self.nslots):
-            sl = _Slot(HbmBuffer(nbytes, self.device),
+        # one registered HBM ring for every slot: one MAP (dma-buf export +
+        # BAR mapping) per scan object instead of one per slot (cold cost)
+        self._hbm = HbmBuffer(nbytes * self.nslots, self.device)
+        for k in range(self.nslots):
+            sl = _Slot(k * nbytes, nbytes,
                        torch.empty(dec, dtype=torch.uint8, device=self.device),
                        torch.empty(words, dtype=torch.int64, device=self.device))
             sl.stream = torch.cuda.Stream(device=self.device)
@@ -285,7 +313,7 @@ class ArrowScan:
             if self._wbs[k % self.nslots] is None:
                 self._wbs[k % self.nslots] = host_buffer(self._wb_bytes)
             wb = self._wbs[k % self.nslots]
-        res, landed = self.reader.submit(s.hbm, 0, g.ids.astype(np.uint32), wb=wb)
+        res, landed = self.reader.submit(self._hbm, s.off, g.ids.astype(np.uint32), wb=wb)
         s.pending = (res, landed, g)
 
     @staticmethod
@@ -302,7 +330,7 @@ class ArrowScan:
         t0 = time.perf_counter()
         self.reader.finish(res)
         state["wait_s"] += time.perf_counter() - t0
-        region = s.hbm.tensor[:len(g.ids) * self.chunk_sz]
+        region = self._hbm.tensor[s.off:s.off + len(g.ids) * self.chunk_sz]
         # write-back copies of page-cache chunks (FileReader.submit without a
         # BAR) were queued on the current stream
         cs = s.stream
@@ -311,7 +339,7 @@ class ArrowScan:
             if res.nr_ram and not np.array_equal(landed, g.ids.astype(np.uint32)):
                 # page-cache chunks landed at the tail: restore chunk order
                 if s.scratch is None:
-                    s.scratch = torch.empty(s.hbm.nbytes, dtype=torch.uint8, device=self.device)
+                    s.scratch = torch.empty(s.cap, dtype=torch.uint8, device=self.device)
                 tmp = s.scratch[:region.numel()]
                 tmp.copy_(region)
                 chunk_scatter(tmp, region, landing_positions(g.ids.astype(np.uint32), landed,
@@ -437,8 +465,8 @@ class ArrowScan:
     filter = scan
 
     def _free_slots(self) -> None:
-        for s in self._slots:
-            s.hbm.close()
+        if self._slots:
+            self._hbm.close()
         self._slots = []
 
     def close(self) -> None:
