@@ -117,7 +117,6 @@ class ArrowScan:
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
     # to fill the GPU, so compressed groups grow to hold that many buffers
     TARGET_STREAMS = 8192
-    MIN_STREAMS = 512              # per group, before splitting for overlap
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -183,16 +182,12 @@ class ArrowScan:
                 if d.compressed and 0 < d.length < 0.9 * d.need]
         if comp:
             # the decoder runs one stream per buffer: a group needs thousands
-            # of them to fill the GPU, but the column is also cut into at
-            # least nslots groups when that still leaves ~1,000 streams each,
-            # so group g's decode overlaps the reads of g+1.. and the decodes
-            # of successive groups run concurrently on their slot streams
+            # of them to fill the GPU.  (Cutting a 2,048-stream column into 3
+            # groups to overlap reads with decodes measured slower, 72 -> 83-
+            # 125 ms, profiles/r3/arrow_split3.json: each launch still takes
+            # one stream's serial time and the launches did not overlap.)
             avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
-            total = sum(d.length + (v.length if v else 0) for d, v in comp)
-            want = avg * self.TARGET_STREAMS
-            if len(comp) >= self.nslots * self.MIN_STREAMS:
-                want = min(want, total / self.nslots)
-            slot = int(min(self.max_slot_bytes, max(slot, want)))
+            slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
         limit = max(1, slot // self.chunk_sz)
         # chunk ranges of every batch at once (vectorised: the qualifier-list
         # plans touch several buffers per batch)
