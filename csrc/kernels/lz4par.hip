@@ -1,0 +1,632 @@
+// lz4par.hip — LZ4 decode with parallelism INSIDE a stream, for few long
+// streams (BASELINE config 5: pyarrow writes each 512 KiB column buffer as
+// one LZ4 frame of linked 64 KiB blocks, so a 134M-row column is only 2,048
+// streams and decompress.hip — one stream per lane group, parse serial —
+// leaves most of the chip idle: 27.5 GB/s, profiles/r2/dec/SUMMARY.md).
+//
+// One workgroup of NT threads per stream.  The compressed input is taken in
+// windows of PW bytes that start on a known token:
+//
+//  1. speculative parse: thread t follows the token chain from the start of
+//     its SL-byte slice, marking token starts in an LDS bitmap, up to its
+//     exit (first token at or past the slice end).  Chains from wrong
+//     starts merge into the true chain within a few tokens.
+//  2. validation: slice t is right when its true entry (slice t-1's exit)
+//     is one of its marked tokens; the few that are not re-parse from the
+//     true entry, in rounds, until nothing changes (correct for any input,
+//     fast when chains merge — the usual case).
+//  3. every thread walks its true sequences: output bytes -> block scan ->
+//     each slice's output start.
+//  4. output in batches of OB bytes: a source pointer per output byte
+//     (literal byte: its input position; match byte: the byte `off` back —
+//     "history" when that lies before the batch, already stored), then
+//     pointer doubling p = ptr[p] until every pointer is a literal or
+//     history root (chain depth d resolves in log2 d rounds; the r2 replay,
+//     tools/lz4_pointer_jump_sim.py, measured <= 7 rounds for 4 KiB), then
+//     one gather per byte, dword stores.
+//
+// Matches reaching into earlier batches, windows or linked blocks read the
+// stream's own stored output back with L1-bypassing loads after a
+// workgroup release fence (the stores are this workgroup's, on this XCD).
+//
+// The phases are plain functions of (shared state, thread id); the kernel
+// runs them with barriers between, strom_lz4par_host() runs the SAME
+// functions thread by thread on the CPU (tests/test_codecs_cpu.py pins it
+// against the host LZ4 codec and pyarrow's frames).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "strom/strom.h"
+
+#define HD __host__ __device__ inline
+
+namespace lz4p {
+
+constexpr uint32_t NT = 256;             // threads per stream (4 waves)
+constexpr uint32_t PW = 16384;           // compressed bytes per parse window
+constexpr uint32_t SL = PW / NT;         // slice per thread (64 B = 2 bitmap words)
+constexpr uint32_t PAD = 64;             // window overhang (reads past the window end)
+constexpr uint32_t OB = 8192;            // output bytes per resolve batch
+#ifndef LZ4PAR_LOOKBACK
+#define LZ4PAR_LOOKBACK 512
+#endif
+// a speculative chain starts this many bytes before its slice (its bits
+// are recorded from the slice start on): a chain from a wrong start needs
+// ~100 bytes to fall onto the true token grid on int columns, and a slice
+// whose chain has not merged by its true entry costs a serial fix-up round
+constexpr uint32_t LB = LZ4PAR_LOOKBACK;
+constexpr uint32_t kLit = 0x80000000u;   // pointer tag: literal, input position
+constexpr uint32_t kHist = 0x40000000u;  // pointer tag: stored output position
+constexpr uint32_t kTag = kLit | kHist;
+constexpr uint32_t kPosMax = 1u << 30;   // streams and outputs below 1 GiB
+static_assert(SL % 32 == 0, "slices cover whole bitmap words");
+
+enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3 };
+enum : uint32_t { kModeBlock = 0, kModeDone = 1 };
+
+struct Smem {
+  uint8_t win[PW + PAD];
+  uint32_t bits[PW / 32];
+  uint32_t ex[NT];       // exit of slice t's chain
+  uint32_t en[NT];       // true entry of slice t
+  uint32_t olen[NT];     // output bytes of slice t's true sequences
+  uint32_t ost[NT];      // inclusive prefix of olen
+  uint32_t ptr[OB];
+  // stream scalars (thread 0 writes, everyone reads after a barrier)
+  uint32_t ip;           // input position of the next block header
+  uint32_t bstart, bend; // current block
+  uint32_t braw;         // current block stored uncompressed
+  uint32_t ws, wend, wload;   // window start (a true token), parse end, bytes in win
+  uint32_t op;           // output bytes so far
+  uint32_t total;        // output bytes of the current window
+  int32_t err;
+  uint32_t mode;
+  uint32_t bcs;          // 4-byte checksum after each block
+  uint32_t raw_block;    // codec LZ4: the whole input is one block
+};
+
+struct Ctx {
+  const uint8_t *in;
+  uint8_t *out;
+  uint32_t len;          // input bytes
+  uint32_t cap;          // output capacity
+};
+
+// ---------------------------------------------------------------- input
+HD uint8_t inb(const Smem &s, const Ctx &c, uint32_t p) {
+  const uint32_t r = p - s.ws;
+  if (r < s.wload) return s.win[r];
+  return p < c.len ? c.in[p] : 0;
+}
+
+HD uint32_t rd32(const Ctx &c, uint32_t p) {
+  if (p + 4 > c.len) return 0xffffffffu;
+  return (uint32_t)c.in[p] | ((uint32_t)c.in[p + 1] << 8) | ((uint32_t)c.in[p + 2] << 16) |
+         ((uint32_t)c.in[p + 3] << 24);
+}
+
+struct Seq {
+  uint32_t lit0, lit, off, mlen, next;
+  bool last;
+};
+
+// One LZ4 sequence at p (block ends at bend).  false: malformed (for a
+// speculative chain that just means "wrong start").
+HD bool parse(const Smem &s, const Ctx &c, uint32_t p, uint32_t bend, Seq &q) {
+  const uint32_t tok = inb(s, c, p);
+  uint32_t x = p + 1;
+  uint32_t lit = tok >> 4;
+  if (lit == 15) {
+    uint32_t b;
+    do {
+      b = inb(s, c, x);
+      ++x;
+      lit += b;
+    } while (b == 255 && x < bend);
+  }
+  q.lit0 = x;
+  q.lit = lit;
+  const uint64_t le = (uint64_t)x + lit;
+  if (le >= bend) {                      // the last sequence: literals only
+    q.last = true;
+    q.off = 0;
+    q.mlen = 0;
+    q.next = bend;
+    return le == bend;
+  }
+  x = (uint32_t)le;
+  q.off = (uint32_t)inb(s, c, x) | ((uint32_t)inb(s, c, x + 1) << 8);
+  x += 2;
+  uint32_t m = tok & 15;
+  if (m == 15) {
+    uint32_t b;
+    do {
+      b = inb(s, c, x);
+      ++x;
+      m += b;
+    } while (b == 255 && x < bend);
+  }
+  q.mlen = m + 4;
+  q.last = false;
+  q.next = x < bend ? x : bend;
+  return x < bend && q.off != 0;         // a match is never the block's end
+}
+
+HD void setbit(Smem &s, uint32_t p) {
+  const uint32_t r = p - s.ws;
+  s.bits[r >> 5] |= 1u << (r & 31);
+}
+
+HD bool getbit(const Smem &s, uint32_t p) {
+  const uint32_t r = p - s.ws;
+  return (s.bits[r >> 5] >> (r & 31)) & 1u;
+}
+
+HD uint32_t slice_lo(const Smem &s, uint32_t t) { return s.ws + t * SL; }
+HD uint32_t slice_hi(const Smem &s, uint32_t t) {
+  const uint32_t e = s.ws + (t + 1) * SL;
+  return e < s.wend ? e : s.wend;
+}
+
+// ---------------------------------------------------------------- phases
+// window load: input bytes [ws, ws + wload) into LDS
+HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
+  for (uint32_t i = t; i < s.wload; i += NT) s.win[i] = c.in[s.ws + i];
+}
+
+// (1) speculative chain of slice t
+HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  s.bits[2 * t] = 0;
+  s.bits[2 * t + 1] = 0;
+  if (lo >= hi) {
+    s.ex[t] = lo;
+    return;
+  }
+  uint32_t p = lo - s.ws > LB ? lo - LB : s.ws;   // the window start is a true token
+  Seq q;
+  while (p < hi) {
+    if (p >= lo) setbit(s, p);
+    parse(s, c, p, s.bend, q);
+    p = q.next;
+  }
+  s.ex[t] = p;
+}
+
+// (2) validation round, read half: the entry slice t sees now
+HD uint32_t ph_entry(const Smem &s, uint32_t t) { return t == 0 ? s.ws : s.ex[t - 1]; }
+
+// (2) validation round, fix half: true when slice t had to re-parse
+HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  if (lo >= hi) return false;
+  s.en[t] = ent;
+  bool valid;
+  if (ent < hi) {
+    valid = getbit(s, ent);
+  } else {
+    valid = s.bits[2 * t] == 0 && s.bits[2 * t + 1] == 0 && s.ex[t] == ent;
+  }
+  if (valid) return false;
+  s.bits[2 * t] = 0;
+  s.bits[2 * t + 1] = 0;
+  uint32_t p = ent;
+  Seq q;
+  while (p < hi) {
+    setbit(s, p);
+    parse(s, c, p, s.bend, q);
+    p = q.next;
+  }
+  s.ex[t] = p;
+  return true;
+}
+
+// (3) output bytes of slice t's true sequences (errors set s.err)
+HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  uint32_t o = 0;
+  if (lo < hi) {
+    uint32_t p = s.en[t];
+    Seq q;
+    while (p < hi) {
+      if (!parse(s, c, p, s.bend, q)) {
+        s.err = kErrFormat;
+        break;
+      }
+      const uint64_t n = (uint64_t)o + q.lit + q.mlen;
+      if (n >= kPosMax) {
+        s.err = kErrOverflow;
+        break;
+      }
+      o = (uint32_t)n;
+      p = q.next;
+    }
+  }
+  s.olen[t] = o;
+  s.ost[t] = o;
+}
+
+// (3) inclusive scan step d (Hillis-Steele; read and write halves)
+HD uint32_t ph_scan_read(const Smem &s, uint32_t t, uint32_t d) { return t >= d ? s.ost[t - d] : 0; }
+HD void ph_scan_write(Smem &s, uint32_t t, uint32_t v) { s.ost[t] += v; }
+
+// (4a) source pointers of the batch [b0, b0 + OB) for slice t's sequences
+HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  if (lo >= hi) return;
+  const uint32_t o1 = s.ost[t], o0 = o1 - s.olen[t];
+  const uint32_t b1 = b0 + OB;
+  if (o1 <= b0 || o0 >= b1) return;
+  const uint32_t opw = s.op;             // output position of the window start
+  uint32_t p = s.en[t], o = o0;
+  Seq q;
+  while (p < hi && o < b1) {
+    parse(s, c, p, s.bend, q);           // checked by ph_count
+    const uint32_t le = o + q.lit;
+    if (le > b0) {
+      const uint32_t x0 = o > b0 ? o : b0, x1 = le < b1 ? le : b1;
+      for (uint32_t x = x0; x < x1; ++x) s.ptr[x - b0] = kLit | (q.lit0 + (x - o));
+    }
+    o = le;
+    if (!q.last) {
+      const uint32_t me = o + q.mlen;
+      if (me > b0 && o < b1) {
+        if ((uint64_t)q.off > (uint64_t)opw + o) {
+          s.err = kErrDistance;
+          return;
+        }
+        const uint32_t x0 = o > b0 ? o : b0, x1 = me < b1 ? me : b1;
+        for (uint32_t x = x0; x < x1; ++x) {
+          const uint32_t src = opw + x - q.off;            // absolute output position
+          s.ptr[x - b0] = src < opw + b0 ? (kHist | src) : (x - q.off - b0);
+        }
+      }
+      o = me;
+    }
+    p = q.next;
+  }
+}
+
+// (4b) one pointer-doubling round over the batch; true while any pointer
+// still points inside the batch
+HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
+  bool more = false;
+  for (uint32_t e = t; e < nb; e += NT) {
+    const uint32_t v = s.ptr[e];
+    if (!(v & kTag)) {
+      const uint32_t w = s.ptr[v];
+      s.ptr[e] = w;
+      more |= !(w & kTag);
+    }
+  }
+  return more;
+}
+
+HD uint8_t hist_byte(const Ctx &c, uint32_t pos) {
+#ifdef __HIP_DEVICE_COMPILE__
+  // stored by this workgroup in an earlier batch, visible after the
+  // release fence + barrier that ended it; bypass L1 (it may hold an older
+  // copy of the line)
+  const uint32_t *w = (const uint32_t *)(((uintptr_t)(c.out + pos)) & ~(uintptr_t)3);
+  const uint32_t d = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(d >> (8 * (((uintptr_t)(c.out + pos)) & 3)));
+#else
+  return c.out[pos];
+#endif
+}
+
+HD uint8_t resolve(const Smem &s, const Ctx &c, uint32_t v) {
+  if (v & kLit) return inb(s, c, v & ~kLit);
+  return hist_byte(c, v & ~kHist);
+}
+
+// (4c) gather + store: thread t owns aligned output dwords
+HD void ph_store(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb) {
+  uint8_t *base = c.out + s.op + b0;
+  const uint32_t mis = (uint32_t)((uintptr_t)base & 3);
+  const uint32_t nw = (nb + mis + 3) / 4;
+  for (uint32_t k = t; k < nw; k += NT) {
+    const int32_t e0 = (int32_t)(4 * k) - (int32_t)mis;
+    if (e0 >= 0 && (uint32_t)e0 + 4 <= nb) {
+      uint32_t w = 0;
+      for (uint32_t j = 0; j < 4; ++j) w |= (uint32_t)resolve(s, c, s.ptr[e0 + j]) << (8 * j);
+      *(uint32_t *)(base + e0) = w;
+    } else {
+      for (int32_t j = 0; j < 4; ++j) {
+        const int32_t e = e0 + j;
+        if (e >= 0 && (uint32_t)e < nb) base[e] = resolve(s, c, s.ptr[e]);
+      }
+    }
+  }
+}
+
+// stored (uncompressed) block: [bstart, bend) -> out[op..]
+HD void ph_rawcopy(Smem &s, const Ctx &c, uint32_t t) {
+  const uint32_t n = s.bend - s.bstart;
+  for (uint32_t i = t; i < n; i += NT) c.out[s.op + i] = c.in[s.bstart + i];
+}
+
+// ---------------------------------------------------------------- scalar steps (thread 0)
+// stream header: sets ip / bcs / raw_block, or mode done with op = bytes copied
+HD void st_header(Smem &s, const Ctx &c, int codec) {
+  s.op = 0;
+  s.err = 0;
+  s.mode = kModeBlock;
+  s.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
+  s.raw_block = codec == STROM_CODEC_LZ4;
+  s.ip = 0;
+  s.ws = 0;
+  s.wload = 0;
+  if (c.len >= kPosMax || c.cap >= kPosMax) {
+    s.err = kErrOverflow;
+    s.mode = kModeDone;
+    return;
+  }
+  if (codec != STROM_CODEC_ARROW_LZ4) return;
+  if (c.len < 8) {
+    s.err = kErrFormat;
+    s.mode = kModeDone;
+    return;
+  }
+  const uint32_t lo = rd32(c, 0), hi = rd32(c, 4);
+  if (lo == 0xffffffffu && hi == 0xffffffffu) {   // -1: stored raw after the prefix
+    s.bstart = 8;
+    s.bend = c.len;
+    s.braw = 1;
+    s.raw_block = 2;                              // one stored block, then done
+    return;
+  }
+  uint32_t p = 8;
+  if (rd32(c, p) != 0x184D2204u || p + 7 > c.len) {
+    s.err = kErrFormat;
+    s.mode = kModeDone;
+    return;
+  }
+  const uint32_t flg = c.in[p + 4];
+  if ((flg >> 6) != 1) {
+    s.err = kErrFormat;
+    s.mode = kModeDone;
+    return;
+  }
+  p += 6;                                         // magic, FLG, BD
+  if (flg & 0x08) p += 8;                         // content size
+  if (flg & 0x01) p += 4;                         // dictionary id
+  p += 1;                                         // header checksum
+  s.bcs = (flg >> 4) & 1;
+  s.ip = p;
+}
+
+// next block: sets bstart/bend/braw, or mode done
+HD void st_block(Smem &s, const Ctx &c) {
+  if (s.raw_block == 1) {                         // codec LZ4: one raw block
+    s.raw_block = 3;
+    s.bstart = 0;
+    s.bend = c.len;
+    s.braw = 0;
+    return;
+  }
+  if (s.raw_block == 2) {                         // Arrow "-1": the stored copy
+    s.raw_block = 3;
+    return;
+  }
+  if (s.raw_block == 3) {
+    s.mode = kModeDone;
+    return;
+  }
+  const uint32_t h = rd32(c, s.ip);
+  if (h == 0xffffffffu && s.ip + 4 > c.len) {     // ran off the input: no end mark
+    s.mode = kModeDone;
+    return;
+  }
+  if (h == 0) {                                   // end mark
+    s.mode = kModeDone;
+    return;
+  }
+  const uint32_t n = h & 0x7fffffffu;
+  const uint64_t end = (uint64_t)s.ip + 4 + n;
+  if (end > c.len) {
+    s.err = kErrFormat;
+    s.mode = kModeDone;
+    return;
+  }
+  s.bstart = s.ip + 4;
+  s.bend = (uint32_t)end;
+  s.braw = h >> 31;
+  s.ip = s.bend + (s.bcs ? 4 : 0);
+}
+
+HD void st_window(Smem &s, const Ctx &c, uint32_t ws) {
+  s.ws = ws;
+  const uint32_t we = ws + PW;
+  s.wend = we < s.bend ? we : s.bend;
+  const uint32_t ld = PW + PAD;
+  s.wload = ws + ld <= c.len ? ld : c.len - ws;
+}
+
+}  // namespace lz4p
+
+// ---------------------------------------------------------------- device
+namespace {
+using namespace lz4p;
+
+__global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__restrict__ src,
+                                                    uint8_t *__restrict__ dst,
+                                                    const strom_decomp_desc *__restrict__ desc,
+                                                    uint32_t nstreams, int32_t *status) {
+  __shared__ __attribute__((aligned(16))) Smem s;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t b = blockIdx.x; b < nstreams; b += gridDim.x) {
+    const strom_decomp_desc d = desc[b];
+    Ctx c{src + d.src_off, dst + d.dst_off, d.src_len, d.dst_len};
+    if (t == 0) st_header(s, c, codec);
+    __syncthreads();
+    for (;;) {
+      if (t == 0 && s.mode != kModeDone) st_block(s, c);
+      __syncthreads();
+      if (s.mode == kModeDone || s.err) break;
+      if (s.braw) {
+        const uint64_t n = s.bend - s.bstart;
+        if ((uint64_t)s.op + n > c.cap) {
+          if (t == 0) s.err = kErrOverflow;
+          __syncthreads();
+          break;
+        }
+        ph_rawcopy(s, c, t);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if (t == 0) s.op += (uint32_t)n;
+        __syncthreads();
+        continue;
+      }
+      uint32_t ws = s.bstart;
+      while (ws < s.bend && !s.err) {
+        if (t == 0) st_window(s, c, ws);
+        __syncthreads();
+        ph_load(s, c, t);
+        __syncthreads();
+        ph_spec(s, c, t);
+        __syncthreads();
+        bool changed;
+        do {
+          const uint32_t ent = ph_entry(s, t);
+          __syncthreads();
+          changed = ph_fix(s, c, t, ent);
+        } while (__syncthreads_or(changed));
+        ph_count(s, c, t);
+        for (uint32_t dd = 1; dd < NT; dd <<= 1) {
+          __syncthreads();
+          const uint32_t v = ph_scan_read(s, t, dd);
+          __syncthreads();
+          ph_scan_write(s, t, v);
+        }
+        __syncthreads();
+        if (t == 0) {
+          s.total = s.ost[NT - 1];
+          if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
+        }
+        __syncthreads();
+        if (s.err) break;
+        const uint32_t total = s.total;
+        for (uint32_t b0 = 0; b0 < total; b0 += OB) {
+          const uint32_t nb = total - b0 < OB ? total - b0 : OB;
+          ph_fill(s, c, t, b0);
+          __syncthreads();
+          if (s.err) break;
+          while (__syncthreads_or(ph_double(s, t, nb))) {
+          }
+          ph_store(s, c, t, b0, nb);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __syncthreads();
+        }
+        // the next window starts at the last slice's true exit
+        const uint32_t last = (s.wend - s.ws + SL - 1) / SL - 1;
+        ws = s.ex[last];
+        __syncthreads();
+        if (t == 0) s.op += total;
+        __syncthreads();
+      }
+      __syncthreads();
+      if (s.err) break;
+    }
+    if (t == 0) status[b] = s.err ? s.err : (int32_t)s.op;
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// Few long LZ4 streams (raw blocks, frames, Arrow IPC buffers): one
+// workgroup per stream, parallel parse + pointer-doubling resolve.
+extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
+                                    const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                    int32_t *d_status, void *stream) {
+  if (codec != STROM_CODEC_LZ4 && codec != STROM_CODEC_LZ4_FRAME &&
+      codec != STROM_CODEC_LZ4_FRAME_BCS && codec != STROM_CODEC_ARROW_LZ4)
+    return -22;
+  if (!nstreams) return 0;
+  const uint32_t grid = nstreams < 65535 ? nstreams : 65535;
+  hipLaunchKernelGGL(lz4par_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
+                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The same phases run thread by thread on the CPU: the algorithm's
+// reference (tests/test_codecs_cpu.py), no GPU involved.  Returns decoded
+// bytes or a negative error as the kernel's status.
+extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
+                                 uint32_t cap, uint32_t *stats) {
+  using namespace lz4p;
+  static_assert(sizeof(Smem) < 64 * 1024, "LDS");
+  Smem *sp = new Smem;
+  Smem &s = *sp;
+  Ctx c{src, dst, src_len, cap};
+  uint32_t ent[NT];
+  bool flag[NT];
+  uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0;
+  st_header(s, c, codec);
+  for (;;) {
+    if (s.mode != kModeDone) st_block(s, c);
+    if (s.mode == kModeDone || s.err) break;
+    if (s.braw) {
+      if ((uint64_t)s.op + (s.bend - s.bstart) > c.cap) {
+        s.err = kErrOverflow;
+        break;
+      }
+      for (uint32_t t = 0; t < NT; ++t) ph_rawcopy(s, c, t);
+      s.op += s.bend - s.bstart;
+      continue;
+    }
+    uint32_t ws = s.bstart;
+    while (ws < s.bend && !s.err) {
+      ++windows;
+      st_window(s, c, ws);
+      for (uint32_t t = 0; t < NT; ++t) ph_load(s, c, t);
+      for (uint32_t t = 0; t < NT; ++t) ph_spec(s, c, t);
+      bool any;
+      do {
+        ++rounds;
+        for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_entry(s, t);
+        any = false;
+        for (uint32_t t = 0; t < NT; ++t) {
+          flag[t] = ph_fix(s, c, t, ent[t]);
+          any |= flag[t];
+          fixes += flag[t];
+        }
+      } while (any);
+      for (uint32_t t = 0; t < NT; ++t) ph_count(s, c, t);
+      for (uint32_t dd = 1; dd < NT; dd <<= 1) {
+        for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_scan_read(s, t, dd);
+        for (uint32_t t = 0; t < NT; ++t) ph_scan_write(s, t, ent[t]);
+      }
+      s.total = s.ost[NT - 1];
+      if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
+      if (s.err) break;
+      for (uint32_t b0 = 0; b0 < s.total; b0 += OB) {
+        const uint32_t nb = s.total - b0 < OB ? s.total - b0 : OB;
+        for (uint32_t t = 0; t < NT; ++t) ph_fill(s, c, t, b0);
+        if (s.err) break;
+        do {
+          ++dbl;
+          any = false;
+          for (uint32_t t = 0; t < NT; ++t) any |= ph_double(s, t, nb);
+        } while (any);
+        for (uint32_t t = 0; t < NT; ++t) ph_store(s, c, t, b0, nb);
+      }
+      const uint32_t last = (s.wend - s.ws + SL - 1) / SL - 1;
+      ws = s.ex[last];
+      s.op += s.total;
+    }
+    if (s.err) break;
+  }
+  if (stats) {
+    stats[0] = windows;
+    stats[1] = rounds;
+    stats[2] = fixes;
+    stats[3] = dbl;
+  }
+  const int r = s.err ? s.err : (int)s.op;
+  delete sp;
+  return r;
+}

@@ -113,6 +113,24 @@ def _xxh32(data: bytes, seed: int = 0) -> int:
         return 0
 
 
+def lz4par_host(codec: int, data: bytes, cap: int):
+    """The block-parallel decoder's phases (csrc/kernels/lz4par.hip) run on
+    the CPU, thread by thread: -> (status, output bytes, stats dict).  The
+    reference for the GPU kernel's algorithm."""
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    st = np.zeros(4, dtype=np.uint32)
+    n = N.lib().strom_lz4par_host(codec, src.ctypes.data, len(data), out.ctypes.data, cap,
+                                  st.ctypes.data)
+    stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]))
+    return n, (out[:n].tobytes() if n >= 0 else b""), stats
+
+
+def arrow_lz4_buffer(data: bytes, frame: bytes) -> bytes:
+    """An Arrow IPC compressed buffer: i64 uncompressed length + LZ4 frame."""
+    return struct.pack("<q", len(data)) + frame
+
+
 # ------------------------------------------------------------ GPU decode
 def make_descs(items: Sequence[tuple]) -> np.ndarray:
     """items: (src_off, src_len, dst_off, dst_len) per stream."""

@@ -1,0 +1,113 @@
+"""Block-parallel LZ4 decoder (csrc/kernels/lz4par.hip) vs the lane-group
+decoder (csrc/kernels/decompress.hip) on config-5 streams.
+
+Streams are Arrow IPC LZ4 buffers exactly as pyarrow writes a 64K-row int64
+column batch (i64 length + one LZ4 frame of linked 64 KiB blocks): ``val``
+(uniform in [0, 1e6) — arrow_bench's val column), ``ids`` (sorted) and
+``text``.  K distinct frames are built on the host; stream i decodes frame
+i mod K into its own output.  Every output is verified against the source
+bytes on the device.  GB/s = decoded bytes / kernel time (device events),
+median of --iters launches, both decoders in the same process.
+
+``python -m nvme_strom_amd.tools.lz4par_bench --out gpurun_out/lz4par.json``
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+
+import numpy as np
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def frames(kind: str, k: int, seed: int = 1):
+    import pyarrow as pa
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(seed)
+    raws, bufs = [], []
+    words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
+    for i in range(k):
+        if kind == "val":
+            d = rng.integers(0, 1_000_000, 65536, dtype=np.int64).tobytes()
+        elif kind == "ids":
+            d = np.arange(i * 65536, (i + 1) * 65536, dtype=np.int64).tobytes()
+        else:
+            d = b" ".join(words[j] for j in rng.integers(0, len(words), 110000))[:512 << 10]
+        raws.append(d)
+        bufs.append(D.arrow_lz4_buffer(d, pa.compress(d, codec="lz4", asbytes=True)))
+    return raws, bufs
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kinds", default="val,ids,text")
+    ap.add_argument("--streams", default="256,1024,2048,8192")
+    ap.add_argument("--distinct", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args(argv)
+    import torch
+
+    from nvme_strom_amd.ops import decompress as D
+    from nvme_strom_amd.ops._util import check, lib, ptr
+
+    dev = torch.device("cuda")
+    res = {"rows": []}
+    for kind in a.kinds.split(","):
+        raws, bufs = frames(kind, a.distinct)
+        rawlen = len(raws[0])
+        src_off = np.cumsum([0] + [len(b) for b in bufs[:-1]])
+        src = torch.from_numpy(np.frombuffer(b"".join(bufs), dtype=np.uint8).copy()).to(dev)
+        ref = torch.from_numpy(np.frombuffer(b"".join(raws), dtype=np.uint8).copy()).to(dev)
+        ratio = sum(len(b) for b in bufs) / sum(len(r) for r in raws)
+        for n in [int(x) for x in a.streams.split(",")]:
+            idx = np.arange(n) % a.distinct
+            cap = (rawlen + 63) // 64 * 64
+            descs = D.make_descs_arrays(src_off[idx], np.array([len(bufs[i]) for i in idx]),
+                                        np.arange(n) * cap, np.full(n, cap))
+            d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+            dst = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+            status = torch.empty(n, dtype=torch.int32, device=dev)
+            row = dict(kind=kind, streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
+            for name, fn in (("lanes", "strom_decompress"), ("par", "strom_decompress_par")):
+                f = getattr(lib(), fn)
+                times = []
+                ok = True
+                for it in range(a.iters + 1):
+                    dst.fill_(0x5a)
+                    status.fill_(-99)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    check(f(D.ARROW_LZ4, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status), None), fn)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    if it:
+                        times.append(e0.elapsed_time(e1) / 1e3)
+                    if it == a.iters:                       # verify the last run
+                        st = status.cpu().numpy()
+                        out = dst.view(n, cap)[:, :rawlen]
+                        want = ref.view(a.distinct, rawlen)[torch.from_numpy(idx).to(dev)]
+                        ok = bool((st == rawlen).all()) and bool(torch.equal(out, want))
+                med = float(np.median(times))
+                row[f"{name}_GBps"] = round(n * rawlen / med / 1e9, 2)
+                row[f"{name}_ms"] = round(med * 1e3, 3)
+                row[f"{name}_verified"] = ok
+            row["speedup"] = round(row["par_GBps"] / row["lanes_GBps"], 2) if row["lanes_GBps"] else None
+            _log(json.dumps(row))
+            res["rows"].append(row)
+            del dst
+            torch.cuda.empty_cache()
+    js = json.dumps(res)
+    if a.out:
+        with open(a.out, "w") as fo:
+            fo.write(js)
+    print(js)
+    return 0 if all(r["par_verified"] and r["lanes_verified"] for r in res["rows"]) else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -117,3 +117,61 @@ def test_pg_tuple_visible_rules():
     assert not V(pgpage.HEAP_XMAX_INVALID, 0)                               # xmin unknown
     assert not V(pgpage.HEAP_XMIN_COMMITTED, 0)                             # deleted / unknown xmax
     assert V(0, pgpage.PD_ALL_VISIBLE)
+
+
+# ---------------------------------------------- block-parallel LZ4 decoder
+def _ints(kind, n, seed=0):
+    rng = np.random.default_rng(seed)
+    if kind == "uniform":          # the config-5 val column: int64 in [0, 1e6)
+        return rng.integers(0, 1_000_000, n // 8, dtype=np.int64).tobytes()
+    if kind == "sorted":
+        return np.arange(n // 8, dtype=np.int64).tobytes()
+    return rng.random(n // 8).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "runs", "zeros", "uniform", "sorted", "floats"])
+@pytest.mark.parametrize("n", [1, 13, 100, 4096, 70000, 300000])
+def test_lz4par_raw_block_matches_host(kind, n):
+    """Speculative parallel parse + pointer doubling (the GPU kernel's own
+    phases, run thread by thread on the CPU) == the serial host decoder."""
+    d = (_data(kind, n) if kind in ("random", "text", "runs", "zeros") else _ints(kind, n))[:n]
+    c = D.lz4_compress(d)
+    st, out, stats = D.lz4par_host(D.LZ4, c, len(d))
+    assert st == len(d) and out == d, (st, stats)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "sorted", "text", "random"])
+def test_lz4par_arrow_frames_from_pyarrow(kind):
+    """pyarrow's LZ4 frames (linked 64 KiB blocks: matches reach into the
+    previous block) as Arrow IPC buffers, and a stored (-1) buffer."""
+    pa = pytest.importorskip("pyarrow")
+    d = _ints(kind, 512 << 10, 3) if kind in ("uniform", "sorted") else _data(kind, 512 << 10, 3)
+    frame = pa.compress(d, codec="lz4", asbytes=True)
+    buf = D.arrow_lz4_buffer(d, frame)
+    st, out, stats = D.lz4par_host(D.ARROW_LZ4, buf, len(d))
+    assert st == len(d) and out == d, (st, stats)
+    raw = b"\xff" * 8 + d[:5000]
+    st, out, _ = D.lz4par_host(D.ARROW_LZ4, raw, 5000)
+    assert st == 5000 and out == d[:5000]
+
+
+def test_lz4par_frames_and_errors():
+    d = _data("text", 200000, 5)
+    f = D.lz4_frame_compress(d, 64 << 10)
+    info = D.parse_lz4_frame_header(f)
+    st, out, _ = D.lz4par_host(D.LZ4_FRAME, f[info.data_offset:], len(d))
+    assert st == len(d) and out == d
+    # random data: stored (uncompressed) blocks
+    r = _data("random", 150000, 6)
+    f = D.lz4_frame_compress(r, 64 << 10)
+    info = D.parse_lz4_frame_header(f)
+    st, out, _ = D.lz4par_host(D.LZ4_FRAME, f[info.data_offset:], len(r))
+    assert st == len(r) and out == r
+    # overflow, truncation and garbage are reported, never crash
+    c = D.lz4_compress(d)
+    assert D.lz4par_host(D.LZ4, c, len(d) - 1)[0] == -2
+    assert D.lz4par_host(D.LZ4, c[: len(c) // 2], len(d))[0] < 0
+    rng = np.random.default_rng(9)
+    for _ in range(20):
+        g = rng.integers(0, 256, int(rng.integers(1, 5000)), dtype=np.uint8).tobytes()
+        assert D.lz4par_host(D.LZ4, g, 1 << 16)[0] <= 1 << 16
