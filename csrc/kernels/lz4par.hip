@@ -296,7 +296,9 @@ HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
   for (uint32_t e = t; e < nb; e += NT) {
     const uint32_t v = s.ptr[e];
     if (!(v & kTag)) {
-      const uint32_t w = s.ptr[v];
+      // v < e always (a match reads backwards); the bound only keeps a
+      // corrupt table inside the array
+      const uint32_t w = v < e ? s.ptr[v] : kLit;
       s.ptr[e] = w;
       more |= !(w & kTag);
     }
