@@ -40,9 +40,9 @@ $(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ) $(CORE_OBJ)
 	$(HIPCC) $(LDFLAGS) --offload-arch=$(ARCH) -o $@ $^
 
 # the LZ4/snappy decoder with its cycle profile compiled in (tools/decomp_prof.py)
-$(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip csrc/include/strom/strom.h
+$(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip csrc/include/strom/strom.h
 	@mkdir -p $(OUT)
-	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip
+	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip
 
 # the wave-per-stream decoder with its phase profile (tools/wave_prof.py)
 $(OUT)/libstrom_waveprof.so: csrc/kernels/decompress_wave.hip csrc/include/strom/strom.h
@@ -52,7 +52,7 @@ $(OUT)/libstrom_waveprof.so: csrc/kernels/decompress_wave.hip csrc/include/strom
 # a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
 # make ab AB=name [SRC=path/to/decompress.hip]
 SRC ?= csrc/kernels/decompress.hip
-WSRC ?= csrc/kernels/decompress_wave.hip
+WSRC ?= csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip
 ab:
 	@mkdir -p $(OUT)/ab
 	$(HIPCC) $(HIPFLAGS) -Icsrc/include -shared -o $(OUT)/ab/$(AB).so $(SRC) $(WSRC)

@@ -839,6 +839,15 @@ int launch(int codec, const void *d_src, void *d_dst, const strom_decomp_desc *d
 
 }  // namespace
 
+// lz4par.hip: one workgroup per stream, parallel parse + pointer doubling
+extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
+                                    const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                    int32_t *d_status, void *stream);
+
+extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
+                                      const strom_decomp_desc *d_desc, uint32_t nblocks,
+                                      int32_t *d_status, void *stream);
+
 // decompress_wave.hip: one wave per stream (few, long streams)
 extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
                                      const strom_decomp_desc *d_desc, uint32_t nblocks,
@@ -852,6 +861,24 @@ extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
+  if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_ARROW_LZ4) return -22;
+  if (!nblocks) return 0;
+  // Few LZ4 streams: the block-parallel decoder (lz4par.hip) — a stream is
+  // decoded by a whole workgroup, so a launch no longer takes one serial
+  // stream's time (profiles/r3/dec: 2,048 config-5 frames 27.8 -> 65.5
+  // GB/s, 256 frames 3.8 -> 35).  From ~8k streams the lane groups keep
+  // up or win (val equal, ids / text faster).  STROM_DECOMP_PAR=0/1 forces.
+  const char *pe = getenv("STROM_DECOMP_PAR");
+  const bool lz4 = codec != STROM_CODEC_SNAPPY && codec != STROM_CODEC_COPY;
+  if (lz4 && (pe ? atoi(pe) != 0 : nblocks <= 4096))
+    return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+  return strom_decompress_lanes(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+}
+
+// the lane-group decoders only (A/B runs: tools/lz4par_bench.py)
+extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
+                                      const strom_decomp_desc *d_desc, uint32_t nblocks,
+                                      int32_t *d_status, void *stream) {
   if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_ARROW_LZ4) return -22;
   if (!nblocks) return 0;
   const char *e = getenv("STROM_DECOMP_G");

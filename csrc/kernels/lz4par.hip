@@ -48,7 +48,9 @@ constexpr uint32_t NT = 256;             // threads per stream (4 waves)
 constexpr uint32_t PW = 16384;           // compressed bytes per parse window
 constexpr uint32_t SL = PW / NT;         // slice per thread (64 B = 2 bitmap words)
 constexpr uint32_t PAD = 64;             // window overhang (reads past the window end)
-constexpr uint32_t OB = 8192;            // output bytes per resolve batch
+constexpr uint32_t OB = 4096;            // output bytes per resolve batch
+constexpr uint32_t HR = 32768;           // LDS ring of the latest output (history)
+constexpr uint32_t KW = OB / 4 / NT + 1; // output dwords a thread holds per batch
 #ifndef LZ4PAR_LOOKBACK
 #define LZ4PAR_LOOKBACK 512
 #endif
@@ -74,6 +76,7 @@ struct Smem {
   uint32_t olen[NT];     // output bytes of slice t's true sequences
   uint32_t ost[NT];      // inclusive prefix of olen
   uint32_t ptr[OB];
+  uint8_t ring[HR];      // output byte at absolute position x: ring[x % HR]
   // stream scalars (thread 0 writes, everyone reads after a barrier)
   uint32_t ip;           // input position of the next block header
   uint32_t bstart, bend; // current block
@@ -173,7 +176,22 @@ HD uint32_t slice_hi(const Smem &s, uint32_t t) {
 // ---------------------------------------------------------------- phases
 // window load: input bytes [ws, ws + wload) into LDS
 HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
-  for (uint32_t i = t; i < s.wload; i += NT) s.win[i] = c.in[s.ws + i];
+  // all loads of a thread issued before the first LDS store (16 at a time):
+  // a plain loop waited for each load in turn
+  constexpr uint32_t U = 16;
+  for (uint32_t j0 = 0; j0 * NT < s.wload; j0 += U) {
+    uint8_t r[U];
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint32_t i = t + (j0 + j) * NT;
+      r[j] = i < s.wload ? c.in[s.ws + i] : 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < U; ++j) {
+      const uint32_t i = t + (j0 + j) * NT;
+      if (i < s.wload) s.win[i] = r[j];
+    }
+  }
 }
 
 // (1) speculative chain of slice t
@@ -324,30 +342,76 @@ HD uint8_t resolve(const Smem &s, const Ctx &c, uint32_t v) {
   return hist_byte(c, v & ~kHist);
 }
 
-// (4c) gather + store: thread t owns aligned output dwords
-HD void ph_store(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb) {
+// (4c) gather: thread t resolves the output dwords it owns (aligned in
+// HBM) into registers; history within HR bytes comes from the LDS ring
+// (read-only in this phase), older history from HBM
+struct Held {
+  uint32_t w[KW];
+};
+
+HD void ph_resolve(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb, Held &h) {
+  const uint8_t *base = c.out + s.op + b0;
+  const uint32_t mis = (uint32_t)((uintptr_t)base & 3);
+  const uint32_t nw = (nb + mis + 3) / 4;
+  const uint32_t bs = s.op + b0;         // absolute output position of the batch
+  for (uint32_t j = 0; j < KW; ++j) {
+    const uint32_t k = t + j * NT;
+    uint32_t w = 0;
+    if (k < nw) {
+      for (uint32_t b = 0; b < 4; ++b) {
+        const int32_t e = (int32_t)(4 * k + b) - (int32_t)mis;
+        if (e < 0 || (uint32_t)e >= nb) continue;
+        const uint32_t v = s.ptr[e];
+        uint8_t x;
+        if (v & kLit) {
+          x = inb(s, c, v & ~kLit);
+        } else {
+          const uint32_t hp = v & ~kHist;
+          x = bs - hp <= HR ? s.ring[hp & (HR - 1)] : hist_byte(c, hp);
+        }
+        w |= (uint32_t)x << (8 * b);
+      }
+    }
+    h.w[j] = w;
+  }
+}
+
+// (4d) store the held dwords to HBM and to the history ring
+HD void ph_write(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb, const Held &h) {
   uint8_t *base = c.out + s.op + b0;
   const uint32_t mis = (uint32_t)((uintptr_t)base & 3);
   const uint32_t nw = (nb + mis + 3) / 4;
-  for (uint32_t k = t; k < nw; k += NT) {
+  const uint32_t bs = s.op + b0;
+  for (uint32_t j = 0; j < KW; ++j) {
+    const uint32_t k = t + j * NT;
+    if (k >= nw) break;
     const int32_t e0 = (int32_t)(4 * k) - (int32_t)mis;
+    const uint32_t w = h.w[j];
     if (e0 >= 0 && (uint32_t)e0 + 4 <= nb) {
-      uint32_t w = 0;
-      for (uint32_t j = 0; j < 4; ++j) w |= (uint32_t)resolve(s, c, s.ptr[e0 + j]) << (8 * j);
       *(uint32_t *)(base + e0) = w;
+      for (uint32_t b = 0; b < 4; ++b) s.ring[(bs + e0 + b) & (HR - 1)] = (uint8_t)(w >> (8 * b));
     } else {
-      for (int32_t j = 0; j < 4; ++j) {
-        const int32_t e = e0 + j;
-        if (e >= 0 && (uint32_t)e < nb) base[e] = resolve(s, c, s.ptr[e]);
+      for (uint32_t b = 0; b < 4; ++b) {
+        const int32_t e = e0 + (int32_t)b;
+        if (e >= 0 && (uint32_t)e < nb) {
+          base[e] = (uint8_t)(w >> (8 * b));
+          s.ring[(bs + e) & (HR - 1)] = (uint8_t)(w >> (8 * b));
+        }
       }
     }
   }
 }
 
-// stored (uncompressed) block: [bstart, bend) -> out[op..]
+// stored (uncompressed) block: [bstart, bend) -> out[op..]; its last HR
+// bytes also go to the history ring
 HD void ph_rawcopy(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t n = s.bend - s.bstart;
-  for (uint32_t i = t; i < n; i += NT) c.out[s.op + i] = c.in[s.bstart + i];
+  const uint32_t keep = n > HR ? n - HR : 0;
+  for (uint32_t i = t; i < n; i += NT) {
+    const uint8_t x = c.in[s.bstart + i];
+    c.out[s.op + i] = x;
+    if (i >= keep) s.ring[(s.op + i) & (HR - 1)] = x;
+  }
 }
 
 // ---------------------------------------------------------------- scalar steps (thread 0)
@@ -518,7 +582,10 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
           if (s.err) break;
           while (__syncthreads_or(ph_double(s, t, nb))) {
           }
-          ph_store(s, c, t, b0, nb);
+          Held h;
+          ph_resolve(s, c, t, b0, nb, h);
+          __syncthreads();
+          ph_write(s, c, t, b0, nb, h);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __syncthreads();
         }
@@ -560,12 +627,13 @@ extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
 extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
                                  uint32_t cap, uint32_t *stats) {
   using namespace lz4p;
-  static_assert(sizeof(Smem) < 64 * 1024, "LDS");
+  static_assert(sizeof(Smem) <= 80 * 1024, "LDS: two workgroups per CU");
   Smem *sp = new Smem;
   Smem &s = *sp;
   Ctx c{src, dst, src_len, cap};
   uint32_t ent[NT];
   bool flag[NT];
+  Held *held = new Held[NT];
   uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0;
   st_header(s, c, codec);
   for (;;) {
@@ -614,7 +682,8 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
           any = false;
           for (uint32_t t = 0; t < NT; ++t) any |= ph_double(s, t, nb);
         } while (any);
-        for (uint32_t t = 0; t < NT; ++t) ph_store(s, c, t, b0, nb);
+        for (uint32_t t = 0; t < NT; ++t) ph_resolve(s, c, t, b0, nb, held[t]);
+        for (uint32_t t = 0; t < NT; ++t) ph_write(s, c, t, b0, nb, held[t]);
       }
       const uint32_t last = (s.wend - s.ws + SL - 1) / SL - 1;
       ws = s.ex[last];
@@ -630,5 +699,6 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
   }
   const int r = s.err ? s.err : (int)s.op;
   delete sp;
+  delete[] held;
   return r;
 }

@@ -73,7 +73,7 @@ def main(argv=None) -> int:
             dst = torch.empty(n * cap, dtype=torch.uint8, device=dev)
             status = torch.empty(n, dtype=torch.int32, device=dev)
             row = dict(kind=kind, streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
-            for name, fn in (("lanes", "strom_decompress"), ("par", "strom_decompress_par")):
+            for name, fn in (("lanes", "strom_decompress_lanes"), ("par", "strom_decompress_par")):
                 f = getattr(lib(), fn)
                 times = []
                 ok = True
