@@ -514,6 +514,33 @@ HD void st_window(Smem &s, const Ctx &c, uint32_t ws) {
 }  // namespace lz4p
 
 // ---------------------------------------------------------------- device
+// -DSTROM_DECOMP_PROF (libstrom_decprof.so): thread 0 of every workgroup
+// stamps s_memtime at each phase boundary; strom_lz4par_prof() returns the
+// sums (tools/lz4par_bench.py --prof)
+enum : int { kLpHdr, kLpLoad, kLpSpec, kLpValid, kLpScan, kLpFill, kLpDouble, kLpResolve,
+             kLpWrite, kLpRaw, kLpNWin, kLpNRound, kLpNBatch, kLpNDouble, kLpN };
+#ifdef STROM_DECOMP_PROF
+__device__ unsigned long long g_lz4par_prof[kLpN];
+#define LP_INIT() uint64_t lp[kLpN] = {0}; uint64_t lp_t = __builtin_amdgcn_s_memtime()
+#define LP_MARK(k)                                                    \
+  do {                                                                \
+    const uint64_t _n = __builtin_amdgcn_s_memtime();                 \
+    lp[k] += _n - lp_t;                                               \
+    lp_t = _n;                                                        \
+  } while (0)
+#define LP_CNT(k) (lp[k] += 1)
+#define LP_FLUSH()                                                    \
+  do {                                                                \
+    if (t == 0)                                                       \
+      for (int _i = 0; _i < kLpN; ++_i) atomicAdd(&g_lz4par_prof[_i], (unsigned long long)lp[_i]); \
+  } while (0)
+#else
+#define LP_INIT() (void)0
+#define LP_MARK(k) (void)0
+#define LP_CNT(k) (void)0
+#define LP_FLUSH() (void)0
+#endif
+
 namespace {
 using namespace lz4p;
 
@@ -523,6 +550,7 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
                                                     uint32_t nstreams, int32_t *status) {
   __shared__ __attribute__((aligned(16))) Smem s;
   const uint32_t t = threadIdx.x;
+  LP_INIT();
   for (uint32_t b = blockIdx.x; b < nstreams; b += gridDim.x) {
     const strom_decomp_desc d = desc[b];
     Ctx c{src + d.src_off, dst + d.dst_off, d.src_len, d.dst_len};
@@ -532,6 +560,7 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
       if (t == 0 && s.mode != kModeDone) st_block(s, c);
       __syncthreads();
       if (s.mode == kModeDone || s.err) break;
+      LP_MARK(kLpHdr);
       if (s.braw) {
         const uint64_t n = s.bend - s.bstart;
         if ((uint64_t)s.op + n > c.cap) {
@@ -544,22 +573,28 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
         __syncthreads();
         if (t == 0) s.op += (uint32_t)n;
         __syncthreads();
+        LP_MARK(kLpRaw);
         continue;
       }
       uint32_t ws = s.bstart;
       while (ws < s.bend && !s.err) {
+        LP_CNT(kLpNWin);
         if (t == 0) st_window(s, c, ws);
         __syncthreads();
         ph_load(s, c, t);
         __syncthreads();
+        LP_MARK(kLpLoad);
         ph_spec(s, c, t);
         __syncthreads();
+        LP_MARK(kLpSpec);
         bool changed;
         do {
+          LP_CNT(kLpNRound);
           const uint32_t ent = ph_entry(s, t);
           __syncthreads();
           changed = ph_fix(s, c, t, ent);
         } while (__syncthreads_or(changed));
+        LP_MARK(kLpValid);
         ph_count(s, c, t);
         for (uint32_t dd = 1; dd < NT; dd <<= 1) {
           __syncthreads();
@@ -573,21 +608,30 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
           if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
         }
         __syncthreads();
+        LP_MARK(kLpScan);
         if (s.err) break;
         const uint32_t total = s.total;
         for (uint32_t b0 = 0; b0 < total; b0 += OB) {
+          LP_CNT(kLpNBatch);
           const uint32_t nb = total - b0 < OB ? total - b0 : OB;
           ph_fill(s, c, t, b0);
           __syncthreads();
+          LP_MARK(kLpFill);
           if (s.err) break;
-          while (__syncthreads_or(ph_double(s, t, nb))) {
-          }
+          bool more;
+          do {
+            LP_CNT(kLpNDouble);
+            more = ph_double(s, t, nb);
+          } while (__syncthreads_or(more));
+          LP_MARK(kLpDouble);
           Held h;
           ph_resolve(s, c, t, b0, nb, h);
           __syncthreads();
+          LP_MARK(kLpResolve);
           ph_write(s, c, t, b0, nb, h);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
           __syncthreads();
+          LP_MARK(kLpWrite);
         }
         // the next window starts at the last slice's true exit
         const uint32_t last = (s.wend - s.ws + SL - 1) / SL - 1;
@@ -602,6 +646,7 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
     if (t == 0) status[b] = s.err ? s.err : (int32_t)s.op;
     __syncthreads();
   }
+  LP_FLUSH();
 }
 
 }  // namespace
@@ -620,6 +665,19 @@ extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
                      (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
+
+#ifdef STROM_DECOMP_PROF
+// phase cycle sums of thread 0 of every workgroup (and event counts), zeroed
+extern "C" int strom_lz4par_prof(uint64_t *out) {
+  unsigned long long h[kLpN] = {0};
+  if (hipDeviceSynchronize() != hipSuccess) return -5;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_lz4par_prof), sizeof h) != hipSuccess) return -5;
+  unsigned long long z[kLpN] = {0};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lz4par_prof), z, sizeof z);
+  for (int i = 0; i < kLpN; ++i) out[i] = h[i];
+  return kLpN;
+}
+#endif
 
 // The same phases run thread by thread on the CPU: the algorithm's
 // reference (tests/test_codecs_cpu.py), no GPU involved.  Returns decoded

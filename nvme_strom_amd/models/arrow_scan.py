@@ -117,6 +117,7 @@ class ArrowScan:
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
     # to fill the GPU, so compressed groups grow to hold that many buffers
     TARGET_STREAMS = 8192
+    MIN_STREAMS = 256              # per group when cutting a column for overlap
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -181,13 +182,18 @@ class ArrowScan:
         comp = [(d, v) for b in batches for d, v in b.cols
                 if d.compressed and 0 < d.length < 0.9 * d.need]
         if comp:
-            # the decoder runs one stream per buffer: a group needs thousands
-            # of them to fill the GPU.  (Cutting a 2,048-stream column into 3
-            # groups to overlap reads with decodes measured slower, 72 -> 83-
-            # 125 ms, profiles/r3/arrow_split3.json: each launch still takes
-            # one stream's serial time and the launches did not overlap.)
+            # few streams per launch are fine for the block-parallel decoder
+            # (lz4par.hip: a workgroup per stream), so a column of many
+            # buffers is cut into nslots groups: the decode of group g then
+            # overlaps the reads of groups g+1.. (with the round-2 lane
+            # decoder every launch took one serial stream's time and the
+            # split measured slower, profiles/r3/arrow_split3.json)
             avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
-            slot = int(min(self.max_slot_bytes, max(slot, avg * self.TARGET_STREAMS)))
+            total = sum(d.length + (v.length if v else 0) for d, v in comp)
+            want = avg * self.TARGET_STREAMS
+            if len(comp) >= self.nslots * self.MIN_STREAMS:
+                want = min(want, total / self.nslots)
+            slot = int(min(self.max_slot_bytes, max(slot, want)))
         limit = max(1, slot // self.chunk_sz)
         # chunk ranges of every batch at once (vectorised: the qualifier-list
         # plans touch several buffers per batch)
@@ -272,15 +278,18 @@ class ArrowScan:
         nbytes = max(len(g.ids) for g in groups) * self.chunk_sz
         dec = max(max(g.dec_bytes for g in groups), 64)
         words = max(max(g.words for g in groups), 1)
-        if self._slots and (self._slots[0].cap >= nbytes and
+        if self._slots and len(self._slots) >= min(self.nslots, len(groups)) and (
+                self._slots[0].cap >= nbytes and
                             self._slots[0].dec.numel() >= dec and
                             self._slots[0].bitmap.numel() >= words):
             return
         self._free_slots()
         # one registered HBM ring for every slot: one MAP (dma-buf export +
-        # BAR mapping) per scan object instead of one per slot (cold cost)
-        self._hbm = HbmBuffer(nbytes * self.nslots, self.device)
-        for k in range(self.nslots):
+        # BAR mapping) per scan object instead of one per slot (cold cost);
+        # no more slots than groups
+        nsl = max(1, min(self.nslots, len(groups)))
+        self._hbm = HbmBuffer(nbytes * nsl, self.device)
+        for k in range(nsl):
             sl = _Slot(k * nbytes, nbytes,
                        torch.empty(dec, dtype=torch.uint8, device=self.device),
                        torch.empty(words, dtype=torch.int64, device=self.device))
@@ -294,20 +303,20 @@ class ArrowScan:
                                      max_chunks=nbytes // self.chunk_sz)
         # pinned write-back buffers only once the BAR path is refused (a
         # cold-scan cost otherwise: GiBs of pinned host memory per scan)
-        self._wbs = [None] * self.nslots
+        self._wbs = [None] * len(self._slots)
         self._wb_bytes = nbytes
 
     def _submit(self, k: int, g: _Group) -> None:
-        s = self._slots[k % self.nslots]
+        s = self._slots[k % len(self._slots)]
         if s.event is not None:
             s.event.synchronize()            # the slot's previous group is consumed
             s.event = None
         s.keep = []
         wb = None
         if self.reader._direct_ram is False:  # page-cache chunks go through host memory
-            if self._wbs[k % self.nslots] is None:
-                self._wbs[k % self.nslots] = host_buffer(self._wb_bytes)
-            wb = self._wbs[k % self.nslots]
+            if self._wbs[k % len(self._wbs)] is None:
+                self._wbs[k % len(self._wbs)] = host_buffer(self._wb_bytes)
+            wb = self._wbs[k % len(self._wbs)]
         res, landed = self.reader.submit(self._hbm, s.off, g.ids.astype(np.uint32), wb=wb)
         s.pending = (res, landed, g)
 
@@ -319,7 +328,7 @@ class ArrowScan:
         return t
 
     def _compute(self, k: int, quals, proj, state) -> None:
-        s = self._slots[k % self.nslots]
+        s = self._slots[k % len(self._slots)]
         res, landed, g = s.pending
         s.pending = None
         t0 = time.perf_counter()
@@ -426,7 +435,7 @@ class ArrowScan:
                      column_bytes=0, pout=pout, pvalid=pvalid)
         t_alloc = time.perf_counter()
         # depth nslots - 1 of reads ahead of the group being computed
-        ahead = self.nslots - 1
+        ahead = max(1, len(self._slots) - 1)
         for k in range(min(ahead, len(groups))):
             self._submit(k, groups[k])
         for k in range(len(groups)):

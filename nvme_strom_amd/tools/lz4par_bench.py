@@ -42,12 +42,43 @@ def frames(kind: str, k: int, seed: int = 1):
     return raws, bufs
 
 
+PHASES = ("hdr", "load", "spec", "validate", "count_scan", "fill", "double", "resolve", "write",
+          "rawcopy")
+COUNTS = ("windows", "valid_rounds", "batches", "double_rounds")
+
+
+def prof(n, src, dst, d_desc, status) -> dict:
+    """One launch of the profiled build: share of thread-0 cycles per phase
+    and events per stream."""
+    import ctypes as C
+    import os
+    from nvme_strom_amd.ops import decompress as D
+    from nvme_strom_amd.ops._util import ptr
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib",
+                              "libstrom_decprof.so"))
+    out = np.zeros(len(PHASES) + len(COUNTS), dtype=np.uint64)
+    lib.strom_lz4par_prof(out.ctypes.data_as(C.c_void_p))           # zero
+    rc = lib.strom_decompress_par(D.ARROW_LZ4, C.c_void_p(ptr(src)), C.c_void_p(ptr(dst)),
+                                  C.c_void_p(ptr(d_desc)), C.c_uint32(n), C.c_void_p(ptr(status)),
+                                  None)
+    assert rc == 0
+    lib.strom_lz4par_prof(out.ctypes.data_as(C.c_void_p))
+    cyc = out[:len(PHASES)].astype(np.float64)
+    tot = cyc.sum()
+    res = {p: round(float(c / tot), 3) for p, c in zip(PHASES, cyc)}
+    res.update({k: round(float(v) / n, 2) for k, v in zip(COUNTS, out[len(PHASES):])})
+    res["cycles_per_stream"] = round(float(tot) / n)
+    return res
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--kinds", default="val,ids,text")
     ap.add_argument("--streams", default="256,1024,2048,8192")
     ap.add_argument("--distinct", type=int, default=64)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--prof", action="store_true",
+                    help="phase cycle profile of the par decoder (libstrom_decprof.so)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -97,6 +128,8 @@ def main(argv=None) -> int:
                 row[f"{name}_ms"] = round(med * 1e3, 3)
                 row[f"{name}_verified"] = ok
             row["speedup"] = round(row["par_GBps"] / row["lanes_GBps"], 2) if row["lanes_GBps"] else None
+            if a.prof:
+                row["par_phases"] = prof(n, src, dst, d_desc, status)
             _log(json.dumps(row))
             res["rows"].append(row)
             del dst
