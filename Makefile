@@ -88,6 +88,10 @@ build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
 	@mkdir -p build
 	$(ROCM)/llvm/bin/clang++ $(SELFTEST_FLAGS) -fsanitize=thread -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
 
+build/arrow_meta_fuzz: csrc/tests/arrow_meta_fuzz.cc csrc/engine/arrow_meta.cc
+	@mkdir -p build
+	$(CXX) -std=c++17 -O1 -g -fsanitize=address,undefined -fno-sanitize-recover=all -o $@ $^ -lpthread
+
 selftest: build/selftest build/selftest-asan build/selftest-tsan
 	STROM_STAT_SHM=0 ./build/selftest && STROM_STAT_SHM=0 ./build/selftest-asan && STROM_STAT_SHM=0 TSAN_OPTIONS=report_signal_unsafe=0 ./build/selftest-tsan
 

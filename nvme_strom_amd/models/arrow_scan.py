@@ -112,6 +112,10 @@ def _up64(n: int) -> int:
     return (n + 63) // 64 * 64
 
 
+def _up64_np(n: np.ndarray) -> np.ndarray:
+    return (n + 63) // 64 * 64
+
+
 class ArrowScan:
     # the decoder runs one stream per compressed buffer at a roughly fixed
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
@@ -146,25 +150,30 @@ class ArrowScan:
             cis.append(ci)
             dtypes.append(_TORCH[col.numpy_dtype])
             widths.append(col.bit_width // 8)
-        out, base = [], 0
-        for b in self.meta.batches:
-            if b.codec not in (None, "lz4_frame"):
-                raise NotImplementedError(f"body compression {b.codec} (GPU decoder: LZ4 frame)")
-            comp = b.codec is not None
-            cols = []
-            for ci, width in zip(cis, widths):
-                cc = b.columns[ci]
-                need = cc.length * width
-                data = _Buf(cc.data.offset, cc.data.length, need, _up64(need), comp)
-                valid = None
-                if cc.null_count and cc.validity.length:
-                    vn = (cc.length + 7) // 8
-                    valid = _Buf(cc.validity.offset, cc.validity.length, vn, _up64(vn) + 64, comp)
-                cols.append((data, valid))
-            n = b.columns[cis[0]].length
-            out.append(_Batch(n, base, cols))
-            base += n
-        return out, dtypes, base
+        m = self.meta
+        for c in set(m.codecs):
+            if c not in (None, "lz4_frame"):
+                raise NotImplementedError(f"body compression {c} (GPU decoder: LZ4 frame)")
+        comp = [c is not None for c in m.codecs]
+        # per column, lists over batches (the metadata is array-backed)
+        percol = []
+        for ci, width in zip(cis, widths):
+            a = m.columns[ci]
+            need = a.length * width
+            vn = (a.length + 7) // 8
+            hasv = (a.null_count != 0) & (a.v_len != 0)
+            percol.append(zip(a.d_off.tolist(), a.d_len.tolist(), need.tolist(),
+                              _up64_np(need).tolist(), a.v_off.tolist(), a.v_len.tolist(),
+                              vn.tolist(), (_up64_np(vn) + 64).tolist(), hasv.tolist(), comp))
+        rows = m.columns[cis[0]].length if m.nbatches else np.zeros(0, np.int64)
+        base = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
+        cols_by_batch = zip(*percol) if percol else iter(())
+        out = []
+        for n, b0, cols in zip(rows.tolist(), base[:-1].tolist(), cols_by_batch):
+            out.append(_Batch(n, b0, [
+                (_Buf(do, dl, nd, cap, cp), _Buf(vo, vl, vn, vcap, cp) if hv else None)
+                for do, dl, nd, cap, vo, vl, vn, vcap, hv, cp in cols]))
+        return out, dtypes, int(base[-1])
 
     def _chunks(self, b: _Batch) -> np.ndarray:
         c = self.chunk_sz

@@ -17,6 +17,8 @@ import struct
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
+import numpy as np
+
 MAGIC = b"ARROW1"
 
 
@@ -140,10 +142,57 @@ class Batch:
 
 
 @dataclass
+class ColumnArrays:
+    """One column's chunks over all record batches, as arrays (batch order)."""
+    length: np.ndarray
+    null_count: np.ndarray
+    v_off: np.ndarray          # validity buffer: absolute file offset, stored bytes
+    v_len: np.ndarray
+    d_off: np.ndarray          # data buffer
+    d_len: np.ndarray
+
+
 class ArrowFile:
-    schema: List[Column]
-    batches: List[Batch]
-    size: int
+    """Schema + record-batch layout.  The layout is held as arrays
+    (``rows``, ``codecs``, ``columns[i]``: ColumnArrays); ``batches`` builds
+    the per-batch objects on first use (a scan plan reads the arrays)."""
+
+    def __init__(self, schema: List[Column], size: int, offset=None, rows=None, body=None,
+                 body_len=None, codecs=None, columns=None):
+        self.schema = schema
+        self.size = size
+        z = np.zeros(0, np.int64)
+        self.offset = offset if offset is not None else z
+        self.rows = rows if rows is not None else z
+        self.body = body if body is not None else z
+        self.body_len = body_len if body_len is not None else z
+        self.codecs: List[Optional[str]] = codecs if codecs is not None else []
+        self.columns: List[ColumnArrays] = columns if columns is not None else []
+        self._batches: Optional[List[Batch]] = None
+
+    @property
+    def nbatches(self) -> int:
+        return len(self.rows)
+
+    @property
+    def batches(self) -> List[Batch]:
+        if self._batches is None:
+            percol = []
+            for c in self.columns:
+                it = zip(*(a.tolist() for a in (c.length, c.null_count, c.v_off, c.v_len,
+                                                 c.d_off, c.d_len)))
+                percol.append([ColumnChunk(a, b, BufferRef(vo, vl), BufferRef(do, dl))
+                               for a, b, vo, vl, do, dl in it])
+            self._batches = [
+                Batch(o, r, bo, bl, cd, [c[j] for c in percol])
+                for j, (o, r, bo, bl, cd) in enumerate(zip(
+                    self.offset.tolist(), self.rows.tolist(), self.body.tolist(),
+                    self.body_len.tolist(), self.codecs))]
+        return self._batches
+
+    def __eq__(self, other) -> bool:
+        return (isinstance(other, ArrowFile) and self.schema == other.schema
+                and self.size == other.size and self.batches == other.batches)
 
     def column_index(self, name: str) -> int:
         for i, c in enumerate(self.schema):
@@ -177,24 +226,8 @@ class _Src:
     def read(self, off: int, n: int) -> bytes:
         if self.buf is not None:
             return self.buf[off:off + n]
-        hit = self._cache.pop((off, n), None) if hasattr(self, "_cache") else None
-        if hit is not None:
-            return hit
         import os
         return os.pread(self.fd, n, off)
-
-    def prefetch(self, ranges, threads: int = 16) -> None:
-        """Read many small ranges at once: a file's record-batch headers sit
-        between the bodies, one small read each, which on a cold file cost
-        one storage round trip apiece when read in sequence (the cold-scan
-        cost of an Arrow file with thousands of batches)."""
-        if self.buf is not None or len(ranges) < 8:
-            return
-        import os
-        from concurrent.futures import ThreadPoolExecutor
-        with ThreadPoolExecutor(max_workers=threads) as ex:
-            got = list(ex.map(lambda r: os.pread(self.fd, r[1], r[0]), ranges))
-        self._cache = dict(zip(ranges, got))
 
     def close(self):
         if self.fd is not None:
@@ -202,15 +235,92 @@ class _Src:
             os.close(self.fd)
 
 
-def read_metadata(path_or_bytes) -> ArrowFile:
+def read_metadata(path_or_bytes, native: Optional[bool] = None) -> ArrowFile:
+    """Schema and record-batch layout of an Arrow IPC file.  For a file path
+    the record-batch headers are read and parsed by libstrom
+    (csrc/engine/arrow_meta.cc: many reads in flight, no per-header Python);
+    ``native=False`` (or an in-memory source) takes the Python walk below."""
     src = _Src(path_or_bytes)
     try:
-        return _read(src)
+        return _read(src, native if native is not None else src.fd is not None)
     finally:
         src.close()
 
 
-def _read(src: "_Src") -> ArrowFile:
+def _layout(schema: List[Column]) -> Tuple[List[Tuple[int, int, int]], int, int]:
+    """(first node, first buffer, own buffers) of every top-level column:
+    the same in every record batch (children follow their parent)."""
+    cur = [0, 0]
+
+    def walk(col: Column):
+        if col.nbuffers < 0:
+            raise ValueError(f"column {col.name}: layout not supported")
+        me = (cur[0], cur[1], col.nbuffers)
+        cur[0] += 1
+        cur[1] += col.nbuffers
+        for ch in col.children:
+            walk(ch)
+        return me
+
+    return [walk(c) for c in schema], cur[0], cur[1]
+
+
+_CODECS = {-1: None, 0: "lz4_frame", 1: "zstd"}
+
+
+def _headers_py(src: "_Src", blocks: np.ndarray, nn: int, nb: int):
+    """Python reference of strom_arrow_headers: the same output arrays."""
+    n = len(blocks)
+    rows = np.zeros(n, np.int64)
+    codec = np.zeros(n, np.int32)
+    nodes = np.zeros((n, nn, 2), np.int64)
+    bufs = np.zeros((n, nb, 2), np.int64)
+    for k, (boff, mlen, _) in enumerate(blocks.tolist()):
+        buf = src.read(boff, mlen)
+        msg, _ = _message(buf, 0)
+        if msg.scalar(1, "B", 0) != 3:
+            codec[k] = -2
+            continue
+        rb = msg.table(2)
+        comp = rb.table(3)
+        codec[k] = -1 if comp is None else comp.scalar(0, "b", 0)
+        rows[k] = rb.scalar(0, "q", 0)
+        for vi, arr, cap in ((1, nodes, nn), (2, bufs, nb)):
+            start, cnt = rb.vector(vi)
+            if cnt < cap:
+                raise ValueError(f"record batch {k}: {cnt} entries, schema needs {cap}")
+            arr[k] = np.frombuffer(buf, "<i8", 2 * cap, start).reshape(cap, 2)
+    return rows, codec, nodes, bufs
+
+
+def _headers_native(src: "_Src", blocks: np.ndarray, nn: int, nb: int, threads: int = 32):
+    import ctypes as C
+
+    from .. import _native
+    n = len(blocks)
+    mx_n, mx_b = nn + 64, nb + 128          # room for trailing entries the schema walk ignores
+    rows = np.zeros(n, np.int64)
+    codec = np.zeros(n, np.int32)
+    cn = np.zeros(n, np.int32)
+    cb = np.zeros(n, np.int32)
+    nodes = np.zeros((n, mx_n, 2), np.int64)
+    bufs = np.zeros((n, mx_b, 2), np.int64)
+    bad = np.full(1, -1, np.int64)
+    blk = np.ascontiguousarray(blocks, dtype=np.int64)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)
+    rc = _native.lib().strom_arrow_headers(src.fd, p(blk), n, mx_n, mx_b, p(rows), p(codec),
+                                           p(cn), p(cb), p(nodes), p(bufs), threads, p(bad))
+    if rc != 0:
+        raise ValueError(f"Arrow record-batch headers: rc={rc}, first bad block {int(bad[0])}")
+    ok = codec == -2
+    short = ~ok & ((cn < nn) | (cb < nb))
+    if short.any():
+        k = int(np.flatnonzero(short)[0])
+        raise ValueError(f"record batch {k}: {cn[k]}/{cb[k]} entries, schema needs {nn}/{nb}")
+    return rows, codec, nodes[:, :nn], bufs[:, :nb]
+
+
+def _read(src: "_Src", native: bool = False) -> ArrowFile:
     if src.read(0, 6) != MAGIC or src.read(src.size - 6, 6) != MAGIC:
         raise ValueError("not an Arrow IPC file")
     flen, = struct.unpack("<i", src.read(src.size - 10, 4))
@@ -219,44 +329,26 @@ def _read(src: "_Src") -> ArrowFile:
     schema_fb = footer.table(1)
     schema = [_column(f) for f in schema_fb.tables(1)] if schema_fb else []
     start, n = footer.vector(3)
-    batches = []
-    src.prefetch([tuple(struct.unpack_from("<qi", fbuf, start + 24 * k)) for k in range(n)])
-    for k in range(n):
-        boff, mlen, blen = struct.unpack_from("<qi4xq", fbuf, start + 24 * k)
-        buf = src.read(boff, mlen)
-        msg, _ = _message(buf, 0)
-        htype = msg.scalar(1, "B", 0)
-        if htype != 3:
-            continue
-        rb = msg.table(2)
-        body = boff + mlen
-        comp = rb.table(3)
-        codec = None
-        if comp is not None:
-            codec = {0: "lz4_frame", 1: "zstd"}.get(comp.scalar(0, "b", 0), "unknown")
-        nstart, nn = rb.vector(1)
-        nodes = [struct.unpack_from("<qq", buf, nstart + 16 * i) for i in range(nn)]
-        bstart, bn = rb.vector(2)
-        bufs = [struct.unpack_from("<qq", buf, bstart + 16 * i) for i in range(bn)]
-        b = Batch(boff, rb.scalar(0, "q", 0), body, blen, codec)
-        cursor = [0, 0]                     # next node, next buffer
-
-        def walk(col: Column) -> Optional[ColumnChunk]:
-            if col.nbuffers < 0:
-                raise ValueError(f"column {col.name}: layout not supported")
-            ni, bi = cursor
-            ln, nc = nodes[ni]
-            own = bufs[bi:bi + col.nbuffers]
-            cursor[0] += 1
-            cursor[1] += col.nbuffers
-            for ch in col.children:
-                walk(ch)
-            if col.nbuffers == 2:
-                (vo, vl), (do, dl) = own
-                return ColumnChunk(ln, nc, BufferRef(body + vo, vl), BufferRef(body + do, dl))
-            return ColumnChunk(ln, nc, BufferRef(0, 0), BufferRef(0, 0))
-
-        for col in schema:
-            b.columns.append(walk(col))
-        batches.append(b)
-    return ArrowFile(schema, batches, src.size)
+    # Block structs: offset i64, metaDataLength i32 (+4 pad), bodyLength i64
+    raw = np.frombuffer(fbuf, np.dtype([("off", "<i8"), ("mlen", "<i4"), ("pad", "<i4"),
+                                        ("blen", "<i8")]), n, start)
+    blocks = np.stack([raw["off"], raw["mlen"].astype(np.int64), raw["blen"]], axis=1)
+    if n == 0:
+        return ArrowFile(schema, src.size)
+    lay, nn, nb = _layout(schema)
+    rows, codec, nodes, bufs = (_headers_native if native else _headers_py)(src, blocks, nn, nb)
+    body = blocks[:, 0] + blocks[:, 1]
+    keep = np.flatnonzero(codec != -2)
+    names = {c: _CODECS.get(c, "unknown") for c in set(codec[keep].tolist())}
+    bo = body[keep]
+    cols = []
+    for ni, bi, own in lay:
+        z = np.zeros(len(keep), np.int64)
+        if own == 2:
+            cols.append(ColumnArrays(nodes[keep, ni, 0], nodes[keep, ni, 1],
+                                     bo + bufs[keep, bi, 0], bufs[keep, bi, 1],
+                                     bo + bufs[keep, bi + 1, 0], bufs[keep, bi + 1, 1]))
+        else:
+            cols.append(ColumnArrays(nodes[keep, ni, 0], nodes[keep, ni, 1], z, z, z, z))
+    return ArrowFile(schema, src.size, blocks[keep, 0], rows[keep], bo, blocks[keep, 2],
+                     [names[c] for c in codec[keep].tolist()], cols)

@@ -2,6 +2,8 @@
 stream loader order restoration with page-cache chunks (emulated HBM)."""
 import os
 
+import struct
+
 import numpy as np
 import pytest
 
@@ -103,6 +105,10 @@ def test_arrow_ipc_metadata(tmp_path):
             for k in range(4):
                 w.write_batch(tbl.slice(k * 2500, 2500).to_batches()[0])
         m = read_metadata(path)
+        # native header reader (csrc/engine/arrow_meta.cc) == the Python walk,
+        # and == an in-memory source
+        assert m == read_metadata(path, native=False)
+        assert m == read_metadata(open(path, "rb").read())
         assert [c.name for c in m.schema] == ["s", "a", "f", "l"]
         assert [c.supported for c in m.schema] == [False, True, True, False]
         assert m.schema[2].numpy_dtype == "f4"
@@ -114,6 +120,63 @@ def test_arrow_ipc_metadata(tmp_path):
                 ref = b.columns[1].data
                 vals = raw[ref.offset:ref.offset + 2500 * 8].view(np.int64)
                 assert np.array_equal(vals, a[k * 2500:(k + 1) * 2500])
+
+
+def test_arrow_headers_malformed(tmp_path):
+    """A corrupted record-batch header is an error naming the batch, from
+    the native reader and from the Python walk (never a wild read)."""
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.utils.arrow_ipc import read_metadata
+    tbl = pa.table({"a": np.arange(4000, dtype=np.int64)})
+    path = str(tmp_path / "ok.arrow")
+    with ipc.new_file(path, tbl.schema) as w:
+        for k in range(4):
+            w.write_batch(tbl.slice(k * 1000, 1000).to_batches()[0])
+    m = read_metadata(path)
+    raw = bytearray(open(path, "rb").read())
+    hdr = m.batches[2].offset
+    rng = np.random.default_rng(3)
+    for trial in range(40):
+        bad = bytearray(raw)
+        # clobber the root offset / vtable region of batch 2's message
+        pos = hdr + 8 + int(rng.integers(0, 24))
+        bad[pos:pos + 4] = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        p = str(tmp_path / f"bad{trial}.arrow")
+        open(p, "wb").write(bad)
+        for native in (True, False):
+            try:
+                got = read_metadata(p, native=native)
+            except (ValueError, struct.error, IndexError, KeyError, UnicodeDecodeError):
+                continue
+            # an edit that still parses must leave the other batches intact
+            assert got.batches[0] == m.batches[0] or not native
+
+
+def test_arrow_headers_fuzz_asan(tmp_path):
+    """20k random edits of a real header through the native parser built
+    with ASan + UBSan (csrc/tests/arrow_meta_fuzz.cc)."""
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    import subprocess
+    from nvme_strom_amd.utils.arrow_ipc import read_metadata
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "build/arrow_meta_fuzz"], cwd=root, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rng = np.random.default_rng(0)
+    tbl = pa.table({"a": np.arange(4000, dtype=np.int64),
+                    "x": pa.array(rng.random(4000), mask=rng.random(4000) < 0.1)})
+    path = str(tmp_path / "f.arrow")
+    with ipc.new_file(path, tbl.schema, options=ipc.IpcWriteOptions(compression="lz4")) as w:
+        for k in range(4):
+            w.write_batch(tbl.slice(k * 1000, 1000).to_batches()[0])
+    b = read_metadata(path).batches[1]
+    r = subprocess.run([os.path.join(root, "build", "arrow_meta_fuzz"), path, str(b.offset),
+                        str(b.body_offset - b.offset), "20000"], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, TMPDIR=str(tmp_path)))
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "arrow_meta_fuzz:" in r.stdout and "rejected" in r.stdout
 
 
 def test_cpu_scan_block_range_and_resumable(strom, tmp_path):
