@@ -45,12 +45,27 @@
 namespace lz4p {
 
 constexpr uint32_t NT = 256;             // threads per stream (4 waves)
-constexpr uint32_t PW = 16384;           // compressed bytes per parse window
+#ifndef LZ4PAR_PW
+#define LZ4PAR_PW 16384
+#endif
+constexpr uint32_t PW = LZ4PAR_PW;       // compressed bytes per parse window
 constexpr uint32_t SL = PW / NT;         // slice per thread (64 B = 2 bitmap words)
+constexpr uint32_t SW = SL / 32;         // bitmap words per slice
 constexpr uint32_t PAD = 64;             // window overhang (reads past the window end)
-constexpr uint32_t OB = 4096;            // output bytes per resolve batch
-constexpr uint32_t HR = 32768;           // LDS ring of the latest output (history)
+#ifndef LZ4PAR_OB
+#define LZ4PAR_OB 4096
+#endif
+#ifndef LZ4PAR_HR
+#define LZ4PAR_HR 0
+#endif
+constexpr uint32_t OB = LZ4PAR_OB;       // output bytes per resolve batch
+constexpr uint32_t HR = LZ4PAR_HR;       // LDS ring of the latest output (history), 0: none
 constexpr uint32_t KW = OB / 4 / NT + 1; // output dwords a thread holds per batch
+constexpr uint32_t EPT = OB / NT;        // batch entries a thread expands (contiguous)
+constexpr uint32_t HW = OB / 32;         // run-head bitmap words
+constexpr uint32_t HS = (HW + 31) / 32;  // summary words (bit w: head word w not empty)
+static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT, "expansion tiling");
+static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 #ifndef LZ4PAR_LOOKBACK
 #define LZ4PAR_LOOKBACK 512
 #endif
@@ -76,7 +91,9 @@ struct Smem {
   uint32_t olen[NT];     // output bytes of slice t's true sequences
   uint32_t ost[NT];      // inclusive prefix of olen
   uint32_t ptr[OB];
-  uint8_t ring[HR];      // output byte at absolute position x: ring[x % HR]
+  uint32_t hb[HW];       // run heads of the batch (entries whose pointer fill wrote)
+  uint32_t hsum[HS];
+  uint8_t ring[HR ? HR : 4];   // output byte at absolute position x: ring[x % HR]
   // stream scalars (thread 0 writes, everyone reads after a barrier)
   uint32_t ip;           // input position of the next block header
   uint32_t bstart, bend; // current block
@@ -197,8 +214,7 @@ HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
 // (1) speculative chain of slice t
 HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
-  s.bits[2 * t] = 0;
-  s.bits[2 * t + 1] = 0;
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
   if (lo >= hi) {
     s.ex[t] = lo;
     return;
@@ -225,11 +241,12 @@ HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   if (ent < hi) {
     valid = getbit(s, ent);
   } else {
-    valid = s.bits[2 * t] == 0 && s.bits[2 * t + 1] == 0 && s.ex[t] == ent;
+    uint32_t any = 0;
+    for (uint32_t i = 0; i < SW; ++i) any |= s.bits[SW * t + i];
+    valid = any == 0 && s.ex[t] == ent;
   }
   if (valid) return false;
-  s.bits[2 * t] = 0;
-  s.bits[2 * t + 1] = 0;
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
   uint32_t p = ent;
   Seq q;
   while (p < hi) {
@@ -264,13 +281,34 @@ HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
   }
   s.olen[t] = o;
   s.ost[t] = o;
+  if (t < HW) s.hb[t] = 0;
+  if (t < HS) s.hsum[t] = 0;
 }
 
 // (3) inclusive scan step d (Hillis-Steele; read and write halves)
 HD uint32_t ph_scan_read(const Smem &s, uint32_t t, uint32_t d) { return t >= d ? s.ost[t - d] : 0; }
 HD void ph_scan_write(Smem &s, uint32_t t, uint32_t v) { s.ost[t] += v; }
 
-// (4a) source pointers of the batch [b0, b0 + OB) for slice t's sequences
+// (4a) source pointers of the batch [b0, b0 + OB): slice t's sequences
+// write the pointer of the FIRST byte of each run (literal run, match run;
+// a match run whose source crosses the batch start is two runs) and mark
+// it in the head bitmap; (4a') fills the rest.  Within a run the pointer
+// grows by one per byte in all three kinds (input position, stored output
+// position, batch index), so entry e = ptr[h] + (e - h) for the last head
+// h <= e.  Only the ~OB/(output per slice) threads whose slices meet the
+// batch have work in (4a); (4a') spreads the per-byte writes over all.
+HD void head(Smem &s, uint32_t e, uint32_t v) {
+  s.ptr[e] = v;
+  const uint32_t w = e >> 5;
+#ifdef __HIP_DEVICE_COMPILE__
+  atomicOr(&s.hb[w], 1u << (e & 31));
+  atomicOr(&s.hsum[w >> 5], 1u << (w & 31));
+#else
+  s.hb[w] |= 1u << (e & 31);
+  s.hsum[w >> 5] |= 1u << (w & 31);
+#endif
+}
+
 HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   if (lo >= hi) return;
@@ -283,9 +321,9 @@ HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
   while (p < hi && o < b1) {
     parse(s, c, p, s.bend, q);           // checked by ph_count
     const uint32_t le = o + q.lit;
-    if (le > b0) {
-      const uint32_t x0 = o > b0 ? o : b0, x1 = le < b1 ? le : b1;
-      for (uint32_t x = x0; x < x1; ++x) s.ptr[x - b0] = kLit | (q.lit0 + (x - o));
+    if (le > b0 && q.lit) {
+      const uint32_t x0 = o > b0 ? o : b0;
+      head(s, x0 - b0, kLit | (q.lit0 + (x0 - o)));
     }
     o = le;
     if (!q.last) {
@@ -296,14 +334,53 @@ HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
           return;
         }
         const uint32_t x0 = o > b0 ? o : b0, x1 = me < b1 ? me : b1;
-        for (uint32_t x = x0; x < x1; ++x) {
-          const uint32_t src = opw + x - q.off;            // absolute output position
-          s.ptr[x - b0] = src < opw + b0 ? (kHist | src) : (x - q.off - b0);
+        // source of byte x: absolute opw + x - off; inside the batch (index
+        // x - off - b0) from x = b0 + off on, stored history before
+        const uint32_t xs = b0 + q.off;
+        if (x0 < xs) {
+          head(s, x0 - b0, kHist | (opw + x0 - q.off));
+          if (xs < x1) head(s, xs - b0, 0);
+        } else {
+          head(s, x0 - b0, x0 - q.off - b0);
         }
       }
       o = me;
     }
     p = q.next;
+  }
+}
+
+HD uint32_t clz32(uint32_t x) { return (uint32_t)__builtin_clz(x); }
+
+// (4a') expansion: thread t fills entries [t * EPT, t * EPT + EPT)
+HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
+  const uint32_t e0 = t * EPT;
+  if (e0 >= nb) return;
+  const uint32_t w = e0 >> 5, sh = e0 & 31;
+  // the last head at or before e0 (entry 0 always is one)
+  const uint32_t m = s.hb[w] & (0xffffffffu >> (31 - sh));
+  uint32_t h = 0;
+  if (m) {
+    h = (w << 5) + 31 - clz32(m);
+  } else if (w) {
+    int32_t sw = (int32_t)((w - 1) >> 5);
+    uint32_t sm = s.hsum[sw] & (0xffffffffu >> (31 - ((w - 1) & 31)));
+    while (!sm && --sw >= 0) sm = s.hsum[sw];
+    if (sm) {
+      const uint32_t wl = ((uint32_t)sw << 5) + 31 - clz32(sm);
+      h = (wl << 5) + 31 - clz32(s.hb[wl]);
+    }
+  }
+  uint32_t cur = h, base = s.ptr[h];
+  const uint32_t hm = s.hb[w] >> sh;
+  for (uint32_t i = 0; i < EPT; ++i) {
+    const uint32_t e = e0 + i;
+    if ((hm >> i) & 1u) {
+      cur = e;
+      base = s.ptr[e];
+    } else {
+      s.ptr[e] = base + (e - cur);
+    }
   }
 }
 
@@ -367,7 +444,7 @@ HD void ph_resolve(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_
           x = inb(s, c, v & ~kLit);
         } else {
           const uint32_t hp = v & ~kHist;
-          x = bs - hp <= HR ? s.ring[hp & (HR - 1)] : hist_byte(c, hp);
+          x = HR && bs - hp <= HR ? s.ring[hp & (HR - 1)] : hist_byte(c, hp);
         }
         w |= (uint32_t)x << (8 * b);
       }
@@ -382,6 +459,8 @@ HD void ph_write(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb, co
   const uint32_t mis = (uint32_t)((uintptr_t)base & 3);
   const uint32_t nw = (nb + mis + 3) / 4;
   const uint32_t bs = s.op + b0;
+  if (t < HW) s.hb[t] = 0;               // heads of the next batch start empty
+  if (t < HS) s.hsum[t] = 0;
   for (uint32_t j = 0; j < KW; ++j) {
     const uint32_t k = t + j * NT;
     if (k >= nw) break;
@@ -389,13 +468,14 @@ HD void ph_write(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb, co
     const uint32_t w = h.w[j];
     if (e0 >= 0 && (uint32_t)e0 + 4 <= nb) {
       *(uint32_t *)(base + e0) = w;
-      for (uint32_t b = 0; b < 4; ++b) s.ring[(bs + e0 + b) & (HR - 1)] = (uint8_t)(w >> (8 * b));
+      if (HR)
+        for (uint32_t b = 0; b < 4; ++b) s.ring[(bs + e0 + b) & (HR - 1)] = (uint8_t)(w >> (8 * b));
     } else {
       for (uint32_t b = 0; b < 4; ++b) {
         const int32_t e = e0 + (int32_t)b;
         if (e >= 0 && (uint32_t)e < nb) {
           base[e] = (uint8_t)(w >> (8 * b));
-          s.ring[(bs + e) & (HR - 1)] = (uint8_t)(w >> (8 * b));
+          if (HR) s.ring[(bs + e) & (HR - 1)] = (uint8_t)(w >> (8 * b));
         }
       }
     }
@@ -410,7 +490,7 @@ HD void ph_rawcopy(Smem &s, const Ctx &c, uint32_t t) {
   for (uint32_t i = t; i < n; i += NT) {
     const uint8_t x = c.in[s.bstart + i];
     c.out[s.op + i] = x;
-    if (i >= keep) s.ring[(s.op + i) & (HR - 1)] = x;
+    if (HR && i >= keep) s.ring[(s.op + i) & (HR - 1)] = x;
   }
 }
 
@@ -518,7 +598,7 @@ HD void st_window(Smem &s, const Ctx &c, uint32_t ws) {
 // stamps s_memtime at each phase boundary; strom_lz4par_prof() returns the
 // sums (tools/lz4par_bench.py --prof)
 enum : int { kLpHdr, kLpLoad, kLpSpec, kLpValid, kLpScan, kLpFill, kLpDouble, kLpResolve,
-             kLpWrite, kLpRaw, kLpNWin, kLpNRound, kLpNBatch, kLpNDouble, kLpN };
+             kLpWrite, kLpRaw, kLpExpand, kLpNWin, kLpNRound, kLpNBatch, kLpNDouble, kLpN };
 #ifdef STROM_DECOMP_PROF
 __device__ unsigned long long g_lz4par_prof[kLpN];
 #define LP_INIT() uint64_t lp[kLpN] = {0}; uint64_t lp_t = __builtin_amdgcn_s_memtime()
@@ -618,6 +698,9 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
           __syncthreads();
           LP_MARK(kLpFill);
           if (s.err) break;
+          ph_expand(s, t, nb);
+          __syncthreads();
+          LP_MARK(kLpExpand);
           bool more;
           do {
             LP_CNT(kLpNDouble);
@@ -735,6 +818,7 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
         const uint32_t nb = s.total - b0 < OB ? s.total - b0 : OB;
         for (uint32_t t = 0; t < NT; ++t) ph_fill(s, c, t, b0);
         if (s.err) break;
+        for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
         do {
           ++dbl;
           any = false;

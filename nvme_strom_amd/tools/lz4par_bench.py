@@ -43,7 +43,7 @@ def frames(kind: str, k: int, seed: int = 1):
 
 
 PHASES = ("hdr", "load", "spec", "validate", "count_scan", "fill", "double", "resolve", "write",
-          "rawcopy")
+          "rawcopy", "expand")
 COUNTS = ("windows", "valid_rounds", "batches", "double_rounds")
 
 
@@ -79,6 +79,9 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--prof", action="store_true",
                     help="phase cycle profile of the par decoder (libstrom_decprof.so)")
+    ap.add_argument("--variants", default="",
+                    help="comma list of lib/lz4v/<name>.so geometry builds (make lz4v) to time too")
+    ap.add_argument("--no-lanes", dest="lanes", action="store_false")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -88,6 +91,18 @@ def main(argv=None) -> int:
 
     dev = torch.device("cuda")
     res = {"rows": []}
+    import ctypes as C
+    import os
+    decoders = ([("lanes", lib().strom_decompress_lanes)] if a.lanes else []) + \
+        [("par", lib().strom_decompress_par)]
+    for v in [x for x in a.variants.split(",") if x]:
+        so = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib", "lz4v",
+                                 v + ".so"))
+        f = so.strom_decompress_par
+        f.restype = C.c_int
+        f.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                      C.c_void_p]
+        decoders.append((v, f))
     for kind in a.kinds.split(","):
         raws, bufs = frames(kind, a.distinct)
         rawlen = len(raws[0])
@@ -104,8 +119,8 @@ def main(argv=None) -> int:
             dst = torch.empty(n * cap, dtype=torch.uint8, device=dev)
             status = torch.empty(n, dtype=torch.int32, device=dev)
             row = dict(kind=kind, streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
-            for name, fn in (("lanes", "strom_decompress_lanes"), ("par", "strom_decompress_par")):
-                f = getattr(lib(), fn)
+            for name, f in decoders:
+                fn = name
                 times = []
                 ok = True
                 for it in range(a.iters + 1):
@@ -127,7 +142,8 @@ def main(argv=None) -> int:
                 row[f"{name}_GBps"] = round(n * rawlen / med / 1e9, 2)
                 row[f"{name}_ms"] = round(med * 1e3, 3)
                 row[f"{name}_verified"] = ok
-            row["speedup"] = round(row["par_GBps"] / row["lanes_GBps"], 2) if row["lanes_GBps"] else None
+            if a.lanes:
+                row["speedup"] = round(row["par_GBps"] / row["lanes_GBps"], 2)
             if a.prof:
                 row["par_phases"] = prof(n, src, dst, d_desc, status)
             _log(json.dumps(row))
@@ -139,7 +155,8 @@ def main(argv=None) -> int:
         with open(a.out, "w") as fo:
             fo.write(js)
     print(js)
-    return 0 if all(r["par_verified"] and r["lanes_verified"] for r in res["rows"]) else 3
+    ok = all(v for r in res["rows"] for k, v in r.items() if k.endswith("_verified"))
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":
