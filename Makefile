@@ -19,7 +19,7 @@ ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
-all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_waveprof.so
+all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so
 
 tools: $(TOOLS)
 
@@ -40,19 +40,14 @@ $(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ) $(CORE_OBJ)
 	$(HIPCC) $(LDFLAGS) --offload-arch=$(ARCH) -o $@ $^
 
 # the LZ4/snappy decoder with its cycle profile compiled in (tools/decomp_prof.py)
-$(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip csrc/include/strom/strom.h
+$(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/kernels/lz4par.hip csrc/include/strom/strom.h
 	@mkdir -p $(OUT)
-	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ csrc/kernels/decompress.hip csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip
-
-# the wave-per-stream decoder with its phase profile (tools/wave_prof.py)
-$(OUT)/libstrom_waveprof.so: csrc/kernels/decompress_wave.hip csrc/include/strom/strom.h
-	@mkdir -p $(OUT)
-	$(HIPCC) $(HIPFLAGS) -DSTROM_WAVE_PROF -shared -o $@ $<
+	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ csrc/kernels/decompress.hip csrc/kernels/lz4par.hip
 
 # a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
 # make ab AB=name [SRC=path/to/decompress.hip]
 SRC ?= csrc/kernels/decompress.hip
-WSRC ?= csrc/kernels/decompress_wave.hip csrc/kernels/lz4par.hip
+WSRC ?= csrc/kernels/lz4par.hip
 ab:
 	@mkdir -p $(OUT)/ab
 	$(HIPCC) $(HIPFLAGS) -Icsrc/include -shared -o $(OUT)/ab/$(AB).so $(SRC) $(WSRC)
@@ -62,7 +57,7 @@ $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
-	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_waveprof.so $(TOOLS)
+	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(TOOLS)
 
 .PHONY: all tools clean ab
 

@@ -848,29 +848,26 @@ extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
                                       const strom_decomp_desc *d_desc, uint32_t nblocks,
                                       int32_t *d_status, void *stream);
 
-// decompress_wave.hip: one wave per stream (few, long streams)
-extern "C" int strom_decompress_wave(int codec, const void *d_src, void *d_dst,
-                                     const strom_decomp_desc *d_desc, uint32_t nblocks,
-                                     int32_t *d_status, void *stream);
-
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
 // STROM_DECOMP_G (1, 4, 8, 16; 32 = 16 with the small ring; 3 / 2 / 6 = 1 /
-// 2 / 4 streams per wave with 16 / 16 / 8 KiB rings; 64 = wave per stream)
+// 2 / 4 streams per wave with 16 / 16 / 8 KiB rings)
 // forces a geometry (A/B runs).
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
   if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_ARROW_LZ4) return -22;
   if (!nblocks) return 0;
-  // Few LZ4 streams: the block-parallel decoder (lz4par.hip) — a stream is
-  // decoded by a whole workgroup, so a launch no longer takes one serial
-  // stream's time (profiles/r3/dec: 2,048 config-5 frames 27.8 -> 65.5
-  // GB/s, 256 frames 3.8 -> 35).  From ~8k streams the lane groups keep
-  // up or win (val equal, ids / text faster).  STROM_DECOMP_PAR=0/1 forces.
+  // Up to 8,192 LZ4 streams: the block-parallel decoder (lz4par.hip) — a
+  // stream is decoded by a whole workgroup, so a launch no longer takes one
+  // serial stream's time (profiles/r3/dec/lz4par_threshold.json, 512 KiB
+  // frames, par vs lanes GB/s: 4,096 val 115/48, ids 104/58, text 56/54;
+  // 8,192 val 116/66, ids 106/83, text 56/78).  From 16k streams the lane
+  // groups win on near-match data (ids 194/108, text 170/57; val, a quarter
+  // of its matches past 2 KiB, stays 118/52).  STROM_DECOMP_PAR=0/1 forces.
   const char *pe = getenv("STROM_DECOMP_PAR");
   const bool lz4 = codec != STROM_CODEC_SNAPPY && codec != STROM_CODEC_COPY;
-  if (lz4 && (pe ? atoi(pe) != 0 : nblocks <= 4096))
+  if (lz4 && (pe ? atoi(pe) != 0 : nblocks <= 8192))
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   return strom_decompress_lanes(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
 }
@@ -893,10 +890,6 @@ extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
   //   <= 4,096: 4 per wave, 8 KiB rings;  <= 8,192: 4 per wave, 2 KiB rings
   if (!e)
     g = nblocks <= 1024 ? 3 : nblocks <= 2048 ? 2 : nblocks <= 4096 ? 6 : nblocks <= 8192 ? 4 : 16;
-  // wave per stream (decompress_wave.hip): forced only; the large-ring lane
-  // groups measured as fast or faster at every count
-  if (g == 64 || g == 65)
-    return strom_decompress_wave(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   if (g != 1 && g != 2 && g != 3 && g != 4 && g != 6 && g != 8 && g != 16 && g != 32) g = 16;
   hipStream_t st = (hipStream_t)stream;
   if (g == 2) return launch<S2L>(codec, d_src, d_dst, d_desc, nblocks, d_status, st);
