@@ -84,13 +84,13 @@ build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
 	$(ROCM)/llvm/bin/clang++ $(SELFTEST_FLAGS) -fsanitize=thread -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
 
 # lz4par geometry variants for A/B timing (tools/lz4par_bench.py --variants):
-# make lz4v LZ4V="PW:OB:HR:LB ..." -> $(OUT)/lz4v/pw<PW>_ob<OB>_hr<HR>_lb<LB>.so
-LZ4V ?= 16384:4096:0:512 8192:4096:0:256 8192:4096:0:512 8192:2048:0:256 16384:2048:0:512
+# make lz4v LZ4V="name:-DX=1,-DY=2 ..." -> $(OUT)/lz4v/<name>.so (lz4par.hip
+# with those macros: LZ4PAR_PW / _OB / _HR / _LOOKBACK / _DBL / _RES)
+LZ4V ?= base:-DLZ4PAR_HR=0
 lz4v:
 	@rm -rf $(OUT)/lz4v && mkdir -p $(OUT)/lz4v
-	@for v in $(LZ4V); do set -- $$(echo $$v | tr : ' '); pw=$$1; ob=$$2; hr=$$3; lb=$$4; \
-	  $(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_PW=$$pw -DLZ4PAR_OB=$$ob -DLZ4PAR_HR=$$hr \
-	    -DLZ4PAR_LOOKBACK=$$lb -shared -o $(OUT)/lz4v/pw$${pw}_ob$${ob}_hr$${hr}_lb$${lb}.so \
+	@for v in $(LZ4V); do name=$${v%%:*}; defs=$$(echo $${v#*:} | tr , ' '); \
+	  $(HIPCC) $(HIPFLAGS) -Icsrc/include $$defs -shared -o $(OUT)/lz4v/$$name.so \
 	    csrc/kernels/lz4par.hip || exit 1; done
 .PHONY: lz4v
 

@@ -64,7 +64,7 @@ constexpr uint32_t KW = OB / 4 / NT + 1; // output dwords a thread holds per bat
 constexpr uint32_t EPT = OB / NT;        // batch entries a thread expands (contiguous)
 constexpr uint32_t HW = OB / 32;         // run-head bitmap words
 constexpr uint32_t HS = (HW + 31) / 32;  // summary words (bit w: head word w not empty)
-static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT, "expansion tiling");
+static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 #ifndef LZ4PAR_LOOKBACK
 #define LZ4PAR_LOOKBACK 512
@@ -83,14 +83,21 @@ static_assert(SL % 32 == 0, "slices cover whole bitmap words");
 enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3 };
 enum : uint32_t { kModeBlock = 0, kModeDone = 1 };
 
+// LDS bank spreading (32 banks of 4 bytes).  Thread t works at slice t of
+// the window (SL = 64 bytes: the same bank every 2 lanes) and expands
+// entries [16t, 16t + 16) of the pointer batch (again every 2 lanes): one
+// pad dword per 128 window bytes / per 32 entries puts 32 lanes on 32
+// distinct banks.
+HD constexpr uint32_t WI(uint32_t r) { return r + ((r >> 7) << 2); }
+HD constexpr uint32_t PI(uint32_t e) { return e + (e >> 5); }
+
 struct Smem {
-  uint8_t win[PW + PAD];
+  uint8_t win[WI(PW + PAD) + 4];
   uint32_t bits[PW / 32];
   uint32_t ex[NT];       // exit of slice t's chain
   uint32_t en[NT];       // true entry of slice t
-  uint32_t olen[NT];     // output bytes of slice t's true sequences
-  uint32_t ost[NT];      // inclusive prefix of olen
-  uint32_t ptr[OB];
+  uint32_t ost[NT];      // output bytes of slice t's true sequences, then their inclusive prefix
+  uint32_t ptr[PI(OB)];
   uint32_t hb[HW];       // run heads of the batch (entries whose pointer fill wrote)
   uint32_t hsum[HS];
   uint8_t ring[HR ? HR : 4];   // output byte at absolute position x: ring[x % HR]
@@ -117,7 +124,7 @@ struct Ctx {
 // ---------------------------------------------------------------- input
 HD uint8_t inb(const Smem &s, const Ctx &c, uint32_t p) {
   const uint32_t r = p - s.ws;
-  if (r < s.wload) return s.win[r];
+  if (r < s.wload) return s.win[WI(r)];
   return p < c.len ? c.in[p] : 0;
 }
 
@@ -206,7 +213,7 @@ HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
 #pragma unroll
     for (uint32_t j = 0; j < U; ++j) {
       const uint32_t i = t + (j0 + j) * NT;
-      if (i < s.wload) s.win[i] = r[j];
+      if (i < s.wload) s.win[WI(i)] = r[j];
     }
   }
 }
@@ -279,7 +286,6 @@ HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
       p = q.next;
     }
   }
-  s.olen[t] = o;
   s.ost[t] = o;
   if (t < HW) s.hb[t] = 0;
   if (t < HS) s.hsum[t] = 0;
@@ -298,7 +304,7 @@ HD void ph_scan_write(Smem &s, uint32_t t, uint32_t v) { s.ost[t] += v; }
 // h <= e.  Only the ~OB/(output per slice) threads whose slices meet the
 // batch have work in (4a); (4a') spreads the per-byte writes over all.
 HD void head(Smem &s, uint32_t e, uint32_t v) {
-  s.ptr[e] = v;
+  s.ptr[PI(e)] = v;
   const uint32_t w = e >> 5;
 #ifdef __HIP_DEVICE_COMPILE__
   atomicOr(&s.hb[w], 1u << (e & 31));
@@ -309,14 +315,25 @@ HD void head(Smem &s, uint32_t e, uint32_t v) {
 #endif
 }
 
-HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
+// where slice t's walk resumes in the next batch: its first sequence not
+// completely before the batch (set per window, advanced by ph_fill)
+struct FillPos {
+  uint32_t p, o;
+};
+
+HD void ph_fill_init(const Smem &s, uint32_t t, FillPos &f) {
+  f.p = s.en[t];
+  f.o = t ? s.ost[t - 1] : 0;
+}
+
+HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, FillPos &f) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   if (lo >= hi) return;
-  const uint32_t o1 = s.ost[t], o0 = o1 - s.olen[t];
+  const uint32_t o1 = s.ost[t], o0 = t ? s.ost[t - 1] : 0;
   const uint32_t b1 = b0 + OB;
   if (o1 <= b0 || o0 >= b1) return;
   const uint32_t opw = s.op;             // output position of the window start
-  uint32_t p = s.en[t], o = o0;
+  uint32_t p = f.p, o = f.o;
   Seq q;
   while (p < hi && o < b1) {
     parse(s, c, p, s.bend, q);           // checked by ph_count
@@ -347,6 +364,10 @@ HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
       o = me;
     }
     p = q.next;
+    if (o <= b1) {                       // done with it: the next batch starts later
+      f.p = p;
+      f.o = o;
+    }
   }
 }
 
@@ -371,15 +392,15 @@ HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
       h = (wl << 5) + 31 - clz32(s.hb[wl]);
     }
   }
-  uint32_t cur = h, base = s.ptr[h];
+  uint32_t cur = h, base = s.ptr[PI(h)];
   const uint32_t hm = s.hb[w] >> sh;
   for (uint32_t i = 0; i < EPT; ++i) {
     const uint32_t e = e0 + i;
     if ((hm >> i) & 1u) {
       cur = e;
-      base = s.ptr[e];
+      base = s.ptr[PI(e)];
     } else {
-      s.ptr[e] = base + (e - cur);
+      s.ptr[PI(e)] = base + (e - cur);
     }
   }
 }
@@ -387,14 +408,17 @@ HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
 // (4b) one pointer-doubling round over the batch; true while any pointer
 // still points inside the batch
 HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
+  // in order, each replacement visible to the thread's later entries (a
+  // chain through this thread's entries collapses within the round;
+  // reading all entries before writing any measured 30 % slower)
   bool more = false;
   for (uint32_t e = t; e < nb; e += NT) {
-    const uint32_t v = s.ptr[e];
+    const uint32_t v = s.ptr[PI(e)];
     if (!(v & kTag)) {
       // v < e always (a match reads backwards); the bound only keeps a
       // corrupt table inside the array
-      const uint32_t w = v < e ? s.ptr[v] : kLit;
-      s.ptr[e] = w;
+      const uint32_t w = v < e ? s.ptr[PI(v)] : kLit;
+      s.ptr[PI(e)] = w;
       more |= !(w & kTag);
     }
   }
@@ -438,7 +462,7 @@ HD void ph_resolve(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_
       for (uint32_t b = 0; b < 4; ++b) {
         const int32_t e = (int32_t)(4 * k + b) - (int32_t)mis;
         if (e < 0 || (uint32_t)e >= nb) continue;
-        const uint32_t v = s.ptr[e];
+        const uint32_t v = s.ptr[PI(e)];
         uint8_t x;
         if (v & kLit) {
           x = inb(s, c, v & ~kLit);
@@ -691,10 +715,12 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
         LP_MARK(kLpScan);
         if (s.err) break;
         const uint32_t total = s.total;
+        FillPos fpos;
+        ph_fill_init(s, t, fpos);
         for (uint32_t b0 = 0; b0 < total; b0 += OB) {
           LP_CNT(kLpNBatch);
           const uint32_t nb = total - b0 < OB ? total - b0 : OB;
-          ph_fill(s, c, t, b0);
+          ph_fill(s, c, t, b0, fpos);
           __syncthreads();
           LP_MARK(kLpFill);
           if (s.err) break;
@@ -768,13 +794,15 @@ extern "C" int strom_lz4par_prof(uint64_t *out) {
 extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
                                  uint32_t cap, uint32_t *stats) {
   using namespace lz4p;
-  static_assert(sizeof(Smem) <= 80 * 1024, "LDS: two workgroups per CU");
+  static_assert(PW != 16384 || OB != 4096 || HR != 0 || sizeof(Smem) <= 40 * 1024,
+                "default geometry: four workgroups per CU (160 KiB LDS)");
   Smem *sp = new Smem;
   Smem &s = *sp;
   Ctx c{src, dst, src_len, cap};
   uint32_t ent[NT];
   bool flag[NT];
   Held *held = new Held[NT];
+  FillPos *fpos = new FillPos[NT];
   uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0;
   st_header(s, c, codec);
   for (;;) {
@@ -814,9 +842,10 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
       s.total = s.ost[NT - 1];
       if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
       if (s.err) break;
+      for (uint32_t t = 0; t < NT; ++t) ph_fill_init(s, t, fpos[t]);
       for (uint32_t b0 = 0; b0 < s.total; b0 += OB) {
         const uint32_t nb = s.total - b0 < OB ? s.total - b0 : OB;
-        for (uint32_t t = 0; t < NT; ++t) ph_fill(s, c, t, b0);
+        for (uint32_t t = 0; t < NT; ++t) ph_fill(s, c, t, b0, fpos[t]);
         if (s.err) break;
         for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
         do {
@@ -842,5 +871,6 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
   const int r = s.err ? s.err : (int)s.op;
   delete sp;
   delete[] held;
+  delete[] fpos;
   return r;
 }

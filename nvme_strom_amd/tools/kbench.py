@@ -105,11 +105,13 @@ def main(argv=None):
             if codec == "lz4" and dname == "words":
                 # the same streams under each geometry (streams per wave), and
                 # a few-streams launch (an Arrow scan group: ~1k buffers)
+                os.environ["STROM_DECOMP_PAR"] = "0"         # lane groups only
                 for g in (16, 8, 4, 1):
                     os.environ["STROM_DECOMP_G"] = str(g)
                     log(f"decompress_lz4_64k_g{g}",
                         timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
                 os.environ.pop("STROM_DECOMP_G", None)
+                os.environ.pop("STROM_DECOMP_PAR", None)
                 few = min(nblk, 1024)
                 log(f"decompress_lz4_64k_{few}streams",
                     timed(lambda: D.decompress(cid, src, dst, descs[:few]), 3), few * len(blk))
@@ -133,8 +135,8 @@ def main(argv=None):
             log(f"decompress_{codec}_{tag}_distinct61",
                 timed(lambda: D.decompress(cid, src, dst, descs), 3), nblk * len(blk))
             del src, dst
-    if "wave" in only:
-        _wave_rows(D, dev, log)
+    if "par" in only:
+        _par_rows(D, dev, log)
     if "filter" in only:
         nv = n // 8
         v = torch.randint(-1000, 1000, (nv,), dtype=torch.int64, device=dev)
@@ -148,9 +150,9 @@ def main(argv=None):
     print(js)
 
 
-def _wave_rows(D, dev, log):
-    """Lane-group (g16) vs wave-per-stream (g64) decoder by stream count:
-    61 distinct 64 KiB blocks per codec/corpus, and config-5-shaped streams
+def _par_rows(D, dev, log):
+    """Lane-group vs block-parallel (lz4par.hip) LZ4 decoder by stream
+    count: 61 distinct 64 KiB blocks per corpus, and config-5-shaped streams
     (pyarrow LZ4 frames of 512 KiB, eight linked 64 KiB blocks each)."""
     from nvme_strom_amd.tools.decomp_ab import corpora
 
@@ -167,19 +169,19 @@ def _wave_rows(D, dev, log):
                                    (i // k) * int(osz[-1]) + int(osz[i % k]), sizes[i % k])
                                   for i in range(cnt)])
             total = sum(sizes[i % k] for i in range(cnt))
-            for g in ("16", "64"):
-                os.environ["STROM_DECOMP_G"] = g
+            for g in ("lanes", "par"):
+                os.environ["STROM_DECOMP_PAR"] = "1" if g == "par" else "0"
                 st = D.decompress(cid, src, dst, descs)
                 assert (st == np.array([sizes[i % k] for i in range(cnt)])).all(), (g, st[:4])
                 j = cnt - 1
                 lo = (j // k) * int(osz[-1]) + int(osz[j % k])
                 assert bytes(dst[lo:lo + 4096].cpu().numpy()) == corpus_out[j % k][:4096]
-                log(f"wave_{tag}_{cnt}streams_g{g}",
+                log(f"{g}_{tag}_{cnt}streams",
                     timed(lambda: D.decompress(cid, src, dst, descs), 3), total)
-            os.environ.pop("STROM_DECOMP_G", None)
+            os.environ.pop("STROM_DECOMP_PAR", None)
             del src, dst
 
-    for codec in ("lz4", "snappy"):
+    for codec in ("lz4",):
         for dname in ("words", "ints"):
             corpus_out = [corpora(1 + k)[dname] for k in range(61)]
             comps = [D.lz4_compress(b) if codec == "lz4" else D.snappy_compress(b) for b in corpus_out]

@@ -7,9 +7,8 @@
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (default flagship config)
 #   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
-#   wave       decoder rows by stream count: lane-group (g16) vs wave-per-stream (g64)
+#   par        LZ4 decoder rows by stream count: lane groups vs block-parallel (lz4par)
 #   dtests     decoder numerics tests only
-#   waveprof   wave-per-stream decoder phase profile (libstrom_waveprof.so)
 #   ktrace     rocprofv3 kernel trace + stats of a short kbench
 #   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
 #   btrace     rocprofv3 kernel + memory-copy trace of a short bench run
@@ -45,8 +44,7 @@ for phase in "$@"; do
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
-    wave) step wave 300 python -u -m nvme_strom_amd.tools.kbench --only wave --out "$OUT/wave.json" ;;
-    waveprof) step waveprof 200 python -u -m nvme_strom_amd.tools.wave_prof --out "$OUT/waveprof.json" ;;
+    par) step par 300 python -u -m nvme_strom_amd.tools.kbench --only par --out "$OUT/par.json" ;;
     dtests) step dtests 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q \
               --timeout 120 --timeout-method thread -k "lz4 or snappy or malformed or geometr" ;;
     ktrace) (cd /tmp && step ktrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o trace \
