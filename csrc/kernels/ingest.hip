@@ -28,6 +28,19 @@
 // Termination: the host sets *stop whenever the engine goes idle (no request
 // outstanding) and before it exits; every spin in here re-reads *stop, so the
 // grid always drains.
+//
+// Consumer contract (what the visibility argument above covers): done[] is
+// read by the HOST (ingest.cc), which then completes the task; the bytes
+// are consumed by work ordered after that completion — a kernel launched
+// afterwards (launch = acquire at agent scope, so every XCD's L2 sees the
+// written-through lines), hipMemcpy/SDMA, or an RCCL collective issued
+// afterwards (tests: test_pread_gpu_visible_to_next_kernel,
+// test_pread_gpu_visible_to_sdma_readback).  An ALREADY-RUNNING kernel
+// polling done[] on another XCD is NOT a supported consumer: it would need
+// a system-scope acquire on done[] and an L2 invalidate of its own XCD
+// (buffer_inv sc1) before reading the payload, and nothing in the engine
+// does that — a fused ingest-then-decode pipeline would have to add both and
+// its own test first.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
