@@ -21,7 +21,8 @@ ceiling — GiB/s, IOPS and QD1 p50/p99 of the engine alone — and ``raw_*`` is
 the same rings reading the cached file into host RAM.
 
 ``--ab KEY`` runs every size twice, KEY=0 and KEY=1 interleaved (e.g.
-``--ab fixed_bufs``: io_uring registered staging + READ_FIXED vs plain READ).
+``--ab fixed_bufs``: io_uring registered staging + READ_FIXED vs plain READ);
+``--ab KEY=v1,v2,..`` takes those values (e.g. ``--ab workers=4,8,16``).
 
 ``python -m nvme_strom_amd.tools.sweep --out gpurun_out/sweep.json``
 """
@@ -79,10 +80,16 @@ def main(argv=None) -> int:
                     help="skip the raw io_uring ceiling per block size")
     ap.add_argument("--engine-only", action="store_true",
                     help="backend=cache: page-cache reads through the full engine path")
-    ap.add_argument("--ab", default="", help="config key to A/B (0 vs 1) at every size")
+    ap.add_argument("--ab", default="",
+                    help="config key to A/B at every size: KEY (0 vs 1) or KEY=v1,v2,..")
     ap.add_argument("--reps", type=int, default=1, help="repetitions of every (size, arm)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
+    arms = (None,)
+    if a.ab:
+        key, _, vals = a.ab.partition("=")
+        a.ab = key
+        arms = tuple(int(v) for v in vals.split(",")) if vals else (0, 1)
 
     import torch
 
@@ -113,8 +120,7 @@ def main(argv=None) -> int:
     rows = []
     sizes = [size(x) for x in a.blocks.split(",")]
     # interleaved arms, --reps times each (the box's storage drifts)
-    runs = [(B, v) for B in sizes for _ in range(a.reps)
-            for v in ((0, 1) if a.ab else (None,))]
+    runs = [(B, v) for B in sizes for _ in range(a.reps) for v in arms]
     try:
         for B, abv in runs:
             kv = {"max_request": B}
