@@ -1,8 +1,13 @@
-"""Build libstrom.so (engine + gfx950 kernels) and the CLI tools in-tree.
+"""Build libstrom.so (engine + gfx950 kernels) and the CLI tools in-tree,
+then check what was built.
 
-``python -m nvme_strom_amd.build [-j N] [--clean]`` — a thin driver over the
-top-level Makefile so the same build runs here (cross-compiling for gfx950
-without a GPU) and on the GPU box.
+``python -m nvme_strom_amd.build [-j N] [--clean]`` drives the top-level
+Makefile (the same build runs here, cross-compiling for gfx950 without a
+GPU, and on the GPU box) and then ``check()``s the result: every entry
+point the ctypes binding declares (``_native._SIGS``) must be exported by
+the library, and the library must carry a gfx950 code object — a missing
+kernel or a stale build fails here, not at the first call on a GPU box.
+``__graft_entry__.build()`` is this function.
 """
 from __future__ import annotations
 
@@ -23,6 +28,26 @@ def build(jobs: int = 0, clean: bool = False, target: str = "all") -> None:
     subprocess.run(["make", "-C", ROOT, f"-j{jobs}", target], check=True, env=env)
 
 
+def check() -> dict:
+    """Exported symbols and the offload target of the built libstrom.so."""
+    import ctypes as C
+
+    from . import _native
+    path = _native.LIB_PATH
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: the build produced no library")
+    lib = C.CDLL(path)
+    missing = [n for n in _native._SIGS if not hasattr(lib, n)]
+    if missing:
+        raise RuntimeError(f"{path} lacks entry points the binding declares: {missing}")
+    with open(path, "rb") as f:
+        blob = f.read()
+    if b"gfx950" not in blob:
+        raise RuntimeError(f"{path} carries no gfx950 code object")
+    return dict(library=path, entry_points=len(_native._SIGS), target="gfx950",
+                bytes=len(blob))
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", "--jobs", type=int, default=0)
@@ -30,6 +55,7 @@ def main(argv=None) -> int:
     ap.add_argument("target", nargs="?", default="all")
     a = ap.parse_args(argv)
     build(a.jobs, a.clean, a.target)
+    print(check())
     return 0
 
 
