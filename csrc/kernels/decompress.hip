@@ -844,9 +844,22 @@ extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
                                     const strom_decomp_desc *d_desc, uint32_t nstreams,
                                     int32_t *d_status, void *stream);
 
+extern "C" int strom_decompress_par512(int codec, const void *d_src, void *d_dst,
+                                       const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                       int32_t *d_status, void *stream);
+
 extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
                                       const strom_decomp_desc *d_desc, uint32_t nblocks,
                                       int32_t *d_status, void *stream);
+
+// CUs of the current device (resident-workgroup arithmetic of the dispatch)
+static uint32_t device_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return (uint32_t)n;
+}
 
 // Streams per wave by stream count: keep >= ~8 waves per CU (256 CUs)
 // when there are enough streams, else give each stream more lanes.
@@ -864,11 +877,20 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // frames, par vs lanes GB/s: 4,096 val 115/48, ids 104/58, text 56/54;
   // 8,192 val 116/66, ids 106/83, text 56/78).  From 16k streams the lane
   // groups win on near-match data (ids 194/108, text 170/57; val, a quarter
-  // of its matches past 2 KiB, stays 118/52).  STROM_DECOMP_PAR=0/1 forces.
+  // of its matches past 2 KiB, stays 118/52).  Streams that fit in one
+  // round of the 512-thread build's resident workgroups (2 per CU) take it:
+  // shorter per-stream chains (lz4par_nt512.hip; 512 config-5 frames 61 ->
+  // 85 GB/s, 640 frames 73 -> 56: profiles/r3/dec/lz4par_nt_crossover.json).
+  // STROM_DECOMP_PAR=0 forces the lane groups, 1 the block-parallel choice,
+  // 256 / 512 a build.
   const char *pe = getenv("STROM_DECOMP_PAR");
+  const int pv = pe ? atoi(pe) : -1;
   const bool lz4 = codec != STROM_CODEC_SNAPPY && codec != STROM_CODEC_COPY;
-  if (lz4 && (pe ? atoi(pe) != 0 : nblocks <= 8192))
+  if (lz4 && (pe ? pv != 0 : nblocks <= 8192)) {
+    if (pv == 512 || (pv != 256 && nblocks <= 2 * device_cus()))
+      return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+  }
   return strom_decompress_lanes(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
 }
 

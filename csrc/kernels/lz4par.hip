@@ -42,9 +42,21 @@
 
 #define HD __host__ __device__ inline
 
-namespace lz4p {
+// lz4par_nt512.hip builds this file again with 512 threads per stream under
+// its own namespace and entry point (LZ4P_NS / LZ4PAR_ENTRY, no host copy)
+#ifndef LZ4P_NS
+#define LZ4P_NS lz4p
+#endif
+#ifndef LZ4PAR_ENTRY
+#define LZ4PAR_ENTRY strom_decompress_par
+#endif
 
-constexpr uint32_t NT = 256;             // threads per stream (4 waves)
+namespace LZ4P_NS {
+
+#ifndef LZ4PAR_NT
+#define LZ4PAR_NT 256
+#endif
+constexpr uint32_t NT = LZ4PAR_NT;       // threads per stream (4 waves)
 #ifndef LZ4PAR_PW
 #define LZ4PAR_PW 16384
 #endif
@@ -615,7 +627,7 @@ HD void st_window(Smem &s, const Ctx &c, uint32_t ws) {
   s.wload = ws + ld <= c.len ? ld : c.len - ws;
 }
 
-}  // namespace lz4p
+}  // namespace LZ4P_NS
 
 // ---------------------------------------------------------------- device
 // -DSTROM_DECOMP_PROF (libstrom_decprof.so): thread 0 of every workgroup
@@ -646,7 +658,7 @@ __device__ unsigned long long g_lz4par_prof[kLpN];
 #endif
 
 namespace {
-using namespace lz4p;
+using namespace LZ4P_NS;
 
 __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__restrict__ src,
                                                     uint8_t *__restrict__ dst,
@@ -762,9 +774,9 @@ __global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__
 
 // Few long LZ4 streams (raw blocks, frames, Arrow IPC buffers): one
 // workgroup per stream, parallel parse + pointer-doubling resolve.
-extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
-                                    const strom_decomp_desc *d_desc, uint32_t nstreams,
-                                    int32_t *d_status, void *stream) {
+extern "C" int LZ4PAR_ENTRY(int codec, const void *d_src, void *d_dst,
+                            const strom_decomp_desc *d_desc, uint32_t nstreams,
+                            int32_t *d_status, void *stream) {
   if (codec != STROM_CODEC_LZ4 && codec != STROM_CODEC_LZ4_FRAME &&
       codec != STROM_CODEC_LZ4_FRAME_BCS && codec != STROM_CODEC_ARROW_LZ4)
     return -22;
@@ -775,6 +787,7 @@ extern "C" int strom_decompress_par(int codec, const void *d_src, void *d_dst,
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+#ifndef LZ4PAR_NO_HOST
 #ifdef STROM_DECOMP_PROF
 // phase cycle sums of thread 0 of every workgroup (and event counts), zeroed
 extern "C" int strom_lz4par_prof(uint64_t *out) {
@@ -793,8 +806,8 @@ extern "C" int strom_lz4par_prof(uint64_t *out) {
 // bytes or a negative error as the kernel's status.
 extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
                                  uint32_t cap, uint32_t *stats) {
-  using namespace lz4p;
-  static_assert(PW != 16384 || OB != 4096 || HR != 0 || sizeof(Smem) <= 40 * 1024,
+  using namespace LZ4P_NS;
+  static_assert(NT != 256 || PW != 16384 || OB != 4096 || HR != 0 || sizeof(Smem) <= 40 * 1024,
                 "default geometry: four workgroups per CU (160 KiB LDS)");
   Smem *sp = new Smem;
   Smem &s = *sp;
@@ -874,3 +887,4 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
   delete[] fpos;
   return r;
 }
+#endif  // LZ4PAR_NO_HOST

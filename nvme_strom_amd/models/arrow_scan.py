@@ -121,7 +121,12 @@ class ArrowScan:
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
     # to fill the GPU, so compressed groups grow to hold that many buffers
     TARGET_STREAMS = 8192
-    MIN_STREAMS = 256              # per group when cutting a column for overlap
+    # streams per group: one round of the block-parallel decoder's
+    # resident workgroups (256-thread build: 4 per CU).  Same-box A/B of 2 /
+    # 4 per CU and the nslots cut (0) on config 5 was inside the storage
+    # noise (profiles/r3/arrow_group_policy_ab/); 4 keeps a two-column
+    # qualifier list at 8 groups instead of 16
+    ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "4"))
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -175,6 +180,12 @@ class ArrowScan:
                 for do, dl, nd, cap, vo, vl, vn, vcap, hv, cp in cols]))
         return out, dtypes, int(base[-1])
 
+    def _round_streams(self) -> int:
+        cus = 256
+        if self.device.type == "cuda":
+            cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return self.ROUND_STREAMS_PER_CU * cus
+
     def _chunks(self, b: _Batch) -> np.ndarray:
         c = self.chunk_sz
         parts = []
@@ -200,9 +211,16 @@ class ArrowScan:
             avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
             total = sum(d.length + (v.length if v else 0) for d, v in comp)
             want = avg * self.TARGET_STREAMS
-            if len(comp) >= self.nslots * self.MIN_STREAMS:
-                want = min(want, total / self.nslots)
-            slot = int(min(self.max_slot_bytes, max(slot, want)))
+            # groups of at most one resident round of streams: the decode of
+            # a group takes one stream's latency, and the last group's
+            # decode (the part no read overlaps) is as short as it gets
+            rnd = self._round_streams()
+            if rnd and len(comp) > rnd:
+                slot = int(min(self.max_slot_bytes, want, total / -(-len(comp) // rnd) * 1.02))
+            else:
+                if not rnd and len(comp) >= self.nslots * 256:
+                    want = min(want, total / self.nslots)     # one group per slot
+                slot = int(min(self.max_slot_bytes, max(slot, want)))
         limit = max(1, slot // self.chunk_sz)
         # chunk ranges of every batch at once (vectorised: the qualifier-list
         # plans touch several buffers per batch)

@@ -94,7 +94,8 @@ def main(argv=None) -> int:
     import ctypes as C
     import os
     decoders = ([("lanes", lib().strom_decompress_lanes)] if a.lanes else []) + \
-        [("par", lib().strom_decompress_par)]
+        [("par", lib().strom_decompress_par), ("par512", lib().strom_decompress_par512),
+         ("auto", lib().strom_decompress)]
     for v in [x for x in a.variants.split(",") if x]:
         so = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib", "lz4v",
                                  v + ".so"))

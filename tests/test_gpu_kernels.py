@@ -130,19 +130,20 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, "par"])
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, "par256", "par512"])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant of the lane-group decoder
     (STROM_DECOMP_G, the block-parallel decoder switched off) decodes the
     same payloads: the fast LZ4 step's pass width differs per geometry (a
     length-15 match nibble must still take the extended-length path);
-    3 / 2 / 6 = the large-ring few-stream geometries; "par" = the
-    block-parallel decoder (lz4par.hip, LZ4 only)."""
+    3 / 2 / 6 = the large-ring few-stream geometries; "par256" / "par512" =
+    the block-parallel decoder's two builds (lz4par.hip, lz4par_nt512.hip;
+    LZ4 only)."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
-    if g == "par":
-        monkeypatch.setenv("STROM_DECOMP_PAR", "1")
+    if str(g).startswith("par"):
+        monkeypatch.setenv("STROM_DECOMP_PAR", g[3:])
     else:
         monkeypatch.setenv("STROM_DECOMP_PAR", "0")
         monkeypatch.setenv("STROM_DECOMP_G", str(g))
@@ -169,14 +170,14 @@ def test_snappy(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["auto", "lanes", "par"])
+@pytest.mark.parametrize("g", ["auto", "lanes", "256", "512"])
 def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     """pyarrow's 'lz4' codec = LZ4 frame with linked 64 KiB blocks: matches
     may reach into the previous block (lane groups: the LDS history ring;
     block-parallel: stored output read back)."""
     pa = pytest.importorskip("pyarrow")
     if g != "auto":
-        monkeypatch.setenv("STROM_DECOMP_PAR", "1" if g == "par" else "0")
+        monkeypatch.setenv("STROM_DECOMP_PAR", "0" if g == "lanes" else g)
     from nvme_strom_amd.ops import decompress as D
     pays = [p for p in _payloads() if p]
     frames = [pa.compress(p, codec="lz4", asbytes=True) for p in pays]
@@ -188,10 +189,10 @@ def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["lanes", "par"])
+@pytest.mark.parametrize("g", ["0", "256", "512"])
 def test_malformed_streams_report_errors(dev, monkeypatch, g):
     from nvme_strom_amd.ops import decompress as D
-    monkeypatch.setenv("STROM_DECOMP_PAR", "1" if g == "par" else "0")
+    monkeypatch.setenv("STROM_DECOMP_PAR", g)
     rng = np.random.default_rng(5)
     junk = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (10, 1000, 5000)]
     good = D.lz4_compress(b"hello world " * 1000)
