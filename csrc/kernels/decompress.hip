@@ -878,16 +878,16 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // 8,192 val 116/66, ids 106/83, text 56/78).  From 16k streams the lane
   // groups win on near-match data (ids 194/108, text 170/57; val, a quarter
   // of its matches past 2 KiB, stays 118/52).  Streams that fit in one
-  // round of the 512-thread build's resident workgroups (2 per CU) take it:
-  // shorter per-stream chains (lz4par_nt512.hip; 512 config-5 frames 61 ->
-  // 85 GB/s, 640 frames 73 -> 56: profiles/r3/dec/lz4par_nt_crossover.json).
+  // round of the 512-thread build's resident workgroups (3 per CU) take it:
+  // shorter per-stream chains (lz4par_nt512.hip; config-5 frames 512: 61 ->
+  // 85 GB/s, 768: 86 -> 115; profiles/r3/dec/lz4par_nt_occupancy_ab.json).
   // STROM_DECOMP_PAR=0 forces the lane groups, 1 the block-parallel choice,
   // 256 / 512 a build.
   const char *pe = getenv("STROM_DECOMP_PAR");
   const int pv = pe ? atoi(pe) : -1;
   const bool lz4 = codec != STROM_CODEC_SNAPPY && codec != STROM_CODEC_COPY;
   if (lz4 && (pe ? pv != 0 : nblocks <= 8192)) {
-    if (pv == 512 || (pv != 256 && nblocks <= 2 * device_cus()))
+    if (pv == 512 || (pv != 256 && nblocks <= 3 * device_cus()))
       return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   }

@@ -211,10 +211,13 @@ HD uint32_t slice_hi(const Smem &s, uint32_t t) {
 
 // ---------------------------------------------------------------- phases
 // window load: input bytes [ws, ws + wload) into LDS
+#ifndef LZ4PAR_LOADU
+#define LZ4PAR_LOADU 16
+#endif
 HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
   // all loads of a thread issued before the first LDS store (16 at a time):
   // a plain loop waited for each load in turn
-  constexpr uint32_t U = 16;
+  constexpr uint32_t U = LZ4PAR_LOADU;
   for (uint32_t j0 = 0; j0 * NT < s.wload; j0 += U) {
     uint8_t r[U];
 #pragma unroll
@@ -660,7 +663,12 @@ __device__ unsigned long long g_lz4par_prof[kLpN];
 namespace {
 using namespace LZ4P_NS;
 
-__global__ __launch_bounds__(NT) void lz4par_kernel(int codec, const uint8_t *__restrict__ src,
+#ifdef LZ4PAR_WPE
+#define LZ4PAR_OCC __attribute__((amdgpu_waves_per_eu(LZ4PAR_WPE)))
+#else
+#define LZ4PAR_OCC
+#endif
+__global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel(int codec, const uint8_t *__restrict__ src,
                                                     uint8_t *__restrict__ dst,
                                                     const strom_decomp_desc *__restrict__ desc,
                                                     uint32_t nstreams, int32_t *status) {

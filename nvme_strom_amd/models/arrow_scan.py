@@ -121,12 +121,14 @@ class ArrowScan:
     # per-stream rate (profiles/r2/dec): a launch needs thousands of streams
     # to fill the GPU, so compressed groups grow to hold that many buffers
     TARGET_STREAMS = 8192
-    # streams per group: one round of the block-parallel decoder's
-    # resident workgroups (256-thread build: 4 per CU).  Same-box A/B of 2 /
-    # 4 per CU and the nslots cut (0) on config 5 was inside the storage
-    # noise (profiles/r3/arrow_group_policy_ab/); 4 keeps a two-column
-    # qualifier list at 8 groups instead of 16
-    ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "4"))
+    # streams per group: one round of the block-parallel decoder's resident
+    # workgroups (its 512-thread build: 3 per CU, 768 config-5 frames at
+    # 115 GB/s), so a group's decode takes one stream's latency and the last
+    # group's decode — the part no read overlaps — stays short.  0: cut a
+    # compressed column into nslots groups instead.  (Same-box A/B of 2 / 4
+    # per CU and 0 on config 5 was inside the storage noise:
+    # profiles/r3/arrow_group_policy_ab/.)
+    ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
