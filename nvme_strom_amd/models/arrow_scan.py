@@ -143,8 +143,9 @@ class ArrowScan:
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
         self._wbs: List[Optional[torch.Tensor]] = []
-        # column tuple -> (dtypes, rows, groups)
+        # (column tuple, batch range) -> (dtypes, rows, groups)
         self._plans: Dict[tuple, tuple] = {}
+        self._bplans: Dict[tuple, tuple] = {}   # column tuple -> _plan()
 
     # ------------------------------------------------------------- plan
     def _plan(self, names: Sequence[str]) -> tuple:
@@ -426,13 +427,16 @@ class ArrowScan:
         state["column_bytes"] += g.column_bytes
 
     def scan_where(self, quals: Sequence[Tuple[str, object, object]],
-                   project: Optional[str] = None) -> ScanOut:
+                   project: Optional[str] = None,
+                   batches: Optional[Tuple[int, int]] = None) -> ScanOut:
         """Row ids (int64, file order) where every ``lo <= column <= hi`` of
         ``quals`` holds (nulls never qualify) — a PG-Strom qualifier list.
         Each referenced column is read from storage and decoded once per
         group; the per-column bitmaps are ANDed on the device.  ``project``
         names a column whose values (and validity, when it has nulls) are
-        gathered for the selected rows while their ids are written."""
+        gathered for the selected rows while their ids are written.
+        ``batches=(b0, b1)`` scans only record batches [b0, b1) (row ids stay
+        file-global: parallel/scan.py splits a file over ranks this way)."""
         if not quals:
             raise ValueError("at least one qualifier")
         t0 = time.perf_counter()
@@ -440,10 +444,15 @@ class ArrowScan:
         for n in [q[0] for q in quals] + ([project] if project else []):
             if n not in names:
                 names.append(n)
-        key = tuple(names)
+        nb = self.meta.nbatches
+        rng = (0, nb) if batches is None else (max(0, int(batches[0])), min(nb, int(batches[1])))
+        key = (tuple(names), rng)
         if key not in self._plans:                # the file's layout is fixed once opened
-            batches, dtypes, nrows = self._plan(names)
-            self._plans[key] = (dtypes, nrows, self._groups(batches))
+            if tuple(names) not in self._bplans:
+                self._bplans[tuple(names)] = self._plan(names)
+            allb, dtypes, _ = self._bplans[tuple(names)]
+            sel = allb[rng[0]:rng[1]] if rng[0] < rng[1] else []
+            self._plans[key] = (dtypes, sum(b.rows for b in sel), self._groups(sel))
         dtypes, nrows, groups = self._plans[key]
         spec = [(names.index(n), dtypes[names.index(n)], lo, hi) for n, lo, hi in quals]
         t_plan = time.perf_counter()
