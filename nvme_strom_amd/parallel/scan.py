@@ -21,9 +21,18 @@ its own engine, so the file is cut up front instead:
 Every rank returns the same result (``gather="all"``) or only its own part
 (``gather="none"``: a consumer that keeps the data sharded, e.g. the next
 operator of a distributed query).
+
+``DistributedHeapScan`` does the same for a PostgreSQL relation, the way
+the reference's parallel workers do it but with a GPU per process: every
+rank's ``HeapRelationScan`` claims chunks from ONE cross-process block
+cursor in shared memory (``SharedCursor``, the reference's DSM
+``nsp_cblock``), so faster ranks take more chunks (dynamic balancing
+instead of a static cut), and the item pointers are combined by the same
+padded all-gather, then put in block order.
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -33,6 +42,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.arrow_scan import ArrowScan
+from ..models import pg_scan
 
 
 def partition(weights: np.ndarray, parts: int) -> List[Tuple[int, int]]:
@@ -157,6 +167,98 @@ class DistributedArrowScan:
         res.seconds = {"scan_s": t_scan - t0, "combine_s": t_end - t_scan,
                        "total_s": t_end - t0, **{f"local_{k}": v for k, v in out.seconds.items()}}
         return res
+
+    def close(self) -> None:
+        self.scan.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class _Combiner:
+    """Padded variable-length all-gather over a group (device tensors with
+    nccl, staged through host memory with gloo)."""
+
+    def __init__(self, device: torch.device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        backend = dist.get_backend(group) if self.world > 1 else None
+        self.cdev = device if (device.type == "cuda" and backend != "gloo") else torch.device("cpu")
+
+    def gather(self, t: torch.Tensor) -> Tuple[torch.Tensor, List[int]]:
+        if self.world == 1:
+            return t, [t.numel()]
+        n = torch.tensor([t.numel()], dtype=torch.int64, device=self.cdev)
+        ns = torch.empty(self.world, dtype=torch.int64, device=self.cdev)
+        dist.all_gather_into_tensor(ns, n, group=self.group)
+        counts = [int(x) for x in ns.tolist()]
+        mx = max(counts)
+        if mx == 0:
+            return t[:0], counts
+        pad = torch.zeros(mx, dtype=t.dtype, device=self.cdev)
+        pad[:t.numel()] = t.to(self.cdev)
+        out = torch.empty(self.world * mx, dtype=t.dtype, device=self.cdev)
+        dist.all_gather_into_tensor(out, pad, group=self.group)
+        out = out.view(self.world, mx)
+        return torch.cat([out[r, :c] for r, c in enumerate(counts)]), counts
+
+
+class DistributedHeapScan:
+    """``HeapRelationScan`` over the ranks of ``group``, one GPU per rank,
+    sharing one block cursor (see module docstring).  ``run()`` is
+    collective; every rank returns the full, block-ordered result."""
+
+    def __init__(self, rel: "pg_scan.Relation", cfg: Optional["pg_scan.ScanConfig"] = None,
+                 device=None, group=None, **pred):
+        self.rel = rel
+        self.group = group
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.scan = pg_scan.HeapRelationScan(rel, cfg, self.device, **pred)
+        self.comb = _Combiner(self.device, group)
+
+    def _cursor(self, b0: int, b1: int):
+        """Rank 0 creates the shared cursor, the others attach by name."""
+        name = [None]
+        if self.comb.rank == 0:
+            name[0] = f"dist-{os.getpid()}-{time.monotonic_ns()}"
+            cur = pg_scan.SharedCursor(name[0], nblocks=b1, start=b0, create=True)
+        if self.comb.world > 1:
+            dist.broadcast_object_list(name, src=0, group=self.group)
+            if self.comb.rank != 0:
+                cur = pg_scan.SharedCursor(name[0])
+        return cur
+
+    def run(self, workers: int = 1, blocks: Optional[Tuple[int, int]] = None) -> dict:
+        b0, b1 = pg_scan._block_range(blocks, self.rel.nblocks)
+        t0 = time.perf_counter()
+        cur = self._cursor(b0, b1)
+        try:
+            r = self.scan.run(workers, cursor=cur)
+            cur.add(r)
+            t_scan = time.perf_counter()
+            mine = torch.from_numpy(r.items.astype(np.int64))
+            allv, counts = self.comb.gather(mine)
+            items = np.sort(allv.cpu().numpy().astype(np.uint64))
+            if self.comb.world > 1:
+                dist.barrier(group=self.group)   # every rank has added its counters
+            totals = cur.counters()
+        finally:
+            cur.close(unlink=False)
+        if self.comb.world > 1:
+            dist.barrier(group=self.group)       # everyone detached
+        if self.comb.rank == 0:
+            try:
+                os.unlink(cur.path)
+            except FileNotFoundError:
+                pass
+        t_end = time.perf_counter()
+        return dict(items=items, per_rank_items=counts, pages=int(r.pages), totals=totals,
+                    seconds={"scan_s": t_scan - t0, "combine_s": t_end - t_scan,
+                             "total_s": t_end - t0})
 
     def close(self) -> None:
         self.scan.close()

@@ -30,6 +30,10 @@ def main(argv=None) -> int:
     ap.add_argument("--dir", default="/tmp/strom_arrow")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--backend", default="")
+    ap.add_argument("--kind", default="arrow", choices=("arrow", "pg"),
+                    help="pg: a PostgreSQL relation scanned by DistributedHeapScan (ranks "
+                         "share one block cursor)")
+    ap.add_argument("--pg-mib", type=int, default=512)
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -54,6 +58,8 @@ def main(argv=None) -> int:
         else:
             dist.init_process_group(backend)
     os.makedirs(a.dir, exist_ok=True)
+    if a.kind == "pg":
+        return _pg(a, rank, world, dev, backend)
     path = os.path.join(a.dir, f"t_{a.rows}_{a.batch_rows}.arrow")
     if rank == 0:
         make_file(path, a.rows, a.batch_rows)
@@ -119,6 +125,73 @@ def main(argv=None) -> int:
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0 if (rank != 0 or ok) else 3
+
+
+def _pg(a, rank: int, world: int, dev, backend: str) -> int:
+    """DistributedHeapScan of a synthetic relation; rank 0 verifies."""
+    import time
+
+    import torch.distributed as dist
+
+    import nvme_strom_amd as S
+    from nvme_strom_amd.models import pg_scan
+    from nvme_strom_amd.parallel.scan import DistributedHeapScan
+    from nvme_strom_amd.utils import pgpage
+    path = os.path.join(a.dir, "16400")
+    tmpl_pages = 2048
+    reps = max(1, (a.pg_mib << 20) // (tmpl_pages * 8192))
+    if rank == 0:
+        rng = np.random.default_rng(0)
+        vals = rng.integers(-5000, 5000, tmpl_pages * 150).astype(np.int64)
+        tmpl = pgpage.build_table(vals, per_page=150, width=8, with_checksum=False,
+                                  invisible_every=9)
+        pg_scan.Relation.write(path, tmpl * reps)
+    if world > 1:
+        dist.barrier()
+    rel = pg_scan.Relation(path)
+    cfg = pg_scan.ScanConfig(verify_checksum=False, chunk_size=32 << 20, buffer_size=256 << 20)
+    pred = dict(attr_off=0, attr_width=8, lo=-100, hi=2500)
+    ds = DistributedHeapScan(rel, cfg, dev, **pred)
+    times = []
+    for r in range(a.reps + 1):
+        for seg in rel.segments:
+            fd = os.open(seg, os.O_RDONLY)
+            S.evict_file(fd)
+            os.close(fd)
+        if world > 1:
+            dist.barrier()
+        out = ds.run(2)
+        times.append(out["seconds"]["total_s"])
+    ds.close()
+    ok = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        one = pg_scan.Relation.write(os.path.join(a.dir, "16401"), tmpl)
+        ref = pg_scan.cpu_scan(one, cfg, **pred).items
+        blk = (out["items"] >> np.uint64(16)).astype(np.int64)
+        first = out["items"][blk < tmpl_pages]
+        ok = bool(len(out["items"]) == len(ref) * reps and np.array_equal(first, ref))
+        for sp in one.segments:
+            os.unlink(sp)
+        res = dict(kind="pg", world=world, backend=backend if world > 1 else None,
+                   relation_bytes=rel.nblocks * 8192, items=int(len(out["items"])),
+                   per_rank_items=out["per_rank_items"], pages_total=out["totals"]["pages"],
+                   warm_median_ms=round(float(np.median(times[1:])) * 1e3, 2),
+                   first_run_ms=round(times[0] * 1e3, 2),
+                   GBps=round(rel.nblocks * 8192 / float(np.median(times[1:])) / 1e9, 2),
+                   verified=ok, verify_s=round(time.perf_counter() - t0, 2))
+        js = json.dumps(res)
+        if a.out:
+            with open(a.out, "w") as f:
+                f.write(js)
+        print(js, flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        for sp in rel.segments:
+            os.unlink(sp)
     return 0 if (rank != 0 or ok) else 3
 
 

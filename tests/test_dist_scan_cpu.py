@@ -1,5 +1,6 @@
-"""Multi-rank Arrow scan (parallel/scan.py) on CPU: the batch partition,
-and the combine step over gloo with 3 ranks.
+"""Multi-rank scans (parallel/scan.py) on CPU over gloo with 3 ranks: the
+Arrow batch partition and combine step, and the PostgreSQL heap scan whose
+ranks share one cross-process block cursor.
 
 The GPU scan itself runs in tests/test_gpu_models.py; here each rank's
 ArrowScan is replaced by a numpy scan of the same record-batch range of a
@@ -151,3 +152,78 @@ def test_distributed_scan_combine_3_ranks(tmp_path):
         mine_all.append(d["mine"])
         assert np.array_equal(d["mine_vals"], d["mine"])         # id projected = row id
     assert np.array_equal(np.concatenate(mine_all), np.arange(len(ids)))   # sharded: file order
+
+
+class _CpuHeapScan:
+    """Stand-in for HeapRelationScan on CPU: claims chunks from the given
+    cursor like the GPU participants and scans each with cpu_scan."""
+
+    def __init__(self, rel, cfg, device, **pred):
+        self.rel, self.cfg, self.pred = rel, cfg, pred
+
+    def run(self, workers=1, blocks=None, cursor=None):
+        from nvme_strom_amd.models import pg_scan
+        parts, pages = [], 0
+        while True:
+            lo, n = cursor.claim(3, boundary=self.rel.relseg_size)
+            if n == 0:
+                break
+            r = pg_scan.cpu_scan(self.rel, self.cfg, blocks=(lo, lo + n), **self.pred)
+            parts.append(r.items)
+            pages += r.pages
+        items = np.concatenate(parts) if parts else np.zeros(0, np.uint64)
+        return pg_scan.ScanResult(items, pages=pages)
+
+    def close(self):
+        pass
+
+
+def _heap_worker(rank, world, port, path, q):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch
+        import torch.distributed as dist
+        from nvme_strom_amd.models import pg_scan
+        import nvme_strom_amd.parallel.scan as PS
+        PS.pg_scan.HeapRelationScan = _CpuHeapScan
+        dist.init_process_group("gloo")
+        rel = pg_scan.Relation(path, relseg_size=8)
+        cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192)
+        ds = PS.DistributedHeapScan(rel, cfg, torch.device("cpu"), attr_off=0, attr_width=8,
+                                    lo=50, hi=1749)
+        out = ds.run(1)
+        q.put((rank, dict(items=out["items"], counts=out["per_rank_items"],
+                          pages=out["totals"]["pages"])))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def test_distributed_heap_scan_shared_cursor_3_ranks(tmp_path):
+    from nvme_strom_amd.models import pg_scan
+    from nvme_strom_amd.utils import pgpage
+    vals = np.arange(4000, dtype=np.int64)
+    data = pgpage.build_table(vals, per_page=100, width=8, invisible_every=10)   # 40 pages
+    rel = pg_scan.Relation.write(str(tmp_path / "16390"), data, relseg_size=8)
+    cfg = pg_scan.ScanConfig(chunk_size=4 * 8192, buffer_size=8 * 8192)
+    full = pg_scan.cpu_scan(rel, cfg, attr_off=0, attr_width=8, lo=50, hi=1749)
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_heap_worker, args=(r, world, port, rel.path, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert isinstance(res[r], dict), res[r]
+        assert np.array_equal(res[r]["items"], full.items), r     # block order, exactly once
+        assert sum(res[r]["counts"]) == len(full.items)
+        assert res[r]["pages"] == rel.nblocks                    # shared counters: all pages
+    assert not any(f.startswith("nvme-strom-scan.dist-") for f in os.listdir("/dev/shm"))

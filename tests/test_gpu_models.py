@@ -134,6 +134,26 @@ def test_distributed_scan_two_ranks_one_gpu(tmp_path):
     assert all(b > 0 for b in out["bytes_read_per_rank"])
 
 
+def test_distributed_heap_scan_two_ranks_one_gpu(tmp_path):
+    """DistributedHeapScan on the GPU: 2 ranks (gloo, one GPU) claim chunks
+    of one relation from a shared cursor; rank 0 checks the combined item
+    pointers against the CPU executor."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29549", "-m",
+           "nvme_strom_amd.tools.dist_scan_bench", "--kind", "pg", "--pg-mib", "64",
+           "--dir", str(tmp_path), "--reps", "1", "--backend", "gloo"]
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-4000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["world"] == 2 and out["verified"] is True
+    assert sum(out["per_rank_items"]) == out["items"] > 0
+    assert out["pages_total"] == out["relation_bytes"] // 8192
+
+
 def test_sharded_loader_single_rank(S, tmp_path):
     from nvme_strom_amd.parallel import ShardedLoader
     data = np.random.default_rng(1).integers(0, 256, 16 << 20, dtype=np.uint8)
