@@ -240,9 +240,14 @@ class DistributedHeapScan:
             r = self.scan.run(workers, cursor=cur)
             cur.add(r)
             t_scan = time.perf_counter()
-            mine = torch.from_numpy(r.items.astype(np.int64))
-            allv, counts = self.comb.gather(mine)
-            items = np.sort(allv.cpu().numpy().astype(np.uint64))
+            if self.comb.world == 1:
+                items, counts = r.items, [len(r.items)]
+            else:
+                mine = torch.from_numpy(r.items.view(np.int64))
+                allv, counts = self.comb.gather(mine)
+                # every rank's part is in block order, interleaved chunk by
+                # chunk with the others': one radix sort puts them together
+                items = np.sort(allv.cpu().numpy().view(np.uint64), kind="stable")
             if self.comb.world > 1:
                 dist.barrier(group=self.group)   # every rank has added its counters
             totals = cur.counters()
