@@ -19,7 +19,7 @@ ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
-all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so
+all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so
 
 tools: $(TOOLS)
 
@@ -57,7 +57,7 @@ $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
-	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(TOOLS)
+	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so $(TOOLS)
 
 .PHONY: all tools clean ab
 
@@ -82,6 +82,12 @@ build/selftest-asan: $(SELFTEST_SRC) csrc/engine/engine.h
 build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
 	@mkdir -p build
 	$(ROCM)/llvm/bin/clang++ $(SELFTEST_FLAGS) -fsanitize=thread -o $@ $(SELFTEST_SRC) $(SELFTEST_LIBS)
+
+# the 512-thread build of the block-parallel decoder WITH its host copy:
+# the CPU tests run its phases thread by thread (tests/test_codecs_cpu.py)
+$(OUT)/libstrom_lz4par512_host.so: csrc/kernels/lz4par.hip csrc/include/strom/strom.h
+	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_NT=512 -DLZ4PAR_LOADU=8 -DLZ4P_NS=lz4p512 \
+	  -DLZ4PAR_ENTRY=strom_decompress_par512 -shared -o $@ $<
 
 # lz4par geometry variants for A/B timing (tools/lz4par_bench.py --variants):
 # make lz4v LZ4V="name:-DX=1,-DY=2 ..." -> $(OUT)/lz4v/<name>.so (lz4par.hip

@@ -129,29 +129,32 @@ def _ints(kind, n, seed=0):
     return rng.random(n // 8).tobytes()
 
 
+@pytest.mark.parametrize("threads", [256, 512])
 @pytest.mark.parametrize("kind", ["random", "text", "runs", "zeros", "uniform", "sorted", "floats"])
 @pytest.mark.parametrize("n", [1, 13, 100, 4096, 70000, 300000])
-def test_lz4par_raw_block_matches_host(kind, n):
+def test_lz4par_raw_block_matches_host(kind, n, threads):
     """Speculative parallel parse + pointer doubling (the GPU kernel's own
-    phases, run thread by thread on the CPU) == the serial host decoder."""
+    phases, run thread by thread on the CPU, in both builds' geometry) ==
+    the serial host decoder."""
     d = (_data(kind, n) if kind in ("random", "text", "runs", "zeros") else _ints(kind, n))[:n]
     c = D.lz4_compress(d)
-    st, out, stats = D.lz4par_host(D.LZ4, c, len(d))
+    st, out, stats = D.lz4par_host(D.LZ4, c, len(d), threads)
     assert st == len(d) and out == d, (st, stats)
 
 
+@pytest.mark.parametrize("threads", [256, 512])
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "text", "random"])
-def test_lz4par_arrow_frames_from_pyarrow(kind):
+def test_lz4par_arrow_frames_from_pyarrow(kind, threads):
     """pyarrow's LZ4 frames (linked 64 KiB blocks: matches reach into the
     previous block) as Arrow IPC buffers, and a stored (-1) buffer."""
     pa = pytest.importorskip("pyarrow")
     d = _ints(kind, 512 << 10, 3) if kind in ("uniform", "sorted") else _data(kind, 512 << 10, 3)
     frame = pa.compress(d, codec="lz4", asbytes=True)
     buf = D.arrow_lz4_buffer(d, frame)
-    st, out, stats = D.lz4par_host(D.ARROW_LZ4, buf, len(d))
+    st, out, stats = D.lz4par_host(D.ARROW_LZ4, buf, len(d), threads)
     assert st == len(d) and out == d, (st, stats)
     raw = b"\xff" * 8 + d[:5000]
-    st, out, _ = D.lz4par_host(D.ARROW_LZ4, raw, 5000)
+    st, out, _ = D.lz4par_host(D.ARROW_LZ4, raw, 5000, threads)
     assert st == 5000 and out == d[:5000]
 
 
