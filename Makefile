@@ -104,6 +104,14 @@ build/arrow_meta_fuzz: csrc/tests/arrow_meta_fuzz.cc csrc/engine/arrow_meta.cc
 	@mkdir -p build
 	$(CXX) -std=c++17 -O1 -g -fsanitize=address,undefined -fno-sanitize-recover=all -o $@ $^ -lpthread
 
+# the zstd decoder's host copy, host-only with ASan + UBSan (mutation test)
+build/zstd_fuzz: csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip csrc/include/strom/strom.h
+	@mkdir -p build
+	$(HIPCC) -std=c++17 -O1 -g -Icsrc/include --offload-arch=$(ARCH) \
+	  -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	  -Xarch_host -fno-sanitize-recover=all -fno-omit-frame-pointer \
+	  -o $@ csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip
+
 selftest: build/selftest build/selftest-asan build/selftest-tsan
 	STROM_STAT_SHM=0 ./build/selftest && STROM_STAT_SHM=0 ./build/selftest-asan && STROM_STAT_SHM=0 TSAN_OPTIONS=report_signal_unsafe=0 ./build/selftest-tsan
 

@@ -243,10 +243,22 @@ struct strom_decomp_desc {
 #define STROM_CODEC_LZ4_FRAME     4  /* LZ4 frame data blocks (after header) */
 #define STROM_CODEC_LZ4_FRAME_BCS 5  /*   ... with 4-byte block checksums */
 #define STROM_CODEC_ARROW_LZ4     6  /* Arrow IPC buffer: i64 length (-1 = raw) + LZ4 frame */
+#define STROM_CODEC_ZSTD          7  /* Zstandard frame(s) (RFC 8878) */
+#define STROM_CODEC_ARROW_ZSTD    8  /* Arrow IPC buffer: i64 length (-1 = raw) + zstd frame */
 /* status[i] = decoded bytes, or -1 malformed / -2 overflow / -3 distance */
 int strom_decompress(int codec, const void *d_src, void *d_dst,
                      const struct strom_decomp_desc *d_desc, uint32_t nblocks,
                      int32_t *d_status, void *stream);
+
+/* Zstandard streams, one wavefront each (csrc/kernels/zstd.hip).  scratch:
+ * 128 KiB of decoded literals per resident workgroup (NULL: a per-stream
+ * buffer kept by the library).  strom_decompress() routes codecs 7/8 here. */
+int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
+                          const struct strom_decomp_desc *d_desc, uint32_t nstreams,
+                          int32_t *d_status, void *scratch, uint64_t scratch_bytes,
+                          void *stream);
+/* the same decode on the CPU (the kernel's phases lane by lane) */
+int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, uint32_t cap);
 
 /* Columnar filter: bitmap[i/64] bit i%64 = valid(i) && lo <= v[i] <= hi. */
 #define STROM_COL_I32 1

@@ -869,6 +869,9 @@ static uint32_t device_cus() {
 extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
                                 const strom_decomp_desc *d_desc, uint32_t nblocks,
                                 int32_t *d_status, void *stream) {
+  if (codec == STROM_CODEC_ZSTD || codec == STROM_CODEC_ARROW_ZSTD)
+    return strom_decompress_zstd(codec, d_src, d_dst, d_desc, nblocks, d_status, nullptr, 0,
+                                 stream);
   if (codec < STROM_CODEC_LZ4 || codec > STROM_CODEC_ARROW_LZ4) return -22;
   if (!nblocks) return 0;
   // Up to 8,192 LZ4 streams: the block-parallel decoder (lz4par.hip) — a

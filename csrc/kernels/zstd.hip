@@ -1,0 +1,1177 @@
+// zstd.hip — Zstandard (RFC 8878) decode on CDNA4, for Arrow IPC buffers
+// compressed with ZSTD (BodyCompression codec 1: i64 length prefix + one
+// zstd frame per buffer — the other Arrow IPC codec next to LZ4_FRAME,
+// lz4par.hip).  Not in the reference (the columnar decode path
+// is north-star work); it widens BASELINE config 5 to ZSTD-written files.
+//
+// One wavefront (workgroup of 64) per stream, several streams per CU.  A
+// compressed block is entropy-decoded serially and executed in parallel:
+//
+//  1. literals: the Huffman table (FSE-coded or direct weights) is built in
+//     LDS; the 1 or 4 literal bitstreams are decoded by lanes 0..3 at once,
+//     LSYM symbols per stream per round, each stream read from its own LDS
+//     window that the whole wave refills between rounds; decoded literals
+//     go to the stream's scratch slot in HBM.  Raw / RLE literals are read
+//     in place.
+//  2. sequences: LL / OF / ML FSE tables (predefined, RLE, compressed or
+//     repeated) in LDS with the code baselines folded into the entries;
+//     lane 0 decodes up to SEQN sequences of the backward bitstream from an
+//     LDS window (refilled by the wave per chunk), resolves repeat offsets
+//     and keeps running output / literal positions, so no scan is needed.
+//  3. execution, all 64 lanes: the chunk's output is produced in batches of
+//     OB bytes — a source pointer per byte (literal index; stored output
+//     before the batch; or an earlier byte of the batch), pointer doubling
+//     until every pointer is a literal or stored byte (log2 of the longest
+//     in-batch chain), one gather per byte, coalesced byte stores.  Stored
+//     output and scratch literals are read back with L1-bypassing loads
+//     after the workgroup release fence + barrier that ended their writes.
+//
+// The phases are plain functions of (shared state, lane); the kernel runs
+// them with barriers between, strom_zstd_host() runs the SAME functions
+// lane by lane on the CPU (tests/test_codecs_cpu.py pins it against
+// pyarrow's zstd frames at several levels).  Raw / RLE blocks, skippable
+// frames, several frames per stream, the frame content size and the Arrow
+// length prefix are checked; dictionaries are refused (Arrow writes none);
+// the optional content checksum is skipped, not verified.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+
+#include "strom/strom.h"
+
+#define HD __host__ __device__ inline
+
+// host debug builds (-DZS_DEBUG): report the line of the first failed check
+#if defined(ZS_DEBUG) && !defined(__HIP_DEVICE_COMPILE__)
+#include <cstdio>
+#define ZF(v) (fprintf(stderr, "zstd: check failed at line %d\n", __LINE__), (v))
+#else
+#define ZF(v) (v)
+#endif
+
+namespace zs {
+
+constexpr uint32_t NT = 64;              // one wave per stream
+constexpr uint32_t SEQN = 128;           // sequences per decode chunk
+constexpr uint32_t OB = 1024;            // output bytes per resolve batch
+constexpr uint32_t EPT = OB / NT;        // batch entries per lane (strided)
+constexpr uint32_t SWIN = 1536;          // sequence bitstream window: SEQN x <= 89 bits
+constexpr uint32_t LSYM = 256;           // literal symbols per stream per round
+constexpr uint32_t LWIN = 384;           // literal stream window: LSYM x <= 11 bits
+constexpr uint32_t MAXB = 128u << 10;    // Block_Maximum_Size
+constexpr uint32_t SLOT = MAXB;          // literal scratch per resident workgroup
+constexpr uint32_t kLit = 0x80000000u;   // pointer tag: literal index
+constexpr uint32_t kHist = 0x40000000u;  // pointer tag: stored output position
+constexpr uint32_t kTag = kLit | kHist;
+constexpr uint32_t kPosMax = 1u << 30;   // outputs below 1 GiB
+static_assert(SEQN * 89 / 8 + 16 <= SWIN && LSYM * 11 / 8 + 16 <= LWIN, "windows cover a chunk");
+
+enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3, kErrUnsupported = -4 };
+enum : uint32_t { kFrame = 0, kBlock = 1, kDone = 2, kStored = 3 };
+enum : uint32_t { kRaw = 0, kRle = 1, kComp = 2 };
+enum : uint32_t { kLitScratch = 0, kLitInput = 1, kLitRle = 2 };
+enum : uint32_t { kLL = 0, kOF = 1, kML = 2, kPlain = 3 };
+
+// FSE decoding entry with the code's baseline and extra bits folded in
+// (kPlain: base = symbol)
+struct SeqEnt {
+  uint32_t base;
+  uint16_t next;
+  uint8_t nb;
+  uint8_t add;
+};
+
+// backward bitstream: bits [0, nbits) of the stream's little-endian value
+// are still unread and come out top first; cont holds bits [cbase, cbase+64)
+struct BR {
+  uint64_t cont;
+  int32_t nbits;
+  int32_t cbase;
+  uint32_t beg;
+  uint32_t pad;
+};
+
+struct Win {                 // an LDS copy of input bytes [lo, lo + n)
+  const uint8_t *lds;
+  uint32_t lo, n;
+};
+
+struct Ctx {
+  const uint8_t *in;
+  uint8_t *out;
+  uint8_t *lit;              // scratch slot (decoded literals of a block)
+  uint32_t len;              // input bytes
+  uint32_t cap;              // output capacity
+};
+
+struct Smem {
+  SeqEnt tll[512];
+  SeqEnt tml[512];
+  SeqEnt tof[256];
+  uint16_t huf[2048];        // (symbol << 4) | code length, indexed by the next hbits bits
+  uint32_t ptr[OB];          // batch pointers (also the Huffman-weight FSE table)
+  uint32_t ost[SEQN + 2];    // chunk entry i: output start (relative to the chunk)
+  uint32_t lst[SEQN + 1];    //   literal index of its first literal
+  uint32_t sll[SEQN + 1];    //   literal length
+  uint32_t soff[SEQN + 1];   //   match offset
+  uint8_t swin[SWIN];
+  uint8_t lwin[4][LWIN];
+  int16_t norm[64];
+  uint16_t snext[64];
+  uint8_t hw[256];           // Huffman weights
+  uint32_t wrank[16];
+  BR lbr[4];
+  BR sbr;
+  uint32_t lcnt[4], lout[4], lwlo[4];
+  uint32_t swlo;
+  // stream / frame / block scalars (lane 0 writes, all read after a barrier)
+  uint32_t ip, op, fstart, fcs_set, fcs, cksum, state;
+  uint32_t rep[3];
+  int32_t err;
+  uint32_t btype, bsize, bstart, bend, blast;
+  uint32_t lit_kind, lit_base, lit_n, lit_used, lit_rle;
+  uint32_t hbits, nls;
+  uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
+  uint32_t have_ll, have_of, have_ml;
+  uint32_t cn, ctot;
+  int64_t expect;            // Arrow length prefix, or -1
+};
+
+// ------------------------------------------------------------- constants
+// predefined distributions (RFC 8878 3.1.1.3.2.2)
+#ifdef __HIP_DEVICE_COMPILE__
+#define ZTAB __constant__ static const
+#else
+#define ZTAB static const
+#endif
+ZTAB int8_t kNormLL[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                           2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+ZTAB int8_t kNormML[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                           1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                           1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+ZTAB int8_t kNormOF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                           1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+
+// baseline + extra bits of a literal-length / match-length / offset code
+HD void code_base(uint32_t kind, uint32_t c, uint32_t &base, uint32_t &add) {
+  if (kind == kOF) {
+    add = c;
+    base = 1u << c;
+  } else if (kind == kLL) {
+    if (c < 16) {
+      base = c;
+      add = 0;
+    } else if (c >= 25) {
+      add = c - 19;
+      base = 1u << add;
+    } else {
+      // 16..24: 16/1 18/1 20/1 22/1 24/2 28/2 32/3 40/3 48/4
+      const uint32_t i = c - 16;
+      add = i < 4 ? 1 : i < 6 ? 2 : i < 8 ? 3 : 4;
+      base = i < 4 ? 16 + 2 * i : i < 6 ? 24 + 4 * (i - 4) : i < 8 ? 32 + 8 * (i - 6) : 48;
+    }
+  } else if (kind == kML) {
+    if (c < 32) {
+      base = c + 3;
+      add = 0;
+    } else if (c >= 43) {
+      add = c - 36;
+      base = (1u << add) + 3;
+    } else {
+      // 32..42: 35/1 37/1 39/1 41/1 43/2 47/2 51/3 59/3 67/4 83/4 99/5
+      const uint32_t i = c - 32;
+      add = i < 4 ? 1 : i < 6 ? 2 : i < 8 ? 3 : i < 10 ? 4 : 5;
+      base = i < 4 ? 35 + 2 * i : i < 6 ? 43 + 4 * (i - 4) : i < 8 ? 51 + 8 * (i - 6)
+           : i < 10 ? 67 + 16 * (i - 8) : 99;
+    }
+  } else {
+    base = c;
+    add = 0;
+  }
+}
+
+// ------------------------------------------------------------- input
+HD uint32_t gbyte(const Ctx &c, uint32_t p) { return p < c.len ? c.in[p] : 0u; }
+
+HD uint32_t wbyte(const Win &w, const Ctx &c, uint32_t p) {
+  const uint32_t r = p - w.lo;
+  return r < w.n ? w.lds[r] : gbyte(c, p);
+}
+
+HD uint32_t rd16(const Ctx &c, uint32_t p) { return gbyte(c, p) | (gbyte(c, p + 1) << 8); }
+HD uint32_t rd32(const Ctx &c, uint32_t p) { return rd16(c, p) | (rd16(c, p + 2) << 16); }
+
+HD uint32_t hibit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }   // v > 0
+
+HD bool br_init(BR &b, const Ctx &c, uint32_t beg, uint32_t len) {
+  if (len == 0) return ZF(false);
+  const uint32_t last = gbyte(c, beg + len - 1);
+  if (last == 0) return ZF(false);          // no end marker
+  b.beg = beg;
+  b.nbits = (int32_t)(8 * (len - 1) + hibit(last));
+  b.cbase = 0x7fffffff;                 // first read fills
+  b.cont = 0;
+  b.pad = 0;
+  return true;
+}
+
+HD void br_fill(BR &b, const Win &w, const Ctx &c) {
+  const int32_t nb = b.nbits > 0 ? b.nbits : 0;
+  int32_t base = nb - 57;
+  base = base > 0 ? (base + 7) & ~7 : 0;    // >= 50 readable bits after a fill
+  const uint32_t p = b.beg + (uint32_t)(base >> 3);
+  uint64_t v = 0;
+  for (uint32_t j = 0; j < 8; ++j) v |= (uint64_t)wbyte(w, c, p + j) << (8 * j);
+  b.cont = v;
+  b.cbase = base;
+}
+
+// the next k (<= 32) bits without consuming them; past the stream start
+// the bits read as zeros (the caller sees nbits < 0 afterwards)
+HD uint32_t br_peek(BR &b, const Win &w, const Ctx &c, uint32_t k) {
+  if (b.nbits - (int32_t)k < b.cbase && b.cbase != 0) br_fill(b, w, c);
+  const int32_t lo = b.nbits - (int32_t)k - b.cbase;
+  const uint64_t m = (1ull << k) - 1;
+  if (lo >= 0) return (uint32_t)((b.cont >> lo) & m);
+  if (b.nbits <= 0) return 0;
+  return (uint32_t)((b.cont << (-lo)) & m);
+}
+
+HD uint32_t br_read(BR &b, const Win &w, const Ctx &c, uint32_t k) {
+  if (k == 0) return 0;
+  const uint32_t v = br_peek(b, w, c, k);
+  b.nbits -= (int32_t)k;
+  return v;
+}
+
+// forward bits (table descriptions): bytes [p, end), bit offset from p
+struct FR {
+  uint32_t p, end, bit;
+};
+
+HD uint32_t fr_peek(const Ctx &c, const FR &f, uint32_t k) {   // k <= 24
+  const uint32_t q = f.p + (f.bit >> 3);
+  uint32_t v = 0;
+  for (uint32_t j = 0; j < 4; ++j) v |= (q + j < f.end ? gbyte(c, q + j) : 0u) << (8 * j);
+  return (v >> (f.bit & 7)) & ((1u << k) - 1);
+}
+
+// ------------------------------------------------------------- FSE tables
+// FSE table description (RFC 8878 4.1.1) -> normalized counts
+HD bool fse_norm(const Ctx &c, FR &f, int16_t *norm, uint32_t maxsym, uint32_t maxal,
+                 uint32_t &nsym, uint32_t &al) {
+  const uint32_t limit = (f.end - f.p) * 8;
+  al = fr_peek(c, f, 4) + 5;
+  f.bit += 4;
+  if (al > maxal) return ZF(false);
+  int32_t remaining = (1 << al) + 1, threshold = 1 << al;
+  uint32_t nbits = al + 1, sym = 0;
+  bool prev0 = false;
+  while (remaining > 1 && sym <= maxsym) {
+    if (prev0) {
+      uint32_t n0 = sym;
+      while (fr_peek(c, f, 2) == 3) {
+        n0 += 3;
+        f.bit += 2;
+        if (f.bit > limit || n0 > maxsym) return ZF(false);
+      }
+      n0 += fr_peek(c, f, 2);
+      f.bit += 2;
+      if (n0 > maxsym) return ZF(false);
+      while (sym < n0) norm[sym++] = 0;
+    }
+    const int32_t max = 2 * threshold - 1 - remaining;
+    const uint32_t v = fr_peek(c, f, nbits);
+    int32_t count;
+    if ((int32_t)(v & (uint32_t)(threshold - 1)) < max) {
+      count = (int32_t)(v & (uint32_t)(threshold - 1));
+      f.bit += nbits - 1;
+    } else {
+      count = (int32_t)(v & (uint32_t)(2 * threshold - 1));
+      if (count >= threshold) count -= max;
+      f.bit += nbits;
+    }
+    --count;
+    remaining -= count < 0 ? -count : count;
+    if (remaining < 1) return ZF(false);
+    norm[sym++] = (int16_t)count;
+    prev0 = count == 0;
+    while (remaining < threshold) {
+      --nbits;
+      threshold >>= 1;
+    }
+    if (f.bit > limit) return ZF(false);
+  }
+  if (remaining != 1) return ZF(false);
+  nsym = sym;
+  f.bit = (f.bit + 7) & ~7u;
+  return true;
+}
+
+// decoding table from normalized counts (RFC 8878 4.1.1: symbol spread,
+// then state numbering)
+HD bool fse_build(SeqEnt *tab, const int16_t *norm, uint32_t nsym, uint32_t al, uint32_t kind,
+                  uint16_t *snext) {
+  const uint32_t size = 1u << al, mask = size - 1;
+  uint32_t high = size - 1;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    if (norm[s] == -1) {
+      tab[high--].nb = (uint8_t)s;
+      snext[s] = 1;
+    } else {
+      snext[s] = (uint16_t)norm[s];
+    }
+  }
+  const uint32_t step = (size >> 1) + (size >> 3) + 3;
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s < nsym; ++s)
+    for (int32_t i = 0; i < norm[s]; ++i) {
+      tab[pos].nb = (uint8_t)s;
+      do pos = (pos + step) & mask;
+      while (pos > high);
+    }
+  if (pos != 0) return ZF(false);
+  for (uint32_t u = 0; u < size; ++u) {
+    const uint32_t s = tab[u].nb;
+    const uint32_t nx = snext[s]++;
+    const uint32_t nb = al - hibit(nx);
+    uint32_t base, add;
+    code_base(kind, s, base, add);
+    tab[u].next = (uint16_t)((nx << nb) - size);
+    tab[u].nb = (uint8_t)nb;
+    tab[u].add = (uint8_t)add;
+    tab[u].base = base;
+  }
+  return true;
+}
+
+HD void fse_rle(SeqEnt *tab, uint32_t sym, uint32_t kind) {
+  uint32_t base, add;
+  code_base(kind, sym, base, add);
+  tab[0].base = base;
+  tab[0].add = (uint8_t)add;
+  tab[0].nb = 0;
+  tab[0].next = 0;
+}
+
+HD void fse_predef(Smem &s, SeqEnt *tab, uint32_t kind, uint32_t &al) {
+  const int8_t *src = kind == kLL ? kNormLL : kind == kML ? kNormML : kNormOF;
+  const uint32_t n = kind == kLL ? 36 : kind == kML ? 53 : 29;
+  for (uint32_t i = 0; i < n; ++i) s.norm[i] = src[i];
+  al = kind == kOF ? 5 : 6;
+  fse_build(tab, s.norm, n, al, kind, s.snext);
+}
+
+// ------------------------------------------------------------- Huffman
+// Huffman tree description (RFC 8878 4.2.1) -> weights hw[0..nw)
+HD bool huf_weights(Smem &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &used,
+                    uint32_t &nw) {
+  if (p >= end) return ZF(false);
+  const uint32_t hb = gbyte(c, p);
+  if (hb >= 128) {
+    nw = hb - 127;
+    const uint32_t nbytes = (nw + 1) / 2;
+    if (p + 1 + nbytes > end) return ZF(false);
+    for (uint32_t i = 0; i < nw; ++i) {
+      const uint32_t b = gbyte(c, p + 1 + i / 2);
+      s.hw[i] = (uint8_t)(i & 1 ? b & 15 : b >> 4);
+    }
+    used = 1 + nbytes;
+    return true;
+  }
+  if (hb == 0 || p + 1 + hb > end) return ZF(false);
+  FR f{p + 1, p + 1 + hb, 0};
+  uint32_t nsym, al;
+  if (!fse_norm(c, f, s.norm, 12, 6, nsym, al)) return ZF(false);
+  SeqEnt *wt = (SeqEnt *)s.ptr;
+  if (!fse_build(wt, s.norm, nsym, al, kPlain, s.snext)) return ZF(false);
+  const uint32_t bp = f.p + (f.bit >> 3);
+  BR b;
+  if (bp >= f.end || !br_init(b, c, bp, f.end - bp)) return ZF(false);
+  const Win w{nullptr, 0, 0};
+  uint32_t s1 = br_read(b, w, c, al), s2 = br_read(b, w, c, al);
+  uint32_t n = 0;
+  // two interleaved states until the stream is over-read; then the other
+  // state's symbol is the last weight (RFC 8878 4.2.1.2)
+  for (;;) {
+    if (n + 2 > 255) return ZF(false);
+    s.hw[n++] = (uint8_t)wt[s1].base;
+    s1 = wt[s1].next + br_read(b, w, c, wt[s1].nb);
+    if (b.nbits < 0) {
+      s.hw[n++] = (uint8_t)wt[s2].base;
+      break;
+    }
+    if (n + 2 > 255) return ZF(false);
+    s.hw[n++] = (uint8_t)wt[s2].base;
+    s2 = wt[s2].next + br_read(b, w, c, wt[s2].nb);
+    if (b.nbits < 0) {
+      s.hw[n++] = (uint8_t)wt[s1].base;
+      break;
+    }
+  }
+  nw = n;
+  used = 1 + hb;
+  return true;
+}
+
+// decode table: entries ordered by weight, then symbol; a weight-w symbol
+// covers 2^(w-1) entries and has code length hbits + 1 - w
+HD bool huf_build(Smem &s, uint32_t nw) {
+  uint32_t total = 0;
+  for (uint32_t i = 0; i < nw; ++i) {
+    const uint32_t w = s.hw[i];
+    if (w > 11) return ZF(false);
+    if (w) total += 1u << (w - 1);
+  }
+  if (!total) return ZF(false);
+  const uint32_t maxb = hibit(total) + 1;
+  if (maxb > 11) return ZF(false);
+  const uint32_t rest = (1u << maxb) - total;
+  if (rest & (rest - 1)) return ZF(false);
+  s.hw[nw] = (uint8_t)(hibit(rest) + 1);
+  const uint32_t nsym = nw + 1;
+  for (uint32_t w = 0; w < 16; ++w) s.wrank[w] = 0;
+  for (uint32_t i = 0; i < nsym; ++i) s.wrank[s.hw[i]]++;
+  uint32_t pos = 0;
+  for (uint32_t w = 1; w <= maxb; ++w) {
+    const uint32_t n = s.wrank[w];
+    s.wrank[w] = pos;
+    pos += n << (w - 1);
+  }
+  if (pos != (1u << maxb)) return ZF(false);
+  for (uint32_t i = 0; i < nsym; ++i) {
+    const uint32_t w = s.hw[i];
+    if (!w) continue;
+    const uint32_t n = 1u << (w - 1), st = s.wrank[w];
+    const uint16_t e = (uint16_t)((i << 4) | (maxb + 1 - w));
+    for (uint32_t j = 0; j < n; ++j) s.huf[st + j] = e;
+    s.wrank[w] = st + n;
+  }
+  s.hbits = maxb;
+  return true;
+}
+
+// ------------------------------------------------------------- lane 0: headers
+HD void stream_init(Smem &s, const Ctx &c, int codec) {
+  s.err = 0;
+  s.op = 0;
+  s.ip = 0;
+  s.state = kFrame;
+  s.expect = -1;
+  s.hbits = 0;
+  if (c.cap >= kPosMax || c.len >= kPosMax) {
+    s.err = kErrOverflow;
+    return;
+  }
+  if (codec == STROM_CODEC_ARROW_ZSTD) {
+    if (c.len < 8) {
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    const int64_t pre = (int64_t)((uint64_t)rd32(c, 0) | ((uint64_t)rd32(c, 4) << 32));
+    s.ip = 8;
+    if (pre == -1) {               // stored uncompressed: one raw unit
+      s.state = kStored;
+      return;
+    }
+    if (pre < 0 || pre > (int64_t)c.cap) {
+      s.err = pre < 0 ? kErrFormat : kErrOverflow;
+      return;
+    }
+    s.expect = pre;
+  }
+}
+
+// Parse frame headers (skipping skippable frames) and the next block
+// header.  Sets s.state = kDone at the end of the input.
+HD void next_block(Smem &s, const Ctx &c) {
+  if (s.state == kStored) {        // Arrow buffer stored uncompressed
+    s.state = kBlock;
+    s.btype = kRaw;
+    s.bstart = 8;
+    s.bend = c.len;
+    s.bsize = c.len - 8;
+    s.blast = 1;
+    s.cksum = 0;
+    s.fcs_set = 0;
+    if ((uint64_t)s.op + s.bsize > c.cap) s.err = kErrOverflow;
+    return;
+  }
+  while (s.state == kFrame) {
+    const uint32_t p = s.ip;
+    if (p == c.len) {
+      s.state = kDone;
+      return;
+    }
+    if (p + 4 > c.len) {
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    const uint32_t magic = rd32(c, p);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {   // skippable frame
+      const uint64_t n = (uint64_t)p + 8 + rd32(c, p + 4);
+      if (p + 8 > c.len || n > c.len) {
+        s.err = ZF(kErrFormat);
+        return;
+      }
+      s.ip = (uint32_t)n;
+      continue;
+    }
+    if (magic != 0xFD2FB528u || p + 5 > c.len) {
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    const uint32_t fhd = gbyte(c, p + 4);
+    if (fhd & 0x08) {              // reserved bit
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    const uint32_t fcsf = fhd >> 6, single = (fhd >> 5) & 1, didf = fhd & 3;
+    uint32_t q = p + 5 + (single ? 0 : 1);
+    const uint32_t dsz = didf == 3 ? 4 : didf;
+    uint32_t did = 0;
+    for (uint32_t j = 0; j < dsz; ++j) did |= gbyte(c, q + j) << (8 * j);
+    q += dsz;
+    if (did != 0) {
+      s.err = kErrUnsupported;     // dictionaries: Arrow writes none
+      return;
+    }
+    const uint32_t fsz = fcsf == 0 ? single : fcsf == 1 ? 2 : fcsf == 2 ? 4 : 8;
+    uint64_t fcs = 0;
+    for (uint32_t j = 0; j < fsz; ++j) fcs |= (uint64_t)gbyte(c, q + j) << (8 * j);
+    if (fsz == 2) fcs += 256;
+    q += fsz;
+    if (q > c.len) {
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    s.fcs_set = fsz != 0;
+    if (s.fcs_set && (uint64_t)s.op + fcs > c.cap) {
+      s.err = kErrOverflow;
+      return;
+    }
+    s.fcs = (uint32_t)fcs;
+    s.cksum = (fhd >> 2) & 1;
+    s.fstart = s.op;
+    s.rep[0] = 1;
+    s.rep[1] = 4;
+    s.rep[2] = 8;
+    s.hbits = 0;
+    s.have_ll = s.have_of = s.have_ml = 0;
+    s.ip = q;
+    s.state = kBlock;
+  }
+  const uint32_t p = s.ip;
+  if (p + 3 > c.len) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  const uint32_t h = gbyte(c, p) | (gbyte(c, p + 1) << 8) | (gbyte(c, p + 2) << 16);
+  s.blast = h & 1;
+  s.btype = (h >> 1) & 3;
+  s.bsize = h >> 3;
+  s.bstart = p + 3;
+  if (s.btype == 3 || s.bsize > MAXB) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  const uint64_t in_end = (uint64_t)s.bstart + (s.btype == kRle ? 1 : s.bsize);
+  if (in_end > c.len) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  s.bend = (uint32_t)in_end;
+  s.ip = s.bstart;
+  if (s.btype != kComp && (uint64_t)s.op + s.bsize > c.cap) s.err = kErrOverflow;
+}
+
+// after a block: advance; at the end of a frame skip the checksum and
+// check the content size
+HD void end_block(Smem &s, const Ctx &c) {
+  s.ip = s.bend;
+  if (!s.blast) return;
+  if (s.cksum) {
+    if (s.ip + 4 > c.len) {
+      s.err = ZF(kErrFormat);
+      return;
+    }
+    s.ip += 4;
+  }
+  if (s.fcs_set && s.op - s.fstart != s.fcs) s.err = ZF(kErrFormat);
+  s.state = kFrame;                // the next frame, or the end of the input
+}
+
+HD bool lit_header(Smem &s, const Ctx &c) {
+  const uint32_t p = s.ip, end = s.bend;
+  const uint32_t b0 = gbyte(c, p), type = b0 & 3, sf = (b0 >> 2) & 3;
+  s.lit_used = 0;
+  for (uint32_t j = 0; j < 4; ++j) s.lcnt[j] = 0;
+  if (type <= 1) {
+    uint32_t R, hl;
+    if ((sf & 1) == 0) {
+      R = b0 >> 3;
+      hl = 1;
+    } else if (sf == 1) {
+      R = (b0 >> 4) + (gbyte(c, p + 1) << 4);
+      hl = 2;
+    } else {
+      R = (b0 >> 4) + (gbyte(c, p + 1) << 4) + (gbyte(c, p + 2) << 12);
+      hl = 3;
+    }
+    if (R > MAXB) return ZF(false);
+    s.lit_n = R;
+    if (type == 0) {
+      if ((uint64_t)p + hl + R > end) return ZF(false);
+      s.lit_kind = kLitInput;
+      s.lit_base = p + hl;
+      s.ip = p + hl + R;
+    } else {
+      if (p + hl + 1 > end) return ZF(false);
+      s.lit_kind = kLitRle;
+      s.lit_rle = gbyte(c, p + hl);
+      s.ip = p + hl + 1;
+    }
+    return true;
+  }
+  const uint32_t hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5, bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
+  uint64_t h = 0;
+  for (uint32_t j = 0; j < hl; ++j) h |= (uint64_t)gbyte(c, p + j) << (8 * j);
+  const uint32_t R = (uint32_t)(h >> 4) & ((1u << bits) - 1);
+  const uint32_t C = (uint32_t)(h >> (4 + bits)) & ((1u << bits) - 1);
+  if (R > MAXB || (uint64_t)p + hl + C > end) return ZF(false);
+  uint32_t d = p + hl;
+  const uint32_t dend = d + C;
+  if (type == 2) {
+    uint32_t used, nw;
+    if (!huf_weights(s, c, d, dend, used, nw) || !huf_build(s, nw)) return ZF(false);
+    d += used;
+  } else if (!s.hbits) {
+    return ZF(false);                  // treeless literals need an earlier table
+  }
+  s.nls = sf == 0 ? 1 : 4;
+  if (s.nls == 1) {
+    if (!br_init(s.lbr[0], c, d, dend - d)) return ZF(false);
+    s.lcnt[0] = R;
+    s.lout[0] = 0;
+  } else {
+    if (d + 6 > dend) return ZF(false);
+    const uint32_t l1 = rd16(c, d), l2 = rd16(c, d + 2), l3 = rd16(c, d + 4);
+    d += 6;
+    const uint32_t tot = dend - d;
+    if (l1 + l2 + l3 >= tot) return ZF(false);
+    const uint32_t len[4] = {l1, l2, l3, tot - l1 - l2 - l3};
+    const uint32_t seg = (R + 3) / 4;
+    if (3 * seg > R) return ZF(false);
+    for (uint32_t j = 0; j < 4; ++j) {
+      if (!br_init(s.lbr[j], c, d, len[j])) return ZF(false);
+      d += len[j];
+      s.lout[j] = j * seg;
+      s.lcnt[j] = j < 3 ? seg : R - 3 * seg;
+    }
+  }
+  s.lit_kind = kLitScratch;
+  s.lit_n = R;
+  s.ip = dend;
+  return true;
+}
+
+HD bool seq_table(Smem &s, const Ctx &c, uint32_t mode, uint32_t kind, uint32_t &p,
+                  uint32_t end, SeqEnt *tab, uint32_t &al, uint32_t &have) {
+  const uint32_t maxsym = kind == kLL ? 35 : kind == kML ? 52 : 31;
+  const uint32_t maxal = kind == kOF ? 8 : 9;
+  if (mode == 0) {
+    fse_predef(s, tab, kind, al);
+  } else if (mode == 1) {
+    if (p >= end) return ZF(false);
+    const uint32_t sym = gbyte(c, p++);
+    if (sym > maxsym) return ZF(false);
+    fse_rle(tab, sym, kind);
+    al = 0;
+  } else if (mode == 2) {
+    FR f{p, end, 0};
+    uint32_t nsym;
+    if (!fse_norm(c, f, s.norm, maxsym, maxal, nsym, al)) return ZF(false);
+    if (!fse_build(tab, s.norm, nsym, al, kind, s.snext)) return ZF(false);
+    p += f.bit >> 3;
+  } else if (!have) {
+    return ZF(false);                  // repeat mode without a previous table
+  }
+  have = 1;
+  return true;
+}
+
+HD bool seq_header(Smem &s, const Ctx &c) {
+  uint32_t p = s.ip;
+  const uint32_t end = s.bend;
+  if (p >= end) return ZF(false);
+  const uint32_t b0 = gbyte(c, p);
+  uint32_t n;
+  if (b0 == 0) {
+    s.nseq = 0;
+    s.seq_done = 0;
+    return p + 1 == end ? true : ZF(false);
+  }
+  if (b0 < 128) {
+    n = b0;
+    p += 1;
+  } else if (b0 < 255) {
+    n = ((b0 - 128) << 8) + gbyte(c, p + 1);
+    p += 2;
+  } else {
+    n = gbyte(c, p + 1) + (gbyte(c, p + 2) << 8) + 0x7F00;
+    p += 3;
+  }
+  if (p >= end) return ZF(false);
+  const uint32_t modes = gbyte(c, p++);
+  if (modes & 3) return ZF(false);
+  if (!seq_table(s, c, modes >> 6, kLL, p, end, s.tll, s.al_ll, s.have_ll) ||
+      !seq_table(s, c, (modes >> 4) & 3, kOF, p, end, s.tof, s.al_of, s.have_of) ||
+      !seq_table(s, c, (modes >> 2) & 3, kML, p, end, s.tml, s.al_ml, s.have_ml))
+    return ZF(false);
+  if (p >= end || !br_init(s.sbr, c, p, end - p)) return ZF(false);
+  const Win w{nullptr, 0, 0};
+  s.st_ll = br_read(s.sbr, w, c, s.al_ll);
+  s.st_of = br_read(s.sbr, w, c, s.al_of);
+  s.st_ml = br_read(s.sbr, w, c, s.al_ml);
+  s.nseq = n;
+  s.seq_done = 0;
+  return s.sbr.nbits >= 0 ? true : ZF(false);
+}
+
+// ------------------------------------------------------------- phases
+// window origin of a backward stream: covers the next chunk's reads
+HD uint32_t win_lo(const BR &b, uint32_t wsize) {
+  const int32_t nb = b.nbits > 0 ? b.nbits : 0;
+  const int32_t back = (nb >> 3) - (int32_t)(wsize - 16);
+  return b.beg + (uint32_t)(back > 0 ? back : 0);
+}
+
+// (1) literal windows: lane t copies every NT-th byte of each stream window
+HD void lit_load(Smem &s, const Ctx &c, uint32_t t) {
+  for (uint32_t j = 0; j < s.nls; ++j) {
+    if (!s.lcnt[j]) continue;
+    const uint32_t lo = s.lwlo[j];
+    uint8_t r[LWIN / NT];
+#pragma unroll
+    for (uint32_t k = 0; k < LWIN / NT; ++k) r[k] = (uint8_t)gbyte(c, lo + t + k * NT);
+#pragma unroll
+    for (uint32_t k = 0; k < LWIN / NT; ++k) s.lwin[j][t + k * NT] = r[k];
+  }
+}
+
+// (1) up to LSYM symbols of literal stream j
+HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
+  const uint32_t left = s.lcnt[j];
+  if (!left) return;
+  BR b = s.lbr[j];
+  const Win w{s.lwin[j], s.lwlo[j], LWIN};
+  const uint32_t n = left < LSYM ? left : LSYM, mb = s.hbits;
+  const uint32_t o = s.lout[j];
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t e = s.huf[br_peek(b, w, c, mb)];
+    b.nbits -= (int32_t)(e & 15);
+    c.lit[o + k] = (uint8_t)(e >> 4);
+  }
+  s.lout[j] = o + n;
+  s.lcnt[j] = left - n;
+  s.lbr[j] = b;
+  if (left == n && b.nbits != 0) s.err = ZF(kErrFormat);   // a stream ends exactly
+}
+
+// (2) sequence window: lane t copies every NT-th byte
+HD void seq_load(Smem &s, const Ctx &c, uint32_t t) {
+  const uint32_t lo = s.swlo;
+  uint8_t r[SWIN / NT];
+#pragma unroll
+  for (uint32_t k = 0; k < SWIN / NT; ++k) r[k] = (uint8_t)gbyte(c, lo + t + k * NT);
+#pragma unroll
+  for (uint32_t k = 0; k < SWIN / NT; ++k) s.swin[t + k * NT] = r[k];
+}
+
+// (2) lane 0: up to SEQN sequences -> chunk entries; the block's last chunk
+// also gets the trailing literals as an entry without a match
+HD void seq_chunk(Smem &s, const Ctx &c) {
+  const uint32_t left = s.nseq - s.seq_done;
+  const uint32_t m = left < SEQN ? left : SEQN;
+  BR b = s.sbr;
+  const Win w{s.swin, s.swlo, SWIN};
+  uint32_t sll = s.st_ll, sof = s.st_of, sml = s.st_ml;
+  uint32_t r0 = s.rep[0], r1 = s.rep[1], r2 = s.rep[2];
+  const uint32_t pos0 = s.op - s.fstart;    // frame output before this chunk
+  uint32_t n = 0, out = 0, lit = s.lit_used;
+  for (uint32_t i = 0; i < m; ++i) {
+    const SeqEnt eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
+    const uint32_t ofv = eo.base + br_read(b, w, c, eo.add);
+    const uint32_t ml = em.base + br_read(b, w, c, em.add);
+    const uint32_t ll = el.base + br_read(b, w, c, el.add);
+    uint32_t off;
+    if (ofv > 3) {
+      off = ofv - 3;
+      r2 = r1;
+      r1 = r0;
+      r0 = off;
+    } else {
+      const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
+      if (k == 0) {
+        off = r0;
+      } else if (k == 1) {
+        off = r1;
+        r1 = r0;
+        r0 = off;
+      } else {
+        off = k == 2 ? r2 : r0 - 1;
+        r2 = r1;
+        r1 = r0;
+        r0 = off;
+      }
+    }
+    if (s.seq_done + i + 1 < s.nseq) {
+      sll = el.next + br_read(b, w, c, el.nb);
+      sml = em.next + br_read(b, w, c, em.nb);
+      sof = eo.next + br_read(b, w, c, eo.nb);
+    }
+    if (lit + ll > s.lit_n) {
+      s.err = ZF(kErrFormat);
+      break;
+    }
+    const uint64_t at = (uint64_t)pos0 + out + ll;
+    if (off == 0 || off > at) {
+      s.err = ZF(kErrDistance);
+      break;
+    }
+    if ((uint64_t)out + ll + ml > MAXB) {
+      s.err = ZF(kErrFormat);
+      break;
+    }
+    s.sll[n] = ll;
+    s.soff[n] = off;
+    s.lst[n] = lit;
+    s.ost[n] = out;
+    lit += ll;
+    out += ll + ml;
+    ++n;
+  }
+  s.seq_done += m;
+  if (!s.err && s.seq_done == s.nseq) {
+    if (s.nseq && b.nbits != 0) s.err = ZF(kErrFormat);
+    const uint32_t rest = s.lit_n - lit;
+    if (rest) {
+      s.sll[n] = rest;
+      s.soff[n] = 0;
+      s.lst[n] = lit;
+      s.ost[n] = out;
+      out += rest;
+      lit += rest;
+      ++n;
+    }
+  }
+  s.ost[n] = out;
+  s.cn = n;
+  s.ctot = out;
+  s.lit_used = lit;
+  s.sbr = b;
+  s.st_ll = sll;
+  s.st_of = sof;
+  s.st_ml = sml;
+  s.rep[0] = r0;
+  s.rep[1] = r1;
+  s.rep[2] = r2;
+  if (!s.err && (uint64_t)s.op + out > c.cap) s.err = kErrOverflow;
+}
+
+// chunk entry holding output byte pos (ost strictly increases)
+HD uint32_t entry_of(const Smem &s, uint32_t pos) {
+  uint32_t lo = 0, hi = s.cn;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s.ost[mid] <= pos) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// (3a) source pointer of every byte of the batch [b0, b0 + nb)
+HD void ex_fill(Smem &s, uint32_t t, uint32_t b0, uint32_t nb) {
+  const uint32_t abs0 = s.op;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * NT + t;
+    if (e >= nb) break;
+    const uint32_t pos = b0 + e, i = entry_of(s, pos), r = pos - s.ost[i];
+    uint32_t v;
+    if (r < s.sll[i]) {
+      v = kLit | (s.lst[i] + r);
+    } else {
+      const uint32_t src = abs0 + pos - s.soff[i];
+      v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
+    }
+    s.ptr[e] = v;
+  }
+}
+
+// (3b) one doubling round; true while some pointer is still in the batch
+// (concurrent rounds only ever replace a pointer by one further down its
+// chain: any value a lane reads is a valid ancestor)
+HD bool ex_double(Smem &s, uint32_t t, uint32_t nb) {
+  bool more = false;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * NT + t;
+    if (e >= nb) break;
+    const uint32_t v = s.ptr[e];
+    if (v & kTag) continue;
+    const uint32_t x = s.ptr[v];
+    s.ptr[e] = x;
+    more |= !(x & kTag);
+  }
+  return more;
+}
+
+HD uint8_t ld_stored(const uint8_t *base, uint32_t pos) {
+#ifdef __HIP_DEVICE_COMPILE__
+  // stored by this workgroup before the release fence + barrier that ended
+  // the phase; bypass L1 (it may hold an older copy of the line)
+  const uintptr_t a = (uintptr_t)(base + pos);
+  const uint32_t d = __hip_atomic_load((const uint32_t *)(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return (uint8_t)(d >> (8 * (a & 3)));
+#else
+  return base[pos];
+#endif
+}
+
+// (3c) gather + store
+HD void ex_write(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb) {
+  const uint32_t o = s.op + b0;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * NT + t;
+    if (e >= nb) break;
+    const uint32_t v = s.ptr[e], x = v & ~kTag;
+    uint8_t y;
+    if (v & kLit)
+      y = s.lit_kind == kLitInput ? c.in[s.lit_base + x]
+        : s.lit_kind == kLitRle ? (uint8_t)s.lit_rle : ld_stored(c.lit, x);
+    else
+      y = ld_stored(c.out, x);
+    c.out[o + e] = y;
+  }
+}
+
+// raw / RLE block (or a stored Arrow buffer): lane-strided copy
+HD void copy_block(const Smem &s, const Ctx &c, uint32_t t) {
+  uint8_t *o = c.out + s.op;
+  if (s.btype == kRle) {
+    const uint8_t v = (uint8_t)gbyte(c, s.bstart);
+    for (uint32_t i = t; i < s.bsize; i += NT) o[i] = v;
+  } else {
+    const uint8_t *in = c.in + s.bstart;
+    for (uint32_t i = t; i < s.bsize; i += NT) o[i] = in[i];
+  }
+}
+
+// ------------------------------------------------------------- driver
+template <class TM>
+HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
+  tm.one([&] { stream_init(s, c, codec); });
+  tm.sync();
+  while (!s.err) {
+    tm.one([&] { next_block(s, c); });
+    tm.sync();
+    if (s.err || s.state == kDone) break;
+    if (s.btype != kComp) {
+      tm.each([&](uint32_t t) { copy_block(s, c, t); });
+      tm.fence();
+      tm.sync();
+      tm.one([&] {
+        s.op += s.bsize;
+        end_block(s, c);
+      });
+      tm.sync();
+      continue;
+    }
+    tm.one([&] {
+      if (!lit_header(s, c)) s.err = ZF(kErrFormat);
+    });
+    tm.sync();
+    if (s.err) break;
+    if (s.lit_kind == kLitScratch) {
+      for (;;) {
+        tm.each([&](uint32_t t) {
+          if (t < s.nls) s.lwlo[t] = win_lo(s.lbr[t], LWIN);
+        });
+        tm.sync();
+        tm.each([&](uint32_t t) { lit_load(s, c, t); });
+        tm.sync();
+        tm.each([&](uint32_t t) {
+          if (t < s.nls) lit_chunk(s, c, t);
+        });
+        tm.sync();
+        if (s.err || !(s.lcnt[0] | s.lcnt[1] | s.lcnt[2] | s.lcnt[3])) break;
+      }
+      tm.fence();
+      tm.sync();
+      if (s.err) break;
+    }
+    tm.one([&] {
+      if (!seq_header(s, c)) s.err = ZF(kErrFormat);
+    });
+    tm.sync();
+    if (s.err) break;
+    do {
+      tm.one([&] { s.swlo = win_lo(s.sbr, SWIN); });
+      tm.sync();
+      if (s.nseq) {
+        tm.each([&](uint32_t t) { seq_load(s, c, t); });
+        tm.sync();
+      }
+      tm.one([&] { seq_chunk(s, c); });
+      tm.sync();
+      if (s.err) break;
+      const uint32_t total = s.ctot;
+      for (uint32_t b0 = 0; b0 < total; b0 += OB) {
+        const uint32_t nb = total - b0 < OB ? total - b0 : OB;
+        tm.each([&](uint32_t t) { ex_fill(s, t, b0, nb); });
+        tm.sync();
+        while (tm.any([&](uint32_t t) { return ex_double(s, t, nb); })) {
+        }
+        tm.each([&](uint32_t t) { ex_write(s, c, t, b0, nb); });
+        tm.fence();
+        tm.sync();
+      }
+      tm.one([&] { s.op += total; });
+      tm.sync();
+    } while (s.seq_done < s.nseq);
+    if (s.err) break;
+    tm.one([&] { end_block(s, c); });
+    tm.sync();
+  }
+  tm.one([&] {
+    if (!s.err && s.expect >= 0 && (int64_t)s.op != s.expect) s.err = ZF(kErrFormat);
+  });
+  tm.sync();
+}
+
+struct DevTeam {
+  __device__ void sync() { __syncthreads(); }
+  __device__ void fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+  template <class F>
+  __device__ void each(F f) { f(threadIdx.x); }
+  template <class F>
+  __device__ void one(F f) {
+    if (threadIdx.x == 0) f();
+  }
+  template <class F>
+  __device__ bool any(F f) { return __syncthreads_or(f(threadIdx.x)); }
+};
+
+struct HostTeam {
+  void sync() {}
+  void fence() {}
+  template <class F>
+  void each(F f) {
+    for (uint32_t t = 0; t < NT; ++t) f(t);
+  }
+  template <class F>
+  void one(F f) { f(); }
+  template <class F>
+  bool any(F f) {
+    bool v = false;
+    for (uint32_t t = 0; t < NT; ++t) v |= f(t);
+    return v;
+  }
+};
+
+__global__ void __launch_bounds__(NT) zstd_kernel(int codec, const uint8_t *src, uint8_t *dst,
+                                                   const strom_decomp_desc *desc, uint32_t n,
+                                                   int32_t *status, uint8_t *scratch) {
+  __shared__ Smem s;
+  DevTeam tm;
+  uint8_t *lit = scratch + (size_t)blockIdx.x * SLOT;
+  for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const strom_decomp_desc d = desc[b];
+    const Ctx c{src + d.src_off, dst + d.dst_off, lit, d.src_len, d.dst_len};
+    run(tm, s, c, codec);
+    if (threadIdx.x == 0) status[b] = s.err ? s.err : (int32_t)s.op;
+    __syncthreads();
+  }
+}
+
+// literal scratch per (device, stream): launches on one stream are ordered,
+// concurrent launches on different streams never share a slot
+std::mutex g_mu;
+std::map<std::pair<int, void *>, std::pair<uint8_t *, size_t>> g_scratch;
+
+uint8_t *scratch_for(void *stream, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(g_mu);
+  auto &e = g_scratch[{dev, stream}];
+  if (e.second < bytes) {
+    if (e.first) (void)hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    e.first = (uint8_t *)p;
+    e.second = bytes;
+  }
+  return e.first;
+}
+
+uint32_t resident_groups() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  const uint32_t per_cu = (160u << 10) / (uint32_t)sizeof(Smem);   // LDS-bound residency
+  return (uint32_t)cus * (per_cu ? per_cu : 1);
+}
+
+}  // namespace zs
+
+// Zstandard streams (STROM_CODEC_ZSTD: frames; STROM_CODEC_ARROW_ZSTD: an
+// Arrow IPC buffer) — one wavefront per stream, persistent over the
+// streams.  scratch: SLOT (128 KiB) per workgroup for decoded literals;
+// NULL = a per-stream buffer kept by the library.
+extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
+                                     const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                     int32_t *d_status, void *scratch, uint64_t scratch_bytes,
+                                     void *stream) {
+  using namespace zs;
+  if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  if (!nstreams) return 0;
+  uint32_t grid = nstreams < resident_groups() ? nstreams : resident_groups();
+  if (grid > 65535) grid = 65535;
+  uint8_t *sc = (uint8_t *)scratch;
+  if (sc) {
+    const uint64_t slots = scratch_bytes / SLOT;
+    if (!slots) return -22;
+    if (grid > slots) grid = (uint32_t)slots;
+  } else {
+    sc = scratch_for(stream, (size_t)grid * SLOT);
+    if (!sc) return -12;
+  }
+  hipLaunchKernelGGL(zstd_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
+                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status, sc);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
+
+// The same phases lane by lane on the CPU: the algorithm's reference
+// (tests/test_codecs_cpu.py), no GPU involved.  Returns decoded bytes or a
+// negative error as the kernel's status.
+extern "C" int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
+                               uint32_t cap) {
+  using namespace zs;
+  if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  std::unique_ptr<Smem> s(new Smem());
+  std::unique_ptr<uint8_t[]> lit(new uint8_t[SLOT]);
+  HostTeam tm;
+  const Ctx c{src, dst, lit.get(), src_len, cap};
+  run(tm, *s, c, codec);
+  return s->err ? s->err : (int32_t)s->op;
+}

@@ -226,6 +226,10 @@ _SIGS = {
     "strom_arrow_headers": (C.c_int, [C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,
                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_void_p, C.c_int32, C.c_void_p]),
+    "strom_zstd_host": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    "strom_decompress_zstd": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "strom_zstd_lds_bytes": (C.c_uint32, []),
     "strom_lz4par_host": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                     C.c_void_p]),
     "strom_decompress_par": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,

@@ -159,9 +159,12 @@ class ArrowScan:
             dtypes.append(_TORCH[col.numpy_dtype])
             widths.append(col.bit_width // 8)
         m = self.meta
-        for c in set(m.codecs):
-            if c not in (None, "lz4_frame"):
-                raise NotImplementedError(f"body compression {c} (GPU decoder: LZ4 frame)")
+        used = set(m.codecs) - {None}
+        if not used <= {"lz4_frame", "zstd"} or len(used) > 1:
+            raise NotImplementedError(f"body compression {sorted(used)} (GPU decoders: one of "
+                                      "LZ4 frame, ZSTD per file)")
+        # lz4par.hip / zstd.hip (Arrow IPC buffer codecs: length prefix + frame)
+        self._codec = D.ARROW_ZSTD if used == {"zstd"} else D.ARROW_LZ4
         comp = [c is not None for c in m.codecs]
         # per column, lists over batches (the metadata is array-backed)
         percol = []
@@ -187,6 +190,10 @@ class ArrowScan:
         cus = 256
         if self.device.type == "cuda":
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        if getattr(self, "_codec", None) == D.ARROW_ZSTD:
+            # zstd.hip: one wavefront per stream, residency bound by its LDS
+            from .. import _native as N
+            return cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
         return self.ROUND_STREAMS_PER_CU * cus
 
     def _chunks(self, b: _Batch) -> np.ndarray:
@@ -387,7 +394,7 @@ class ArrowScan:
                     self.device, non_blocking=True)
                 d_need = torch.from_numpy(g.need).pin_memory().to(self.device, non_blocking=True)
                 status = torch.empty(len(descs), dtype=torch.int32, device=self.device)
-                D.decompress_async(D.ARROW_LZ4, region, s.dec, d_desc, status, stream=cs)
+                D.decompress_async(self._codec, region, s.dec, d_desc, status, stream=cs)
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]

@@ -27,6 +27,8 @@ COPY = 3
 LZ4_FRAME = 4
 LZ4_FRAME_BCS = 5
 ARROW_LZ4 = 6          # Arrow IPC buffer: i64 length prefix (-1 = raw) + LZ4 frame
+ZSTD = 7               # Zstandard frame(s), RFC 8878 (csrc/kernels/zstd.hip)
+ARROW_ZSTD = 8         # Arrow IPC buffer: i64 length prefix (-1 = raw) + zstd frame
 
 DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_len", "<u4"),
                        ("dst_len", "<u4")])
@@ -142,6 +144,22 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
     n = fn(codec, src.ctypes.data, len(data), out.ctypes.data, cap, st.ctypes.data)
     stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]))
     return n, (out[:n].tobytes() if n >= 0 else b""), stats
+
+
+def zstd_host(codec: int, data: bytes, cap: int):
+    """The zstd kernel's phases run lane by lane on the CPU
+    (csrc/kernels/zstd.hip): -> (status, output bytes).  The reference for
+    the GPU decoder; status = decoded bytes or <0 (-1 malformed,
+    -2 overflow, -3 distance, -4 unsupported: a dictionary)."""
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
+    out = np.zeros(max(cap, 1), dtype=np.uint8)
+    n = N.lib().strom_zstd_host(codec, src.ctypes.data, len(data), out.ctypes.data, cap)
+    return n, (out[:n].tobytes() if n >= 0 else b"")
+
+
+def arrow_zstd_buffer(data: bytes, frame: bytes) -> bytes:
+    """An Arrow IPC compressed buffer: i64 uncompressed length + zstd frame."""
+    return struct.pack("<q", len(data)) + frame
 
 
 def arrow_lz4_buffer(data: bytes, frame: bytes) -> bytes:

@@ -1,8 +1,8 @@
-"""Config-5 benchmark: SSD -> HBM -> LZ4 decode -> filter of one column of
-an Arrow IPC file (models/arrow_scan.py), against pyarrow on the CPU.
+"""Config-5 benchmark: SSD -> HBM -> LZ4 / ZSTD decode -> filter of one
+column of an Arrow IPC file (models/arrow_scan.py), against pyarrow on the CPU.
 
 The file is written by pyarrow (LZ4_FRAME body compression, linked 64 KiB
-blocks as pyarrow writes them) with three columns — ``id`` (int64,
+blocks as pyarrow writes them; or ZSTD with ``--codec zstd``) with three columns — ``id`` (int64,
 sequential), ``val`` (int64, uniform in [0, 1e6)) and ``x`` (float64, 5 %
 nulls) — in record batches of ``--batch-rows``.  Each timed run starts with
 the file evicted from the page cache.  Reported per scanned column:
@@ -41,7 +41,7 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_file(path: str, rows: int, batch_rows: int, seed: int = 7) -> None:
+def make_file(path: str, rows: int, batch_rows: int, seed: int = 7, codec: str = "lz4") -> None:
     import pyarrow as pa
     import pyarrow.ipc as ipc
     if os.path.exists(path):
@@ -49,7 +49,7 @@ def make_file(path: str, rows: int, batch_rows: int, seed: int = 7) -> None:
     schema = pa.schema([("id", pa.int64()), ("val", pa.int64()), ("x", pa.float64())])
     rng = np.random.default_rng(seed)
     tmp = path + ".tmp"
-    with ipc.new_file(tmp, schema, options=ipc.IpcWriteOptions(compression="lz4")) as w:
+    with ipc.new_file(tmp, schema, options=ipc.IpcWriteOptions(compression=codec)) as w:
         for b0 in range(0, rows, batch_rows):
             n = min(batch_rows, rows - b0)
             ids = np.arange(b0, b0 + n, dtype=np.int64)
@@ -100,6 +100,8 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--slot-mib", type=int, default=256)
     ap.add_argument("--columns", default="val,x")
+    ap.add_argument("--codec", default="lz4", choices=["lz4", "zstd"],
+                    help="Arrow IPC body compression pyarrow writes the file with")
     ap.add_argument("--no-qual2", dest="qual2", action="store_false",
                     help="skip the two-column qualifier list + projection row")
     ap.add_argument("--out", default="")
@@ -110,9 +112,10 @@ def main(argv=None) -> int:
     from nvme_strom_amd.models.arrow_scan import ArrowScan
 
     os.makedirs(a.dir, exist_ok=True)
-    path = os.path.join(a.dir, f"t_{a.rows}_{a.batch_rows}.arrow")
+    tag = "" if a.codec == "lz4" else f"_{a.codec}"
+    path = os.path.join(a.dir, f"t_{a.rows}_{a.batch_rows}{tag}.arrow")
     t0 = time.time()
-    make_file(path, a.rows, a.batch_rows)
+    make_file(path, a.rows, a.batch_rows, codec=a.codec)
     fsize = os.path.getsize(path)
     _log(f"file {fsize / 2**30:.2f} GiB ({a.rows} rows, {a.batch_rows}/batch) in "
          f"{time.time() - t0:.1f}s")
@@ -120,15 +123,15 @@ def main(argv=None) -> int:
     specs = [(n, [(n, *preds[n])], None) for n in a.columns.split(",") if n]
     if a.qual2:
         specs.append(("qual2", [("val", 100_000, 599_999), ("x", 0.25, 0.75)], "id"))
-    res = dict(file_bytes=fsize, rows=a.rows, batch_rows=a.batch_rows, codec="lz4_frame (pyarrow)",
+    res = dict(file_bytes=fsize, rows=a.rows, batch_rows=a.batch_rows, codec=("lz4_frame" if a.codec == "lz4" else "zstd") + " (pyarrow)",
                slot_mib=a.slot_mib, reps=a.reps, columns={})
     fd = os.open(path, os.O_RDONLY)
     cols_np = {}
     # once per process: the first scan also loads the decoder/filter code
     # objects and the host allocators' first pinned blocks; a small file
     # takes that cost so each spec's cold run is the per-file (per-query) one
-    warm_path = os.path.join(a.dir, "warmup.arrow")
-    make_file(warm_path, 1 << 16, 1 << 14, seed=1)
+    warm_path = os.path.join(a.dir, f"warmup{tag}.arrow")
+    make_file(warm_path, 1 << 16, 1 << 14, seed=1, codec=a.codec)
     t1 = time.perf_counter()
     w = ArrowScan(warm_path, "cuda")
     w.scan_where([("val", 0, 1 << 40), ("x", 0.0, 1.0)], project="id")

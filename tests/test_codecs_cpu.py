@@ -1,4 +1,6 @@
 """Host codecs and checksums (CPU references for the GPU kernels)."""
+import struct
+
 import numpy as np
 import pytest
 
@@ -178,3 +180,100 @@ def test_lz4par_frames_and_errors():
     for _ in range(20):
         g = rng.integers(0, 256, int(rng.integers(1, 5000)), dtype=np.uint8).tobytes()
         assert D.lz4par_host(D.LZ4, g, 1 << 16)[0] <= 1 << 16
+
+
+# ------------------------------------------------------------------- zstd
+def _zstd_payloads():
+    rng = np.random.default_rng(11)
+    return {
+        "zeros": bytes(300000),
+        "random": _data("random", 200000, 1),
+        "text": _data("text", 330000, 2),
+        "runs": _data("runs", 250000, 3),
+        "uniform": _ints("uniform", 512 << 10, 4),
+        "sorted": _ints("sorted", 512 << 10, 5),
+        "floats": _ints("floats", 512 << 10, 6),
+        "tiny": b"abc",
+        "empty": b"",
+        "mixed": b"".join([_data("text", 5000, 7), _data("random", 3000, 8)] * 40),
+        "big": _data("text", 1 << 20, 9) + _ints("uniform", 1 << 20, 10),
+    }
+
+
+@pytest.mark.parametrize("level", [-5, 1, 3, 9, 19])
+def test_zstd_host_matches_pyarrow(level):
+    """The zstd kernel's phases (run lane by lane on the CPU) decode
+    pyarrow's zstd frames at fast, default and high levels: raw / RLE /
+    compressed blocks, raw / RLE / Huffman literals (1 and 4 streams, FSE
+    and direct weights, treeless), predefined / RLE / FSE / repeat sequence
+    tables, repeat offsets, multi-block frames."""
+    pa = pytest.importorskip("pyarrow")
+    codec = pa.Codec("zstd", compression_level=level)
+    for kind, d in _zstd_payloads().items():
+        st, out = D.zstd_host(D.ZSTD, codec.compress(d, asbytes=True), len(d))
+        assert st == len(d) and out == d, (kind, st)
+
+
+def test_zstd_arrow_buffers_and_frames():
+    pa = pytest.importorskip("pyarrow")
+    d = _ints("uniform", 512 << 10, 12)
+    frame = pa.Codec("zstd").compress(d, asbytes=True)
+    buf = D.arrow_zstd_buffer(d, frame)
+    assert D.zstd_host(D.ARROW_ZSTD, buf, len(d)) == (len(d), d)
+    # stored (-1) buffer, wrong length prefix
+    raw = b"\xff" * 8 + d[:5000]
+    assert D.zstd_host(D.ARROW_ZSTD, raw, 5000) == (5000, d[:5000])
+    bad = struct.pack("<q", len(d) - 8) + frame
+    assert D.zstd_host(D.ARROW_ZSTD, bad, len(d))[0] < 0
+    # two frames with a skippable frame between them
+    a, b = _data("text", 70000, 13), _data("runs", 90000, 14)
+    skip = struct.pack("<II", 0x184D2A53, 5) + b"12345"
+    two = pa.Codec("zstd").compress(a, asbytes=True) + skip + pa.Codec("zstd", compression_level=7).compress(b, asbytes=True)
+    assert D.zstd_host(D.ZSTD, two, len(a) + len(b)) == (len(a) + len(b), a + b)
+
+
+def test_zstd_errors_are_bounded():
+    pa = pytest.importorskip("pyarrow")
+    d = _data("text", 200000, 15)
+    c = pa.Codec("zstd").compress(d, asbytes=True)
+    assert D.zstd_host(D.ZSTD, c, len(d) - 1)[0] == -2          # overflow
+    assert D.zstd_host(D.ZSTD, c[: len(c) // 2], len(d))[0] < 0  # truncated
+    # a dictionary id is refused (Arrow writes none)
+    hdr = bytes([0x28, 0xB5, 0x2F, 0xFD, 0x21, 0x07]) + b"\x01\x00\x00"
+    assert D.zstd_host(D.ZSTD, hdr, 100)[0] == -4
+    # mutated frames never read or write out of range (the GPU kernel
+    # runs the same checks); ASan coverage: csrc/tests/zstd_fuzz.cc
+    rng = np.random.default_rng(16)
+    base = bytearray(c)
+    for i in range(200):
+        m = bytearray(base)
+        for _ in range(int(rng.integers(1, 6))):
+            m[int(rng.integers(4, len(m)))] = int(rng.integers(0, 256))
+        st, out = D.zstd_host(D.ZSTD, bytes(m), len(d))
+        assert st <= len(d)
+
+
+def test_zstd_fuzz_asan(tmp_path):
+    """8k random edits / truncations of real zstd frames through the
+    decoder's phases built host-only with ASan + UBSan
+    (csrc/tests/zstd_fuzz.cc): seeds decode exactly, mutants end in a
+    clean status, never an out-of-range access."""
+    pa = pytest.importorskip("pyarrow")
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "build/zstd_fuzz"], cwd=root, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    args = []
+    seeds = [(1, _ints("uniform", 160000, 1)), (3, _data("text", 150000, 2)),
+             (19, _ints("sorted", 240000, 3)), (-3, _ints("floats", 40000, 4))]
+    for i, (lvl, d) in enumerate(seeds):
+        z = pa.Codec("zstd", compression_level=lvl).compress(d, asbytes=True)
+        (tmp_path / f"{i}.zst").write_bytes(z)
+        (tmp_path / f"{i}.raw").write_bytes(d)
+        args += [str(tmp_path / f"{i}.zst"), str(tmp_path / f"{i}.raw")]
+    r = subprocess.run([os.path.join(root, "build", "zstd_fuzz"), "2000"] + args,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "4 seeds ok" in r.stdout

@@ -203,6 +203,62 @@ def test_malformed_streams_report_errors(dev, monkeypatch, g):
     assert (st < 0).all()
 
 
+# ---------------------------------------------------------------------- zstd
+@pytest.mark.parametrize("level", [-5, 1, 3, 19])
+def test_zstd_from_pyarrow(dev, level):
+    """zstd.hip (one wavefront per stream) == the input, for pyarrow's zstd
+    frames of every payload kind in one launch."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd.ops import decompress as D
+    codec = pa.Codec("zstd", compression_level=level)
+    pays = _payloads()
+    comp = [codec.compress(p, asbytes=True) for p in pays]
+    st, outs = _run(D.ZSTD, comp, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
+def test_zstd_persistent_slots_and_arrow(dev):
+    """More streams than scratch slots (each workgroup loops over streams
+    and reuses its literal slot), Arrow IPC buffers incl. a stored one, and
+    malformed streams reported without touching memory out of range."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd import _native as N
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(21)
+    pays = [rng.integers(0, 1_000_000, int(n), dtype=np.int64).tobytes()
+            for n in rng.integers(1000, 70000, 40)]
+    bufs = [D.arrow_zstd_buffer(p, pa.Codec("zstd").compress(p, asbytes=True)) for p in pays]
+    bufs[3] = b"\xff" * 8 + pays[3]
+    good = len(bufs)
+    junk = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (10, 1000, 5000)]
+    trunc = bufs[0][: len(bufs[0]) // 2]
+    streams = bufs + junk + [trunc]
+    sizes = [len(p) for p in pays] + [4096] * 3 + [len(pays[0])]
+    src = b"".join(streams)
+    offs = np.cumsum([0] + [len(x) for x in streams])[:-1]
+    doffs = np.cumsum([0] + sizes)[:-1]
+    descs = D.make_descs([(int(o), len(x), int(do), n) for o, x, do, n in zip(offs, streams, doffs, sizes)])
+    d_src = _t(src + b"\0", dev)
+    dst = torch.zeros(sum(sizes) + 64, dtype=torch.uint8, device=dev)
+    guard = dst[sum(sizes):]
+    d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+    status = torch.empty(len(streams), dtype=torch.int32, device=dev)
+    scratch = torch.empty(3 * (128 << 10), dtype=torch.uint8, device=dev)   # 3 slots
+    rc = N.lib().strom_decompress_zstd(D.ARROW_ZSTD, d_src.data_ptr(), dst.data_ptr(),
+                                        d_desc.data_ptr(), len(streams), status.data_ptr(),
+                                        scratch.data_ptr(), scratch.numel(), None)
+    assert rc == 0
+    st = status.cpu().numpy()
+    out = dst.cpu().numpy().tobytes()
+    assert list(st[:good]) == sizes[:good]
+    for p, do in zip(pays, doffs[:good]):
+        assert out[int(do):int(do) + len(p)] == p
+    assert (st[good:] < 0).all() or (st[good:] <= np.array(sizes[good:])).all()
+    assert st[-1] < 0
+    assert int(guard.count_nonzero()) == 0
+
+
 # -------------------------------------------------------------- column filter
 @pytest.mark.parametrize("dtype", [torch.int32, torch.int64, torch.float32, torch.float64])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 255 * 64 + 7, 1_000_003])

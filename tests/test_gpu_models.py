@@ -61,7 +61,8 @@ def test_pg_relation_scan_resumable_gpu(S, tmp_path):
     assert np.array_equal(r.items, full.items) and r.pages == rel.nblocks and r.bad_pages == 0
 
 
-def test_arrow_scan_lz4(S, tmp_path):
+@pytest.mark.parametrize("codecs", [("lz4", None), ("zstd",)])
+def test_arrow_scan(S, tmp_path, codecs):
     pa = pytest.importorskip("pyarrow")
     import pyarrow.ipc as ipc
     from nvme_strom_amd.models.arrow_scan import ArrowScan
@@ -74,7 +75,7 @@ def test_arrow_scan_lz4(S, tmp_path):
                     "b": pa.array(b, type=pa.float64(), mask=mask),
                     "s": pa.array([str(x % 100) for x in range(n * nb)])})
     path = str(tmp_path / "t.arrow")
-    for comp in ("lz4", None):
+    for comp in codecs:
         with ipc.new_file(path, tbl.schema, options=ipc.IpcWriteOptions(compression=comp)) as w:
             for k in range(nb):
                 w.write_batch(tbl.slice(k * n, n).to_batches()[0])

@@ -4,6 +4,7 @@
 # Phases (each under its own time limit; the first failure ends the call):
 #   tests      pytest -m gpu (one process)
 #   ktests     GPU kernel numerics only (crc/heap/decoder/filter tests)
+#   ztests     zstd decoder numerics only
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (default flagship config)
 #   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
@@ -41,6 +42,8 @@ for phase in "$@"; do
     tests) step tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     ktests) step ktests 300 python -u -m pytest tests/test_gpu_core.py tests/test_gpu_kernels.py -m gpu -x -q \
               --timeout 120 --timeout-method thread -k "crc or heap or lz4 or snappy or malformed or filter or compact" ;;
+    ztests) step ztests 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -v \
+              --timeout 120 --timeout-method thread -k zstd ;;
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
