@@ -35,6 +35,7 @@
 // the optional content checksum is skipped, not verified.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -43,7 +44,9 @@
 
 #include "strom/strom.h"
 
-#define HD __host__ __device__ inline
+// everything inlines into the kernel: an outlined phase would reach LDS
+// through generic pointers
+#define HD __host__ __device__ inline __attribute__((always_inline))
 
 // host debug builds (-DZS_DEBUG): report the line of the first failed check
 #if defined(ZS_DEBUG) && !defined(__HIP_DEVICE_COMPILE__)
@@ -95,9 +98,9 @@ struct BR {
   uint32_t pad;
 };
 
-struct Win {                 // an LDS copy of input bytes [lo, lo + n)
-  const uint8_t *lds;
-  uint32_t lo, n;
+struct Win {                 // an LDS copy of input bytes [lo, lo + n) at
+  uint32_t off;              // byte offset off of Smem (an offset, not a pointer:
+  uint32_t lo, n;            // reads through &s keep the LDS address space)
 };
 
 struct Ctx {
@@ -118,8 +121,8 @@ struct Smem {
   uint32_t lst[SEQN + 1];    //   literal index of its first literal
   uint32_t sll[SEQN + 1];    //   literal length
   uint32_t soff[SEQN + 1];   //   match offset
-  uint8_t swin[SWIN];
-  uint8_t lwin[4][LWIN];
+  alignas(4) uint8_t swin[SWIN];
+  alignas(4) uint8_t lwin[4][LWIN];
   int16_t norm[64];
   uint16_t snext[64];
   uint8_t hw[256];           // Huffman weights
@@ -197,9 +200,11 @@ HD void code_base(uint32_t kind, uint32_t c, uint32_t &base, uint32_t &add) {
 // ------------------------------------------------------------- input
 HD uint32_t gbyte(const Ctx &c, uint32_t p) { return p < c.len ? c.in[p] : 0u; }
 
-HD uint32_t wbyte(const Win &w, const Ctx &c, uint32_t p) {
+HD const uint8_t *sbytes(const Smem &s) { return (const uint8_t *)&s; }
+
+HD uint32_t wbyte(const Smem &s, const Win &w, const Ctx &c, uint32_t p) {
   const uint32_t r = p - w.lo;
-  return r < w.n ? w.lds[r] : gbyte(c, p);
+  return r < w.n ? sbytes(s)[w.off + r] : gbyte(c, p);
 }
 
 HD uint32_t rd16(const Ctx &c, uint32_t p) { return gbyte(c, p) | (gbyte(c, p + 1) << 8); }
@@ -219,21 +224,31 @@ HD bool br_init(BR &b, const Ctx &c, uint32_t beg, uint32_t len) {
   return true;
 }
 
-HD void br_fill(BR &b, const Win &w, const Ctx &c) {
+HD void br_fill(BR &b, const Smem &s, const Win &w, const Ctx &c) {
   const int32_t nb = b.nbits > 0 ? b.nbits : 0;
   int32_t base = nb - 57;
   base = base > 0 ? (base + 7) & ~7 : 0;    // >= 50 readable bits after a fill
   const uint32_t p = b.beg + (uint32_t)(base >> 3);
+  const uint32_t r = p - w.lo;
   uint64_t v = 0;
-  for (uint32_t j = 0; j < 8; ++j) v |= (uint64_t)wbyte(w, c, p + j) << (8 * j);
+  if (r + 12 <= w.n) {
+    // inside the LDS window: three aligned dwords and a funnel shift
+    // (windows start 4-byte aligned in Smem)
+    const uint32_t *d = (const uint32_t *)(sbytes(s) + w.off + (r & ~3u));
+    const uint64_t lo = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
+    const uint32_t sh = 8 * (r & 3);
+    v = sh ? (lo >> sh) | ((uint64_t)d[2] << (64 - sh)) : lo;
+  } else {
+    for (uint32_t j = 0; j < 8; ++j) v |= (uint64_t)wbyte(s, w, c, p + j) << (8 * j);
+  }
   b.cont = v;
   b.cbase = base;
 }
 
 // the next k (<= 32) bits without consuming them; past the stream start
 // the bits read as zeros (the caller sees nbits < 0 afterwards)
-HD uint32_t br_peek(BR &b, const Win &w, const Ctx &c, uint32_t k) {
-  if (b.nbits - (int32_t)k < b.cbase && b.cbase != 0) br_fill(b, w, c);
+HD uint32_t br_peek(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k) {
+  if (b.nbits - (int32_t)k < b.cbase && b.cbase != 0) br_fill(b, s, w, c);
   const int32_t lo = b.nbits - (int32_t)k - b.cbase;
   const uint64_t m = (1ull << k) - 1;
   if (lo >= 0) return (uint32_t)((b.cont >> lo) & m);
@@ -241,9 +256,9 @@ HD uint32_t br_peek(BR &b, const Win &w, const Ctx &c, uint32_t k) {
   return (uint32_t)((b.cont << (-lo)) & m);
 }
 
-HD uint32_t br_read(BR &b, const Win &w, const Ctx &c, uint32_t k) {
+HD uint32_t br_read(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k) {
   if (k == 0) return 0;
-  const uint32_t v = br_peek(b, w, c, k);
+  const uint32_t v = br_peek(b, s, w, c, k);
   b.nbits -= (int32_t)k;
   return v;
 }
@@ -392,22 +407,22 @@ HD bool huf_weights(Smem &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &u
   const uint32_t bp = f.p + (f.bit >> 3);
   BR b;
   if (bp >= f.end || !br_init(b, c, bp, f.end - bp)) return ZF(false);
-  const Win w{nullptr, 0, 0};
-  uint32_t s1 = br_read(b, w, c, al), s2 = br_read(b, w, c, al);
+  const Win w{0, 0, 0};
+  uint32_t s1 = br_read(b, s, w, c, al), s2 = br_read(b, s, w, c, al);
   uint32_t n = 0;
   // two interleaved states until the stream is over-read; then the other
   // state's symbol is the last weight (RFC 8878 4.2.1.2)
   for (;;) {
     if (n + 2 > 255) return ZF(false);
     s.hw[n++] = (uint8_t)wt[s1].base;
-    s1 = wt[s1].next + br_read(b, w, c, wt[s1].nb);
+    s1 = wt[s1].next + br_read(b, s, w, c, wt[s1].nb);
     if (b.nbits < 0) {
       s.hw[n++] = (uint8_t)wt[s2].base;
       break;
     }
     if (n + 2 > 255) return ZF(false);
     s.hw[n++] = (uint8_t)wt[s2].base;
-    s2 = wt[s2].next + br_read(b, w, c, wt[s2].nb);
+    s2 = wt[s2].next + br_read(b, s, w, c, wt[s2].nb);
     if (b.nbits < 0) {
       s.hw[n++] = (uint8_t)wt[s1].base;
       break;
@@ -663,12 +678,12 @@ HD bool lit_header(Smem &s, const Ctx &c) {
     d += 6;
     const uint32_t tot = dend - d;
     if (l1 + l2 + l3 >= tot) return ZF(false);
-    const uint32_t len[4] = {l1, l2, l3, tot - l1 - l2 - l3};
     const uint32_t seg = (R + 3) / 4;
     if (3 * seg > R) return ZF(false);
     for (uint32_t j = 0; j < 4; ++j) {
-      if (!br_init(s.lbr[j], c, d, len[j])) return ZF(false);
-      d += len[j];
+      const uint32_t lj = j == 0 ? l1 : j == 1 ? l2 : j == 2 ? l3 : tot - l1 - l2 - l3;
+      if (!br_init(s.lbr[j], c, d, lj)) return ZF(false);
+      d += lj;
       s.lout[j] = j * seg;
       s.lcnt[j] = j < 3 ? seg : R - 3 * seg;
     }
@@ -733,10 +748,10 @@ HD bool seq_header(Smem &s, const Ctx &c) {
       !seq_table(s, c, (modes >> 2) & 3, kML, p, end, s.tml, s.al_ml, s.have_ml))
     return ZF(false);
   if (p >= end || !br_init(s.sbr, c, p, end - p)) return ZF(false);
-  const Win w{nullptr, 0, 0};
-  s.st_ll = br_read(s.sbr, w, c, s.al_ll);
-  s.st_of = br_read(s.sbr, w, c, s.al_of);
-  s.st_ml = br_read(s.sbr, w, c, s.al_ml);
+  const Win w{0, 0, 0};
+  s.st_ll = br_read(s.sbr, s, w, c, s.al_ll);
+  s.st_of = br_read(s.sbr, s, w, c, s.al_of);
+  s.st_ml = br_read(s.sbr, s, w, c, s.al_ml);
   s.nseq = n;
   s.seq_done = 0;
   return s.sbr.nbits >= 0 ? true : ZF(false);
@@ -768,11 +783,11 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
   const uint32_t left = s.lcnt[j];
   if (!left) return;
   BR b = s.lbr[j];
-  const Win w{s.lwin[j], s.lwlo[j], LWIN};
+  const Win w{(uint32_t)offsetof(Smem, lwin) + j * LWIN, s.lwlo[j], LWIN};
   const uint32_t n = left < LSYM ? left : LSYM, mb = s.hbits;
   const uint32_t o = s.lout[j];
   for (uint32_t k = 0; k < n; ++k) {
-    const uint32_t e = s.huf[br_peek(b, w, c, mb)];
+    const uint32_t e = s.huf[br_peek(b, s, w, c, mb)];
     b.nbits -= (int32_t)(e & 15);
     c.lit[o + k] = (uint8_t)(e >> 4);
   }
@@ -798,16 +813,16 @@ HD void seq_chunk(Smem &s, const Ctx &c) {
   const uint32_t left = s.nseq - s.seq_done;
   const uint32_t m = left < SEQN ? left : SEQN;
   BR b = s.sbr;
-  const Win w{s.swin, s.swlo, SWIN};
+  const Win w{(uint32_t)offsetof(Smem, swin), s.swlo, SWIN};
   uint32_t sll = s.st_ll, sof = s.st_of, sml = s.st_ml;
   uint32_t r0 = s.rep[0], r1 = s.rep[1], r2 = s.rep[2];
   const uint32_t pos0 = s.op - s.fstart;    // frame output before this chunk
   uint32_t n = 0, out = 0, lit = s.lit_used;
   for (uint32_t i = 0; i < m; ++i) {
     const SeqEnt eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
-    const uint32_t ofv = eo.base + br_read(b, w, c, eo.add);
-    const uint32_t ml = em.base + br_read(b, w, c, em.add);
-    const uint32_t ll = el.base + br_read(b, w, c, el.add);
+    const uint32_t ofv = eo.base + br_read(b, s, w, c, eo.add);
+    const uint32_t ml = em.base + br_read(b, s, w, c, em.add);
+    const uint32_t ll = el.base + br_read(b, s, w, c, el.add);
     uint32_t off;
     if (ofv > 3) {
       off = ofv - 3;
@@ -830,9 +845,9 @@ HD void seq_chunk(Smem &s, const Ctx &c) {
       }
     }
     if (s.seq_done + i + 1 < s.nseq) {
-      sll = el.next + br_read(b, w, c, el.nb);
-      sml = em.next + br_read(b, w, c, em.nb);
-      sof = eo.next + br_read(b, w, c, eo.nb);
+      sll = el.next + br_read(b, s, w, c, el.nb);
+      sml = em.next + br_read(b, s, w, c, em.nb);
+      sof = eo.next + br_read(b, s, w, c, eo.nb);
     }
     if (lit + ll > s.lit_n) {
       s.err = ZF(kErrFormat);
@@ -1053,17 +1068,18 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
   tm.sync();
 }
 
+#define DI __device__ inline __attribute__((always_inline))
 struct DevTeam {
-  __device__ void sync() { __syncthreads(); }
-  __device__ void fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+  DI void sync() { __syncthreads(); }
+  DI void fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
   template <class F>
-  __device__ void each(F f) { f(threadIdx.x); }
+  DI void each(F f) { f(threadIdx.x); }
   template <class F>
-  __device__ void one(F f) {
+  DI void one(F f) {
     if (threadIdx.x == 0) f();
   }
   template <class F>
-  __device__ bool any(F f) { return __syncthreads_or(f(threadIdx.x)); }
+  DI bool any(F f) { return __syncthreads_or(f(threadIdx.x)); }
 };
 
 struct HostTeam {

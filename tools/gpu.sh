@@ -5,6 +5,9 @@
 #   tests      pytest -m gpu (one process)
 #   ktests     GPU kernel numerics only (crc/heap/decoder/filter tests)
 #   ztests     zstd decoder numerics only
+#   zbench     zstd decoder GB/s by column kind / level / stream count (+ LZ4 rows)
+#   zarrow     config-5 Arrow scan of a ZSTD-written file
+#   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (default flagship config)
 #   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
@@ -47,6 +50,10 @@ for phase in "$@"; do
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
+    zbench) step zbench 300 python -u -m nvme_strom_amd.tools.zstd_bench --out "$OUT/zstd.json" ;;
+    zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
+    ztrace) (cd /tmp && step ztrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ztrace" -o trace \
+              -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds val,x --levels 1 --streams 2048 --no-lz4) ;;
     par) step par 300 python -u -m nvme_strom_amd.tools.kbench --only par --out "$OUT/par.json" ;;
     dtests) step dtests 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q \
               --timeout 120 --timeout-method thread -k "lz4 or snappy or malformed or geometr" ;;
