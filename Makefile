@@ -19,7 +19,8 @@ ENGINE_OBJ := $(patsubst csrc/engine/%.cc,$(OBJ)/engine/%.o,$(ENGINE_SRC))
 KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
-all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so
+all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so \
+     $(OUT)/libstrom_zstdprof.so
 
 tools: $(TOOLS)
 
@@ -44,6 +45,11 @@ $(OUT)/libstrom_decprof.so: csrc/kernels/decompress.hip csrc/kernels/lz4par.hip 
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -DSTROM_DECOMP_PROF -shared -o $@ csrc/kernels/decompress.hip csrc/kernels/lz4par.hip
 
+# the zstd decoder with its phase profile compiled in (tools/zstd_bench.py --prof)
+$(OUT)/libstrom_zstdprof.so: csrc/kernels/zstd.hip csrc/include/strom/strom.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -DZS_PROF -shared -o $@ $<
+
 # a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
 # make ab AB=name [SRC=path/to/decompress.hip]
 SRC ?= csrc/kernels/decompress.hip
@@ -57,7 +63,8 @@ $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 	$(HIPCC) $(HIPFLAGS) -x hip -o $@ $< -L$(OUT) -lstrom -Wl,-rpath,'$$ORIGIN' -lpthread
 
 clean:
-	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so $(TOOLS)
+	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so \
+	  $(OUT)/libstrom_zstdprof.so $(TOOLS)
 
 .PHONY: all tools clean ab
 

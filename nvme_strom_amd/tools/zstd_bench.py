@@ -52,6 +52,33 @@ def frames(kind: str, k: int, codec: str, level: int, seed: int = 1):
     return raws, bufs
 
 
+PHASES = ("hdr", "copy", "lit_load", "lit_dec", "seq_load", "seq_dec", "fill", "double", "write")
+COUNTS = ("chunks", "batches", "double_rounds", "lit_rounds")
+
+
+def prof(cid, n, src, dst, d_desc, status) -> dict:
+    """One launch of the profiled build (libstrom_zstdprof.so): share of
+    lane-0 cycles per phase, cycles and events per stream."""
+    import ctypes as C
+    import os
+    from nvme_strom_amd.ops._util import ptr
+    lib = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib",
+                              "libstrom_zstdprof.so"))
+    out = np.zeros(len(PHASES) + len(COUNTS), dtype=np.uint64)
+    lib.strom_zstd_prof(out.ctypes.data_as(C.c_void_p))             # zero
+    rc = lib.strom_decompress_zstd(cid, C.c_void_p(ptr(src)), C.c_void_p(ptr(dst)),
+                                   C.c_void_p(ptr(d_desc)), C.c_uint32(n),
+                                   C.c_void_p(ptr(status)), None, C.c_uint64(0), None)
+    assert rc == 0
+    lib.strom_zstd_prof(out.ctypes.data_as(C.c_void_p))
+    cyc = out[:len(PHASES)].astype(np.float64)
+    tot = cyc.sum()
+    res = {p: round(float(c / tot), 3) for p, c in zip(PHASES, cyc)}
+    res.update({k: round(float(v) / n, 2) for k, v in zip(COUNTS, out[len(PHASES):])})
+    res["cycles_per_stream"] = round(float(tot) / n)
+    return res
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--kinds", default="val,ids,x,text")
@@ -61,6 +88,8 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--no-lz4", dest="lz4", action="store_false",
                     help="skip the LZ4 rows of the same columns")
+    ap.add_argument("--prof", action="store_true",
+                    help="phase cycle profile of each zstd row (libstrom_zstdprof.so)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -112,6 +141,8 @@ def main(argv=None) -> int:
                            streams=n, bytes=n * rawlen, ratio=round(ratio, 3),
                            GBps=round(n * rawlen / med / 1e9, 2), ms=round(med * 1e3, 3),
                            verified=ok)
+                if a.prof and codec == "zstd":
+                    row["phases"] = prof(cid, n, src, dst, d_desc, status)
                 _log(json.dumps(row))
                 res["rows"].append(row)
                 del dst

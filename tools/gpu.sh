@@ -6,6 +6,7 @@
 #   ktests     GPU kernel numerics only (crc/heap/decoder/filter tests)
 #   ztests     zstd decoder numerics only
 #   zbench     zstd decoder GB/s by column kind / level / stream count (+ LZ4 rows)
+#   zprof      zstd decoder phase profile (libstrom_zstdprof.so) by column kind
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
 #   smoke      __graft_entry__.smoke()
@@ -51,6 +52,7 @@ for phase in "$@"; do
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
     zbench) step zbench 300 python -u -m nvme_strom_amd.tools.zstd_bench --out "$OUT/zstd.json" ;;
+    zprof) step zprof 300 python -u -m nvme_strom_amd.tools.zstd_bench --prof --no-lz4 --streams ${ZSTREAMS:-2048} --out "$OUT/zprof.json" ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
     ztrace) (cd /tmp && step ztrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ztrace" -o trace \
               -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds val,x --levels 1 --streams 2048 --no-lz4) ;;
