@@ -86,8 +86,10 @@ enum : uint32_t { kLL = 0, kOF = 1, kML = 2, kPlain = 3 };
 enum { kZpHdr, kZpCopy, kZpLitLoad, kZpLitDec, kZpSeqLoad, kZpSeqDec, kZpFill, kZpDouble,
        kZpWrite, kZpNChunk, kZpNBatch, kZpNDouble, kZpNLitRound, kZpN };
 
-// FSE decoding entry with the code's baseline and extra bits folded in
-// (kPlain: base = symbol)
+// FSE decoding entry (8 bytes): the state's code folded into baseline +
+// extra bits (for Huffman weights: base = the weight), its bit count and
+// the next state's base — the wave-uniform sequence loop is bound by
+// scalar issue, so per-sequence arithmetic is traded for LDS
 struct SeqEnt {
   uint32_t base;
   uint16_t next;
@@ -130,13 +132,14 @@ struct Smem {
   uint32_t soff[SEQN + 1];   //   match offset
   alignas(4) uint8_t swin[SWIN];
   alignas(4) uint8_t lwin[4][LWIN];
+  uint8_t lstage[4 * LSYM];  // a round's decoded literals, copied out coalesced
   int16_t norm[64];
   uint16_t snext[64];
   uint8_t hw[256];           // Huffman weights
   uint32_t wrank[16];
   BR lbr[4];
   BR sbr;
-  uint32_t lcnt[4], lout[4], lwlo[4];
+  uint32_t lcnt[4], lout[4], lwlo[4], lrn[4];
   uint32_t swlo;
   // stream / frame / block scalars (lane 0 writes, all read after a barrier)
   uint32_t ip, op, fstart, fcs_set, fcs, cksum, state;
@@ -167,37 +170,29 @@ ZTAB int8_t kNormOF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                            1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
 // baseline + extra bits of a literal-length / match-length / offset code
+// (RFC 8878 3.1.1.3.2.1.1): arithmetic plus packed constants, no tables
+// (it runs once per code in the wave-uniform sequence loop)
 HD void code_base(uint32_t kind, uint32_t c, uint32_t &base, uint32_t &add) {
   if (kind == kOF) {
     add = c;
     base = 1u << c;
   } else if (kind == kLL) {
-    if (c < 16) {
-      base = c;
-      add = 0;
-    } else if (c >= 25) {
-      add = c - 19;
-      base = 1u << add;
-    } else {
-      // 16..24: 16/1 18/1 20/1 22/1 24/2 28/2 32/3 40/3 48/4
-      const uint32_t i = c - 16;
-      add = i < 4 ? 1 : i < 6 ? 2 : i < 8 ? 3 : 4;
-      base = i < 4 ? 16 + 2 * i : i < 6 ? 24 + 4 * (i - 4) : i < 8 ? 32 + 8 * (i - 6) : 48;
-    }
+    // 16..24: 16/1 18/1 20/1 22/1 24/2 28/2 32/3 40/3 48/4
+    const uint32_t i = c - 16;
+    const uint32_t mid_add = (uint32_t)(0x433221111ull >> (4 * (i & 15))) & 15;
+    const uint64_t b0 = 0x28201C1816141210ull;   // bases of 16..23, one byte each
+    const uint32_t mid_base = i < 8 ? (uint32_t)(b0 >> (8 * i)) & 255 : 48;
+    add = c < 16 ? 0 : c >= 25 ? c - 19 : mid_add;
+    base = c < 16 ? c : c >= 25 ? 1u << (c - 19) : mid_base;
   } else if (kind == kML) {
-    if (c < 32) {
-      base = c + 3;
-      add = 0;
-    } else if (c >= 43) {
-      add = c - 36;
-      base = (1u << add) + 3;
-    } else {
-      // 32..42: 35/1 37/1 39/1 41/1 43/2 47/2 51/3 59/3 67/4 83/4 99/5
-      const uint32_t i = c - 32;
-      add = i < 4 ? 1 : i < 6 ? 2 : i < 8 ? 3 : i < 10 ? 4 : 5;
-      base = i < 4 ? 35 + 2 * i : i < 6 ? 43 + 4 * (i - 4) : i < 8 ? 51 + 8 * (i - 6)
-           : i < 10 ? 67 + 16 * (i - 8) : 99;
-    }
+    // 32..42: 35/1 37/1 39/1 41/1 43/2 47/2 51/3 59/3 67/4 83/4 99/5
+    const uint32_t i = c - 32;
+    const uint32_t mid_add = (uint32_t)(0x54433221111ull >> (4 * (i & 15))) & 15;
+    const uint64_t b0 = 0x3B332F2B29272523ull;   // bases of 32..39
+    const uint32_t b1 = 0x00635343u;              // bases of 40..42
+    const uint32_t mid_base = i < 8 ? (uint32_t)(b0 >> (8 * i)) & 255 : (b1 >> (8 * ((i - 8) & 3))) & 255;
+    add = c < 32 ? 0 : c >= 43 ? c - 36 : mid_add;
+    base = c < 32 ? c + 3 : c >= 43 ? (1u << (c - 36)) + 3 : mid_base;
   } else {
     base = c;
     add = 0;
@@ -301,7 +296,13 @@ HD uint32_t br_look(const BR &b, uint32_t k) {   // after br_need(>= k); k = 0 g
   return (uint32_t)((b.cont >> lo) & ((1ull << k) - 1));
 }
 
-HD uint32_t br_get(BR &b, uint32_t k) {
+HD uint64_t br_get64(BR &b, uint32_t k) {        // k <= 56, after br_need(>= k)
+  const uint32_t lo = (uint32_t)(b.nbits - (int32_t)k - b.cbase) & 63;
+  b.nbits -= (int32_t)k;
+  return (b.cont >> lo) & ((1ull << k) - 1);
+}
+
+[[maybe_unused]] HD uint32_t br_get(BR &b, uint32_t k) {
   const uint32_t v = br_look(b, k);
   b.nbits -= (int32_t)k;
   return v;
@@ -668,7 +669,7 @@ HD bool lit_header(Smem &s, const Ctx &c) {
   const uint32_t p = s.ip, end = s.bend;
   const uint32_t b0 = gbyte(c, p), type = b0 & 3, sf = (b0 >> 2) & 3;
   s.lit_used = 0;
-  for (uint32_t j = 0; j < 4; ++j) s.lcnt[j] = 0;
+  for (uint32_t j = 0; j < 4; ++j) s.lcnt[j] = s.lrn[j] = 0;
   if (type <= 1) {
     uint32_t R, hl;
     if ((sf & 1) == 0) {
@@ -831,17 +832,25 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
   BR b = s.lbr[j];
   const Win w{(uint32_t)offsetof(Smem, lwin) + j * LWIN, s.lwlo[j], LWIN};
   const uint32_t n = left < LSYM ? left : LSYM, mb = s.hbits;
-  const uint32_t o = s.lout[j];
+  uint8_t *stage = s.lstage + j * LSYM;
   for (uint32_t k = 0; k < n; ++k) {
     br_need(b, s, w, mb);
     const uint32_t e = s.huf[br_look(b, mb)];
     b.nbits -= (int32_t)(e & 15);
-    c.lit[o + k] = (uint8_t)(e >> 4);
+    stage[k] = (uint8_t)(e >> 4);
   }
-  s.lout[j] = o + n;
+  s.lrn[j] = n;
   s.lcnt[j] = left - n;
   s.lbr[j] = b;
   if (left == n && b.nbits != 0) s.err = ZF(kErrFormat);   // a stream ends exactly
+}
+
+// (1) the round's staged literals -> the scratch slot (lane-strided)
+HD void lit_flush(Smem &s, const Ctx &c, uint32_t t) {
+  for (uint32_t j = 0; j < s.nls; ++j) {
+    const uint32_t n = s.lrn[j], o = s.lout[j];
+    for (uint32_t i = t; i < n; i += NT) c.lit[o + i] = s.lstage[j * LSYM + i];
+  }
 }
 
 // (2) sequence window: lane t copies every NT-th byte
@@ -860,7 +869,6 @@ HD void seq_load(Smem &s, const Ctx &c, uint32_t t) {
 // scalar branches, no exec-mask juggling around a one-lane loop); lane 0
 // stores.
 HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
-  const bool w0 = t == 0;
   const uint32_t left = s.nseq - s.seq_done;
   const uint32_t m = left < SEQN ? left : SEQN;
   BR b = s.sbr;
@@ -871,13 +879,31 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lit_n = s.lit_n, last = s.nseq - s.seq_done;
   uint32_t n = 0, out = 0, lit = s.lit_used;
   int32_t err = 0;
+  // entry i's fields are held by lane i % NT (slot i / NT) and stored
+  // together after the loop: no one-lane branch inside it
+  constexpr uint32_t SL = SEQN / NT;
+  uint32_t h_ll[SL], h_off[SL], h_lst[SL], h_ost[SL];
+  for (uint32_t q = 0; q < SL; ++q) h_ll[q] = h_off[q] = h_lst[q] = h_ost[q] = 0;
   for (uint32_t i = 0; i < m; ++i) {
     const SeqEnt eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
-    br_need(b, s, w, 47);                  // offset (<= 31) + match length (<= 16) bits
-    const uint32_t ofv = eo.base + br_get(b, eo.add);
-    const uint32_t ml = em.base + br_get(b, em.add);
-    br_need(b, s, w, 42);                  // literal length (<= 16) + three states (<= 26)
-    const uint32_t ll = el.base + br_get(b, el.add);
+    // offset + match-length extra bits in one extraction (<= 47 bits)
+    br_need(b, s, w, 47);
+    const uint32_t na = eo.add + em.add;
+    const uint64_t x1 = br_get64(b, na);
+    const uint32_t ofv = eo.base + (uint32_t)(x1 >> em.add);
+    const uint32_t ml = em.base + ((uint32_t)x1 & ((1u << em.add) - 1));
+    // literal-length extra bits + the three state updates (<= 42 bits)
+    br_need(b, s, w, 42);
+    const bool more = i + 1 < last;
+    const uint32_t nst = more ? el.nb + em.nb + eo.nb : 0;
+    const uint64_t x2 = br_get64(b, el.add + nst);
+    const uint32_t ll = el.base + (uint32_t)(x2 >> nst);
+    if (more) {
+      const uint32_t y = (uint32_t)x2;      // ll state | ml state | of state, high to low
+      sof = eo.next + (y & ((1u << eo.nb) - 1));
+      sml = em.next + ((y >> eo.nb) & ((1u << em.nb) - 1));
+      sll = el.next + ((y >> (eo.nb + em.nb)) & ((1u << el.nb) - 1));
+    }
     uint32_t off;
     if (ofv > 3) {
       off = ofv - 3;
@@ -899,11 +925,6 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
         r0 = off;
       }
     }
-    if (i + 1 < last) {
-      sll = el.next + br_get(b, el.nb);
-      sml = em.next + br_get(b, em.nb);
-      sof = eo.next + br_get(b, eo.nb);
-    }
     if (lit + ll > lit_n) {
       err = ZF(kErrFormat);
       break;
@@ -916,16 +937,44 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       err = ZF(kErrFormat);
       break;
     }
-    if (w0) {
-      s.sll[n] = ll;
-      s.soff[n] = off;
-      s.lst[n] = lit;
-      s.ost[n] = out;
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t q = i / NT;
+    const bool mine = t == i % NT;
+    for (uint32_t z = 0; z < SL; ++z) {
+      const bool sel = mine && q == z;
+      h_ll[z] = sel ? ll : h_ll[z];
+      h_off[z] = sel ? off : h_off[z];
+      h_lst[z] = sel ? lit : h_lst[z];
+      h_ost[z] = sel ? out : h_ost[z];
     }
+#else
+    // the CPU runs the phase once (HostTeam::uni): it holds every entry
+    s.sll[n] = ll;
+    s.soff[n] = off;
+    s.lst[n] = lit;
+    s.ost[n] = out;
+#endif
     lit += ll;
     out += ll + ml;
     ++n;
   }
+#ifdef __HIP_DEVICE_COMPILE__
+  for (uint32_t z = 0; z < SL; ++z) {
+    const uint32_t e = z * NT + t;
+    if (e < n) {
+      s.sll[e] = h_ll[z];
+      s.soff[e] = h_off[z];
+      s.lst[e] = h_lst[z];
+      s.ost[e] = h_ost[z];
+    }
+  }
+#else
+  (void)h_ll;
+  (void)h_off;
+  (void)h_lst;
+  (void)h_ost;
+#endif
+  const bool w0 = t == 0;
   if (!err && m == last) {
     if (s.nseq && b.nbits != 0) err = ZF(kErrFormat);
     const uint32_t rest = lit_n - lit;
@@ -970,18 +1019,34 @@ HD uint32_t entry_of(const Smem &s, uint32_t pos) {
   return lo;
 }
 
-// (3a) source pointer of every byte of the batch [b0, b0 + nb)
+// (3a) source pointer of every byte of the batch [b0, b0 + nb): lane t
+// fills the EPT contiguous entries from t * EPT — one binary search for
+// the first, then a walk along the chunk entries (the write phase reads
+// the pointers strided, so its stores stay coalesced)
 HD void ex_fill(Smem &s, uint32_t t, uint32_t b0, uint32_t nb) {
-  const uint32_t abs0 = s.op;
+  const uint32_t abs0 = s.op, e0 = t * EPT;
+  if (e0 >= nb) return;
+  uint32_t i = entry_of(s, b0 + e0);
+  uint32_t start = s.ost[i], next = s.ost[i + 1];
+  uint32_t ll = s.sll[i], off = s.soff[i], lst = s.lst[i];
   for (uint32_t k = 0; k < EPT; ++k) {
-    const uint32_t e = k * NT + t;
+    const uint32_t e = e0 + k;
     if (e >= nb) break;
-    const uint32_t pos = b0 + e, i = entry_of(s, pos), r = pos - s.ost[i];
+    const uint32_t pos = b0 + e;
+    while (pos >= next) {                  // the next chunk entry (ost strictly increases)
+      ++i;
+      start = next;
+      next = s.ost[i + 1];
+      ll = s.sll[i];
+      off = s.soff[i];
+      lst = s.lst[i];
+    }
+    const uint32_t r = pos - start;
     uint32_t v;
-    if (r < s.sll[i]) {
-      v = kLit | (s.lst[i] + r);
+    if (r < ll) {
+      v = kLit | (lst + r);
     } else {
-      const uint32_t src = abs0 + pos - s.soff[i];
+      const uint32_t src = abs0 + pos - off;
       v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
     }
     s.ptr[e] = v;
@@ -1087,6 +1152,12 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
         tm.count(kZpNLitRound);
         tm.each([&](uint32_t t) {
           if (t < s.nls) lit_chunk(s, c, t);
+        });
+        tm.sync();
+        tm.each([&](uint32_t t) { lit_flush(s, c, t); });
+        tm.sync();
+        tm.each([&](uint32_t t) {
+          if (t < s.nls) s.lout[t] += s.lrn[t];
         });
         tm.sync();
         tm.mark(kZpLitDec);
