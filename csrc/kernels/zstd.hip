@@ -90,7 +90,7 @@ enum { kZpHdr, kZpCopy, kZpLitLoad, kZpLitDec, kZpSeqLoad, kZpSeqDec, kZpFill, k
 // extra bits (for Huffman weights: base = the weight), its bit count and
 // the next state's base — the wave-uniform sequence loop is bound by
 // scalar issue, so per-sequence arithmetic is traded for LDS
-struct SeqEnt {
+struct alignas(8) SeqEnt {   // one ds_read_b64 per lookup
   uint32_t base;
   uint16_t next;
   uint8_t nb;
