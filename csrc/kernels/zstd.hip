@@ -884,6 +884,10 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   constexpr uint32_t SL = SEQN / NT;
   uint32_t h_ll[SL], h_off[SL], h_lst[SL], h_ost[SL];
   for (uint32_t q = 0; q < SL; ++q) h_ll[q] = h_off[q] = h_lst[q] = h_ost[q] = 0;
+  // the loop body is branch-free but for the two container refills: the
+  // repeat-offset update is selects, the checks accumulate into flags that
+  // end the stream after the chunk (its entries are then never executed)
+  bool bad_fmt = false, bad_dist = false;
   for (uint32_t i = 0; i < m; ++i) {
     const SeqEnt eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
     // offset + match-length extra bits in one extraction (<= 47 bits)
@@ -898,45 +902,25 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     const uint32_t nst = more ? el.nb + em.nb + eo.nb : 0;
     const uint64_t x2 = br_get64(b, el.add + nst);
     const uint32_t ll = el.base + (uint32_t)(x2 >> nst);
-    if (more) {
-      const uint32_t y = (uint32_t)x2;      // ll state | ml state | of state, high to low
-      sof = eo.next + (y & ((1u << eo.nb) - 1));
-      sml = em.next + ((y >> eo.nb) & ((1u << em.nb) - 1));
-      sll = el.next + ((y >> (eo.nb + em.nb)) & ((1u << el.nb) - 1));
-    }
-    uint32_t off;
-    if (ofv > 3) {
-      off = ofv - 3;
-      r2 = r1;
-      r1 = r0;
-      r0 = off;
-    } else {
-      const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
-      if (k == 0) {
-        off = r0;
-      } else if (k == 1) {
-        off = r1;
-        r1 = r0;
-        r0 = off;
-      } else {
-        off = k == 2 ? r2 : r0 - 1;
-        r2 = r1;
-        r1 = r0;
-        r0 = off;
-      }
-    }
-    if (lit + ll > lit_n) {
-      err = ZF(kErrFormat);
-      break;
-    }
-    if (off == 0 || off > pos0 + out + ll) {
-      err = ZF(kErrDistance);
-      break;
-    }
-    if (out + ll + ml > MAXB) {
-      err = ZF(kErrFormat);
-      break;
-    }
+    const uint32_t y = (uint32_t)x2;        // ll state | ml state | of state, high to low
+    const uint32_t nof = eo.next + (y & ((1u << eo.nb) - 1));
+    const uint32_t nml = em.next + ((y >> eo.nb) & ((1u << em.nb) - 1));
+    const uint32_t nll = el.next + ((y >> (eo.nb + em.nb)) & ((1u << el.nb) - 1));
+    sof = more ? nof : sof;
+    sml = more ? nml : sml;
+    sll = more ? nll : sll;
+    // repeat offsets (RFC 8878 3.1.2.5): k = repeat index, shifted by one
+    // when the literal length is 0; k = 3 is "first repeat minus one"
+    const bool isnew = ofv > 3;
+    const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
+    const uint32_t rep = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r0 - 1;
+    const uint32_t off = isnew ? ofv - 3 : rep;
+    const bool shift1 = isnew || k >= 1, shift2 = isnew || k >= 2;
+    r2 = shift2 ? r1 : r2;
+    r1 = shift1 ? r0 : r1;
+    r0 = off;
+    bad_fmt |= lit + ll > lit_n;
+    bad_dist |= off == 0 || off > pos0 + out + ll;
 #ifdef __HIP_DEVICE_COMPILE__
     const uint32_t q = i / NT;
     const bool mine = t == i % NT;
@@ -958,6 +942,8 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     out += ll + ml;
     ++n;
   }
+  if (bad_fmt || out > MAXB) err = ZF(kErrFormat);
+  else if (bad_dist) err = ZF(kErrDistance);
 #ifdef __HIP_DEVICE_COMPILE__
   for (uint32_t z = 0; z < SL; ++z) {
     const uint32_t e = z * NT + t;
@@ -1070,18 +1056,12 @@ HD bool ex_double(Smem &s, uint32_t t, uint32_t nb) {
   return more;
 }
 
-HD uint8_t ld_stored(const uint8_t *base, uint32_t pos) {
-#ifdef __HIP_DEVICE_COMPILE__
-  // stored by this workgroup before the release fence + barrier that ended
-  // the phase; bypass L1 (it may hold an older copy of the line)
-  const uintptr_t a = (uintptr_t)(base + pos);
-  const uint32_t d = __hip_atomic_load((const uint32_t *)(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-  return (uint8_t)(d >> (8 * (a & 3)));
-#else
-  return base[pos];
-#endif
-}
+// A byte stored by this workgroup in an earlier phase: visible to a plain
+// load after the release fence + barrier that ended that phase — the
+// workgroup's waves share the CU's vector L1 (write-through), so no
+// L1-bypassing atomic is needed, and plain loads pipeline (EPT per lane in
+// flight instead of one atomic round trip each)
+HD uint8_t ld_stored(const uint8_t *base, uint32_t pos) { return base[pos]; }
 
 // (3c) gather + store
 HD void ex_write(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb) {
