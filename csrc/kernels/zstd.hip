@@ -64,7 +64,7 @@ namespace {
 
 constexpr uint32_t NT = 64;              // one wave per stream
 constexpr uint32_t SEQN = 128;           // sequences per decode chunk
-constexpr uint32_t OB = 1024;            // output bytes per resolve batch
+constexpr uint32_t OB = 512;             // output bytes per resolve batch
 constexpr uint32_t EPT = OB / NT;        // batch entries per lane (strided)
 constexpr uint32_t SWIN = 1536;          // sequence bitstream window: SEQN x <= 89 bits
 constexpr uint32_t LSYM = 256;           // literal symbols per stream per round
@@ -120,23 +120,42 @@ struct Ctx {
   uint32_t cap;              // output capacity
 };
 
+// Per-stream LDS, phase-shared so that more streams fit a CU (the decode is
+// latency-bound per stream: throughput follows the streams in flight).  A
+// block's Huffman table lives in the table area only during its literal
+// phase, its FSE tables during its sequence phase; treeless literals and
+// repeat-mode tables are rebuilt from the saved descriptions (their input
+// positions) instead of being kept.
 struct Smem {
-  SeqEnt tll[512];
-  SeqEnt tml[512];
-  SeqEnt tof[256];
-  uint16_t huf[2048];        // (symbol << 4) | code length, indexed by the next hbits bits
-  uint32_t ptr[OB];          // batch pointers (also the Huffman-weight FSE table)
-  uint32_t ost[SEQN + 2];    // chunk entry i: output start (relative to the chunk)
-  uint32_t lst[SEQN + 1];    //   literal index of its first literal
-  uint32_t sll[SEQN + 1];    //   literal length
-  uint32_t soff[SEQN + 1];   //   match offset
-  alignas(4) uint8_t swin[SWIN];
-  alignas(4) uint8_t lwin[4][LWIN];
-  uint8_t lstage[4 * LSYM];  // a round's decoded literals, copied out coalesced
-  int16_t norm[64];
-  uint16_t snext[64];
-  uint8_t hw[256];           // Huffman weights
-  uint32_t wrank[16];
+  union {
+    struct {
+      SeqEnt tll[512];
+      SeqEnt tml[512];
+      SeqEnt tof[256];
+    };
+    uint16_t huf[2048];      // (symbol << 4) | code length, indexed by the next hbits bits
+  };
+  union {
+    struct {                 // building a table (Huffman weights + FSE counts)
+      SeqEnt hwt[64];        //   the Huffman-weight FSE table
+      uint8_t hw[256];       //   Huffman weights
+      int16_t norm[64];
+      uint16_t snext[64];
+      uint32_t wrank[16];
+    };
+    struct {                 // literal phase
+      alignas(4) uint8_t lwin[4][LWIN];
+      uint8_t lstage[4 * LSYM];   // a round's decoded literals, copied out coalesced
+    };
+    struct {                 // sequence + execution phase
+      alignas(4) uint8_t swin[SWIN];
+      uint32_t ost[SEQN + 2];     // chunk entry i: output start (relative to the chunk)
+      uint32_t lst[SEQN + 1];     //   literal index of its first literal
+      uint32_t sll[SEQN + 1];     //   literal length
+      uint32_t soff[SEQN + 1];    //   match offset
+      uint32_t ptr[OB];           // batch pointers
+    };
+  };
   BR lbr[4];
   BR sbr;
   uint32_t lcnt[4], lout[4], lwlo[4], lrn[4];
@@ -148,6 +167,8 @@ struct Smem {
   uint32_t btype, bsize, bstart, bend, blast;
   uint32_t lit_kind, lit_base, lit_n, lit_used, lit_rle;
   uint32_t hbits, nls;
+  uint32_t hdesc, hdesc_end;           // the frame's last Huffman tree description
+  uint32_t tmode[3], tpos[3], tend[3]; // ... and LL / OF / ML table definitions
   uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
   uint32_t have_ll, have_of, have_ml;
   uint32_t cn, ctot;
@@ -447,7 +468,7 @@ HD bool huf_weights(Smem &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &u
   FR f{p + 1, p + 1 + hb, 0};
   uint32_t nsym, al;
   if (!fse_norm(c, f, s.norm, 12, 6, nsym, al)) return ZF(false);
-  SeqEnt *wt = (SeqEnt *)s.ptr;
+  SeqEnt *wt = s.hwt;
   if (!fse_build(wt, s.norm, nsym, al, kPlain, s.snext)) return ZF(false);
   const uint32_t bp = f.p + (f.bit >> 3);
   BR b;
@@ -708,9 +729,15 @@ HD bool lit_header(Smem &s, const Ctx &c) {
   if (type == 2) {
     uint32_t used, nw;
     if (!huf_weights(s, c, d, dend, used, nw) || !huf_build(s, nw)) return ZF(false);
+    s.hdesc = d;
+    s.hdesc_end = dend;
     d += used;
-  } else if (!s.hbits) {
-    return ZF(false);                  // treeless literals need an earlier table
+  } else {
+    // treeless: the frame's previous table, rebuilt from its description
+    // (the table area held this frame's FSE tables since)
+    uint32_t used, nw;
+    if (!s.hbits || !huf_weights(s, c, s.hdesc, s.hdesc_end, used, nw) || !huf_build(s, nw))
+      return ZF(false);
   }
   s.nls = sf == 0 ? 1 : 4;
   if (s.nls == 1) {
@@ -739,26 +766,39 @@ HD bool lit_header(Smem &s, const Ctx &c) {
   return true;
 }
 
+// One of the LL / OF / ML tables.  Every block with sequences builds all
+// three (its literal phase reused the table area); a repeat-mode table is
+// rebuilt from the frame's saved definition of that table.
 HD bool seq_table(Smem &s, const Ctx &c, uint32_t mode, uint32_t kind, uint32_t &p,
                   uint32_t end, SeqEnt *tab, uint32_t &al, uint32_t &have) {
   const uint32_t maxsym = kind == kLL ? 35 : kind == kML ? 52 : 31;
   const uint32_t maxal = kind == kOF ? 8 : 9;
-  if (mode == 0) {
+  const bool repeat = mode == 3;
+  if (repeat && !have) return ZF(false);
+  const uint32_t m = repeat ? s.tmode[kind] : mode;
+  const uint32_t q0 = repeat ? s.tpos[kind] : p;
+  const uint32_t qend = repeat ? s.tend[kind] : end;
+  uint32_t q = q0;
+  if (m == 0) {
     fse_predef(s, tab, kind, al);
-  } else if (mode == 1) {
-    if (p >= end) return ZF(false);
-    const uint32_t sym = gbyte(c, p++);
+  } else if (m == 1) {
+    if (q >= qend) return ZF(false);
+    const uint32_t sym = gbyte(c, q++);
     if (sym > maxsym) return ZF(false);
     fse_rle(tab, sym, kind);
     al = 0;
-  } else if (mode == 2) {
-    FR f{p, end, 0};
+  } else {
+    FR f{q, qend, 0};
     uint32_t nsym;
     if (!fse_norm(c, f, s.norm, maxsym, maxal, nsym, al)) return ZF(false);
     if (!fse_build(tab, s.norm, nsym, al, kind, s.snext)) return ZF(false);
-    p += f.bit >> 3;
-  } else if (!have) {
-    return ZF(false);                  // repeat mode without a previous table
+    q += f.bit >> 3;
+  }
+  if (!repeat) {
+    s.tmode[kind] = m;
+    s.tpos[kind] = q0;
+    s.tend[kind] = end;
+    p = q;
   }
   have = 1;
   return true;
@@ -833,11 +873,19 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
   const Win w{(uint32_t)offsetof(Smem, lwin) + j * LWIN, s.lwlo[j], LWIN};
   const uint32_t n = left < LSYM ? left : LSYM, mb = s.hbits;
   uint8_t *stage = s.lstage + j * LSYM;
-  for (uint32_t k = 0; k < n; ++k) {
-    br_need(b, s, w, mb);
-    const uint32_t e = s.huf[br_look(b, mb)];
-    b.nbits -= (int32_t)(e & 15);
-    stage[k] = (uint8_t)(e >> 4);
+  // four symbols per container check (4 x 11 <= 56 readable bits): the
+  // lanes' refills fall on the same iterations far more often, and three
+  // of four lookups carry no check at all
+  for (uint32_t k = 0; k < n; k += 4) {
+    br_need(b, s, w, 4 * mb);
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      if (k + g < n) {
+        const uint32_t e = s.huf[br_look(b, mb)];
+        b.nbits -= (int32_t)(e & 15);
+        stage[k + g] = (uint8_t)(e >> 4);
+      }
+    }
   }
   s.lrn[j] = n;
   s.lcnt[j] = left - n;
@@ -1256,7 +1304,9 @@ struct HostTeam {
   }
 };
 
-__global__ void __launch_bounds__(NT) zstd_kernel(int codec, const uint8_t *src, uint8_t *dst,
+// 3 waves per SIMD (<= 168 VGPRs): with the phase-shared LDS, up to 12
+// streams per CU
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) zstd_kernel(int codec, const uint8_t *src, uint8_t *dst,
                                                    const strom_decomp_desc *desc, uint32_t n,
                                                    int32_t *status, uint8_t *scratch) {
   __shared__ Smem s;
@@ -1300,7 +1350,8 @@ uint32_t resident_groups() {
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  const uint32_t per_cu = (160u << 10) / (uint32_t)sizeof(Smem);   // LDS-bound residency
+  uint32_t per_cu = (160u << 10) / (uint32_t)sizeof(Smem);   // LDS-bound residency
+  if (per_cu > 12) per_cu = 12;                                // 3 waves per SIMD
   return (uint32_t)cus * (per_cu ? per_cu : 1);
 }
 
