@@ -4,27 +4,33 @@
 // lz4par.hip).  Not in the reference (the columnar decode path
 // is north-star work); it widens BASELINE config 5 to ZSTD-written files.
 //
-// One wavefront (workgroup of 64) per stream, several streams per CU.  A
-// compressed block is entropy-decoded serially and executed in parallel:
+// One wavefront (workgroup of 64) per stream, up to 9 streams per CU (the
+// serial entropy stage is latency-bound, so throughput follows the streams
+// in flight: the LDS is phase-shared to 16.5 KB per stream).  A compressed
+// block is entropy-decoded serially and executed in parallel:
 //
 //  1. literals: the Huffman table (FSE-coded or direct weights) is built in
 //     LDS; the 1 or 4 literal bitstreams are decoded by lanes 0..3 at once,
-//     LSYM symbols per stream per round, each stream read from its own LDS
-//     window that the whole wave refills between rounds; decoded literals
-//     go to the stream's scratch slot in HBM.  Raw / RLE literals are read
+//     LSYM symbols per stream per round (four per container check), each
+//     stream read from its own LDS window that the whole wave refills
+//     between rounds; decoded literals are staged in LDS and copied to the
+//     stream's scratch slot in HBM, coalesced.  Raw / RLE literals are read
 //     in place.
 //  2. sequences: LL / OF / ML FSE tables (predefined, RLE, compressed or
-//     repeated) in LDS with the code baselines folded into the entries;
-//     lane 0 decodes up to SEQN sequences of the backward bitstream from an
-//     LDS window (refilled by the wave per chunk), resolves repeat offsets
-//     and keeps running output / literal positions, so no scan is needed.
+//     repeated) in LDS with the code baselines folded into the entries; the
+//     wave decodes up to SEQN sequences of the backward bitstream from an
+//     LDS window (refilled by the wave per chunk) in a branch-free loop —
+//     every lane computes, lane i % 64 keeps entry i in registers — with
+//     two bit extractions per sequence, select-based repeat offsets and
+//     running output / literal positions, so no scan is needed.
 //  3. execution, all 64 lanes: the chunk's output is produced in batches of
 //     OB bytes — a source pointer per byte (literal index; stored output
 //     before the batch; or an earlier byte of the batch), pointer doubling
 //     until every pointer is a literal or stored byte (log2 of the longest
 //     in-batch chain), one gather per byte, coalesced byte stores.  Stored
-//     output and scratch literals are read back with L1-bypassing loads
-//     after the workgroup release fence + barrier that ended their writes.
+//     output and scratch literals are read back with plain loads after the
+//     workgroup release fence + barrier that ended their writes (the
+//     workgroup's waves share the CU's L1).
 //
 // The phases are plain functions of (shared state, lane); the kernel runs
 // them with barriers between, strom_zstd_host() runs the SAME functions
@@ -293,7 +299,7 @@ HD uint32_t br_read(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k
 // stream (cbase < 0, those bits zeroed), so an extraction is one shift and
 // mask with no branch; the fill offset is clamped into the window so that
 // even a corrupt stream cannot read outside it.  br_need(k) makes k <= 56
-// bits available, br_get(k) then extracts them.
+// bits available, br_look / br_get64 then extract them.
 HD void br_wfill(BR &b, const Smem &s, const Win &w) {
   const int32_t nb = b.nbits > 0 ? b.nbits : 0;
   const int32_t base = (nb - 57) & ~7;             // floor to a byte: 57..64 bits readable
@@ -323,11 +329,6 @@ HD uint64_t br_get64(BR &b, uint32_t k) {        // k <= 56, after br_need(>= k)
   return (b.cont >> lo) & ((1ull << k) - 1);
 }
 
-[[maybe_unused]] HD uint32_t br_get(BR &b, uint32_t k) {
-  const uint32_t v = br_look(b, k);
-  b.nbits -= (int32_t)k;
-  return v;
-}
 
 // forward bits (table descriptions): bytes [p, end), bit offset from p
 struct FR {
