@@ -912,6 +912,17 @@ HD void seq_load(Smem &s, const Ctx &c, uint32_t t) {
   for (uint32_t k = 0; k < SWIN / NT; ++k) s.swin[t + k * NT] = r[k];
 }
 
+// one FSE entry as a single 64-bit LDS load (a field-wise copy splits it)
+HD SeqEnt ld_ent(const SeqEnt *tab, uint32_t i) {
+  const uint64_t v = *(const uint64_t *)(tab + i);
+  SeqEnt e;
+  e.base = (uint32_t)v;
+  e.next = (uint16_t)(v >> 32);
+  e.nb = (uint8_t)(v >> 48);
+  e.add = (uint8_t)(v >> 56);
+  return e;
+}
+
 // (2) up to SEQN sequences -> chunk entries; the block's last chunk also
 // gets the trailing literals as an entry without a match.  Run by every
 // lane of the wave on the same values (wave-uniform: scalar registers and
@@ -938,7 +949,7 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   // end the stream after the chunk (its entries are then never executed)
   bool bad_fmt = false, bad_dist = false;
   for (uint32_t i = 0; i < m; ++i) {
-    const SeqEnt eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
+    const SeqEnt eo = ld_ent(s.tof, sof), em = ld_ent(s.tml, sml), el = ld_ent(s.tll, sll);
     // offset + match-length extra bits in one extraction (<= 47 bits)
     br_need(b, s, w, 47);
     const uint32_t na = eo.add + em.add;
@@ -962,7 +973,9 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     // when the literal length is 0; k = 3 is "first repeat minus one"
     const bool isnew = ofv > 3;
     const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
-    const uint32_t rep = k == 0 ? r0 : k == 1 ? r1 : k == 2 ? r2 : r0 - 1;
+    const uint32_t rep01 = k == 1 ? r1 : r0;
+    const uint32_t rep012 = k == 2 ? r2 : rep01;
+    const uint32_t rep = k == 3 ? r0 - 1 : rep012;
     const uint32_t off = isnew ? ofv - 3 : rep;
     const bool shift1 = isnew || k >= 1, shift2 = isnew || k >= 2;
     r2 = shift2 ? r1 : r2;
