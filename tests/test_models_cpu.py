@@ -230,3 +230,29 @@ def test_scan_key_tracks_relation_and_predicate(strom, tmp_path):
     assert k1 == pg_scan.scan_key(rel, attr_off=0, lo=1, hi=5)
     assert k1 != pg_scan.scan_key(rel, attr_off=0, lo=1, hi=6)
     assert k1 != pg_scan.scan_key(rel, pg_scan.ScanConfig(verify_checksum=True), attr_off=0, lo=1, hi=5)
+
+
+def test_arrow_scan_plans_zstd_and_refuses_mixed(tmp_path):
+    """ArrowScan's plan (no GPU needed) takes a pyarrow ZSTD file with the
+    zstd decoder's codec and refuses a file mixing LZ4 and ZSTD batches."""
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+    from nvme_strom_amd.ops import decompress as D
+    tbl = pa.table({"a": np.arange(50_000, dtype=np.int64) * 7})
+    path = str(tmp_path / "z.arrow")
+    with ipc.new_file(path, tbl.schema, options=ipc.IpcWriteOptions(compression="zstd")) as w:
+        for k in range(4):
+            w.write_batch(tbl.slice(k * 12_500, 12_500).to_batches()[0])
+    sc = ArrowScan(path, "cpu")
+    batches, dtypes, rows = sc._plan(["a"])
+    assert sc._codec == D.ARROW_ZSTD and rows == 50_000 and len(batches) == 4
+    assert all(d.compressed for b in batches for d, _ in b.cols)
+    mixed = str(tmp_path / "m.arrow")
+    with ipc.new_file(mixed, tbl.schema, options=ipc.IpcWriteOptions(compression="zstd")) as w:
+        w.write_batch(tbl.slice(0, 100).to_batches()[0])
+    # pyarrow writes one codec per file: the mixed case is built in the metadata
+    sc2 = ArrowScan(mixed, "cpu")
+    sc2.meta.codecs = ["zstd", "lz4_frame"]
+    with pytest.raises(NotImplementedError):
+        sc2._plan(["a"])
