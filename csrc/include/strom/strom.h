@@ -257,6 +257,8 @@ int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
                           const struct strom_decomp_desc *d_desc, uint32_t nstreams,
                           int32_t *d_status, void *scratch, uint64_t scratch_bytes,
                           void *stream);
+/* free the library-kept zstd scratch (after the streams' last decodes) */
+int strom_zstd_release(void);
 /* the same decode on the CPU (the kernel's phases lane by lane) */
 int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, uint32_t cap);
 

@@ -1347,6 +1347,8 @@ uint8_t *scratch_for(void *stream, size_t bytes) {
   std::lock_guard<std::mutex> g(g_mu);
   auto &e = g_scratch[{dev, stream}];
   if (e.second < bytes) {
+    // a smaller buffer may still be in use by this stream's last launch
+    if (e.first && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return nullptr;
     if (e.first) (void)hipFree(e.first);
     e.first = nullptr;
     e.second = 0;
@@ -1360,10 +1362,16 @@ uint8_t *scratch_for(void *stream, size_t bytes) {
 
 uint32_t resident_groups() {
   int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      cus <= 0)
-    cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  static int cached[64] = {0};
+  if (dev >= 0 && dev < 64 && cached[dev]) {
+    cus = cached[dev];
+  } else {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    if (dev >= 0 && dev < 64) cached[dev] = cus;
+  }
   uint32_t per_cu = (160u << 10) / (uint32_t)sizeof(Smem);   // LDS-bound residency
   if (per_cu > 12) per_cu = 12;                                // 3 waves per SIMD
   return (uint32_t)cus * (per_cu ? per_cu : 1);
@@ -1383,7 +1391,8 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
   using namespace zs;
   if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
   if (!nstreams) return 0;
-  uint32_t grid = nstreams < resident_groups() ? nstreams : resident_groups();
+  const uint32_t res = resident_groups();
+  uint32_t grid = nstreams < res ? nstreams : res;
   if (grid > 65535) grid = 65535;
   uint8_t *sc = (uint8_t *)scratch;
   if (sc) {
@@ -1400,6 +1409,20 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
 }
 
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
+
+// Free the literal scratch kept per (device, stream) (128 KiB per resident
+// workgroup, up to ~290 MiB per stream): after the streams' last decodes.
+extern "C" int strom_zstd_release(void) {
+  std::lock_guard<std::mutex> g(zs::g_mu);
+  int rc = 0;
+  for (auto &kv : zs::g_scratch) {
+    if (!kv.second.first) continue;
+    if (hipStreamSynchronize((hipStream_t)kv.first.second) != hipSuccess) rc = -5;
+    if (hipFree(kv.second.first) != hipSuccess) rc = -5;
+  }
+  zs::g_scratch.clear();
+  return rc;
+}
 
 #ifdef ZS_PROF
 // read (and zero) the phase profile: out[kZpN] (cycles per phase, counts)
