@@ -129,6 +129,8 @@ class ArrowScan:
     # per CU and 0 on config 5 was inside the storage noise:
     # profiles/r3/arrow_group_policy_ab/.)
     ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
+    # ZSTD groups: 1 / ZSTD_ROUND_DIV of the zstd decoder's resident round
+    ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "4"))
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -191,9 +193,14 @@ class ArrowScan:
         if self.device.type == "cuda":
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
         if getattr(self, "_codec", None) == D.ARROW_ZSTD:
-            # zstd.hip: one wavefront per stream, residency bound by its LDS
+            # zstd.hip: one wavefront per stream, residency bound by its LDS.
+            # A group's decode takes one stream's latency whatever its size
+            # (the entropy stage is serial per stream), so zstd groups are a
+            # fraction of a round: their decodes pipeline with the reads of
+            # the next groups, and fewer co-resident streams decode faster
             from .. import _native as N
-            return cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
+            rnd = cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
+            return max(1, rnd // self.ZSTD_ROUND_DIV)
         return self.ROUND_STREAMS_PER_CU * cus
 
     def _chunks(self, b: _Batch) -> np.ndarray:
