@@ -130,7 +130,7 @@ class ArrowScan:
     # profiles/r3/arrow_group_policy_ab/.)
     ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
     # ZSTD groups: 1 / ZSTD_ROUND_DIV of the zstd decoder's resident round
-    ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "4"))
+    ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "1"))
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -194,10 +194,11 @@ class ArrowScan:
             cus = torch.cuda.get_device_properties(self.device).multi_processor_count
         if getattr(self, "_codec", None) == D.ARROW_ZSTD:
             # zstd.hip: one wavefront per stream, residency bound by its LDS.
-            # A group's decode takes one stream's latency whatever its size
-            # (the entropy stage is serial per stream), so zstd groups are a
-            # fraction of a round: their decodes pipeline with the reads of
-            # the next groups, and fewer co-resident streams decode faster
+            # A group's decode takes about one stream's latency whatever its
+            # size (the entropy stage is serial per stream), so groups stay a
+            # whole round: smaller ones queue on the HBM slot ring one
+            # latency each (A/B, profiles/r3/zstd/arrow_group_div_ab.json:
+            # val 11.0-12.8 GB/s at a round, 5.8 at a quarter, 4.2 at an eighth)
             from .. import _native as N
             rnd = cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
             return max(1, rnd // self.ZSTD_ROUND_DIV)
