@@ -38,7 +38,7 @@
 // pyarrow's zstd frames at several levels).  Raw / RLE blocks, skippable
 // frames, several frames per stream, the frame content size and the Arrow
 // length prefix are checked; dictionaries are refused (Arrow writes none);
-// the optional content checksum is skipped, not verified.
+// a frame's content checksum, when present, is verified (XXH64, -5).
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -83,7 +83,8 @@ constexpr uint32_t kTag = kLit | kHist;
 constexpr uint32_t kPosMax = 1u << 30;   // outputs below 1 GiB
 static_assert(SEQN * 89 / 8 + 24 <= SWIN && LSYM * 11 / 8 + 24 <= LWIN, "windows cover a chunk");
 
-enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3, kErrUnsupported = -4 };
+enum : int32_t { kErrFormat = -1, kErrOverflow = -2, kErrDistance = -3, kErrUnsupported = -4,
+                 kErrChecksum = -5 };
 enum : uint32_t { kFrame = 0, kBlock = 1, kDone = 2, kStored = 3 };
 enum : uint32_t { kRaw = 0, kRle = 1, kComp = 2 };
 enum : uint32_t { kLitScratch = 0, kLitInput = 1, kLitRle = 2 };
@@ -178,6 +179,8 @@ struct Smem {
   uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
   uint32_t have_ll, have_of, have_ml;
   uint32_t cn, ctot;
+  uint32_t ck_pos, ck_need;  // the frame's content checksum (XXH64 low 32 bits)
+  uint64_t xacc[4];
   int64_t expect;            // Arrow length prefix, or -1
 };
 
@@ -545,6 +548,7 @@ HD void stream_init(Smem &s, const Ctx &c, int codec) {
   s.state = kFrame;
   s.expect = -1;
   s.hbits = 0;
+  s.ck_need = 0;
   if (c.cap >= kPosMax || c.len >= kPosMax) {
     s.err = kErrOverflow;
     return;
@@ -681,6 +685,8 @@ HD void end_block(Smem &s, const Ctx &c) {
       s.err = ZF(kErrFormat);
       return;
     }
+    s.ck_pos = s.ip;               // verified by the xxh phase (run())
+    s.ck_need = 1;
     s.ip += 4;
   }
   if (s.fcs_set && s.op - s.fstart != s.fcs) s.err = ZF(kErrFormat);
@@ -1154,7 +1160,79 @@ HD void copy_block(const Smem &s, const Ctx &c, uint32_t t) {
   }
 }
 
+// ------------------------------------------------------------- XXH64
+// The content checksum of a frame (RFC 8878 3.1.1: the low 32 bits of
+// XXH64, seed 0, over the frame's decoded bytes): lanes 0..3 each run one
+// of the four stripe accumulators over the frame's output, lane 0 merges
+// them and the tail.
+constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull, kP2 = 0xC2B2AE3D27D4EB4Full,
+                   kP3 = 0x165667B19E3779F9ull, kP4 = 0x85EBCA77C2B2AE63ull,
+                   kP5 = 0x27D4EB2F165667C5ull;
+
+HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+HD uint64_t xround(uint64_t acc, uint64_t in) { return rotl64(acc + in * kP2, 31) * kP1; }
+
+HD uint64_t rd64(const uint8_t *p) {
+  if (((uintptr_t)p & 7) == 0) return *(const uint64_t *)p;
+  uint64_t v = 0;
+  for (int j = 0; j < 8; ++j) v |= (uint64_t)p[j] << (8 * j);
+  return v;
+}
+
+HD void xxh_lane(Smem &s, const Ctx &c, uint32_t t) {
+  if (t >= 4) return;
+  const uint8_t *p = c.out + s.fstart;
+  const uint32_t len = s.op - s.fstart, stripes = len / 32;
+  uint64_t v = t == 0 ? kP1 + kP2 : t == 1 ? kP2 : t == 2 ? 0 : 0 - kP1;
+  for (uint32_t j = 0; j < stripes; ++j) v = xround(v, rd64(p + 32 * j + 8 * t));
+  s.xacc[t] = v;
+}
+
+HD void xxh_finish(Smem &s, const Ctx &c) {
+  const uint8_t *p = c.out + s.fstart;
+  const uint32_t len = s.op - s.fstart;
+  uint64_t h;
+  uint32_t i = 0;
+  if (len >= 32) {
+    const uint64_t v1 = s.xacc[0], v2 = s.xacc[1], v3 = s.xacc[2], v4 = s.xacc[3];
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = (h ^ xround(0, v1)) * kP1 + kP4;
+    h = (h ^ xround(0, v2)) * kP1 + kP4;
+    h = (h ^ xround(0, v3)) * kP1 + kP4;
+    h = (h ^ xround(0, v4)) * kP1 + kP4;
+    i = len / 32 * 32;
+  } else {
+    h = kP5;
+  }
+  h += len;
+  for (; i + 8 <= len; i += 8) h = rotl64(h ^ xround(0, rd64(p + i)), 27) * kP1 + kP4;
+  if (i + 4 <= len) {
+    const uint64_t w = (uint64_t)p[i] | ((uint64_t)p[i + 1] << 8) | ((uint64_t)p[i + 2] << 16) |
+                       ((uint64_t)p[i + 3] << 24);
+    h = rotl64(h ^ (w * kP1), 23) * kP2 + kP3;
+    i += 4;
+  }
+  for (; i < len; ++i) h = rotl64(h ^ (p[i] * kP5), 11) * kP1;
+  h ^= h >> 33;
+  h *= kP2;
+  h ^= h >> 29;
+  h *= kP3;
+  h ^= h >> 32;
+  s.ck_need = 0;
+  if ((uint32_t)h != rd32(c, s.ck_pos)) s.err = ZF(kErrChecksum);
+}
+
 // ------------------------------------------------------------- driver
+template <class TM>
+HD void verify_frame(TM &tm, Smem &s, const Ctx &c) {
+  tm.fence();                      // the frame's last output stores
+  tm.sync();
+  tm.each([&](uint32_t t) { xxh_lane(s, c, t); });
+  tm.sync();
+  tm.one([&] { xxh_finish(s, c); });
+  tm.sync();
+}
+
 template <class TM>
 HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
   tm.one([&] { stream_init(s, c, codec); });
@@ -1174,6 +1252,7 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
       });
       tm.sync();
       tm.mark(kZpCopy);
+      if (s.ck_need && !s.err) verify_frame(tm, s, c);
       continue;
     }
     tm.one([&] {
@@ -1250,6 +1329,7 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
     if (s.err) break;
     tm.one([&] { end_block(s, c); });
     tm.sync();
+    if (s.ck_need && !s.err) verify_frame(tm, s, c);
   }
   tm.one([&] {
     if (!s.err && s.expect >= 0 && (int64_t)s.op != s.expect) s.err = ZF(kErrFormat);

@@ -277,3 +277,25 @@ def test_zstd_fuzz_asan(tmp_path):
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "4 seeds ok" in r.stdout
+
+
+def _with_checksum(frame: bytes, data: bytes) -> bytes:
+    """A pyarrow zstd frame re-marked with the content-checksum flag and the
+    XXH64 (seed 0) low 32 bits appended, as the zstd CLI writes frames."""
+    xxhash = pytest.importorskip("xxhash")
+    f = bytearray(frame)
+    f[4] |= 0x04
+    return bytes(f) + struct.pack("<I", xxhash.xxh64_intdigest(data, 0) & 0xFFFFFFFF)
+
+
+@pytest.mark.parametrize("n", [0, 5, 31, 32, 33, 100, 4096 + 7, 300000])
+def test_zstd_content_checksum(n):
+    """Frames carrying a content checksum decode and verify (XXH64 over the
+    frame's output: the four stripe accumulators on lanes 0..3 + the tail);
+    a wrong checksum is reported as -5."""
+    pa = pytest.importorskip("pyarrow")
+    d = _data("text", n, 17)
+    z = _with_checksum(pa.Codec("zstd").compress(d, asbytes=True), d)
+    assert D.zstd_host(D.ZSTD, z, len(d)) == (len(d), d)
+    bad = z[:-1] + bytes([z[-1] ^ 0x01])
+    assert D.zstd_host(D.ZSTD, bad, len(d))[0] == -5

@@ -218,6 +218,26 @@ def test_zstd_from_pyarrow(dev, level):
     assert outs == pays
 
 
+def test_zstd_content_checksum(dev):
+    """Frames with the content-checksum flag verify on the GPU (XXH64 on
+    lanes 0..3 over each frame's output); a flipped checksum bit gives -5."""
+    pa = pytest.importorskip("pyarrow")
+    xxhash = pytest.importorskip("xxhash")
+    import struct
+    from nvme_strom_amd.ops import decompress as D
+    pays = [p for p in _payloads() if p]
+    comp = []
+    for p in pays:
+        f = bytearray(pa.Codec("zstd").compress(p, asbytes=True))
+        f[4] |= 0x04
+        comp.append(bytes(f) + struct.pack("<I", xxhash.xxh64_intdigest(p, 0) & 0xFFFFFFFF))
+    bad = comp[0][:-1] + bytes([comp[0][-1] ^ 0x80])
+    st, outs = _run(D.ZSTD, comp + [bad], [len(p) for p in pays] + [len(pays[0])], dev)
+    assert list(st[:-1]) == [len(p) for p in pays]
+    assert outs[:-1] == pays
+    assert st[-1] == -5
+
+
 def test_zstd_persistent_slots_and_arrow(dev):
     """More streams than scratch slots (each workgroup loops over streams
     and reuses its literal slot), Arrow IPC buffers incl. a stored one, and
