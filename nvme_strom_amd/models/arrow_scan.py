@@ -305,9 +305,15 @@ class ArrowScan:
         reg = kind == 1
         rel[reg] = slot_off(rel[reg])
         if so:
-            g.descs = D.make_descs_arrays(slot_off(so), np.asarray(sl), np.asarray(do),
-                                          np.asarray(dl))
-            g.need = np.asarray(need, dtype=np.int32)
+            # largest decodes first: a stream's decode time grows with its
+            # size, and the decoders hand streams to workgroups in descriptor
+            # order (zstd.hip's persistent grid takes stream w, w + grid, ...),
+            # so the small validity buffers fill in behind the data buffers
+            # instead of taking a resident round of their own
+            order = np.argsort(-np.asarray(dl, dtype=np.int64), kind="stable")
+            g.descs = D.make_descs_arrays(slot_off(so)[order], np.asarray(sl)[order],
+                                          np.asarray(do)[order], np.asarray(dl)[order])
+            g.need = np.asarray(need, dtype=np.int32)[order]
         g.ptr_kind, g.ptr_rel = kind, rel
         rows = np.array([b.rows for b in g.batches], dtype=np.int64)
         words = (rows + 63) // 64

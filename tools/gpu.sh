@@ -9,6 +9,7 @@
 #   zprof      zstd decoder phase profile (libstrom_zstdprof.so) by column kind
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
+#   mtests     model-level GPU tests only (PG / Arrow / multi-rank scans)
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (default flagship config)
 #   kbench     per-kernel throughput (nvme_strom_amd.tools.kbench)
@@ -48,6 +49,8 @@ for phase in "$@"; do
               --timeout 120 --timeout-method thread -k "crc or heap or lz4 or snappy or malformed or filter or compact" ;;
     ztests) step ztests 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -v \
               --timeout 120 --timeout-method thread -k zstd ;;
+    mtests) step mtests 300 python -u -m pytest tests/test_gpu_models.py -m gpu -x -v \
+              --timeout 120 --timeout-method thread ;;
     smoke) step smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 400 python bench.py; grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"; cat "$OUT/bench.json" ;;
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
