@@ -217,8 +217,11 @@ class ArrowScan:
         groups: List[_Group] = []
         slot = self.slot_bytes
         # really compressed buffers (a stored-raw one is as long as its data)
+        # (zstd: every compressed buffer takes the entropy stage's latency,
+        # however little it compressed — only stored ones are skipped)
+        lim = 1.0 if getattr(self, "_codec", None) == D.ARROW_ZSTD else 0.9
         comp = [(d, v) for b in batches for d, v in b.cols
-                if d.compressed and 0 < d.length < 0.9 * d.need]
+                if d.compressed and 0 < d.length < lim * d.need]
         if comp:
             # few streams per launch are fine for the block-parallel decoder
             # (lz4par.hip: a workgroup per stream), so a column of many
