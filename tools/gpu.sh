@@ -7,6 +7,7 @@
 #   ztests     zstd decoder numerics only
 #   zbench     zstd decoder GB/s by column kind / level / stream count (+ LZ4 rows)
 #   zprof      zstd decoder phase profile (libstrom_zstdprof.so) by column kind
+#   zpmc       two PMC passes (issue / wait / LDS / memory mix) over zstd_bench val + x
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
 #   mtests     model-level GPU tests only (PG / Arrow / multi-rank scans)
@@ -56,6 +57,13 @@ for phase in "$@"; do
     kbench) step kbench 300 python -u -m nvme_strom_amd.tools.kbench --out "$OUT/kbench.json" ;;
     zbench) step zbench 300 python -u -m nvme_strom_amd.tools.zstd_bench --out "$OUT/zstd.json" ;;
     zprof) step zprof 300 python -u -m nvme_strom_amd.tools.zstd_bench --prof --no-lz4 --streams ${ZSTREAMS:-2048} --out "$OUT/zprof.json" ;;
+    zpmc) for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+            n=$((n + 1))
+            (cd /tmp && step zpmc$n 120 rocprofv3 --pmc $pass --output-format csv -d "$OUT/zpmc$n" -o pmc \
+              -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,x} --levels 1 --streams 2048 \
+                 --no-lz4 --iters 1) || exit 1
+          done ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
     ztrace) (cd /tmp && step ztrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ztrace" -o trace \
               -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds val,x --levels 1 --streams 2048 --no-lz4) ;;
