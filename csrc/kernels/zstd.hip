@@ -93,6 +93,12 @@ enum : uint32_t { kLL = 0, kOF = 1, kML = 2, kPlain = 3 };
 enum { kZpHdr, kZpCopy, kZpLitLoad, kZpLitDec, kZpSeqLoad, kZpSeqDec, kZpFill, kZpDouble,
        kZpWrite, kZpNChunk, kZpNBatch, kZpNDouble, kZpNLitRound, kZpN };
 
+// Batch pointer index, skewed by one dword per EPT entries: the fill phase
+// writes EPT contiguous entries per lane (lane t at t * EPT + k), which
+// without the skew puts every 4th lane on one of 4 banks (PMC: 4.0G
+// bank-conflict cycles against 4.9G active LDS cycles, profiles/r3/zstd/)
+HD constexpr uint32_t PI(uint32_t e) { return e + e / EPT; }
+
 // FSE decoding entry (8 bytes): the state's code folded into baseline +
 // extra bits (for Huffman weights: base = the weight), its bit count and
 // the next state's base — the wave-uniform sequence loop is bound by
@@ -160,7 +166,7 @@ struct Smem {
       uint32_t lst[SEQN + 1];     //   literal index of its first literal
       uint32_t sll[SEQN + 1];     //   literal length
       uint32_t soff[SEQN + 1];    //   match offset
-      uint32_t ptr[OB];           // batch pointers
+      uint32_t ptr[OB + OB / EPT];  // batch pointers, bank-skewed (PI)
     };
   };
   BR lbr[4];
@@ -1103,7 +1109,7 @@ HD void ex_fill(Smem &s, uint32_t t, uint32_t b0, uint32_t nb) {
       const uint32_t src = abs0 + pos - off;
       v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
     }
-    s.ptr[e] = v;
+    s.ptr[PI(e)] = v;
   }
 }
 
@@ -1115,10 +1121,10 @@ HD bool ex_double(Smem &s, uint32_t t, uint32_t nb) {
   for (uint32_t k = 0; k < EPT; ++k) {
     const uint32_t e = k * NT + t;
     if (e >= nb) break;
-    const uint32_t v = s.ptr[e];
+    const uint32_t v = s.ptr[PI(e)];
     if (v & kTag) continue;
-    const uint32_t x = s.ptr[v];
-    s.ptr[e] = x;
+    const uint32_t x = s.ptr[PI(v)];
+    s.ptr[PI(e)] = x;
     more |= !(x & kTag);
   }
   return more;
@@ -1137,7 +1143,7 @@ HD void ex_write(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_t 
   for (uint32_t k = 0; k < EPT; ++k) {
     const uint32_t e = k * NT + t;
     if (e >= nb) break;
-    const uint32_t v = s.ptr[e], x = v & ~kTag;
+    const uint32_t v = s.ptr[PI(e)], x = v & ~kTag;
     uint8_t y;
     if (v & kLit)
       y = s.lit_kind == kLitInput ? c.in[s.lit_base + x]
