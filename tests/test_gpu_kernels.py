@@ -218,6 +218,41 @@ def test_zstd_from_pyarrow(dev, level):
     assert outs == pays
 
 
+def test_zstd_randomized_differential(dev):
+    """200 random payloads (mixtures of text, runs, random bytes, ints and
+    floats, 0 B - 400 KB) at random levels -7..19 in one launch: every
+    block / literal / table mode pyarrow's encoder picks, raw blocks inside
+    compressed frames, decoded on the GPU == the input."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(2024)
+    words = [b"alpha", b"beta", b"gamma", b"nvme", b"strom", b"hbm", b"gfx950"]
+    pays, comp = [], []
+    for i in range(200):
+        parts = []
+        for _ in range(int(rng.integers(1, 6))):
+            k = int(rng.integers(0, 5))
+            n = int(rng.integers(0, 120_000))
+            if k == 0:
+                parts.append(b" ".join(words[j] for j in rng.integers(0, len(words), n // 5 + 1))[:n])
+            elif k == 1:
+                parts.append(bytes([int(rng.integers(0, 256))]) * n)
+            elif k == 2:
+                parts.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+            elif k == 3:
+                parts.append(rng.integers(0, int(rng.integers(2, 1 << 40)), n // 8 + 1,
+                                          dtype=np.int64).tobytes())
+            else:
+                parts.append(rng.random(n // 8 + 1).tobytes())
+        p = b"".join(parts)[: int(rng.integers(0, 400_000))]
+        level = int(rng.integers(-7, 20))
+        pays.append(p)
+        comp.append(pa.Codec("zstd", compression_level=level).compress(p, asbytes=True))
+    st, outs = _run(D.ZSTD, comp, [len(p) for p in pays], dev)
+    assert list(st) == [len(p) for p in pays]
+    assert outs == pays
+
+
 def test_zstd_content_checksum(dev):
     """Frames with the content-checksum flag verify on the GPU (XXH64 on
     lanes 0..3 over each frame's output); a flipped checksum bit gives -5."""
