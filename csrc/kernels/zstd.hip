@@ -1425,25 +1425,47 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) zs
 // literal scratch per (device, stream): launches on one stream are ordered,
 // concurrent launches on different streams never share a slot
 std::mutex g_mu;
-std::map<std::pair<int, void *>, std::pair<uint8_t *, size_t>> g_scratch;
+struct Scratch {
+  uint8_t *p = nullptr;
+  size_t bytes = 0;
+  uint64_t used = 0;         // LRU stamp
+};
+std::map<std::pair<int, void *>, Scratch> g_scratch;
+uint64_t g_scratch_clock = 0;
+constexpr size_t kScratchKeep = 8;   // streams with a cached buffer
 
 uint8_t *scratch_for(void *stream, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(g_mu);
-  auto &e = g_scratch[{dev, stream}];
-  if (e.second < bytes) {
-    // a smaller buffer may still be in use by this stream's last launch
-    if (e.first && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return nullptr;
-    if (e.first) (void)hipFree(e.first);
-    e.first = nullptr;
-    e.second = 0;
-    void *p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    e.first = (uint8_t *)p;
-    e.second = bytes;
+  auto it = g_scratch.find({dev, stream});
+  if (it == g_scratch.end()) {
+    // bound the cache: a caller cycling through many streams would
+    // otherwise keep up to ~290 MiB per stream; the least recently used
+    // entry goes (hipFree waits for the device's outstanding work)
+    if (g_scratch.size() >= kScratchKeep) {
+      auto lru = g_scratch.begin();
+      for (auto j = g_scratch.begin(); j != g_scratch.end(); ++j)
+        if (j->second.used < lru->second.used) lru = j;
+      if (lru->second.p) (void)hipFree(lru->second.p);
+      g_scratch.erase(lru);
+    }
+    it = g_scratch.emplace(std::make_pair(dev, stream), Scratch{}).first;
   }
-  return e.first;
+  Scratch &e = it->second;
+  e.used = ++g_scratch_clock;
+  if (e.bytes < bytes) {
+    // a smaller buffer may still be in use by this stream's last launch
+    if (e.p && hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return nullptr;
+    if (e.p) (void)hipFree(e.p);
+    e.p = nullptr;
+    e.bytes = 0;
+    void *q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
+    e.p = (uint8_t *)q;
+    e.bytes = bytes;
+  }
+  return e.p;
 }
 
 uint32_t resident_groups() {
@@ -1497,14 +1519,15 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
 
 // Free the literal scratch kept per (device, stream) (128 KiB per resident
-// workgroup, up to ~290 MiB per stream): after the streams' last decodes.
+// workgroup, up to ~290 MiB per stream, at most kScratchKeep streams):
+// after the streams' last decodes.
 extern "C" int strom_zstd_release(void) {
   std::lock_guard<std::mutex> g(zs::g_mu);
   int rc = 0;
   for (auto &kv : zs::g_scratch) {
-    if (!kv.second.first) continue;
+    if (!kv.second.p) continue;
     if (hipStreamSynchronize((hipStream_t)kv.first.second) != hipSuccess) rc = -5;
-    if (hipFree(kv.second.first) != hipSuccess) rc = -5;
+    if (hipFree(kv.second.p) != hipSuccess) rc = -5;
   }
   zs::g_scratch.clear();
   return rc;

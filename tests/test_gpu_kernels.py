@@ -253,6 +253,36 @@ def test_zstd_randomized_differential(dev):
     assert outs == pays
 
 
+def test_zstd_scratch_cache_many_streams(dev):
+    """Decodes on 12 HIP streams in turn: the library's per-stream literal
+    scratch is capped (least recently used evicted) and every decode stays
+    right; strom_zstd_release() frees what is left."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd import _native as N
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(31)
+    pays = [rng.integers(0, 1000, 30000, dtype=np.int64).tobytes() for _ in range(6)]
+    comp = [pa.Codec("zstd").compress(p, asbytes=True) for p in pays]
+    src = b"".join(comp)
+    offs = np.cumsum([0] + [len(c) for c in comp])[:-1]
+    doffs = np.arange(len(pays)) * len(pays[0])
+    descs = D.make_descs([(int(o), len(c), int(do), len(p))
+                          for o, c, do, p in zip(offs, comp, doffs, pays)])
+    d_src = _t(src + b"\0", dev)
+    d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
+    want = b"".join(pays)
+    for k in range(12):
+        st = torch.cuda.Stream(device=dev)
+        dst = torch.zeros(len(want), dtype=torch.uint8, device=dev)
+        status = torch.empty(len(pays), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        D.decompress_async(D.ZSTD, d_src, dst, d_desc, status, stream=st)
+        st.synchronize()
+        assert status.cpu().tolist() == [len(p) for p in pays], k
+        assert dst.cpu().numpy().tobytes() == want, k
+    assert N.lib().strom_zstd_release() == 0
+
+
 def test_zstd_content_checksum(dev):
     """Frames with the content-checksum flag verify on the GPU (XXH64 on
     lanes 0..3 over each frame's output); a flipped checksum bit gives -5."""
