@@ -76,16 +76,6 @@ constexpr uint32_t SWIN = 1536;          // sequence bitstream window: SEQN x <=
 constexpr uint32_t LSYM = 256;           // literal symbols per stream per round
 constexpr uint32_t LWIN = 384;           // literal stream window: LSYM x <= 11 bits
 constexpr uint32_t MAXB = 128u << 10;    // Block_Maximum_Size
-// lane-parallel literal streams: 64 / nls lanes per Huffman stream, each
-// decoding a PSEG-bit segment speculatively plus a POV-bit overlap where
-// its chain must meet the next lane's (Huffman codes self-synchronise)
-constexpr uint32_t PSEG = 256;
-constexpr uint32_t POV = 96;
-constexpr uint32_t PBW = (PSEG + POV) / 32;   // bitmap words per lane
-constexpr uint32_t PWIN = 2304;               // window bytes, split over the streams
-static_assert(PSEG % 32 == 0 && POV % 32 == 0, "bitmap words");
-static_assert(16 * PSEG / 8 + POV / 8 + 40 <= PWIN / 4 && 64 * PSEG / 8 + POV / 8 + 40 <= PWIN,
-              "a round's span fits the window");
 constexpr uint32_t SLOT = MAXB;          // literal scratch per resident workgroup
 constexpr uint32_t kLit = 0x80000000u;   // pointer tag: literal index
 constexpr uint32_t kHist = 0x40000000u;  // pointer tag: stored output position
@@ -99,13 +89,6 @@ enum : uint32_t { kFrame = 0, kBlock = 1, kDone = 2, kStored = 3 };
 enum : uint32_t { kRaw = 0, kRle = 1, kComp = 2 };
 enum : uint32_t { kLitScratch = 0, kLitInput = 1, kLitRle = 2 };
 enum : uint32_t { kLL = 0, kOF = 1, kML = 2, kPlain = 3 };
-// literal streams decoded lane-parallel (0: four lanes, one per stream —
-// the A/B and fallback build, -DZS_LITPAR=0)
-#ifndef ZS_LITPAR
-#define ZS_LITPAR 1
-#endif
-constexpr bool kLitPar = ZS_LITPAR != 0;
-
 // phase profile slots (-DZS_PROF builds, DevTeam::mark / count)
 enum { kZpHdr, kZpCopy, kZpLitLoad, kZpLitDec, kZpSeqLoad, kZpSeqDec, kZpFill, kZpDouble,
        kZpWrite, kZpNChunk, kZpNBatch, kZpNDouble, kZpNLitRound, kZpN };
@@ -173,18 +156,9 @@ struct Smem {
       uint16_t snext[64];
       uint32_t wrank[16];
     };
-    struct {                 // literal phase (four lanes, one per stream)
+    struct {                 // literal phase
       alignas(4) uint8_t lwin[4][LWIN];
       uint8_t lstage[4 * LSYM];   // a round's decoded literals, copied out coalesced
-    };
-    struct {                 // literal phase (lane-parallel streams)
-      alignas(4) uint8_t pwin[PWIN];
-      uint32_t pbm[NT][PBW];       // lane chains' symbol starts, by offset below the segment top
-      uint32_t psync[NT];          // where lane t's chain meets lane t+1's (0xffffffff: none)
-      int32_t pfin[NT];            // where lane t's chain stopped
-      uint32_t pcnt[NT];           // symbols lane t emits this round
-      int32_t pend[4];             // the round's end position per stream
-      uint32_t ptot[4];            // symbols of the round per stream
     };
     struct {                 // sequence + execution phase
       alignas(4) uint8_t swin[SWIN];
@@ -940,163 +914,6 @@ HD void lit_flush(Smem &s, const Ctx &c, uint32_t t) {
   }
 }
 
-// ---- lane-parallel literal streams (one round) ---------------------------
-HD uint32_t lp_lps(const Smem &s) { return NT / s.nls; }           // lanes per stream
-HD uint32_t lp_ws(const Smem &s) { return PWIN / s.nls; }          // window bytes per stream
-HD int32_t lp_top(const Smem &s, uint32_t t) {                     // lane t's segment top
-  const uint32_t q = t / lp_lps(s), j = t % lp_lps(s);
-  return s.lbr[q].nbits - (int32_t)(j * PSEG);
-}
-
-HD void lp_load(Smem &s, const Ctx &c, uint32_t t) {
-  const uint32_t ws = lp_ws(s);
-  for (uint32_t q = 0; q < s.nls; ++q) {
-    if (!s.lcnt[q]) continue;
-    const uint32_t lo = s.lwlo[q];
-    for (uint32_t i = t; i < ws; i += NT) s.pwin[q * ws + i] = (uint8_t)gbyte(c, lo + i);
-  }
-}
-
-// pass A: lane t's chain from its segment top (lane 0 of a stream: the true
-// position) through its segment and the overlap, symbol starts -> bitmap
-HD void lp_spec(Smem &s, const Ctx &c, uint32_t t) {
-  for (uint32_t w = 0; w < PBW; ++w) s.pbm[t][w] = 0;
-  const uint32_t q = t / lp_lps(s);
-  const int32_t T = lp_top(s, t);
-  s.pfin[t] = T;
-  if (q >= s.nls || !s.lcnt[q] || T <= 0) return;
-  const Win w{(uint32_t)offsetof(Smem, pwin) + q * lp_ws(s), s.lwlo[q], lp_ws(s)};
-  BR b = s.lbr[q];
-  b.nbits = T;
-  b.cbase = 0x7fffffff;
-  const uint32_t mb = s.hbits;
-  const int32_t stop = T - (int32_t)(PSEG + POV);
-  while (b.nbits > stop && b.nbits > 0) {
-    const uint32_t o = (uint32_t)(T - b.nbits);
-    s.pbm[t][o >> 5] |= 1u << (o & 31);
-    br_need(b, s, w, mb);
-    const uint32_t len = s.huf[br_look(b, mb)] & 15;
-    if (!len) break;                      // not a code of this table
-    b.nbits -= (int32_t)len;
-  }
-  s.pfin[t] = b.nbits;
-}
-
-// where lane t's chain (overlap offsets [PSEG, PSEG+POV)) meets lane t+1's
-// (its first POV bits): the highest common symbol start
-HD void lp_meet(Smem &s, uint32_t t) {
-  const uint32_t lps = lp_lps(s), q = t / lps, j = t % lps;
-  uint32_t m = 0xffffffffu;
-  if (q < s.nls && j + 1 < lps && lp_top(s, t + 1) > 0) {
-    for (uint32_t w = 0; w < POV / 32; ++w) {
-      const uint32_t x = s.pbm[t][PSEG / 32 + w] & s.pbm[t + 1][w];
-      if (x) {
-        m = (uint32_t)(lp_top(s, t + 1) - (int32_t)(32 * w + (uint32_t)__builtin_ctz(x)));
-        break;
-      }
-    }
-  }
-  s.psync[t] = m;
-}
-
-HD uint32_t popc(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
-
-// bits [a, b) of lane t's bitmap set (chain starts between two offsets)
-HD uint32_t lp_bits(const Smem &s, uint32_t t, uint32_t a, uint32_t b) {
-  uint32_t n = 0;
-  for (uint32_t w = a >> 5; w < PBW && 32 * w < b; ++w) {
-    uint32_t x = s.pbm[t][w];
-    const uint32_t lo = 32 * w, hi = lo + 32;
-    if (a > lo) x &= ~0u << (a - lo);
-    if (b < hi) x &= (1u << (b - lo)) - 1;
-    n += popc(x);
-  }
-  return n;
-}
-
-// lane t's valid start / end this round: valid lanes are a prefix whose
-// chains met pairwise; the last of them ends where its chain left its
-// segment.  -> pcnt[t] (0 if not valid), pend / ptot per stream (lane 0)
-HD bool lp_range(const Smem &s, uint32_t t, int32_t &st, int32_t &en, bool &last) {
-  const uint32_t lps = lp_lps(s), q = t / lps, j = t % lps, q0 = q * lps;
-  if (q >= s.nls || !s.lcnt[q] || lp_top(s, t) <= 0) return false;
-  for (uint32_t i = 0; i < j; ++i)
-    if (s.psync[q0 + i] == 0xffffffffu) return false;
-  st = j == 0 ? s.lbr[q].nbits : (int32_t)s.psync[t - 1];
-  last = s.psync[t] == 0xffffffffu;
-  if (!last) {
-    en = (int32_t)s.psync[t];
-    return true;
-  }
-  // the chain's first start at or below the segment bottom, else where it
-  // stopped (the stream's start)
-  const int32_t T = lp_top(s, t);
-  en = s.pfin[t];
-  for (uint32_t w = PSEG / 32; w < PBW; ++w)
-    if (s.pbm[t][w]) {
-      en = T - (int32_t)(32 * w + (uint32_t)__builtin_ctz(s.pbm[t][w]));
-      break;
-    }
-  return true;
-}
-
-HD void lp_count(Smem &s, uint32_t t) {
-  int32_t st, en;
-  bool last;
-  uint32_t n = 0;
-  if (lp_range(s, t, st, en, last)) {
-    const int32_t T = lp_top(s, t);
-    const uint32_t a = (uint32_t)(T - st);
-    const int32_t bb = T - en;
-    n = lp_bits(s, t, a, bb > (int32_t)(PSEG + POV) ? PSEG + POV : (uint32_t)bb);
-    if (last) {
-      const uint32_t q = t / lp_lps(s);
-      s.pend[q] = en;
-    }
-  }
-  s.pcnt[t] = n;
-}
-
-// pass B: re-decode lane t's valid range into the scratch slot
-HD void lp_emit(Smem &s, const Ctx &c, uint32_t t) {
-  int32_t st, en;
-  bool last;
-  if (!s.pcnt[t] || !lp_range(s, t, st, en, last)) return;
-  const uint32_t lps = lp_lps(s), q = t / lps, q0 = q * lps;
-  uint32_t off = s.lout[q];
-  for (uint32_t i = q0; i < t; ++i) off += s.pcnt[i];
-  const Win w{(uint32_t)offsetof(Smem, pwin) + q * lp_ws(s), s.lwlo[q], lp_ws(s)};
-  BR b = s.lbr[q];
-  b.nbits = st;
-  b.cbase = 0x7fffffff;
-  const uint32_t mb = s.hbits, n = s.pcnt[t];
-  const uint32_t lim = s.lout[q] + s.lcnt[q];   // the stream's slice of the scratch
-  for (uint32_t k = 0; k < n; ++k) {
-    br_need(b, s, w, mb);
-    const uint32_t e = s.huf[br_look(b, mb)];
-    b.nbits -= (int32_t)(e & 15);
-    if (off + k < lim) c.lit[off + k] = (uint8_t)(e >> 4);
-  }
-}
-
-// lane 0 of each stream: advance it by the round
-HD void lp_advance(Smem &s, uint32_t t) {
-  const uint32_t lps = lp_lps(s), q = t / lps;
-  if (t % lps || q >= s.nls || !s.lcnt[q]) return;
-  uint32_t tot = 0;
-  for (uint32_t i = 0; i < lps; ++i) tot += s.pcnt[t + i];
-  const int32_t en = s.pend[q];
-  if (tot > s.lcnt[q] || en < 0 || (en == 0) != (tot == s.lcnt[q]) || tot == 0) {
-    s.err = ZF(kErrFormat);
-    s.lcnt[q] = 0;
-    return;
-  }
-  s.lcnt[q] -= tot;
-  s.lout[q] += tot;
-  s.lbr[q].nbits = en;
-  s.lbr[q].cbase = 0x7fffffff;
-}
-
 // (2) sequence window: lane t copies every NT-th byte
 HD void seq_load(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lo = s.swlo;
@@ -1450,33 +1267,7 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
     tm.sync();
     tm.mark(kZpHdr);
     if (s.err) break;
-    if (s.lit_kind == kLitScratch && kLitPar) {
-      for (;;) {
-        tm.each([&](uint32_t t) {
-          if (t < s.nls) s.lwlo[t] = win_lo(s.lbr[t], lp_ws(s));
-        });
-        tm.sync();
-        tm.each([&](uint32_t t) { lp_load(s, c, t); });
-        tm.sync();
-        tm.mark(kZpLitLoad);
-        tm.count(kZpNLitRound);
-        tm.each([&](uint32_t t) { lp_spec(s, c, t); });
-        tm.sync();
-        tm.each([&](uint32_t t) { lp_meet(s, t); });
-        tm.sync();
-        tm.each([&](uint32_t t) { lp_count(s, t); });
-        tm.sync();
-        tm.each([&](uint32_t t) { lp_emit(s, c, t); });
-        tm.sync();
-        tm.each([&](uint32_t t) { lp_advance(s, t); });
-        tm.sync();
-        tm.mark(kZpLitDec);
-        if (s.err || !(s.lcnt[0] | s.lcnt[1] | s.lcnt[2] | s.lcnt[3])) break;
-      }
-      tm.fence();
-      tm.sync();
-      if (s.err) break;
-    } else if (s.lit_kind == kLitScratch) {
+    if (s.lit_kind == kLitScratch) {
       for (;;) {
         tm.each([&](uint32_t t) {
           if (t < s.nls) s.lwlo[t] = win_lo(s.lbr[t], LWIN);
