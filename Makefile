@@ -50,6 +50,16 @@ $(OUT)/libstrom_zstdprof.so: csrc/kernels/zstd.hip csrc/include/strom/strom.h
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -DZS_PROF -shared -o $@ $<
 
+# zstd geometry variants for A/B timing (tools/zstd_bench.py --lib):
+# make zv ZV="name:-DZS_OB=1024 ..." -> $(OUT)/zv/<name>.so
+ZV ?= base:-DZS_OB=512
+zv:
+	@rm -rf $(OUT)/zv && mkdir -p $(OUT)/zv
+	@for v in $(ZV); do name=$${v%%:*}; defs=$$(echo $${v#*:} | tr , ' '); \
+	  $(HIPCC) $(HIPFLAGS) -Icsrc/include $$defs -shared -o $(OUT)/zv/$$name.so \
+	    csrc/kernels/zstd.hip || exit 1; done
+.PHONY: zv
+
 # a standalone decoder build for same-box A/B runs (tools/decomp_ab.py):
 # make ab AB=name [SRC=path/to/decompress.hip]
 SRC ?= csrc/kernels/decompress.hip

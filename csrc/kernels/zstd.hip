@@ -69,10 +69,16 @@ namespace zs {
 namespace {
 
 constexpr uint32_t NT = 64;              // one wave per stream
-constexpr uint32_t SEQN = 128;           // sequences per decode chunk
-constexpr uint32_t OB = 512;             // output bytes per resolve batch
+#ifndef ZS_SEQN
+#define ZS_SEQN 128
+#endif
+#ifndef ZS_OB
+#define ZS_OB 512
+#endif
+constexpr uint32_t SEQN = ZS_SEQN;       // sequences per decode chunk
+constexpr uint32_t OB = ZS_OB;           // output bytes per resolve batch
 constexpr uint32_t EPT = OB / NT;        // batch entries per lane (strided)
-constexpr uint32_t SWIN = 1536;          // sequence bitstream window: SEQN x <= 89 bits
+constexpr uint32_t SWIN = (SEQN * 89 / 8 + 24 + 63) / 64 * 64;   // sequence bitstream window: SEQN x <= 89 bits
 constexpr uint32_t LSYM = 256;           // literal symbols per stream per round
 constexpr uint32_t LWIN = 384;           // literal stream window: LSYM x <= 11 bits
 constexpr uint32_t MAXB = 128u << 10;    // Block_Maximum_Size

@@ -90,6 +90,8 @@ def main(argv=None) -> int:
                     help="skip the LZ4 rows of the same columns")
     ap.add_argument("--prof", action="store_true",
                     help="phase cycle profile of each zstd row (libstrom_zstdprof.so)")
+    ap.add_argument("--libs", default="",
+                    help="comma list of lib/zv/<name>.so geometry builds (make zv) timed too")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -100,6 +102,17 @@ def main(argv=None) -> int:
     dev = torch.device("cuda")
     res = {"lds_bytes_per_stream": int(lib().strom_zstd_lds_bytes()), "rows": []}
     cases = [("zstd", int(l)) for l in a.levels.split(",") if l] + ([("lz4", 0)] if a.lz4 else [])
+    import ctypes as C
+    import os
+    variants = [("lib", None)]
+    for v in [x for x in a.libs.split(",") if x]:
+        so = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib", "zv", v + ".so"))
+        so.strom_decompress_zstd.restype = C.c_int
+        so.strom_decompress_zstd.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        so.strom_zstd_lds_bytes.restype = C.c_uint32
+        res.setdefault("variant_lds_bytes", {})[v] = int(so.strom_zstd_lds_bytes())
+        variants.append((v, so.strom_decompress_zstd))
     for kind in a.kinds.split(","):
         for codec, level in cases:
             raws, bufs = frames(kind, a.distinct, codec, level)
@@ -117,30 +130,38 @@ def main(argv=None) -> int:
                 d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
                 dst = torch.empty(n * cap, dtype=torch.uint8, device=dev)
                 status = torch.empty(n, dtype=torch.int32, device=dev)
-                times = []
-                ok = True
-                for it in range(a.iters + 1):
-                    dst.fill_(0x5a)
-                    status.fill_(-99)
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    check(lib().strom_decompress(cid, ptr(src), ptr(dst), ptr(d_desc), n,
-                                                 ptr(status), None), codec)
-                    e1.record()
-                    torch.cuda.synchronize()
-                    if it:
-                        times.append(e0.elapsed_time(e1) / 1e3)
-                    if it == a.iters:                       # verify the last run
-                        st = status.cpu().numpy()
-                        out = dst.view(n, cap)[:, :rawlen]
-                        want = ref.view(a.distinct, rawlen)[torch.from_numpy(idx).to(dev)]
-                        ok = bool((st == rawlen).all()) and bool(torch.equal(out, want))
-                med = float(np.median(times))
                 row = dict(kind=kind, codec=codec, level=level if codec == "zstd" else None,
-                           streams=n, bytes=n * rawlen, ratio=round(ratio, 3),
-                           GBps=round(n * rawlen / med / 1e9, 2), ms=round(med * 1e3, 3),
-                           verified=ok)
+                           streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
+                for vname, vfn in (variants if codec == "zstd" else variants[:1]):
+                    times = []
+                    ok = True
+                    for it in range(a.iters + 1):
+                        dst.fill_(0x5a)
+                        status.fill_(-99)
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        if vfn is None:
+                            rc = lib().strom_decompress(cid, ptr(src), ptr(dst), ptr(d_desc), n,
+                                                        ptr(status), None)
+                        else:
+                            rc = vfn(cid, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status),
+                                     None, 0, None)
+                        check(rc, codec)
+                        e1.record()
+                        torch.cuda.synchronize()
+                        if it:
+                            times.append(e0.elapsed_time(e1) / 1e3)
+                        if it == a.iters:                       # verify the last run
+                            st = status.cpu().numpy()
+                            out = dst.view(n, cap)[:, :rawlen]
+                            want = ref.view(a.distinct, rawlen)[torch.from_numpy(idx).to(dev)]
+                            ok = bool((st == rawlen).all()) and bool(torch.equal(out, want))
+                    med = float(np.median(times))
+                    pre = "" if vfn is None else vname + "_"
+                    row[pre + "GBps"] = round(n * rawlen / med / 1e9, 2)
+                    row[pre + "ms"] = round(med * 1e3, 3)
+                    row[pre + "verified"] = ok
                 if a.prof and codec == "zstd":
                     row["phases"] = prof(cid, n, src, dst, d_desc, status)
                 _log(json.dumps(row))
@@ -152,7 +173,7 @@ def main(argv=None) -> int:
         with open(a.out, "w") as fo:
             fo.write(js)
     print(js)
-    return 0 if all(r["verified"] for r in res["rows"]) else 3
+    return 0 if all(v for r in res["rows"] for k, v in r.items() if k.endswith("verified")) else 3
 
 
 if __name__ == "__main__":
