@@ -73,7 +73,7 @@ constexpr uint32_t NT = 64;              // one wave per stream
 #define ZS_SEQN 128
 #endif
 #ifndef ZS_OB
-#define ZS_OB 512
+#define ZS_OB 1024
 #endif
 constexpr uint32_t SEQN = ZS_SEQN;       // sequences per decode chunk
 constexpr uint32_t OB = ZS_OB;           // output bytes per resolve batch
