@@ -72,6 +72,15 @@ constexpr uint32_t NT = 64;              // one wave per stream
 #ifndef ZS_SEQN
 #define ZS_SEQN 128
 #endif
+#ifndef ZS_WPE       // the occupancy target given to the register allocator
+#define ZS_WPE 2
+#endif
+#ifndef ZS_WZERO      // 1: a container fill zeroes the bits below the stream start
+#define ZS_WZERO 0
+#endif
+#ifndef ZS_SEQHOLD   // 1: chunk entries held in lane registers, stored after the loop
+#define ZS_SEQHOLD 0  // 0: lane 0 stores each entry inside the loop
+#endif
 #ifndef ZS_OB
 #define ZS_OB 1024
 #endif
@@ -164,7 +173,7 @@ struct Smem {
     };
     struct {                 // literal phase
       alignas(4) uint8_t lwin[4][LWIN];
-      uint8_t lstage[4 * LSYM];   // a round's decoded literals, copied out coalesced
+      alignas(4) uint8_t lstage[4 * LSYM];   // a round's decoded literals, copied out coalesced
     };
     struct {                 // sequence + execution phase
       alignas(4) uint8_t swin[SWIN];
@@ -315,17 +324,45 @@ HD uint32_t br_read(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k
 // mask with no branch; the fill offset is clamped into the window so that
 // even a corrupt stream cannot read outside it.  br_need(k) makes k <= 56
 // bits available, br_look / br_get64 then extract them.
+// bits [off, off + w) of v, w <= 31, off + w <= 32; w = 0 gives 0
+HD uint32_t ubfe(uint32_t v, uint32_t off, uint32_t w) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_ubfe(v, off, w);
+#else
+  return (v >> off) & ((1u << w) - 1);
+#endif
+}
+
+// the low 32 bits of ({hi, lo} >> sh), sh < 32
+HD uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t sh) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+#endif
+}
+
 HD void br_wfill(BR &b, const Smem &s, const Win &w) {
   const int32_t nb = b.nbits > 0 ? b.nbits : 0;
   const int32_t base = (nb - 57) & ~7;             // floor to a byte: 57..64 bits readable
   int32_t r = (int32_t)(b.beg - w.lo) + (base >> 3);
   r = r < 0 ? 0 : r > (int32_t)w.n - 12 ? (int32_t)w.n - 12 : r;
   const uint32_t *d = (const uint32_t *)(sbytes(s) + w.off + ((uint32_t)r & ~3u));
-  const uint64_t lo = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
   const uint32_t sh = 8 * ((uint32_t)r & 3);
+#if ZS_WZERO
+  const uint64_t lo = (uint64_t)d[0] | ((uint64_t)d[1] << 32);
   uint64_t v = sh ? (lo >> sh) | ((uint64_t)d[2] << (64 - sh)) : lo;
   if (base < 0) v = base > -64 ? v & (~0ull << (-base)) : 0;   // bits below the stream: 0
   b.cont = v;
+#else
+  // two funnel shifts; the bits below a stream's start are whatever
+  // bytes precede it in the window: a valid stream never consumes them
+  // (lookups past a literal stream's end consume nothing, a block's last
+  // sequence reads no state bits, Huffman entries are replicated over the
+  // unread low bits), and a malformed one ends with nbits != 0
+  const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+  b.cont = (uint64_t)alignbit(d1, d0, sh) | ((uint64_t)alignbit(d2, d1, sh) << 32);
+#endif
   b.cbase = base;
 }
 
@@ -343,6 +380,16 @@ HD uint64_t br_get64(BR &b, uint32_t k) {        // k <= 56, after br_need(>= k)
   b.nbits -= (int32_t)k;
   return (b.cont >> lo) & ((1ull << k) - 1);
 }
+
+// consume k bits (after br_need(>= k)) and return the container shifted
+// so that they are its low bits, unmasked: the caller cuts its fields
+// out with ubfe (one v_bfe_u32 each)
+HD uint64_t br_take(BR &b, uint32_t k) {
+  const uint32_t lo = (uint32_t)(b.nbits - (int32_t)k - b.cbase) & 63;
+  b.nbits -= (int32_t)k;
+  return b.cont >> lo;
+}
+
 
 
 // forward bits (table descriptions): bytes [p, end), bit offset from p
@@ -895,16 +942,19 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
   // four symbols per container check (4 x 11 <= 56 readable bits): the
   // lanes' refills fall on the same iterations far more often, and three
   // of four lookups carry no check at all
+  // and one dword store of the four (past the stream's end the lookups
+  // consume nothing and their bytes are never flushed)
   for (uint32_t k = 0; k < n; k += 4) {
     br_need(b, s, w, 4 * mb);
+    uint32_t word = 0;
 #pragma unroll
     for (uint32_t g = 0; g < 4; ++g) {
-      if (k + g < n) {
-        const uint32_t e = s.huf[br_look(b, mb)];
-        b.nbits -= (int32_t)(e & 15);
-        stage[k + g] = (uint8_t)(e >> 4);
-      }
+      const uint32_t lo = (uint32_t)(b.nbits - (int32_t)mb - b.cbase) & 63;
+      const uint32_t e = s.huf[ubfe((uint32_t)(b.cont >> lo), 0, mb)];
+      b.nbits -= k + g < n ? (int32_t)(e & 15) : 0;
+      word |= (e >> 4) << (8 * g);
     }
+    *(uint32_t *)(stage + k) = word;
   }
   s.lrn[j] = n;
   s.lcnt[j] = left - n;
@@ -960,8 +1010,10 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   // entry i's fields are held by lane i % NT (slot i / NT) and stored
   // together after the loop: no one-lane branch inside it
   constexpr uint32_t SL = SEQN / NT;
+#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
   uint32_t h_ll[SL], h_off[SL], h_lst[SL], h_ost[SL];
   for (uint32_t q = 0; q < SL; ++q) h_ll[q] = h_off[q] = h_lst[q] = h_ost[q] = 0;
+#endif
   // the loop body is branch-free but for the two container refills: the
   // repeat-offset update is selects, the checks accumulate into flags that
   // end the stream after the chunk (its entries are then never executed)
@@ -970,23 +1022,21 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     const SeqEnt eo = ld_ent(s.tof, sof), em = ld_ent(s.tml, sml), el = ld_ent(s.tll, sll);
     // offset + match-length extra bits in one extraction (<= 47 bits)
     br_need(b, s, w, 47);
-    const uint32_t na = eo.add + em.add;
-    const uint64_t x1 = br_get64(b, na);
-    const uint32_t ofv = eo.base + (uint32_t)(x1 >> em.add);
-    const uint32_t ml = em.base + ((uint32_t)x1 & ((1u << em.add) - 1));
-    // literal-length extra bits + the three state updates (<= 42 bits)
+    const uint64_t x1 = br_take(b, eo.add + em.add);
+    const uint32_t ml = em.base + ubfe((uint32_t)x1, 0, em.add);
+    const uint32_t ofv = eo.base + ubfe((uint32_t)(x1 >> em.add), 0, eo.add);
+    // literal-length extra bits + the three state updates (<= 42 bits);
+    // after a block's last sequence no state bits follow (the states are
+    // then never used again)
     br_need(b, s, w, 42);
     const bool more = i + 1 < last;
     const uint32_t nst = more ? el.nb + em.nb + eo.nb : 0;
-    const uint64_t x2 = br_get64(b, el.add + nst);
-    const uint32_t ll = el.base + (uint32_t)(x2 >> nst);
+    const uint64_t x2 = br_take(b, el.add + nst);
+    const uint32_t ll = el.base + ubfe((uint32_t)(x2 >> nst), 0, el.add);
     const uint32_t y = (uint32_t)x2;        // ll state | ml state | of state, high to low
-    const uint32_t nof = eo.next + (y & ((1u << eo.nb) - 1));
-    const uint32_t nml = em.next + ((y >> eo.nb) & ((1u << em.nb) - 1));
-    const uint32_t nll = el.next + ((y >> (eo.nb + em.nb)) & ((1u << el.nb) - 1));
-    sof = more ? nof : sof;
-    sml = more ? nml : sml;
-    sll = more ? nll : sll;
+    sof = eo.next + ubfe(y, 0, eo.nb);
+    sml = em.next + ubfe(y, eo.nb, em.nb);
+    sll = el.next + ubfe(y, eo.nb + em.nb, el.nb);
     // repeat offsets (RFC 8878 3.1.2.5): k = repeat index, shifted by one
     // when the literal length is 0; k = 3 is "first repeat minus one"
     const bool isnew = ofv > 3;
@@ -1001,7 +1051,7 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     r0 = off;
     bad_fmt |= lit + ll > lit_n;
     bad_dist |= off == 0 || off > pos0 + out + ll;
-#ifdef __HIP_DEVICE_COMPILE__
+#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
     const uint32_t q = i / NT;
     const bool mine = t == i % NT;
     for (uint32_t z = 0; z < SL; ++z) {
@@ -1012,11 +1062,13 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       h_ost[z] = sel ? out : h_ost[z];
     }
 #else
-    // the CPU runs the phase once (HostTeam::uni): it holds every entry
-    s.sll[n] = ll;
-    s.soff[n] = off;
-    s.lst[n] = lit;
-    s.ost[n] = out;
+    // lane 0 stores (the CPU runs the phase once, HostTeam::uni, as t = 0)
+    if (t == 0) {
+      s.sll[n] = ll;
+      s.soff[n] = off;
+      s.lst[n] = lit;
+      s.ost[n] = out;
+    }
 #endif
     lit += ll;
     out += ll + ml;
@@ -1024,7 +1076,7 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   }
   if (bad_fmt || out > MAXB) err = ZF(kErrFormat);
   else if (bad_dist) err = ZF(kErrDistance);
-#ifdef __HIP_DEVICE_COMPILE__
+#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
   for (uint32_t z = 0; z < SL; ++z) {
     const uint32_t e = z * NT + t;
     if (e < n) {
@@ -1034,11 +1086,6 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       s.ost[e] = h_ost[z];
     }
   }
-#else
-  (void)h_ll;
-  (void)h_off;
-  (void)h_lst;
-  (void)h_ost;
 #endif
   const bool w0 = t == 0;
   if (!err && m == last) {
@@ -1412,7 +1459,7 @@ struct HostTeam {
 
 // 3 waves per SIMD (<= 168 VGPRs): with the phase-shared LDS, up to 12
 // streams per CU
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) zstd_kernel(int codec, const uint8_t *src, uint8_t *dst,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ZS_WPE))) zstd_kernel(int codec, const uint8_t *src, uint8_t *dst,
                                                    const strom_decomp_desc *desc, uint32_t n,
                                                    int32_t *status, uint8_t *scratch) {
   __shared__ Smem s;
