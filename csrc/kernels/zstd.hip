@@ -161,7 +161,10 @@ struct Smem {
       SeqEnt tml[512];
       SeqEnt tof[256];
     };
-    uint16_t huf[2048];      // (symbol << 4) | code length, indexed by the next hbits bits
+    struct {                 // indexed by the next hbits bits: no index scaling,
+      uint8_t hsym[2048];    // and the length is one byte load off the chain
+      uint8_t hlen[2048];
+    };
   };
   union {
     struct {                 // building a table (Huffman weights + FSE counts)
@@ -485,7 +488,9 @@ HD bool fse_build(SeqEnt *tab, const int16_t *norm, uint32_t nsym, uint32_t al, 
     const uint32_t nb = al - hibit(nx);
     uint32_t base, add;
     code_base(kind, s, base, add);
-    tab[u].next = (uint16_t)((nx << nb) - size);
+    // sequence tables number their states as byte offsets (8-byte entries):
+    // a state update is one v_lshl_add and indexes LDS without a shift
+    tab[u].next = (uint16_t)(((nx << nb) - size) << (kind == kPlain ? 0 : 3));
     tab[u].nb = (uint8_t)nb;
     tab[u].add = (uint8_t)add;
     tab[u].base = base;
@@ -591,8 +596,10 @@ HD bool huf_build(Smem &s, uint32_t nw) {
     const uint32_t w = s.hw[i];
     if (!w) continue;
     const uint32_t n = 1u << (w - 1), st = s.wrank[w];
-    const uint16_t e = (uint16_t)((i << 4) | (maxb + 1 - w));
-    for (uint32_t j = 0; j < n; ++j) s.huf[st + j] = e;
+    for (uint32_t j = 0; j < n; ++j) {
+      s.hsym[st + j] = (uint8_t)i;
+      s.hlen[st + j] = (uint8_t)(maxb + 1 - w);
+    }
     s.wrank[w] = st + n;
   }
   s.hbits = maxb;
@@ -900,9 +907,9 @@ HD bool seq_header(Smem &s, const Ctx &c) {
     return ZF(false);
   if (p >= end || !br_init(s.sbr, c, p, end - p)) return ZF(false);
   const Win w{0, 0, 0};
-  s.st_ll = br_read(s.sbr, s, w, c, s.al_ll);
-  s.st_of = br_read(s.sbr, s, w, c, s.al_of);
-  s.st_ml = br_read(s.sbr, s, w, c, s.al_ml);
+  s.st_ll = br_read(s.sbr, s, w, c, s.al_ll) << 3;   // byte offsets
+  s.st_of = br_read(s.sbr, s, w, c, s.al_of) << 3;
+  s.st_ml = br_read(s.sbr, s, w, c, s.al_ml) << 3;
   s.nseq = n;
   s.seq_done = 0;
   return s.sbr.nbits >= 0 ? true : ZF(false);
@@ -942,19 +949,32 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
   // four symbols per container check (4 x 11 <= 56 readable bits): the
   // lanes' refills fall on the same iterations far more often, and three
   // of four lookups carry no check at all
-  // and one dword store of the four (past the stream's end the lookups
-  // consume nothing and their bytes are never flushed)
-  for (uint32_t k = 0; k < n; k += 4) {
+  // and one dword store of the four; the last, partial group's lookups
+  // past the stream's end consume nothing (their bytes are never flushed)
+  const uint32_t nf = n & ~3u;
+  for (uint32_t k = 0; k < nf; k += 4) {
     br_need(b, s, w, 4 * mb);
     uint32_t word = 0;
 #pragma unroll
     for (uint32_t g = 0; g < 4; ++g) {
       const uint32_t lo = (uint32_t)(b.nbits - (int32_t)mb - b.cbase) & 63;
-      const uint32_t e = s.huf[ubfe((uint32_t)(b.cont >> lo), 0, mb)];
-      b.nbits -= k + g < n ? (int32_t)(e & 15) : 0;
-      word |= (e >> 4) << (8 * g);
+      const uint32_t x = ubfe((uint32_t)(b.cont >> lo), 0, mb);
+      b.nbits -= (int32_t)s.hlen[x];
+      word |= (uint32_t)s.hsym[x] << (8 * g);
     }
     *(uint32_t *)(stage + k) = word;
+  }
+  if (nf < n) {
+    br_need(b, s, w, 4 * mb);
+    uint32_t word = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t lo = (uint32_t)(b.nbits - (int32_t)mb - b.cbase) & 63;
+      const uint32_t x = ubfe((uint32_t)(b.cont >> lo), 0, mb);
+      b.nbits -= nf + g < n ? (int32_t)s.hlen[x] : 0;
+      word |= (uint32_t)s.hsym[x] << (8 * g);
+    }
+    *(uint32_t *)(stage + nf) = word;
   }
   s.lrn[j] = n;
   s.lcnt[j] = left - n;
@@ -981,8 +1001,8 @@ HD void seq_load(Smem &s, const Ctx &c, uint32_t t) {
 }
 
 // one FSE entry as a single 64-bit LDS load (a field-wise copy splits it)
-HD SeqEnt ld_ent(const SeqEnt *tab, uint32_t i) {
-  const uint64_t v = *(const uint64_t *)(tab + i);
+HD SeqEnt ld_ent(const SeqEnt *tab, uint32_t off) {   // off: state x 8
+  const uint64_t v = *(const uint64_t *)((const uint8_t *)tab + off);
   SeqEnt e;
   e.base = (uint32_t)v;
   e.next = (uint16_t)(v >> 32);
@@ -1034,9 +1054,9 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
     const uint64_t x2 = br_take(b, el.add + nst);
     const uint32_t ll = el.base + ubfe((uint32_t)(x2 >> nst), 0, el.add);
     const uint32_t y = (uint32_t)x2;        // ll state | ml state | of state, high to low
-    sof = eo.next + ubfe(y, 0, eo.nb);
-    sml = em.next + ubfe(y, eo.nb, em.nb);
-    sll = el.next + ubfe(y, eo.nb + em.nb, el.nb);
+    sof = eo.next + (ubfe(y, 0, eo.nb) << 3);
+    sml = em.next + (ubfe(y, eo.nb, em.nb) << 3);
+    sll = el.next + (ubfe(y, eo.nb + em.nb, el.nb) << 3);
     // repeat offsets (RFC 8878 3.1.2.5): k = repeat index, shifted by one
     // when the literal length is 0; k = 3 is "first repeat minus one"
     const bool isnew = ofv > 3;
