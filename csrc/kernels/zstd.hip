@@ -47,6 +47,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 
 #include "strom/strom.h"
 
@@ -77,9 +78,6 @@ constexpr uint32_t NT = 64;              // one wave per stream
 #endif
 #ifndef ZS_WZERO      // 1: a container fill zeroes the bits below the stream start
 #define ZS_WZERO 0
-#endif
-#ifndef ZS_SEQHOLD   // 1: chunk entries held in lane registers, stored after the loop
-#define ZS_SEQHOLD 0  // 0: lane 0 stores each entry inside the loop
 #endif
 #ifndef ZS_OB
 #define ZS_OB 1024
@@ -1027,61 +1025,49 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lit_n = s.lit_n, last = s.nseq - s.seq_done;
   uint32_t n = 0, out = 0, lit = s.lit_used;
   int32_t err = 0;
-  // entry i's fields are held by lane i % NT (slot i / NT) and stored
-  // together after the loop: no one-lane branch inside it
-  constexpr uint32_t SL = SEQN / NT;
-#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
-  uint32_t h_ll[SL], h_off[SL], h_lst[SL], h_ost[SL];
-  for (uint32_t q = 0; q < SL; ++q) h_ll[q] = h_off[q] = h_lst[q] = h_ost[q] = 0;
-#endif
-  // the loop body is branch-free but for the two container refills: the
-  // repeat-offset update is selects, the checks accumulate into flags that
-  // end the stream after the chunk (its entries are then never executed)
-  bool bad_fmt = false, bad_dist = false;
-  for (uint32_t i = 0; i < m; ++i) {
+  // the offset-distance check accumulates into a flag that ends the stream
+  // after the chunk (its entries are then never executed); literal and
+  // output totals only grow, so their bounds are checked once after it
+  bool bad_dist = false;
+  // one sequence; MORE (every sequence but a block's last): the three
+  // state updates follow its literal-length bits
+  auto step = [&](auto more) __attribute__((always_inline)) {
+    constexpr bool MORE = decltype(more)::value;
     const SeqEnt eo = ld_ent(s.tof, sof), em = ld_ent(s.tml, sml), el = ld_ent(s.tll, sll);
     // offset + match-length extra bits in one extraction (<= 47 bits)
     br_need(b, s, w, 47);
     const uint64_t x1 = br_take(b, eo.add + em.add);
     const uint32_t ml = em.base + ubfe((uint32_t)x1, 0, em.add);
     const uint32_t ofv = eo.base + ubfe((uint32_t)(x1 >> em.add), 0, eo.add);
-    // literal-length extra bits + the three state updates (<= 42 bits);
-    // after a block's last sequence no state bits follow (the states are
-    // then never used again)
+    // literal-length extra bits + the three state updates (<= 42 bits)
     br_need(b, s, w, 42);
-    const bool more = i + 1 < last;
-    const uint32_t nst = more ? el.nb + em.nb + eo.nb : 0;
+    const uint32_t nst = MORE ? el.nb + em.nb + eo.nb : 0;
     const uint64_t x2 = br_take(b, el.add + nst);
     const uint32_t ll = el.base + ubfe((uint32_t)(x2 >> nst), 0, el.add);
-    const uint32_t y = (uint32_t)x2;        // ll state | ml state | of state, high to low
-    sof = eo.next + (ubfe(y, 0, eo.nb) << 3);
-    sml = em.next + (ubfe(y, eo.nb, em.nb) << 3);
-    sll = el.next + (ubfe(y, eo.nb + em.nb, el.nb) << 3);
-    // repeat offsets (RFC 8878 3.1.2.5): k = repeat index, shifted by one
-    // when the literal length is 0; k = 3 is "first repeat minus one"
-    const bool isnew = ofv > 3;
-    const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
-    const uint32_t rep01 = k == 1 ? r1 : r0;
-    const uint32_t rep012 = k == 2 ? r2 : rep01;
-    const uint32_t rep = k == 3 ? r0 - 1 : rep012;
-    const uint32_t off = isnew ? ofv - 3 : rep;
-    const bool shift1 = isnew || k >= 1, shift2 = isnew || k >= 2;
-    r2 = shift2 ? r1 : r2;
-    r1 = shift1 ? r0 : r1;
-    r0 = off;
-    bad_fmt |= lit + ll > lit_n;
-    bad_dist |= off == 0 || off > pos0 + out + ll;
-#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
-    const uint32_t q = i / NT;
-    const bool mine = t == i % NT;
-    for (uint32_t z = 0; z < SL; ++z) {
-      const bool sel = mine && q == z;
-      h_ll[z] = sel ? ll : h_ll[z];
-      h_off[z] = sel ? off : h_off[z];
-      h_lst[z] = sel ? lit : h_lst[z];
-      h_ost[z] = sel ? out : h_ost[z];
+    if (MORE) {
+      const uint32_t y = (uint32_t)x2;      // ll state | ml state | of state, high to low
+      sof = eo.next + (ubfe(y, 0, eo.nb) << 3);
+      sml = em.next + (ubfe(y, eo.nb, em.nb) << 3);
+      sll = el.next + (ubfe(y, eo.nb + em.nb, el.nb) << 3);
     }
-#else
+    // repeat offsets (RFC 8878 3.1.2.5): the first repeat offset after a
+    // literal run is the common case and changes nothing; otherwise k =
+    // repeat index, shifted by one when the literal length is 0, k = 3 is
+    // "first repeat minus one"
+    uint32_t off = r0;
+    if (ofv != 1 || ll == 0) {
+      const bool isnew = ofv > 3;
+      const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
+      const uint32_t rep01 = k == 1 ? r1 : r0;
+      const uint32_t rep012 = k == 2 ? r2 : rep01;
+      const uint32_t rep = k == 3 ? r0 - 1 : rep012;
+      off = isnew ? ofv - 3 : rep;
+      const bool shift2 = isnew || k >= 2;
+      r2 = shift2 ? r1 : r2;
+      r1 = r0;                             // k >= 1 or new here
+      r0 = off;
+    }
+    bad_dist |= off - 1 >= pos0 + out + ll;  // off == 0 wraps
     // lane 0 stores (the CPU runs the phase once, HostTeam::uni, as t = 0)
     if (t == 0) {
       s.sll[n] = ll;
@@ -1089,24 +1075,15 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       s.lst[n] = lit;
       s.ost[n] = out;
     }
-#endif
     lit += ll;
     out += ll + ml;
     ++n;
-  }
-  if (bad_fmt || out > MAXB) err = ZF(kErrFormat);
+  };
+  const bool tail = m && m == last;         // the chunk ends the block
+  for (uint32_t i = 0, e = tail ? m - 1 : m; i < e; ++i) step(std::true_type{});
+  if (tail) step(std::false_type{});
+  if (lit > lit_n || out > MAXB) err = ZF(kErrFormat);
   else if (bad_dist) err = ZF(kErrDistance);
-#if defined(__HIP_DEVICE_COMPILE__) && ZS_SEQHOLD
-  for (uint32_t z = 0; z < SL; ++z) {
-    const uint32_t e = z * NT + t;
-    if (e < n) {
-      s.sll[e] = h_ll[z];
-      s.soff[e] = h_off[z];
-      s.lst[e] = h_lst[z];
-      s.ost[e] = h_ost[z];
-    }
-  }
-#endif
   const bool w0 = t == 0;
   if (!err && m == last) {
     if (s.nseq && b.nbits != 0) err = ZF(kErrFormat);
