@@ -76,6 +76,9 @@ constexpr uint32_t NT = 64;              // one wave per stream
 #ifndef ZS_WPE       // the occupancy target given to the register allocator
 #define ZS_WPE 2
 #endif
+#ifndef ZS_LITDIRECT  // 1: a literals-only block's literals decode straight into the output
+#define ZS_LITDIRECT 0
+#endif
 #ifndef ZS_WZERO      // 1: a container fill zeroes the bits below the stream start
 #define ZS_WZERO 0
 #endif
@@ -195,6 +198,7 @@ struct Smem {
   int32_t err;
   uint32_t btype, bsize, bstart, bend, blast;
   uint32_t lit_kind, lit_base, lit_n, lit_used, lit_rle;
+  uint32_t lit_direct;        // a literals-only block: literals decode into the output
   uint32_t hbits, nls;
   uint32_t hdesc, hdesc_end;           // the frame's last Huffman tree description
   uint32_t tmode[3], tpos[3], tend[3]; // ... and LL / OF / ML table definitions
@@ -761,6 +765,7 @@ HD bool lit_header(Smem &s, const Ctx &c) {
   const uint32_t p = s.ip, end = s.bend;
   const uint32_t b0 = gbyte(c, p), type = b0 & 3, sf = (b0 >> 2) & 3;
   s.lit_used = 0;
+  s.lit_direct = 0;
   for (uint32_t j = 0; j < 4; ++j) s.lcnt[j] = s.lrn[j] = 0;
   if (type <= 1) {
     uint32_t R, hl;
@@ -834,6 +839,11 @@ HD bool lit_header(Smem &s, const Ctx &c) {
   s.lit_kind = kLitScratch;
   s.lit_n = R;
   s.ip = dend;
+  // Number_of_Sequences = 0 as the block's last byte (an incompressible
+  // column's blocks): the literals are the block's output, so they are
+  // flushed straight into it and the block has no execution phase
+  s.lit_direct = ZS_LITDIRECT && dend + 1 == end && gbyte(c, dend) == 0 &&
+                 (uint64_t)s.op + R <= c.cap;
   return true;
 }
 
@@ -982,9 +992,10 @@ HD void lit_chunk(Smem &s, const Ctx &c, uint32_t j) {
 
 // (1) the round's staged literals -> the scratch slot (lane-strided)
 HD void lit_flush(Smem &s, const Ctx &c, uint32_t t) {
+  uint8_t *dst = s.lit_direct ? c.out + s.op : c.lit;
   for (uint32_t j = 0; j < s.nls; ++j) {
     const uint32_t n = s.lrn[j], o = s.lout[j];
-    for (uint32_t i = t; i < n; i += NT) c.lit[o + i] = s.lstage[j * LSYM + i];
+    for (uint32_t i = t; i < n; i += NT) dst[o + i] = s.lstage[j * LSYM + i];
   }
 }
 
@@ -1343,6 +1354,16 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
       tm.fence();
       tm.sync();
       if (s.err) break;
+      if (s.lit_direct) {
+        tm.one([&] {
+          if (!seq_header(s, c)) s.err = ZF(kErrFormat);   // the 0 sequences byte
+          s.op += s.lit_n;
+          end_block(s, c);
+        });
+        tm.sync();
+        if (s.ck_need && !s.err) verify_frame(tm, s, c);
+        continue;
+      }
     }
     tm.one([&] {
       if (!seq_header(s, c)) s.err = ZF(kErrFormat);
