@@ -121,10 +121,11 @@ build/arrow_meta_fuzz: csrc/tests/arrow_meta_fuzz.cc csrc/engine/arrow_meta.cc
 	@mkdir -p build
 	$(CXX) -std=c++17 -O1 -g -fsanitize=address,undefined -fno-sanitize-recover=all -o $@ $^ -lpthread
 
-# the zstd decoder's host copy, host-only with ASan + UBSan (mutation test)
+# the zstd decoder's host copy, host-only with ASan + UBSan (mutation test);
+# built with the literals-only direct path on, so the mutants cover it too
 build/zstd_fuzz: csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip csrc/include/strom/strom.h
 	@mkdir -p build
-	$(HIPCC) -std=c++17 -O1 -g -Icsrc/include --offload-arch=$(ARCH) \
+	$(HIPCC) -std=c++17 -O1 -g -Icsrc/include --offload-arch=$(ARCH) -DZS_LITDIRECT=1 \
 	  -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
 	  -Xarch_host -fno-sanitize-recover=all -fno-omit-frame-pointer \
 	  -o $@ csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip
