@@ -77,7 +77,7 @@ constexpr uint32_t NT = 64;              // one wave per stream
 #define ZS_WPE 2
 #endif
 #ifndef ZS_LITDIRECT  // 1: a literals-only block's literals decode straight into the output
-#define ZS_LITDIRECT 0
+#define ZS_LITDIRECT 1
 #endif
 #ifndef ZS_WZERO      // 1: a container fill zeroes the bits below the stream start
 #define ZS_WZERO 0
