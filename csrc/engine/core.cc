@@ -35,7 +35,8 @@ Config Config::from_env() {
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
                                "bar_map", "bar_max", "coalesce", "trace",
-                               "ingest", "ingest_grid", "ingest_piece", "hdp_sync", "fixed_bufs",
+                               "ingest", "ingest_grid", "ingest_piece", "ingest_min", "hdp_sync",
+                               "fixed_bufs", "io_prof",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind", "check_freed",
                                "stat_info", "verbose"};
@@ -88,6 +89,12 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "ingest") { ingest = parse_bool(v); return 0; }
   if (k == "hdp_sync") { hdp_sync = parse_bool(v); return 0; }
   if (k == "fixed_bufs") { fixed_bufs = parse_bool(v); return 0; }
+  if (k == "io_prof") { io_prof = parse_bool(v); return 0; }
+  if (k == "ingest_min") {
+    if (n < 0 || n > (64l << 20)) return -EINVAL;
+    ingest_min = (uint32_t)n;
+    return 0;
+  }
   if (k == "ingest_grid") { if (n < 1 || n > 256) return -EINVAL; ingest_grid = (int)n; return 0; }
   if (k == "ingest_piece") {
     if (n < 4096 || n > (16l << 20) || (n & 4095)) return -EINVAL;
@@ -134,6 +141,8 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "ingest_piece") v = ingest_piece;
   else if (k == "hdp_sync") v = hdp_sync;
   else if (k == "fixed_bufs") v = fixed_bufs;
+  else if (k == "io_prof") v = io_prof;
+  else if (k == "ingest_min") v = ingest_min;
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "strict") v = strict;
@@ -164,25 +173,31 @@ uint64_t mono_ns() {
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
-void Hist::add(uint64_t ns) {
-  int bkt = ns ? 64 - __builtin_clzll(ns) : 0;   // bucket k: [2^(k-1), 2^k)
-  if (bkt >= STROM_HIST_BUCKETS) bkt = STROM_HIST_BUCKETS - 1;
-  b[bkt].fetch_add(1, std::memory_order_relaxed);
+uint64_t tsc_khz() {
+  static const uint64_t khz = [] {
+    const uint64_t n0 = mono_ns(), c0 = tsc_now();
+    while (mono_ns() - n0 < 5000000) _mm_pause();
+    const uint64_t n1 = mono_ns(), c1 = tsc_now();
+    return (c1 - c0) * 1000000ull / (n1 - n0);
+  }();
+  return khz;
 }
+
+void Hist::add(uint64_t ns) { b[bucket(ns)].fetch_add(1, std::memory_order_relaxed); }
 
 void Hist::copy_to(uint64_t *out, bool reset) {
   for (int i = 0; i < STROM_HIST_BUCKETS; ++i)
     out[i] = reset ? b[i].exchange(0) : b[i].load();
 }
 
-void Stats::inflight_inc() {
-  uint64_t cur = cur_dma_count.fetch_add(1, std::memory_order_relaxed) + 1;
+void Stats::inflight_inc(uint64_t n) {
+  uint64_t cur = cur_dma_count.fetch_add(n, std::memory_order_relaxed) + n;
   uint64_t mx = max_dma_count.load(std::memory_order_relaxed);
   while (cur > mx && !max_dma_count.compare_exchange_weak(mx, cur)) {
   }
 }
 
-void Stats::inflight_dec() { cur_dma_count.fetch_sub(1, std::memory_order_relaxed); }
+void Stats::inflight_dec(uint64_t n) { cur_dma_count.fetch_sub(n, std::memory_order_relaxed); }
 
 int Stats::fill(strom_stat_info *o) {
   if (o->version != 1) return -EINVAL;
@@ -259,6 +274,11 @@ Stats &stats() {
   return *s;
 }
 
+CallerProf &caller_prof() {
+  static CallerProf p;
+  return p;
+}
+
 // ------------------------------------------------------------- task table
 Task *TaskTable::create(int session) {
   Task *t = new Task();
@@ -271,17 +291,17 @@ Task *TaskTable::create(int session) {
   return t;
 }
 
-void TaskTable::get(Task *t) {
+void TaskTable::get(Task *t, int n) {
   // a frozen task accepts no new requests (reference :663 Assert)
-  t->refcnt.fetch_add(1, std::memory_order_relaxed);
+  t->refcnt.fetch_add(n, std::memory_order_relaxed);
 }
 
-void TaskTable::put(Task *t, long status) {
+void TaskTable::put_n(Task *t, int n, long status) {
   if (status != 0) {
     long zero = 0;
     t->status.compare_exchange_strong(zero, status);
   }
-  if (t->refcnt.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+  if (t->refcnt.fetch_sub(n, std::memory_order_acq_rel) != n) return;
   stats().task_ns.add(mono_ns() - t->t_start_ns);
   Slot &s = slot_of(t->id);
   {

@@ -320,7 +320,7 @@ static void build_requests(Task *t, const ChunkPlan &plan, int fd_direct, int fd
                            const Engine::StripeSet *ss = nullptr) {
   uint64_t t0 = tsc_now();
   out->reserve(plan.ssd.size());
-  uint64_t now_ns = mono_ns();
+  const uint64_t now_ns = mono_ns(), now_tsc = tsc_now();
   for (const IoRange &r : plan.ssd) {
     IoReq q;
     q.task = t;
@@ -345,11 +345,16 @@ static void build_requests(Task *t, const ChunkPlan &plan, int fd_direct, int fd
     }
     q.gmap = gmap;
     q.t_submit_ns = now_ns;
-    q.t_submit_tsc = tsc_now();
-    tasks().get(t);
-    if (gmap) gmap->inflight.fetch_add(1);
-    stats().inflight_inc();
+    q.t_submit_tsc = now_tsc;
     out->push_back(q);
+  }
+  // one reference / in-flight count per request, taken for the whole batch
+  // before any of them is queued (per-request RMWs on the task and mapping
+  // lines contended with the workers' completions: profiles/r4/engine)
+  if (const int n = (int)plan.ssd.size()) {
+    tasks().get(t, n);
+    if (gmap) gmap->inflight.fetch_add(n);
+    stats().inflight_inc((uint64_t)n);
   }
   stats().nr_setup_prps.fetch_add(plan.ssd.size(), std::memory_order_relaxed);
   stats().clk_setup_prps.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
@@ -389,6 +394,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
     pp.bmap = stripe_ident_bmap;
   }
   phase_mark(0);
+  const uint64_t c0 = tsc_now();
   std::vector<unsigned char> resv;
   uint64_t res_lo = 0;
   if (f && config().pgcache_probe && f->map) attach_residency(f.get(), &pp, &resv, &res_lo);
@@ -396,6 +402,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   int rc = plan_chunks(pp, &plan);
   if (rc) return rc;
   phase_mark(1);
+  const uint64_t c1 = tsc_now();
   // MI355X extension: wb_buffer == NULL asks the engine to put page-cache
   // chunks straight into HBM (buffered reads into the large-BAR mapping);
   // they still land at the tail and are reported as nr_ram2gpu.
@@ -419,8 +426,16 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
     io_->run_inline(reqs[0]);
   else
     io_->submit(reqs);
+  const uint64_t t1 = tsc_now();
   stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
-  stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+  stats().clk_submit_dma.fetch_add(t1 - t0, std::memory_order_relaxed);
+  if (config().io_prof) {
+    CallerProf &cp = caller_prof();
+    cp.calls.fetch_add(1, std::memory_order_relaxed);
+    cp.plan.fetch_add(c1 - c0, std::memory_order_relaxed);
+    cp.build.fetch_add(t0 - c1, std::memory_order_relaxed);
+    cp.submit.fetch_add(t1 - t0, std::memory_order_relaxed);
+  }
 
   // page-cache chunks overlap with the storage reads (none for stripe sets:
   // their members are read with O_DIRECT, coherent with dirty pages)

@@ -72,6 +72,9 @@ struct Config {
                                  // pinning); falls back to READ when the
                                  // kernel or RLIMIT_MEMLOCK refuses
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
+  uint32_t ingest_min = 0;       // worker requests below this go staging -> BAR by
+                                 // CPU stores even when the ingest grid runs
+  bool io_prof = false;          // per-worker phase attribution (strom_io_prof)
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks
   bool pgcache_probe = true;     // residency scoring (mincore)
@@ -93,9 +96,14 @@ Config &config();                // process-wide, guarded by engine lock
 // ------------------------------------------------------------------- stats
 uint64_t tsc_now();
 uint64_t mono_ns();
+uint64_t tsc_khz();   // calibrated once against CLOCK_MONOTONIC
 
 struct Hist {
   std::atomic<uint64_t> b[STROM_HIST_BUCKETS];
+  static int bucket(uint64_t ns) {   // bucket k: [2^(k-1), 2^k)
+    int k = ns ? 64 - __builtin_clzll(ns) : 0;
+    return k >= STROM_HIST_BUCKETS ? STROM_HIST_BUCKETS - 1 : k;
+  }
   void add(uint64_t ns);
   void copy_to(uint64_t *out, bool reset);
 };
@@ -110,13 +118,21 @@ struct Stats {
   std::atomic<uint64_t> nr_debug[4]{}, clk_debug[4]{};
   Hist io_ns, copy_ns, task_ns;
 
-  void inflight_inc();
-  void inflight_dec();
+  void inflight_inc(uint64_t n = 1);
+  void inflight_dec(uint64_t n = 1);
   int fill(strom_stat_info *out);
   int fill_hist(strom_stat_hist *out);
 };
 
 Stats &stats();
+
+// submitting-thread side of the attribution (config io_prof): SSD2GPU /
+// SSD2RAM calls and the TSC cycles they spent planning, building requests
+// and handing them to the workers
+struct CallerProf {
+  std::atomic<uint64_t> calls{0}, plan{0}, build{0}, submit{0};
+};
+CallerProf &caller_prof();
 
 // Readers (strom_stat, nvme_strom_amd/utils/stat.py) index the export as a
 // flat array of u64: 11 scalars, debug nr[4], debug clk[4], 3 x 48 buckets.
@@ -152,8 +168,11 @@ class TaskTable {
  public:
   static constexpr int kSlots = 512;
   Task *create(int session);
-  void get(Task *t);
-  void put(Task *t, long status);
+  void get(Task *t, int n = 1);
+  void put(Task *t, long status) { put_n(t, 1, status); }
+  // drop n references at once (a worker's batch of completions of one task);
+  // a non-zero status is recorded first (first error wins)
+  void put_n(Task *t, int n, long status);
   // 0 done OK; -EIO failed (status set); -ENOENT never issued; -ETIME timeout
   int wait(uint64_t id, long *status, int64_t timeout_ns);
   int reclaim(int session);         // fd-close analogue: drop failed records
@@ -373,6 +392,11 @@ class IoEngine {
   explicit IoEngine(const Config &cfg);
   ~IoEngine();
   void submit(std::vector<IoReq> &reqs);
+  // per-worker phase attribution summed over the workers (config io_prof):
+  // out[0] workers, out[1] TSC kHz, then kProfPhases cycle sums, then
+  // kProfCounts counters; returns the number of u64 written
+  static constexpr int kProfPhases = 11, kProfCounts = 5;
+  int prof(uint64_t *out, int nout, bool reset);
   // Small single-request tasks run on the caller's thread (no worker
   // hand-off, no WAIT wake-up): the 4 KiB latency path.
   void run_inline(IoReq &r);
@@ -416,6 +440,17 @@ class Ingest {
   bool post(const void *src, uint64_t dst, uint32_t len, uint64_t *seq);
   bool post_many(const void *src, uint64_t dst, uint32_t len, uint32_t piece, uint64_t *first,
                  uint32_t *n);
+  // Post several ranges under one lock acquisition (a worker's batch of
+  // finished reads); each run's ok / first / n are filled in.
+  struct Run {
+    const void *src;
+    uint64_t dst;
+    uint32_t len;
+    bool ok;
+    uint64_t first;
+    uint32_t n;
+  };
+  void post_runs(Run *runs, size_t nruns, uint32_t piece);
   bool is_done(uint64_t seq) const;
   void retired(uint32_t n);         // the poster observed n descriptors done
   void idle();                      // stop the grid when nothing is outstanding
@@ -427,18 +462,21 @@ class Ingest {
   bool init();
   int launch_grid();
   int start_locked();
-  void stop_locked();
-  bool post_locked(const void *src, uint64_t dst, uint32_t len, uint64_t *seq);
+  void write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len);
 
   int device_;
   uint32_t nslots_ = 0, grid_ = 0;
   void *host_ = nullptr, *ring_ = nullptr, *next_ = nullptr;
   volatile uint64_t *done_ = nullptr, *stop_ = nullptr;
   void *stream_ = nullptr, *end_ev_ = nullptr;
-  std::mutex mu_;
-  uint64_t post_seq_ = 0;
-  bool running_ = false, launched_ = false, dead_ = false;
-  std::atomic<long> outstanding_{0};
+  std::mutex mu_;                      // grid start / stop only
+  std::atomic<uint64_t> post_seq_{0};  // next sequence number to reserve
+  // 2 x descriptors outstanding | grid running: a poster adds before it
+  // reserves, and the grid is stopped only by a CAS from exactly "running,
+  // nothing outstanding", so no reservation can race a stop
+  std::atomic<uint64_t> state_{0};
+  bool launched_ = false;              // under mu_
+  std::atomic<bool> dead_{false};
   uint64_t nr_launch_ = 0;
 };
 

@@ -7,8 +7,9 @@
 //   done_   nslots x u64 completion words (written by the GPU, system scope)
 //   stop_   one u64 the grid polls between descriptors
 //   next_   a device u32 the grid's workgroups claim sequence numbers from
-// Posting is a mutex-protected store sequence (fields, then seq with release
-// order); completion is a plain load of done_[s % nslots].
+// Posting is lock-free: a batch reserves its sequence numbers with one
+// fetch_add and stores each descriptor (fields, then seq with release order);
+// completion is a plain load of done_[s % nslots].
 //
 // Lifecycle: the grid is launched on the first post after an idle period and
 // stopped by the first worker that goes to sleep with nothing outstanding
@@ -109,15 +110,17 @@ int Ingest::launch_grid() {
   (void)hipSetDevice(device_);
   if (hipMemsetAsync(next_, 0, sizeof(uint32_t), (hipStream_t)stream_) != hipSuccess) return -EIO;
   int rc = strom_ingest_kernel_launch(ring_, (void *)done_, (const void *)stop_, next_, nslots_,
-                                      post_seq_, grid_, stream_);
+                                      post_seq_.load(), grid_, stream_);
   if (rc) return rc;
   if (hipEventRecord((hipEvent_t)end_ev_, (hipStream_t)stream_) != hipSuccess) return -EIO;
   launched_ = true;
   return 0;
 }
 
+// under mu_, with the running bit clear: no descriptor is reserved until
+// the bit is set again, so post_seq_ is the first number the grid serves
 int Ingest::start_locked() {
-  if (running_) return 0;
+  if (state_.load() & 1) return 0;
   if (launched_) {
     // the previous grid was told to stop: it must be gone before the
     // device counter restarts
@@ -128,15 +131,9 @@ int Ingest::start_locked() {
   __atomic_store_n(stop_, 0, __ATOMIC_SEQ_CST);
   int rc = launch_grid();
   if (rc) return rc;
-  running_ = true;
+  state_.fetch_or(1);
   nr_launch_++;
   return 0;
-}
-
-void Ingest::stop_locked() {
-  if (!running_) return;
-  __atomic_store_n(stop_, 1, __ATOMIC_SEQ_CST);
-  running_ = false;
 }
 
 bool Ingest::post(const void *src, uint64_t dst, uint32_t len, uint64_t *seq) {
@@ -146,39 +143,59 @@ bool Ingest::post(const void *src, uint64_t dst, uint32_t len, uint64_t *seq) {
 
 bool Ingest::post_many(const void *src, uint64_t dst, uint32_t len, uint32_t piece,
                        uint64_t *first, uint32_t *n) {
-  if (len == 0 || (len & 15) || (((uint64_t)src | dst) & 15)) return false;
-  piece = std::max<uint32_t>(16, piece & ~15u);
-  std::lock_guard<std::mutex> g(mu_);
-  if (dead_) return false;
-  if (start_locked() != 0) {
-    dead_ = true;
-    return false;
-  }
-  *n = 0;
-  for (uint32_t off = 0; off < len; off += piece) {
-    uint64_t s;
-    post_locked((const char *)src + off, dst + off, std::min(piece, len - off), &s);
-    if (*n == 0) *first = s;
-    ++*n;
-  }
-  return true;
+  Run r{src, dst, len, false, 0, 0};
+  post_runs(&r, 1, piece);
+  *first = r.first;
+  *n = r.n;
+  return r.ok;
 }
 
-bool Ingest::post_locked(const void *src, uint64_t dst, uint32_t len, uint64_t *seq) {
-  const uint64_t s = post_seq_++;
+// Lock-free posting: one RMW on state_ and one on post_seq_ for the whole
+// batch; the mutex is taken only when the grid has to be (re)started.
+void Ingest::post_runs(Run *runs, size_t nruns, uint32_t piece) {
+  piece = std::max<uint32_t>(16, piece & ~15u);
+  uint64_t total = 0;
+  for (size_t i = 0; i < nruns; ++i) {
+    Run &r = runs[i];
+    r.n = 0;
+    r.ok = r.len != 0 && !(r.len & 15) && !(((uint64_t)r.src | r.dst) & 15);
+    if (r.ok) total += (r.len + piece - 1) / piece;
+  }
+  auto fail_all = [&] {
+    for (size_t i = 0; i < nruns; ++i) runs[i].ok = false;
+  };
+  if (total == 0) return;
+  if (dead_.load(std::memory_order_relaxed)) return fail_all();
+  const uint64_t old = state_.fetch_add(2 * total);
+  if (!(old & 1)) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (dead_.load() || start_locked() != 0) {
+      dead_.store(true);
+      state_.fetch_sub(2 * total);
+      return fail_all();
+    }
+  }
+  uint64_t s = post_seq_.fetch_add(total);
+  for (size_t i = 0; i < nruns; ++i) {
+    Run &r = runs[i];
+    if (!r.ok) continue;
+    r.first = s + 1;
+    for (uint32_t off = 0; off < r.len; off += piece, ++s, ++r.n)
+      write_desc(s, (const char *)r.src + off, r.dst + off, std::min(piece, r.len - off));
+  }
+}
+
+void Ingest::write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len) {
   const uint32_t k = (uint32_t)(s % nslots_);
   // the slot's previous occupant (s - nslots) must be done: in-flight
   // requests are bounded by the workers' staging, far below nslots
   if (s >= nslots_)
-    while (done_[k] < s - nslots_ + 1) _mm_pause();
+    while (__atomic_load_n(&done_[k], __ATOMIC_ACQUIRE) < s - nslots_ + 1) _mm_pause();
   IngestDesc *d = (IngestDesc *)ring_ + k;
   d->src = (uint64_t)src;
   d->dst = dst;
   d->len_tag = len;
   __atomic_store_n(&d->seq, s + 1, __ATOMIC_RELEASE);
-  outstanding_.fetch_add(1, std::memory_order_relaxed);
-  *seq = s + 1;
-  return true;
 }
 
 bool Ingest::is_done(uint64_t seq) const {
@@ -186,32 +203,36 @@ bool Ingest::is_done(uint64_t seq) const {
 }
 
 void Ingest::info(uint64_t *out) {
-  std::lock_guard<std::mutex> g(mu_);
-  out[0] = dead_ ? 0 : 1;
-  out[1] = nr_launch_;
-  out[2] = post_seq_;
-  out[3] = (uint64_t)outstanding_.load();
+  out[0] = dead_.load() ? 0 : 1;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    out[1] = nr_launch_;
+  }
+  out[2] = post_seq_.load();
+  out[3] = state_.load() >> 1;
 }
 
-void Ingest::retired(uint32_t n) { outstanding_.fetch_sub(n, std::memory_order_relaxed); }
+void Ingest::retired(uint32_t n) { state_.fetch_sub(2ull * n); }
 
 void Ingest::idle() {
-  if (outstanding_.load(std::memory_order_relaxed) != 0) return;
+  if (state_.load(std::memory_order_relaxed) != 1) return;  // stopped, or work outstanding
   std::lock_guard<std::mutex> g(mu_);
-  if (outstanding_.load() == 0) stop_locked();
+  uint64_t running_idle = 1;
+  if (state_.compare_exchange_strong(running_idle, 0)) __atomic_store_n(stop_, 1, __ATOMIC_SEQ_CST);
 }
 
 void Ingest::shutdown() {
   std::lock_guard<std::mutex> g(mu_);
-  stop_locked();
+  dead_.store(true);
+  state_.fetch_and(~1ull);
+  __atomic_store_n(stop_, 1, __ATOMIC_SEQ_CST);
   if (launched_) {
-    // bounded: every waiting workgroup re-reads stop within microseconds
+    // bounded: every waiting wave re-reads stop within microseconds
     const uint64_t end = mono_ns() + 2000000000ull;
     while (hipEventQuery((hipEvent_t)end_ev_) == hipErrorNotReady && mono_ns() < end)
       _mm_pause();
     launched_ = false;
   }
-  dead_ = true;
 }
 
 }  // namespace strom

@@ -31,6 +31,7 @@
 #include <unistd.h>
 #include <x86intrin.h>
 
+#include <algorithm>
 #include <fstream>
 
 #include "engine.h"
@@ -188,6 +189,26 @@ static long finalize_read(const IoReq &r, uint8_t *dst, uint32_t len, long got) 
 }
 
 // ------------------------------------------------------------------ worker
+// Phase attribution of a worker's loop (config io_prof): every TSC cycle of
+// the loop is charged to exactly one phase ("lap" timer), so the phases sum
+// to the worker's wall time.
+enum ProfPhase {
+  PF_IDLE,     // idle spin + sleeping for work
+  PF_TAKE,     // taking the queue (lock + swap)
+  PF_START,    // preparing reads (SQEs, staging slots)
+  PF_SUBMIT,   // io_uring_enter to submit (page-cache reads copy in here)
+  PF_REAP,     // CQE handling, read finalisation
+  PF_BAR,      // CPU stores through the large BAR
+  PF_POST,     // ingest descriptors (lock + stores)
+  PF_HDP,      // sfence + HDP flush, once per batch and mapping
+  PF_FINISH,   // publishing a batch: stats, mapping counts, task puts
+  PF_RETIRE,   // polling ingest done words / SDMA events
+  PF_WAIT,     // blocked on a read or an HBM copy
+};
+static_assert(PF_WAIT + 1 == IoEngine::kProfPhases, "phase count");
+enum ProfCount { PC_REQ, PC_BATCH, PC_ENTER, PC_SLEEP, PC_DESC };
+static_assert(PC_DESC + 1 == IoEngine::kProfCounts, "count count");
+
 struct IoEngine::Worker {
   struct Slot {
     uint8_t *buf = nullptr;
@@ -199,6 +220,7 @@ struct IoEngine::Worker {
     Ingest *ing = nullptr;   // ingest descriptors seq_first .. + nseq - 1
     uint64_t seq_first = 0;
     uint32_t nseq = 0;
+    uint32_t nret = 0;   // descriptors this slot reports retired (run head)
   };
   struct Ctx {           // one in-flight storage read
     IoReq req;
@@ -226,6 +248,7 @@ struct IoEngine::Worker {
   }
 
   void reap_fake() {
+    now_ns = mono_ns();
     while (!fake_cq.empty()) {
       const size_t i = (size_t)(fake_rand() % fake_cq.size());
       Ctx c = fake_cq[i];
@@ -237,6 +260,7 @@ struct IoEngine::Worker {
       fake_next = c.seq + 1;
       on_read_done(c, c.got);
     }
+    post_ingest();
     flush_staged();
   }
 
@@ -245,7 +269,8 @@ struct IoEngine::Worker {
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<IoReq> q;
+  std::vector<IoReq> q;             // handed over in slices (one copy, no
+                                    // per-request allocation)
   bool stop = false;
   bool sleeping = false;            // in cv.wait (guarded by mu)
   std::atomic<int> pending{0};      // q non-empty hint for the idle spin
@@ -257,8 +282,11 @@ struct IoEngine::Worker {
   std::deque<int> free_slots;     // FIFO: consecutive requests get adjacent slots
   std::deque<int> copying;        // FIFO of slots with copies in flight
   std::vector<int> staged;        // reads done, HBM copy not yet issued
+  std::vector<int> ing_staged;    // reads done, ingest descriptor not yet posted
   std::vector<int> ingesting;     // slots whose bytes the ingest grid is pulling
   std::vector<std::pair<int, Ingest *>> ings;  // device -> ingest grid (or null)
+  std::vector<Ingest::Run> runs;  // post_ingest scratch: ranges and their
+  std::vector<std::pair<size_t, size_t>> span;  // [lo, hi) in ing_staged
   std::vector<hipStream_t> streams;
   int cur_dev = -2;
   Uring ring;
@@ -266,6 +294,122 @@ struct IoEngine::Worker {
   std::vector<int> free_ctx;
   int reads_inflight = 0;
   int numa_node = -1;
+  uint64_t now_ns = 0;            // one clock read per batch of completions
+
+  // ---- completion batching.  Requests finished in one pass of the loop are
+  // published together by flush_done(): one RMW per task, per mapping and per
+  // counter for the batch, and one sfence + HDP flush per mapping for all its
+  // BAR stores.  Per request these were ~8 RMWs on lines shared with the
+  // submitter and the other workers.
+  struct Fin {
+    Task *task;
+    GpuMapping *gmap;
+    long status;
+    long *status_out;
+  };
+  std::vector<Fin> fin;
+  uint64_t fin_clk = 0;           // sum of (completion - submission) TSC cycles
+  std::vector<std::pair<GpuMapping *, const uint8_t *>> bar_dirty;
+  uint32_t nbar = 0;              // BAR-stored requests in this batch
+  uint64_t ndesc = 0;             // HBM copies / ingest descriptors issued
+  uint64_t copy_clk = 0;
+  uint32_t lh_io[STROM_HIST_BUCKETS] = {}, lh_copy[STROM_HIST_BUCKETS] = {};
+  uint64_t lh_io_mask = 0, lh_copy_mask = 0;
+
+  // ---- attribution (config io_prof), read racily by IoEngine::prof
+  bool prof_on = false;
+  uint64_t prof_t = 0;
+  uint64_t prof_cyc[kProfPhases] = {};
+  uint64_t prof_cnt[kProfCounts] = {};
+  void lap(int k) {
+    if (__builtin_expect(prof_on, 0)) {
+      const uint64_t t = tsc_now();
+      prof_cyc[k] += t - prof_t;
+      prof_t = t;
+    }
+  }
+
+  void hist_io(uint64_t ns) {
+    const int b = Hist::bucket(ns);
+    ++lh_io[b];
+    lh_io_mask |= 1ull << b;
+  }
+  void hist_copy(uint64_t ns, uint32_t n = 1) {
+    const int b = Hist::bucket(ns);
+    lh_copy[b] += n;
+    lh_copy_mask |= 1ull << b;
+  }
+
+  void complete(const IoReq &r, long status) {
+    fin.push_back(Fin{r.task, r.gmap, status, r.status_out});
+    fin_clk += tsc_now() - r.t_submit_tsc;
+  }
+
+  void flush_done() {
+    if (fin.empty()) return;
+    for (auto &b : bar_dirty) b.first->bar_flush(b.second);
+    bar_dirty.clear();
+    if (nbar) {
+      hist_copy(mono_ns() - now_ns, nbar);
+      nbar = 0;
+    }
+    lap(PF_HDP);
+    Stats &st = stats();
+    const uint64_t n = fin.size();
+    st.nr_ssd2gpu.fetch_add(n, std::memory_order_relaxed);
+    st.clk_ssd2gpu.fetch_add(fin_clk, std::memory_order_relaxed);
+    st.inflight_dec(n);
+    fin_clk = 0;
+    if (ndesc) {
+      st.nr_debug[0].fetch_add(ndesc, std::memory_order_relaxed);
+      st.clk_debug[0].fetch_add(copy_clk, std::memory_order_relaxed);
+      ndesc = copy_clk = 0;
+    }
+    for (uint64_t m = lh_io_mask; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      st.io_ns.b[b].fetch_add(lh_io[b], std::memory_order_relaxed);
+      lh_io[b] = 0;
+    }
+    for (uint64_t m = lh_copy_mask; m; m &= m - 1) {
+      const int b = __builtin_ctzll(m);
+      st.copy_ns.b[b].fetch_add(lh_copy[b], std::memory_order_relaxed);
+      lh_copy[b] = 0;
+    }
+    lh_io_mask = lh_copy_mask = 0;
+    // mappings first: a task's last put may drop the mapping's last owner
+    for (size_t i = 0; i < fin.size();) {
+      GpuMapping *g = fin[i].gmap;
+      size_t j = i + 1;
+      while (j < fin.size() && fin[j].gmap == g) ++j;
+      if (g) {
+        const int k = (int)(j - i);
+        if (g->inflight.fetch_sub(k) == k && g->draining.load()) {
+          std::lock_guard<std::mutex> lk(g->mu);
+          g->cv.notify_all();
+        }
+      }
+      i = j;
+    }
+    for (size_t i = 0; i < fin.size();) {
+      Task *t = fin[i].task;
+      long status = fin[i].status;
+      size_t j = i + 1;
+      if (t) {
+        while (j < fin.size() && fin[j].task == t) {
+          if (!status) status = fin[j].status;
+          ++j;
+        }
+        tasks().put_n(t, (int)(j - i), status);
+      } else if (fin[i].status_out) {
+        *fin[i].status_out = status;
+      }
+      i = j;
+    }
+    prof_cnt[PC_REQ] += n;
+    ++prof_cnt[PC_BATCH];
+    fin.clear();
+    lap(PF_FINISH);
+  }
 
   void bind_numa() {
     if (!cfg.numa_bind || numa_node < 0) return;
@@ -298,15 +442,16 @@ struct IoEngine::Worker {
   }
 
   // staging slots (each max_request bytes): at least staging_slots; small
-  // requests get up to queue_depth slots within the same in-flight byte
-  // budget (staging_slots x 1 MiB), so a 16-128 KiB stream keeps the queue
-  // as deep as the raw ceiling's (round 2 sweep: 4 slots capped 64 KiB
-  // reads at 0.72 of raw); staging_bytes opts into more
+  // requests get up to 4 x queue_depth slots within the same in-flight byte
+  // budget (staging_slots x 1 MiB), so reads keep the queue as deep as the
+  // raw ceiling's while earlier slots are still on their way to HBM (round 2
+  // sweep: 4 slots capped 64 KiB reads at 0.72 of raw); staging_bytes opts
+  // into more
   int nslots() const {
     const size_t budget = (size_t)cfg.staging_slots << 20;
-    const size_t small = std::min<size_t>((size_t)cfg.queue_depth, budget / cfg.max_request);
+    const size_t small = std::min<size_t>((size_t)cfg.queue_depth * 4, budget / cfg.max_request);
     const size_t by_bytes = std::min<size_t>(cfg.staging_bytes / cfg.max_request, 256);
-    return (int)std::max<size_t>(cfg.staging_slots, std::max(small, by_bytes));
+    return (int)std::min<size_t>(256, std::max<size_t>(cfg.staging_slots, std::max(small, by_bytes)));
   }
 
   bool ensure_slots() {
@@ -376,6 +521,7 @@ struct IoEngine::Worker {
   // retire slots whose ingest descriptors are all done
   bool retire_ingest() {
     bool any = false;
+    uint64_t now = 0;
     for (size_t i = 0; i < ingesting.size();) {
       const int si = ingesting[i];
       Slot &s = slots[si];
@@ -385,14 +531,15 @@ struct IoEngine::Worker {
         ++i;
         continue;
       }
-      const uint64_t dt = mono_ns() - s.t_copy_ns;
-      stats().copy_ns.add(dt);
-      stats().clk_debug[0].fetch_add(dt, std::memory_order_relaxed);
-      s.ing->retired(s.nseq);
+      if (!now) now = mono_ns();
+      const uint64_t dt = now - s.t_copy_ns;
+      hist_copy(dt);
+      copy_clk += dt;
+      if (s.nret) s.ing->retired(s.nret);
       ingesting[i] = ingesting.back();
       ingesting.pop_back();
       free_slots.push_back(si);
-      finish_request(s.req, 0);
+      complete(s.req, 0);
       any = true;
     }
     return any;
@@ -401,48 +548,114 @@ struct IoEngine::Worker {
   // storage read finished for ctx c with `got` bytes or -errno
   void on_read_done(Ctx &c, long got) {
     IoReq &r = c.req;
-    uint64_t now = mono_ns();
-    stats().io_ns.add(now - c.t0);
+    hist_io(now_ns - c.t0);
     long status = finalize_read(r, c.dst, c.len, got);
     if (c.slot < 0) {
-      finish_request(r, status);
+      complete(r, status);
       return;
     }
     Slot &s = slots[c.slot];
     if (status != 0) {
       free_slots.push_back(c.slot);
-      finish_request(r, status);
+      complete(r, status);
       return;
     }
-    if (Ingest *ing = r.gmap ? ingest_for(r.device) : nullptr) {
-      uint64_t first = 0;
-      uint32_t n = 0;
-      if (ing->post_many(c.dst, r.gpu_dst, r.len, cfg.ingest_piece, &first, &n)) {
-        s.req = r;
-        s.t_copy_ns = now;
-        s.ing = ing;
-        s.seq_first = first;
-        s.nseq = n;
-        ingesting.push_back(c.slot);
-        stats().nr_debug[0].fetch_add(n, std::memory_order_relaxed);
-        return;
-      }
+    s.req = r;
+    s.t_copy_ns = now_ns;
+    if (r.gmap && r.len >= cfg.ingest_min && ingest_for(r.device)) {
+      ing_staged.push_back(c.slot);  // posted per batch (post_ingest)
+      return;
     }
+    to_hbm(c.slot);
+  }
+
+  // the slot's bytes reach HBM without the ingest grid: CPU stores through
+  // the BAR (small requests) or a staged SDMA copy (flush_staged)
+  void to_hbm(int si) {
+    Slot &s = slots[si];
+    const IoReq &r = s.req;
     // worker requests take the BAR only up to 64 KiB: past that the workers'
     // CPU stores fall behind SDMA (256 KiB: 14.2 vs 17.8 GiB/s, 512 KiB: 23.7
     // vs 26.5, profiles/r1j/sweep_barmax_*); synchronous reads keep bar_max
     constexpr uint32_t kWorkerBarMax = 64u << 10;
-    if (r.len <= std::min(cfg.bar_max, kWorkerBarMax) && r.gmap &&
-        r.gmap->bar_write(r.gpu_dst, c.dst, r.len)) {
-      // small request: CPU stores through the large BAR beat an SDMA round trip
-      stats().copy_ns.add(mono_ns() - now);
-      free_slots.push_back(c.slot);
-      finish_request(r, 0);
-      return;
+    if (r.len <= std::min(cfg.bar_max, kWorkerBarMax) && r.gmap) {
+      lap(PF_REAP);
+      const bool ok = r.gmap->bar_write(r.gpu_dst, s.buf, r.len, false);
+      lap(PF_BAR);
+      if (ok) {
+        // small request: CPU stores through the large BAR beat an SDMA round
+        // trip; the sfence + HDP flush is paid once per batch (flush_done)
+        const uint8_t *last = r.gmap->bar + (r.gpu_dst - r.gmap->bar_va) + ((r.len - 1) & ~3u);
+        if (!bar_dirty.empty() && bar_dirty.back().first == r.gmap) bar_dirty.back().second = last;
+        else bar_dirty.emplace_back(r.gmap, last);
+        ++nbar;
+        ++ndesc;
+        free_slots.push_back(si);
+        complete(r, 0);
+        return;
+      }
     }
-    s.req = r;
-    s.t_copy_ns = now;
-    staged.push_back(c.slot);
+    staged.push_back(si);
+  }
+
+  // Post the ingest descriptors of the reads that finished in this batch:
+  // adjacent staging slots whose destinations are adjacent in HBM go out as
+  // one range (split into ingest_piece descriptors), and the whole batch
+  // takes the grid's lock once.
+  void post_ingest() {
+    if (ing_staged.empty()) return;
+    lap(PF_REAP);
+    std::sort(ing_staged.begin(), ing_staged.end());
+    size_t i = 0;
+    while (i < ing_staged.size()) {
+      // one device per post_runs call
+      const int dev = slots[ing_staged[i]].req.device;
+      Ingest *ing = ingest_for(dev);
+      runs.clear();
+      span.clear();
+      size_t k = i;
+      while (k < ing_staged.size() && slots[ing_staged[k]].req.device == dev) {
+        size_t j = k + 1;
+        uint64_t bytes = slots[ing_staged[k]].req.len;
+        while (cfg.coalesce && j < ing_staged.size()) {
+          const Slot &p = slots[ing_staged[j - 1]], &q2 = slots[ing_staged[j]];
+          if (ing_staged[j] != ing_staged[j - 1] + 1 || p.req.len != cfg.max_request ||
+              q2.req.device != dev || q2.req.gpu_dst != p.req.gpu_dst + p.req.len ||
+              bytes + q2.req.len > (64u << 20))
+            break;
+          bytes += q2.req.len;
+          ++j;
+        }
+        const Slot &h = slots[ing_staged[k]];
+        runs.push_back(Ingest::Run{h.buf, h.req.gpu_dst, (uint32_t)bytes, false, 0, 0});
+        span.emplace_back(k, j);
+        k = j;
+      }
+      ing->post_runs(runs.data(), runs.size(), cfg.ingest_piece);
+      for (size_t r = 0; r < runs.size(); ++r) {
+        const Ingest::Run &run = runs[r];
+        for (size_t m = span[r].first; m < span[r].second; ++m) {
+          const int si = ing_staged[m];
+          if (!run.ok) {
+            to_hbm(si);
+            continue;
+          }
+          Slot &s = slots[si];
+          s.ing = ing;
+          s.seq_first = run.first;
+          s.nseq = run.n;
+          s.nret = m == span[r].first ? run.n : 0;
+          ingesting.push_back(si);
+        }
+        if (run.ok) {
+          ndesc += run.n;
+          prof_cnt[PC_DESC] += run.n;
+        }
+      }
+      i = k;
+    }
+    ing_staged.clear();
+    lap(PF_POST);
   }
 
   // Issue the HBM copies of the reads that finished in this batch.  Reads of
@@ -482,14 +695,14 @@ struct IoEngine::Worker {
         const int si = staged[k];
         if (e != hipSuccess) {
           free_slots.push_back(si);
-          finish_request(slots[si].req, -EIO);
+          complete(slots[si].req, -EIO);
           continue;
         }
         slots[si].ev_slot = last;
         copying.push_back(si);
       }
       if (e != hipSuccess) STROM_LOG(0, "hipMemcpyAsync failed: %s", hipGetErrorString(e));
-      else stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+      else ++ndesc;
       i = j;
     }
     staged.clear();
@@ -503,12 +716,12 @@ struct IoEngine::Worker {
       hipError_t e = block ? hipEventSynchronize(ev) : hipEventQuery(ev);
       if (e == hipErrorNotReady) return;
       uint64_t dt = mono_ns() - s.t_copy_ns;
-      stats().copy_ns.add(dt);
-      stats().clk_debug[0].fetch_add(dt, std::memory_order_relaxed);
+      hist_copy(dt);
+      copy_clk += dt;
       int si = copying.front();
       copying.pop_front();
       free_slots.push_back(si);
-      finish_request(s.req, e == hipSuccess ? 0 : -EIO);
+      complete(s.req, e == hipSuccess ? 0 : -EIO);
       block = false;
     }
   }
@@ -519,7 +732,7 @@ struct IoEngine::Worker {
     uint8_t *dst = r.host_dst;
     if (!dst) {
       if (!ensure_slots()) {
-        finish_request(r, -ENOMEM);
+        complete(r, -ENOMEM);
         return true;
       }
       if (free_slots.empty()) return false;
@@ -539,9 +752,10 @@ struct IoEngine::Worker {
     c.slot = slot;
     c.dst = dst;
     c.len = len;
-    c.t0 = mono_ns();
+    c.t0 = now_ns;
     if (frc && cfg.backend != BackendKind::kFake) {
       on_read_done(c, frc);
+      post_ingest();
       flush_staged();
       return true;
     }
@@ -582,7 +796,9 @@ struct IoEngine::Worker {
       return true;
     }
     long got = pread_full(read_fd(r), dst, len, r.off);
+    now_ns = mono_ns();
     on_read_done(c, got);
+    post_ingest();
     flush_staged();
     return true;
   }
@@ -592,7 +808,12 @@ struct IoEngine::Worker {
 
   void reap() {
     io_uring_cqe cqe;
+    bool first = true;
     while (ring.peek(&cqe)) {
+      if (first) {
+        now_ns = mono_ns();
+        first = false;
+      }
       int ci = (int)cqe.user_data;
       Ctx c = ctx[ci];
       free_ctx.push_back(ci);
@@ -605,21 +826,30 @@ struct IoEngine::Worker {
       }
       on_read_done(c, got);
     }
+    post_ingest();
     flush_staged();
+    lap(PF_REAP);
   }
 
   void run() {
     bind_numa();
     const bool fake = cfg.backend == BackendKind::kFake;
     bool use_ring = cfg.backend == BackendKind::kUring || cfg.backend == BackendKind::kCache;
-    const int qd_cfg = std::max(cfg.queue_depth, nslots());
+    // reads in flight: queue_depth, or the staging_bytes opt-in's slot count
+    const int qd_cfg = (int)std::max<size_t>(
+        {(size_t)cfg.queue_depth, (size_t)cfg.staging_slots,
+         std::min<size_t>(cfg.staging_bytes / cfg.max_request, 256)});
     if (use_ring && ring.init((unsigned)std::max(8, qd_cfg * 2)) != 0) use_ring = false;
     int qd = use_ring || fake ? qd_cfg : 1;
     fake_rng = faults().fake_seed.load() * 2654435761u + (uint64_t)idx * 0x9E3779B97F4A7C15ull + 1;
     const uint64_t spin_ns = (uint64_t)cfg.spin_us * 1000;
-    std::deque<IoReq> local;
+    prof_on = cfg.io_prof;
+    prof_t = tsc_now();
+    std::vector<IoReq> local;
+    size_t lpos = 0;                // next request of `local` to start
     for (;;) {
-      if (local.empty()) {
+      flush_done();
+      if (lpos == local.size()) {
         const bool quiet = reads_inflight == 0 && copying.empty() && ingesting.empty();
         if (spin_ns && quiet && !pending.load(std::memory_order_acquire)) {
           // idle: poll briefly before sleeping, so back-to-back work skips
@@ -634,31 +864,47 @@ struct IoEngine::Worker {
           for (auto &p : ings)
             if (p.second) p.second->idle();
         }
+        lap(PF_IDLE);
         std::unique_lock<std::mutex> g(mu);
         if (q.empty() && quiet) {
           if (stop) break;
           sleeping = true;
+          ++prof_cnt[PC_SLEEP];
           cv.wait(g, [&] { return stop || !q.empty(); });
           sleeping = false;
+          lap(PF_IDLE);
         }
+        local.clear();
+        lpos = 0;
         local.swap(q);
         pending.store(0, std::memory_order_relaxed);
+        g.unlock();
+        lap(PF_TAKE);
       }
       // issue as much as the queue depth and staging allow
       bool blocked = false;
-      while (!local.empty() && reads_inflight < qd) {
-        if (!start(local.front(), use_ring)) {
+      now_ns = mono_ns();
+      while (lpos < local.size() && reads_inflight < qd) {
+        if (!start(local[lpos], use_ring)) {
           blocked = true;
           break;
         }
-        local.pop_front();
+        ++lpos;
       }
-      if (use_ring && ring.pending()) ring.enter(0);
-      if (fake && (local.empty() || blocked || reads_inflight >= qd)) reap_fake();
+      lap(PF_START);
+      if (use_ring && ring.pending()) {
+        ring.enter(0);
+        ++prof_cnt[PC_ENTER];
+        lap(PF_SUBMIT);
+      }
+      const bool drained = lpos == local.size();
+      if (fake && (drained || blocked || reads_inflight >= qd)) reap_fake();
       retire(false);
       retire_ingest();
+      lap(PF_RETIRE);
       if (use_ring) reap();
-      if (!local.empty() && !blocked && reads_inflight < qd) continue;
+      flush_done();
+      if (lpos < local.size() && !blocked && reads_inflight < qd) continue;
       // nothing more can start: wait for a read, a copy, or new work
       const bool hbm_busy = !copying.empty() || !ingesting.empty();
       if (reads_inflight > 0 && !hbm_busy) {
@@ -666,10 +912,12 @@ struct IoEngine::Worker {
           reap_fake();
         } else {
           ring.enter(1);
+          ++prof_cnt[PC_ENTER];
+          lap(PF_WAIT);
           reap();
         }
       } else if (reads_inflight == 0 && hbm_busy) {
-        if (local.empty()) {
+        if (lpos == local.size()) {
           std::lock_guard<std::mutex> g(mu);
           if (!q.empty()) continue;
         }
@@ -682,11 +930,14 @@ struct IoEngine::Worker {
             if (pending.load(std::memory_order_acquire)) break;
           }
           retire(false);
+          lap(PF_WAIT);
         } else {
           retire(true);
+          lap(PF_WAIT);
         }
       } else if (reads_inflight > 0) {
         if (!retire_ingest()) sched_yield();  // both pipes busy
+        lap(PF_WAIT);
       }
     }
     for (auto &s : slots)
@@ -696,6 +947,28 @@ struct IoEngine::Worker {
       if (st) (void)hipStreamDestroy(st);
   }
 };
+
+int IoEngine::prof(uint64_t *out, int nout, bool reset) {
+  const int need = 2 + kProfPhases + kProfCounts + 4;
+  if (nout < need) return -EINVAL;
+  memset(out, 0, sizeof(uint64_t) * need);
+  out[0] = workers_.size();
+  out[1] = tsc_khz();
+  for (auto &w : workers_) {
+    for (int k = 0; k < kProfPhases; ++k) {
+      out[2 + k] += w->prof_cyc[k];
+      if (reset) w->prof_cyc[k] = 0;
+    }
+    for (int k = 0; k < kProfCounts; ++k) {
+      out[2 + kProfPhases + k] += w->prof_cnt[k];
+      if (reset) w->prof_cnt[k] = 0;
+    }
+  }
+  CallerProf &cp = caller_prof();
+  std::atomic<uint64_t> *c[4] = {&cp.calls, &cp.plan, &cp.build, &cp.submit};
+  for (int k = 0; k < 4; ++k) out[2 + kProfPhases + kProfCounts + k] = reset ? c[k]->exchange(0) : c[k]->load();
+  return need;
+}
 
 IoEngine::IoEngine(const Config &cfg) {
   int node = -1;
@@ -779,6 +1052,10 @@ void IoEngine::run_inline(IoReq &r) {
     for (uint32_t k = 0; k < nseq; ++k)
       while (!ing->is_done(first + k)) _mm_pause();
     ing->retired(nseq);
+    // no worker may go idle after this (the task never reached one): stop
+    // the grid here if nothing else is outstanding, or a device-wide
+    // synchronize would wait on it forever
+    ing->idle();
     phase_mark(4);
     stats().copy_ns.add(mono_ns() - t1);
     stats().nr_debug[0].fetch_add(nseq, std::memory_order_relaxed);
@@ -813,7 +1090,7 @@ void IoEngine::submit(std::vector<IoReq> &reqs) {
     bool wake;
     {
       std::lock_guard<std::mutex> g(w.mu);
-      for (size_t i = lo; i < hi; ++i) w.q.push_back(reqs[i]);
+      w.q.insert(w.q.end(), reqs.begin() + lo, reqs.begin() + hi);
       w.pending.store(1, std::memory_order_release);
       wake = w.sleeping;
     }
@@ -822,6 +1099,12 @@ void IoEngine::submit(std::vector<IoReq> &reqs) {
 }
 
 }  // namespace strom
+
+// per-worker phase attribution (IoEngine::prof); -ENODEV before the engine
+// exists, else the number of u64 written
+extern "C" int strom_io_prof(uint64_t *out, int nout, int reset) {
+  return strom::engine().io().prof(out, nout, reset != 0);
+}
 
 // workers whose staging is registered (READ_FIXED), refusals, last errno
 extern "C" int strom_io_info(uint64_t *out) {

@@ -127,6 +127,15 @@ int strom_gpu_pci_bdf(int device, char *buf, size_t len);
  * posted, descriptors outstanding}.  -ENODEV when it cannot run there. */
 int strom_ingest_info(int device, uint64_t *out);
 
+/* Worker phase attribution (config io_prof=1): out[0] workers, out[1] TSC
+ * kHz, out[2..12] TSC cycles summed over the workers per phase (idle, take,
+ * start, submit, reap, bar, post, hdp, finish, retire, wait), out[13..17]
+ * counts (requests, batches, io_uring_enter calls, sleeps, HBM
+ * descriptors), out[18..21] the submitting side (SSD2GPU/SSD2RAM calls and
+ * TSC cycles planning, building requests, handing them over).  reset != 0
+ * zeroes them.  Returns the number of u64 written (22) or -errno. */
+int strom_io_prof(uint64_t *out, int nout, int reset);
+
 /* ---- configuration (env STROM_<KEY> is read at first use) ------------- */
 int strom_config_set(const char *key, const char *value);
 int strom_config_get(const char *key, char *buf, size_t buflen);

@@ -8,7 +8,7 @@
 // capped 4-128 KiB streams at 65-75% of the storage rate.  Here the copy is
 // PULLED by the GPU: a small persistent grid polls a descriptor ring in
 // fine-grained host memory, copies each staged range over PCIe with 16-byte
-// loads (32 KiB in flight per workgroup), and publishes completion into a
+// loads (16 KiB in flight per wave), and publishes completion into a
 // host-memory done[] word.  Posting a request costs the host one 32-byte
 // store sequence; no HIP API call, no syscall.
 //
@@ -16,12 +16,12 @@
 //   ring[s % nslots] = {src, dst, len, seq = s + 1}   host stores seq last
 //   done[s % nslots] = s + 1                          device, after the bytes
 //                                                     are written through to HBM
-//   *stop != 0                                        every waiting workgroup exits
-// A workgroup claims the next sequence number from a device counter, waits
-// for the host to post it (or for stop), copies, and publishes.  Payload
-// stores are write-through (sc1: the line leaves this XCD's L2), every wave
-// drains its stores (s_waitcnt vmcnt(0)), the workgroup meets at a barrier,
-// then one lane stores done[] at system scope: the valid hand-off form of
+//   *stop != 0                                        every waiting wave exits
+// A wave claims the next sequence number from a device counter, waits for
+// the host to post it (or for stop), copies, and publishes.  Payload stores
+// are write-through (sc1: the line leaves this XCD's L2), the wave drains
+// its stores (s_waitcnt vmcnt(0)), then its lane 0 stores done[] at system
+// scope: the valid hand-off form of
 // MI355X_MICROARCH.md §visibility without an L2 write-back of the whole XCD
 // (other kernels' dirty lines are not ours to flush).
 //
@@ -57,25 +57,38 @@ struct IngestDesc {          // 32 bytes, ingest.cc writes the same layout
   uint64_t seq;              // s + 1 once posted
 };
 
-constexpr int kThreads = 256;
-constexpr int kUnroll = 8;   // 16-B loads in flight per lane
-constexpr int kAuxSc1 = 16;  // buffer store cache policy: sc1 (write-through)
+constexpr int kThreads = 256;  // 4 waves, each an independent copier
+constexpr int kUnroll = 16;    // 16-B loads in flight per lane (16 KiB per wave)
+constexpr int kAuxSc1 = 16;    // buffer store cache policy: sc1 (write-through)
 
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// readfirstlane returns int: both halves go through uint32_t, or the low
+// word's bit 31 would sign-extend over the high word
+__device__ __forceinline__ uint64_t bcast64(uint64_t v) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Every WAVE claims, copies and publishes descriptors on its own: a 4 KiB
+// request is one 16-B load per lane of one wave, so the grid keeps 4x as
+// many small descriptors in flight as a workgroup-wide claim did (round 4:
+// 2.3 M descriptors/s from 8 workers queued behind 16 one-at-a-time
+// workgroups, profiles/r4/engine).  Large descriptors move 16 KiB per wave
+// per round trip.
 __global__ __launch_bounds__(kThreads) void ingest_kernel(const IngestDesc *ring, uint64_t *done,
                                                           const uint64_t *stop, uint32_t *next,
                                                           uint32_t nslots, uint64_t base) {
-  __shared__ uint64_t s_src, s_dst, s_seq;
-  __shared__ uint32_t s_len;
-  __shared__ int s_ok;
+  const uint32_t lane = threadIdx.x & 63;
   for (;;) {
-    if (threadIdx.x == 0) {
-      const uint64_t s = base + atomicAdd(next, 1u);
+    uint64_t s = 0, src = 0, dst = 0, len = 0;
+    int ok = 0;
+    if (lane == 0) {
+      s = base + atomicAdd(next, 1u);
       const IngestDesc *d = ring + (s % nslots);
-      int ok = 0;
       for (uint32_t spin = 0;; ++spin) {
         if (ld_sys(&d->seq) == s + 1) {
           ok = 1;
@@ -88,45 +101,39 @@ __global__ __launch_bounds__(kThreads) void ingest_kernel(const IngestDesc *ring
       // the field loads below are issued after the seq load returned
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (ok) {
-        s_src = ld_sys(&d->src);
-        s_dst = ld_sys(&d->dst);
-        s_len = (uint32_t)ld_sys(&d->len_tag);
+        src = ld_sys(&d->src);
+        dst = ld_sys(&d->dst);
+        len = ld_sys(&d->len_tag);
       }
-      s_seq = s;
-      s_ok = ok;
     }
-    __syncthreads();
-    if (!s_ok) return;  // uniform: stop requested
-    gv4u *src = (gv4u *)s_src;
-    const uint32_t n16 = s_len >> 4;
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    if (!ok) return;  // wave-uniform: stop requested
+    s = bcast64(s);
+    src = bcast64(src);
+    dst = bcast64(dst);
+    const uint32_t nbytes = __builtin_amdgcn_readfirstlane((uint32_t)len);
+    gv4u *sp = (gv4u *)src;
+    const uint32_t n16 = nbytes >> 4;
     // wave-uniform descriptor for the destination (SGPRs: no waterfall loop)
-    const uint64_t dst = s_dst;
-    const uint32_t dlo = __builtin_amdgcn_readfirstlane((uint32_t)dst);
-    const uint32_t dhi = __builtin_amdgcn_readfirstlane((uint32_t)(dst >> 32));
-    const uint32_t nbytes = __builtin_amdgcn_readfirstlane(s_len);
-    __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(((uint64_t)dhi << 32) | dlo), (short)0, (int)nbytes, 0x00020000);
-    for (uint32_t i = threadIdx.x; i < n16; i += kThreads * kUnroll) {
+    __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)dst, (short)0, (int)nbytes, 0x00020000);
+    for (uint32_t i = lane; i < n16; i += 64 * kUnroll) {
       v4u r[kUnroll];
 #pragma unroll
       for (int k = 0; k < kUnroll; ++k) {
-        const uint32_t idx = i + k * kThreads;
-        if (idx < n16) r[k] = __builtin_nontemporal_load(src + idx);
+        const uint32_t idx = i + k * 64;
+        if (idx < n16) r[k] = __builtin_nontemporal_load(sp + idx);
       }
 #pragma unroll
       for (int k = 0; k < kUnroll; ++k) {
-        const uint32_t idx = i + k * kThreads;
+        const uint32_t idx = i + k * 64;
         if (idx < n16) __builtin_amdgcn_raw_buffer_store_b128(r[k], rsrc, (int)(idx * 16), 0, kAuxSc1);
       }
     }
-    // every storing wave drains its write-through stores, then one lane publishes
+    // the wave drains its own write-through stores, then one lane publishes
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint64_t s = s_seq;
+    if (lane == 0)
       __hip_atomic_store(done + (s % nslots), s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();  // s_* are rewritten by the next claim
   }
 }
 

@@ -140,6 +140,33 @@ def io_info() -> dict:
     return dict(fixed_workers=int(out[0]), fixed_refused=int(out[1]), fixed_errno=int(out[2]))
 
 
+IO_PROF_PHASES = ("idle", "take", "start", "submit", "reap", "bar", "post", "hdp", "finish",
+                  "retire", "wait")
+IO_PROF_COUNTS = ("requests", "batches", "enters", "sleeps", "descriptors")
+
+
+def io_prof(reset: bool = False) -> dict:
+    """Per-worker phase attribution of the I/O workers (needs
+    ``configure(io_prof=1)`` before the engine starts): for every phase of
+    the worker loop the summed time in ns, plus ns per completed request,
+    and the submitting thread's plan / build / submit time
+    (``csrc/engine/io.cc`` ProfPhase)."""
+    n = 2 + len(IO_PROF_PHASES) + len(IO_PROF_COUNTS) + 4
+    out = np.zeros(n, dtype=np.uint64)
+    _check(N.lib().strom_io_prof(out.ctypes.data, n, 1 if reset else 0), "io_prof")
+    khz = max(int(out[1]), 1)
+    ns = {k: int(out[2 + i]) * 1e6 / khz for i, k in enumerate(IO_PROF_PHASES)}
+    cnt = {k: int(out[2 + len(IO_PROF_PHASES) + i]) for i, k in enumerate(IO_PROF_COUNTS)}
+    req = max(cnt["requests"], 1)
+    c0 = 2 + len(IO_PROF_PHASES) + len(IO_PROF_COUNTS)
+    caller = dict(calls=int(out[c0]), **{k: round(int(out[c0 + 1 + i]) * 1e6 / khz / req, 1)
+                                         for i, k in enumerate(("plan_ns_per_req", "build_ns_per_req",
+                                                                "submit_ns_per_req"))})
+    return dict(workers=int(out[0]), tsc_khz=khz, ns=ns, counts=cnt, caller=caller,
+                ns_per_req={k: round(v / req, 1) for k, v in ns.items()},
+                busy_ns_per_req=round(sum(v for k, v in ns.items() if k != "idle") / req, 1))
+
+
 HOST_COSTS = ("clock_gettime", "rdtsc", "fstat", "mincore", "syscall", "mutex", "cv_notify")
 
 

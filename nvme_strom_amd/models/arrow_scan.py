@@ -366,11 +366,16 @@ class ArrowScan:
             s.event.synchronize()            # the slot's previous group is consumed
             s.event = None
         s.keep = []
-        wb = None
-        if self.reader._direct_ram is False:  # page-cache chunks go through host memory
-            if self._wbs[k % len(self._wbs)] is None:
-                self._wbs[k % len(self._wbs)] = host_buffer(self._wb_bytes)
-            wb = self._wbs[k % len(self._wbs)]
+        # the slot's own write-back buffer, sized for this scan's groups and
+        # pinned only if page-cache chunks have to go through host memory
+        # (a group may outgrow the reader's own buffer, and slots in flight
+        # must not share one)
+        i = k % len(self._wbs)
+
+        def wb():
+            if self._wbs[i] is None:
+                self._wbs[i] = host_buffer(self._wb_bytes)
+            return self._wbs[i]
         res, landed = self.reader.submit(self._hbm, s.off, g.ids.astype(np.uint32), wb=wb)
         s.pending = (res, landed, g)
 

@@ -105,7 +105,12 @@ class FileReader:
     def submit(self, buf: HbmBuffer, offset: int, chunk_ids, wb: Optional[torch.Tensor] = None):
         """Start a copy; returns (CopyResult, landed ids).  Caller must
         ``finish()`` it.  ``wb`` overrides the reader's write-back buffer
-        (needed when several submissions are in flight)."""
+        (needed when several submissions are in flight); it may be a
+        callable returning the buffer, called only when page-cache chunks
+        have to go through host memory (the BAR refused them)."""
+        wb_fn = wb if callable(wb) else None
+        if wb_fn is not None:
+            wb = None
         ids = np.array(chunk_ids, dtype=np.uint32, copy=True)
         if self._direct_ram is not False:
             # page-cache chunks straight into HBM through the large BAR
@@ -120,6 +125,8 @@ class FileReader:
                     raise
                 self._direct_ram = False
                 ids = np.array(chunk_ids, dtype=np.uint32, copy=True)
+        if wb is None and wb_fn is not None:
+            wb = wb_fn()
         if len(ids) > self.max_chunks and wb is None:
             raise ValueError("too many chunks for the write-back buffer")
         wbt = self._wb if wb is None else wb

@@ -83,6 +83,10 @@ def main(argv=None) -> int:
     ap.add_argument("--ab", default="",
                     help="config key to A/B at every size: KEY (0 vs 1) or KEY=v1,v2,..")
     ap.add_argument("--reps", type=int, default=1, help="repetitions of every (size, arm)")
+    ap.add_argument("--prof", action="store_true",
+                    help="per-worker phase attribution of every stream (io_prof)")
+    ap.add_argument("--no-lat", dest="lat", action="store_false", help="skip the QD1 latency")
+    ap.add_argument("--set", default="", help="extra config for every run: k=v,k=v")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     arms = (None,)
@@ -109,9 +113,15 @@ def main(argv=None) -> int:
     F = int(a.file_gib * (1 << 30)) // (4 << 20) * (4 << 20)
     _mk(path, F)
     fd = os.open(path, os.O_RDONLY)
-    keys = ["max_request", "queue_depth", "backend", "pgcache_probe"] + ([a.ab] if a.ab else [])
+    extra = dict(kv.split("=", 1) for kv in a.set.split(",") if kv)
+    keys = ["max_request", "queue_depth", "backend", "pgcache_probe", "io_prof"] + \
+        ([a.ab] if a.ab else []) + [k for k in extra if k != a.ab]
     defaults = {k: S.config_get(k) for k in keys}
     evict = (lambda f: None) if a.engine_only else S.evict_file
+    if extra:
+        S.configure(**extra)
+    if a.prof:
+        S.configure(io_prof=1)
     if a.engine_only:
         S.configure(backend="cache", pgcache_probe=0)
         with open(path, "rb") as f:                 # hold the file in the page cache
@@ -138,20 +148,27 @@ def main(argv=None) -> int:
             ld.run(0, 32 << 20)                      # warm the engine, not the cache
             evict(fd)
             sync()
+            if a.prof:
+                S.io_prof(reset=True)
             st = ld.run(0, nbytes)
             sync()
+            prof = S.io_prof() if a.prof else None
             gibs = nbytes / st.seconds / (1 << 30)
             iops = st.nr_submit / st.seconds
             # QD1 latency of B-byte reads at random aligned offsets
-            evict(fd)
-            rng = np.random.default_rng(B)
-            offs = rng.integers(0, F // B, size=a.lat_samples + 20) * B
-            ns = S.pread_gpu_latency(ld.buf.handle, 0, fd, offs, B)[20:] / 1e3
+            ns = np.zeros(1)
+            if a.lat:
+                evict(fd)
+                rng = np.random.default_rng(B)
+                offs = rng.integers(0, F // B, size=a.lat_samples + 20) * B
+                ns = S.pread_gpu_latency(ld.buf.handle, 0, fd, offs, B)[20:] / 1e3
             row = dict(block=B, GiBps=round(gibs, 2), iops=round(iops), bytes=nbytes,
                        **({a.ab: abv} if a.ab else {}),
                        avg_req_kib=round(0.5 * st.nr_blocks / st.nr_submit, 1) if st.nr_submit else 0,
                        ram_chunks=st.nr_ram, p50_us=round(float(np.percentile(ns, 50)), 2),
                        p99_us=round(float(np.percentile(ns, 99)), 2))
+            if prof:
+                row["prof"] = prof
             if a.raw:
                 nraw = max(2000, min(nbytes // B, 200000))
                 kw = dict(threads=int(S.config_get("workers")), qd=int(S.config_get("queue_depth")))

@@ -112,6 +112,43 @@ def test_arrow_scan(S, tmp_path, codecs):
         sc.close()
 
 
+def test_arrow_scan_bar_refused_after_cold_scan(S, tmp_path):
+    """a cold one-column scan (no page-cache chunks, so the reader
+    never learns the BAR is refused), then a warm two-column scan_where whose
+    groups are larger, with the large-BAR mapping off: the page-cache chunks
+    go through a per-slot write-back buffer sized for the larger groups."""
+    pa = pytest.importorskip("pyarrow")
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+    rng = np.random.default_rng(7)
+    n, nb = 200_000, 4
+    a = rng.integers(-10**6, 10**6, n * nb)
+    b = rng.integers(-10**6, 10**6, n * nb)
+    tbl = pa.table({"a": pa.array(a, type=pa.int64()), "b": pa.array(b, type=pa.int64())})
+    path = str(tmp_path / "w.arrow")
+    with ipc.new_file(path, tbl.schema) as w:
+        for k in range(nb):
+            w.write_batch(tbl.slice(k * n, n).to_batches()[0])
+    S.configure(bar_map=0)
+    try:
+        fd = os.open(path, os.O_RDONLY)
+        S.evict_file(fd)
+        os.close(fd)
+        sc = ArrowScan(path, "cuda")
+        out = sc.filter("a", -1000, 5000)
+        assert np.array_equal(out.indices.cpu().numpy(), np.nonzero((a >= -1000) & (a <= 5000))[0])
+        with open(path, "rb") as f:     # now every chunk is in the page cache
+            f.read()
+        sel = (a >= -500_000) & (a <= 200_000) & (b >= 0) & (b <= 700_000)
+        out = sc.scan_where([("a", -500_000, 200_000), ("b", 0, 700_000)], project="b")
+        ref = np.nonzero(sel)[0]
+        assert np.array_equal(out.indices.cpu().numpy(), ref)
+        assert np.array_equal(out.values.cpu().numpy(), b[ref])
+        sc.close()
+    finally:
+        S.configure(bar_map=1)
+
+
 def test_distributed_scan_two_ranks_one_gpu(tmp_path):
     """parallel/scan.py end to end on the GPU: 2 ranks (gloo, both on the
     box's one GPU, collectives staged via host memory) each scan their share

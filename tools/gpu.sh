@@ -20,6 +20,10 @@
 #   kpmc       one PMC pass (LDS / VALU / wave counters) over crc, heap, lz4
 #   btrace     rocprofv3 kernel + memory-copy trace of a short bench run
 #   sweep      block-size sweep 4K..4M vs the raw O_DIRECT ceiling
+#   esweep     engine-only sweep (backend=cache) with per-worker attribution
+#   lz4par     block-parallel LZ4 decoder by stream count (LZ4PAR_STREAMS / _KINDS / _ARGS)
+#   dist       multi-rank Arrow / PG scans: 1 rank (RCCL) and 2 gloo ranks (DIST_ARGS)
+#   benchtests bench.py contract tests (tests/test_gpu_bench.py)
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   decprof    decoder cycle profile per code path (libstrom_decprof.so)
 #   decpmc     two PMC passes (issue / wait / LDS / memory instruction mix)
@@ -28,7 +32,9 @@
 #   ceiling    engine + ingest ceiling: page-cache reads (backend=cache) vs O_DIRECT
 #   pg         end-to-end PostgreSQL heap scan (GPU ring vs the reference-shaped CPU scan)
 #   stripe     config-3 proxy: 4-member stripe set vs one file (tools.stripe_bench)
-# Output lands in gpurun_out/TAG/.
+# Output lands in gpurun_out/TAG/.  One-off recipes (several phases with
+# env overrides) live in tools/run/, which git ignores; the commands behind
+# every committed profile are written into its profiles/rN/*/SUMMARY.md.
 set -o pipefail
 TAG=${1:?tag}; shift
 OUT=$PWD/gpurun_out/$TAG
@@ -77,6 +83,20 @@ for phase in "$@"; do
               -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only crc,heap,lz4) ;;
     btrace) (cd /tmp && step btrace 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d "$OUT/btrace" -o btrace \
               -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --lat-samples 300) ;;
+    esweep) # engine-only sweep with worker phase attribution; ESWEEP_NAME / ESWEEP_ARGS
+            nm=${ESWEEP_NAME:-esweep}
+            step $nm 500 python -u -m nvme_strom_amd.tools.sweep --engine-only --prof --no-lat \
+              --blocks ${SWEEP_BLOCKS:-4K,8K,16K} ${ESWEEP_ARGS:-} --out "$OUT/$nm.json" ;;
+    lz4par) step lz4par 500 python -u -m nvme_strom_amd.tools.lz4par_bench --kinds ${LZ4PAR_KINDS:-val,ids,text} \
+              --streams ${LZ4PAR_STREAMS:-512,2048,8192} --distinct 32 --iters 5 ${LZ4PAR_ARGS:-} --out "$OUT/lz4par.json" ;;
+    dist) # multi-rank scan (parallel/scan.py): 1 rank RCCL, 2 ranks gloo on the one GPU; DIST_ARGS
+          step dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr 127.0.0.1 \
+            --master-port 29561 -m nvme_strom_amd.tools.dist_scan_bench ${DIST_ARGS:---rows 134217728} --reps 3 \
+            --out "$OUT/dist1.json"
+          step dist2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 \
+            --master-port 29562 -m nvme_strom_amd.tools.dist_scan_bench ${DIST_ARGS:---rows 134217728} --reps 3 \
+            --backend gloo --out "$OUT/dist2_gloo.json" ;;
+    benchtests) step benchtests 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_bench.py ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
     ram) step ram 500 python -u -m nvme_strom_amd.tools.ram_bench --file-gib ${RAM_GIB:-8} --reps ${RAM_REPS:-7} --out "$OUT/ram.json" ;;
     decprof) step decprof 300 python -u -m nvme_strom_amd.tools.decomp_prof --out "$OUT/decprof.json" ;;
