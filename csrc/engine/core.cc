@@ -35,7 +35,7 @@ Config Config::from_env() {
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
                                "bar_map", "bar_max", "coalesce", "trace",
-                               "ingest", "ingest_grid", "ingest_piece", "ingest_min", "hdp_sync",
+                               "ingest", "ingest_grid", "ingest_piece", "ingest_min", "ingest_prio", "hdp_sync",
                                "fixed_bufs", "io_prof",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind", "check_freed",
@@ -95,6 +95,7 @@ int Config::set(const std::string &k, const std::string &v) {
     ingest_min = (uint32_t)n;
     return 0;
   }
+  if (k == "ingest_prio") { if (n < 0 || n > 1) return -EINVAL; ingest_prio = (int)n; return 0; }
   if (k == "ingest_grid") { if (n < 1 || n > 256) return -EINVAL; ingest_grid = (int)n; return 0; }
   if (k == "ingest_piece") {
     if (n < 4096 || n > (16l << 20) || (n & 4095)) return -EINVAL;
@@ -138,6 +139,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "coalesce") v = coalesce;
   else if (k == "ingest") v = ingest;
   else if (k == "ingest_grid") v = ingest_grid;
+  else if (k == "ingest_prio") v = ingest_prio;
   else if (k == "ingest_piece") v = ingest_piece;
   else if (k == "hdp_sync") v = hdp_sync;
   else if (k == "fixed_bufs") v = fixed_bufs;

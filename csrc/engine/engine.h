@@ -63,6 +63,9 @@ struct Config {
   bool ingest = true;            // staged reads reach HBM through the GPU ingest
                                  // grid (ingest.hip) instead of SDMA copies
   int ingest_grid = 16;          // workgroups of the ingest grid (CUs it holds)
+  int ingest_prio = 0;           // 1: the grid's stream is created at the
+                                 // greatest priority (a hardware queue of its
+                                 // own, not shared with normal-priority streams)
   uint32_t ingest_piece = 256u << 10;  // bytes per ingest descriptor
   bool hdp_sync = false;         // wait for each HDP flush to complete (read
                                  // back) instead of posting it

@@ -92,8 +92,12 @@ bool Ingest::init() {
   ring_ = h;
   done_ = (volatile uint64_t *)((char *)h + nslots_ * sizeof(IngestDesc));
   stop_ = (volatile uint64_t *)((char *)done_ + nslots_ * sizeof(uint64_t));
+  int prio_least = 0, prio_greatest = 0;
+  if (config().ingest_prio && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
+    prio_greatest = 0;
   if (hipMalloc(&next_, 64) != hipSuccess ||
-      hipStreamCreateWithFlags((hipStream_t *)&stream_, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority((hipStream_t *)&stream_, hipStreamNonBlocking,
+                                  config().ingest_prio ? prio_greatest : 0) != hipSuccess ||
       hipEventCreateWithFlags((hipEvent_t *)&end_ev_, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
     return false;
