@@ -23,6 +23,8 @@
 #   esweep     engine-only sweep (backend=cache) with per-worker attribution
 #   lz4par     block-parallel LZ4 decoder by stream count (LZ4PAR_STREAMS / _KINDS / _ARGS)
 #   dist       multi-rank Arrow / PG scans: 1 rank (RCCL) and 2 gloo ranks (DIST_ARGS)
+#   overlap    load <-> side-stream collective overlap test + bench (both grid priorities)
+#   otrace     rocprofv3 kernel trace of overlap_bench + grid/side concurrency summary
 #   benchtests bench.py contract tests (tests/test_gpu_bench.py)
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   decprof    decoder cycle profile per code path (libstrom_decprof.so)
@@ -96,6 +98,15 @@ for phase in "$@"; do
           step dist2 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 \
             --master-port 29562 -m nvme_strom_amd.tools.dist_scan_bench ${DIST_ARGS:---rows 134217728} --reps 3 \
             --backend gloo --out "$OUT/dist2_gloo.json" ;;
+    overlap) step otests 300 python -u -m pytest tests/test_gpu_overlap.py -m gpu -x -v --timeout 200 --timeout-method thread
+             step overlap 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 --gather-reps ${OV_REPS:-8} \
+               --n 2,8 --out "$OUT/overlap.json"
+             STROM_INGEST_PRIO=1 step overlap_prio 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 \
+               --gather-reps ${OV_REPS:-8} --n 2,8 --out "$OUT/overlap_prio.json" ;;
+    otrace) (cd /tmp && step otrace 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/otrace" -o trace \
+              -- python3 -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 8 --gather-reps ${OV_REPS:-8} --n 8 --modes overlap) && \
+            python -m nvme_strom_amd.tools.overlap_trace $(find "$OUT/otrace" -name '*kernel_trace.csv' | head -1) \
+              --md "$OUT/otrace_summary.md" ;;
     benchtests) step benchtests 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_bench.py ;;
     sweep) step sweep 400 python -u -m nvme_strom_amd.tools.sweep --out "$OUT/sweep.json" ;;
     ram) step ram 500 python -u -m nvme_strom_amd.tools.ram_bench --file-gib ${RAM_GIB:-8} --reps ${RAM_REPS:-7} --out "$OUT/ram.json" ;;
