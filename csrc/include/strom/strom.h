@@ -223,6 +223,64 @@ struct strom_heap_scan_args {
 #define STROM_PAGE_BAD_CHECKSUM 2u
 #define STROM_PAGE_EMPTY       4u
 int strom_heap_scan(const struct strom_heap_scan_args *a, void *stream);
+
+/* General tuple deforming + qualifier lists (the reference hands every tuple
+ * to ExecScan, which deforms it and evaluates any qual list:
+ * pgsql/nvme_strom.c:1137-1143, :1054-1092).  A tuple descriptor in
+ * PostgreSQL's pg_attribute terms locates every attribute: the null bitmap
+ * (HEAP_HASNULL, t_bits), attalign padding, fixed lengths, and varlena
+ * headers (1-byte short, 4-byte, 1-byte-external TOAST pointers).  Tuples
+ * with fewer stored attributes than the descriptor (ALTER TABLE ADD COLUMN)
+ * read the missing ones as NULL. */
+#define STROM_HEAP_MAX_ATTS  64
+#define STROM_HEAP_MAX_QUALS 8
+struct strom_heap_tupdesc {
+	int32_t natts;
+	int16_t attlen[STROM_HEAP_MAX_ATTS];    /* > 0 fixed, -1 varlena, -2 cstring */
+	uint8_t attalign[STROM_HEAP_MAX_ATTS];  /* 1, 2, 4 or 8 ('c' 's' 'i' 'd') */
+	int16_t cacheoff[STROM_HEAP_MAX_ATTS];  /* offset after t_hoff when every earlier
+	                                           attribute is fixed-length (tuples without
+	                                           nulls), else -1 (attcacheoff) */
+};
+#define STROM_QUAL_INT_RANGE    1  /* lo <= v <= hi, v an int of attlen 1/2/4/8 */
+#define STROM_QUAL_FLOAT_RANGE  2  /* lo <= v <= hi as doubles (bit patterns in lo/hi),
+                                      v a float4 / float8 */
+#define STROM_QUAL_IS_NULL      3
+#define STROM_QUAL_NOT_NULL     4
+#define STROM_QUAL_TEXT_EQ      5  /* varlena bytes == cbytes[0..nconst) */
+#define STROM_QUAL_TEXT_PREFIX  6  /* varlena bytes start with cbytes[0..nconst) */
+#define STROM_QUAL_INT_IN       7  /* v in { ((int64_t *)cbytes)[0..nconst) } (<= 4) */
+struct strom_heap_qual {
+	int16_t attno;       /* 0-based column */
+	uint8_t kind;        /* STROM_QUAL_* */
+	uint8_t nconst;      /* TEXT_*: constant length (<= 32); INT_IN: values (<= 4) */
+	uint32_t pad;
+	int64_t lo, hi;
+	uint8_t cbytes[32];
+};
+/* A text qualifier meets a compressed or out-of-line (TOAST) value: the GPU
+ * cannot decide it, the tuple is not emitted and its page is flagged
+ * STROM_PAGE_RECHECK for the host to re-evaluate. */
+#define STROM_PAGE_RECHECK     8u
+struct strom_heap_scan2_args {
+	struct strom_heap_scan_args base;     /* base.attr_off must be -1 */
+	struct strom_heap_tupdesc desc;
+	int32_t nquals;                       /* ANDed; NULL never qualifies
+	                                         except for IS_NULL */
+	struct strom_heap_qual quals[STROM_HEAP_MAX_QUALS];
+	uint32_t *recheck_count;              /* device, optional: undecidable tuples */
+};
+int strom_heap_scan2(const struct strom_heap_scan2_args *a, void *stream);
+/* Projection of one attribute of the tuples `items` (page << 16 | lineno,
+ * as strom_heap_scan writes them) names: values[i] (8 bytes: the int
+ * sign-extended, float4 widened to double, varlena: (offset in pages <<
+ * 32 | data length) of the uncompressed inline bytes) and valid[i] (0 NULL,
+ * 1 value, 2 compressed / out-of-line varlena).  *d_count (device) is the
+ * number of items; at most cap are read. */
+int strom_heap_project(const void *pages, uint32_t page_sz, const uint32_t *items,
+                       const uint32_t *d_count, uint32_t cap,
+                       const struct strom_heap_tupdesc *desc, int attno, int as_float,
+                       uint64_t *values, uint8_t *valid, void *stream);
 uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
                                 uint32_t page_sz);
 /* Per-tuple MVCC check of a heap page against a snapshot (xmin, xmax,

@@ -24,6 +24,16 @@
 //   4. output reservation once per WORKGROUP (4 waves x 8 pages): the waves'
 //      counts are summed in LDS and thread 0 does a single atomicAdd, then
 //      each wave replays its masks to write (page << 16 | lineno) item ids.
+//
+// strom_heap_scan2 replaces the fixed-offset predicate of step 3 with what
+// ExecScan does for the reference (pgsql/nvme_strom.c:1137-1143): every lane
+// deforms its tuple in LDS with a tuple descriptor — null bitmap, attalign
+// padding, fixed lengths, 1-byte / 4-byte / TOAST-pointer varlena headers,
+// attcacheoff shortcuts for null-free tuples — and evaluates an AND-list of
+// qualifiers (int / float ranges, IN lists, IS [NOT] NULL, text equality and
+// prefix).  Quals are sorted by attribute, so one walk per tuple serves them
+// all.  strom_heap_project gathers one attribute of the selected tuples with
+// the same deformer, reading the pages in HBM.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -116,8 +126,205 @@ __device__ uint32_t page_status(const strom_heap_scan_args &a, const uint8_t *pg
   return (c & 0xffffu) != h.checksum ? STROM_PAGE_BAD_CHECKSUM : 0u;
 }
 
-__device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const uint8_t *pg,
-                                           uint32_t lp, bool all_visible) {
+// ---------------------------------------------------------------- deformer
+__device__ __forceinline__ uint32_t align_up(uint32_t off, uint32_t al) {
+  return (off + al - 1) & ~(al - 1);
+}
+
+// TOAST pointer payload size by vartag (postgres.h VARTAG_SIZE): indirect
+// and expanded pointers are 8 bytes, an on-disk varatt_external 16
+__device__ __forceinline__ uint32_t vartag_size(uint32_t tag) {
+  return tag == 18 ? 16u : (tag >= 1 && tag <= 3) ? 8u : 0u;
+}
+
+// One tuple's attribute walk.  `t` points at the tuple (LDS page image or
+// HBM), offsets are from the tuple start; attributes are visited in
+// increasing order (quals are sorted by attno on the host).
+struct Deform {
+  const uint8_t *t;
+  uint32_t tlen, hoff, natts;   // natts stored in this tuple (t_infomask2)
+  bool hasnull, bad;
+  uint32_t next, off;           // next attribute to pass, where its storage may start
+};
+
+struct Att {
+  uint32_t off, len, hdr;       // datum offset, total bytes, varlena header bytes
+  bool null, ext;               // ext: compressed or out-of-line varlena
+};
+
+__device__ __forceinline__ Deform deform_init(const uint8_t *t, uint32_t tlen) {
+  Deform s;
+  s.t = t;
+  s.tlen = tlen;
+  const uint32_t w16 = lds_u32(t, 16), w20 = lds_u32(t, 20);
+  s.natts = (w16 >> 16) & 0x7ff;
+  s.hasnull = (w20 & kHeapHasNull) != 0;
+  s.hoff = (w20 >> 16) & 0xff;
+  s.bad = s.hoff < 23 || s.hoff > tlen || (s.hasnull && 23 + ((s.natts + 7) >> 3) > s.hoff);
+  s.next = 0;
+  s.off = s.hoff;
+  return s;
+}
+
+__device__ __forceinline__ Att deform_to(const strom_heap_tupdesc &d, Deform &s, uint32_t k) {
+  Att a;
+  a.off = a.len = a.hdr = 0;
+  a.null = true;
+  a.ext = false;
+  if (s.bad) return a;
+  if (k >= s.natts) {             // not stored (added later): NULL
+    s.next = k + 1;
+    return a;
+  }
+  if (!s.hasnull && d.cacheoff[k] >= 0 && d.attlen[k] > 0) {
+    // attcacheoff: every earlier attribute is fixed-length and none is null
+    a.off = s.hoff + (uint32_t)d.cacheoff[k];
+    a.len = (uint32_t)d.attlen[k];
+    a.null = false;
+    if (a.off + a.len > s.tlen) s.bad = true;
+    s.next = k + 1;
+    s.off = a.off + a.len;
+    return a;
+  }
+  for (uint32_t i = s.next; i <= k; ++i) {
+    if (s.hasnull && !((s.t[23 + (i >> 3)] >> (i & 7)) & 1)) continue;  // NULL: no storage
+    const int len = d.attlen[i];
+    uint32_t o = s.off, L = 0, H = 0;
+    bool E = false;
+    if (len > 0) {
+      o = align_up(o, d.attalign[i]);
+      L = (uint32_t)len;
+    } else if (len == -1) {
+      if (o >= s.tlen) { s.bad = true; return a; }
+      uint32_t b = s.t[o];
+      if (b == 0) {               // a pad byte: the datum is an aligned 4-byte header
+        o = align_up(o, d.attalign[i]);
+        if (o >= s.tlen) { s.bad = true; return a; }
+        b = s.t[o];
+      }
+      if ((b & 1) == 0) {         // 4-byte header; (b & 3) == 2: compressed inline
+        if (o + 4 > s.tlen) { s.bad = true; return a; }
+        L = (lds_u32(s.t, o) >> 2) & 0x3fffffffu;
+        H = 4;
+        E = (b & 3) == 2;
+      } else if (b == 1) {        // 1-byte header 0x01: TOAST pointer, tag next
+        if (o + 2 > s.tlen) { s.bad = true; return a; }
+        const uint32_t ts = vartag_size(s.t[o + 1]);
+        if (!ts) { s.bad = true; return a; }
+        L = 2 + ts;
+        H = 2;
+        E = true;
+      } else {                    // 1-byte header: short inline value
+        L = b >> 1;
+        H = 1;
+      }
+    } else {                      // cstring: bytes up to and including NUL
+      uint32_t e = o;
+      while (e < s.tlen && s.t[e]) ++e;
+      L = e - o + 1;
+    }
+    if (L < H || o + L > s.tlen) { s.bad = true; return a; }
+    s.off = o + L;
+    if (i == k) {
+      a.off = o;
+      a.len = L;
+      a.hdr = H;
+      a.null = false;
+      a.ext = E;
+    }
+  }
+  s.next = k + 1;
+  return a;
+}
+
+__device__ __forceinline__ int64_t att_int(const uint8_t *t, const Att &a) {
+  switch (a.len) {
+    case 1: return (int8_t)t[a.off];
+    case 2: return (int16_t)(t[a.off] | (t[a.off + 1] << 8));
+    case 4: return (int32_t)lds_u32(t, a.off);
+    default: return (int64_t)((uint64_t)lds_u32(t, a.off) | ((uint64_t)lds_u32(t, a.off + 4) << 32));
+  }
+}
+
+__device__ __forceinline__ double att_float(const uint8_t *t, const Att &a) {
+  if (a.len == 4) return (double)__uint_as_float(lds_u32(t, a.off));
+  return __longlong_as_double((long long)att_int(t, a));
+}
+
+// PostgreSQL float ordering: NaN equals NaN and sorts above every number
+__device__ __forceinline__ bool pg_le(double x, double y) {
+  if (isnan(y)) return true;
+  if (isnan(x)) return false;
+  return x <= y;
+}
+
+// 1 keep, 0 drop, 2 undecidable here (text qual on a compressed / TOAST value)
+__device__ __forceinline__ int eval_quals(const strom_heap_scan2_args &g, const uint8_t *t,
+                                          uint32_t tlen) {
+  Deform s = deform_init(t, tlen);
+  Att a;
+  int last = -1;
+  int verdict = 1;
+  for (int qi = 0; qi < g.nquals; ++qi) {
+    const strom_heap_qual &q = g.quals[qi];
+    if (q.attno != last) {
+      a = deform_to(g.desc, s, (uint32_t)q.attno);
+      last = q.attno;
+    }
+    if (s.bad) return 0;
+    if (q.kind == STROM_QUAL_IS_NULL) {
+      if (!a.null) return 0;
+      continue;
+    }
+    if (a.null) return 0;
+    switch (q.kind) {
+      case STROM_QUAL_NOT_NULL:
+        break;
+      case STROM_QUAL_INT_RANGE: {
+        const int64_t v = att_int(t, a);
+        if (v < q.lo || v > q.hi) return 0;
+        break;
+      }
+      case STROM_QUAL_INT_IN: {
+        const int64_t v = att_int(t, a);
+        bool hit = false;
+        for (uint32_t k = 0; k < q.nconst && k < 4; ++k) {
+          int64_t c;
+          __builtin_memcpy(&c, q.cbytes + 8 * k, 8);
+          hit |= v == c;
+        }
+        if (!hit) return 0;
+        break;
+      }
+      case STROM_QUAL_FLOAT_RANGE: {
+        const double v = att_float(t, a);
+        if (!pg_le(__longlong_as_double(q.lo), v) || !pg_le(v, __longlong_as_double(q.hi))) return 0;
+        break;
+      }
+      case STROM_QUAL_TEXT_EQ:
+      case STROM_QUAL_TEXT_PREFIX: {
+        if (a.ext) {              // keep checking: a later qual may still reject it
+          verdict = 2;
+          break;
+        }
+        const uint32_t n = a.len - a.hdr;
+        if (q.kind == STROM_QUAL_TEXT_EQ ? n != q.nconst : n < q.nconst) return 0;
+        for (uint32_t k = 0; k < q.nconst; ++k)
+          if (t[a.off + a.hdr + k] != q.cbytes[k]) return 0;
+        break;
+      }
+      default:
+        return 0;
+    }
+  }
+  return verdict;
+}
+
+// 1 keep, 0 drop, 2 undecidable (GEN: a text qual met a compressed value)
+template <bool GEN>
+__device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const uint8_t *pg,
+                                          uint32_t lp, bool all_visible) {
+  const strom_heap_scan_args &a = g.base;
   const uint32_t off = lp & 0x7fff, flags = (lp >> 15) & 3, len = lp >> 17;
   if (flags != kLpNormal || len < 23 || off < kSizeOfPageHeader || off + len > a.page_sz ||
       (off & 1))
@@ -129,6 +336,7 @@ __device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const 
     if (!(infomask & kXminCommitted)) return false;
     if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return false;
   }
+  if (GEN) return g.nquals ? eval_quals(g, pg + off, len) : 1;
   if (a.attr_off < 0) return true;
   const uint32_t at = hoff + (uint32_t)a.attr_off;
   if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return false;
@@ -150,9 +358,10 @@ __device__ __forceinline__ bool tuple_keep(const strom_heap_scan_args &a, const 
 // row "dequeue" — 2.1 TB/s).
 constexpr int kPerWave = 8;
 
-template <int PAGE>
-__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, uint32_t maxchunks,
+template <int PAGE, bool GEN>
+__global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan2_args g, uint32_t maxchunks,
                                                         uint32_t ppw) {
+  const strom_heap_scan_args &a = g.base;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t page_sz = PAGE ? (uint32_t)PAGE : a.page_sz;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -204,22 +413,29 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
       uint32_t nchunks = 0;
       if (have) {
         const PageHdr h = read_hdr(mypage);
-        const uint32_t status = page_status(a, mypage, h, pg, lane);
-        if (lane == 0 && a.page_status) a.page_status[pg] = status;
+        uint32_t status = page_status(a, mypage, h, pg, lane);
         if (status == 0) {
           const bool all_visible = (h.flags & kPdAllVisible) != 0;
           const uint32_t nitems = (h.lower - kSizeOfPageHeader) / 4;
           nchunks = (nitems + 63) / 64;
+          uint32_t recheck = 0;
           for (uint32_t c = 0; c < nchunks; ++c) {
             const uint32_t i = c * 64 + lane;
-            const bool keep =
-                i < nitems && tuple_keep(a, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i),
-                                         all_visible);
-            const uint64_t m = __ballot(keep);
+            const int keep =
+                i < nitems
+                    ? tuple_keep<GEN>(g, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i), all_visible)
+                    : 0;
+            const uint64_t m = __ballot(keep == 1);
             if (lane == 0) masks[j * maxchunks + c] = m;
             count += __popcll(m);
+            if (GEN) recheck += __popcll(__ballot(keep == 2));
+          }
+          if (GEN && recheck) {
+            status |= STROM_PAGE_RECHECK;
+            if (lane == 0 && g.recheck_count) atomicAdd(g.recheck_count, recheck);
           }
         }
+        if (lane == 0 && a.page_status) a.page_status[pg] = status;
       }
       if (lane == 0) nch[j] = nchunks;
       // the wave's own page image is overwritten next
@@ -258,10 +474,9 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan_args a, 
 #undef STROM_HS_ISSUE
 }
 
-}  // namespace
-
-extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
-  if (!a || !a->pages || !a->out_count) return -22;
+int heap_scan_launch(const strom_heap_scan2_args &g, bool gen, void *stream) {
+  const strom_heap_scan_args *a = &g.base;
+  if (!a->pages || !a->out_count) return -22;
   if (a->page_sz < 1024 || (a->page_sz & 1023) || a->page_sz > 32768) return -22;
   if (a->attr_off >= 0 && a->attr_width != 4 && a->attr_width != 8) return -22;
   // (page << 16 | lineno) item ids address at most 65535 pages per call
@@ -282,9 +497,118 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   uint32_t grid = (a->npages + kWaves * ppw - 1) / (kWaves * ppw);
   const uint32_t cap = 256u * (per_cu ? per_cu : 1u) * 2u;
   if (grid > cap) grid = cap;
-  if (a->page_sz == 8192)
-    hipLaunchKernelGGL(heap_scan_kernel<8192>, dim3(grid), dim3(256), lds, st, *a, maxchunks, ppw);
-  else
-    hipLaunchKernelGGL(heap_scan_kernel<0>, dim3(grid), dim3(256), lds, st, *a, maxchunks, ppw);
+  if (a->page_sz == 8192) {
+    if (gen)
+      hipLaunchKernelGGL((heap_scan_kernel<8192, true>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+    else
+      hipLaunchKernelGGL((heap_scan_kernel<8192, false>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+  } else {
+    if (gen)
+      hipLaunchKernelGGL((heap_scan_kernel<0, true>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+    else
+      hipLaunchKernelGGL((heap_scan_kernel<0, false>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// one thread per selected item: deform its tuple from the page in HBM
+__global__ __launch_bounds__(256) void heap_project_kernel(const uint8_t *pages, uint32_t page_sz,
+                                                           const uint32_t *items, const uint32_t *d_count,
+                                                           uint32_t cap, strom_heap_tupdesc desc,
+                                                           uint32_t attno, int as_float,
+                                                           uint64_t *values, uint8_t *valid) {
+  const uint32_t n = min(*d_count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t it = items[i], pg = it >> 16, lineno = it & 0xffff;
+    const uint8_t *page = pages + (uint64_t)pg * page_sz;
+    uint64_t v = 0;
+    uint8_t ok = 0;
+    const uint32_t lower = lds_u32a(page, 12) & 0xffff;
+    if (lineno >= 1 && kSizeOfPageHeader + 4 * lineno <= lower) {
+      const uint32_t lp = lds_u32a(page, kSizeOfPageHeader + 4 * (lineno - 1));
+      const uint32_t off = lp & 0x7fff, len = lp >> 17;
+      if (len >= 23 && off >= kSizeOfPageHeader && off + len <= page_sz && !(off & 1)) {
+        Deform s = deform_init(page + off, len);
+        const Att a = deform_to(desc, s, attno);
+        if (!s.bad && !a.null) {
+          if (desc.attlen[attno] < 0) {   // varlena / cstring: where its bytes are
+            v = ((uint64_t)((uint64_t)pg * page_sz + off + a.off + a.hdr) << 32) | (a.len - a.hdr);
+            ok = a.ext ? 2 : 1;
+          } else if (as_float) {
+            v = (uint64_t)__double_as_longlong(att_float(page + off, a));
+            ok = 1;
+          } else {
+            v = (uint64_t)att_int(page + off, a);
+            ok = 1;
+          }
+        }
+      }
+    }
+    values[i] = v;
+    if (valid) valid[i] = ok;
+  }
+}
+
+}  // namespace
+
+extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
+  if (!a) return -22;
+  strom_heap_scan2_args g;
+  __builtin_memset(&g, 0, sizeof g);
+  g.base = *a;
+  return heap_scan_launch(g, false, stream);
+}
+
+extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
+  if (!g || g->base.attr_off >= 0) return -22;
+  if (g->nquals < 0 || g->nquals > STROM_HEAP_MAX_QUALS) return -22;
+  if (g->desc.natts < 1 || g->desc.natts > STROM_HEAP_MAX_ATTS) return -22;
+  for (int i = 0; i < g->desc.natts; ++i) {
+    const int al = g->desc.attalign[i], len = g->desc.attlen[i];
+    if ((al != 1 && al != 2 && al != 4 && al != 8) || len == 0 || len < -2) return -22;
+  }
+  int last = -1;
+  for (int q = 0; q < g->nquals; ++q) {
+    const strom_heap_qual &x = g->quals[q];
+    if (x.attno < last || x.attno >= g->desc.natts) return -22;  // sorted by attno
+    last = x.attno;
+    const int len = g->desc.attlen[x.attno];
+    switch (x.kind) {
+      case STROM_QUAL_INT_RANGE:
+      case STROM_QUAL_INT_IN:
+        if (len != 1 && len != 2 && len != 4 && len != 8) return -22;
+        if (x.kind == STROM_QUAL_INT_IN && x.nconst > 4) return -22;
+        break;
+      case STROM_QUAL_FLOAT_RANGE:
+        if (len != 4 && len != 8) return -22;
+        break;
+      case STROM_QUAL_TEXT_EQ:
+      case STROM_QUAL_TEXT_PREFIX:
+        if (len != -1 || x.nconst > 32) return -22;
+        break;
+      case STROM_QUAL_IS_NULL:
+      case STROM_QUAL_NOT_NULL:
+        break;
+      default:
+        return -22;
+    }
+  }
+  return heap_scan_launch(*g, true, stream);
+}
+
+extern "C" int strom_heap_project(const void *pages, uint32_t page_sz, const uint32_t *items,
+                                  const uint32_t *d_count, uint32_t cap,
+                                  const strom_heap_tupdesc *desc, int attno, int as_float,
+                                  uint64_t *values, uint8_t *valid, void *stream) {
+  if (!pages || !items || !d_count || !desc || !values) return -22;
+  if (attno < 0 || attno >= desc->natts || desc->natts > STROM_HEAP_MAX_ATTS) return -22;
+  if (page_sz < 1024 || (page_sz & 1023) || page_sz > 32768) return -22;
+  const int len = desc->attlen[attno];
+  if (as_float && len != 4 && len != 8) return -22;
+  if (cap == 0) return 0;
+  const uint32_t grid = std::min<uint32_t>((cap + 255) / 256, 4096);
+  hipLaunchKernelGGL(heap_project_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t *)pages, page_sz, items, d_count, cap, *desc, (uint32_t)attno,
+                     as_float, values, valid);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

@@ -131,6 +131,26 @@ class HeapScanArgs(C.Structure):
                 ("blkno_base", C.c_uint32), ("blknos", C.c_void_p)]
 
 
+HEAP_MAX_ATTS = 64
+HEAP_MAX_QUALS = 8
+
+
+class HeapTupDesc(C.Structure):
+    _fields_ = [("natts", C.c_int32), ("attlen", C.c_int16 * HEAP_MAX_ATTS),
+                ("attalign", C.c_uint8 * HEAP_MAX_ATTS), ("cacheoff", C.c_int16 * HEAP_MAX_ATTS)]
+
+
+class HeapQual(C.Structure):
+    _fields_ = [("attno", C.c_int16), ("kind", C.c_uint8), ("nconst", C.c_uint8),
+                ("pad", C.c_uint32), ("lo", C.c_int64), ("hi", C.c_int64),
+                ("cbytes", C.c_uint8 * 32)]
+
+
+class HeapScan2Args(C.Structure):
+    _fields_ = [("base", HeapScanArgs), ("desc", HeapTupDesc), ("nquals", C.c_int32),
+                ("quals", HeapQual * HEAP_MAX_QUALS), ("recheck_count", C.c_void_p)]
+
+
 class DecompDesc(C.Structure):
     _fields_ = [("src_off", C.c_uint64), ("dst_off", C.c_uint64), ("src_len", C.c_uint32),
                 ("dst_len", C.c_uint32)]
@@ -205,6 +225,10 @@ _SIGS = {
                                      C.c_void_p]),
     "strom_fill_pattern": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     "strom_heap_scan": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p]),
+    "strom_heap_scan2": (C.c_int, [C.POINTER(HeapScan2Args), C.c_void_p]),
+    "strom_heap_project": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32,
+                                     C.POINTER(HeapTupDesc), C.c_int, C.c_int, C.c_void_p,
+                                     C.c_void_p, C.c_void_p]),
     "strom_decompress": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                    C.c_void_p, C.c_void_p]),
     "strom_column_filter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_double,

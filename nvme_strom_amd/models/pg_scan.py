@@ -39,13 +39,13 @@ import threading
 import time
 import weakref
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple, Any
 
 import numpy as np
 import torch
 
 from .. import api
-from ..ops.heapscan import heap_scan
+from ..ops.heapscan import PAGE_RECHECK, heap_project, heap_scan, heap_scan2
 from ..tensor import FileReader, HbmBuffer, host_buffer
 from ..utils import pgmvcc, pgpage
 from ..utils.pgmvcc import CommitLog, Snapshot
@@ -325,6 +325,14 @@ class ScanResult:
     # MVCC mode: blocks that took the checked (host) path, tuples it removed
     nr_checked: int = 0
     removed: int = 0
+    # qualifier-list scans: the projected column of every item (numpy int64 /
+    # float64, or a list of bytes for a varlena column) and its validity (0
+    # NULL, 1 value, 2 compressed / out-of-line: the executor detoasts it)
+    values: Optional[Any] = None
+    valid: Optional[np.ndarray] = None
+    # blocks holding tuples a text qualifier could not decide on the GPU
+    # (compressed / TOAST values): the executor re-evaluates those blocks
+    recheck_blocks: List[int] = field(default_factory=list)
 
     @property
     def ntuples(self) -> int:
@@ -348,6 +356,8 @@ class ScanResult:
             self.chunks += p.chunks
             self.nr_checked += p.nr_checked
             self.removed += p.removed
+            self.recheck_blocks += p.recheck_blocks
+        self.recheck_blocks.sort()
 
     def explain(self) -> str:
         """EXPLAIN ANALYZE-style summary of the scan's I/O split and rates."""
@@ -372,12 +382,22 @@ class HeapRelationScan:
 
     def __init__(self, rel: Relation, cfg: Optional[ScanConfig] = None, device=None,
                  attr_off: int = -1, attr_width: int = 8, lo: int = -(1 << 63),
-                 hi: int = (1 << 63) - 1):
+                 hi: int = (1 << 63) - 1, desc=None, quals=None, project=None):
+        """``attr_off``..``hi``: the fixed-offset int predicate of the round-1
+        kernel.  ``desc`` (utils.pgtuple.TupleDesc) + ``quals`` (a list of
+        pgtuple.Qual, ANDed) + optional ``project`` column: every tuple is
+        deformed on the GPU and the qualifier list evaluated there, as the
+        reference's ExecScan does on the CPU (pgsql/nvme_strom.c:1137-1143)."""
         self.rel = rel
         self.cfg = cfg or ScanConfig()
         self.cfg.validate()
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.pred = dict(attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi)
+        if (quals is not None or project is not None) and desc is None:
+            raise ValueError("quals / project need a tuple descriptor (desc)")
+        if desc is not None and attr_off >= 0:
+            raise ValueError("a fixed-offset predicate and a qualifier list are exclusive")
+        self.desc, self.quals, self.project = desc, list(quals or []), project
         # idle participant resources (session, HBM ring, readers, pinned
         # write-back buffers), reused by later runs: allocating and pinning
         # them per run cost more than the scan of a GiB-sized relation.
@@ -481,6 +501,14 @@ class HeapRelationScan:
         chunks = sorted((c for r in results for c in r.chunk_items), key=lambda c: c[0])
         items = np.concatenate([c[1] for c in chunks]) if chunks else np.zeros(0, np.uint64)
         out = ScanResult(items, seconds=time.perf_counter() - t0, workers=workers)
+        if self.project is not None:
+            vals = [c[2] for c in chunks]
+            if vals and isinstance(vals[0], list):
+                out.values = [v for part in vals for v in part]
+            else:
+                out.values = np.concatenate(vals) if vals else np.zeros(0)
+            out.valid = (np.concatenate([c[3] for c in chunks]) if chunks
+                         else np.zeros(0, np.uint8))
         out.merge(results)
         return out
 
@@ -558,24 +586,71 @@ class HeapRelationScan:
         # MVCC mode: visibility is settled (all-visible blocks unchecked, the
         # rest filtered against the snapshot): every LP_NORMAL tuple counts
         skip = self.cfg.skip_invisible and self.cfg.snapshot is None
-        r = heap_scan(pages, BLCKSZ, verify_checksum=self.cfg.verify_checksum,
-                      skip_invisible=skip, blknos=blk, **self.pred)
+        general = self.desc is not None
+        if general:
+            r = heap_scan2(pages, self.desc, self.quals, BLCKSZ,
+                           verify_checksum=self.cfg.verify_checksum, skip_invisible=skip,
+                           blknos=blk)
+        else:
+            r = heap_scan(pages, BLCKSZ, verify_checksum=self.cfg.verify_checksum,
+                          skip_invisible=skip, blknos=blk, **self.pred)
         # the kernel reserves output per workgroup (arbitrary order across
         # workgroups): sort the chunk's items on the GPU (page order) before
         # the copy, so chunks only need ordering by their first block
-        it = torch.sort(r.items[:r.count].to(torch.int64) & 0xFFFFFFFF).values.cpu().numpy().astype(np.uint32)
+        srt, perm = torch.sort(r.items[:r.count].to(torch.int64) & 0xFFFFFFFF)
+        it = srt.cpu().numpy().astype(np.uint32)
         page_idx = (it >> 16).astype(np.int64)
         lineno = (it & 0xFFFF).astype(np.uint64)
         blocks = landed.astype(np.uint64)[page_idx]
         ptrs = (blocks << np.uint64(16)) | lineno
+        vals = valid = None
+        if general and self.project is not None:
+            cnt = torch.tensor([r.count], dtype=torch.int32, device=pages.device)
+            v, ok = heap_project(pages, r.items, cnt, self.desc, self.project, BLCKSZ,
+                                 cap=max(r.count, 1))
+            v, ok = v[:r.count][perm], ok[:r.count][perm]
+            valid = ok.cpu().numpy()
+            if self.desc.attlen[self.desc.attno(self.project)] < 0:
+                vals = _gather_varlena(pages, v, ok)
+            else:
+                vals = v.cpu().numpy()
         if n > 1 and bool((landed[1:] < landed[:-1]).any()):
-            ptrs = np.sort(ptrs)        # page-cache chunks landed at the tail
-        found.append((int(landed.min()) if n else 0, ptrs))
+            o = np.argsort(ptrs, kind="stable")  # page-cache chunks landed at the tail
+            ptrs = ptrs[o]
+            if valid is not None:
+                valid = valid[o]
+                vals = [vals[j] for j in o] if isinstance(vals, list) else vals[o]
+        found.append((int(landed.min()) if n else 0, ptrs, vals, valid))
         status = r.page_status.cpu().numpy()
+        if general:
+            st.recheck_blocks += [int(landed[j]) for j in np.nonzero(status & PAGE_RECHECK)[0]]
         st.pages += n
         st.bad_pages += int(((status & 3) != 0).sum())
         if res is not None:
             st.add_io(res)
+
+
+def _gather_varlena(pages: torch.Tensor, v: torch.Tensor, ok: torch.Tensor) -> list:
+    """Bytes of projected inline varlena values ((offset << 32 | length) into
+    ``pages``), gathered on the device into one packed copy; b"" where the
+    value is NULL or not inline."""
+    n = v.numel()
+    if n == 0:
+        return []
+    inline = ok == 1
+    lens = torch.where(inline, v & 0xFFFFFFFF, torch.zeros_like(v))
+    offs = torch.where(inline, v >> 32, torch.zeros_like(v))
+    ends = torch.cumsum(lens, 0)
+    total = int(ends[-1].item())
+    starts = ends - lens
+    if total:
+        row = torch.repeat_interleave(torch.arange(n, device=v.device), lens)
+        pos = torch.arange(total, device=v.device) - starts[row] + offs[row]
+        packed = pages[pos].cpu().numpy().tobytes()
+    else:
+        packed = b""
+    s, e = starts.cpu().numpy(), ends.cpu().numpy()
+    return [packed[a:b] for a, b in zip(s.tolist(), e.tolist())]
 
 
 def _block_range(blocks: Optional[Tuple[int, int]], nblocks: int) -> Tuple[int, int]:
@@ -589,9 +664,32 @@ def _block_range(blocks: Optional[Tuple[int, int]], nblocks: int) -> Tuple[int, 
 
 def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1,
              attr_width: int = 8, lo: int = -(1 << 63), hi: int = (1 << 63) - 1,
-             blocks: Optional[Tuple[int, int]] = None) -> ScanResult:
-    """Reference-shaped path: SSD2RAM into a NUMA DMA buffer, host tuple walk."""
+             blocks: Optional[Tuple[int, int]] = None, desc=None, quals=None,
+             project=None) -> ScanResult:
+    """Reference-shaped path: SSD2RAM into a NUMA DMA buffer, host tuple walk
+    (with ``desc`` / ``quals`` / ``project``: the host deformer,
+    utils.pgtuple.host_scan2)."""
+    from ..utils import pgtuple
     cfg = cfg or ScanConfig()
+    general = desc is not None
+    vals_out, valid_out = [], []
+
+    def walk(raw, blkno):
+        """(item ids, statuses) of pages ``raw`` starting at block ``blkno``"""
+        if not general:
+            return pgpage.host_scan(raw, BLCKSZ, skip, attr_off, attr_width, lo, hi,
+                                    cfg.verify_checksum, blkno)
+        its, stt, pv = pgtuple.host_scan2(raw, desc, quals or [], BLCKSZ, skip,
+                                          cfg.verify_checksum, blkno, project)
+        if project is not None:
+            k = desc.attno(project)
+            for v in pv:
+                valid_out.append(0 if v is None else 2 if v is pgtuple.EXT else 1)
+                vals_out.append(b"" if v is None or v is pgtuple.EXT else v)
+        for j, x in enumerate(stt):
+            if x & pgtuple.PAGE_RECHECK:
+                st.recheck_blocks.append(blkno + j)
+        return its, stt
     mvcc = cfg.snapshot is not None
     b0, b1 = _block_range(blocks, rel.nblocks)
     per_chunk = cfg.chunk_size // BLCKSZ
@@ -632,22 +730,29 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                     skip = cfg.skip_invisible and not mvcc
                     raw = bytes(buf.array[:n * BLCKSZ])
                     if np.array_equal(blocks_here, np.arange(base + c0, base + c0 + n)):
-                        its, status = pgpage.host_scan(raw, BLCKSZ, skip, attr_off, attr_width,
-                                                       lo, hi, cfg.verify_checksum, base + c0)
+                        its, status = walk(raw, base + c0)
                         items.extend(((base + c0 + (i >> 16)) << 16) | (i & 0xFFFF) for i in its)
                     else:
                         status = []
                         for j, b in enumerate(blocks_here.tolist()):
-                            its, stt = pgpage.host_scan(raw[j * BLCKSZ:(j + 1) * BLCKSZ], BLCKSZ,
-                                                        skip, attr_off, attr_width, lo, hi,
-                                                        cfg.verify_checksum, b)
+                            its, stt = walk(raw[j * BLCKSZ:(j + 1) * BLCKSZ], b)
                             items.extend((b << 16) | (i & 0xFFFF) for i in its)
                             status += stt
                     st.pages += n
                     st.bad_pages += sum(1 for s in status if s & 3)
             finally:
                 os.close(fd)
-    st.items = np.array(sorted(items), dtype=np.uint64)
+    order = np.argsort(np.array(items, dtype=np.uint64), kind="stable")
+    st.items = np.array(items, dtype=np.uint64)[order]
+    if general and project is not None:
+        k = desc.attno(project)
+        st.valid = np.array(valid_out, dtype=np.uint8)[order]
+        if desc.attlen[k] < 0:
+            st.values = [vals_out[j] for j in order]
+        else:
+            dt = np.float64 if desc.kinds[k] == "float" else np.int64
+            st.values = np.array([0 if isinstance(v, bytes) else v for v in vals_out], dtype=dt)[order]
+    st.recheck_blocks.sort()
     st.seconds = time.perf_counter() - t0
     return st
 

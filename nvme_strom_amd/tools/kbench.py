@@ -79,6 +79,26 @@ def main(argv=None):
             timed(lambda: heap_scan(pages, verify_checksum=True, attr_off=0, attr_width=8,
                                     lo=100, hi=5000)), nb)
         del pages
+        # tuple descriptor + qualifier lists (strom_heap_scan2): 10 columns
+        # with NULLs, short / long / TOASTed text before the predicated ones
+        from nvme_strom_amd.ops.heapscan import heap_scan2
+        from nvme_strom_amd.utils import pgtuple as T
+        desc, rows = T.synthetic(4000, seed=2)
+        tmpl = T.build_pages(rows, desc)
+        reps = max(1, min(n // len(tmpl), 0xFFFF // (len(tmpl) // 8192)))
+        pages = torch.from_numpy(np.frombuffer(tmpl * reps, dtype=np.uint8).copy()).to(dev)
+        nb = pages.numel()
+        for name, qs in (("heap_scan2_1qual", [T.Qual("a", "between", (-200_000, 300_000))]),
+                         ("heap_scan2_2qual", [T.Qual("a", "between", (-500_000, 200_000)),
+                                               T.Qual("b", "between", (0.1, 0.6))]),
+                         ("heap_scan2_text_eq", [T.Qual("name", "text_eq", ("k17",))]),
+                         ("heap_scan2_4qual_last_col", [T.Qual("c", "in", ([1, 2, 3],)),
+                                                        T.Qual("d", "notnull"),
+                                                        T.Qual("e", "between", (-0.5, 0.5)),
+                                                        T.Qual("tail", "between", (0, 50))])):
+            log(name, timed(lambda: heap_scan2(pages, desc, qs, verify_checksum=True,
+                                               skip_invisible=True)), nb)
+        del pages
     rng = np.random.default_rng(1)
     words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
     datasets = {

@@ -45,6 +45,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cpu-blocks", type=int, default=16384,
                     help="blocks the CPU baseline scans (a prefix: its tuple walk is slow)")
     ap.add_argument("--dir", default="/tmp/strom_pg")
+    ap.add_argument("--no-quals", dest="quals", action="store_false",
+                    help="skip the qualifier-list rows (10-column relation)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import nvme_strom_amd as S
@@ -110,6 +112,59 @@ def main(argv=None) -> int:
             best = row
     res["gpu_best_GBps"] = best["GBps"]            # best configuration's warm median
     res["gpu_best_cold_ms"] = best["cold_ms"]
+    # qualifier lists over a 10-column relation of the same size (NULLs,
+    # short / long / TOASTed text before the predicated columns): every tuple
+    # deformed on the GPU (strom_heap_scan2), at the best configuration above
+    if a.quals:
+        from nvme_strom_amd.utils import pgtuple as T
+        desc, rows = T.synthetic(a.template_pages * 56, seed=4)
+        tmpl2 = T.build_pages(rows, desc, with_checksum=False)
+        reps2 = max(1, int(a.gib * (1 << 30)) // len(tmpl2))
+        rel2 = pg_scan.Relation.write(os.path.join(a.dir, "16386"), tmpl2 * reps2)
+        one2 = pg_scan.Relation.write(os.path.join(a.dir, "16387"), tmpl2)
+        n2 = rel2.nblocks * 8192
+        t_pages = len(tmpl2) // 8192
+        qsets = {"quals1": [T.Qual("a", "between", (-200_000, 300_000))],
+                 "quals2": [T.Qual("a", "between", (-500_000, 200_000)),
+                            T.Qual("b", "between", (0.1, 0.6))]}
+        ccfg = pg_scan.ScanConfig(verify_checksum=False, chunk_size=best["chunk_mib"] << 20,
+                                  buffer_size=8 * best["chunk_mib"] << 20)
+        for name, qs in qsets.items():
+            ref2 = pg_scan.cpu_scan(one2, cfg, desc=desc, quals=qs)
+            g = pg_scan.HeapRelationScan(rel2, ccfg, "cuda", desc=desc, quals=qs)
+            for seg in rel2.segments:
+                fd = os.open(seg, os.O_RDONLY)
+                S.evict_file(fd)
+                os.close(fd)
+            t1 = time.perf_counter()
+            out = g.run(best["workers"])
+            cold = time.perf_counter() - t1
+            times = []
+            for r in range(a.reps):
+                for seg in rel2.segments:
+                    fd = os.open(seg, os.O_RDONLY)
+                    S.evict_file(fd)
+                    os.close(fd)
+                t1 = time.perf_counter()
+                out = g.run(best["workers"])
+                times.append(time.perf_counter() - t1)
+            g.close()
+            blk = (out.items >> np.uint64(16)).astype(np.int64)
+            ok = (len(out.items) == len(ref2.items) * reps2 and
+                  np.array_equal(out.items[blk < t_pages], ref2.items) and out.pages == rel2.nblocks)
+            med = float(np.median(times))
+            row = dict(GBps=round(n2 / med / 1e9, 2), ms=[round(t * 1e3, 1) for t in times],
+                       cold_ms=round(cold * 1e3, 1), workers=best["workers"],
+                       chunk_mib=best["chunk_mib"], quals=len(qs), selected=int(len(out.items)),
+                       relation_bytes=n2, verified=bool(ok),
+                       of_single_predicate=round(n2 / med / 1e9 / best["GBps"], 3))
+            res["runs"][f"gpu_{name}"] = row
+            _log("gpu", name, row)
+        for p in rel2.segments + one2.segments:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
     # the same bytes as a plain stream into HBM (bench shape), same storage
     # state: the I/O ceiling the scan runs against
     import torch

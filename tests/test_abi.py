@@ -79,3 +79,25 @@ int f(void) {
 ''')
     inc = os.path.join(ROOT, "csrc", "include")
     subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-I", inc, str(src)], check=True)
+
+
+def test_heap_scan2_layout_matches_c(tmp_path):
+    """The general heap-scan argument block (tuple descriptor + qualifier
+    list) as ctypes lays it out equals the C compiler's layout."""
+    src = tmp_path / "heap.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "strom/strom.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu\\n\","
+        "sizeof(struct strom_heap_tupdesc), sizeof(struct strom_heap_qual),"
+        "sizeof(struct strom_heap_scan2_args), offsetof(struct strom_heap_scan2_args, desc),"
+        "offsetof(struct strom_heap_scan2_args, nquals), offsetof(struct strom_heap_scan2_args, quals),"
+        "offsetof(struct strom_heap_scan2_args, recheck_count));return 0;}\n")
+    exe = tmp_path / "heap"
+    inc = os.path.join(ROOT, "csrc", "include")
+    subprocess.run(["gcc", "-std=c11", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [C.sizeof(N.HeapTupDesc), C.sizeof(N.HeapQual), C.sizeof(N.HeapScan2Args),
+            N.HeapScan2Args.desc.offset, N.HeapScan2Args.nquals.offset,
+            N.HeapScan2Args.quals.offset, N.HeapScan2Args.recheck_count.offset]
+    assert got == want
