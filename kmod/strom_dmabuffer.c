@@ -12,7 +12,12 @@
  * ONCE per NVMe controller, on first use, with one dma_map_page() of the
  * whole physically contiguous segment, and stays mapped until the buffer is
  * released (the request path does no per-page map/unmap and no allocation).
- * The node is validated before any allocation (reference pmemmap.c:646-650).
+ * A controller whose DMA layer cannot map 4 MiB at once (swiotlb bouncing
+ * caps a mapping at ~256 KiB) gets the segment mapped page by page instead.
+ * Any number of controllers may map one buffer (a raid0 route has up to
+ * STROM_ROUTE_MAX_DISKS members; a buffer may be reused across volumes).
+ * The node is validated before any allocation (reference pmemmap.c:646-650),
+ * and an mmap must lie inside the buffer (pmemmap.c:593).
  */
 #include <linux/anon_inodes.h>
 #include <linux/file.h>
@@ -24,18 +29,21 @@
 #define SEG_ORDER (22 - PAGE_SHIFT)          /* 4 MiB segments */
 #define SEG_SIZE (PAGE_SIZE << SEG_ORDER)
 
+#define SEG_PAGES (1 << SEG_ORDER)
+
 struct strom_dbuf_map {                  /* the segments as one controller sees them */
 	struct device *dev;              /* held (get_device) */
-	dma_addr_t *seg_dma;
+	bool per_page;                   /* dma[] holds one address per page */
+	dma_addr_t dma[];                /* per segment, or per page (per_page) */
 };
 
 struct strom_dma_buffer {
 	size_t length;
 	int node;
 	int nsegs;
-	struct mutex map_lock;
-	int nmaps;
-	struct strom_dbuf_map maps[STROM_MAX_ATTACH];
+	struct mutex map_lock;           /* guards maps / nmaps / cap_maps */
+	int nmaps, cap_maps;
+	struct strom_dbuf_map **maps;    /* each map stays put until release */
 	struct page *segs[];
 };
 
@@ -59,7 +67,13 @@ static const struct vm_operations_struct dmabuf_vm_ops = {
 
 static int dmabuf_mmap(struct file *filp, struct vm_area_struct *vma)
 {
+	struct strom_dma_buffer *b = filp->private_data;
+
 	if (!(vma->vm_flags & VM_SHARED))
+		return -EINVAL;
+	/* the mapping must lie inside the buffer (reference pmemmap.c:593) */
+	if (vma->vm_pgoff > (b->length >> PAGE_SHIFT) ||
+	    vma_pages(vma) > (b->length >> PAGE_SHIFT) - vma->vm_pgoff)
 		return -EINVAL;
 	vm_flags_set(vma, VM_DONTEXPAND | VM_DONTDUMP);
 	vma->vm_ops = &dmabuf_vm_ops;
@@ -74,14 +88,17 @@ static int dmabuf_release(struct inode *inode, struct file *filp)
 	/* the last reference: no request can still target the buffer (every
 	 * SSD2RAM task holds the file until its last completion) */
 	for (j = 0; j < b->nmaps; j++) {
-		struct strom_dbuf_map *m = &b->maps[j];
+		struct strom_dbuf_map *m = b->maps[j];
+		const int n = m->per_page ? b->nsegs * SEG_PAGES : b->nsegs;
 
-		for (i = 0; i < b->nsegs; i++)
-			if (m->seg_dma[i])
-				dma_unmap_page(m->dev, m->seg_dma[i], SEG_SIZE, DMA_FROM_DEVICE);
-		kfree(m->seg_dma);
+		for (i = 0; i < n; i++)
+			if (m->dma[i])
+				dma_unmap_page(m->dev, m->dma[i], m->per_page ? PAGE_SIZE : SEG_SIZE,
+					       DMA_FROM_DEVICE);
 		put_device(m->dev);
+		kfree(m);
 	}
+	kfree(b->maps);
 	for (i = 0; i < b->nsegs; i++) {
 		struct page *p = b->segs[i];
 		int k;
@@ -114,57 +131,104 @@ struct page *strom_dma_buffer_page(struct vm_area_struct *vma, unsigned long off
 	return b->segs[off / SEG_SIZE] + ((off % SEG_SIZE) >> PAGE_SHIFT);
 }
 
-/* the segment table of `b` as seen by `dev`, mapped on first use */
-static struct strom_dbuf_map *dbuf_map_for(struct strom_dma_buffer *b, struct device *dev)
+/* map every segment for `dev`: whole segments, or page by page when the
+ * DMA layer refuses a 4 MiB mapping; NULL on failure */
+static struct strom_dbuf_map *dbuf_map_new(struct strom_dma_buffer *b, struct device *dev,
+					   bool per_page)
 {
+	const int n = per_page ? b->nsegs * SEG_PAGES : b->nsegs;
+	struct strom_dbuf_map *m = kzalloc(struct_size(m, dma, n), GFP_KERNEL);
+	int i;
+
+	if (!m)
+		return NULL;
+	m->per_page = per_page;
+	for (i = 0; i < n; i++) {
+		struct page *pg = per_page ? b->segs[i / SEG_PAGES] + i % SEG_PAGES : b->segs[i];
+		const size_t sz = per_page ? PAGE_SIZE : SEG_SIZE;
+
+		m->dma[i] = dma_map_page(dev, pg, 0, sz, DMA_FROM_DEVICE);
+		if (dma_mapping_error(dev, m->dma[i])) {
+			while (i-- > 0)
+				dma_unmap_page(dev, m->dma[i], sz, DMA_FROM_DEVICE);
+			kfree(m);
+			return NULL;
+		}
+	}
+	m->dev = get_device(dev);
+	return m;
+}
+
+/* The segment table of the DMA buffer behind `filp` as controller `dev` sees
+ * it, mapped on first use.  The result stays valid until the buffer is
+ * released (every SSD2RAM task holds the file), so a request resolves it
+ * once and then computes its PRP entries without the lock. */
+struct strom_dbuf_map *strom_dma_buffer_map(struct file *filp, struct device *dev)
+{
+	struct strom_dma_buffer *b = filp->private_data;
 	struct strom_dbuf_map *m = NULL;
-	dma_addr_t *seg;
-	int i, j;
+	int j;
 
 	mutex_lock(&b->map_lock);
 	for (j = 0; j < b->nmaps; j++)
-		if (b->maps[j].dev == dev) {
-			m = &b->maps[j];
+		if (b->maps[j]->dev == dev) {
+			m = b->maps[j];
 			goto out;
 		}
-	if (b->nmaps == ARRAY_SIZE(b->maps))
-		goto out;
-	seg = kmalloc_array(b->nsegs, sizeof(*seg), GFP_KERNEL | __GFP_ZERO);
-	if (!seg)
-		goto out;
-	for (i = 0; i < b->nsegs; i++) {
-		seg[i] = dma_map_page(dev, b->segs[i], 0, SEG_SIZE, DMA_FROM_DEVICE);
-		if (dma_mapping_error(dev, seg[i])) {
-			while (i-- > 0)
-				dma_unmap_page(dev, seg[i], SEG_SIZE, DMA_FROM_DEVICE);
-			kfree(seg);
+	if (b->nmaps == b->cap_maps) {
+		int cap = b->cap_maps ? 2 * b->cap_maps : 4;
+		struct strom_dbuf_map **nm = krealloc_array(b->maps, cap, sizeof(*nm), GFP_KERNEL);
+
+		if (!nm)
 			goto out;
-		}
+		b->maps = nm;
+		b->cap_maps = cap;
 	}
-	m = &b->maps[b->nmaps];
-	m->dev = get_device(dev);
-	m->seg_dma = seg;
-	b->nmaps++;
+	m = dbuf_map_new(b, dev, false);
+	if (!m)
+		m = dbuf_map_new(b, dev, true);
+	if (m)
+		b->maps[b->nmaps++] = m;
 out:
 	mutex_unlock(&b->map_lock);
 	return m;
 }
 
-/* Bus address, for controller `dev`, of byte `off` of the DMA buffer behind
- * `filp`; *contig = bytes to the end of its segment. */
-int strom_dma_buffer_dma(struct file *filp, struct device *dev, u64 off, u64 *addr, u64 *contig)
+/* Bus address through map `m` of byte `off` of the DMA buffer behind
+ * `filp`; *contig = bytes that stay bus-contiguous from there (to the end of
+ * the segment, or of the page for a page-by-page map).  No lock. */
+int strom_dma_buffer_addr(struct file *filp, const struct strom_dbuf_map *m, u64 off, u64 *addr,
+			  u64 *contig)
 {
 	struct strom_dma_buffer *b = filp->private_data;
-	struct strom_dbuf_map *m;
 
 	if (off >= b->length)
 		return -EFAULT;
-	m = dbuf_map_for(b, dev);
-	if (!m)
-		return -EIO;
-	*addr = m->seg_dma[off / SEG_SIZE] + off % SEG_SIZE;
-	*contig = SEG_SIZE - off % SEG_SIZE;
+	if (m->per_page) {
+		*addr = m->dma[off >> PAGE_SHIFT] + (off & (PAGE_SIZE - 1));
+		*contig = PAGE_SIZE - (off & (PAGE_SIZE - 1));
+	} else {
+		*addr = m->dma[off / SEG_SIZE] + off % SEG_SIZE;
+		*contig = SEG_SIZE - off % SEG_SIZE;
+	}
 	return 0;
+}
+
+/* hand [off, off+len) back to the CPU after the device wrote it */
+void strom_dma_buffer_sync_for_cpu(struct file *filp, const struct strom_dbuf_map *m, u64 off,
+				   u64 len)
+{
+	while (len) {
+		u64 a, contig;
+
+		if (strom_dma_buffer_addr(filp, m, off, &a, &contig))
+			return;
+		if (contig > len)
+			contig = len;
+		dma_sync_single_for_cpu(m->dev, a, contig, DMA_FROM_DEVICE);
+		off += contig;
+		len -= contig;
+	}
 }
 
 int strom_alloc_dma_buffer(struct strom_alloc_dma_buffer *arg)

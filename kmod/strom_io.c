@@ -107,7 +107,8 @@ struct strom_req {
 	unsigned int acct_sectors;
 	/* SSD2RAM: the DMA buffer range written (one segment: merges never
 	 * cross one), handed back to the CPU on completion */
-	dma_addr_t ram_dma;
+	const struct strom_dbuf_map *ram_map;
+	u64 ram_off;
 	u32 ram_len;
 };
 
@@ -129,8 +130,8 @@ static enum rq_end_io_ret strom_end_io(struct request *rq, blk_status_t err)
 	bdev_end_io_acct(r->mbr->disk->part0, REQ_OP_READ, r->acct_sectors, r->acct_start);
 	if (r->vol_part)
 		bdev_end_io_acct(r->vol_part, REQ_OP_READ, r->acct_sectors, r->vol_acct_start);
-	if (r->ram_len)
-		dma_sync_single_for_cpu(r->mbr->dma_dev, r->ram_dma, r->ram_len, DMA_FROM_DEVICE);
+	if (r->ram_len)          /* the task (not yet put) holds the buffer's file */
+		strom_dma_buffer_sync_for_cpu(r->task->dbuf_filp, r->ram_map, r->ram_off, r->ram_len);
 	req_release_dma(r);
 	if (r->gmap && atomic_dec_and_test(&r->gmap->inflight))
 		wake_up_all(&r->gmap->drain);
@@ -150,12 +151,15 @@ struct copy_ctx {
 	u64 ram_base;                    /* SSD2RAM: buffer offset of dest_uaddr; the
 					    planner works in buffer offsets so that
 					    dest_segment matches the real segments */
+	/* SSD2RAM: the buffer's map per route member, resolved on the member's
+	 * first request (one lock then, none per request or PRP entry) */
+	const struct strom_dbuf_map *ram_maps[STROM_ROUTE_MAX_DISKS];
 	struct strom_planner pl;
 };
 
 struct ram_addr_ctx {
-	struct device *dev;
 	struct file *dbuf;
+	const struct strom_dbuf_map *map;
 	u64 base;                        /* buffer offset of the request */
 };
 
@@ -164,10 +168,11 @@ static int ram_page_addr(void *p, u64 off, u32 need, u64 *a)
 {
 	struct ram_addr_ctx *x = p;
 	u64 contig;
-	int rc = strom_dma_buffer_dma(x->dbuf, x->dev, x->base + off, a, &contig);
+	int rc = strom_dma_buffer_addr(x->dbuf, x->map, x->base + off, a, &contig);
 
 	if (!rc && contig < need)
-		rc = -EINVAL;          /* a merge never crosses a segment */
+		rc = -EINVAL;          /* a merge never crosses a segment (or, mapped
+					  page by page, a PRP entry a page) */
 	return rc;
 }
 
@@ -209,12 +214,17 @@ static int submit_extent(void *p, const struct strom_extent *e)
 						   e->len, (u64 *)r->prp_list, STROM_CORE_PRP_LIST_MAX,
 						   r->prp_dma, &prps);
 	} else {
-		struct ram_addr_ctx rx = { mbr->dma_dev, x->t->dbuf_filp, e->dest };
+		const int mi = e->member < 0 ? 0 : e->member;
+		struct ram_addr_ctx rx = { x->t->dbuf_filp, x->ram_maps[mi], e->dest };
 
-		rc = strom_core_build_prps(ram_page_addr, &rx, 0, e->len, (u64 *)r->prp_list,
-					   STROM_CORE_PRP_LIST_MAX, r->prp_dma, &prps);
+		if (!rx.map)
+			rx.map = x->ram_maps[mi] = strom_dma_buffer_map(x->t->dbuf_filp, mbr->dma_dev);
+		rc = rx.map ? strom_core_build_prps(ram_page_addr, &rx, 0, e->len, (u64 *)r->prp_list,
+						    STROM_CORE_PRP_LIST_MAX, r->prp_dma, &prps)
+			    : -EIO;
 		if (!rc) {
-			r->ram_dma = prps.prp1;
+			r->ram_map = rx.map;
+			r->ram_off = e->dest;
 			r->ram_len = e->len;
 		}
 	}

@@ -216,7 +216,12 @@ int strom_memcpy_ssd2ram(struct strom_session *s,
 int strom_alloc_dma_buffer(struct strom_alloc_dma_buffer *arg);
 bool strom_is_dma_buffer(struct vm_area_struct *vma);
 struct page *strom_dma_buffer_page(struct vm_area_struct *vma, unsigned long off);
-int strom_dma_buffer_dma(struct file *filp, struct device *dev, u64 off, u64 *addr, u64 *contig);
+struct strom_dbuf_map;
+struct strom_dbuf_map *strom_dma_buffer_map(struct file *filp, struct device *dev);
+int strom_dma_buffer_addr(struct file *filp, const struct strom_dbuf_map *m, u64 off, u64 *addr,
+			  u64 *contig);
+void strom_dma_buffer_sync_for_cpu(struct file *filp, const struct strom_dbuf_map *m, u64 off,
+				   u64 len);
 
 /* ---- statistics ---------------------------------------------------------- */
 struct strom_stats {

@@ -14,8 +14,10 @@
  *     or, for hidden path disks, by "<pci>/<ctrl>/<disk>" name.  Every member
  *     must be a blk-mq NVMe namespace, and the geometry must be consistent
  *     (strom_core_raid0_check) and fit the members' capacity and the
- *     volume's size.  A single-path alias must answer NVME_IOCTL_ID with the
- *     head's nsid and have exactly the head's capacity.  That md members
+ *     volume's size.  A single-path alias must be named as a path of the
+ *     head ("nvme<S>c<C>n<H>" for head "nvme<S>n<H>": same subsystem and
+ *     head instance), answer NVME_IOCTL_ID with the head's nsid and have
+ *     exactly the head's capacity.  That md members
  *     really are the array's slaves is NOT verifiable through exported
  *     interfaces (md's rdev list and the holder links are private): it is
  *     asserted by the administrator who registers the route
@@ -37,6 +39,21 @@
 #include <linux/slab.h>
 
 #include "strom_kmod.h"
+
+/* Native multipath names a head "nvme<S>n<H>" and each of its paths
+ * "nvme<S>c<C>n<H>" (S the subsystem instance, H the head's): a path belongs
+ * to a head exactly when S and H agree. */
+static bool path_of_head(const char *head, const char *path)
+{
+	unsigned int s1, h1, s2, c2, h2;
+	char tail;
+
+	if (sscanf(head, "nvme%un%u%c", &s1, &h1, &tail) != 2)
+		return false;
+	if (sscanf(path, "nvme%uc%un%u%c", &s2, &c2, &h2, &tail) != 3)
+		return false;
+	return s1 == s2 && h1 == h2;
+}
 
 static LIST_HEAD(routes);
 static DEFINE_MUTEX(routes_lock);
@@ -368,8 +385,9 @@ int strom_set_route(const struct strom_set_route *r)
 			}
 		}
 	} else {
-		/* a path alias of a multipath head: one member with the head's
-		 * nsid and exactly its capacity */
+		/* a path alias of a multipath head: one member that is a path of
+		 * THIS head by name (same subsystem and head instance), answers
+		 * the head's nsid and has exactly its capacity */
 		int head_nsid = -1;
 
 		rc = -EINVAL;
@@ -379,7 +397,10 @@ int strom_set_route(const struct strom_set_route *r)
 		if (vd) {
 			struct gendisk *hd = dev_to_disk(vd);
 
-			if (hd->fops && hd->fops->ioctl)
+			/* only an NVMe head is asked NVME_IOCTL_ID (never another
+			 * driver's ioctl, e.g. dm passing it through) */
+			if (path_of_head(hd->disk_name, v->m[0].disk->disk_name) && hd->fops &&
+			    hd->fops->ioctl)
 				head_nsid = hd->fops->ioctl(hd->part0, BLK_OPEN_READ, NVME_IOCTL_ID, 0);
 			put_device(vd);
 		}

@@ -771,6 +771,111 @@ static int scn_raid0_route(void)
 	return counters_clean("after teardown");
 }
 
+/* SSD2RAM from a 12-controller raid0 route into one DMA buffer whose DMA
+ * layer cannot map a 4 MiB segment at once (swiotlb-like 256 KiB cap): the
+ * buffer keeps a map per controller (more than STROM_MAX_ATTACH), each page
+ * by page, and every chunk lands intact.  Also: mmap of the buffer must lie
+ * inside it (reference pmemmap.c:593). */
+static int scn_ssd2ram_wide_route(void)
+{
+	enum { NM = 12 };
+	const u32 chunk_sects = 128, cs = 128 << 10, n = 96;
+	struct strom_set_route *r = calloc(1, sizeof(*r));
+	struct strom_alloc_dma_buffer ab = { 12ull << 20, -1, -1 };
+	struct strom_memcpy_ssd2ram q = { 0 };
+	struct ksim_counters c0, c1;
+	int ctrl[NM], ns[NM], md, fs, dev, fd, i;
+	unsigned long ua;
+	struct fmodel f;
+	u32 ids[96];
+	u8 *got, *exp;
+	long st;
+
+	ksim_init();
+	for (i = 0; i < NM; i++) {
+		char pci[16];
+
+		snprintf(pci, sizeof(pci), "0000:%02x:00.0", 0x41 + i);
+		ctrl[i] = ksim_ctrl_new(pci, 0);
+		ns[i] = ksim_ns_new(ctrl[i], 1, 9, 32ull << 11, 256, 0);
+		ksim_ctrl_config(ctrl[i], 1, 0, 0);
+	}
+	md = ksim_md_new(ns, NM, chunk_sects, NULL);
+	fs = ksim_fs_new(md, 0, "xfs", 12);
+	f = new_file(fs, 12ull << 20, 67, linear_map(3072, 256));
+	CHECK_EQ(ksim_module_load(), 0);
+	dev = ksim_dev_open(0);
+	fd = ksim_file_open(f.fi, 1);
+	r->volume_major = ksim_disk_devt(md) >> 20;
+	r->volume_minor = ksim_disk_devt(md) & 0xfffff;
+	r->nmembers = NM;
+	r->chunk_sects = chunk_sects;
+	r->nzones = 1;
+	r->zone_end[0] = (32ull << 11) / chunk_sects * chunk_sects * NM;
+	r->zone_nb_dev[0] = NM;
+	for (i = 0; i < NM; i++) {
+		r->zone_devs[0][i] = (unsigned char)i;
+		r->member_major[i] = ksim_disk_devt(ns[i]) >> 20;
+		r->member_minor[i] = ksim_disk_devt(ns[i]) & 0xfffff;
+	}
+	ksim_set_admin(1);
+	CHECK_EQ(ksim_ioctl(dev, STROM_IOCTL__SET_ROUTE, r), 0);
+	ksim_set_admin(0);
+	CHECK_EQ(ksim_ioctl(dev, STROM_IOCTL__ALLOC_DMA_BUFFER, &ab), 0);
+	/* mappings must lie inside the 12 MiB buffer */
+	CHECK(ksim_mmap(ab.dmabuf_fdesc, 13ull << 20, 0, 1) == 0);
+	CHECK_EQ(ksim_last_mmap_rc(), -EINVAL);
+	CHECK(ksim_mmap(ab.dmabuf_fdesc, 2ull << 20, 11ull << 20, 1) == 0);
+	CHECK_EQ(ksim_last_mmap_rc(), -EINVAL);
+	CHECK(ksim_mmap(ab.dmabuf_fdesc, 4096, 12ull << 20, 1) == 0);
+	CHECK_EQ(ksim_last_mmap_rc(), -EINVAL);
+	ua = ksim_mmap(ab.dmabuf_fdesc, 12ull << 20, 0, 1);
+	CHECK(ua);
+	ksim_close(ab.dmabuf_fdesc);
+	ksim_dma_max_mapping(256 << 10);
+	for (i = 0; i < (int)n; i++)
+		ids[i] = (u32)((i * 37 + 5) % 96);
+	ksim_counters(&c0);
+	q.dest_uaddr = (void *)ua;
+	q.file_desc = fd;
+	q.nr_chunks = n;
+	q.chunk_sz = cs;
+	q.chunk_ids = ids;
+	CHECK_EQ(ksim_ioctl(dev, STROM_IOCTL__MEMCPY_SSD2RAM, &q), 0);
+	CHECK_EQ(wait_task(dev, q.dma_task_id, &st), 0);
+	CHECK_EQ(st, 0);
+	CHECK_EQ(q.nr_ssd2ram, n);
+	got = malloc((u64)n * cs);
+	exp = malloc(cs);
+	CHECK_EQ(ksim_user_read(ua, got, (u64)n * cs), 0);
+	for (i = 0; i < (int)n; i++) {
+		chunk_bytes(&f, (u64)ids[i] * cs, cs, exp);
+		CHECK(!memcmp(got + (u64)i * cs, exp, cs));
+	}
+	/* one refused segment map, then page by page, once per controller */
+	ksim_counters(&c1);
+	CHECK(c1.dma_map_calls - c0.dma_map_calls <= NM * (1 + 3 * 1024));
+	CHECK(c1.dma_map_calls - c0.dma_map_calls >= NM * 3 * 1024);
+	/* a second copy reuses the maps */
+	CHECK_EQ(ksim_ioctl(dev, STROM_IOCTL__MEMCPY_SSD2RAM, &q), 0);
+	CHECK_EQ(wait_task(dev, q.dma_task_id, &st), 0);
+	CHECK_EQ(st, 0);
+	ksim_counters(&c0);
+	CHECK_EQ(c0.dma_map_calls - c1.dma_map_calls, 0);
+	ksim_dma_max_mapping(0);
+	free(got);
+	free(exp);
+	CHECK_EQ(ksim_munmap(ua), 0);
+	ksim_close(fd);
+	ksim_close(dev);
+	ksim_quiesce();
+	ksim_module_unload();
+	ksim_fini();
+	free(r);
+	free(f.data);
+	return counters_clean("after teardown");
+}
+
 /* NVMe multipath: the head is bio-based; its hidden path disk is named */
 static int scn_multipath_alias(void)
 {
@@ -1024,6 +1129,7 @@ static const struct { const char *name; int (*fn)(void); } scenarios[] = {
 	{ "errors_and_reclaim", scn_errors_and_reclaim },
 	{ "unmap_inflight", scn_unmap_inflight },
 	{ "raid0_route", scn_raid0_route },
+	{ "ssd2ram_wide_route", scn_ssd2ram_wide_route },
 	{ "multipath_alias", scn_multipath_alias },
 	{ "stale_volume_cache", scn_stale_volume_cache },
 	{ "registry_and_stats", scn_registry_and_stats },

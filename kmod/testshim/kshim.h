@@ -225,6 +225,10 @@ struct fd { struct file *file; };
 #endif
 struct vm_area_struct { unsigned long vm_start, vm_end, vm_pgoff, vm_flags; struct file *vm_file;
 	const struct vm_operations_struct *vm_ops; };
+static inline unsigned long vma_pages(const struct vm_area_struct *v)
+{
+	return (v->vm_end - v->vm_start) >> PAGE_SHIFT;
+}
 struct vm_fault { struct vm_area_struct *vma; pgoff_t pgoff; struct page *page; };
 struct vm_operations_struct { vm_fault_t (*fault)(struct vm_fault *); };
 struct mm_struct;
@@ -401,6 +405,7 @@ bool node_online(int nid);
 /* memory + strings */
 void *kzalloc(size_t, gfp_t);
 void *kmalloc_array(size_t n, size_t size, gfp_t);
+void *krealloc_array(void *p, size_t n, size_t size, gfp_t);
 void *kvmalloc_array(size_t n, size_t size, gfp_t);
 void kfree(const void *);
 void kvfree(const void *);
@@ -408,6 +413,7 @@ void *memdup_user(const void __user *, size_t);
 void *memset(void *, int, size_t);
 void *memcpy(void *, const void *, size_t);
 int strcmp(const char *, const char *);
+int sscanf(const char *, const char *, ...);
 int strncmp(const char *, const char *, size_t);
 char *strchr(const char *, int);
 long strscpy(char *dst, const char *src, size_t count);

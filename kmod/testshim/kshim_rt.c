@@ -192,6 +192,8 @@ unsigned long clear_user(void __user *to, unsigned long n)
 	return 0;
 }
 
+#define KSIM_MD_MAX 32   /* md members (the route ABI allows STROM_ROUTE_MAX_DISKS) */
+
 /* ------------------------------------------------------------ allocations */
 static void *kalloc(size_t n, gfp_t gfp, bool zero)
 {
@@ -215,6 +217,20 @@ void *kmalloc_array(size_t n, size_t size, gfp_t gfp)
 	if (size && n > SIZE_MAX / size)
 		return NULL;
 	return kalloc(n * size, gfp, gfp & __GFP_ZERO);
+}
+
+void *krealloc_array(void *p, size_t n, size_t size, gfp_t gfp)
+{
+	void *q;
+
+	if (size && n > SIZE_MAX / size)
+		return NULL;
+	if (!(gfp & GFP_ATOMIC))
+		check_sleepable("GFP_KERNEL allocation", NULL, 0);
+	q = realloc(p, n * size ? n * size : 1);
+	if (q && !p)
+		CNT_ADD(kmallocs_live, 1);
+	return q;
 }
 
 void *kvmalloc_array(size_t n, size_t size, gfp_t gfp)
@@ -915,6 +931,12 @@ void kunmap_local(const void *p) { (void)p; }
 /* ------------------------------------------------------------ DMA API */
 static int g_fail_map_at;                 /* fail the Nth dma_map_page (1-based) */
 static int g_nmaps;
+static size_t g_max_mapping;              /* swiotlb-like cap on one mapping (0: none) */
+
+void ksim_dma_max_mapping(size_t bytes)
+{
+	__atomic_store_n(&g_max_mapping, bytes, __ATOMIC_SEQ_CST);
+}
 
 void ksim_fail_map(int nth)
 {
@@ -936,6 +958,12 @@ dma_addr_t dma_map_page(struct device *dev, struct page *pg, size_t off, size_t 
 	}
 	if (f && n == f)
 		return DMA_MAPPING_ERROR;
+	{
+		size_t cap = __atomic_load_n(&g_max_mapping, __ATOMIC_SEQ_CST);
+
+		if (cap && sz > cap)
+			return DMA_MAPPING_ERROR;   /* what a bounce-buffered device does */
+	}
 	return iommu_map(dev->iommu, (char *)pg->kaddr + off, sz);
 }
 
@@ -1218,9 +1246,9 @@ struct ksim_disk {
 	u8 *image;
 	/* md raid0 (single zone) / multipath head */
 	int nmembers;
-	struct ksim_disk *members[8];
+	struct ksim_disk *members[KSIM_MD_MAX];
 	u32 chunk_sects;
-	u64 data_offset[8];
+	u64 data_offset[KSIM_MD_MAX];
 };
 
 #define MAX_DISKS 64
@@ -1659,6 +1687,8 @@ int ksim_md_new(const int *members, int n, u32 chunk_sects, const u64 *data_offs
 	u64 per = UINT64_MAX;
 	int i;
 
+	if (n < 1 || n > KSIM_MD_MAX)
+		abort();
 	snprintf(name, sizeof(name), "md%d", g_next_minor[9]);
 	d = disk_new(DK_MD, name, 9, true);
 	d->nmembers = n;
@@ -2040,12 +2070,20 @@ void vm_flags_set(struct vm_area_struct *vma, unsigned long flags)
 	vma->vm_flags |= flags;
 }
 
+static int g_last_mmap_rc;
+
+int ksim_last_mmap_rc(void)
+{
+	return __atomic_load_n(&g_last_mmap_rc, __ATOMIC_SEQ_CST);
+}
+
 unsigned long ksim_mmap(int fd, u64 len, u64 off, int shared)
 {
 	struct file *f = fget(fd);
 	struct ksim_vma *v;
 	int i, rc;
 
+	__atomic_store_n(&g_last_mmap_rc, 0, __ATOMIC_SEQ_CST);
 	if (!f)
 		return 0;
 	v = calloc(1, sizeof(*v));
@@ -2059,6 +2097,7 @@ unsigned long ksim_mmap(int fd, u64 len, u64 off, int shared)
 	v->pages = calloc(v->npages, sizeof(*v->pages));
 	rc = f->f_op && f->f_op->mmap ? f->f_op->mmap(f, &v->vma) : -ENODEV_SIM;
 	if (rc) {
+		__atomic_store_n(&g_last_mmap_rc, rc, __ATOMIC_SEQ_CST);
 		fput(f);
 		free(v->pages);
 		free(v);

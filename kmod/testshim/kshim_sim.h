@@ -51,6 +51,7 @@ void ksim_set_verbose(int v);
 void ksim_poison_user(const void *p, size_t n);
 void ksim_fail_cmd(int nth, int blk_status);
 void ksim_fail_map(int nth);
+void ksim_dma_max_mapping(size_t bytes);   /* refuse dma_map_page larger than this */
 
 int ksim_ctrl_new(const char *pci_name, int numa_node);
 void ksim_ctrl_config(int ctrl, int reorder, int delay_us, int hold);
@@ -85,6 +86,7 @@ long ksim_read(int fd, void *buf, uint64_t n);
 int ksim_close(int fd);
 const char *ksim_fd_name(int fd);
 unsigned long ksim_mmap(int fd, uint64_t len, uint64_t off, int shared);
+int ksim_last_mmap_rc(void);   /* the mmap handler's error of the last failed ksim_mmap */
 int ksim_munmap(unsigned long addr);
 int ksim_user_read(unsigned long addr, void *dst, uint64_t len);
 #endif

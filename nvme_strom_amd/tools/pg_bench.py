@@ -149,9 +149,9 @@ def main(argv=None) -> int:
                 out = g.run(best["workers"])
                 times.append(time.perf_counter() - t1)
             g.close()
-            blk = (out.items >> np.uint64(16)).astype(np.int64)
+            blk2 = (out.items >> np.uint64(16)).astype(np.int64)
             ok = (len(out.items) == len(ref2.items) * reps2 and
-                  np.array_equal(out.items[blk < t_pages], ref2.items) and out.pages == rel2.nblocks)
+                  np.array_equal(out.items[blk2 < t_pages], ref2.items) and out.pages == rel2.nblocks)
             med = float(np.median(times))
             row = dict(GBps=round(n2 / med / 1e9, 2), ms=[round(t * 1e3, 1) for t in times],
                        cold_ms=round(cold * 1e3, 1), workers=best["workers"],
