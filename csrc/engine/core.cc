@@ -87,7 +87,12 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "bar_map") { bar_map = parse_bool(v); return 0; }
   if (k == "coalesce") { coalesce = parse_bool(v); return 0; }
   if (k == "ingest") { ingest = parse_bool(v); return 0; }
-  if (k == "hdp_sync") { hdp_sync = parse_bool(v); return 0; }
+  if (k == "hdp_sync") {
+    if (!num_ok) { hdp_sync = parse_bool(v) ? 1 : 0; return 0; }
+    if (n < 0 || n > 2) return -EINVAL;
+    hdp_sync = (int)n;
+    return 0;
+  }
   if (k == "fixed_bufs") { fixed_bufs = parse_bool(v); return 0; }
   if (k == "io_prof") { io_prof = parse_bool(v); return 0; }
   if (k == "ingest_min") {

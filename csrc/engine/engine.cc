@@ -441,7 +441,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   // their members are read with O_DIRECT, coherent with dirty pages)
   if (plan.nr_ram && f) {
     rc = copy_ram_chunks(f->fd_buffered, plan, a->chunk_sz, pp.file_size, ram_dest);
-    if (rc == 0 && !a->wb_buffer) gmap->bar_flush((const uint8_t *)ram_dest);
+    if (rc == 0 && !a->wb_buffer) gmap->bar_flush((const uint8_t *)ram_dest, true);
   }
   t->frozen = true;
   uint64_t id = t->id;

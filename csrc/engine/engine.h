@@ -67,8 +67,11 @@ struct Config {
                                  // greatest priority (a hardware queue of its
                                  // own, not shared with normal-priority streams)
   uint32_t ingest_piece = 256u << 10;  // bytes per ingest descriptor
-  bool hdp_sync = false;         // wait for each HDP flush to complete (read
-                                 // back) instead of posting it
+  int hdp_sync = 2;              // HDP flush after CPU stores through the BAR:
+                                 // 0 posted; 1 read back after every write; 2 read
+                                 // back once per worker batch / per ioctl's page-cache
+                                 // chunks, posted on the synchronous small-read path
+                                 // (same-thread consumer; A/B in profiles/r4/hdp)
   bool fixed_bufs = true;        // register each worker's pinned staging with its
                                  // io_uring (IORING_REGISTER_BUFFERS) and read
                                  // into it with READ_FIXED (no per-I/O page
@@ -227,7 +230,8 @@ struct GpuMapping {
   // sfence, then an HDP flush (write + read back the flush register, as
   // the runtime does for CPU-written kernargs in VRAM); without the
   // register, a read-back of the last dword drains the posted writes
-  void bar_flush(const uint8_t *last) const;
+  // `batch`: the flush ends a batch / ioctl (hdp_sync=2 reads it back)
+  void bar_flush(const uint8_t *last, bool batch = false) const;
   ~GpuMapping();
   bool detached = false;
   std::atomic<bool> draining{false};  // an UNMAP waits for inflight == 0

@@ -347,7 +347,7 @@ struct IoEngine::Worker {
 
   void flush_done() {
     if (fin.empty()) return;
-    for (auto &b : bar_dirty) b.first->bar_flush(b.second);
+    for (auto &b : bar_dirty) b.first->bar_flush(b.second, true);
     bar_dirty.clear();
     if (nbar) {
       hist_copy(mono_ns() - now_ns, nbar);

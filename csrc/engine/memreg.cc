@@ -68,20 +68,26 @@ bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len, bool flush
   return true;
 }
 
-// The HDP flush is POSTED by default: the register write travels behind the
-// data writes (PCIe posted writes stay in order), and anything that can
-// consume the bytes afterwards — a kernel launch, an SDMA copy — is started
-// by a later doorbell write, itself posted behind the flush.  Reading the
-// register back (hdp_sync=1, what the runtime does for kernargs) waits for
-// the flush to finish: +1.4 us per call on MI355X (round 1 p50 phases).
-// tests/test_gpu_core.py::test_pread_gpu_visible_to_next_kernel checks the
-// posted form on 1000 distinct offsets, each read by a kernel launched right
-// after pread_gpu returns.
-void GpuMapping::bar_flush(const uint8_t *last) const {
+// HDP flush after CPU stores through the BAR (config hdp_sync):
+//   2 (default)  read back once per worker batch and per ioctl's page-cache
+//                chunks (`batch`): the flush has completed before the task
+//                completes, for any consumer (another thread's kernel, an RCCL
+//                peer).  Posted on the synchronous small-read path (pread_gpu):
+//                there the consumer is started by the same thread, whose
+//                doorbell write is posted behind the flush, and the read-back
+//                would add its PCIe round trip to every 4 KiB read
+//                (profiles/r4/hdp has the A/B).
+//   1            read back after every write (what the runtime does for
+//                kernargs it writes into VRAM).
+//   0            posted everywhere.
+// tests/test_gpu_core.py checks the posted form (next kernel, SDMA readback,
+// a kernel on another stream) on hundreds of distinct offsets.
+void GpuMapping::bar_flush(const uint8_t *last, bool batch) const {
   _mm_sfence();
   if (hdp) {
     *hdp = 1u;
-    if (config().hdp_sync) (void)*hdp;
+    const int mode = config().hdp_sync;
+    if (mode == 1 || (mode == 2 && batch)) (void)*hdp;
   } else {
     // no flush register: a read from the device cannot pass the posted
     // writes before it

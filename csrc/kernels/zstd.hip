@@ -1505,10 +1505,13 @@ std::map<std::pair<int, void *>, Scratch> g_scratch;
 uint64_t g_scratch_clock = 0;
 constexpr size_t kScratchKeep = 8;   // streams with a cached buffer
 
+// Caller holds g_mu until its launch is enqueued: an eviction (or
+// strom_zstd_release) by another thread frees a buffer only with hipFree /
+// hipStreamSynchronize, which wait for work already QUEUED — so the launch
+// that uses the pointer must be queued before the lock drops.
 uint8_t *scratch_for(void *stream, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(g_mu);
   auto it = g_scratch.find({dev, stream});
   if (it == g_scratch.end()) {
     // bound the cache: a caller cycling through many streams would
@@ -1574,11 +1577,13 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
   uint32_t grid = nstreams < res ? nstreams : res;
   if (grid > 65535) grid = 65535;
   uint8_t *sc = (uint8_t *)scratch;
+  std::unique_lock<std::mutex> g(g_mu, std::defer_lock);
   if (sc) {
     const uint64_t slots = scratch_bytes / SLOT;
     if (!slots) return -22;
     if (grid > slots) grid = (uint32_t)slots;
   } else {
+    g.lock();                  // held through the launch (scratch_for)
     sc = scratch_for(stream, (size_t)grid * SLOT);
     if (!sc) return -12;
   }

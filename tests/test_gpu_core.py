@@ -198,6 +198,35 @@ def test_pread_gpu_visible_to_sdma_readback(S, tmp_path):
     assert not bad, f"{len(bad)} stale D2H reads, first at {bad[:5]}"
 
 
+def test_pread_gpu_visible_to_other_stream_kernel(S, tmp_path):
+    """a peer-style consumer — a kernel on ANOTHER stream
+    (created beforehand, as RCCL's would be), launched without any host sync
+    after each 4 KiB pread_gpu returns — sees the bytes, with the posted HDP
+    flush of the synchronous path (hdp_sync=2 default) and with hdp_sync=0."""
+    from nvme_strom_amd.ops import verify as V
+    from nvme_strom_amd.tensor import HbmBuffer
+    n = 500
+    p, data = _mkfile(tmp_path, 8 << 20, seed=41)
+    fd = os.open(p, os.O_RDONLY)
+    offs = np.random.default_rng(5).choice((8 << 20) // 4096, n, replace=False) * 4096
+    side = torch.cuda.Stream()
+    ref = [S.crc32c_host(data[o:o + 4096].tobytes()) for o in offs.tolist()]
+    for mode in (2, 0):
+        S.configure(hdp_sync=mode, bar_map=1)
+        crcs = []
+        with HbmBuffer(n * 4096, "cuda") as hb:
+            for i, off in enumerate(offs.tolist()):
+                assert S.pread_gpu(hb.handle, i * 4096, fd, off, 4096) == 4096
+                with torch.cuda.stream(side):
+                    crcs.append(V.crc32c_chunks(hb.tensor[i * 4096:(i + 1) * 4096], 4096))
+            side.synchronize()
+            got = [int(V.u32(c)[0]) for c in crcs]
+        bad = [i for i in range(n) if got[i] != ref[i]]
+        assert not bad, f"hdp_sync={mode}: {len(bad)} stale reads, first at {bad[:5]}"
+    os.close(fd)
+    S.configure(hdp_sync=2)
+
+
 def test_read_chunks_hybrid_reorder(S, tmp_path):
     """Page-cache chunks land at the tail via the write-back buffer; the
     reader scatters everything back into the requested order on the GPU."""
