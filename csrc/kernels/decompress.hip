@@ -888,8 +888,9 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // 256 / 512 a build.
   const char *pe = getenv("STROM_DECOMP_PAR");
   const int pv = pe ? atoi(pe) : -1;
-  const bool lz4 = codec != STROM_CODEC_SNAPPY && codec != STROM_CODEC_COPY;
-  if (lz4 && (pe ? pv != 0 : nblocks <= 8192)) {
+  // snappy takes the same block-parallel decoder (its element grammar, round 4)
+  const bool par_codec = codec != STROM_CODEC_COPY;
+  if (par_codec && (pe ? pv != 0 : nblocks <= 8192)) {
     if (pv == 512 || (pv != 256 && nblocks <= 3 * device_cus()))
       return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);

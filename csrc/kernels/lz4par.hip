@@ -33,6 +33,13 @@
 // runs them with barriers between, strom_lz4par_host() runs the SAME
 // functions thread by thread on the CPU (tests/test_codecs_cpu.py pins it
 // against the host LZ4 codec and pyarrow's frames).
+//
+// Snappy (raw format: varint length preamble, then elements) takes the same
+// path with its own element grammar (template SN): an element is a literal
+// run (tag 00, lengths in the tag or 1-4 bytes after it) or a copy (tags
+// 01 / 10 / 11: 1-, 2- or 4-byte offsets) — a sequence with either no
+// match or no literals — so speculation, validation, counting, the pointer
+// fill and doubling are shared; the preamble's length is checked at the end.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -86,6 +93,10 @@ static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 // ~100 bytes to fall onto the true token grid on int columns, and a slice
 // whose chain has not merged by its true entry costs a serial fix-up round
 constexpr uint32_t LB = LZ4PAR_LOOKBACK;
+#ifndef LZ4PAR_RESTART
+#define LZ4PAR_RESTART 1
+#endif
+constexpr bool RESTART = LZ4PAR_RESTART;   // restart a speculative chain at a failed parse
 constexpr uint32_t kLit = 0x80000000u;   // pointer tag: literal, input position
 constexpr uint32_t kHist = 0x40000000u;  // pointer tag: stored output position
 constexpr uint32_t kTag = kLit | kHist;
@@ -124,6 +135,9 @@ struct Smem {
   uint32_t mode;
   uint32_t bcs;          // 4-byte checksum after each block
   uint32_t raw_block;    // codec LZ4: the whole input is one block
+  uint32_t expect;       // snappy: the preamble's decoded length (else ~0)
+  uint32_t minfix;       // snappy: first slice not yet settled
+  uint32_t cov;          // snappy: last slice settled by the current round
 };
 
 struct Ctx {
@@ -136,8 +150,19 @@ struct Ctx {
 // ---------------------------------------------------------------- input
 HD uint8_t inb(const Smem &s, const Ctx &c, uint32_t p) {
   const uint32_t r = p - s.ws;
+#ifdef __HIP_DEVICE_COMPILE__
+  // explicit address spaces: left generic, the two loads were merged into
+  // one flat load of a selected pointer on the parse paths (round 4: 54
+  // flat_load_ubyte in the LZ4 kernel, ~10 % slower than round 3's
+  // ds_read / global_load split)
+  typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+  typedef __attribute__((address_space(1))) const uint8_t glb_u8;
+  if (r < s.wload) return ((lds_u8 *)s.win)[WI(r)];
+  return p < c.len ? ((glb_u8 *)c.in)[p] : 0;
+#else
   if (r < s.wload) return s.win[WI(r)];
   return p < c.len ? c.in[p] : 0;
+#endif
 }
 
 HD uint32_t rd32(const Ctx &c, uint32_t p) {
@@ -151,9 +176,55 @@ struct Seq {
   bool last;
 };
 
+// One snappy element at p: a literal run (off = mlen = 0) or a copy (lit =
+// 0).  false: malformed.
+HD bool parse_snappy(const Smem &s, const Ctx &c, uint32_t p, uint32_t bend, Seq &q) {
+  const uint32_t tag = inb(s, c, p);
+  uint32_t x = p + 1;
+  const uint32_t kind = tag & 3;
+  if (kind == 0) {
+    uint32_t n = tag >> 2;
+    if (n >= 60) {                       // 1-4 length bytes follow
+      const uint32_t nb = n - 59;
+      const uint32_t v = (uint32_t)inb(s, c, x) | ((uint32_t)inb(s, c, x + 1) << 8) |
+                         ((uint32_t)inb(s, c, x + 2) << 16) | ((uint32_t)inb(s, c, x + 3) << 24);
+      n = nb == 4 ? v : v & ((1u << (8 * nb)) - 1u);
+      x += nb;
+    }
+    const uint64_t le = (uint64_t)x + n + 1;
+    q.lit0 = x;
+    q.lit = n + 1;
+    q.off = q.mlen = 0;
+    q.last = le >= bend;
+    q.next = le < bend ? (uint32_t)le : bend;
+    return le <= bend && n < kPosMax;
+  }
+  q.lit0 = x;
+  q.lit = 0;
+  if (kind == 1) {
+    q.mlen = 4 + ((tag >> 2) & 7);
+    q.off = ((tag >> 5) << 8) | inb(s, c, x);
+    x += 1;
+  } else if (kind == 2) {
+    q.mlen = (tag >> 2) + 1;
+    q.off = (uint32_t)inb(s, c, x) | ((uint32_t)inb(s, c, x + 1) << 8);
+    x += 2;
+  } else {
+    q.mlen = (tag >> 2) + 1;
+    q.off = (uint32_t)inb(s, c, x) | ((uint32_t)inb(s, c, x + 1) << 8) |
+            ((uint32_t)inb(s, c, x + 2) << 16) | ((uint32_t)inb(s, c, x + 3) << 24);
+    x += 4;
+  }
+  q.last = x >= bend;
+  q.next = x < bend ? x : bend;
+  return x <= bend && q.off != 0;
+}
+
 // One LZ4 sequence at p (block ends at bend).  false: malformed (for a
 // speculative chain that just means "wrong start").
+template <bool SN>
 HD bool parse(const Smem &s, const Ctx &c, uint32_t p, uint32_t bend, Seq &q) {
+  if (SN) return parse_snappy(s, c, p, bend, q);
   const uint32_t tok = inb(s, c, p);
   uint32_t x = p + 1;
   uint32_t lit = tok >> 4;
@@ -234,6 +305,7 @@ HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
 }
 
 // (1) speculative chain of slice t
+template <bool SN>
 HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
@@ -245,7 +317,19 @@ HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
   Seq q;
   while (p < hi) {
     if (p >= lo) setbit(s, p);
-    parse(s, c, p, s.bend, q);
+    // a token no valid stream can hold (a length running past the block, a
+    // zero offset) proves the chain wrong: restart it at the next byte
+    // instead of letting it die.  The true chain never fails a parse, so
+    // from any marked token it reaches, the chain continues as the true one.
+    // Snappy only: a garbage literal tag of kind 60-63 carries a 1-4 byte
+    // length — one tag in 64 of random bytes — and killed most chains
+    // (round 4, val columns 182 validation rounds per window, 12 after);
+    // LZ4 chains merge anyway and the restarts only cost there
+    // (profiles/r4/dec/lz4_variant_ab.json).
+    if (!parse<SN>(s, c, p, s.bend, q) && SN && RESTART) {
+      ++p;
+      continue;
+    }
     p = q.next;
   }
   s.ex[t] = p;
@@ -255,6 +339,7 @@ HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
 HD uint32_t ph_entry(const Smem &s, uint32_t t) { return t == 0 ? s.ws : s.ex[t - 1]; }
 
 // (2) validation round, fix half: true when slice t had to re-parse
+template <bool SN>
 HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   if (lo >= hi) return false;
@@ -273,14 +358,68 @@ HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   Seq q;
   while (p < hi) {
     setbit(s, p);
-    parse(s, c, p, s.bend, q);
+    parse<SN>(s, c, p, s.bend, q);
     p = q.next;
   }
   s.ex[t] = p;
   return true;
 }
 
+// (2') snappy validation: a SETTLED prefix instead of rounds in which every
+// slice re-parses from its predecessor's current exit.  Snappy chains from
+// wrong starts merge within ~100 bytes, but one that reads a garbage
+// literal tag with a 1-4 byte length jumps kilobytes ahead; in the round
+// scheme that wrong exit travelled forward one slice per round ahead of the
+// correction (round 4: 220 rounds in one 16 KiB window of val data).  Here:
+//   link(t)   slice t accepts its predecessor's speculative exit (a token
+//             its own chain marked): then its speculative exit is right
+//             whenever its predecessor's is;
+//   a round   settles the FIRST slice S without a link (its entry, the
+//             settled exit of S-1, is final): parse from it (or pass it
+//             through when it lies past the slice), then every later slice
+//             wholly before the new exit sits inside one element and takes
+//             it too (a long literal of incompressible bytes spans hundreds
+//             of slices); the next slice re-checks its link against it;
+//   meanwhile every other broken slice re-walks from its predecessor's
+//   current exit (the round-4 A/B: sorted-id columns break often and
+//   resolve in parallel this way), unless that exit lies past the slice —
+//   a far jump is never passed on before it is settled.
+// Rounds <= breaks in the chain of links, not slices.
+HD bool sn_link(const Smem &s, uint32_t t, uint32_t ent) {
+  const uint32_t hi = slice_hi(s, t);
+  return ent < hi && getbit(s, ent);
+}
+
+// slice t's chain from `ent`: its marks and exit replace the old ones (a
+// slice's marks and exit always belong to one chain, so a link check stays
+// sound whatever entry the chain came from)
+HD void sn_walk(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  uint32_t p = ent;
+  if (lo < hi && ent < hi) {
+    for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
+    Seq q;
+    while (p < hi) {
+      setbit(s, p);
+      parse<true>(s, c, p, s.bend, q);
+      p = q.next;
+    }
+  }
+  s.ex[t] = p;
+}
+
+// settle slice t from its final entry; returns the last slice it covers
+HD uint32_t sn_settle(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
+  sn_walk(s, c, t, ent);
+  const uint32_t p = s.ex[t];
+  const uint32_t n = (s.wend - s.ws + SL - 1) / SL;
+  uint32_t j = t + 1;
+  for (; j < n && slice_hi(s, j) <= p; ++j) s.ex[j] = p;
+  return j - 1;
+}
+
 // (3) output bytes of slice t's true sequences (errors set s.err)
+template <bool SN>
 HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   uint32_t o = 0;
@@ -288,7 +427,7 @@ HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
     uint32_t p = s.en[t];
     Seq q;
     while (p < hi) {
-      if (!parse(s, c, p, s.bend, q)) {
+      if (!parse<SN>(s, c, p, s.bend, q)) {
         s.err = kErrFormat;
         break;
       }
@@ -341,6 +480,7 @@ HD void ph_fill_init(const Smem &s, uint32_t t, FillPos &f) {
   f.o = t ? s.ost[t - 1] : 0;
 }
 
+template <bool SN>
 HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, FillPos &f) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   if (lo >= hi) return;
@@ -351,14 +491,14 @@ HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, FillPos &f) {
   uint32_t p = f.p, o = f.o;
   Seq q;
   while (p < hi && o < b1) {
-    parse(s, c, p, s.bend, q);           // checked by ph_count
+    parse<SN>(s, c, p, s.bend, q);       // checked by ph_count
     const uint32_t le = o + q.lit;
     if (le > b0 && q.lit) {
       const uint32_t x0 = o > b0 ? o : b0;
       head(s, x0 - b0, kLit | (q.lit0 + (x0 - o)));
     }
     o = le;
-    if (!q.last) {
+    if (SN ? q.mlen != 0 : !q.last) {
       const uint32_t me = o + q.mlen;
       if (me > b0 && o < b1) {
         if ((uint64_t)q.off > (uint64_t)opw + o) {
@@ -541,12 +681,35 @@ HD void st_header(Smem &s, const Ctx &c, int codec) {
   s.mode = kModeBlock;
   s.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
   s.raw_block = codec == STROM_CODEC_LZ4;
+  s.expect = 0xffffffffu;
   s.ip = 0;
   s.ws = 0;
   s.wload = 0;
   if (c.len >= kPosMax || c.cap >= kPosMax) {
     s.err = kErrOverflow;
     s.mode = kModeDone;
+    return;
+  }
+  if (codec == STROM_CODEC_SNAPPY) {     // varint preamble: the decoded length
+    uint32_t ul = 0, sh = 0, p = 0, b;
+    do {
+      if (p >= c.len || sh > 28) {
+        s.err = kErrFormat;
+        s.mode = kModeDone;
+        return;
+      }
+      b = c.in[p++];
+      ul |= (b & 0x7fu) << sh;
+      sh += 7;
+    } while (b & 0x80);
+    if (ul > c.cap || ul >= kPosMax) {
+      s.err = kErrOverflow;
+      s.mode = kModeDone;
+      return;
+    }
+    s.expect = ul;
+    s.ip = p;
+    s.raw_block = 4;                     // one element stream to the input end
     return;
   }
   if (codec != STROM_CODEC_ARROW_LZ4) return;
@@ -585,6 +748,14 @@ HD void st_header(Smem &s, const Ctx &c, int codec) {
 
 // next block: sets bstart/bend/braw, or mode done
 HD void st_block(Smem &s, const Ctx &c) {
+  if (s.raw_block == 4) {                         // snappy: the elements after the preamble
+    s.raw_block = 3;
+    s.bstart = s.ip;
+    s.bend = c.len;
+    s.braw = 0;
+    if (s.bstart >= s.bend) s.mode = kModeDone;   // empty input
+    return;
+  }
   if (s.raw_block == 1) {                         // codec LZ4: one raw block
     s.raw_block = 3;
     s.bstart = 0;
@@ -663,16 +834,26 @@ __device__ unsigned long long g_lz4par_prof[kLpN];
 namespace {
 using namespace LZ4P_NS;
 
+// Occupancy hints per grammar: the 512-thread build holds its LZ4 kernel at
+// 80 VGPRs (6 waves per SIMD, 3 workgroups per CU — what round 3 measured
+// 85 -> 115 GB/s with) without spilling; the snappy instantiation keeps the
+// compiler's choice (it would spill there).
 #ifdef LZ4PAR_WPE
 #define LZ4PAR_OCC __attribute__((amdgpu_waves_per_eu(LZ4PAR_WPE)))
 #else
 #define LZ4PAR_OCC
 #endif
-__global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel(int codec, const uint8_t *__restrict__ src,
-                                                    uint8_t *__restrict__ dst,
-                                                    const strom_decomp_desc *__restrict__ desc,
-                                                    uint32_t nstreams, int32_t *status) {
-  __shared__ __attribute__((aligned(16))) Smem s;
+#ifdef LZ4PAR_WPE_LZ4
+#define LZ4PAR_OCC_LZ4 __attribute__((amdgpu_waves_per_eu(LZ4PAR_WPE_LZ4)))
+#else
+#define LZ4PAR_OCC_LZ4 LZ4PAR_OCC
+#endif
+
+template <bool SN>
+__device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *__restrict__ src,
+                                            uint8_t *__restrict__ dst,
+                                            const strom_decomp_desc *__restrict__ desc,
+                                            uint32_t nstreams, int32_t *status) {
   const uint32_t t = threadIdx.x;
   LP_INIT();
   for (uint32_t b = blockIdx.x; b < nstreams; b += gridDim.x) {
@@ -708,18 +889,48 @@ __global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel(int codec, const 
         ph_load(s, c, t);
         __syncthreads();
         LP_MARK(kLpLoad);
-        ph_spec(s, c, t);
+        ph_spec<SN>(s, c, t);
         __syncthreads();
         LP_MARK(kLpSpec);
-        bool changed;
-        do {
-          LP_CNT(kLpNRound);
-          const uint32_t ent = ph_entry(s, t);
+        if (SN) {
+          const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+          if (t == 0) s.minfix = nsl;
           __syncthreads();
-          changed = ph_fix(s, c, t, ent);
-        } while (__syncthreads_or(changed));
+          bool link = t == 0 || t >= nsl || sn_link(s, t, s.ex[t - 1]);
+          if (!link) atomicMin(&s.minfix, t);
+          __syncthreads();
+          for (;;) {
+            const uint32_t S = s.minfix;
+            if (S >= nsl) break;
+            LP_CNT(kLpNRound);
+            // entries of the other broken slices, read before anything moves
+            const uint32_t e = t > S && !link ? s.ex[t - 1] : 0;
+            __syncthreads();               // everyone has read minfix and e
+            if (t == 0) s.minfix = nsl;
+            if (t == S) s.cov = sn_settle(s, c, t, s.ex[t - 1]);
+            __syncthreads();
+            const uint32_t cov = s.cov;
+            if (t > cov + 1 && !link && e < slice_hi(s, t)) sn_walk(s, c, t, e);
+            __syncthreads();
+            if (t > cov) {
+              link = t >= nsl || sn_link(s, t, s.ex[t - 1]);
+              if (!link) atomicMin(&s.minfix, t);
+            }
+            __syncthreads();
+          }
+          s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
+          __syncthreads();
+        } else {
+          bool changed;
+          do {
+            LP_CNT(kLpNRound);
+            const uint32_t ent = ph_entry(s, t);
+            __syncthreads();
+            changed = ph_fix<SN>(s, c, t, ent);
+          } while (__syncthreads_or(changed));
+        }
         LP_MARK(kLpValid);
-        ph_count(s, c, t);
+        ph_count<SN>(s, c, t);
         for (uint32_t dd = 1; dd < NT; dd <<= 1) {
           __syncthreads();
           const uint32_t v = ph_scan_read(s, t, dd);
@@ -740,7 +951,7 @@ __global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel(int codec, const 
         for (uint32_t b0 = 0; b0 < total; b0 += OB) {
           LP_CNT(kLpNBatch);
           const uint32_t nb = total - b0 < OB ? total - b0 : OB;
-          ph_fill(s, c, t, b0, fpos);
+          ph_fill<SN>(s, c, t, b0, fpos);
           __syncthreads();
           LP_MARK(kLpFill);
           if (s.err) break;
@@ -772,10 +983,28 @@ __global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel(int codec, const 
       __syncthreads();
       if (s.err) break;
     }
+    if (SN) {
+      if (t == 0 && !s.err && s.op != s.expect) s.err = kErrFormat;
+      __syncthreads();
+    }
     if (t == 0) status[b] = s.err ? s.err : (int32_t)s.op;
     __syncthreads();
   }
   LP_FLUSH();
+}
+
+__global__ __launch_bounds__(NT) LZ4PAR_OCC_LZ4 void lz4par_kernel_lz4(
+    int codec, const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+    const strom_decomp_desc *__restrict__ desc, uint32_t nstreams, int32_t *status) {
+  __shared__ __attribute__((aligned(16))) Smem s;
+  lz4par_body<false>(s, codec, src, dst, desc, nstreams, status);
+}
+
+__global__ __launch_bounds__(NT) LZ4PAR_OCC void lz4par_kernel_snappy(
+    int codec, const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+    const strom_decomp_desc *__restrict__ desc, uint32_t nstreams, int32_t *status) {
+  __shared__ __attribute__((aligned(16))) Smem s;
+  lz4par_body<true>(s, codec, src, dst, desc, nstreams, status);
 }
 
 }  // namespace
@@ -786,12 +1015,17 @@ extern "C" int LZ4PAR_ENTRY(int codec, const void *d_src, void *d_dst,
                             const strom_decomp_desc *d_desc, uint32_t nstreams,
                             int32_t *d_status, void *stream) {
   if (codec != STROM_CODEC_LZ4 && codec != STROM_CODEC_LZ4_FRAME &&
-      codec != STROM_CODEC_LZ4_FRAME_BCS && codec != STROM_CODEC_ARROW_LZ4)
+      codec != STROM_CODEC_LZ4_FRAME_BCS && codec != STROM_CODEC_ARROW_LZ4 &&
+      codec != STROM_CODEC_SNAPPY)
     return -22;
   if (!nstreams) return 0;
   const uint32_t grid = nstreams < 65535 ? nstreams : 65535;
-  hipLaunchKernelGGL(lz4par_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
-                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status);
+  if (codec == STROM_CODEC_SNAPPY)
+    hipLaunchKernelGGL(lz4par_kernel_snappy, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status);
+  else
+    hipLaunchKernelGGL(lz4par_kernel_lz4, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -812,8 +1046,10 @@ extern "C" int strom_lz4par_prof(uint64_t *out) {
 // The same phases run thread by thread on the CPU: the algorithm's
 // reference (tests/test_codecs_cpu.py), no GPU involved.  Returns decoded
 // bytes or a negative error as the kernel's status.
-extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
-                                 uint32_t cap, uint32_t *stats) {
+namespace {
+template <bool SN>
+int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, uint32_t cap,
+                uint32_t *stats) {
   using namespace LZ4P_NS;
   static_assert(NT != 256 || PW != 16384 || OB != 4096 || HR != 0 || sizeof(Smem) <= 40 * 1024,
                 "default geometry: four workgroups per CU (160 KiB LDS)");
@@ -843,19 +1079,42 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
       ++windows;
       st_window(s, c, ws);
       for (uint32_t t = 0; t < NT; ++t) ph_load(s, c, t);
-      for (uint32_t t = 0; t < NT; ++t) ph_spec(s, c, t);
+      for (uint32_t t = 0; t < NT; ++t) ph_spec<SN>(s, c, t);
       bool any;
-      do {
-        ++rounds;
-        for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_entry(s, t);
-        any = false;
-        for (uint32_t t = 0; t < NT; ++t) {
-          flag[t] = ph_fix(s, c, t, ent[t]);
-          any |= flag[t];
-          fixes += flag[t];
+      if (SN) {
+        const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+        for (uint32_t t = 0; t < NT; ++t)
+          flag[t] = t == 0 || t >= nsl || sn_link(s, t, s.ex[t - 1]);   // link
+        for (;;) {
+          uint32_t S = 1;
+          while (S < nsl && flag[S]) ++S;
+          if (S >= nsl) break;
+          ++rounds;
+          for (uint32_t t = 0; t < NT; ++t) ent[t] = t > S && !flag[t] ? s.ex[t - 1] : 0;
+          const uint32_t cov = sn_settle(s, c, S, s.ex[S - 1]);
+          ++fixes;
+          for (uint32_t t = cov + 2; t < nsl; ++t)
+            if (!flag[t] && ent[t] < slice_hi(s, t)) {
+              sn_walk(s, c, t, ent[t]);
+              ++fixes;
+            }
+          for (uint32_t t = cov + 1; t < NT; ++t) flag[t] = t >= nsl || sn_link(s, t, s.ex[t - 1]);
+          for (uint32_t t = S; t <= cov; ++t) flag[t] = true;
         }
-      } while (any);
-      for (uint32_t t = 0; t < NT; ++t) ph_count(s, c, t);
+        for (uint32_t t = 0; t < NT; ++t) s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
+      } else {
+        do {
+          ++rounds;
+          for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_entry(s, t);
+          any = false;
+          for (uint32_t t = 0; t < NT; ++t) {
+            flag[t] = ph_fix<SN>(s, c, t, ent[t]);
+            any |= flag[t];
+            fixes += flag[t];
+          }
+        } while (any);
+      }
+      for (uint32_t t = 0; t < NT; ++t) ph_count<SN>(s, c, t);
       for (uint32_t dd = 1; dd < NT; dd <<= 1) {
         for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_scan_read(s, t, dd);
         for (uint32_t t = 0; t < NT; ++t) ph_scan_write(s, t, ent[t]);
@@ -866,7 +1125,7 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
       for (uint32_t t = 0; t < NT; ++t) ph_fill_init(s, t, fpos[t]);
       for (uint32_t b0 = 0; b0 < s.total; b0 += OB) {
         const uint32_t nb = s.total - b0 < OB ? s.total - b0 : OB;
-        for (uint32_t t = 0; t < NT; ++t) ph_fill(s, c, t, b0, fpos[t]);
+        for (uint32_t t = 0; t < NT; ++t) ph_fill<SN>(s, c, t, b0, fpos[t]);
         if (s.err) break;
         for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
         do {
@@ -889,10 +1148,18 @@ extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len
     stats[2] = fixes;
     stats[3] = dbl;
   }
+  if (!s.err && s.expect != 0xffffffffu && s.op != s.expect) s.err = kErrFormat;
   const int r = s.err ? s.err : (int)s.op;
   delete sp;
   delete[] held;
   delete[] fpos;
   return r;
+}
+}  // namespace
+
+extern "C" int strom_lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
+                                 uint32_t cap, uint32_t *stats) {
+  return codec == STROM_CODEC_SNAPPY ? lz4par_host<true>(codec, src, src_len, dst, cap, stats)
+                                     : lz4par_host<false>(codec, src, src_len, dst, cap, stats);
 }
 #endif  // LZ4PAR_NO_HOST

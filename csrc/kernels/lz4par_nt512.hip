@@ -12,4 +12,5 @@
 #define LZ4PAR_ENTRY strom_decompress_par512
 #define LZ4PAR_NO_HOST 1
 #define LZ4PAR_LOADU 8
+#define LZ4PAR_WPE_LZ4 6
 #include "lz4par.hip"

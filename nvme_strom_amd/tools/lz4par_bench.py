@@ -24,7 +24,7 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def frames(kind: str, k: int, seed: int = 1):
+def frames(kind: str, k: int, seed: int = 1, codec: str = "lz4"):
     import pyarrow as pa
     from nvme_strom_amd.ops import decompress as D
     rng = np.random.default_rng(seed)
@@ -38,7 +38,10 @@ def frames(kind: str, k: int, seed: int = 1):
         else:
             d = b" ".join(words[j] for j in rng.integers(0, len(words), 110000))[:512 << 10]
         raws.append(d)
-        bufs.append(D.arrow_lz4_buffer(d, pa.compress(d, codec="lz4", asbytes=True)))
+        if codec == "snappy":       # raw snappy, as Parquet pages carry it
+            bufs.append(pa.compress(d, codec="snappy", asbytes=True))
+        else:
+            bufs.append(D.arrow_lz4_buffer(d, pa.compress(d, codec="lz4", asbytes=True)))
     return raws, bufs
 
 
@@ -47,7 +50,7 @@ PHASES = ("hdr", "load", "spec", "validate", "count_scan", "fill", "double", "re
 COUNTS = ("windows", "valid_rounds", "batches", "double_rounds")
 
 
-def prof(n, src, dst, d_desc, status) -> dict:
+def prof(n, src, dst, d_desc, status, codec=None) -> dict:
     """One launch of the profiled build: share of thread-0 cycles per phase
     and events per stream."""
     import ctypes as C
@@ -58,7 +61,7 @@ def prof(n, src, dst, d_desc, status) -> dict:
                               "libstrom_decprof.so"))
     out = np.zeros(len(PHASES) + len(COUNTS), dtype=np.uint64)
     lib.strom_lz4par_prof(out.ctypes.data_as(C.c_void_p))           # zero
-    rc = lib.strom_decompress_par(D.ARROW_LZ4, C.c_void_p(ptr(src)), C.c_void_p(ptr(dst)),
+    rc = lib.strom_decompress_par(codec or D.ARROW_LZ4, C.c_void_p(ptr(src)), C.c_void_p(ptr(dst)),
                                   C.c_void_p(ptr(d_desc)), C.c_uint32(n), C.c_void_p(ptr(status)),
                                   None)
     assert rc == 0
@@ -82,6 +85,8 @@ def main(argv=None) -> int:
     ap.add_argument("--variants", default="",
                     help="comma list of lib/lz4v/<name>.so geometry builds (make lz4v) to time too")
     ap.add_argument("--no-lanes", dest="lanes", action="store_false")
+    ap.add_argument("--codec", default="lz4", choices=("lz4", "snappy"),
+                    help="lz4: Arrow IPC LZ4 frames; snappy: raw snappy buffers (pyarrow)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -105,7 +110,8 @@ def main(argv=None) -> int:
                       C.c_void_p]
         decoders.append((v, f))
     for kind in a.kinds.split(","):
-        raws, bufs = frames(kind, a.distinct)
+        raws, bufs = frames(kind, a.distinct, codec=a.codec)
+        cid = D.SNAPPY if a.codec == "snappy" else D.ARROW_LZ4
         rawlen = len(raws[0])
         src_off = np.cumsum([0] + [len(b) for b in bufs[:-1]])
         src = torch.from_numpy(np.frombuffer(b"".join(bufs), dtype=np.uint8).copy()).to(dev)
@@ -119,7 +125,7 @@ def main(argv=None) -> int:
             d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
             dst = torch.empty(n * cap, dtype=torch.uint8, device=dev)
             status = torch.empty(n, dtype=torch.int32, device=dev)
-            row = dict(kind=kind, streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
+            row = dict(kind=kind, codec=a.codec, streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
             for name, f in decoders:
                 fn = name
                 times = []
@@ -129,7 +135,7 @@ def main(argv=None) -> int:
                     status.fill_(-99)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    check(f(D.ARROW_LZ4, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status), None), fn)
+                    check(f(cid, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status), None), fn)
                     e1.record()
                     torch.cuda.synchronize()
                     if it:
@@ -146,7 +152,7 @@ def main(argv=None) -> int:
             if a.lanes:
                 row["speedup"] = round(row["par_GBps"] / row["lanes_GBps"], 2)
             if a.prof:
-                row["par_phases"] = prof(n, src, dst, d_desc, status)
+                row["par_phases"] = prof(n, src, dst, d_desc, status, cid)
             _log(json.dumps(row))
             res["rows"].append(row)
             del dst

@@ -160,6 +160,39 @@ def test_lz4par_arrow_frames_from_pyarrow(kind, threads):
     assert st == 5000 and out == d[:5000]
 
 
+@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("kind", ["uniform", "sorted", "floats", "text", "random", "zeros", "runs"])
+def test_snappy_block_parallel_from_pyarrow(kind, threads):
+    """Raw snappy buffers from pyarrow (and our host compressor) decode
+    through the block-parallel phases with snappy's element grammar
+    (lz4par.hip SN=true), with the preamble length checked."""
+    pa = pytest.importorskip("pyarrow")
+    d = (_ints(kind, 512 << 10, 13) if kind in ("uniform", "sorted", "floats")
+         else _data(kind, 512 << 10, 13))
+    for c in (pa.compress(d, codec="snappy", asbytes=True), D.snappy_compress(d)):
+        st, out, stats = D.lz4par_host(D.SNAPPY, c, len(d), threads)
+        assert st == len(d) and out == d, (st, stats)
+    for n in (0, 1, 2, 63, 64, 65, 70000):
+        c = pa.compress(d[:n], codec="snappy", asbytes=True)
+        st, out, _ = D.lz4par_host(D.SNAPPY, c, max(n, 1), threads)
+        assert st == n and out[:n] == d[:n]
+
+
+def test_snappy_block_parallel_errors():
+    pa = pytest.importorskip("pyarrow")
+    d = _data("text", 100000, 5)
+    c = pa.compress(d, codec="snappy", asbytes=True)
+    assert D.lz4par_host(D.SNAPPY, c, len(d) - 1)[0] == -2      # preamble > capacity
+    assert D.lz4par_host(D.SNAPPY, c[: len(c) // 2], len(d))[0] < 0
+    # a stream that decodes to fewer bytes than its preamble claims
+    short = bytes([0x90, 0x03]) + c[3:]
+    assert D.lz4par_host(D.SNAPPY, short, 1 << 20)[0] < 0
+    rng = np.random.default_rng(9)
+    for _ in range(30):
+        g = rng.integers(0, 256, int(rng.integers(1, 5000)), dtype=np.uint8).tobytes()
+        assert D.lz4par_host(D.SNAPPY, g, 1 << 16)[0] <= 1 << 16
+
+
 def test_lz4par_frames_and_errors():
     d = _data("text", 200000, 5)
     f = D.lz4_frame_compress(d, 64 << 10)
