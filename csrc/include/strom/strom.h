@@ -377,6 +377,58 @@ int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwords,
                               const struct strom_filter_batch *d_proj, uint32_t width,
                               void *d_pout, uint8_t *d_pvalid, void *stream);
 
+/* General column qualifiers (Arrow scans; nvme_strom_amd/ops/colpred.py
+ * compiles the predicates).  Storage types beyond STROM_COL_I32..F64: */
+#define STROM_COL_I8 5
+#define STROM_COL_I16 6
+#define STROM_COL_U8 7
+#define STROM_COL_U16 8
+#define STROM_COL_U32 9
+#define STROM_COL_U64 10
+#define STROM_COL_BOOL 11   /* bit-packed values */
+#define STROM_COL_STR32 12  /* utf8/binary: int32 offsets in values, bytes in aux */
+#define STROM_COL_STR64 13  /* large utf8/binary: int64 offsets */
+/* operators */
+#define STROM_QOP_RANGES 1     /* v in one of nconst inclusive ranges: sorted, disjoint
+                                  (lo, hi) pairs of int64 (U64: uint64; floats: double) */
+#define STROM_QOP_STR_IN 2     /* the string equals one of nconst constants */
+#define STROM_QOP_STR_PREFIX 3 /* starts with one of nconst constants */
+#define STROM_QOP_LUT 4        /* index v < nconst with bit v of the uint32 LUT words set
+                                  (dictionary-encoded columns) */
+#define STROM_QOP_VALID 5      /* the row is not null (NEGATE: is null) */
+#define STROM_QOP_STR_RANGES 6 /* bytewise-lexicographic ranges: per range two bounds of
+                                  (start, len, mode) in offs, mode 0 unbounded,
+                                  1 inclusive, 2 exclusive */
+#define STROM_QUAL_NEGATE 1    /* NOT of the comparison (still false for nulls) */
+#define STROM_QUAL_NAN 2       /* floats: NaN also matches (IN-lists holding NaN) */
+struct strom_col_qual {
+	int32_t type;
+	int32_t op;
+	uint32_t flags;
+	uint32_t nconst;
+	uint64_t consts;       /* device: ranges / string blob / LUT words */
+	uint64_t offs;         /* device: strings, (start, len) uint32 pairs; starts 4-aligned */
+	uint64_t const_bytes;  /* bytes at consts (staged in LDS, <= 64 KiB) */
+	uint64_t offs_bytes;
+};
+/* strom_filter_batch + aux (the character data of a string column, aux_len
+ * bytes: offsets outside it never match and are never followed) */
+struct strom_qual_batch {
+	uint64_t values;
+	uint64_t valid;
+	uint64_t nrows;
+	uint64_t word_base;
+	uint64_t row_base;
+	uint64_t aux;
+	uint64_t aux_len;
+};
+/* bitmap[w] = (pred_bits | (d_or ? d_or[w] : 0)) & (and_dst ? bitmap[w] : ~0);
+ * *d_count += popcount of the words written.  A CNF qualifier list is a
+ * sequence of these launches (OR within a clause, AND across clauses). */
+int strom_column_qual(const struct strom_col_qual *q, const struct strom_qual_batch *d_batches,
+                      uint32_t nbatches, uint64_t nwords, uint64_t *d_bitmap,
+                      const uint64_t *d_or, int and_dst, uint64_t *d_count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -275,7 +275,9 @@ __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restri
     if (W) {
       const uint64_t r = local0 + bit;
       if (W == 8) ((uint64_t *)pout)[pos] = ((const uint64_t *)pv)[r];
-      else ((uint32_t *)pout)[pos] = ((const uint32_t *)pv)[r];
+      else if (W == 4) ((uint32_t *)pout)[pos] = ((const uint32_t *)pv)[r];
+      else if (W == 2) ((uint16_t *)pout)[pos] = ((const uint16_t *)pv)[r];
+      else ((uint8_t *)pout)[pos] = pv[r];
       if (pvalid) pvalid[pos] = pval ? (pval[r >> 3] >> (r & 7)) & 1 : 1;
     }
     ++pos;
@@ -303,6 +305,260 @@ int launch_filter(const void *v, const uint8_t *valid, uint64_t n, double lo, do
   hipLaunchKernelGGL(filter_kernel<T>, dim3(grid), dim3(256), 0, st, (const T *)v,
                      (const uint64_t *)valid, n, (T)lo, (T)hi, bm, (unsigned long long *)cnt);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+
+// ------------------------------------------------------------ qualifiers
+// General predicates of an Arrow scan (strom_column_qual): one lane per row,
+// one wave per 64-row word, as filter_batched_kernel, with the predicate's
+// constants (ranges, string constants, a dictionary lookup table) staged
+// once per workgroup in LDS.  The written word is
+// (pred | or_src[w]) & (and_dst ? bitmap[w] : ~0): a CNF qualifier list is a
+// chain of launches, ORs inside a clause and ANDs across clauses, no
+// per-clause bitmaps beyond one scratch.
+enum QKind { QK_RANGE, QK_LUT, QK_STR, QK_VALID };
+
+template <typename T> struct CmpOf { typedef int64_t type; };
+template <> struct CmpOf<uint64_t> { typedef uint64_t type; };
+template <> struct CmpOf<float> { typedef double type; };
+template <> struct CmpOf<double> { typedef double type; };
+
+struct BitT {};   // STROM_COL_BOOL: one bit per row
+template <> struct CmpOf<BitT> { typedef int64_t type; };
+
+template <typename T>
+__device__ __forceinline__ typename CmpOf<T>::type qload(const strom_qual_batch &b, uint64_t i) {
+  return (typename CmpOf<T>::type)((const T *)b.values)[i];
+}
+template <>
+__device__ __forceinline__ int64_t qload<BitT>(const strom_qual_batch &b, uint64_t i) {
+  return (((const uint8_t *)b.values)[i >> 3] >> (i & 7)) & 1;
+}
+
+// sorted disjoint inclusive ranges in LDS: linear for a few, else a binary
+// search for the first range whose hi >= x (NaN: no range)
+template <typename CT>
+__device__ __forceinline__ bool in_ranges(CT x, const CT *r, uint32_t n) {
+  if (n <= 8) {
+    bool h = false;
+    for (uint32_t k = 0; k < n; ++k) h |= (x >= r[2 * k]) & (x <= r[2 * k + 1]);
+    return h;
+  }
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (r[2 * mid + 1] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < n && r[2 * lo] <= x;
+}
+
+template <typename CT> __device__ __forceinline__ bool is_nan(CT) { return false; }
+template <> __device__ __forceinline__ bool is_nan<double>(double x) { return x != x; }
+
+// len bytes at global p == the LDS constant c (4-aligned).  Whole dwords:
+// aligned loads funnel-shifted into place (v_alignbyte), never reading a
+// dword that holds no byte of the string, so no access past the buffer.
+__device__ __forceinline__ bool str_eq(const uint8_t *p, const uint32_t *c, uint32_t len) {
+  if (!len) return true;
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+  const uint32_t *last = (const uint32_t *)((a + len - 1) & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t cur = *w;
+  for (uint32_t j = 0; j < len; j += 4) {
+    const uint32_t *nx = w + 1 <= last ? w + 1 : last;
+    const uint32_t nxt = *nx;
+    const uint32_t v = __builtin_amdgcn_alignbyte(nxt, cur, sh);
+    const uint32_t rem = len - j;
+    const uint32_t m = rem >= 4 ? ~0u : (1u << (8 * rem)) - 1;
+    if ((v ^ c[j >> 2]) & m) return false;
+    cur = nxt;
+    ++w;
+  }
+  return true;
+}
+
+// bytewise-lexicographic compare of len bytes at global p with the LDS
+// constant c of clen bytes: <0, 0, >0 (dwords compared big-endian)
+__device__ __forceinline__ int str_cmp(const uint8_t *p, uint32_t len, const uint32_t *c,
+                                       uint32_t clen) {
+  const uint32_t n = len < clen ? len : clen;
+  if (n) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t *last = (const uint32_t *)((a + n - 1) & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t cur = *w;
+    for (uint32_t j = 0; j < n; j += 4) {
+      const uint32_t *nx = w + 1 <= last ? w + 1 : last;
+      const uint32_t nxt = *nx;
+      const uint32_t rem = n - j;
+      const uint32_t m = rem >= 4 ? ~0u : (1u << (8 * rem)) - 1;
+      const uint32_t v = __builtin_amdgcn_alignbyte(nxt, cur, sh) & m;
+      const uint32_t k = c[j >> 2] & m;
+      if (v != k) return __builtin_bswap32(v) < __builtin_bswap32(k) ? -1 : 1;
+      cur = nxt;
+      ++w;
+    }
+  }
+  return len < clen ? -1 : (len > clen ? 1 : 0);
+}
+
+// one bound of a string range: offs (start, len, mode); mode 0 unbounded
+__device__ __forceinline__ bool str_bound(const uint8_t *p, uint32_t len, const uint32_t *qs,
+                                          const uint32_t *b, bool upper) {
+  const uint32_t mode = b[2];
+  if (!mode) return true;
+  const int r = str_cmp(p, len, qs + b[0] / 4, b[1]);
+  if (upper) return mode == 1 ? r <= 0 : r < 0;
+  return mode == 1 ? r >= 0 : r > 0;
+}
+
+template <typename T, int K>
+__global__ __launch_bounds__(256) void qual_kernel(strom_col_qual q,
+                                                   const strom_qual_batch *__restrict__ bt,
+                                                   uint32_t nb, uint64_t nwords,
+                                                   uint64_t *__restrict__ bitmap,
+                                                   const uint64_t *__restrict__ or_src, int and_dst,
+                                                   unsigned long long *__restrict__ count) {
+  typedef typename CmpOf<T>::type CT;
+  extern __shared__ uint32_t qs[];
+  __shared__ uint32_t wave_cnt[4];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // constants -> LDS (consts, then the string (start, len) pairs)
+  const uint32_t cw = (uint32_t)(q.const_bytes / 4), ow = (uint32_t)(q.offs_bytes / 4);
+  if (K != QK_VALID) {
+    for (uint32_t k = threadIdx.x; k < cw; k += 256) qs[k] = ((const uint32_t *)q.consts)[k];
+    if (K == QK_STR)
+      for (uint32_t k = threadIdx.x; k < ow; k += 256) qs[cw + k] = ((const uint32_t *)q.offs)[k];
+  }
+  __syncthreads();
+  const bool neg = q.flags & STROM_QUAL_NEGATE;
+  const bool nan_hit = q.flags & STROM_QUAL_NAN;
+  uint32_t local = 0;
+  constexpr uint32_t U = K == QK_STR ? 1 : kU;
+  const uint64_t step = (uint64_t)gridDim.x * 4 * U;
+  for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + wid) * U; w0 < nwords; w0 += step) {
+    // pass 1: batch lookup + every lane's load of U words issued before the
+    // first compare (kU rows per lane in flight, as filter_batched_kernel)
+    bool hit[U];
+    uint32_t bi[U];
+    CT x[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t w = w0 + u;
+      hit[u] = false;
+      bi[u] = 0;
+      x[u] = 0;
+      if (w >= nwords) continue;
+      uint32_t lo = 0, hi = nb;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bt[mid].word_base <= w) lo = mid;
+        else hi = mid;
+      }
+      bi[u] = lo;
+      const strom_qual_batch &b = bt[lo];
+      const uint64_t i = (w - b.word_base) * 64 + lane;
+      if constexpr (K == QK_RANGE || K == QK_LUT)
+        if (i < b.nrows) x[u] = qload<T>(b, i);
+    }
+    // pass 2: the predicate
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t w = w0 + u;
+      if (w >= nwords) break;
+      const strom_qual_batch &b = bt[bi[u]];
+      const uint64_t i = (w - b.word_base) * 64 + lane;
+      if (i >= b.nrows || K == QK_VALID) continue;
+      if constexpr (K == QK_RANGE) {
+        hit[u] = in_ranges<CT>(x[u], (const CT *)qs, q.nconst) || (nan_hit && is_nan<CT>(x[u]));
+      } else if constexpr (K == QK_LUT) {
+        const int64_t v = (int64_t)x[u];
+        hit[u] = (uint64_t)v < q.nconst && ((qs[v >> 5] >> (v & 31)) & 1);
+      } else {   // QK_STR: T is the offset type
+        const int64_t s = (int64_t)((const T *)b.values)[i];
+        const int64_t e = (int64_t)((const T *)b.values)[i + 1];
+        // a malformed offset pair (file data) never matches and is never
+        // followed outside the character buffer
+        if (s < 0 || e < s || (uint64_t)e > b.aux_len) continue;
+        const uint32_t len = (uint32_t)(e - s);
+        const uint8_t *p = (const uint8_t *)b.aux + s;
+        const uint32_t *offs = qs + cw;
+        bool h = false;
+        if (q.op == STROM_QOP_STR_RANGES) {
+          for (uint32_t k = 0; k < q.nconst && !h; ++k)
+            h = str_bound(p, len, qs, offs + 6 * k, false) &&
+                str_bound(p, len, qs, offs + 6 * k + 3, true);
+        } else {
+          const bool prefix = q.op == STROM_QOP_STR_PREFIX;
+          for (uint32_t k = 0; k < q.nconst && !h; ++k) {
+            const uint32_t cl = offs[2 * k + 1];
+            if (prefix ? len >= cl : len == cl) h = str_eq(p, qs + offs[2 * k] / 4, cl);
+          }
+        }
+        hit[u] = h;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint64_t w = w0 + u;
+      if (w >= nwords) break;
+      const strom_qual_batch &b = bt[bi[u]];
+      const uint64_t k = w - b.word_base;
+      const uint64_t i = k * 64 + lane;
+      const uint64_t vword = b.valid ? ((const uint64_t *)b.valid)[k] : ~0ull;
+      uint64_t word;
+      if (K == QK_VALID) word = __ballot(i < b.nrows && (((vword >> lane) & 1) != neg));
+      else word = __ballot(i < b.nrows && (hit[u] != neg)) & vword;
+      if (or_src) word |= or_src[w];
+      if (and_dst) word &= bitmap[w];
+      if (lane == 0) bitmap[w] = word;
+      local += __popcll(word);
+    }
+  }
+  if (lane == 0) wave_cnt[wid] = local;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicAdd(count, (unsigned long long)(wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3]));
+}
+
+template <typename T, int K>
+int launch_qual(const strom_col_qual &q, const strom_qual_batch *bt, uint32_t nb, uint64_t nwords,
+                uint64_t *bm, const uint64_t *orv, int and_dst, uint64_t *cnt, hipStream_t st) {
+  const uint32_t U = K == QK_STR ? 1 : kU;
+  uint64_t g = (nwords + 4 * U - 1) / (4 * U);
+  uint32_t grid = (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
+  const size_t lds = K == QK_VALID ? 0 : (size_t)(q.const_bytes + (K == QK_STR ? q.offs_bytes : 0));
+  hipLaunchKernelGGL((qual_kernel<T, K>), dim3(grid), dim3(256), lds, st, q, bt, nb, nwords, bm, orv,
+                     and_dst, (unsigned long long *)cnt);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+template <int K>
+int qual_by_type(const strom_col_qual &q, const strom_qual_batch *bt, uint32_t nb, uint64_t nw,
+                 uint64_t *bm, const uint64_t *orv, int and_dst, uint64_t *cnt, hipStream_t st) {
+  switch (q.type) {
+    case STROM_COL_I8: return launch_qual<int8_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_I16: return launch_qual<int16_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_I32: return launch_qual<int32_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_I64: return launch_qual<int64_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_U8: return launch_qual<uint8_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_U16: return launch_qual<uint16_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_U32: return launch_qual<uint32_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    case STROM_COL_U64: return launch_qual<uint64_t, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+    default: break;
+  }
+  if constexpr (K == QK_RANGE) {
+    switch (q.type) {
+      case STROM_COL_F32: return launch_qual<float, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+      case STROM_COL_F64: return launch_qual<double, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+      case STROM_COL_BOOL: return launch_qual<BitT, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+      default: break;
+    }
+  }
+  return -22;
 }
 
 }  // namespace
@@ -373,7 +629,7 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
                                          void *d_pout, uint8_t *d_pvalid, void *stream) {
   if (!nwords || !nbatches) return 0;
   if (!d_bitmap || !d_batches || !d_out || !d_total) return -22;
-  if (d_proj && ((width != 4 && width != 8) || !d_pout)) return -22;
+  if (d_proj && ((width != 1 && width != 2 && width != 4 && width != 8) || !d_pout)) return -22;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
   if (nb64 > 0xffffffffull) return -75;
@@ -389,8 +645,14 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
   else if (width == 8)
     hipLaunchKernelGGL(emit_rows_kernel<8>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
                        nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
-  else
+  else if (width == 4)
     hipLaunchKernelGGL(emit_rows_kernel<4>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
+  else if (width == 2)
+    hipLaunchKernelGGL(emit_rows_kernel<2>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
+  else
+    hipLaunchKernelGGL(emit_rows_kernel<1>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
                        nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
   (void)hipFreeAsync(cnt, st);
   return hipGetLastError() == hipSuccess ? 0 : -5;
@@ -401,4 +663,49 @@ extern "C" int strom_bitmap_to_rows(const uint64_t *d_bitmap, uint64_t nwords,
                                     int64_t *d_out, uint64_t *d_total, void *stream) {
   return strom_bitmap_to_rows_proj(d_bitmap, nwords, d_batches, nbatches, d_out, d_total, nullptr,
                                    0, nullptr, nullptr, stream);
+}
+
+extern "C" int strom_column_qual(const strom_col_qual *q, const strom_qual_batch *d_batches,
+                                 uint32_t nbatches, uint64_t nwords, uint64_t *d_bitmap,
+                                 const uint64_t *d_or, int and_dst, uint64_t *d_count,
+                                 void *stream) {
+  if (!q) return -22;
+  if (!nbatches || !nwords) return 0;
+  if (!d_batches || !d_bitmap || !d_count || ((uintptr_t)d_bitmap & 7)) return -22;
+  hipStream_t st = (hipStream_t)stream;
+  const bool str = q->type == STROM_COL_STR32 || q->type == STROM_COL_STR64;
+  // constants must fit the LDS staging and be whole dwords
+  if (q->op != STROM_QOP_VALID) {
+    if (!q->consts || (q->const_bytes & 3) || (q->consts & 3)) return -22;
+    if (q->const_bytes + (str ? q->offs_bytes : 0) > (64u << 10)) return -7;
+  }
+  switch (q->op) {
+    case STROM_QOP_RANGES: {
+      const uint64_t need = 16ull * q->nconst;
+      if (str || q->const_bytes < need) return -22;
+      return qual_by_type<QK_RANGE>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
+    }
+    case STROM_QOP_LUT:
+      if (str || q->type == STROM_COL_BOOL || q->type == STROM_COL_F32 || q->type == STROM_COL_F64 ||
+          q->const_bytes * 8 < q->nconst)
+        return -22;
+      return qual_by_type<QK_LUT>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
+    case STROM_QOP_STR_IN:
+    case STROM_QOP_STR_PREFIX:
+    case STROM_QOP_STR_RANGES: {
+      const uint64_t per = q->op == STROM_QOP_STR_RANGES ? 24 : 8;
+      if (!str || !q->offs || (q->offs & 3) || q->offs_bytes < per * q->nconst || (q->offs_bytes & 3))
+        return -22;
+      // every constant inside the blob (checked on the host copy by the
+      // caller's contract: the (start, len) pairs are read from device
+      // memory, so only the sizes can be checked here)
+      if (q->type == STROM_COL_STR32)
+        return launch_qual<int32_t, QK_STR>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
+      return launch_qual<int64_t, QK_STR>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
+    }
+    case STROM_QOP_VALID:
+      return launch_qual<int32_t, QK_VALID>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
+    default:
+      return -22;
+  }
 }

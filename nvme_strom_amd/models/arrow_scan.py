@@ -30,6 +30,7 @@ kmod/nvme_strom.c:1488-1604) is what fetches the scattered buffers.
 from __future__ import annotations
 
 import os
+import struct
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -38,12 +39,19 @@ import numpy as np
 import torch
 
 from ..ops import decompress as D
-from ..ops.colfilter import BATCH_FIELDS, bitmap_to_rows, filter_batched
+from ..ops.colfilter import BATCH_FIELDS, bitmap_to_rows
+from ..ops.colpred import (QUAL_BATCH_FIELDS, Compiled, Pred, clauses, compile_pred, evaluate,
+                           qual_batched)
 from ..ops.reorder import chunk_scatter, landing_positions
 from ..tensor import FileReader, HbmBuffer, host_buffer
-from ..utils.arrow_ipc import ArrowFile, read_metadata
+from ..utils.arrow_ipc import (ArrowFile, Column, _Src, decode_values, dictionary_values,
+                               read_buffer, read_metadata, validity_bits)
 
-_TORCH = {"i4": torch.int32, "i8": torch.int64, "f4": torch.float32, "f8": torch.float64}
+# projection output dtypes by storage (date/time/timestamp/duration: their
+# integer ticks; dictionary-encoded: the indices)
+_TORCH = {"i1": torch.int8, "u1": torch.uint8, "i2": torch.int16, "u2": torch.uint16,
+          "i4": torch.int32, "u4": torch.uint32, "i8": torch.int64, "u8": torch.uint64,
+          "f4": torch.float32, "f8": torch.float64}
 
 
 @dataclass
@@ -57,6 +65,8 @@ class ScanOut:
     groups: int = 0
     values: Optional[torch.Tensor] = None   # projected column, one value per selected row
     valid: Optional[torch.Tensor] = None    # its validity (uint8 0/1) when it has nulls
+    column: Optional[Column] = None         # the projected column's type (units, tz, ...)
+    dictionary: object = None               # its decoded dictionary when dictionary-encoded
 
 
 @dataclass
@@ -72,7 +82,9 @@ class _Buf:
 class _Batch:
     rows: int
     row_base: int
-    cols: List[Tuple[_Buf, Optional[_Buf]]]   # per scanned column: (data, validity)
+    # per scanned column: (data, validity, extra) — data: values / bool bits /
+    # dictionary indices / utf8-binary offsets; extra: the characters
+    cols: List[Tuple[_Buf, Optional[_Buf], Optional[_Buf]]]
 
 
 @dataclass
@@ -86,9 +98,10 @@ class _Group:
     # (kind, offset) with kind 0 none, 1 slot region, 2 decode buffer
     descs: Optional[np.ndarray] = None
     need: Optional[np.ndarray] = None
-    ptr_kind: Optional[np.ndarray] = None   # (n, ncols, 2)
-    ptr_rel: Optional[np.ndarray] = None    # (n, ncols, 2)
-    table: Optional[np.ndarray] = None      # (n, BATCH_FIELDS) with pointer columns 0
+    ptr_kind: Optional[np.ndarray] = None   # (n, ncols, 3)
+    ptr_rel: Optional[np.ndarray] = None    # (n, ncols, 3)
+    aux_len: Optional[np.ndarray] = None    # (n, ncols) decoded character bytes
+    table: Optional[np.ndarray] = None      # (n, QUAL_BATCH_FIELDS), pointer columns 0
     column_bytes: int = 0
 
 
@@ -98,6 +111,7 @@ class _Slot:
     cap: int                               # slot bytes
     dec: torch.Tensor
     bitmap: torch.Tensor
+    bm2: Optional[torch.Tensor] = None     # OR-clause scratch bitmap
     event: Optional[torch.cuda.Event] = None
     stream: Optional[torch.cuda.Stream] = None
     count: Optional[torch.Tensor] = None   # selected rows of the slot's group
@@ -114,6 +128,35 @@ def _up64(n: int) -> int:
 
 def _up64_np(n: np.ndarray) -> np.ndarray:
     return (n + 63) // 64 * 64
+
+
+def _stored_sizes(path: str, off: np.ndarray, ln: np.ndarray, comp: np.ndarray) -> np.ndarray:
+    """Decoded bytes of variable-size buffers (utf8/binary characters):
+    the stored length when raw, else the Arrow BodyCompression prefix
+    (i64 uncompressed length, -1 = stored raw after it), read with a few
+    preads in flight — the plan needs the decode capacity before any data
+    is read into HBM."""
+    out = np.asarray(ln, np.int64).copy()
+    comp = np.asarray(comp, bool)
+    out[comp & (out < 8)] = 0
+    idx = np.flatnonzero(comp & (np.asarray(ln) >= 8))
+    if len(idx):
+        from concurrent.futures import ThreadPoolExecutor
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            with ThreadPoolExecutor(16) as ex:
+                vals = np.array(list(ex.map(
+                    lambda o: struct.unpack("<q", os.pread(fd, 8, o))[0],
+                    np.asarray(off)[idx].tolist())), dtype=np.int64)
+        finally:
+            os.close(fd)
+        raw = vals == -1
+        bad = ~raw & ((vals < 0) | (vals >= (1 << 31)))
+        if bad.any():
+            k = int(idx[np.flatnonzero(bad)[0]])
+            raise ValueError(f"record batch {k}: buffer length prefix {int(vals[bad][0])}")
+        out[idx] = np.where(raw, out[idx] - 8, vals)
+    return out
 
 
 class ArrowScan:
@@ -148,18 +191,24 @@ class ArrowScan:
         # (column tuple, batch range) -> (dtypes, rows, groups)
         self._plans: Dict[tuple, tuple] = {}
         self._bplans: Dict[tuple, tuple] = {}   # column tuple -> _plan()
+        self._dicts: Dict[str, tuple] = {}      # decoded dictionaries
+        self._compiled: Dict[tuple, Compiled] = {}
 
     # ------------------------------------------------------------- plan
     def _plan(self, names: Sequence[str]) -> tuple:
-        cis, dtypes, widths = [], [], []
+        """(per batch _Batch with each column's (data, validity, extra)
+        buffers, the Column metas, total rows).  data: the values / bool
+        bits / dictionary indices / utf8-binary offsets; extra: the
+        characters of a utf8/binary column."""
+        cis, cols = [], []
         for name in names:
             ci = self.meta.column_index(name)
             col = self.meta.schema[ci]
-            if not col.supported or col.numpy_dtype not in _TORCH:
-                raise NotImplementedError(f"column {name}: the GPU filter takes int32/64, float32/64")
+            if not col.supported:
+                raise NotImplementedError(f"column {name}: {col.kind} columns are not scanned "
+                                          "on the GPU")
             cis.append(ci)
-            dtypes.append(_TORCH[col.numpy_dtype])
-            widths.append(col.bit_width // 8)
+            cols.append(col)
         m = self.meta
         used = set(m.codecs) - {None}
         if not used <= {"lz4_frame", "zstd"} or len(used) > 1:
@@ -167,26 +216,51 @@ class ArrowScan:
                                       "LZ4 frame, ZSTD per file)")
         # lz4par.hip / zstd.hip (Arrow IPC buffer codecs: length prefix + frame)
         self._codec = D.ARROW_ZSTD if used == {"zstd"} else D.ARROW_LZ4
-        comp = [c is not None for c in m.codecs]
-        # per column, lists over batches (the metadata is array-backed)
-        percol = []
-        for ci, width in zip(cis, widths):
-            a = m.columns[ci]
-            need = a.length * width
-            vn = (a.length + 7) // 8
-            hasv = (a.null_count != 0) & (a.v_len != 0)
-            percol.append(zip(a.d_off.tolist(), a.d_len.tolist(), need.tolist(),
-                              _up64_np(need).tolist(), a.v_off.tolist(), a.v_len.tolist(),
-                              vn.tolist(), (_up64_np(vn) + 64).tolist(), hasv.tolist(), comp))
+        comp = np.array([c is not None for c in m.codecs], dtype=bool)
         rows = m.columns[cis[0]].length if m.nbatches else np.zeros(0, np.int64)
         base = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
+        percol = []
+        for ci, col in zip(cis, cols):
+            a = m.columns[ci]
+            n = a.length
+            st = col.storage
+            if st == "b1":
+                need = (n + 7) // 8
+            elif col.kind in ("utf8", "binary") and col.dictionary is None:
+                need = np.where(n > 0, (n + 1) * (8 if col.large else 4), 0)
+            else:
+                need = n * np.dtype(st).itemsize
+            vn = (n + 7) // 8
+            hasv = (a.null_count != 0) & (a.v_len != 0)
+            strings = a.x_off is not None and col.dictionary is None
+            if strings:
+                xneed = _stored_sizes(self.path, a.x_off, a.x_len, comp)
+            for what, off, ln, nd in (("data", a.d_off, a.d_len, need),
+                                      ("characters", a.x_off, a.x_len,
+                                       xneed if strings else None)):
+                if nd is None:
+                    continue
+                short = ~comp & (ln < nd)
+                if short.any():
+                    k = int(np.flatnonzero(short)[0])
+                    raise ValueError(f"column {col.name}, record batch {k}: {what} buffer of "
+                                     f"{int(ln[k])} bytes for {int(nd[k])}")
+            z = [None] * len(n)
+            percol.append(zip(a.d_off.tolist(), a.d_len.tolist(), need.tolist(),
+                              _up64_np(need).tolist(), a.v_off.tolist(), a.v_len.tolist(),
+                              vn.tolist(), (_up64_np(vn) + 64).tolist(), hasv.tolist(),
+                              comp.tolist(),
+                              a.x_off.tolist() if strings else z,
+                              a.x_len.tolist() if strings else z,
+                              xneed.tolist() if strings else z))
         cols_by_batch = zip(*percol) if percol else iter(())
         out = []
-        for n, b0, cols in zip(rows.tolist(), base[:-1].tolist(), cols_by_batch):
-            out.append(_Batch(n, b0, [
-                (_Buf(do, dl, nd, cap, cp), _Buf(vo, vl, vn, vcap, cp) if hv else None)
-                for do, dl, nd, cap, vo, vl, vn, vcap, hv, cp in cols]))
-        return out, dtypes, int(base[-1])
+        for nr, b0, cs in zip(rows.tolist(), base[:-1].tolist(), cols_by_batch):
+            out.append(_Batch(nr, b0, [
+                (_Buf(do, dl, nd, cap, cp), _Buf(vo, vl, vn, vcap, cp) if hv else None,
+                 _Buf(xo, xl, xn, _up64(xn) + 64, cp) if xo is not None else None)
+                for do, dl, nd, cap, vo, vl, vn, vcap, hv, cp, xo, xl, xn in cs]))
+        return out, cols, int(base[-1])
 
     def _round_streams(self) -> int:
         cus = 256
@@ -207,8 +281,8 @@ class ArrowScan:
     def _chunks(self, b: _Batch) -> np.ndarray:
         c = self.chunk_sz
         parts = []
-        for data, valid in b.cols:
-            for buf in (data, valid):
+        for bufs in b.cols:
+            for buf in bufs:
                 if buf is not None and buf.length:
                     parts.append(np.arange(buf.off // c, (buf.off + buf.length + c - 1) // c))
         return np.unique(np.concatenate(parts)) if parts else np.zeros(0, dtype=np.int64)
@@ -220,8 +294,9 @@ class ArrowScan:
         # (zstd: every compressed buffer takes the entropy stage's latency,
         # however little it compressed — only stored ones are skipped)
         lim = 1.0 if getattr(self, "_codec", None) == D.ARROW_ZSTD else 0.9
-        comp = [(d, v) for b in batches for d, v in b.cols
-                if d.compressed and 0 < d.length < lim * d.need]
+        comp = [[x for x in bufs if x is not None and x.compressed and 0 < x.length]
+                for b in batches for bufs in b.cols
+                if bufs[0].compressed and 0 < bufs[0].length < lim * bufs[0].need]
         if comp:
             # few streams per launch are fine for the block-parallel decoder
             # (lz4par.hip: a workgroup per stream), so a column of many
@@ -229,8 +304,8 @@ class ArrowScan:
             # overlaps the reads of groups g+1.. (with the round-2 lane
             # decoder every launch took one serial stream's time and the
             # split measured slower, profiles/r3/arrow_split3.json)
-            avg = sum(d.length + (v.length if v else 0) for d, v in comp) / len(comp)
-            total = sum(d.length + (v.length if v else 0) for d, v in comp)
+            avg = sum(x.length for c in comp for x in c) / len(comp)
+            total = sum(x.length for c in comp for x in c)
             want = avg * self.TARGET_STREAMS
             # groups of at most one resident round of streams: the decode of
             # a group takes one stream's latency, and the last group's
@@ -248,8 +323,8 @@ class ArrowScan:
         c = self.chunk_sz
         spans = []                     # (batch index, first chunk, end chunk)
         for i, b in enumerate(batches):
-            for data, valid in b.cols:
-                for buf in (data, valid):
+            for bufs in b.cols:
+                for buf in bufs:
                     if buf is not None and buf.length:
                         spans.append((i, buf.off // c, (buf.off + buf.length + c - 1) // c))
         cur: List[_Batch] = []
@@ -270,7 +345,7 @@ class ArrowScan:
         if cur:
             groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
         for g in groups:
-            g.dec_bytes = sum(buf.cap for b in g.batches for pair in b.cols for buf in pair
+            g.dec_bytes = sum(buf.cap for b in g.batches for bufs in b.cols for buf in bufs
                               if buf is not None and buf.compressed)
             g.words = sum((b.rows + 63) // 64 for b in g.batches)
             self._prepare(g)
@@ -280,13 +355,16 @@ class ArrowScan:
         c = self.chunk_sz
         n = len(g.batches)
         ncols = len(g.batches[0].cols) if n else 0
-        kind = np.zeros((n, ncols, 2), dtype=np.int8)
-        rel = np.zeros((n, ncols, 2), dtype=np.int64)
+        kind = np.zeros((n, ncols, 3), dtype=np.int8)
+        rel = np.zeros((n, ncols, 3), dtype=np.int64)
+        aux_len = np.zeros((n, ncols), dtype=np.int64)
         so, sl, do, dl, need = [], [], [], [], []
         dcur = 0
         for i, b in enumerate(g.batches):
-            for k, pair in enumerate(b.cols):
-                for j, buf in enumerate(pair):
+            for k, bufs in enumerate(b.cols):
+                if bufs[2] is not None:
+                    aux_len[i, k] = bufs[2].need
+                for j, buf in enumerate(bufs):
                     if buf is None:
                         continue
                     if buf.length == 0:
@@ -317,15 +395,17 @@ class ArrowScan:
             g.descs = D.make_descs_arrays(slot_off(so)[order], np.asarray(sl)[order],
                                           np.asarray(do)[order], np.asarray(dl)[order])
             g.need = np.asarray(need, dtype=np.int32)[order]
-        g.ptr_kind, g.ptr_rel = kind, rel
+        g.ptr_kind, g.ptr_rel, g.aux_len = kind, rel, aux_len
         rows = np.array([b.rows for b in g.batches], dtype=np.int64)
         words = (rows + 63) // 64
-        table = np.zeros((n, BATCH_FIELDS), dtype=np.int64)
+        table = np.zeros((n, QUAL_BATCH_FIELDS), dtype=np.int64)
         table[:, 2] = rows
         table[:, 3] = np.concatenate([[0], np.cumsum(words)[:-1]]) if n else 0
         table[:, 4] = [b.row_base for b in g.batches]
         g.table = table
-        g.column_bytes = sum(d.need for b in g.batches for d, _ in b.cols)
+        # decoded bytes the scan reads: values / indices / offsets + characters
+        g.column_bytes = sum(bufs[0].need + (bufs[2].need if bufs[2] is not None else 0)
+                             for b in g.batches for bufs in b.cols)
 
     # --------------------------------------------------------- pipeline
     def _ensure_slots(self, groups: List[_Group]) -> None:
@@ -346,6 +426,7 @@ class ArrowScan:
         for k in range(nsl):
             sl = _Slot(k * nbytes, nbytes,
                        torch.empty(dec, dtype=torch.uint8, device=self.device),
+                       torch.empty(words, dtype=torch.int64, device=self.device),
                        torch.empty(words, dtype=torch.int64, device=self.device))
             sl.stream = torch.cuda.Stream(device=self.device)
             sl.count = torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -381,12 +462,16 @@ class ArrowScan:
 
     @staticmethod
     def _pointers(g: _Group, col: int, base: int, dec_base: int) -> np.ndarray:
+        """The group's strom_qual_batch table for one column: values,
+        validity and character pointers resolved against this slot."""
         t = g.table.copy()
         kind, rel = g.ptr_kind[:, col, :], g.ptr_rel[:, col, :]
-        t[:, :2] = np.where(kind == 1, base + rel, np.where(kind == 2, dec_base + rel, 0))
+        ptrs = np.where(kind == 1, base + rel, np.where(kind == 2, dec_base + rel, 0))
+        t[:, 0], t[:, 1], t[:, 5] = ptrs[:, 0], ptrs[:, 1], ptrs[:, 2]
+        t[:, 6] = g.aux_len[:, col]
         return t
 
-    def _compute(self, k: int, quals, proj, state) -> None:
+    def _compute(self, k: int, spec, proj, state) -> None:
         s = self._slots[k % len(self._slots)]
         res, landed, g = s.pending
         s.pending = None
@@ -420,20 +505,41 @@ class ArrowScan:
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]
-            # the qualifier list: the first writes the bitmap, each later one
-            # ANDs into it; the last one's count is the selection's
-            for q, (col, dtype, lo, hi) in enumerate(quals):
-                tab = self._pointers(g, col, base, dec_base)
-                d_table = torch.from_numpy(tab).pin_memory().to(self.device, non_blocking=True)
-                last = q == len(quals) - 1
-                filter_batched(dtype, d_table, g.words, lo, hi, s.bitmap,
-                               s.count if last else s.junk, stream=cs, combine=q > 0)
-                s.keep.append(d_table)
-            d_proj = None
-            if proj is not None:
-                tab = self._pointers(g, proj, base, dec_base)
-                d_proj = torch.from_numpy(tab).pin_memory().to(self.device, non_blocking=True)
-                s.keep.append(d_proj)
+            # one batch table per referenced column, uploaded once per group
+            tabs: Dict[int, torch.Tensor] = {}
+
+            def table(col: int) -> torch.Tensor:
+                if col not in tabs:
+                    t = self._pointers(g, col, base, dec_base)
+                    tabs[col] = torch.from_numpy(t).pin_memory().to(self.device, non_blocking=True)
+                    s.keep.append(tabs[col])
+                return tabs[col]
+            # the CNF qualifier list: clause 0 writes the bitmap (its
+            # predicates ORed in place), a later single-predicate clause ANDs
+            # into it, a later OR-clause collects in the scratch bitmap and
+            # its last predicate ORs that in and ANDs into the bitmap; the
+            # last launch's count is the selection's
+            for ci, clause in enumerate(spec):
+                for j, (col, cq) in enumerate(clause):
+                    last = ci == len(spec) - 1 and j == len(clause) - 1
+                    cnt = s.count if last else s.junk
+                    if ci == 0:
+                        qual_batched(cq, table(col), g.words, s.bitmap, cnt, stream=cs,
+                                     or_src=s.bitmap if j else None)
+                    elif len(clause) == 1:
+                        qual_batched(cq, table(col), g.words, s.bitmap, cnt, stream=cs,
+                                     and_dst=True)
+                    elif j < len(clause) - 1:
+                        qual_batched(cq, table(col), g.words, s.bm2, cnt, stream=cs,
+                                     or_src=s.bm2 if j else None)
+                    else:
+                        qual_batched(cq, table(col), g.words, s.bitmap, cnt, stream=cs,
+                                     or_src=s.bm2, and_dst=True)
+            # emit tables: the strom_filter_batch prefix of the qual tables
+            any_col = spec[0][0][0]
+            d_rows = table(any_col)[:, :BATCH_FIELDS].contiguous()
+            d_proj = table(proj)[:, :BATCH_FIELDS].contiguous() if proj is not None else None
+            s.keep += [d_rows] + ([d_proj] if d_proj is not None else [])
         # decode + filter of successive groups overlap on their slots'
         # streams; the row-id emit (+ projection gather) runs in group order
         # on one stream (the output cursor is shared), and frees the slot
@@ -442,9 +548,9 @@ class ArrowScan:
         es = self.emit_stream
         es.wait_event(ready)
         with torch.cuda.stream(es):
-            bitmap_to_rows(s.bitmap, g.words, s.keep[-1] if d_proj is None else s.keep[-2],
-                           state["out"], state["cursor"], stream=es, proj=d_proj,
-                           proj_out=state.get("pout"), proj_valid=state.get("pvalid"))
+            bitmap_to_rows(s.bitmap, g.words, d_rows, state["out"], state["cursor"], stream=es,
+                           proj=d_proj, proj_out=state.get("pout"),
+                           proj_valid=state.get("pvalid"))
             state["count"] += s.count
             s.count.zero_()
             if descs is not None:
@@ -455,22 +561,45 @@ class ArrowScan:
         state["bytes_read"] += len(g.ids) * self.chunk_sz
         state["column_bytes"] += g.column_bytes
 
-    def scan_where(self, quals: Sequence[Tuple[str, object, object]],
-                   project: Optional[str] = None,
+    # ------------------------------------------------------------- query
+    def dictionary(self, name: str):
+        """Decoded dictionary of a dictionary-encoded column (host, cached):
+        (values, valid) as utils.arrow_ipc.dictionary_values returns them."""
+        if name not in self._dicts:
+            col = self.meta.schema[self.meta.column_index(name)]
+            self._dicts[name] = dictionary_values(self.meta, col, self.path)
+        return self._dicts[name]
+
+    def _compile(self, p: Pred) -> Compiled:
+        key = (p.col, p.op, repr(p.value))
+        if key not in self._compiled:
+            col = self.meta.schema[self.meta.column_index(p.col)]
+            dic = self.dictionary(p.col) if (col.dictionary is not None and
+                                             p.op not in ("is_null", "is_valid")) else None
+            self._compiled[key] = compile_pred(p, col, dic)
+        return self._compiled[key]
+
+    def scan_where(self, quals, project: Optional[str] = None,
                    batches: Optional[Tuple[int, int]] = None) -> ScanOut:
-        """Row ids (int64, file order) where every ``lo <= column <= hi`` of
-        ``quals`` holds (nulls never qualify) — a PG-Strom qualifier list.
+        """Row ids (int64, file order) of the rows every qualifier selects —
+        a PG-Strom qualifier list.  ``quals`` items: ``(name, lo, hi)``
+        ranges, ``(name, op, value)`` / ``P(name) <op> value`` predicates,
+        or ``Or(...)`` clauses of them (ops/colpred.py: comparisons, IN,
+        OR of ranges, string equality and prefix, null tests, on ints,
+        floats, bool, date/time/timestamp/duration, utf8/binary and
+        dictionary-encoded columns).  Nulls never satisfy a comparison.
         Each referenced column is read from storage and decoded once per
-        group; the per-column bitmaps are ANDed on the device.  ``project``
-        names a column whose values (and validity, when it has nulls) are
-        gathered for the selected rows while their ids are written.
-        ``batches=(b0, b1)`` scans only record batches [b0, b1) (row ids stay
-        file-global: parallel/scan.py splits a file over ranks this way)."""
-        if not quals:
-            raise ValueError("at least one qualifier")
+        group; the predicates' bitmaps are combined on the device.
+        ``project`` names a fixed-width or dictionary-encoded column whose
+        values (indices for a dictionary: ``ScanOut.dictionary`` holds the
+        values) and validity, when it has nulls, are gathered for the
+        selected rows while their ids are written.  ``batches=(b0, b1)``
+        scans only record batches [b0, b1) (row ids stay file-global:
+        parallel/scan.py splits a file over ranks this way)."""
+        cl = clauses(quals)
         t0 = time.perf_counter()
         names: List[str] = []
-        for n in [q[0] for q in quals] + ([project] if project else []):
+        for n in [p.col for c in cl for p in c] + ([project] if project else []):
             if n not in names:
                 names.append(n)
         nb = self.meta.nbatches
@@ -479,22 +608,29 @@ class ArrowScan:
         if key not in self._plans:                # the file's layout is fixed once opened
             if tuple(names) not in self._bplans:
                 self._bplans[tuple(names)] = self._plan(names)
-            allb, dtypes, _ = self._bplans[tuple(names)]
+            allb, cols, _ = self._bplans[tuple(names)]
             sel = allb[rng[0]:rng[1]] if rng[0] < rng[1] else []
-            self._plans[key] = (dtypes, sum(b.rows for b in sel), self._groups(sel))
-        dtypes, nrows, groups = self._plans[key]
-        spec = [(names.index(n), dtypes[names.index(n)], lo, hi) for n, lo, hi in quals]
+            self._plans[key] = (cols, sum(b.rows for b in sel), self._groups(sel))
+        cols, nrows, groups = self._plans[key]
+        spec = [[(names.index(p.col), self._compile(p)) for p in c] for c in cl]
         t_plan = time.perf_counter()
         out = torch.empty(max(nrows, 1), dtype=torch.int64, device=self.device)
         pcol = names.index(project) if project else None
         pout = pvalid = None
+        pmeta = cols[pcol] if project else None
         if project:
-            pout = torch.empty(max(nrows, 1), dtype=dtypes[pcol], device=self.device)
+            st = pmeta.storage
+            if st not in _TORCH or (pmeta.kind in ("utf8", "binary") and pmeta.dictionary is None):
+                raise NotImplementedError(f"projection of {project} ({pmeta.kind}): fixed-width "
+                                          "or dictionary-encoded columns")
+            pout = torch.empty(max(nrows, 1), dtype=_TORCH[st], device=self.device)
             if any(b.cols[pcol][1] is not None for g in groups for b in g.batches):
                 pvalid = torch.empty(max(nrows, 1), dtype=torch.uint8, device=self.device)
+        pdict = self.dictionary(project) if project and pmeta.dictionary is not None else None
         if not groups or nrows == 0:
             return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0},
-                           values=pout[:0] if pout is not None else None)
+                           values=pout[:0] if pout is not None else None,
+                           column=pmeta, dictionary=pdict)
         self._ensure_slots(groups)
         self.emit_stream = torch.cuda.Stream(device=self.device)
         z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
@@ -513,7 +649,8 @@ class ArrowScan:
         cursor, count, err = torch.cat([state["cursor"], state["count"], state["err"]]).tolist()
         t_end = time.perf_counter()
         if err:
-            raise RuntimeError(f"LZ4 decode failed for {err} buffer(s) of columns {names}")
+            raise RuntimeError(f"{'ZSTD' if self._codec == D.ARROW_ZSTD else 'LZ4'} decode "
+                               f"failed for {err} buffer(s) of columns {names}")
         if cursor != count:
             raise RuntimeError(f"row emit mismatch: {cursor} ids for {count} selected")
         for s in self._slots:
@@ -525,7 +662,8 @@ class ArrowScan:
                        bytes_read=state["bytes_read"], column_bytes=state["column_bytes"],
                        groups=len(groups),
                        values=pout[:count] if pout is not None else None,
-                       valid=pvalid[:count] if pvalid is not None else None)
+                       valid=pvalid[:count] if pvalid is not None else None,
+                       column=pmeta, dictionary=pdict)
 
     def scan(self, name: str, lo, hi) -> ScanOut:
         """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never
@@ -534,6 +672,13 @@ class ArrowScan:
 
     # the pre-pipeline name
     filter = scan
+
+    def host_scan_where(self, quals, project: Optional[str] = None,
+                        batches: Optional[Tuple[int, int]] = None) -> "HostScanOut":
+        """The same query on the CPU (buffers read with pread, decoded by
+        the decoders' host twins, predicates by colpred's numpy twin)."""
+        return host_scan_where(self.path, quals, project, batches, meta=self.meta,
+                               dicts=self._dicts)
 
     def _free_slots(self) -> None:
         if self._slots:
@@ -545,3 +690,89 @@ class ArrowScan:
         if self.reader is not None:
             self.reader.close()
             self.reader = None
+
+
+# ------------------------------------------------------------ host twin
+@dataclass
+class HostScanOut:
+    rows: int
+    indices: np.ndarray                # int64 global row ids
+    values: object = None              # projected values (numpy; strings: list of bytes)
+    valid: Optional[np.ndarray] = None
+
+
+def host_scan_where(path: str, quals, project: Optional[str] = None,
+                    batches: Optional[Tuple[int, int]] = None, meta: Optional[ArrowFile] = None,
+                    dicts: Optional[dict] = None) -> HostScanOut:
+    """ArrowScan.scan_where on the CPU: the same metadata, the same
+    compiled predicates (ops/colpred.py), evaluated by the kernel's numpy
+    twin over buffers decoded by the GPU decoders' host twins.  The
+    reference point for the GPU path and a scan for machines without one."""
+    meta = meta if meta is not None else read_metadata(path)
+    dicts = dicts if dicts is not None else {}
+    cl = clauses(quals)
+    schema = {c.name: (i, c) for i, c in enumerate(meta.schema)}
+
+    def dictionary(name):
+        if name not in dicts:
+            dicts[name] = dictionary_values(meta, schema[name][1], path)
+        return dicts[name]
+    comp = []
+    for c in cl:
+        row = []
+        for p in c:
+            col = schema[p.col][1]
+            dic = dictionary(p.col) if col.dictionary is not None and \
+                p.op not in ("is_null", "is_valid") else None
+            row.append((p.col, compile_pred(p, col, dic)))
+        comp.append(row)
+    names = sorted({n for c in comp for n, _ in c} | ({project} if project else set()))
+    nb = meta.nbatches
+    b0, b1 = (0, nb) if batches is None else (max(0, batches[0]), min(nb, batches[1]))
+    base = np.concatenate([[0], np.cumsum(meta.rows)]).astype(np.int64)
+    ids, vals, valid = [], [], []
+    src = _Src(path)
+    try:
+        for bi in range(b0, b1):
+            b = meta.batches[bi]
+            data = {}
+            for n in names:
+                ci, col = schema[n]
+                ch = b.columns[ci]
+                vraw = read_buffer(src, ch.validity, b.codec) if ch.null_count else b""
+                d = read_buffer(src, ch.data, b.codec)
+                vcol = col if col.dictionary is None else Column(n, "int", col.dictionary.index_bits,
+                                                                 col.dictionary.index_signed)
+                x = read_buffer(src, ch.extra, b.codec) if (ch.extra is not None and
+                                                            col.dictionary is None) else b""
+                data[n] = (decode_values(vcol, ch.length, d, x), validity_bits(vraw, ch.length))
+            n = b.length
+            m = np.ones(n, bool)
+            for c in comp:
+                cm = np.zeros(n, bool)
+                for name, cq in c:
+                    v, ok = data[name]
+                    cm |= evaluate(cq, v, ok, n)
+                m &= cm
+            sel = np.flatnonzero(m)
+            ids.append(sel + base[bi])
+            if project:
+                v, ok = data[project]
+                if isinstance(v, tuple):
+                    offs, chars = v
+                    vals.append([chars[offs[i]:offs[i + 1]].tobytes() for i in sel])
+                else:
+                    vals.append(np.asarray(v)[sel])
+                valid.append(ok[sel] if ok is not None else np.ones(len(sel), bool))
+    finally:
+        src.close()
+    out = HostScanOut(int(base[b1] - base[b0]) if b1 > b0 else 0,
+                      np.concatenate(ids) if ids else np.zeros(0, np.int64))
+    if project:
+        if vals and isinstance(vals[0], list):
+            out.values = [x for v in vals for x in v]
+        else:
+            out.values = np.concatenate(vals) if vals else np.zeros(0)
+        vv = np.concatenate(valid) if valid else np.zeros(0, bool)
+        out.valid = None if vv.all() else vv
+    return out

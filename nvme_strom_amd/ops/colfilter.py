@@ -91,7 +91,7 @@ def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out
     ``cursor`` (int64[1], device) advances — successive groups of one scan
     fill ``out`` in order without a host round trip.  ``proj`` (a batch
     table of another column, same batches) gathers that column's value of
-    each selected row into ``proj_out[cursor]`` (4- or 8-byte elements),
+    each selected row into ``proj_out[cursor]`` (1/2/4/8-byte elements),
     and its validity (0/1) into ``proj_valid`` when given."""
     require_cuda(bitmap, "bitmap")
     if out.dtype != torch.int64:
@@ -101,8 +101,8 @@ def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out
         if proj_out is None or proj.shape != batches.shape:
             raise ValueError("projection needs proj_out and a table of the same batches")
         width = proj_out.element_size()
-        if width not in (4, 8):
-            raise ValueError("projected values are 4 or 8 bytes")
+        if width not in (1, 2, 4, 8):
+            raise ValueError("projected values are 1, 2, 4 or 8 bytes")
         pptr = ptr(proj_out)
         vptr = ptr(proj_valid) if proj_valid is not None else 0
     check(lib().strom_bitmap_to_rows_proj(ptr(bitmap), nwords, ptr(batches), batches.shape[0],

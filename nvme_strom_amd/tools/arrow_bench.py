@@ -24,6 +24,14 @@ The ``qual2`` row is a PG-Strom qualifier list: ``val`` and ``x`` ranges
 projected for the selected rows; rows AND projected values are verified
 against numpy.
 
+``--strings`` (default on) adds a second file (``--string-rows``) with a
+utf8 ``name`` column (words of 3-24 bytes), a dictionary-encoded ``cat``
+(1000 categories), a date32 ``day`` and a timestamp ``ts``, and rows for a
+string-equality scan, a string prefix, a dictionary equality, a dictionary
+range, and a date range AND an OR of timestamp ranges — each verified
+against pyarrow.compute (row ids of Table.filter of the same expression),
+whose time on the memory-mapped file is ``cpu_ms``.
+
 ``python -m nvme_strom_amd.tools.arrow_bench --out gpurun_out/arrow.json``
 """
 from __future__ import annotations
@@ -92,6 +100,78 @@ def cpu_scan(path: str, name: str, lo, hi) -> tuple:
     return time.perf_counter() - t0, n
 
 
+def make_string_file(path: str, rows: int, batch_rows: int, seed: int = 9,
+                     codec: str = "lz4") -> None:
+    """name: utf8 words (a 20k vocabulary, 3-24 bytes), cat: dictionary of
+    1000 categories, day: date32, ts: timestamp[us, UTC], sid: int64."""
+    import pyarrow as pa
+    import pyarrow.ipc as ipc
+    if os.path.exists(path):
+        return
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    vocab = []
+    for k in range(20000):
+        n = int(rng.integers(3, 25))
+        vocab.append(letters[rng.integers(0, 26, n)].tobytes().decode())
+    vocab = pa.array(vocab)
+    cats = pa.array([f"cat_{k:05d}" for k in range(1000)])
+    schema = pa.schema([("sid", pa.int64()), ("name", pa.string()),
+                        ("cat", pa.dictionary(pa.int32(), pa.string())),
+                        ("day", pa.date32()), ("ts", pa.timestamp("us", tz="UTC"))])
+    ts0 = np.datetime64("2024-01-01T00:00:00", "us").astype(np.int64)
+    tmp = path + ".tmp"
+    with ipc.new_file(tmp, schema, options=ipc.IpcWriteOptions(compression=codec)) as w:
+        for b0 in range(0, rows, batch_rows):
+            n = min(batch_rows, rows - b0)
+            name = pa.DictionaryArray.from_arrays(
+                pa.array(rng.integers(0, len(vocab), n).astype(np.int32)), vocab).dictionary_decode()
+            cat = pa.DictionaryArray.from_arrays(
+                pa.array(rng.integers(0, 1000, n).astype(np.int32)), cats)
+            day = pa.array(rng.integers(18000, 20000, n).astype(np.int32)).view(pa.date32())
+            ts = pa.array(ts0 + rng.integers(0, 365 * 86400 * 10**6, n)).view(
+                pa.timestamp("us", tz="UTC"))
+            w.write_batch(pa.record_batch([pa.array(np.arange(b0, b0 + n, dtype=np.int64)), name,
+                                           cat, day, ts], schema=schema))
+            if (b0 // batch_rows) % 256 == 255:
+                _log(f"writing {b0 + n}/{rows} string rows")
+    os.replace(tmp, path)
+
+
+def pc_expr(quals):
+    """The qualifier list as a pyarrow compute Expression (Kleene OR: SQL)."""
+    import pyarrow.compute as pc
+    from nvme_strom_amd.ops.colpred import Or, as_pred
+
+    def one(p):
+        f = pc.field(p.col)
+        v = p.value
+        return {"==": lambda: f == v, "!=": lambda: f != v, "<": lambda: f < v,
+                "<=": lambda: f <= v, ">": lambda: f > v, ">=": lambda: f >= v,
+                "between": lambda: (f >= v[0]) & (f <= v[1]),
+                "in": lambda: f.isin(list(v)),
+                "prefix": lambda: pc.starts_with(f, pattern=v)}[p.op]()
+    e = None
+    for q in quals:
+        c = None
+        for p in (q.preds if isinstance(q, Or) else [as_pred(q)]):
+            c = one(p) if c is None else (c | one(p))
+        e = c if e is None else (e & c)
+    return e
+
+
+def pc_scan(path: str, quals) -> tuple:
+    """pyarrow on the host: memory-mapped file, the same expression -> row ids."""
+    import pyarrow as pa
+    import pyarrow.ipc as ipc
+    t0 = time.perf_counter()
+    with pa.memory_map(path) as src:
+        t = ipc.open_file(src).read_all()
+        t = t.append_column("__row", pa.array(np.arange(t.num_rows, dtype=np.int64)))
+        ids = np.asarray(t.filter(pc_expr(quals)).column("__row"))
+    return time.perf_counter() - t0, ids
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1 << 27)
@@ -104,6 +184,9 @@ def main(argv=None) -> int:
                     help="Arrow IPC body compression pyarrow writes the file with")
     ap.add_argument("--no-qual2", dest="qual2", action="store_false",
                     help="skip the two-column qualifier list + projection row")
+    ap.add_argument("--no-strings", dest="strings", action="store_false",
+                    help="skip the utf8 / dictionary / date / timestamp file and rows")
+    ap.add_argument("--string-rows", type=int, default=1 << 26)
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -143,30 +226,51 @@ def main(argv=None) -> int:
             cols_np[name] = column_np(path, name)
         return cols_np[name]
 
-    try:
-        for label, quals, proj in specs:
-            runs = []
-            sc = None
-            try:
-                for r in range(a.reps):
-                    S.evict_file(fd)
-                    torch.cuda.synchronize()
-                    t1 = time.perf_counter()
-                    if sc is None:                  # cold: open + plan + allocate
-                        sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20)
-                        t_open = time.perf_counter() - t1
-                    out = sc.scan_where(quals, project=proj)
-                    dt = time.perf_counter() - t1
-                    runs.append(dt)
-                    if r == 0:
-                        cold_bd = dict(open_s=round(t_open, 4),
-                                       **{k: round(v, 4) for k, v in out.seconds.items()})
-                    _log(f"{label}{' cold' if r == 0 else ''}: {out.selected} rows, "
-                         f"{dt * 1e3:.1f} ms, groups {out.groups}, "
-                         f"{out.column_bytes / dt / 1e9:.1f} GB/s column, {out.seconds}")
-            finally:
-                if sc is not None:
-                    sc.close()
+    def run(path, fd, label, quals, proj, verify):
+        runs = []
+        sc = None
+        try:
+            for r in range(a.reps):
+                S.evict_file(fd)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                if sc is None:                  # cold: open + plan + allocate
+                    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20)
+                    t_open = time.perf_counter() - t1
+                out = sc.scan_where(quals, project=proj)
+                dt = time.perf_counter() - t1
+                runs.append(dt)
+                if r == 0:
+                    cold_bd = dict(open_s=round(t_open, 4),
+                                   **{k: round(v, 4) for k, v in out.seconds.items()})
+                _log(f"{label}{' cold' if r == 0 else ''}: {out.selected} rows, "
+                     f"{dt * 1e3:.1f} ms, groups {out.groups}, "
+                     f"{out.column_bytes / dt / 1e9:.1f} GB/s column, {out.seconds}")
+        finally:
+            if sc is not None:
+                sc.close()
+        ok, cpu_s, cpu_n = verify(out)
+        warm = runs[1:] or runs
+        med = float(np.median(warm))
+        row = dict(
+            quals=[repr(q) for q in quals], project=proj,
+            selected=out.selected, verified=ok, cpu_selected=cpu_n,
+            column_bytes=out.column_bytes, bytes_read=out.bytes_read, groups=out.groups,
+            ms=[round(x * 1e3, 2) for x in runs],
+            cold_ms=round(runs[0] * 1e3, 2), warm_median_ms=round(med * 1e3, 2),
+            column_GBps=round(out.column_bytes / med / 1e9, 2),
+            column_GBps_cold=round(out.column_bytes / runs[0] / 1e9, 2),
+            file_GBps=round(out.bytes_read / med / 1e9, 2),
+            last_breakdown_s={k: round(v, 4) for k, v in out.seconds.items()},
+            cold_breakdown_s=cold_bd)
+        if cpu_s == cpu_s:
+            row.update(cpu_ms=round(cpu_s * 1e3, 1),
+                       cpu_GBps=round(out.column_bytes / cpu_s / 1e9, 2))
+        res["columns"][label] = row
+        _log(json.dumps(row))
+
+    def verify_np(quals, proj):
+        def f(out):
             m = None
             for name, lo, hi in quals:
                 vals, valid = col(name)
@@ -182,27 +286,56 @@ def main(argv=None) -> int:
                 ok = ok and bool(np.array_equal(out.values.cpu().numpy(), pv[ref]))
             cpu_s, cpu_n = (cpu_scan(path, quals[0][0], quals[0][1], quals[0][2])
                             if len(quals) == 1 else (float("nan"), -1))
-            warm = runs[1:] or runs
-            med = float(np.median(warm))
-            row = dict(
-                quals=[list(q) for q in quals], project=proj,
-                selected=out.selected, verified=ok, cpu_selected=cpu_n,
-                column_bytes=out.column_bytes, bytes_read=out.bytes_read, groups=out.groups,
-                ms=[round(x * 1e3, 2) for x in runs],
-                cold_ms=round(runs[0] * 1e3, 2), warm_median_ms=round(med * 1e3, 2),
-                column_GBps=round(out.column_bytes / med / 1e9, 2),
-                column_GBps_cold=round(out.column_bytes / runs[0] / 1e9, 2),
-                file_GBps=round(out.bytes_read / med / 1e9, 2),
-                last_breakdown_s={k: round(v, 4) for k, v in out.seconds.items()},
-                cold_breakdown_s=cold_bd)
-            if cpu_s == cpu_s:
-                row.update(cpu_ms=round(cpu_s * 1e3, 1),
-                           cpu_GBps=round(out.column_bytes / cpu_s / 1e9, 2))
-            res["columns"][label] = row
-            _log(json.dumps(row))
+            return ok, cpu_s, cpu_n
+        return f
+
+    try:
+        for label, quals, proj in specs:
+            run(path, fd, label, quals, proj, verify_np(quals, proj))
     finally:
         os.close(fd)
-    res["arrow_scan_GBps"] = min(c["column_GBps"] for c in res["columns"].values())
+    if a.strings:
+        import datetime as _dt
+
+        from nvme_strom_amd.ops.colpred import Or, P
+        spath = os.path.join(a.dir, f"s_{a.string_rows}_{a.batch_rows}{tag}.arrow")
+        t0 = time.time()
+        make_string_file(spath, a.string_rows, a.batch_rows, codec=a.codec)
+        res["string_file_bytes"] = os.path.getsize(spath)
+        res["string_rows"] = a.string_rows
+        _log(f"string file {res['string_file_bytes'] / 2**30:.2f} GiB in {time.time() - t0:.1f}s")
+        import pyarrow as pa
+        import pyarrow.ipc as ipc
+        with pa.memory_map(spath) as src:
+            word = ipc.open_file(src).get_batch(0).column(1)[7].as_py()
+        t1 = _dt.datetime(2024, 3, 1, tzinfo=_dt.timezone.utc)
+        t2 = _dt.datetime(2024, 11, 1, tzinfo=_dt.timezone.utc)
+        sspecs = [
+            ("str_eq", [P("name") == word], None),
+            ("str_prefix", [P("name").startswith("ab")], None),
+            ("dict_eq", [P("cat") == "cat_00042"], "sid"),
+            ("dict_range", [P("cat").between("cat_00100", "cat_00199")], None),
+            ("date_ts", [P("day").between(_dt.date(2020, 1, 1), _dt.date(2021, 6, 30)),
+                         Or(P("ts") < t1, P("ts") >= t2)], "sid"),
+        ]
+        sfd = os.open(spath, os.O_RDONLY)
+
+        def verify_pc(quals, proj):
+            def f(out):
+                cpu_s, ref = pc_scan(spath, quals)
+                got = out.indices.cpu().numpy()
+                ok = bool(np.array_equal(got, ref))
+                if proj == "sid":       # sid is the row id
+                    ok = ok and bool(np.array_equal(out.values.cpu().numpy(), ref))
+                return ok, cpu_s, len(ref)
+            return f
+        try:
+            for label, quals, proj in sspecs:
+                run(spath, sfd, label, quals, proj, verify_pc(quals, proj))
+        finally:
+            os.close(sfd)
+    base_rows = [res["columns"][lb] for lb, _, _ in specs]
+    res["arrow_scan_GBps"] = min(c["column_GBps"] for c in base_rows)
     res["verified"] = all(c["verified"] for c in res["columns"].values())
     js = json.dumps(res)
     if a.out:

@@ -7,15 +7,22 @@ module walks the flatbuffer metadata (File.fbs Footer/Block, Message.fbs
 Message/RecordBatch/FieldNode/Buffer/BodyCompression, Schema.fbs
 Schema/Field/Int/FloatingPoint) with a ~60-line flatbuffer reader.
 
-Supported columns: fixed-width primitives (int8..64, uint8..64, float16/32/64)
-— the kinds the GPU filter evaluates.  Other columns are listed with
-``supported = False``.
+Scan-able columns (``supported``): fixed-width integers and floats,
+bool (bit-packed), date32/64, time32/64, timestamp (any unit, tz kept),
+duration, utf8/binary and their large (64-bit offset) forms, and
+dictionary-encoded columns of those (the record batches carry the index
+column; the dictionaries come from the file's DictionaryBatch messages,
+Message.fbs DictionaryBatch{id, data, isDelta}, and are decoded on the
+host: they are small and a predicate on one becomes a lookup table over
+the indices).  Other columns (decimal, nested, views) are listed with
+``supported = False``; a file holding a variadic-buffer view column cannot
+be laid out and is refused.
 """
 from __future__ import annotations
 
 import struct
 from dataclasses import dataclass, field
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -78,42 +85,112 @@ class FB:
 
 # ------------------------------------------------------------------ schema
 @dataclass
+class DictEncoding:
+    """Schema.fbs DictionaryEncoding: the record batches hold ``index``
+    integers into dictionary ``id`` (Int indexType, int32 when absent)."""
+    id: int
+    index_bits: int = 32
+    index_signed: bool = True
+    ordered: bool = False
+
+
+@dataclass
 class Column:
     name: str
-    kind: str                  # "int" | "float" | "other"
-    bit_width: int = 0
+    kind: str                  # int float bool date time timestamp duration utf8 binary other
+    bit_width: int = 0         # fixed-width value bits (the date/time/... storage integer)
     signed: bool = True
     nullable: bool = True
     nbuffers: int = 2          # own buffers (validity + data for primitives)
     children: List["Column"] = field(default_factory=list)
-    supported: bool = True     # the GPU filter can evaluate it
+    supported: bool = True     # the GPU scan can evaluate predicates on it
+    unit: str = ""             # date: "d"/"ms"; time/timestamp/duration: "s" "ms" "us" "ns"
+    tz: str = ""               # timestamp time zone ("" = naive)
+    large: bool = False        # utf8/binary with 64-bit offsets
+    dictionary: Optional[DictEncoding] = None
+
+    @property
+    def storage(self) -> str:
+        """numpy dtype of the record-batch data buffer: the value integers
+        or floats, the offsets of a utf8/binary column, the indices of a
+        dictionary-encoded one; "b1" for bit-packed bools."""
+        if self.dictionary is not None:
+            d = self.dictionary
+            return f"{'i' if d.index_signed else 'u'}{d.index_bits // 8}"
+        if self.kind in ("utf8", "binary"):
+            return "i8" if self.large else "i4"
+        if self.kind == "bool":
+            return "b1"
+        if self.kind == "float":
+            return {16: "f2", 32: "f4", 64: "f8"}[self.bit_width]
+        if self.kind in _INTLIKE:
+            return f"{'i' if self.signed else 'u'}{self.bit_width // 8}"
+        raise ValueError(f"column {self.name}: no storage type for {self.kind}")
 
     @property
     def numpy_dtype(self) -> str:
-        if self.kind == "int":
-            return f"{'i' if self.signed else 'u'}{self.bit_width // 8}"
-        return {16: "f2", 32: "f4", 64: "f8"}[self.bit_width]
+        return self.storage
 
 
-_TYPE_INT, _TYPE_FP = 2, 3
+_INTLIKE = ("int", "date", "time", "timestamp", "duration")
+# Schema.fbs Type union ids
+(_TY_INT, _TY_FP, _TY_BIN, _TY_UTF8, _TY_BOOL, _TY_DATE, _TY_TIME, _TY_TS, _TY_DUR,
+ _TY_LBIN, _TY_LUTF8) = 2, 3, 4, 5, 6, 8, 9, 10, 18, 19, 20
+_TUNIT = ("s", "ms", "us", "ns")       # TimeUnit enum
 # own buffer count per Schema.fbs Type id (None = layout not walkable here)
 _NBUF = {1: 0, 2: 2, 3: 2, 4: 3, 5: 3, 6: 2, 7: 2, 8: 2, 9: 2, 10: 2, 11: 2, 12: 2, 13: 1,
          15: 2, 16: 1, 17: 2, 18: 2, 19: 3, 20: 3, 21: 2}
 
 
+def _value_type(name: str, nullable: bool, ttype: int, t: Optional[FB]) -> Column:
+    """The Column of a Schema.fbs type table (flatbuffer defaults applied:
+    writers omit fields equal to them — Date.unit MILLISECOND, Time.unit
+    MILLISECOND + bitWidth 32, Duration.unit MILLISECOND)."""
+    g = (lambda i, fmt, d: t.scalar(i, fmt, d)) if t is not None else (lambda i, fmt, d: d)
+    if ttype == _TY_INT and t is not None:
+        return Column(name, "int", g(0, "i", 0), bool(g(1, "B", 0)), nullable)
+    if ttype == _TY_FP and t is not None:
+        bits = {0: 16, 1: 32, 2: 64}[g(0, "h", 0)]
+        return Column(name, "float", bits, True, nullable, supported=bits != 16)
+    if ttype == _TY_BOOL:
+        return Column(name, "bool", 1, False, nullable)
+    if ttype in (_TY_UTF8, _TY_LUTF8, _TY_BIN, _TY_LBIN):
+        return Column(name, "utf8" if ttype in (_TY_UTF8, _TY_LUTF8) else "binary", 0, False,
+                      nullable, nbuffers=3, large=ttype in (_TY_LBIN, _TY_LUTF8))
+    if ttype == _TY_DATE:
+        day = g(0, "h", 1) == 0
+        return Column(name, "date", 32 if day else 64, True, nullable, unit="d" if day else "ms")
+    if ttype == _TY_TIME:
+        return Column(name, "time", g(1, "i", 32), True, nullable, unit=_TUNIT[g(0, "h", 1)])
+    if ttype == _TY_TS:
+        return Column(name, "timestamp", 64, True, nullable, unit=_TUNIT[g(0, "h", 0)],
+                      tz=t.string(1) if t is not None else "")
+    if ttype == _TY_DUR:
+        return Column(name, "duration", 64, True, nullable, unit=_TUNIT[g(0, "h", 1)])
+    return Column(name, "other", nullable=nullable, nbuffers=_NBUF.get(ttype, -1),
+                  supported=False)
+
+
 def _column(f: FB) -> Column:
     name = f.string(0)
     nullable = bool(f.scalar(1, "B", 0))
-    ttype = f.scalar(2, "B", 0)
-    t = f.table(3)
-    children = [_column(c) for c in f.tables(5)]
-    if ttype == _TYPE_INT and t is not None:
-        return Column(name, "int", t.scalar(0, "i", 0), bool(t.scalar(1, "B", 0)), nullable)
-    if ttype == _TYPE_FP and t is not None:
-        prec = t.scalar(0, "h", 0)
-        return Column(name, "float", {0: 16, 1: 32, 2: 64}[prec], True, nullable)
-    return Column(name, "other", nullable=nullable, nbuffers=_NBUF.get(ttype, -1),
-                  children=children, supported=False)
+    col = _value_type(name, nullable, f.scalar(2, "B", 0), f.table(3))
+    de = f.table(4)
+    if de is not None:
+        # dictionary-encoded: one node + validity/index buffers in the
+        # record batches whatever the value type (its children, if any,
+        # live in the dictionary batches)
+        it = de.table(1)
+        col.dictionary = DictEncoding(de.scalar(0, "q", 0),
+                                      it.scalar(0, "i", 32) if it is not None else 32,
+                                      bool(it.scalar(1, "B", 1)) if it is not None else True,
+                                      bool(de.scalar(2, "B", 0)))
+        col.supported = col.kind != "other"
+        col.nbuffers = 2
+        return col
+    if col.kind == "other":
+        col.children = [_column(c) for c in f.tables(5)]
+    return col
 
 
 # ----------------------------------------------------------------- batches
@@ -128,7 +205,20 @@ class ColumnChunk:
     length: int
     null_count: int
     validity: BufferRef
-    data: BufferRef
+    data: BufferRef            # values / indices / utf8-binary offsets
+    extra: Optional[BufferRef] = None   # utf8/binary: the character data
+
+
+@dataclass
+class DictBatch:
+    """One DictionaryBatch message: the value column's node and buffers
+    (absolute file offsets), in the order the value type lays them out."""
+    id: int
+    length: int
+    null_count: int
+    codec: Optional[str]
+    buffers: List[BufferRef]
+    delta: bool
 
 
 @dataclass
@@ -150,6 +240,8 @@ class ColumnArrays:
     v_len: np.ndarray
     d_off: np.ndarray          # data buffer
     d_len: np.ndarray
+    x_off: Optional[np.ndarray] = None   # third buffer (utf8/binary data)
+    x_len: Optional[np.ndarray] = None
 
 
 class ArrowFile:
@@ -158,7 +250,7 @@ class ArrowFile:
     the per-batch objects on first use (a scan plan reads the arrays)."""
 
     def __init__(self, schema: List[Column], size: int, offset=None, rows=None, body=None,
-                 body_len=None, codecs=None, columns=None):
+                 body_len=None, codecs=None, columns=None, dicts=None):
         self.schema = schema
         self.size = size
         z = np.zeros(0, np.int64)
@@ -169,6 +261,8 @@ class ArrowFile:
         self.codecs: List[Optional[str]] = codecs if codecs is not None else []
         self.columns: List[ColumnArrays] = columns if columns is not None else []
         self._batches: Optional[List[Batch]] = None
+        # dictionary id -> its DictionaryBatch messages in file order
+        self.dicts: Dict[int, List[DictBatch]] = dicts if dicts is not None else {}
 
     @property
     def nbatches(self) -> int:
@@ -181,8 +275,12 @@ class ArrowFile:
             for c in self.columns:
                 it = zip(*(a.tolist() for a in (c.length, c.null_count, c.v_off, c.v_len,
                                                  c.d_off, c.d_len)))
-                percol.append([ColumnChunk(a, b, BufferRef(vo, vl), BufferRef(do, dl))
-                               for a, b, vo, vl, do, dl in it])
+                ch = [ColumnChunk(a, b, BufferRef(vo, vl), BufferRef(do, dl))
+                      for a, b, vo, vl, do, dl in it]
+                if c.x_off is not None:
+                    for k, (xo, xl) in enumerate(zip(c.x_off.tolist(), c.x_len.tolist())):
+                        ch[k].extra = BufferRef(xo, xl)
+                percol.append(ch)
             self._batches = [
                 Batch(o, r, bo, bl, cd, [c[j] for c in percol])
                 for j, (o, r, bo, bl, cd) in enumerate(zip(
@@ -192,7 +290,8 @@ class ArrowFile:
 
     def __eq__(self, other) -> bool:
         return (isinstance(other, ArrowFile) and self.schema == other.schema
-                and self.size == other.size and self.batches == other.batches)
+                and self.size == other.size and self.batches == other.batches
+                and self.dicts == other.dicts)
 
     def column_index(self, name: str) -> int:
         for i, c in enumerate(self.schema):
@@ -344,11 +443,132 @@ def _read(src: "_Src", native: bool = False) -> ArrowFile:
     cols = []
     for ni, bi, own in lay:
         z = np.zeros(len(keep), np.int64)
-        if own == 2:
-            cols.append(ColumnArrays(nodes[keep, ni, 0], nodes[keep, ni, 1],
-                                     bo + bufs[keep, bi, 0], bufs[keep, bi, 1],
-                                     bo + bufs[keep, bi + 1, 0], bufs[keep, bi + 1, 1]))
+        if own in (2, 3):
+            ca = ColumnArrays(nodes[keep, ni, 0], nodes[keep, ni, 1],
+                              bo + bufs[keep, bi, 0], bufs[keep, bi, 1],
+                              bo + bufs[keep, bi + 1, 0], bufs[keep, bi + 1, 1])
+            if own == 3:
+                ca.x_off, ca.x_len = bo + bufs[keep, bi + 2, 0], bufs[keep, bi + 2, 1]
+            cols.append(ca)
         else:
             cols.append(ColumnArrays(nodes[keep, ni, 0], nodes[keep, ni, 1], z, z, z, z))
     return ArrowFile(schema, src.size, blocks[keep, 0], rows[keep], bo, blocks[keep, 2],
-                     [names[c] for c in codec[keep].tolist()], cols)
+                     [names[c] for c in codec[keep].tolist()], cols,
+                     _dictionaries(src, footer, fbuf))
+
+
+def _dictionaries(src: "_Src", footer: FB, fbuf: bytes) -> Dict[int, List[DictBatch]]:
+    """Footer.dictionaries -> DictionaryBatch messages (Message.fbs
+    header_type 2: DictionaryBatch{id, data: RecordBatch, isDelta}).  Only
+    their headers are read here; values are decoded when a scan needs them."""
+    start, n = footer.vector(2)
+    out: Dict[int, List[DictBatch]] = {}
+    for k in range(n):
+        boff, mlen, _, _ = struct.unpack_from("<qiiq", fbuf, start + 24 * k)
+        buf = src.read(boff, mlen)
+        msg, _ = _message(buf, 0)
+        if msg.scalar(1, "B", 0) != 2:
+            raise ValueError(f"dictionary block {k}: not a DictionaryBatch message")
+        db = msg.table(2)
+        rb = db.table(1) if db is not None else None
+        if rb is None:
+            raise ValueError(f"dictionary block {k}: no data")
+        comp = rb.table(3)
+        codec = _CODECS.get(-1 if comp is None else comp.scalar(0, "b", 0), "unknown")
+        ns, nn = rb.vector(1)
+        bs, nb = rb.vector(2)
+        length, nulls = (struct.unpack_from("<qq", buf, ns) if nn else (0, 0))
+        base = boff + mlen
+        bufs = [BufferRef(base + o, ln) for o, ln in
+                (struct.unpack_from("<qq", buf, bs + 16 * j) for j in range(nb))]
+        did = db.scalar(0, "q", 0)
+        out.setdefault(did, []).append(DictBatch(did, rb.scalar(0, "q", length), nulls, codec,
+                                                 bufs, bool(db.scalar(2, "B", 0))))
+    return out
+
+
+# ------------------------------------------------------------ host decode
+def read_buffer(src, ref: BufferRef, codec: Optional[str]) -> bytes:
+    """One stored buffer, decompressed on the host (Arrow BodyCompression:
+    i64 uncompressed length, -1 = stored raw, then the frame).  The host
+    twins of the GPU decoders do the work (ops/decompress.py), so the file's
+    codecs need no CPU library.  ``src``: a path, bytes or an open _Src."""
+    own = not isinstance(src, _Src)
+    s = _Src(src) if own else src
+    try:
+        raw = s.read(ref.offset, ref.length)
+    finally:
+        if own:
+            s.close()
+    if codec is None or not raw:
+        return raw
+    n, = struct.unpack_from("<q", raw, 0)
+    if n == -1:
+        return raw[8:]
+    from ..ops import decompress as D
+    if codec == "zstd":
+        st, out = D.zstd_host(D.ARROW_ZSTD, raw, n)
+    elif codec == "lz4_frame":
+        st, out, _ = D.lz4par_host(D.ARROW_LZ4, raw, n)
+    else:
+        raise ValueError(f"body compression {codec}")
+    if st != n:
+        raise ValueError(f"buffer at {ref.offset}: decoded {st} of {n} bytes")
+    return out
+
+
+def validity_bits(raw: bytes, n: int) -> Optional[np.ndarray]:
+    """Arrow LSB-first validity bytes -> bool[n] (None: all valid)."""
+    if not raw:
+        return None
+    return np.unpackbits(np.frombuffer(raw, np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def decode_values(col: Column, length: int, data: bytes, extra: bytes = b""):
+    """A chunk's values as numpy: fixed-width -> the storage dtype array;
+    bool -> bool array; utf8/binary -> (int64 offsets[length + 1], uint8
+    data).  (For a dictionary-encoded column ``col`` describes the VALUE
+    type and ``data``/``extra`` are the dictionary's buffers.)"""
+    if col.kind == "bool":
+        return np.unpackbits(np.frombuffer(data, np.uint8), bitorder="little")[:length].astype(bool)
+    if col.kind in ("utf8", "binary"):
+        offs = np.frombuffer(data, "<i8" if col.large else "<i4", length + 1) if length else \
+            np.zeros(1, np.int64)
+        return offs.astype(np.int64), np.frombuffer(extra, np.uint8)
+    dt = np.dtype("<" + (Column(col.name, col.kind, col.bit_width, col.signed).storage))
+    return np.frombuffer(data, dt, length)
+
+
+def dictionary_values(meta: "ArrowFile", col: Column, src) -> Tuple[object, Optional[np.ndarray]]:
+    """The decoded dictionary of a dictionary-encoded column: (values,
+    valid) with values as decode_values returns them, deltas appended in
+    file order.  Two non-delta batches for one id (a replacement) are
+    refused: the file format does not allow them."""
+    if col.dictionary is None:
+        raise ValueError(f"column {col.name} is not dictionary-encoded")
+    parts = meta.dicts.get(col.dictionary.id, [])
+    if not parts:
+        raise ValueError(f"column {col.name}: dictionary {col.dictionary.id} missing")
+    if any(not p.delta for p in parts[1:]):
+        raise ValueError(f"column {col.name}: dictionary replaced inside an IPC file")
+    vals, valid, strings = [], [], col.kind in ("utf8", "binary")
+    for p in parts:
+        need = 3 if strings else 2
+        if len(p.buffers) < need:
+            raise ValueError(f"dictionary {p.id}: {len(p.buffers)} buffers")
+        bufs = [read_buffer(src, b, p.codec) for b in p.buffers[:need]]
+        v = decode_values(col, p.length, bufs[1], bufs[2] if strings else b"")
+        vals.append(v)
+        vb = validity_bits(bufs[0], p.length) if p.null_count else None
+        valid.append(vb if vb is not None else np.ones(p.length, bool))
+    if strings:
+        offs, datas, base = [np.zeros(1, np.int64)], [], 0
+        for o, d in vals:
+            offs.append(o[1:] - o[0] + base)
+            datas.append(d[o[0]:o[-1]])
+            base += int(o[-1] - o[0])
+        out = (np.concatenate(offs), np.concatenate(datas) if datas else np.zeros(0, np.uint8))
+    else:
+        out = np.concatenate(vals)
+    vv = np.concatenate(valid)
+    return out, (None if vv.all() else vv)

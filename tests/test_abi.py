@@ -101,3 +101,27 @@ def test_heap_scan2_layout_matches_c(tmp_path):
             N.HeapScan2Args.desc.offset, N.HeapScan2Args.nquals.offset,
             N.HeapScan2Args.quals.offset, N.HeapScan2Args.recheck_count.offset]
     assert got == want
+
+
+def test_column_qual_layout_matches_c(tmp_path):
+    """struct strom_col_qual / strom_qual_batch (the Arrow scan's general
+    qualifier) as ops/colpred.py lays them out equals the C layout, and
+    the storage/operator codes equal the header's."""
+    from nvme_strom_amd.ops import colpred as CP
+    src = tmp_path / "qual.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "strom/strom.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %d %d %d %d %d %d %d %d %d\\n\","
+        "sizeof(struct strom_col_qual), offsetof(struct strom_col_qual, consts),"
+        "offsetof(struct strom_col_qual, offs_bytes), sizeof(struct strom_qual_batch),"
+        "STROM_COL_I8, STROM_COL_U64, STROM_COL_BOOL, STROM_COL_STR32, STROM_COL_STR64,"
+        "STROM_QOP_RANGES, STROM_QOP_LUT, STROM_QOP_VALID, STROM_QUAL_NAN);return 0;}\n")
+    exe = tmp_path / "qual"
+    inc = os.path.join(ROOT, "csrc", "include")
+    subprocess.run(["gcc", "-std=c11", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    want = [C.sizeof(CP.ColQual), CP.ColQual.consts.offset, CP.ColQual.offs_bytes.offset,
+            8 * CP.QUAL_BATCH_FIELDS, CP.COL_CODE["i1"], CP.COL_CODE["u8"], CP.COL_CODE["b1"],
+            CP.COL_STR32, CP.COL_STR64, CP.QOP_RANGES, CP.QOP_LUT, CP.QOP_VALID, CP.FLAG_NAN]
+    assert got == want

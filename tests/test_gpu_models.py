@@ -223,3 +223,53 @@ def test_heap_scan_vm_routing_matches_cpu(S, tmp_path):
     assert g.nr_checked == nchecked and g.bad_pages == 0
     c = pg_scan.cpu_scan(rel, cfg)
     assert np.array_equal(g.items, c.items)
+
+
+@pytest.mark.parametrize("codec", [None, "lz4", "zstd"])
+def test_arrow_scan_predicate_kinds(S, tmp_path, codec):
+    """Every predicate kind on every column kind (tests/arrowgen.py) through
+    the GPU qualifier kernel: row ids == pc.filter of pyarrow.compute's mask,
+    and == the host twin; qualifier lists (CNF with OR clauses) with a
+    timestamp / dictionary projection."""
+    pytest.importorskip("pyarrow")
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from arrowgen import cases, cnf_cases, expected_ids, table, write
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+    tbl = table(6000, seed=11)
+    path = str(tmp_path / f"p_{codec}.arrow")
+    write(path, tbl, codec, batch_rows=1000)
+    sc = ArrowScan(path, "cuda", chunk_sz=64 << 10, slot_bytes=1 << 20)
+    try:
+        bad = []
+        for label, pred, ref in cases():
+            got = sc.scan_where([pred]).indices.cpu().numpy()
+            want = expected_ids(tbl, ref)
+            if not np.array_equal(got, want):
+                bad.append((label, len(got), len(want)))
+        assert not bad, bad
+        for label, quals, ref in cnf_cases():
+            out = sc.scan_where(quals, project="ts")
+            want = expected_ids(tbl, ref)
+            assert np.array_equal(out.indices.cpu().numpy(), want), label
+            ts = tbl.column("ts").combine_chunks()
+            ok = np.asarray(ts.is_valid())[want]
+            assert np.array_equal(out.valid.cpu().numpy().astype(bool), ok)
+            ref_v = np.asarray(ts.cast("int64").fill_null(0))[want]
+            assert np.array_equal(out.values.cpu().numpy()[ok], ref_v[ok])
+            assert out.column.kind == "timestamp" and out.column.unit == "us"
+        from nvme_strom_amd.ops.colpred import P
+        out = sc.scan_where([P("i8") > 60], project="dict")
+        d = tbl.column("dict").combine_chunks()
+        ids = out.indices.cpu().numpy()
+        ok = np.asarray(d.is_valid())[ids]
+        assert np.array_equal(out.values.cpu().numpy()[ok],
+                              np.asarray(d.indices.fill_null(0))[ids][ok])
+        offs, chars = out.dictionary[0]
+        assert [chars[offs[i]:offs[i + 1]].tobytes().decode() for i in range(len(offs) - 1)] == \
+            d.dictionary.to_pylist()
+        host = sc.host_scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
+        assert np.array_equal(sc.scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
+                              .indices.cpu().numpy(), host.indices)
+    finally:
+        sc.close()

@@ -110,7 +110,7 @@ def test_arrow_ipc_metadata(tmp_path):
         assert m == read_metadata(path, native=False)
         assert m == read_metadata(open(path, "rb").read())
         assert [c.name for c in m.schema] == ["s", "a", "f", "l"]
-        assert [c.supported for c in m.schema] == [False, True, True, False]
+        assert [c.supported for c in m.schema] == [True, True, True, False]
         assert m.schema[2].numpy_dtype == "f4"
         assert len(m.batches) == 4 and all(b.length == 2500 for b in m.batches)
         assert m.batches[0].codec == (None if comp is None else "lz4_frame")
@@ -247,7 +247,7 @@ def test_arrow_scan_plans_zstd_and_refuses_mixed(tmp_path):
     sc = ArrowScan(path, "cpu")
     batches, dtypes, rows = sc._plan(["a"])
     assert sc._codec == D.ARROW_ZSTD and rows == 50_000 and len(batches) == 4
-    assert all(d.compressed for b in batches for d, _ in b.cols)
+    assert all(d.compressed for b in batches for d, *_ in b.cols)
     mixed = str(tmp_path / "m.arrow")
     with ipc.new_file(mixed, tbl.schema, options=ipc.IpcWriteOptions(compression="zstd")) as w:
         w.write_batch(tbl.slice(0, 100).to_batches()[0])
