@@ -121,7 +121,7 @@ for phase in "$@"; do
     pg) step pg 400 python -u -m nvme_strom_amd.tools.pg_bench --out "$OUT/pg.json" ;;
     stripe) step stripe 400 python -u -m nvme_strom_amd.tools.stripe_bench --out "$OUT/stripe.json" ;;
     ceiling) step ceiling 400 python -u -m nvme_strom_amd.tools.ceiling_bench --out "$OUT/ceiling.json" ;;
-    arrow) step arrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
+    arrow) step arrow 700 python -u -m nvme_strom_amd.tools.arrow_bench --out "$OUT/arrow.json" ;;
     *) echo "unknown phase $phase"; exit 2 ;;
   esac
 done
