@@ -42,7 +42,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <atomic>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -1025,6 +1027,18 @@ HD SeqEnt ld_ent(const SeqEnt *tab, uint32_t off) {   // off: state x 8
 // lane of the wave on the same values (wave-uniform: scalar registers and
 // scalar branches, no exec-mask juggling around a one-lane loop); lane 0
 // stores.
+//
+// SYM: a block decoded ahead of its predecessors (the frame-parallel
+// decoder, run_fp): the repeat offsets it starts from are not known yet,
+// so they start as symbols — kSym | index << 26 | k meaning "incoming
+// repeat offset `index`, minus k" (RFC 8878 3.1.2.5: the only arithmetic on
+// a repeat offset is the LL = 0, code 3 "first repeat minus one") — and
+// resolve when the block executes (exec_fp).  Offsets are then checked
+// against the output there, not here; a new offset >= kPosMax is an error
+// at once (it would read as a symbol).
+HD bool is_sym(uint32_t off) { return off >= kPosMax; }
+
+template <bool SYM = false>
 HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t left = s.nseq - s.seq_done;
   const uint32_t m = left < SEQN ? left : SEQN;
@@ -1071,14 +1085,15 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
       const uint32_t rep01 = k == 1 ? r1 : r0;
       const uint32_t rep012 = k == 2 ? r2 : rep01;
-      const uint32_t rep = k == 3 ? r0 - 1 : rep012;
+      const uint32_t rep = k == 3 ? (SYM && is_sym(r0) ? r0 + 1 : r0 - 1) : rep012;
       off = isnew ? ofv - 3 : rep;
+      if (SYM) bad_dist |= isnew && is_sym(off);
       const bool shift2 = isnew || k >= 2;
       r2 = shift2 ? r1 : r2;
       r1 = r0;                             // k >= 1 or new here
       r0 = off;
     }
-    bad_dist |= off - 1 >= pos0 + out + ll;  // off == 0 wraps
+    if (!SYM) bad_dist |= off - 1 >= pos0 + out + ll;  // off == 0 wraps
     // lane 0 stores (the CPU runs the phase once, HostTeam::uni, as t = 0)
     if (t == 0) {
       s.sll[n] = ll;
@@ -1111,7 +1126,7 @@ HD void seq_chunk(Smem &s, const Ctx &c, uint32_t t) {
       ++n;
     }
   }
-  if (!err && (uint64_t)s.op + out > c.cap) err = kErrOverflow;
+  if (!SYM && !err && (uint64_t)s.op + out > c.cap) err = kErrOverflow;
   if (w0) {
     s.seq_done += m;
     s.ost[n] = out;
@@ -1300,6 +1315,117 @@ HD void verify_frame(TM &tm, Smem &s, const Ctx &c) {
   tm.sync();
 }
 
+// (3) one chunk's entries, executed: batches of OB output bytes
+template <class TM>
+HD void exec_chunk(TM &tm, Smem &s, const Ctx &c) {
+  const uint32_t total = s.ctot;
+  for (uint32_t b0 = 0; b0 < total; b0 += OB) {
+    const uint32_t nb = total - b0 < OB ? total - b0 : OB;
+    tm.count(kZpNBatch);
+    tm.each([&](uint32_t t) { ex_fill(s, t, b0, nb); });
+    tm.sync();
+    tm.mark(kZpFill);
+    while (tm.any([&](uint32_t t) { return ex_double(s, t, nb); })) {
+      tm.count(kZpNDouble);
+    }
+    tm.mark(kZpDouble);
+    tm.each([&](uint32_t t) { ex_write(s, c, t, b0, nb); });
+    tm.fence();
+    tm.sync();
+    tm.mark(kZpWrite);
+  }
+}
+
+// (1) a compressed block's literal section: header, then the Huffman
+// rounds into the scratch slot (or, for a literals-only block, into the
+// output).  False when the block is done (literals-only) or failed.
+template <class TM>
+HD bool block_literals(TM &tm, Smem &s, const Ctx &c, bool allow_direct) {
+  tm.one([&] {
+    if (!lit_header(s, c)) s.err = ZF(kErrFormat);
+    if (!allow_direct) s.lit_direct = 0;
+  });
+  tm.sync();
+  tm.mark(kZpHdr);
+  if (s.err) return false;
+  if (s.lit_kind == kLitScratch) {
+    for (;;) {
+      tm.each([&](uint32_t t) {
+        if (t < s.nls) s.lwlo[t] = win_lo(s.lbr[t], LWIN);
+      });
+      tm.sync();
+      tm.each([&](uint32_t t) { lit_load(s, c, t); });
+      tm.sync();
+      tm.mark(kZpLitLoad);
+      tm.count(kZpNLitRound);
+      tm.each([&](uint32_t t) {
+        if (t < s.nls) lit_chunk(s, c, t);
+      });
+      tm.sync();
+      tm.each([&](uint32_t t) { lit_flush(s, c, t); });
+      tm.sync();
+      tm.each([&](uint32_t t) {
+        if (t < s.nls) s.lout[t] += s.lrn[t];
+      });
+      tm.sync();
+      tm.mark(kZpLitDec);
+      if (s.err || !(s.lcnt[0] | s.lcnt[1] | s.lcnt[2] | s.lcnt[3])) break;
+    }
+    tm.fence();
+    tm.sync();
+    if (s.err) return false;
+    if (s.lit_direct) {
+      tm.one([&] {
+        if (!seq_header(s, c)) s.err = ZF(kErrFormat);   // the 0 sequences byte
+        s.op += s.lit_n;
+      });
+      tm.sync();
+      return false;
+    }
+  }
+  return true;
+}
+
+// One block after next_block() found it, decoded and executed in place
+// (the serial path, and block 0 of a frame-parallel group): s.op advances
+// by its output; end_block() is the caller's.
+template <class TM>
+HD void block_body(TM &tm, Smem &s, const Ctx &c) {
+  if (s.btype != kComp) {
+    tm.each([&](uint32_t t) { copy_block(s, c, t); });
+    tm.fence();
+    tm.sync();
+    tm.one([&] { s.op += s.bsize; });
+    tm.sync();
+    tm.mark(kZpCopy);
+    return;
+  }
+  if (!block_literals(tm, s, c, true)) return;
+  tm.one([&] {
+    if (!seq_header(s, c)) s.err = ZF(kErrFormat);
+  });
+  tm.sync();
+  tm.mark(kZpHdr);
+  if (s.err) return;
+  do {
+    tm.one([&] { s.swlo = win_lo(s.sbr, SWIN); });
+    tm.sync();
+    if (s.nseq) {
+      tm.each([&](uint32_t t) { seq_load(s, c, t); });
+      tm.sync();
+    }
+    tm.mark(kZpSeqLoad);
+    tm.count(kZpNChunk);
+    tm.uni([&](uint32_t t) { seq_chunk(s, c, t); });
+    tm.sync();
+    tm.mark(kZpSeqDec);
+    if (s.err) return;
+    exec_chunk(tm, s, c);
+    tm.one([&] { s.op += s.ctot; });
+    tm.sync();
+  } while (s.seq_done < s.nseq);
+}
+
 template <class TM>
 HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
   tm.one([&] { stream_init(s, c, codec); });
@@ -1309,100 +1435,7 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
     tm.sync();
     tm.mark(kZpHdr);
     if (s.err || s.state == kDone) break;
-    if (s.btype != kComp) {
-      tm.each([&](uint32_t t) { copy_block(s, c, t); });
-      tm.fence();
-      tm.sync();
-      tm.one([&] {
-        s.op += s.bsize;
-        end_block(s, c);
-      });
-      tm.sync();
-      tm.mark(kZpCopy);
-      if (s.ck_need && !s.err) verify_frame(tm, s, c);
-      continue;
-    }
-    tm.one([&] {
-      if (!lit_header(s, c)) s.err = ZF(kErrFormat);
-    });
-    tm.sync();
-    tm.mark(kZpHdr);
-    if (s.err) break;
-    if (s.lit_kind == kLitScratch) {
-      for (;;) {
-        tm.each([&](uint32_t t) {
-          if (t < s.nls) s.lwlo[t] = win_lo(s.lbr[t], LWIN);
-        });
-        tm.sync();
-        tm.each([&](uint32_t t) { lit_load(s, c, t); });
-        tm.sync();
-        tm.mark(kZpLitLoad);
-        tm.count(kZpNLitRound);
-        tm.each([&](uint32_t t) {
-          if (t < s.nls) lit_chunk(s, c, t);
-        });
-        tm.sync();
-        tm.each([&](uint32_t t) { lit_flush(s, c, t); });
-        tm.sync();
-        tm.each([&](uint32_t t) {
-          if (t < s.nls) s.lout[t] += s.lrn[t];
-        });
-        tm.sync();
-        tm.mark(kZpLitDec);
-        if (s.err || !(s.lcnt[0] | s.lcnt[1] | s.lcnt[2] | s.lcnt[3])) break;
-      }
-      tm.fence();
-      tm.sync();
-      if (s.err) break;
-      if (s.lit_direct) {
-        tm.one([&] {
-          if (!seq_header(s, c)) s.err = ZF(kErrFormat);   // the 0 sequences byte
-          s.op += s.lit_n;
-          end_block(s, c);
-        });
-        tm.sync();
-        if (s.ck_need && !s.err) verify_frame(tm, s, c);
-        continue;
-      }
-    }
-    tm.one([&] {
-      if (!seq_header(s, c)) s.err = ZF(kErrFormat);
-    });
-    tm.sync();
-    tm.mark(kZpHdr);
-    if (s.err) break;
-    do {
-      tm.one([&] { s.swlo = win_lo(s.sbr, SWIN); });
-      tm.sync();
-      if (s.nseq) {
-        tm.each([&](uint32_t t) { seq_load(s, c, t); });
-        tm.sync();
-      }
-      tm.mark(kZpSeqLoad);
-      tm.count(kZpNChunk);
-      tm.uni([&](uint32_t t) { seq_chunk(s, c, t); });
-      tm.sync();
-      tm.mark(kZpSeqDec);
-      if (s.err) break;
-      const uint32_t total = s.ctot;
-      for (uint32_t b0 = 0; b0 < total; b0 += OB) {
-        const uint32_t nb = total - b0 < OB ? total - b0 : OB;
-        tm.count(kZpNBatch);
-        tm.each([&](uint32_t t) { ex_fill(s, t, b0, nb); });
-        tm.sync();
-        tm.mark(kZpFill);
-        while (tm.any([&](uint32_t t) { return ex_double(s, t, nb); })) {
-          tm.count(kZpNDouble);
-        }
-        tm.mark(kZpDouble);
-        tm.each([&](uint32_t t) { ex_write(s, c, t, b0, nb); });
-        tm.fence();
-        tm.sync();
-        tm.mark(kZpWrite);
-      }
-      tm.one([&] { s.op += total; });
-      tm.sync();
-    } while (s.seq_done < s.nseq);
+    block_body(tm, s, c);
     if (s.err) break;
     tm.one([&] { end_block(s, c); });
     tm.sync();
@@ -1412,6 +1445,363 @@ HD void run(TM &tm, Smem &s, const Ctx &c, int codec) {
     if (!s.err && s.expect >= 0 && (int64_t)s.op != s.expect) s.err = ZF(kErrFormat);
   });
   tm.sync();
+}
+
+// ------------------------------------------------------------- frame-parallel
+// The blocks of a frame decode on different waves of one workgroup (NW
+// waves per stream).  A compressed block's entropy stages — literal
+// Huffman streams, FSE tables and the sequence bitstream — depend only on
+// its own bytes, except for the frame's repeat offsets, a treeless
+// literal section (the previous Huffman tree) and a repeat-mode FSE table
+// (the previous definition).  So, per group of up to NW blocks:
+//   prewalk   wave 0, one lane: the group's block headers, and whether any
+//             block needs a previous block's tree or table (then the
+//             group runs serially on wave 0 instead);
+//   decode    wave 0 decodes and executes block 0 in place; wave w > 0
+//             decodes block w's literals into its own scratch slot and its
+//             sequences (repeat offsets symbolic, seq_chunk<true>) into its
+//             own entry buffer in HBM;
+//   execute   waves 1.. in block order: the entries come back chunk by
+//             chunk, symbolic offsets resolve against the repeat offsets
+//             the previous block ended with, every offset is checked
+//             against the output written so far, and the chunk executes
+//             as in the serial path (history of earlier blocks is in the
+//             output, written before the workgroup barrier that ordered
+//             the executions).
+// Wave 0's Smem holds the frame (op, repeat offsets, table definitions for
+// later treeless / repeat-mode blocks).  The same code runs on the CPU,
+// wave after wave (strom_zstd_host_fp), as the algorithm's reference.
+constexpr uint32_t NWMAX = 8;
+constexpr uint32_t kMaxSeq = MAXB / 3;          // a sequence outputs >= 3 bytes
+constexpr uint32_t kMaxEnt = kMaxSeq + 2;       // + the trailing literals
+constexpr uint32_t kSym = 0xC0000000u;
+
+struct alignas(16) Ent {                        // a decoded sequence (HBM)
+  uint32_t ll, off, lst, ost;                   // ost: output start in the block
+};
+
+struct FpBlk {
+  uint32_t bstart, bend, btype, bsize, blast;
+};
+
+struct FpShared {
+  FpBlk blk[NWMAX];
+  uint32_t nblk, serial, nent[NWMAX], bout[NWMAX];
+};
+
+HD uint32_t sym_resolve(uint32_t v, const uint32_t *rin) {
+  if (!is_sym(v)) return v;
+  const uint32_t idx = (v >> 26) & 15;
+  // selects, not an index: a dynamically indexed array lives in private memory
+  const uint32_t r = idx == 0 ? rin[0] : idx == 1 ? rin[1] : rin[2];
+  return idx < 3 ? r - (v & 0x3FFFFFFu) : 0u;   // 0: rejected by the distance check
+}
+
+// lane 0 of wave 0: the next up to nw block headers of the current frame
+// (parsing the frame header first when one starts).  serial = 1 when a
+// block needs a predecessor's tree / table, or the stream is stored.
+HD void prewalk(Smem &s, const Ctx &c, FpShared &f, uint32_t nw) {
+  f.nblk = 0;
+  f.serial = 0;
+  for (uint32_t k = 0; k < nw; ++k) {
+    next_block(s, c);
+    if (s.err || s.state == kDone) break;
+    FpBlk &b = f.blk[k];
+    b.bstart = s.bstart;
+    b.bend = s.bend;
+    b.btype = s.btype;
+    b.bsize = s.bsize;
+    b.blast = s.blast;
+    if (s.btype == kComp) {
+      // literal section type + size, then the sequence modes byte
+      const uint32_t p = s.bstart, b0 = gbyte(c, p), lt = b0 & 3, sf = (b0 >> 2) & 3;
+      uint32_t q;
+      if (lt <= 1) {
+        const uint32_t hl = (sf & 1) == 0 ? 1 : sf == 1 ? 2 : 3;
+        const uint32_t R = hl == 1 ? b0 >> 3 : hl == 2 ? (b0 >> 4) + (gbyte(c, p + 1) << 4)
+                                   : (b0 >> 4) + (gbyte(c, p + 1) << 4) + (gbyte(c, p + 2) << 12);
+        q = p + hl + (lt == 0 ? R : 1);
+      } else {
+        const uint32_t hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5, bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
+        uint64_t h = 0;
+        for (uint32_t j = 0; j < hl; ++j) h |= (uint64_t)gbyte(c, p + j) << (8 * j);
+        q = p + hl + ((uint32_t)(h >> (4 + bits)) & ((1u << bits) - 1));
+      }
+      bool dep = lt == 3;                          // treeless literals
+      const uint32_t n0 = gbyte(c, q);
+      const uint32_t mpos = q + (n0 < 128 ? 1 : n0 < 255 ? 2 : 3);
+      if (n0 && q < s.bend) {
+        const uint32_t modes = gbyte(c, mpos);
+        dep |= (modes >> 6) == 3 || ((modes >> 4) & 3) == 3 || ((modes >> 2) & 3) == 3;
+      }
+      // a block that needs a predecessor's tree / table starts the next
+      // group (as its first block, on wave 0, which holds the definitions)
+      if (dep && k) {
+        f.nblk = k;
+        break;
+      }
+    }
+    f.nblk = k + 1;
+    if (s.blast) break;
+    s.ip = s.bend;                                 // the next block header
+  }
+  if (!f.nblk || s.err) return;
+  // wave 0 decodes the first block from its header fields; the frame's
+  // header (fstart, repeat offsets, ...) was parsed here once
+  const FpBlk &b = f.blk[0];
+  s.bstart = b.bstart;
+  s.bend = b.bend;
+  s.btype = b.btype;
+  s.bsize = b.bsize;
+  s.blast = b.blast;
+  s.ip = b.bstart;
+  s.state = kBlock;
+  if (f.nblk == 1) f.serial = 1;                   // nothing to overlap
+}
+
+// wave w > 0: decode block f.blk[w] — literals into its slot, sequences
+// into its entry buffer (HBM), repeat offsets symbolic
+template <class TM>
+HD void decode_fp(TM &tm, Smem &s, const Smem &s0, const Ctx &c, const FpBlk &b, Ent *ent,
+                  uint32_t &nent, uint32_t &bout) {
+  tm.one([&] {
+    s.err = 0;
+    s.bstart = b.bstart;
+    s.bend = b.bend;
+    s.btype = b.btype;
+    s.bsize = b.bsize;
+    s.blast = b.blast;
+    s.ip = b.bstart;
+    s.op = 0;                                      // block-relative until it executes
+    s.fstart = 0;
+    s.hbits = 0;
+    s.have_ll = s.have_of = s.have_ml = 0;
+    s.rep[0] = kSym | (0u << 26);
+    s.rep[1] = kSym | (1u << 26);
+    s.rep[2] = kSym | (2u << 26);
+    s.nseq = 0;
+    s.seq_done = 0;
+  });
+  tm.sync();
+  nent = 0;
+  bout = 0;
+  if (b.btype != kComp) {
+    bout = b.bsize;
+    return;
+  }
+  if (!block_literals(tm, s, c, false)) return;   // never literals-direct here
+  tm.one([&] {
+    if (!seq_header(s, c) || s.nseq > kMaxSeq) s.err = ZF(kErrFormat);
+  });
+  tm.sync();
+  if (s.err) return;
+  uint32_t n = 0, out = 0;
+  do {
+    tm.one([&] { s.swlo = win_lo(s.sbr, SWIN); });
+    tm.sync();
+    if (s.nseq) {
+      tm.each([&](uint32_t t) { seq_load(s, c, t); });
+      tm.sync();
+    }
+    tm.uni([&](uint32_t t) { seq_chunk<true>(s, c, t); });
+    tm.sync();
+    if (s.err) return;
+    if (n + s.cn > kMaxEnt) {
+      tm.one([&] { s.err = ZF(kErrFormat); });
+      tm.sync();
+      return;
+    }
+    const uint32_t cn = s.cn, n0 = n, o0 = out;
+    tm.each([&](uint32_t t) {
+      for (uint32_t i = t; i < cn; i += NT) {
+        Ent e;
+        e.ll = s.sll[i];
+        e.off = s.soff[i];
+        e.lst = s.lst[i];
+        e.ost = o0 + s.ost[i];
+        ent[n0 + i] = e;
+      }
+    });
+    n += cn;
+    out += s.ctot;
+    tm.sync();
+  } while (s.seq_done < s.nseq);
+  tm.fence();
+  tm.sync();
+  nent = n;
+  bout = out;
+  (void)s0;
+}
+
+// wave w > 0, in block order: execute block w at the frame's output
+// position, resolving its symbolic repeat offsets; the frame state in s0
+// (wave 0's Smem) advances
+template <class TM>
+HD void exec_fp(TM &tm, Smem &s, Smem &s0, const Ctx &c, const Ent *ent, uint32_t nent,
+                uint32_t bout) {
+  tm.one([&] {
+    s.op = s0.op;
+    if ((uint64_t)s0.op + bout > c.cap) s.err = kErrOverflow;
+  });
+  tm.sync();
+  if (s.err) return;
+  if (s.btype != kComp) {
+    tm.each([&](uint32_t t) { copy_block(s, c, t); });
+  } else if (s.nseq == 0 && s.lit_kind == kLitScratch) {
+    // literals-only: the slot is the block's output
+    tm.each([&](uint32_t t) {
+      for (uint32_t i = t; i < s.lit_n; i += NT) c.out[s.op + i] = ld_stored(c.lit, i);
+    });
+  } else {
+    const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
+    const uint32_t fpos = s0.op - s0.fstart;     // frame output before the block
+    for (uint32_t i0 = 0; i0 < nent; i0 += SEQN) {
+      const uint32_t m = nent - i0 < SEQN ? nent - i0 : SEQN;
+      const uint32_t base = ent[i0].ost;
+      tm.each([&](uint32_t t) {
+        bool bad = false;
+        for (uint32_t i = t; i < m; i += NT) {
+          const Ent e = ent[i0 + i];
+          const uint32_t off = sym_resolve(e.off, rin);
+          // the serial path's check (seq_chunk): a match reaches back at
+          // most to the frame start; the trailing-literals entry has no match
+          const bool has_match = (i0 + i + 1 < nent ? ent[i0 + i + 1].ost : bout) - e.ost > e.ll;
+          bad |= has_match && off - 1 >= fpos + e.ost + e.ll;
+          s.sll[i] = e.ll;
+          s.soff[i] = off;
+          s.lst[i] = e.lst;
+          s.ost[i] = e.ost - base;
+        }
+        if (t == 0) {
+          const uint32_t end = i0 + m < nent ? ent[i0 + m].ost : bout;
+          s.ost[m] = end - base;
+          s.cn = m;
+          s.ctot = end - base;
+        }
+        if (bad) s.err = ZF(kErrDistance);
+      });
+      tm.sync();
+      if (s.err) return;
+      exec_chunk(tm, s, c);
+      tm.one([&] { s.op += s.ctot; });
+      tm.sync();
+    }
+  }
+  tm.fence();
+  tm.sync();
+  tm.one([&] {
+    s0.op += bout;
+    if (s.btype == kComp && s.nseq) {
+      const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
+      s0.rep[0] = sym_resolve(s.rep[0], rin);
+      s0.rep[1] = sym_resolve(s.rep[1], rin);
+      s0.rep[2] = sym_resolve(s.rep[2], rin);
+    }
+  });
+  tm.sync();
+}
+
+// wave 0 after a parallel group: the later blocks' Huffman tree and FSE
+// table definitions become the frame's (a treeless / repeat-mode block of
+// a later group starts that group, on wave 0)
+HD void inherit_defs(Smem &s0, const Smem &s) {
+  if (s.btype != kComp) return;
+  if (s.hbits && s.lit_kind == kLitScratch) {
+    s0.hdesc = s.hdesc;
+    s0.hdesc_end = s.hdesc_end;
+    s0.hbits = s.hbits;
+  }
+  if (s.nseq) {
+    for (uint32_t k = 0; k < 3; ++k) {
+      s0.tmode[k] = s.tmode[k];
+      s0.tpos[k] = s.tpos[k];
+      s0.tend[k] = s.tend[k];
+    }
+    s0.have_ll = s0.have_of = s0.have_ml = 1;
+  }
+}
+
+// G: a workgroup of NW wave teams (DevGroup) or their CPU emulation
+// (HostGroup: the waves one after another — their decodes are independent)
+// per-wave views of a workgroup's frame-parallel scratch (computed, not
+// kept in arrays indexed by the wave: those would live in private memory)
+struct FpCtx {
+  Ctx c;                     // lit: wave 0's slot
+  uint8_t *scr;              // fp_scratch(nw) bytes
+  uint32_t nw;
+  HD Ctx wave(uint32_t w) const {
+    return Ctx{c.in, c.out, scr + (size_t)w * SLOT, c.len, c.cap};
+  }
+  HD Ent *ent(uint32_t w) const {
+    return (Ent *)(scr + (size_t)nw * SLOT + (size_t)(w - 1) * kMaxEnt * sizeof(Ent));
+  }
+};
+
+template <class G>
+HD void run_fp(G &g, Smem *sm, FpShared &f, const FpCtx &x, int codec) {
+  Smem &s0 = sm[0];
+  const uint32_t nw = x.nw;
+  const Ctx c0 = x.wave(0);
+  g.wave(0, [&](auto &tm) {
+    tm.one([&] { stream_init(s0, c0, codec); });
+    tm.sync();
+  });
+  g.sync_all();
+  while (!s0.err) {
+    g.wave(0, [&](auto &tm) {
+      tm.one([&] { prewalk(s0, c0, f, nw); });
+      tm.sync();
+    });
+    g.sync_all();
+    if (s0.err || !f.nblk) break;
+    const uint32_t nb = f.serial ? 1 : f.nblk;
+    g.count_group(nb);
+    g.waves(nb, [&](uint32_t w, auto &tm) {
+      if (w == 0) block_body(tm, s0, c0);
+      else decode_fp(tm, sm[w], s0, x.wave(w), f.blk[w], x.ent(w), f.nent[w], f.bout[w]);
+    });
+    g.sync_all();
+    for (uint32_t w = 1; w < nb; ++w) {
+      if (s0.err) break;
+      g.wave(0, [&](auto &tm) {
+        tm.one([&] {
+          if (sm[w].err) s0.err = sm[w].err;
+        });
+        tm.sync();
+      });
+      g.sync_all();
+      if (s0.err) break;
+      g.wave(w, [&](auto &tm) { exec_fp(tm, sm[w], s0, x.wave(w), x.ent(w), f.nent[w], f.bout[w]); });
+      g.sync_all();
+      g.wave(0, [&](auto &tm) {
+        tm.one([&] {
+          if (sm[w].err) s0.err = sm[w].err;
+        });
+        tm.sync();
+      });
+      g.sync_all();
+    }
+    if (s0.err) break;
+    g.wave(0, [&](auto &tm) {
+      tm.one([&] {
+        for (uint32_t w = 1; w < nb; ++w) inherit_defs(s0, sm[w]);
+        const FpBlk &l = f.blk[nb - 1];
+        s0.bend = l.bend;
+        s0.blast = l.blast;
+        end_block(s0, c0);
+      });
+      tm.sync();
+      if (s0.ck_need && !s0.err) verify_frame(tm, s0, c0);
+    });
+    g.sync_all();
+  }
+  g.wave(0, [&](auto &tm) {
+    tm.one([&] {
+      if (!s0.err && s0.expect >= 0 && (int64_t)s0.op != s0.expect) s0.err = ZF(kErrFormat);
+    });
+    tm.sync();
+  });
+  g.sync_all();
 }
 
 #define DI __device__ inline __attribute__((always_inline))
@@ -1474,6 +1864,105 @@ struct HostTeam {
     return v;
   }
 };
+
+// One wave of a multi-wave workgroup as a team (the frame-parallel
+// decoder): its own barrier is a wave barrier with LDS / memory ordering
+// at wavefront scope (a wave's LDS operations complete in order); stores
+// another wave reads are ordered by the workgroup fence + barrier of
+// DevGroup::sync_all.
+struct WaveTeam {
+  DI uint32_t lane() const { return threadIdx.x & (NT - 1); }
+  DI void mark(int) {}
+  DI void count(int) {}
+  DI void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  DI void fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
+  template <class F>
+  DI void each(F f) { f(lane()); }
+  template <class F>
+  DI void one(F f) {
+    if (lane() == 0) f();
+  }
+  template <class F>
+  DI void uni(F f) { f(lane()); }
+  template <class F>
+  DI bool any(F f) {
+    const bool v = f(lane());
+    sync();
+    return __ballot(v) != 0;
+  }
+};
+
+struct DevGroup {
+  WaveTeam tm;
+  DI uint32_t wid() const { return threadIdx.x / NT; }
+  template <class F>
+  DI void wave(uint32_t k, F f) {
+    if (wid() == k) f(tm);
+  }
+  template <class F>
+  DI void waves(uint32_t n, F f) {
+    if (wid() < n) f(wid(), tm);
+  }
+  DI void sync_all() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  DI void count_group(uint32_t) {}
+};
+
+struct HostGroup {
+  HostTeam tm;
+  template <class F>
+  void wave(uint32_t, F f) { f(tm); }
+  template <class F>
+  void waves(uint32_t n, F f) {
+    for (uint32_t w = 0; w < n; ++w) f(w, tm);
+  }
+  void sync_all() {}
+  uint32_t groups = 0, blocks_par = 0;   // groups, and blocks decoded ahead of their turn
+  void count_group(uint32_t nb) {
+    ++groups;
+    blocks_par += nb - 1;
+  }
+};
+
+// frame-parallel scratch per workgroup: NW literal slots, then NW - 1
+// entry buffers
+HD constexpr size_t fp_scratch(uint32_t nw) {
+  return (size_t)nw * SLOT + (size_t)(nw - 1) * kMaxEnt * sizeof(Ent);
+}
+
+#ifndef ZS_FPW
+#define ZS_FPW 4
+#endif
+#ifndef ZS_FP_ROUNDS
+#define ZS_FP_ROUNDS 1
+#endif
+constexpr uint32_t FPW = ZS_FPW;                 // waves (blocks in flight) per stream
+static_assert(FPW >= 2 && FPW <= NWMAX, "frame-parallel waves");
+
+__global__ void __launch_bounds__(NT * FPW) __attribute__((amdgpu_waves_per_eu(2))) zstd_fp_kernel(int codec, const uint8_t *src,
+                                                          uint8_t *dst,
+                                                          const strom_decomp_desc *desc,
+                                                          uint32_t n, int32_t *status,
+                                                          uint8_t *scratch) {
+  __shared__ Smem sm[FPW];
+  __shared__ FpShared f;
+  DevGroup g;
+  uint8_t *base = scratch + (size_t)blockIdx.x * fp_scratch(FPW);
+  for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const strom_decomp_desc d = desc[b];
+    const FpCtx x{Ctx{src + d.src_off, dst + d.dst_off, base, d.src_len, d.dst_len}, base, FPW};
+    run_fp(g, sm, f, x, codec);
+    if (threadIdx.x == 0) status[b] = sm[0].err ? sm[0].err : (int32_t)sm[0].op;
+    __syncthreads();
+  }
+}
 
 // 3 waves per SIMD (<= 168 VGPRs): with the phase-shared LDS, up to 12
 // streams per CU
@@ -1542,21 +2031,51 @@ uint8_t *scratch_for(void *stream, size_t bytes) {
   return e.p;
 }
 
-uint32_t resident_groups() {
+uint32_t cu_count() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   static int cached[64] = {0};
-  if (dev >= 0 && dev < 64 && cached[dev]) {
-    cus = cached[dev];
-  } else {
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    if (dev >= 0 && dev < 64) cached[dev] = cus;
-  }
+  if (dev >= 0 && dev < 64 && cached[dev]) return (uint32_t)cached[dev];
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  if (dev >= 0 && dev < 64) cached[dev] = cus;
+  return (uint32_t)cus;
+}
+
+uint32_t resident_groups() {
   uint32_t per_cu = (160u << 10) / (uint32_t)sizeof(Smem);   // LDS-bound residency
   if (per_cu > 12) per_cu = 12;                                // 3 waves per SIMD
-  return (uint32_t)cus * (per_cu ? per_cu : 1);
+  return cu_count() * (per_cu ? per_cu : 1);
+}
+
+// frame-parallel workgroups resident per CU (LDS-bound: FPW Smem each)
+uint32_t fp_per_cu() {
+  const uint32_t per = (160u << 10) / (uint32_t)(FPW * sizeof(Smem) + sizeof(FpShared));
+  return per ? per : 1;
+}
+
+// Decoder choice: the frame-parallel kernel when the streams are too few to
+// fill the wave-per-stream decoder's resident round — a stream then takes
+// the time of its slowest block plus the executions, not of all its
+// blocks — else one wave per stream (more streams in flight per CU).
+// STROM_ZSTD_FP: 0 never, 1 always, unset/other: by the stream count.
+std::atomic<int> g_fp_mode{-2};
+
+int fp_mode() {
+  int m = g_fp_mode.load(std::memory_order_relaxed);
+  if (m == -2) {
+    const char *e = getenv("STROM_ZSTD_FP");
+    m = e && *e == '0' ? 0 : e && *e == '1' ? 1 : -1;
+    g_fp_mode.store(m, std::memory_order_relaxed);
+  }
+  return m;
+}
+
+bool use_fp(uint32_t nstreams) {
+  const int mode = fp_mode();
+  if (mode >= 0) return mode == 1;
+  return nstreams <= cu_count() * fp_per_cu() * ZS_FP_ROUNDS;
 }
 
 }  // namespace
@@ -1573,26 +2092,49 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
   using namespace zs;
   if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
   if (!nstreams) return 0;
-  const uint32_t res = resident_groups();
+  // a caller's scratch too small for one frame-parallel workgroup keeps
+  // the wave-per-stream decoder
+  const bool fp = use_fp(nstreams) && (!scratch || scratch_bytes >= fp_scratch(FPW));
+  const size_t per_wg = fp ? fp_scratch(FPW) : SLOT;
+  const uint32_t res = fp ? cu_count() * fp_per_cu() : resident_groups();
   uint32_t grid = nstreams < res ? nstreams : res;
   if (grid > 65535) grid = 65535;
   uint8_t *sc = (uint8_t *)scratch;
   std::unique_lock<std::mutex> g(g_mu, std::defer_lock);
   if (sc) {
-    const uint64_t slots = scratch_bytes / SLOT;
+    const uint64_t slots = scratch_bytes / per_wg;
     if (!slots) return -22;
     if (grid > slots) grid = (uint32_t)slots;
   } else {
     g.lock();                  // held through the launch (scratch_for)
-    sc = scratch_for(stream, (size_t)grid * SLOT);
+    sc = scratch_for(stream, (size_t)grid * per_wg);
     if (!sc) return -12;
   }
-  hipLaunchKernelGGL(zstd_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
-                     (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status, sc);
+  if (fp)
+    hipLaunchKernelGGL(zstd_fp_kernel, dim3(grid), dim3(NT * FPW), 0, (hipStream_t)stream, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status, sc);
+  else
+    hipLaunchKernelGGL(zstd_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
+                       (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status, sc);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
+
+// Decoder choice: -1 by the stream count (default), 0 wave per stream,
+// 1 frame-parallel.  Returns the previous setting.
+extern "C" int strom_zstd_fp_mode(int mode) {
+  const int prev = zs::fp_mode();
+  if (mode >= -1 && mode <= 1) zs::g_fp_mode.store(mode);
+  return prev;
+}
+
+// scratch bytes per workgroup of each decoder (callers passing their own
+// scratch size it for the grid): {wave-per-stream, frame-parallel}
+extern "C" void strom_zstd_scratch_sizes(uint64_t *out) {
+  out[0] = zs::SLOT;
+  out[1] = zs::fp_scratch(zs::FPW);
+}
 
 // Free the literal scratch kept per (device, stream) (128 KiB per resident
 // workgroup, up to ~290 MiB per stream, at most kScratchKeep streams):
@@ -1625,6 +2167,31 @@ extern "C" int strom_zstd_prof(uint64_t *out) {
 // The same phases lane by lane on the CPU: the algorithm's reference
 // (tests/test_codecs_cpu.py), no GPU involved.  Returns decoded bytes or a
 // negative error as the kernel's status.
+static thread_local uint32_t g_fp_host_stats[2];
+// groups and blocks decoded ahead by the last strom_zstd_host_fp call
+extern "C" void strom_zstd_host_fp_stats(uint32_t *out) {
+  out[0] = g_fp_host_stats[0];
+  out[1] = g_fp_host_stats[1];
+}
+
+// The frame-parallel decoder's phases on the CPU, waves one after another
+// (nw blocks per group, 2..NWMAX).
+extern "C" int strom_zstd_host_fp(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
+                                  uint32_t cap, uint32_t nw) {
+  using namespace zs;
+  if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  if (nw < 2 || nw > NWMAX) return -22;
+  std::unique_ptr<Smem[]> sm(new Smem[nw]());
+  std::unique_ptr<FpShared> f(new FpShared());
+  std::unique_ptr<uint8_t[]> sc(new uint8_t[fp_scratch(nw)]);
+  const FpCtx x{Ctx{src, dst, sc.get(), src_len, cap}, sc.get(), nw};
+  HostGroup g;
+  run_fp(g, sm.get(), *f, x, codec);
+  g_fp_host_stats[0] = g.groups;
+  g_fp_host_stats[1] = g.blocks_par;
+  return sm[0].err ? sm[0].err : (int32_t)sm[0].op;
+}
+
 extern "C" int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
                                uint32_t cap) {
   using namespace zs;

@@ -1,5 +1,6 @@
 // Mutation test of the zstd decoder's phases (csrc/kernels/zstd.hip, host
-// copy: strom_zstd_host), built host-only with ASan + UBSan
+// copies: strom_zstd_host, and strom_zstd_host_fp — the frame-parallel
+// decoder, 4 waves per stream), built host-only with ASan + UBSan
 // (make build/zstd_fuzz): every seed frame must decode to its reference
 // output, and random edits / truncations of it (byte flips, bit flips,
 // a cut tail) must end in a clean status, never an out-of-range access —
@@ -16,6 +17,8 @@
 
 extern "C" int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
                                uint32_t cap);
+extern "C" int strom_zstd_host_fp(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst,
+                                  uint32_t cap, uint32_t nw);
 
 static std::vector<uint8_t> slurp(const char *path) {
   std::vector<uint8_t> v;
@@ -47,6 +50,12 @@ int main(int argc, char **argv) {
       fprintf(stderr, "seed %s: status %d, want %u\n", argv[a], r, cap);
       return 1;
     }
+    memset(out.data(), 0, out.size());
+    r = strom_zstd_host_fp(7, z.data(), (uint32_t)z.size(), out.data(), cap, 4);
+    if (r != (int)cap || memcmp(out.data(), raw.data(), cap) != 0) {
+      fprintf(stderr, "seed %s (frame-parallel): status %d, want %u\n", argv[a], r, cap);
+      return 1;
+    }
     ++ok;
     for (int i = 0; i < iters; ++i) {
       std::vector<uint8_t> m = z;
@@ -64,9 +73,10 @@ int main(int argc, char **argv) {
       uint8_t *in = (uint8_t *)malloc(m.size() ? m.size() : 1);
       memcpy(in, m.data(), m.size());
       r = strom_zstd_host(7, in, (uint32_t)m.size(), out.data(), cap);
+      const int rf = strom_zstd_host_fp(7, in, (uint32_t)m.size(), out.data(), cap, 4);
       free(in);
-      if (r > (int)cap) {
-        fprintf(stderr, "status %d beyond the capacity %u\n", r, cap);
+      if (r > (int)cap || rf > (int)cap) {
+        fprintf(stderr, "status %d / %d beyond the capacity %u\n", r, rf, cap);
         return 1;
       }
       if (r < 0) ++rejected;

@@ -146,14 +146,19 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
     return n, (out[:n].tobytes() if n >= 0 else b""), stats
 
 
-def zstd_host(codec: int, data: bytes, cap: int):
+def zstd_host(codec: int, data: bytes, cap: int, fp: int = 0):
     """The zstd kernel's phases run lane by lane on the CPU
     (csrc/kernels/zstd.hip): -> (status, output bytes).  The reference for
     the GPU decoder; status = decoded bytes or <0 (-1 malformed,
-    -2 overflow, -3 distance, -4 unsupported: a dictionary)."""
+    -2 overflow, -3 distance, -4 unsupported: a dictionary).  ``fp`` = 2..8
+    runs the frame-parallel decoder's phases (that many blocks per group,
+    waves one after another)."""
     src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
     out = np.zeros(max(cap, 1), dtype=np.uint8)
-    n = N.lib().strom_zstd_host(codec, src.ctypes.data, len(data), out.ctypes.data, cap)
+    if fp:
+        n = N.lib().strom_zstd_host_fp(codec, src.ctypes.data, len(data), out.ctypes.data, cap, fp)
+    else:
+        n = N.lib().strom_zstd_host(codec, src.ctypes.data, len(data), out.ctypes.data, cap)
     return n, (out[:n].tobytes() if n >= 0 else b"")
 
 

@@ -92,6 +92,9 @@ def main(argv=None) -> int:
                     help="phase cycle profile of each zstd row (libstrom_zstdprof.so)")
     ap.add_argument("--libs", default="",
                     help="comma list of lib/zv/<name>.so geometry builds (make zv) timed too")
+    ap.add_argument("--modes", default="auto,wave,fp",
+                    help="zstd decoder choice per row: auto (by stream count), wave (one wave "
+                         "per stream), fp (frame-parallel: a frame's blocks on a workgroup's waves)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -132,7 +135,10 @@ def main(argv=None) -> int:
                 status = torch.empty(n, dtype=torch.int32, device=dev)
                 row = dict(kind=kind, codec=codec, level=level if codec == "zstd" else None,
                            streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
-                for vname, vfn in (variants if codec == "zstd" else variants[:1]):
+                runs = [(vn, vf, md) for vn, vf in (variants if codec == "zstd" else variants[:1])
+                        for md in (a.modes.split(",") if codec == "zstd" and vf is None else ["auto"])]
+                for vname, vfn, mode in runs:
+                    lib().strom_zstd_fp_mode({"auto": -1, "wave": 0, "fp": 1}[mode])
                     times = []
                     ok = True
                     for it in range(a.iters + 1):
@@ -157,8 +163,9 @@ def main(argv=None) -> int:
                             out = dst.view(n, cap)[:, :rawlen]
                             want = ref.view(a.distinct, rawlen)[torch.from_numpy(idx).to(dev)]
                             ok = bool((st == rawlen).all()) and bool(torch.equal(out, want))
+                    lib().strom_zstd_fp_mode(-1)
                     med = float(np.median(times))
-                    pre = "" if vfn is None else vname + "_"
+                    pre = ("" if mode == "auto" else mode + "_") if vfn is None else vname + "_"
                     row[pre + "GBps"] = round(n * rawlen / med / 1e9, 2)
                     row[pre + "ms"] = round(med * 1e3, 3)
                     row[pre + "verified"] = ok

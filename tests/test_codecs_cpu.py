@@ -247,6 +247,51 @@ def test_zstd_host_matches_pyarrow(level):
         assert st == len(d) and out == d, (kind, st)
 
 
+@pytest.mark.parametrize("level", [-5, 1, 3, 9, 19])
+@pytest.mark.parametrize("nw", [2, 4, 8])
+def test_zstd_host_frame_parallel_matches_pyarrow(level, nw):
+    """The frame-parallel decoder's phases (blocks of a frame decoded on
+    nw waves, sequences with symbolic repeat offsets, executed in block
+    order) decode the same frames; groups really run blocks ahead (a
+    treeless / repeat-table block starts a group of its own)."""
+    pa = pytest.importorskip("pyarrow")
+    from nvme_strom_amd import _native as N
+    codec = pa.Codec("zstd", compression_level=level)
+    ahead = 0
+    stats = np.zeros(2, np.uint32)
+    for kind, d in _zstd_payloads().items():
+        st, out = D.zstd_host(D.ZSTD, codec.compress(d, asbytes=True), len(d), fp=nw)
+        assert st == len(d) and out == d, (kind, st)
+        N.lib().strom_zstd_host_fp_stats(stats.ctypes.data)
+        ahead += int(stats[1])
+    assert ahead > 0
+
+
+def test_zstd_host_frame_parallel_arrow_and_errors():
+    pa = pytest.importorskip("pyarrow")
+    d = _ints("uniform", 512 << 10, 12)
+    frame = pa.Codec("zstd").compress(d, asbytes=True)
+    assert D.zstd_host(D.ARROW_ZSTD, D.arrow_zstd_buffer(d, frame), len(d), fp=4) == (len(d), d)
+    raw = b"\xff" * 8 + d[:5000]
+    assert D.zstd_host(D.ARROW_ZSTD, raw, 5000, fp=4) == (5000, d[:5000])
+    assert D.zstd_host(D.ZSTD, frame, len(d) - 1, fp=4)[0] == -2          # overflow
+    assert D.zstd_host(D.ZSTD, frame[: len(frame) // 2], len(d), fp=4)[0] < 0
+    a, b = _data("text", 300000, 13), _data("runs", 290000, 14)
+    skip = struct.pack("<II", 0x184D2A53, 5) + b"12345"
+    two = pa.Codec("zstd").compress(a, asbytes=True) + skip + \
+        pa.Codec("zstd", compression_level=7).compress(b, asbytes=True)
+    assert D.zstd_host(D.ZSTD, two, len(a) + len(b), fp=4) == (len(a) + len(b), a + b)
+    # mutants: bounded status, same as the serial decoder's contract
+    rng = np.random.default_rng(16)
+    base = bytearray(frame)
+    for i in range(300):
+        m = bytearray(base)
+        for _ in range(int(rng.integers(1, 6))):
+            m[int(rng.integers(4, len(m)))] = int(rng.integers(0, 256))
+        st, out = D.zstd_host(D.ZSTD, bytes(m), len(d), fp=4)
+        assert st <= len(d)
+
+
 def test_zstd_arrow_buffers_and_frames():
     pa = pytest.importorskip("pyarrow")
     d = _ints("uniform", 512 << 10, 12)

@@ -204,10 +204,20 @@ def test_malformed_streams_report_errors(dev, monkeypatch, g):
 
 
 # ---------------------------------------------------------------------- zstd
+@pytest.fixture(params=[0, 1], ids=["wave", "fp"])
+def zmode(request, dev):
+    """Both zstd decoders: one wave per stream, and frame-parallel (the
+    blocks of a frame on the waves of a workgroup)."""
+    from nvme_strom_amd import _native as N
+    N.lib().strom_zstd_fp_mode(request.param)
+    yield request.param
+    N.lib().strom_zstd_fp_mode(-1)
+
+
 @pytest.mark.parametrize("level", [-5, 1, 3, 19])
-def test_zstd_from_pyarrow(dev, level):
-    """zstd.hip (one wavefront per stream) == the input, for pyarrow's zstd
-    frames of every payload kind in one launch."""
+def test_zstd_from_pyarrow(dev, zmode, level):
+    """zstd.hip (one wavefront per stream, or frame-parallel) == the input,
+    for pyarrow's zstd frames of every payload kind in one launch."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
     codec = pa.Codec("zstd", compression_level=level)
@@ -218,7 +228,7 @@ def test_zstd_from_pyarrow(dev, level):
     assert outs == pays
 
 
-def test_zstd_randomized_differential(dev):
+def test_zstd_randomized_differential(dev, zmode):
     """200 random payloads (mixtures of text, runs, random bytes, ints and
     floats, 0 B - 400 KB) at random levels -7..19 in one launch: every
     block / literal / table mode pyarrow's encoder picks, raw blocks inside
@@ -283,7 +293,7 @@ def test_zstd_scratch_cache_many_streams(dev):
     assert N.lib().strom_zstd_release() == 0
 
 
-def test_zstd_content_checksum(dev):
+def test_zstd_content_checksum(dev, zmode):
     """Frames with the content-checksum flag verify on the GPU (XXH64 on
     lanes 0..3 over each frame's output); a flipped checksum bit gives -5."""
     pa = pytest.importorskip("pyarrow")
@@ -303,7 +313,7 @@ def test_zstd_content_checksum(dev):
     assert st[-1] == -5
 
 
-def test_zstd_persistent_slots_and_arrow(dev):
+def test_zstd_persistent_slots_and_arrow(dev, zmode):
     """More streams than scratch slots (each workgroup loops over streams
     and reuses its literal slot), Arrow IPC buffers incl. a stored one, and
     malformed streams reported without touching memory out of range."""
@@ -329,7 +339,9 @@ def test_zstd_persistent_slots_and_arrow(dev):
     guard = dst[sum(sizes):]
     d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(dev)
     status = torch.empty(len(streams), dtype=torch.int32, device=dev)
-    scratch = torch.empty(3 * (128 << 10), dtype=torch.uint8, device=dev)   # 3 slots
+    sz = np.zeros(2, np.uint64)
+    N.lib().strom_zstd_scratch_sizes(sz.ctypes.data)
+    scratch = torch.empty(3 * int(sz[zmode]), dtype=torch.uint8, device=dev)   # 3 slots
     rc = N.lib().strom_decompress_zstd(D.ARROW_ZSTD, d_src.data_ptr(), dst.data_ptr(),
                                         d_desc.data_ptr(), len(streams), status.data_ptr(),
                                         scratch.data_ptr(), scratch.numel(), None)
