@@ -87,9 +87,42 @@ class _Batch:
     cols: List[Tuple[_Buf, Optional[_Buf], Optional[_Buf]]]
 
 
+class _PlanArr:
+    """The plan as arrays (no per-batch Python objects: a cold qualifier-list
+    plan over thousands of record batches was ~0.1 s of Python): per batch
+    ``rows`` / ``row_base``, per (batch, column, buffer) with buffer 0 data,
+    1 validity, 2 characters: file ``off``, stored ``length``, decoded
+    ``need``, decode ``cap`` and ``present``; ``comp`` per batch.  Indexing
+    gives the _Batch view of one batch; slicing a range of batches."""
+
+    def __init__(self, rows, row_base, off, length, need, cap, present, comp):
+        self.rows, self.row_base = rows, row_base
+        self.off, self.length, self.need, self.cap = off, length, need, cap
+        self.present, self.comp = present, comp
+
+    def __len__(self) -> int:
+        return len(self.rows)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return _PlanArr(*(a[i] for a in (self.rows, self.row_base, self.off, self.length,
+                                             self.need, self.cap, self.present, self.comp)))
+        cols = []
+        for k in range(self.off.shape[1]):
+            cols.append(tuple(_Buf(int(self.off[i, k, j]), int(self.length[i, k, j]),
+                                   int(self.need[i, k, j]), int(self.cap[i, k, j]),
+                                   bool(self.comp[i])) if self.present[i, k, j] else None
+                              for j in range(3)))
+        return _Batch(int(self.rows[i]), int(self.row_base[i]), cols)
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+
 @dataclass
 class _Group:
-    batches: List[_Batch]
+    b0: int                               # batches [b0, b1) of the scanned range
+    b1: int
     ids: np.ndarray                       # sorted file chunk ids
     dec_bytes: int = 0
     words: int = 0
@@ -103,6 +136,7 @@ class _Group:
     aux_len: Optional[np.ndarray] = None    # (n, ncols) decoded character bytes
     table: Optional[np.ndarray] = None      # (n, QUAL_BATCH_FIELDS), pointer columns 0
     column_bytes: int = 0
+    has_valid: Optional[np.ndarray] = None  # (ncols,) some batch has a validity buffer
 
 
 @dataclass
@@ -219,48 +253,46 @@ class ArrowScan:
         comp = np.array([c is not None for c in m.codecs], dtype=bool)
         rows = m.columns[cis[0]].length if m.nbatches else np.zeros(0, np.int64)
         base = np.concatenate([[0], np.cumsum(rows)]).astype(np.int64)
-        percol = []
-        for ci, col in zip(cis, cols):
+        nb, nc = len(rows), len(cols)
+        off = np.zeros((nb, nc, 3), np.int64)
+        length = np.zeros((nb, nc, 3), np.int64)
+        need = np.zeros((nb, nc, 3), np.int64)
+        present = np.zeros((nb, nc, 3), bool)
+        for k, (ci, col) in enumerate(zip(cis, cols)):
             a = m.columns[ci]
             n = a.length
             st = col.storage
             if st == "b1":
-                need = (n + 7) // 8
+                dneed = (n + 7) // 8
             elif col.kind in ("utf8", "binary") and col.dictionary is None:
-                need = np.where(n > 0, (n + 1) * (8 if col.large else 4), 0)
+                dneed = np.where(n > 0, (n + 1) * (8 if col.large else 4), 0)
             else:
-                need = n * np.dtype(st).itemsize
-            vn = (n + 7) // 8
-            hasv = (a.null_count != 0) & (a.v_len != 0)
+                dneed = n * np.dtype(st).itemsize
             strings = a.x_off is not None and col.dictionary is None
-            if strings:
-                xneed = _stored_sizes(self.path, a.x_off, a.x_len, comp)
-            for what, off, ln, nd in (("data", a.d_off, a.d_len, need),
-                                      ("characters", a.x_off, a.x_len,
-                                       xneed if strings else None)):
+            xneed = _stored_sizes(self.path, a.x_off, a.x_len, comp) if strings else None
+            for what, o, ln, nd in (("data", a.d_off, a.d_len, dneed),
+                                    ("characters", a.x_off, a.x_len, xneed)):
                 if nd is None:
                     continue
                 short = ~comp & (ln < nd)
                 if short.any():
-                    k = int(np.flatnonzero(short)[0])
-                    raise ValueError(f"column {col.name}, record batch {k}: {what} buffer of "
-                                     f"{int(ln[k])} bytes for {int(nd[k])}")
-            z = [None] * len(n)
-            percol.append(zip(a.d_off.tolist(), a.d_len.tolist(), need.tolist(),
-                              _up64_np(need).tolist(), a.v_off.tolist(), a.v_len.tolist(),
-                              vn.tolist(), (_up64_np(vn) + 64).tolist(), hasv.tolist(),
-                              comp.tolist(),
-                              a.x_off.tolist() if strings else z,
-                              a.x_len.tolist() if strings else z,
-                              xneed.tolist() if strings else z))
-        cols_by_batch = zip(*percol) if percol else iter(())
-        out = []
-        for nr, b0, cs in zip(rows.tolist(), base[:-1].tolist(), cols_by_batch):
-            out.append(_Batch(nr, b0, [
-                (_Buf(do, dl, nd, cap, cp), _Buf(vo, vl, vn, vcap, cp) if hv else None,
-                 _Buf(xo, xl, xn, _up64(xn) + 64, cp) if xo is not None else None)
-                for do, dl, nd, cap, vo, vl, vn, vcap, hv, cp, xo, xl, xn in cs]))
-        return out, cols, int(base[-1])
+                    b = int(np.flatnonzero(short)[0])
+                    raise ValueError(f"column {col.name}, record batch {b}: {what} buffer of "
+                                     f"{int(ln[b])} bytes for {int(nd[b])}")
+            off[:, k, 0], length[:, k, 0], need[:, k, 0] = a.d_off, a.d_len, dneed
+            present[:, k, 0] = True
+            off[:, k, 1], length[:, k, 1], need[:, k, 1] = a.v_off, a.v_len, (n + 7) // 8
+            present[:, k, 1] = (a.null_count != 0) & (a.v_len != 0)
+            if strings:
+                off[:, k, 2], length[:, k, 2], need[:, k, 2] = a.x_off, a.x_len, xneed
+                present[:, k, 2] = True
+        # decode capacities: data / characters rounded up to 64, validity
+        # + 64 (the filters read it as whole 64-bit words)
+        cap = _up64_np(need)
+        cap[:, :, 1] += 64
+        cap[:, :, 2] += 64
+        plan = _PlanArr(rows.astype(np.int64), base[:-1], off, length, need, cap, present, comp)
+        return plan, cols, int(base[-1])
 
     def _round_streams(self) -> int:
         cus = 256
@@ -278,134 +310,131 @@ class ArrowScan:
             return max(1, rnd // self.ZSTD_ROUND_DIV)
         return self.ROUND_STREAMS_PER_CU * cus
 
-    def _chunks(self, b: _Batch) -> np.ndarray:
-        c = self.chunk_sz
-        parts = []
-        for bufs in b.cols:
-            for buf in bufs:
-                if buf is not None and buf.length:
-                    parts.append(np.arange(buf.off // c, (buf.off + buf.length + c - 1) // c))
-        return np.unique(np.concatenate(parts)) if parts else np.zeros(0, dtype=np.int64)
-
-    def _groups(self, batches: List[_Batch]) -> List[_Group]:
-        groups: List[_Group] = []
+    def _groups(self, pl: _PlanArr) -> List[_Group]:
         slot = self.slot_bytes
+        nb = len(pl)
         # really compressed buffers (a stored-raw one is as long as its data)
         # (zstd: every compressed buffer takes the entropy stage's latency,
         # however little it compressed — only stored ones are skipped)
         lim = 1.0 if getattr(self, "_codec", None) == D.ARROW_ZSTD else 0.9
-        comp = [[x for x in bufs if x is not None and x.compressed and 0 < x.length]
-                for b in batches for bufs in b.cols
-                if bufs[0].compressed and 0 < bufs[0].length < lim * bufs[0].need]
-        if comp:
+        d_len, d_need = pl.length[:, :, 0], pl.need[:, :, 0]
+        real = pl.comp[:, None] & (d_len > 0) & (d_len < lim * d_need)     # (nb, ncols)
+        ncomp = int(real.sum())
+        if ncomp:
             # few streams per launch are fine for the block-parallel decoder
             # (lz4par.hip: a workgroup per stream), so a column of many
             # buffers is cut into nslots groups: the decode of group g then
             # overlaps the reads of groups g+1.. (with the round-2 lane
             # decoder every launch took one serial stream's time and the
             # split measured slower, profiles/r3/arrow_split3.json)
-            avg = sum(x.length for c in comp for x in c) / len(comp)
-            total = sum(x.length for c in comp for x in c)
+            stored = pl.present & (pl.length > 0)
+            total = float((pl.length * stored * real[:, :, None]).sum())
+            avg = total / ncomp
             want = avg * self.TARGET_STREAMS
             # groups of at most one resident round of streams: the decode of
             # a group takes one stream's latency, and the last group's
             # decode (the part no read overlaps) is as short as it gets
             rnd = self._round_streams()
-            if rnd and len(comp) > rnd:
-                slot = int(min(self.max_slot_bytes, want, total / -(-len(comp) // rnd) * 1.02))
+            if rnd and ncomp > rnd:
+                slot = int(min(self.max_slot_bytes, want, total / -(-ncomp // rnd) * 1.02))
             else:
-                if not rnd and len(comp) >= self.nslots * 256:
+                if not rnd and ncomp >= self.nslots * 256:
                     want = min(want, total / self.nslots)     # one group per slot
                 slot = int(min(self.max_slot_bytes, max(slot, want)))
         limit = max(1, slot // self.chunk_sz)
-        # chunk ranges of every batch at once (vectorised: the qualifier-list
-        # plans touch several buffers per batch)
+        # (batch, chunk) pairs of every stored buffer, in file order: record
+        # batch bodies follow each other, so chunk ids never decrease from one
+        # batch to the next, and the distinct chunks of batches [a, b] are
+        # the "new" pairs among theirs (prefix sums: no per-batch sets)
         c = self.chunk_sz
-        spans = []                     # (batch index, first chunk, end chunk)
-        for i, b in enumerate(batches):
-            for bufs in b.cols:
-                for buf in bufs:
-                    if buf is not None and buf.length:
-                        spans.append((i, buf.off // c, (buf.off + buf.length + c - 1) // c))
-        cur: List[_Batch] = []
-        seen: set = set()              # the current group's chunk ids
-        sp = np.array(spans, dtype=np.int64).reshape(-1, 3)
-        bounds = np.searchsorted(sp[:, 0], np.arange(len(batches) + 1)) if len(sp) else None
-        for i, b in enumerate(batches):
-            mine: set = set()
-            if bounds is not None:
-                for _, lo, hi in sp[bounds[i]:bounds[i + 1]]:
-                    mine.update(range(int(lo), int(hi)))
-            fresh = mine - seen
-            if cur and len(seen) + len(fresh) > limit:
-                groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
-                cur, seen, fresh = [], set(), mine
-            cur.append(b)
-            seen |= fresh
-        if cur:
-            groups.append(_Group(cur, np.array(sorted(seen), dtype=np.int64)))
-        for g in groups:
-            g.dec_bytes = sum(buf.cap for b in g.batches for bufs in b.cols for buf in bufs
-                              if buf is not None and buf.compressed)
-            g.words = sum((b.rows + 63) // 64 for b in g.batches)
-            self._prepare(g)
+        st = pl.present & (pl.length > 0)
+        bi, ki, ji = np.nonzero(st)
+        lo = pl.off[bi, ki, ji] // c
+        hi = (pl.off[bi, ki, ji] + pl.length[bi, ki, ji] + c - 1) // c
+        cnt = hi - lo
+        tot = int(cnt.sum())
+        pb = np.repeat(bi, cnt)
+        start = np.repeat(np.cumsum(cnt) - cnt, cnt)
+        ch = np.repeat(lo, cnt) + (np.arange(tot) - start)
+        order = np.lexsort((ch, pb))
+        pb, ch = pb[order], ch[order]
+        if tot:
+            keep = np.ones(tot, bool)
+            keep[1:] = (pb[1:] != pb[:-1]) | (ch[1:] != ch[:-1])
+            pb, ch = pb[keep], ch[keep]
+        new = np.ones(len(ch), bool)
+        if len(ch):
+            new[1:] = ch[1:] != ch[:-1]
+        cum = np.concatenate([[0], np.cumsum(new)])
+        first = np.searchsorted(pb, np.arange(nb), "left")
+        last = np.searchsorted(pb, np.arange(nb), "right")
+        bounds = []
+        a = 0
+        firstl, lastl, cuml = first.tolist(), last.tolist(), cum.tolist()
+        for b in range(nb):
+            s0, e1 = firstl[a], lastl[b]
+            # distinct chunks of batches [a, b]: the first pair counts too
+            d = (cuml[e1] - cuml[s0 + 1] + 1) if e1 > s0 else 0
+            if b > a and d > limit:
+                bounds.append((a, b))
+                a = b
+        if nb:
+            bounds.append((a, nb))
+        groups = []
+        for a, b in bounds:
+            ids = np.unique(ch[first[a]:last[b - 1]]).astype(np.int64)
+            g = _Group(a, b, ids)
+            sub = pl[a:b]
+            g.dec_bytes = int((sub.cap * (sub.present & sub.comp[:, None, None])).sum())
+            g.words = int(((sub.rows + 63) // 64).sum())
+            self._prepare(g, sub)
+            groups.append(g)
         return groups
 
-    def _prepare(self, g: _Group) -> None:
+    def _prepare(self, g: _Group, pl: _PlanArr) -> None:
         c = self.chunk_sz
-        n = len(g.batches)
-        ncols = len(g.batches[0].cols) if n else 0
-        kind = np.zeros((n, ncols, 3), dtype=np.int8)
-        rel = np.zeros((n, ncols, 3), dtype=np.int64)
-        aux_len = np.zeros((n, ncols), dtype=np.int64)
-        so, sl, do, dl, need = [], [], [], [], []
-        dcur = 0
-        for i, b in enumerate(g.batches):
-            for k, bufs in enumerate(b.cols):
-                if bufs[2] is not None:
-                    aux_len[i, k] = bufs[2].need
-                for j, buf in enumerate(bufs):
-                    if buf is None:
-                        continue
-                    if buf.length == 0:
-                        kind[i, k, j] = 2             # empty batch: nothing is read
-                    elif buf.compressed:
-                        so.append(buf.off)
-                        sl.append(buf.length)
-                        do.append(dcur)
-                        dl.append(buf.cap)
-                        need.append(buf.need)
-                        kind[i, k, j], rel[i, k, j] = 2, dcur
-                        dcur += buf.cap
-                    else:
-                        kind[i, k, j], rel[i, k, j] = 1, buf.off
+        n, ncols = pl.off.shape[0], pl.off.shape[1]
+        pres = pl.present
+        comp3 = np.broadcast_to(pl.comp[:, None, None], pres.shape)
+        empty = pres & (pl.length == 0)               # empty batch: nothing is read
+        dec = pres & ~empty & comp3
+        raw = pres & ~empty & ~comp3
+        kind = np.zeros((n, ncols, 3), np.int8)
+        kind[empty | dec] = 2
+        kind[raw] = 1
+        rel = np.zeros((n, ncols, 3), np.int64)
+        # decode buffer offsets in (batch, column, buffer) order
+        capd = np.where(dec, pl.cap, 0).reshape(-1)
+        dstart = (np.cumsum(capd) - capd).reshape(n, ncols, 3)
+        rel[dec] = dstart[dec]
+
         # file offsets -> offsets in the slot (chunks land in id order)
         def slot_off(off):
             off = np.asarray(off, dtype=np.int64)
             return np.searchsorted(g.ids, off // c) * c + off % c
-        reg = kind == 1
-        rel[reg] = slot_off(rel[reg])
-        if so:
+        rel[raw] = slot_off(pl.off[raw])
+        if dec.any():
             # largest decodes first: a stream's decode time grows with its
             # size, and the decoders hand streams to workgroups in descriptor
             # order (zstd.hip's persistent grid takes stream w, w + grid, ...),
             # so the small validity buffers fill in behind the data buffers
             # instead of taking a resident round of their own
-            order = np.argsort(-np.asarray(dl, dtype=np.int64), kind="stable")
-            g.descs = D.make_descs_arrays(slot_off(so)[order], np.asarray(sl)[order],
-                                          np.asarray(do)[order], np.asarray(dl)[order])
-            g.need = np.asarray(need, dtype=np.int32)[order]
-        g.ptr_kind, g.ptr_rel, g.aux_len = kind, rel, aux_len
-        rows = np.array([b.rows for b in g.batches], dtype=np.int64)
-        words = (rows + 63) // 64
+            dl = pl.cap[dec]
+            order = np.argsort(-dl, kind="stable")
+            g.descs = D.make_descs_arrays(slot_off(pl.off[dec])[order], pl.length[dec][order],
+                                          dstart[dec][order], dl[order])
+            g.need = pl.need[dec].astype(np.int32)[order]
+        g.ptr_kind, g.ptr_rel = kind, rel
+        g.aux_len = np.where(pres[:, :, 2], pl.need[:, :, 2], 0)
+        words = (pl.rows + 63) // 64
         table = np.zeros((n, QUAL_BATCH_FIELDS), dtype=np.int64)
-        table[:, 2] = rows
+        table[:, 2] = pl.rows
         table[:, 3] = np.concatenate([[0], np.cumsum(words)[:-1]]) if n else 0
-        table[:, 4] = [b.row_base for b in g.batches]
+        table[:, 4] = pl.row_base
         g.table = table
         # decoded bytes the scan reads: values / indices / offsets + characters
-        g.column_bytes = sum(bufs[0].need + (bufs[2].need if bufs[2] is not None else 0)
-                             for b in g.batches for bufs in b.cols)
+        g.column_bytes = int(pl.need[:, :, 0].sum() + (pl.need[:, :, 2] * pres[:, :, 2]).sum())
+        g.has_valid = pres[:, :, 1].any(axis=0)
 
     # --------------------------------------------------------- pipeline
     def _ensure_slots(self, groups: List[_Group]) -> None:
@@ -609,8 +638,8 @@ class ArrowScan:
             if tuple(names) not in self._bplans:
                 self._bplans[tuple(names)] = self._plan(names)
             allb, cols, _ = self._bplans[tuple(names)]
-            sel = allb[rng[0]:rng[1]] if rng[0] < rng[1] else []
-            self._plans[key] = (cols, sum(b.rows for b in sel), self._groups(sel))
+            sel = allb[rng[0]:max(rng[0], rng[1])]
+            self._plans[key] = (cols, int(sel.rows.sum()) if len(sel) else 0, self._groups(sel))
         cols, nrows, groups = self._plans[key]
         spec = [[(names.index(p.col), self._compile(p)) for p in c] for c in cl]
         t_plan = time.perf_counter()
@@ -624,7 +653,7 @@ class ArrowScan:
                 raise NotImplementedError(f"projection of {project} ({pmeta.kind}): fixed-width "
                                           "or dictionary-encoded columns")
             pout = torch.empty(max(nrows, 1), dtype=_TORCH[st], device=self.device)
-            if any(b.cols[pcol][1] is not None for g in groups for b in g.batches):
+            if any(bool(g.has_valid[pcol]) for g in groups):
                 pvalid = torch.empty(max(nrows, 1), dtype=torch.uint8, device=self.device)
         pdict = self.dictionary(project) if project and pmeta.dictionary is not None else None
         if not groups or nrows == 0:
