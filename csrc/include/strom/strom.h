@@ -428,6 +428,16 @@ struct strom_qual_batch {
 int strom_column_qual(const struct strom_col_qual *q, const struct strom_qual_batch *d_batches,
                       uint32_t nbatches, uint64_t nwords, uint64_t *d_bitmap,
                       const uint64_t *d_or, int and_dst, uint64_t *d_count, void *stream);
+/* bitmap_to_rows with a utf8/binary column projected (d_strtab: its
+ * strom_qual_batch rows, offsets of owidth 4 or 8 bytes): each selected row's
+ * characters are appended at the device cursor *d_char_cursor in d_pchars,
+ * its start written to d_poff[pos] (and its validity to d_pvalid when given). */
+int strom_bitmap_to_rows_str(const uint64_t *d_bitmap, uint64_t nwords,
+                             const struct strom_filter_batch *d_batches, uint32_t nbatches,
+                             int64_t *d_out, uint64_t *d_total,
+                             const struct strom_qual_batch *d_strtab, uint32_t owidth,
+                             int64_t *d_poff, uint8_t *d_pchars, uint8_t *d_pvalid,
+                             uint64_t *d_char_cursor, void *stream);
 
 #ifdef __cplusplus
 }

@@ -130,7 +130,8 @@ __global__ __launch_bounds__(256) void emit_indices_kernel(const uint64_t *__res
 
 // ---------------------------------------------------------------- batched
 // batch of bitmap word w: the last b with word_base <= w (uniform per wave)
-__device__ __forceinline__ uint32_t batch_of(const strom_filter_batch *b, uint32_t nb, uint64_t w) {
+template <typename B>
+__device__ __forceinline__ uint32_t batch_of(const B *b, uint32_t nb, uint64_t w) {
   uint32_t lo = 0, hi = nb;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -280,6 +281,116 @@ __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restri
       else ((uint8_t *)pout)[pos] = pv[r];
       if (pvalid) pvalid[pos] = pval ? (pval[r >> 3] >> (r & 7)) & 1 : 1;
     }
+    ++pos;
+    word &= word - 1;
+  }
+}
+
+// ------------------------------------------------------------ string projection
+// A selected row's characters (offsets OT of a utf8/binary column, the
+// characters in aux): a malformed offset pair gives an empty string, never
+// a read outside the buffer (as the qualifier kernel).
+template <typename OT>
+__device__ __forceinline__ void str_span(const strom_qual_batch &b, uint64_t r, uint64_t &s,
+                                         uint32_t &len) {
+  const int64_t a = (int64_t)((const OT *)b.values)[r];
+  const int64_t e = (int64_t)((const OT *)b.values)[r + 1];
+  const bool ok = a >= 0 && e >= a && (uint64_t)e <= b.aux_len;
+  s = ok ? (uint64_t)a : 0;
+  len = ok ? (uint32_t)(e - a) : 0;
+}
+
+// per 256-word block: characters of the selected rows (the weights of the
+// character cursor scan, as block_popc64_kernel's counts are of the rows)
+template <typename OT>
+__global__ __launch_bounds__(256) void block_chars_kernel(const uint64_t *__restrict__ bm,
+                                                          uint64_t nwords,
+                                                          const strom_qual_batch *__restrict__ pt,
+                                                          uint32_t nb,
+                                                          uint64_t *__restrict__ block_sum) {
+  __shared__ uint64_t red[256];
+  const uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint64_t word = w < nwords ? bm[w] : 0, sum = 0;
+  if (word) {
+    const strom_qual_batch b = pt[batch_of(pt, nb, w)];
+    const uint64_t local0 = (w - b.word_base) * 64;
+    while (word) {
+      const uint32_t bit = __ffsll((unsigned long long)word) - 1;
+      uint64_t st;
+      uint32_t len;
+      str_span<OT>(b, local0 + bit, st, len);
+      sum += len;
+      word &= word - 1;
+    }
+  }
+  red[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = red[0];
+}
+
+// row ids (as emit_rows_kernel) + each selected row's characters appended
+// at the character cursor: poff[pos] = its start, the bytes in pchars
+template <typename OT>
+__global__ __launch_bounds__(256) void emit_str_kernel(const uint64_t *__restrict__ bm,
+                                                       uint64_t nwords,
+                                                       const strom_qual_batch *__restrict__ pt,
+                                                       uint32_t nb,
+                                                       const uint64_t *__restrict__ rbase,
+                                                       const uint64_t *__restrict__ cbase,
+                                                       int64_t *__restrict__ out,
+                                                       int64_t *__restrict__ poff,
+                                                       uint8_t *__restrict__ pchars,
+                                                       uint8_t *__restrict__ pvalid) {
+  __shared__ uint32_t rs[256];
+  __shared__ uint64_t cs[256];
+  const uint64_t w = (uint64_t)blockIdx.x * kWordsPerBlock + threadIdx.x;
+  uint64_t word = w < nwords ? bm[w] : 0;
+  const uint32_t c = __popcll(word);
+  uint64_t chars = 0;
+  strom_qual_batch b{};
+  uint64_t local0 = 0;
+  if (word) {
+    b = pt[batch_of(pt, nb, w)];
+    local0 = (w - b.word_base) * 64;
+    for (uint64_t x = word; x; x &= x - 1) {
+      uint64_t st;
+      uint32_t len;
+      str_span<OT>(b, local0 + (__ffsll((unsigned long long)x) - 1), st, len);
+      chars += len;
+    }
+  }
+  rs[threadIdx.x] = c;
+  cs[threadIdx.x] = chars;
+  __syncthreads();
+  for (uint32_t off = 1; off < 256; off <<= 1) {
+    const uint32_t ra = threadIdx.x >= off ? rs[threadIdx.x - off] : 0;
+    const uint64_t ca = threadIdx.x >= off ? cs[threadIdx.x - off] : 0;
+    __syncthreads();
+    rs[threadIdx.x] += ra;
+    cs[threadIdx.x] += ca;
+    __syncthreads();
+  }
+  if (!word) return;
+  uint64_t pos = rbase[blockIdx.x] + rs[threadIdx.x] - c;
+  uint64_t cp = cbase[blockIdx.x] + cs[threadIdx.x] - chars;
+  const int64_t row0 = (int64_t)(b.row_base + local0);
+  const uint8_t *val = (const uint8_t *)b.valid;
+  while (word) {
+    const uint32_t bit = __ffsll((unsigned long long)word) - 1;
+    const uint64_t r = local0 + bit;
+    uint64_t st;
+    uint32_t len;
+    str_span<OT>(b, r, st, len);
+    out[pos] = row0 + bit;
+    poff[pos] = (int64_t)cp;
+    const uint8_t *src = (const uint8_t *)b.aux + st;
+    for (uint32_t k = 0; k < len; ++k) pchars[cp + k] = src[k];
+    if (pvalid) pvalid[pos] = val ? (val[r >> 3] >> (r & 7)) & 1 : 1;
+    cp += len;
     ++pos;
     word &= word - 1;
   }
@@ -708,4 +819,48 @@ extern "C" int strom_column_qual(const strom_col_qual *q, const strom_qual_batch
     default:
       return -22;
   }
+}
+
+// bitmap_to_rows with a utf8/binary column projected: d_strtab (the same
+// batches as strom_qual_batch rows: offsets in values, characters in aux),
+// owidth 4 or 8 (offset width); each selected row's characters are appended
+// at the device cursor *d_char_cursor in d_pchars (the caller sizes it for
+// the column's characters) and its start written to d_poff[pos].
+extern "C" int strom_bitmap_to_rows_str(const uint64_t *d_bitmap, uint64_t nwords,
+                                        const strom_filter_batch *d_batches, uint32_t nbatches,
+                                        int64_t *d_out, uint64_t *d_total,
+                                        const strom_qual_batch *d_strtab, uint32_t owidth,
+                                        int64_t *d_poff, uint8_t *d_pchars, uint8_t *d_pvalid,
+                                        uint64_t *d_char_cursor, void *stream) {
+  if (!nwords || !nbatches) return 0;
+  if (!d_bitmap || !d_batches || !d_out || !d_total || !d_strtab || !d_poff || !d_pchars ||
+      !d_char_cursor || (owidth != 4 && owidth != 8))
+    return -22;
+  hipStream_t st = (hipStream_t)stream;
+  const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
+  if (nb64 > 0xffffffffull) return -75;
+  const uint32_t nb = (uint32_t)nb64;
+  uint64_t *cnt = nullptr;
+  if (hipMallocAsync((void **)&cnt, sizeof(uint64_t) * 2 * nb, st) != hipSuccess) return -12;
+  uint64_t *ccnt = cnt + nb;
+  hipLaunchKernelGGL(block_popc64_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, cnt);
+  if (owidth == 4)
+    hipLaunchKernelGGL(block_chars_kernel<int32_t>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords,
+                       d_strtab, nbatches, ccnt);
+  else
+    hipLaunchKernelGGL(block_chars_kernel<int64_t>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords,
+                       d_strtab, nbatches, ccnt);
+  hipLaunchKernelGGL(scan_blocks_cursor_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
+                     (unsigned long long *)d_total);
+  hipLaunchKernelGGL(scan_blocks_cursor_kernel, dim3(1), dim3(1024), 0, st, ccnt, nb,
+                     (unsigned long long *)d_char_cursor);
+  if (owidth == 4)
+    hipLaunchKernelGGL(emit_str_kernel<int32_t>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords,
+                       d_strtab, nbatches, cnt, ccnt, d_out, d_poff, d_pchars, d_pvalid);
+  else
+    hipLaunchKernelGGL(emit_str_kernel<int64_t>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords,
+                       d_strtab, nbatches, cnt, ccnt, d_out, d_poff, d_pchars, d_pvalid);
+  (void)hipFreeAsync(cnt, st);
+  (void)d_batches;
+  return hipGetLastError() == hipSuccess ? 0 : -5;
 }

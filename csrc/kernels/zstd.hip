@@ -1633,12 +1633,81 @@ HD void decode_fp(TM &tm, Smem &s, const Smem &s0, const Ctx &c, const FpBlk &b,
   (void)s0;
 }
 
-// wave w > 0, in block order: execute block w at the frame's output
+// Block executions of the frame-parallel decoder run on the whole
+// workgroup (TN = NW x 64 lanes, batches of TN x EPT output bytes): the
+// batch pointers live in the waves' own execution areas, 1024 entries (+
+// skew) per wave, idle by then — entry e is sm[e / 1024].ptr[PI(e % 1024)].
+HD uint32_t &gptr(Smem *sm, uint32_t e) { return sm[e >> 10].ptr[PI(e & 1023u)]; }
+
+HD void gx_fill(const Smem &s, Smem *sm, uint32_t t, uint32_t b0, uint32_t nb) {
+  const uint32_t abs0 = s.op, e0 = t * EPT;
+  if (e0 >= nb) return;
+  uint32_t i = entry_of(s, b0 + e0);
+  uint32_t start = s.ost[i], next = s.ost[i + 1];
+  uint32_t ll = s.sll[i], off = s.soff[i], lst = s.lst[i];
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = e0 + k;
+    if (e >= nb) break;
+    const uint32_t pos = b0 + e;
+    while (pos >= next) {
+      ++i;
+      start = next;
+      next = s.ost[i + 1];
+      ll = s.sll[i];
+      off = s.soff[i];
+      lst = s.lst[i];
+    }
+    const uint32_t r = pos - start;
+    uint32_t v;
+    if (r < ll) {
+      v = kLit | (lst + r);
+    } else {
+      const uint32_t src = abs0 + pos - off;
+      v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
+    }
+    gptr(sm, e) = v;
+  }
+}
+
+HD bool gx_double(Smem *sm, uint32_t t, uint32_t tn, uint32_t nb) {
+  bool more = false;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * tn + t;
+    if (e >= nb) break;
+    const uint32_t v = gptr(sm, e);
+    if (v & kTag) continue;
+    const uint32_t x = gptr(sm, v);
+    gptr(sm, e) = x;
+    more |= !(x & kTag);
+  }
+  return more;
+}
+
+HD void gx_write(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn, uint32_t b0,
+                 uint32_t nb) {
+  const uint32_t o = s.op + b0;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * tn + t;
+    if (e >= nb) break;
+    const uint32_t v = gptr(sm, e), x = v & ~kTag;
+    uint8_t y;
+    if (v & kLit)
+      y = s.lit_kind == kLitInput ? c.in[s.lit_base + x]
+        : s.lit_kind == kLitRle ? (uint8_t)s.lit_rle : ld_stored(c.lit, x);
+    else
+      y = ld_stored(c.out, x);
+    c.out[o + e] = y;
+  }
+}
+
+// the workgroup, in block order: execute block w at the frame's output
 // position, resolving its symbolic repeat offsets; the frame state in s0
-// (wave 0's Smem) advances
+// (wave 0's Smem) advances.  c: wave w's view (its literal slot).
 template <class TM>
-HD void exec_fp(TM &tm, Smem &s, Smem &s0, const Ctx &c, const Ent *ent, uint32_t nent,
-                uint32_t bout) {
+HD void exec_fp(TM &tm, Smem *sm, uint32_t w, Smem &s0, const Ctx &c, const Ent *ent,
+                uint32_t nent, uint32_t bout) {
+  Smem &s = sm[w];
+  const uint32_t tn = tm.size(), gob = tn * EPT;
   tm.one([&] {
     s.op = s0.op;
     if ((uint64_t)s0.op + bout > c.cap) s.err = kErrOverflow;
@@ -1646,11 +1715,20 @@ HD void exec_fp(TM &tm, Smem &s, Smem &s0, const Ctx &c, const Ent *ent, uint32_
   tm.sync();
   if (s.err) return;
   if (s.btype != kComp) {
-    tm.each([&](uint32_t t) { copy_block(s, c, t); });
+    tm.each([&](uint32_t t) {
+      uint8_t *o = c.out + s.op;
+      if (s.btype == kRle) {
+        const uint8_t v = (uint8_t)gbyte(c, s.bstart);
+        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = v;
+      } else {
+        const uint8_t *in = c.in + s.bstart;
+        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = in[i];
+      }
+    });
   } else if (s.nseq == 0 && s.lit_kind == kLitScratch) {
     // literals-only: the slot is the block's output
     tm.each([&](uint32_t t) {
-      for (uint32_t i = t; i < s.lit_n; i += NT) c.out[s.op + i] = ld_stored(c.lit, i);
+      for (uint32_t i = t; i < s.lit_n; i += tn) c.out[s.op + i] = ld_stored(c.lit, i);
     });
   } else {
     const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
@@ -1660,7 +1738,7 @@ HD void exec_fp(TM &tm, Smem &s, Smem &s0, const Ctx &c, const Ent *ent, uint32_
       const uint32_t base = ent[i0].ost;
       tm.each([&](uint32_t t) {
         bool bad = false;
-        for (uint32_t i = t; i < m; i += NT) {
+        for (uint32_t i = t; i < m; i += tn) {
           const Ent e = ent[i0 + i];
           const uint32_t off = sym_resolve(e.off, rin);
           // the serial path's check (seq_chunk): a match reaches back at
@@ -1682,8 +1760,18 @@ HD void exec_fp(TM &tm, Smem &s, Smem &s0, const Ctx &c, const Ent *ent, uint32_
       });
       tm.sync();
       if (s.err) return;
-      exec_chunk(tm, s, c);
-      tm.one([&] { s.op += s.ctot; });
+      const uint32_t total = s.ctot;
+      for (uint32_t b0 = 0; b0 < total; b0 += gob) {
+        const uint32_t nb = total - b0 < gob ? total - b0 : gob;
+        tm.each([&](uint32_t t) { gx_fill(s, sm, t, b0, nb); });
+        tm.sync();
+        while (tm.any([&](uint32_t t) { return gx_double(sm, t, tn, nb); })) {
+        }
+        tm.each([&](uint32_t t) { gx_write(s, sm, c, t, tn, b0, nb); });
+        tm.fence();
+        tm.sync();
+      }
+      tm.one([&] { s.op += total; });
       tm.sync();
     }
   }
@@ -1771,7 +1859,7 @@ HD void run_fp(G &g, Smem *sm, FpShared &f, const FpCtx &x, int codec) {
       });
       g.sync_all();
       if (s0.err) break;
-      g.wave(w, [&](auto &tm) { exec_fp(tm, sm[w], s0, x.wave(w), x.ent(w), f.nent[w], f.bout[w]); });
+      g.all([&](auto &tm) { exec_fp(tm, sm, w, s0, x.wave(w), x.ent(w), f.nent[w], f.bout[w]); });
       g.sync_all();
       g.wave(0, [&](auto &tm) {
         tm.one([&] {
@@ -1829,6 +1917,7 @@ struct DevTeam {
   DI void count(int) {}
   DI void flush() {}
 #endif
+  DI uint32_t size() const { return blockDim.x; }
   DI void sync() { __syncthreads(); }
   DI void fence() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup"); }
   template <class F>
@@ -1845,13 +1934,15 @@ struct DevTeam {
 };
 
 struct HostTeam {
+  uint32_t n = NT;           // lanes (a workgroup-wide team of the frame-parallel decoder: more)
+  uint32_t size() const { return n; }
   void mark(int) {}
   void count(int) {}
   void sync() {}
   void fence() {}
   template <class F>
   void each(F f) {
-    for (uint32_t t = 0; t < NT; ++t) f(t);
+    for (uint32_t t = 0; t < n; ++t) f(t);
   }
   template <class F>
   void one(F f) { f(); }
@@ -1860,7 +1951,7 @@ struct HostTeam {
   template <class F>
   bool any(F f) {
     bool v = false;
-    for (uint32_t t = 0; t < NT; ++t) v |= f(t);
+    for (uint32_t t = 0; t < n; ++t) v |= f(t);
     return v;
   }
 };
@@ -1871,6 +1962,7 @@ struct HostTeam {
 // another wave reads are ordered by the workgroup fence + barrier of
 // DevGroup::sync_all.
 struct WaveTeam {
+  DI uint32_t size() const { return NT; }
   DI uint32_t lane() const { return threadIdx.x & (NT - 1); }
   DI void mark(int) {}
   DI void count(int) {}
@@ -1907,6 +1999,12 @@ struct DevGroup {
   DI void waves(uint32_t n, F f) {
     if (wid() < n) f(wid(), tm);
   }
+  // the whole workgroup as one team (block executions)
+  template <class F>
+  DI void all(F f) {
+    DevTeam t;
+    f(t);
+  }
   DI void sync_all() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
@@ -1922,6 +2020,13 @@ struct HostGroup {
   template <class F>
   void waves(uint32_t n, F f) {
     for (uint32_t w = 0; w < n; ++w) f(w, tm);
+  }
+  uint32_t nw = 1;
+  template <class F>
+  void all(F f) {
+    HostTeam t;
+    t.n = NT * nw;
+    f(t);
   }
   void sync_all() {}
   uint32_t groups = 0, blocks_par = 0;   // groups, and blocks decoded ahead of their turn
@@ -2186,6 +2291,7 @@ extern "C" int strom_zstd_host_fp(int codec, const uint8_t *src, uint32_t src_le
   std::unique_ptr<uint8_t[]> sc(new uint8_t[fp_scratch(nw)]);
   const FpCtx x{Ctx{src, dst, sc.get(), src_len, cap}, sc.get(), nw};
   HostGroup g;
+  g.nw = nw;
   run_fp(g, sm.get(), *f, x, codec);
   g_fp_host_stats[0] = g.groups;
   g_fp_host_stats[1] = g.blocks_par;

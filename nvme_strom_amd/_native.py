@@ -248,6 +248,10 @@ _SIGS = {
                                             C.c_void_p, C.c_void_p, C.c_void_p]),
     "strom_column_qual": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p,
                                     C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]),
+    "strom_bitmap_to_rows_str": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]),
     "strom_io_info": (C.c_int, [C.c_void_p]),
     "strom_io_prof": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "strom_arrow_headers": (C.c_int, [C.c_int, C.c_void_p, C.c_int64, C.c_int32, C.c_int32,

@@ -39,7 +39,7 @@ import numpy as np
 import torch
 
 from ..ops import decompress as D
-from ..ops.colfilter import BATCH_FIELDS, bitmap_to_rows
+from ..ops.colfilter import BATCH_FIELDS, bitmap_to_rows, bitmap_to_rows_str
 from ..ops.colpred import (QUAL_BATCH_FIELDS, Compiled, Pred, clauses, compile_pred, evaluate,
                            qual_batched)
 from ..ops.reorder import chunk_scatter, landing_positions
@@ -67,6 +67,8 @@ class ScanOut:
     valid: Optional[torch.Tensor] = None    # its validity (uint8 0/1) when it has nulls
     column: Optional[Column] = None         # the projected column's type (units, tz, ...)
     dictionary: object = None               # its decoded dictionary when dictionary-encoded
+    offsets: Optional[torch.Tensor] = None  # utf8/binary projection: int64[selected + 1]
+                                            # into ``values`` (the characters, uint8)
 
 
 @dataclass
@@ -567,7 +569,10 @@ class ArrowScan:
             # emit tables: the strom_filter_batch prefix of the qual tables
             any_col = spec[0][0][0]
             d_rows = table(any_col)[:, :BATCH_FIELDS].contiguous()
-            d_proj = table(proj)[:, :BATCH_FIELDS].contiguous() if proj is not None else None
+            pstr = state.get("pchars") is not None
+            d_proj = None
+            if proj is not None:
+                d_proj = table(proj) if pstr else table(proj)[:, :BATCH_FIELDS].contiguous()
             s.keep += [d_rows] + ([d_proj] if d_proj is not None else [])
         # decode + filter of successive groups overlap on their slots'
         # streams; the row-id emit (+ projection gather) runs in group order
@@ -577,9 +582,14 @@ class ArrowScan:
         es = self.emit_stream
         es.wait_event(ready)
         with torch.cuda.stream(es):
-            bitmap_to_rows(s.bitmap, g.words, d_rows, state["out"], state["cursor"], stream=es,
-                           proj=d_proj, proj_out=state.get("pout"),
-                           proj_valid=state.get("pvalid"))
+            if pstr:
+                bitmap_to_rows_str(s.bitmap, g.words, d_rows, state["out"], state["cursor"],
+                                   d_proj, state["owidth"], state["poff"], state["pchars"],
+                                   state["ccursor"], pvalid=state.get("pvalid"), stream=es)
+            else:
+                bitmap_to_rows(s.bitmap, g.words, d_rows, state["out"], state["cursor"],
+                               stream=es, proj=d_proj, proj_out=state.get("pout"),
+                               proj_valid=state.get("pvalid"))
             state["count"] += s.count
             s.count.zero_()
             if descs is not None:
@@ -619,10 +629,11 @@ class ArrowScan:
         dictionary-encoded columns).  Nulls never satisfy a comparison.
         Each referenced column is read from storage and decoded once per
         group; the predicates' bitmaps are combined on the device.
-        ``project`` names a fixed-width or dictionary-encoded column whose
-        values (indices for a dictionary: ``ScanOut.dictionary`` holds the
-        values) and validity, when it has nulls, are gathered for the
-        selected rows while their ids are written.  ``batches=(b0, b1)``
+        ``project`` names a column whose values (indices for a dictionary:
+        ``ScanOut.dictionary`` holds the values; for utf8/binary the
+        characters, with ``ScanOut.offsets``) and validity, when it has
+        nulls, are gathered for the selected rows while their ids are
+        written.  ``batches=(b0, b1)``
         scans only record batches [b0, b1) (row ids stay file-global:
         parallel/scan.py splits a file over ranks this way)."""
         cl = clauses(quals)
@@ -645,26 +656,37 @@ class ArrowScan:
         t_plan = time.perf_counter()
         out = torch.empty(max(nrows, 1), dtype=torch.int64, device=self.device)
         pcol = names.index(project) if project else None
-        pout = pvalid = None
+        pout = pvalid = pchars = poff = None
         pmeta = cols[pcol] if project else None
+        pstrings = bool(project) and pmeta.kind in ("utf8", "binary") and pmeta.dictionary is None
         if project:
             st = pmeta.storage
-            if st not in _TORCH or (pmeta.kind in ("utf8", "binary") and pmeta.dictionary is None):
-                raise NotImplementedError(f"projection of {project} ({pmeta.kind}): fixed-width "
-                                          "or dictionary-encoded columns")
-            pout = torch.empty(max(nrows, 1), dtype=_TORCH[st], device=self.device)
+            if pstrings:
+                # characters: at most the column's, per the plan
+                nch = sum(int(g.aux_len[:, pcol].sum()) for g in groups)
+                pchars = torch.empty(max(nch, 1), dtype=torch.uint8, device=self.device)
+                poff = torch.empty(max(nrows, 1) + 1, dtype=torch.int64, device=self.device)
+            elif st not in _TORCH:
+                raise NotImplementedError(f"projection of {project} ({pmeta.kind}): fixed-width, "
+                                          "utf8/binary or dictionary-encoded columns")
+            else:
+                pout = torch.empty(max(nrows, 1), dtype=_TORCH[st], device=self.device)
             if any(bool(g.has_valid[pcol]) for g in groups):
                 pvalid = torch.empty(max(nrows, 1), dtype=torch.uint8, device=self.device)
         pdict = self.dictionary(project) if project and pmeta.dictionary is not None else None
         if not groups or nrows == 0:
             return ScanOut(nrows, 0, out[:0], {"total_s": time.perf_counter() - t0},
-                           values=pout[:0] if pout is not None else None,
-                           column=pmeta, dictionary=pdict)
+                           values=pout[:0] if pout is not None else
+                           (pchars[:0] if pchars is not None else None),
+                           column=pmeta, dictionary=pdict,
+                           offsets=torch.zeros(1, dtype=torch.int64, device=self.device)
+                           if pstrings else None)
         self._ensure_slots(groups)
         self.emit_stream = torch.cuda.Stream(device=self.device)
         z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
         state = dict(out=out, cursor=z(), count=z(), err=z(), wait_s=0.0, bytes_read=0,
-                     column_bytes=0, pout=pout, pvalid=pvalid)
+                     column_bytes=0, pout=pout, pvalid=pvalid, pchars=pchars, poff=poff,
+                     ccursor=z(), owidth=8 if pstrings and pmeta.large else 4)
         t_alloc = time.perf_counter()
         # depth nslots - 1 of reads ahead of the group being computed
         ahead = max(1, len(self._slots) - 1)
@@ -675,7 +697,8 @@ class ArrowScan:
             if k + ahead < len(groups):
                 self._submit(k + ahead, groups[k + ahead])
         torch.cuda.synchronize(self.device)
-        cursor, count, err = torch.cat([state["cursor"], state["count"], state["err"]]).tolist()
+        cursor, count, err, nchars = torch.cat([state["cursor"], state["count"], state["err"],
+                                                state["ccursor"]]).tolist()
         t_end = time.perf_counter()
         if err:
             raise RuntimeError(f"{'ZSTD' if self._codec == D.ARROW_ZSTD else 'LZ4'} decode "
@@ -685,14 +708,19 @@ class ArrowScan:
         for s in self._slots:
             s.keep = []
             s.event = None
+        offsets = None
+        if pstrings:
+            poff[count] = nchars
+            offsets = poff[:count + 1]
         return ScanOut(nrows, int(count), out[:count],
                        {"plan_s": t_plan - t0, "alloc_s": t_alloc - t_plan,
                         "wait_s": state["wait_s"], "total_s": t_end - t0},
                        bytes_read=state["bytes_read"], column_bytes=state["column_bytes"],
                        groups=len(groups),
-                       values=pout[:count] if pout is not None else None,
+                       values=pout[:count] if pout is not None else
+                       (pchars[:nchars] if pchars is not None else None),
                        valid=pvalid[:count] if pvalid is not None else None,
-                       column=pmeta, dictionary=pdict)
+                       column=pmeta, dictionary=pdict, offsets=offsets)
 
     def scan(self, name: str, lo, hi) -> ScanOut:
         """Row ids (int64, file order) of ``lo <= column <= hi`` (nulls never

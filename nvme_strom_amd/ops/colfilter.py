@@ -109,3 +109,24 @@ def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out
                                           ptr(out), ptr(cursor),
                                           ptr(proj) if proj is not None else 0, width, pptr,
                                           vptr, stream_handle(stream)), "bitmap_to_rows")
+
+
+def bitmap_to_rows_str(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out: torch.Tensor,
+                       cursor: torch.Tensor, strtab: torch.Tensor, owidth: int,
+                       poff: torch.Tensor, pchars: torch.Tensor, char_cursor: torch.Tensor,
+                       pvalid: Optional[torch.Tensor] = None, stream=None) -> None:
+    """bitmap_to_rows with a utf8/binary column projected: ``strtab`` is its
+    (nbatches, 7) strom_qual_batch table (offsets of ``owidth`` bytes, the
+    characters in aux); each selected row's characters are appended at the
+    device cursor ``char_cursor`` in ``pchars`` and their start written to
+    ``poff`` at the row's output position."""
+    require_cuda(bitmap, "bitmap")
+    if out.dtype != torch.int64 or poff.dtype != torch.int64 or pchars.dtype != torch.uint8:
+        raise ValueError("out / poff int64, pchars uint8")
+    if strtab.shape[0] != batches.shape[0] or strtab.shape[1] != 7:
+        raise ValueError("strtab: (nbatches, 7) of the same batches")
+    check(lib().strom_bitmap_to_rows_str(ptr(bitmap), nwords, ptr(batches), batches.shape[0],
+                                         ptr(out), ptr(cursor), ptr(strtab), owidth, ptr(poff),
+                                         ptr(pchars), ptr(pvalid) if pvalid is not None else 0,
+                                         ptr(char_cursor), stream_handle(stream)),
+          "bitmap_to_rows_str")

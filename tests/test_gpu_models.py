@@ -268,6 +268,20 @@ def test_arrow_scan_predicate_kinds(S, tmp_path, codec):
         offs, chars = out.dictionary[0]
         assert [chars[offs[i]:offs[i + 1]].tobytes().decode() for i in range(len(offs) - 1)] == \
             d.dictionary.to_pylist()
+        # utf8 / large utf8 / binary projections: characters + offsets
+        for pc_name in ("s", "ls", "bin"):
+            out = sc.scan_where([P("i8") > 30], project=pc_name)
+            ids = out.indices.cpu().numpy()
+            col = tbl.column(pc_name).combine_chunks()
+            offs = out.offsets.cpu().numpy()
+            chars = out.values.cpu().numpy().tobytes()
+            ok = np.asarray(col.is_valid())[ids]
+            if out.valid is not None:
+                assert np.array_equal(out.valid.cpu().numpy().astype(bool), ok)
+            got = [chars[offs[i]:offs[i + 1]] for i in range(len(ids))]
+            want = [col[int(r)].as_py() for r in ids]
+            want = [w.encode() if isinstance(w, str) else w for w in want]
+            assert all(g == w for g, w, v in zip(got, want, ok) if v), pc_name
         host = sc.host_scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
         assert np.array_equal(sc.scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
                               .indices.cpu().numpy(), host.indices)
