@@ -365,6 +365,62 @@ HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   return true;
 }
 
+// (2'') LZ4 windows whose chains do not merge: thread 0 walks the rest of
+// the window's true chain itself.  A slice inside a long literal run (an
+// incompressible column: 96 % literals, one token per ~370 input bytes for
+// pyarrow's LZ4 of random-letter strings) sees garbage tokens, and its
+// wrong chain meets the true one only by landing on a true token — never,
+// at that density — so the rounds fix one slice each (110 per 16 KiB
+// window, ~4 us apiece: the whole decode time of such a column, r4
+// strings trace).  A serial walk of the true chain costs one step per TRUE
+// token, ~44 per such window.  Slices from `f` on get their final entry
+// and exit; a slice whose own chain holds the entry keeps its marks.
+template <bool SN>
+HD uint32_t ph_serial(Smem &s, const Ctx &c, uint32_t f, uint32_t nsl) {
+  uint32_t p = s.ex[f - 1], steps = 0;
+  for (uint32_t t = f; t < nsl; ++t) {
+    const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+    if (lo >= hi) break;
+    s.en[t] = p;
+    if (p < hi && getbit(s, p)) {    // merged: the slice's chain from p is its own
+      p = s.ex[t];
+      continue;
+    }
+    for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
+    Seq q;
+    while (p < hi) {
+      setbit(s, p);
+      parse<SN>(s, c, p, s.bend, q);
+      p = q.next;
+      ++steps;
+    }
+    s.ex[t] = p;
+  }
+  return steps;
+}
+
+// From round SERIAL_AFTER on, a window walks serially when its final
+// prefix (slices up to the frontier f) predicts at most SERIAL_TOKENS true
+// tokens in the rest: a serial step costs about what a round's slowest
+// slice does, and the rounds advance the frontier a slice or two each (a
+// dense column — text, 3 input bytes per token — keeps its rounds: its
+// chains merge, and 5,000 serial steps would cost more).
+#ifndef LZ4PAR_SERIAL_AFTER
+#define LZ4PAR_SERIAL_AFTER 3
+#endif
+#ifndef LZ4PAR_SERIAL_TOKENS
+#define LZ4PAR_SERIAL_TOKENS 256
+#endif
+constexpr uint32_t SERIAL_AFTER = LZ4PAR_SERIAL_AFTER;
+constexpr uint32_t SERIAL_TOKENS = LZ4PAR_SERIAL_TOKENS;
+
+HD bool serial_worth(const Smem &s, uint32_t f) {
+  uint32_t tok = 0;
+  for (uint32_t i = 0; i < SW * (f + 1); ++i) tok += (uint32_t)__builtin_popcount(s.bits[i]);
+  const uint32_t done = s.ex[f] - s.ws, rest = s.wend > s.ex[f] ? s.wend - s.ex[f] : 0;
+  return (uint64_t)tok * rest <= (uint64_t)SERIAL_TOKENS * (done ? done : 1);
+}
+
 // (2') snappy validation: a SETTLED prefix instead of rounds in which every
 // slice re-parses from its predecessor's current exit.  Snappy chains from
 // wrong starts merge within ~100 bytes, but one that reads a garbage
@@ -921,13 +977,27 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
           __syncthreads();
         } else {
-          bool changed;
-          do {
+          const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+          for (uint32_t r = 1;; ++r) {
             LP_CNT(kLpNRound);
             const uint32_t ent = ph_entry(s, t);
+            if (t == 0) s.minfix = NT;
             __syncthreads();
-            changed = ph_fix<SN>(s, c, t, ent);
-          } while (__syncthreads_or(changed));
+            const bool changed = ph_fix<SN>(s, c, t, ent);
+            if (changed) atomicMin(&s.minfix, t);
+            const uint32_t nchg = (uint32_t)__syncthreads_count(changed);
+            if (!nchg) break;
+            if (r >= SERIAL_AFTER) {
+              // the frontier slice was just re-parsed from a final entry
+              if (t == 0) s.cov = serial_worth(s, s.minfix) ? 1u : 0u;
+              __syncthreads();
+              if (s.cov) {
+                if (t == 0) ph_serial<SN>(s, c, s.minfix + 1, nsl);
+                __syncthreads();
+                break;
+              }
+            }
+          }
         }
         LP_MARK(kLpValid);
         ph_count<SN>(s, c, t);
@@ -1060,7 +1130,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
   bool flag[NT];
   Held *held = new Held[NT];
   FillPos *fpos = new FillPos[NT];
-  uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0;
+  uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0, serial = 0, serial_windows = 0;
   st_header(s, c, codec);
   for (;;) {
     if (s.mode != kModeDone) st_block(s, c);
@@ -1080,7 +1150,6 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
       st_window(s, c, ws);
       for (uint32_t t = 0; t < NT; ++t) ph_load(s, c, t);
       for (uint32_t t = 0; t < NT; ++t) ph_spec<SN>(s, c, t);
-      bool any;
       if (SN) {
         const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
         for (uint32_t t = 0; t < NT; ++t)
@@ -1103,16 +1172,24 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
         }
         for (uint32_t t = 0; t < NT; ++t) s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
       } else {
-        do {
+        const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+        for (uint32_t r = 1;; ++r) {
           ++rounds;
           for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_entry(s, t);
-          any = false;
+          uint32_t nchg = 0, first = NT;
           for (uint32_t t = 0; t < NT; ++t) {
             flag[t] = ph_fix<SN>(s, c, t, ent[t]);
-            any |= flag[t];
-            fixes += flag[t];
+            nchg += flag[t];
+            if (flag[t] && t < first) first = t;
           }
-        } while (any);
+          fixes += nchg;
+          if (!nchg) break;
+          if (r >= SERIAL_AFTER && serial_worth(s, first)) {
+            serial += ph_serial<SN>(s, c, first + 1, nsl);
+            ++serial_windows;
+            break;
+          }
+        }
       }
       for (uint32_t t = 0; t < NT; ++t) ph_count<SN>(s, c, t);
       for (uint32_t dd = 1; dd < NT; dd <<= 1) {
@@ -1128,6 +1205,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
         for (uint32_t t = 0; t < NT; ++t) ph_fill<SN>(s, c, t, b0, fpos[t]);
         if (s.err) break;
         for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
+        bool any;
         do {
           ++dbl;
           any = false;
@@ -1147,6 +1225,8 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
     stats[1] = rounds;
     stats[2] = fixes;
     stats[3] = dbl;
+    stats[4] = serial_windows;
+    stats[5] = serial;
   }
   if (!s.err && s.expect != 0xffffffffu && s.op != s.expect) s.err = kErrFormat;
   const int r = s.err ? s.err : (int)s.op;

@@ -126,7 +126,7 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
     global _HOST512
     src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
     out = np.zeros(max(cap, 1), dtype=np.uint8)
-    st = np.zeros(4, dtype=np.uint32)
+    st = np.zeros(8, dtype=np.uint32)
     if threads == 512:
         if _HOST512 is None:
             import ctypes as C
@@ -142,7 +142,8 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
     else:
         raise ValueError("threads: 256 or 512")
     n = fn(codec, src.ctypes.data, len(data), out.ctypes.data, cap, st.ctypes.data)
-    stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]))
+    stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]),
+                 serial_windows=int(st[4]), serial_steps=int(st[5]))
     return n, (out[:n].tobytes() if n >= 0 else b""), stats
 
 

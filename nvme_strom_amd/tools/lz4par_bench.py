@@ -35,6 +35,16 @@ def frames(kind: str, k: int, seed: int = 1, codec: str = "lz4"):
             d = rng.integers(0, 1_000_000, 65536, dtype=np.int64).tobytes()
         elif kind == "ids":
             d = np.arange(i * 65536, (i + 1) * 65536, dtype=np.int64).tobytes()
+        elif kind == "chars":
+            # a utf8 column's characters: words of 3-24 random letters
+            # (arrow_bench's string file) — LZ4 leaves them at ratio ~0.97,
+            # one token per ~370 input bytes
+            if i == 0 or not hasattr(frames, "_vocab"):
+                letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+                vr = np.random.default_rng(9)
+                frames._vocab = [letters[vr.integers(0, 26, int(vr.integers(3, 25)))].tobytes()
+                                 for _ in range(20000)]
+            d = b"".join(frames._vocab[j] for j in rng.integers(0, 20000, 40000))[:512 << 10]
         else:
             d = b" ".join(words[j] for j in rng.integers(0, len(words), 110000))[:512 << 10]
         raws.append(d)
