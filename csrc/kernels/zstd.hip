@@ -2045,8 +2045,11 @@ HD constexpr size_t fp_scratch(uint32_t nw) {
 #ifndef ZS_FPW
 #define ZS_FPW 4
 #endif
+// frame-parallel up to this many of its resident rounds: at 1,024 val
+// streams two FP rounds beat the wave decoder's one (26.4 vs 17.0 GB/s,
+// profiles/r4/zstd/), at 2,048 the wave decoder's full round wins
 #ifndef ZS_FP_ROUNDS
-#define ZS_FP_ROUNDS 1
+#define ZS_FP_ROUNDS 2
 #endif
 constexpr uint32_t FPW = ZS_FPW;                 // waves (blocks in flight) per stream
 static_assert(FPW >= 2 && FPW <= NWMAX, "frame-parallel waves");

@@ -133,6 +133,8 @@ class _Group:
     # (kind, offset) with kind 0 none, 1 slot region, 2 decode buffer
     descs: Optional[np.ndarray] = None
     need: Optional[np.ndarray] = None
+    descs_lanes: Optional[np.ndarray] = None   # literal-heavy LZ4 buffers (lane decoder)
+    need_lanes: Optional[np.ndarray] = None
     ptr_kind: Optional[np.ndarray] = None   # (n, ncols, 3)
     ptr_rel: Optional[np.ndarray] = None    # (n, ncols, 3)
     aux_len: Optional[np.ndarray] = None    # (n, ncols) decoded character bytes
@@ -415,17 +417,29 @@ class ArrowScan:
             off = np.asarray(off, dtype=np.int64)
             return np.searchsorted(g.ids, off // c) * c + off % c
         rel[raw] = slot_off(pl.off[raw])
-        if dec.any():
+        g.descs = g.descs_lanes = None
+        # LZ4 buffers that barely compressed (>= 0.9 of their data: long
+        # literal runs, e.g. a utf8 column's characters) go to the
+        # lane-group decoder, which copies literals wide and parses their
+        # few tokens serially; the block-parallel one is for the rest
+        # (lz4par_bench chars: lanes 174 / par 109 GB/s at 2,048 streams;
+        # val: lanes 28 / par 109)
+        lit = dec & (pl.length >= 0.9 * pl.need) if self._codec == D.ARROW_LZ4 else \
+            np.zeros_like(dec)
+        for m, attr in ((dec & ~lit, "descs"), (lit, "descs_lanes")):
+            if not m.any():
+                continue
             # largest decodes first: a stream's decode time grows with its
             # size, and the decoders hand streams to workgroups in descriptor
             # order (zstd.hip's persistent grid takes stream w, w + grid, ...),
             # so the small validity buffers fill in behind the data buffers
             # instead of taking a resident round of their own
-            dl = pl.cap[dec]
+            dl = pl.cap[m]
             order = np.argsort(-dl, kind="stable")
-            g.descs = D.make_descs_arrays(slot_off(pl.off[dec])[order], pl.length[dec][order],
-                                          dstart[dec][order], dl[order])
-            g.need = pl.need[dec].astype(np.int32)[order]
+            setattr(g, attr, D.make_descs_arrays(slot_off(pl.off[m])[order], pl.length[m][order],
+                                                 dstart[m][order], dl[order]))
+            setattr(g, "need" if attr == "descs" else "need_lanes",
+                    pl.need[m].astype(np.int32)[order])
         g.ptr_kind, g.ptr_rel = kind, rel
         g.aux_len = np.where(pres[:, :, 2], pl.need[:, :, 2], 0)
         words = (pl.rows + 63) // 64
@@ -525,14 +539,18 @@ class ArrowScan:
                                                              res.nr_ssd), self.chunk_sz)
             base = region.data_ptr()
             dec_base = s.dec.data_ptr()
-            descs = g.descs
-            if descs is not None:
+            descs = g.descs if g.descs is not None else g.descs_lanes
+            for dsc, need, lanes in ((g.descs, g.need, False), (g.descs_lanes, g.need_lanes, True)):
+                if dsc is None:
+                    continue
                 # every compressed buffer of every scanned column: one launch
-                d_desc = torch.from_numpy(descs.view(np.uint8)).pin_memory().to(
+                # (two when some are literal-heavy LZ4)
+                d_desc = torch.from_numpy(dsc.view(np.uint8)).pin_memory().to(
                     self.device, non_blocking=True)
-                d_need = torch.from_numpy(g.need).pin_memory().to(self.device, non_blocking=True)
-                status = torch.empty(len(descs), dtype=torch.int32, device=self.device)
-                D.decompress_async(self._codec, region, s.dec, d_desc, status, stream=cs)
+                d_need = torch.from_numpy(need).pin_memory().to(self.device, non_blocking=True)
+                status = torch.empty(len(dsc), dtype=torch.int32, device=self.device)
+                D.decompress_async(self._codec, region, s.dec, d_desc, status, stream=cs,
+                                   lanes=lanes)
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]

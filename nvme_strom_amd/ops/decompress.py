@@ -193,15 +193,19 @@ def make_descs_arrays(src_off, src_len, dst_off, dst_len) -> np.ndarray:
 
 
 def decompress_async(codec: int, src: torch.Tensor, dst: torch.Tensor, d_desc: torch.Tensor,
-                     status: torch.Tensor, stream=None) -> None:
+                     status: torch.Tensor, stream=None, lanes: bool = False) -> None:
     """Device-side descriptors (uint8 view of DESC_DTYPE records) and status:
     no host sync; the caller checks ``status`` on the device.  Bounds are
-    the caller's contract (checked by :func:`decompress`)."""
+    the caller's contract (checked by :func:`decompress`).  ``lanes``: the
+    lane-group LZ4 decoder whatever the stream count — the faster one for
+    literal-heavy streams (a serial parse with few tokens, wide literal
+    copies; profiles/r4/dec/lz4par_chars.json)."""
     n = d_desc.numel() // DESC_DTYPE.itemsize
     if n == 0:
         return
-    check(lib().strom_decompress(codec, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status),
-                                 stream_handle(stream)), "decompress")
+    fn = lib().strom_decompress_lanes if lanes else lib().strom_decompress
+    check(fn(codec, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status), stream_handle(stream)),
+          "decompress")
 
 
 def decompress(codec: int, src: torch.Tensor, dst: torch.Tensor, descs: np.ndarray,
