@@ -1484,10 +1484,55 @@ struct FpBlk {
   uint32_t bstart, bend, btype, bsize, blast;
 };
 
+// the frame's state while its blocks decode on every wave (wave 0's Smem
+// holds it otherwise): output position, repeat offsets, and the latest
+// Huffman-tree / FSE-table definitions
+struct FpFrame {
+  uint32_t op, fstart, rep[3];
+  uint32_t hbits, hdesc, hdesc_end, have_ll, have_of, have_ml;
+  uint32_t tmode[3], tpos[3], tend[3];
+};
+
 struct FpShared {
   FpBlk blk[NWMAX];
   uint32_t nblk, serial, nent[NWMAX], bout[NWMAX];
+  int32_t err;
+  FpFrame fr;
 };
+
+HD void frame_save(FpFrame &f, const Smem &s) {
+  f.op = s.op;
+  f.fstart = s.fstart;
+  for (uint32_t k = 0; k < 3; ++k) {
+    f.rep[k] = s.rep[k];
+    f.tmode[k] = s.tmode[k];
+    f.tpos[k] = s.tpos[k];
+    f.tend[k] = s.tend[k];
+  }
+  f.hbits = s.hbits;
+  f.hdesc = s.hdesc;
+  f.hdesc_end = s.hdesc_end;
+  f.have_ll = s.have_ll;
+  f.have_of = s.have_of;
+  f.have_ml = s.have_ml;
+}
+
+HD void frame_restore(Smem &s, const FpFrame &f) {
+  s.op = f.op;
+  s.fstart = f.fstart;
+  for (uint32_t k = 0; k < 3; ++k) {
+    s.rep[k] = f.rep[k];
+    s.tmode[k] = f.tmode[k];
+    s.tpos[k] = f.tpos[k];
+    s.tend[k] = f.tend[k];
+  }
+  s.hbits = f.hbits;
+  s.hdesc = f.hdesc;
+  s.hdesc_end = f.hdesc_end;
+  s.have_ll = f.have_ll;
+  s.have_of = f.have_of;
+  s.have_ml = f.have_ml;
+}
 
 HD uint32_t sym_resolve(uint32_t v, const uint32_t *rin) {
   if (!is_sym(v)) return v;
@@ -1535,11 +1580,13 @@ HD void prewalk(Smem &s, const Ctx &c, FpShared &f, uint32_t nw) {
         dep |= (modes >> 6) == 3 || ((modes >> 4) & 3) == 3 || ((modes >> 2) & 3) == 3;
       }
       // a block that needs a predecessor's tree / table starts the next
-      // group (as its first block, on wave 0, which holds the definitions)
+      // group, and a group starting with one runs it alone, serially, on
+      // wave 0 (which holds the definitions)
       if (dep && k) {
         f.nblk = k;
         break;
       }
+      if (dep) f.serial = 1;
     }
     f.nblk = k + 1;
     if (s.blast) break;
@@ -1562,8 +1609,8 @@ HD void prewalk(Smem &s, const Ctx &c, FpShared &f, uint32_t nw) {
 // wave w > 0: decode block f.blk[w] — literals into its slot, sequences
 // into its entry buffer (HBM), repeat offsets symbolic
 template <class TM>
-HD void decode_fp(TM &tm, Smem &s, const Smem &s0, const Ctx &c, const FpBlk &b, Ent *ent,
-                  uint32_t &nent, uint32_t &bout) {
+HD void decode_fp(TM &tm, Smem &s, const Ctx &c, const FpBlk &b, Ent *ent, uint32_t &nent,
+                  uint32_t &bout) {
   tm.one([&] {
     s.err = 0;
     s.bstart = b.bstart;
@@ -1630,7 +1677,6 @@ HD void decode_fp(TM &tm, Smem &s, const Smem &s0, const Ctx &c, const FpBlk &b,
   tm.sync();
   nent = n;
   bout = out;
-  (void)s0;
 }
 
 // Block executions of the frame-parallel decoder run on the whole
@@ -1704,7 +1750,7 @@ HD void gx_write(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn,
 // position, resolving its symbolic repeat offsets; the frame state in s0
 // (wave 0's Smem) advances.  c: wave w's view (its literal slot).
 template <class TM>
-HD void exec_fp(TM &tm, Smem *sm, uint32_t w, Smem &s0, const Ctx &c, const Ent *ent,
+HD void exec_fp(TM &tm, Smem *sm, uint32_t w, FpFrame &s0, const Ctx &c, const Ent *ent,
                 uint32_t nent, uint32_t bout) {
   Smem &s = sm[w];
   const uint32_t tn = tm.size(), gob = tn * EPT;
@@ -1789,10 +1835,10 @@ HD void exec_fp(TM &tm, Smem *sm, uint32_t w, Smem &s0, const Ctx &c, const Ent 
   tm.sync();
 }
 
-// wave 0 after a parallel group: the later blocks' Huffman tree and FSE
-// table definitions become the frame's (a treeless / repeat-mode block of
-// a later group starts that group, on wave 0)
-HD void inherit_defs(Smem &s0, const Smem &s) {
+// after a parallel group: the blocks' Huffman tree and FSE table
+// definitions, in block order, become the frame's (a treeless /
+// repeat-mode block of a later group runs alone on wave 0)
+HD void inherit_defs(FpFrame &s0, const Smem &s) {
   if (s.btype != kComp) return;
   if (s.hbits && s.lit_kind == kLitScratch) {
     s0.hdesc = s.hdesc;
@@ -1821,7 +1867,7 @@ struct FpCtx {
     return Ctx{c.in, c.out, scr + (size_t)w * SLOT, c.len, c.cap};
   }
   HD Ent *ent(uint32_t w) const {
-    return (Ent *)(scr + (size_t)nw * SLOT + (size_t)(w - 1) * kMaxEnt * sizeof(Ent));
+    return (Ent *)(scr + (size_t)nw * SLOT + (size_t)w * kMaxEnt * sizeof(Ent));
   }
 };
 
@@ -1844,26 +1890,37 @@ HD void run_fp(G &g, Smem *sm, FpShared &f, const FpCtx &x, int codec) {
     if (s0.err || !f.nblk) break;
     const uint32_t nb = f.serial ? 1 : f.nblk;
     g.count_group(nb);
-    g.waves(nb, [&](uint32_t w, auto &tm) {
-      if (w == 0) block_body(tm, s0, c0);
-      else decode_fp(tm, sm[w], s0, x.wave(w), f.blk[w], x.ent(w), f.nent[w], f.bout[w]);
-    });
-    g.sync_all();
-    for (uint32_t w = 1; w < nb; ++w) {
-      if (s0.err) break;
+    if (f.serial) {
+      // one block, decoded and executed in place on wave 0
+      g.wave(0, [&](auto &tm) { block_body(tm, s0, c0); });
+      g.sync_all();
+    } else {
+      // every block of the group on its own wave; wave 0's Smem is a block
+      // decoder too meanwhile, the frame waits in f.fr
       g.wave(0, [&](auto &tm) {
         tm.one([&] {
-          if (sm[w].err) s0.err = sm[w].err;
+          frame_save(f.fr, s0);
+          f.err = 0;
         });
         tm.sync();
       });
       g.sync_all();
-      if (s0.err) break;
-      g.all([&](auto &tm) { exec_fp(tm, sm, w, s0, x.wave(w), x.ent(w), f.nent[w], f.bout[w]); });
+      g.waves(nb, [&](uint32_t w, auto &tm) {
+        decode_fp(tm, sm[w], x.wave(w), f.blk[w], x.ent(w), f.nent[w], f.bout[w]);
+      });
       g.sync_all();
+      for (uint32_t w = 0; w < nb; ++w) {
+        if (sm[w].err) break;                      // its decode failed
+        g.all([&](auto &tm) { exec_fp(tm, sm, w, f.fr, x.wave(w), x.ent(w), f.nent[w], f.bout[w]); });
+        g.sync_all();
+        if (sm[w].err) break;                      // its execution failed
+      }
       g.wave(0, [&](auto &tm) {
         tm.one([&] {
-          if (sm[w].err) s0.err = sm[w].err;
+          for (uint32_t w = 0; w < nb && !f.err; ++w) f.err = sm[w].err;
+          for (uint32_t w = 0; w < nb; ++w) inherit_defs(f.fr, sm[w]);
+          frame_restore(s0, f.fr);
+          s0.err = f.err;
         });
         tm.sync();
       });
@@ -1872,7 +1929,6 @@ HD void run_fp(G &g, Smem *sm, FpShared &f, const FpCtx &x, int codec) {
     if (s0.err) break;
     g.wave(0, [&](auto &tm) {
       tm.one([&] {
-        for (uint32_t w = 1; w < nb; ++w) inherit_defs(s0, sm[w]);
         const FpBlk &l = f.blk[nb - 1];
         s0.bend = l.bend;
         s0.blast = l.blast;
@@ -2039,7 +2095,7 @@ struct HostGroup {
 // frame-parallel scratch per workgroup: NW literal slots, then NW - 1
 // entry buffers
 HD constexpr size_t fp_scratch(uint32_t nw) {
-  return (size_t)nw * SLOT + (size_t)(nw - 1) * kMaxEnt * sizeof(Ent);
+  return (size_t)nw * (SLOT + kMaxEnt * sizeof(Ent));
 }
 
 #ifndef ZS_FPW
