@@ -1685,12 +1685,32 @@ HD void decode_fp(TM &tm, Smem &s, const Ctx &c, const FpBlk &b, Ent *ent, uint3
 // skew) per wave, idle by then — entry e is sm[e / 1024].ptr[PI(e % 1024)].
 HD uint32_t &gptr(Smem *sm, uint32_t e) { return sm[e >> 10].ptr[PI(e & 1023u)]; }
 
-HD void gx_fill(const Smem &s, Smem *sm, uint32_t t, uint32_t b0, uint32_t nb) {
+// a group chunk: up to (TN / 64) x SEQN entries, entry i in wave i / SEQN's
+// chunk arrays at i % SEQN (idle there by then), its end in `end`
+struct GChunk {
+  Smem *sm;
+  uint32_t m, end;
+  HD uint32_t ost(uint32_t i) const { return i >= m ? end : sm[i / SEQN].ost[i % SEQN]; }
+  HD uint32_t sll(uint32_t i) const { return sm[i / SEQN].sll[i % SEQN]; }
+  HD uint32_t soff(uint32_t i) const { return sm[i / SEQN].soff[i % SEQN]; }
+  HD uint32_t lst(uint32_t i) const { return sm[i / SEQN].lst[i % SEQN]; }
+  HD uint32_t entry_of(uint32_t pos) const {   // ost strictly increases
+    uint32_t lo = 0, hi = m;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (ost(mid) <= pos) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+};
+
+HD void gx_fill(const Smem &s, const GChunk &g, uint32_t t, uint32_t b0, uint32_t nb) {
   const uint32_t abs0 = s.op, e0 = t * EPT;
   if (e0 >= nb) return;
-  uint32_t i = entry_of(s, b0 + e0);
-  uint32_t start = s.ost[i], next = s.ost[i + 1];
-  uint32_t ll = s.sll[i], off = s.soff[i], lst = s.lst[i];
+  uint32_t i = g.entry_of(b0 + e0);
+  uint32_t start = g.ost(i), next = g.ost(i + 1);
+  uint32_t ll = g.sll(i), off = g.soff(i), lst = g.lst(i);
   for (uint32_t k = 0; k < EPT; ++k) {
     const uint32_t e = e0 + k;
     if (e >= nb) break;
@@ -1698,10 +1718,10 @@ HD void gx_fill(const Smem &s, Smem *sm, uint32_t t, uint32_t b0, uint32_t nb) {
     while (pos >= next) {
       ++i;
       start = next;
-      next = s.ost[i + 1];
-      ll = s.sll[i];
-      off = s.soff[i];
-      lst = s.lst[i];
+      next = g.ost(i + 1);
+      ll = g.sll(i);
+      off = g.soff(i);
+      lst = g.lst(i);
     }
     const uint32_t r = pos - start;
     uint32_t v;
@@ -1711,7 +1731,7 @@ HD void gx_fill(const Smem &s, Smem *sm, uint32_t t, uint32_t b0, uint32_t nb) {
       const uint32_t src = abs0 + pos - off;
       v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
     }
-    gptr(sm, e) = v;
+    gptr(g.sm, e) = v;
   }
 }
 
@@ -1779,9 +1799,14 @@ HD void exec_fp(TM &tm, Smem *sm, uint32_t w, FpFrame &s0, const Ctx &c, const E
   } else {
     const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
     const uint32_t fpos = s0.op - s0.fstart;     // frame output before the block
-    for (uint32_t i0 = 0; i0 < nent; i0 += SEQN) {
-      const uint32_t m = nent - i0 < SEQN ? nent - i0 : SEQN;
+    // chunks of (tn / 64) x SEQN entries over every wave's chunk arrays:
+    // about one batch of output each (the block's ~16k sequences in 32
+    // chunks, not 128 of a quarter batch)
+    const uint32_t gseq = tn / NT * SEQN;
+    for (uint32_t i0 = 0; i0 < nent; i0 += gseq) {
+      const uint32_t m = nent - i0 < gseq ? nent - i0 : gseq;
       const uint32_t base = ent[i0].ost;
+      const uint32_t end = (i0 + m < nent ? ent[i0 + m].ost : bout) - base;
       tm.each([&](uint32_t t) {
         bool bad = false;
         for (uint32_t i = t; i < m; i += tn) {
@@ -1791,25 +1816,21 @@ HD void exec_fp(TM &tm, Smem *sm, uint32_t w, FpFrame &s0, const Ctx &c, const E
           // most to the frame start; the trailing-literals entry has no match
           const bool has_match = (i0 + i + 1 < nent ? ent[i0 + i + 1].ost : bout) - e.ost > e.ll;
           bad |= has_match && off - 1 >= fpos + e.ost + e.ll;
-          s.sll[i] = e.ll;
-          s.soff[i] = off;
-          s.lst[i] = e.lst;
-          s.ost[i] = e.ost - base;
-        }
-        if (t == 0) {
-          const uint32_t end = i0 + m < nent ? ent[i0 + m].ost : bout;
-          s.ost[m] = end - base;
-          s.cn = m;
-          s.ctot = end - base;
+          Smem &q = sm[i / SEQN];
+          q.sll[i % SEQN] = e.ll;
+          q.soff[i % SEQN] = off;
+          q.lst[i % SEQN] = e.lst;
+          q.ost[i % SEQN] = e.ost - base;
         }
         if (bad) s.err = ZF(kErrDistance);
       });
       tm.sync();
       if (s.err) return;
-      const uint32_t total = s.ctot;
+      const GChunk gc{sm, m, end};
+      const uint32_t total = end;
       for (uint32_t b0 = 0; b0 < total; b0 += gob) {
         const uint32_t nb = total - b0 < gob ? total - b0 : gob;
-        tm.each([&](uint32_t t) { gx_fill(s, sm, t, b0, nb); });
+        tm.each([&](uint32_t t) { gx_fill(s, gc, t, b0, nb); });
         tm.sync();
         while (tm.any([&](uint32_t t) { return gx_double(sm, t, tn, nb); })) {
         }
