@@ -69,7 +69,7 @@ for phase in "$@"; do
                       "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
             n=$((n + 1))
             (cd /tmp && step zpmc$n 120 rocprofv3 --pmc $pass --output-format csv -d "$OUT/zpmc$n" -o pmc \
-              -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,x} --levels 1 --streams 2048 \
+              -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,x} --levels 1 --streams ${ZSTREAMS:-2048} --modes ${ZMODES:-auto} \
                  --no-lz4 --iters 1) || exit 1
           done ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
