@@ -324,6 +324,16 @@ int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
                           const struct strom_decomp_desc *d_desc, uint32_t nstreams,
                           int32_t *d_status, void *scratch, uint64_t scratch_bytes,
                           void *stream);
+/* the same with the decoder chosen by the caller: mode -1 the library's
+ * choice, 0 one wave per stream, 1 frame-parallel (a frame's blocks on the
+ * waves of a workgroup) */
+int strom_decompress_zstd_mode(int codec, const void *d_src, void *d_dst,
+                               const struct strom_decomp_desc *d_desc, uint32_t nstreams,
+                               int32_t *d_status, void *scratch, uint64_t scratch_bytes,
+                               void *stream, int mode);
+/* decoder choice for strom_decompress_zstd: -1 by stream count (default),
+ * 0 / 1 forced; returns the previous setting */
+int strom_zstd_fp_mode(int mode);
 /* free the library-kept zstd scratch (after the streams' last decodes) */
 int strom_zstd_release(void);
 /* the same decode on the CPU (the kernel's phases lane by lane) */

@@ -2270,16 +2270,22 @@ bool use_fp(uint32_t nstreams) {
 // Arrow IPC buffer) — one wavefront per stream, persistent over the
 // streams.  scratch: SLOT (128 KiB) per workgroup for decoded literals;
 // NULL = a per-stream buffer kept by the library.
-extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
-                                     const strom_decomp_desc *d_desc, uint32_t nstreams,
-                                     int32_t *d_status, void *scratch, uint64_t scratch_bytes,
-                                     void *stream) {
+// mode: -1 the library's choice (strom_zstd_fp_mode / stream count), 0 one
+// wave per stream, 1 frame-parallel — a caller that runs several decodes
+// at once (the Arrow scan's slot streams) may want every one of them to
+// take part of the chip rather than all of it.
+extern "C" int strom_decompress_zstd_mode(int codec, const void *d_src, void *d_dst,
+                                          const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                          int32_t *d_status, void *scratch,
+                                          uint64_t scratch_bytes, void *stream, int mode) {
   using namespace zs;
   if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  if (mode < -1 || mode > 1) return -22;
   if (!nstreams) return 0;
   // a caller's scratch too small for one frame-parallel workgroup keeps
   // the wave-per-stream decoder
-  const bool fp = use_fp(nstreams) && (!scratch || scratch_bytes >= fp_scratch(FPW));
+  const bool fp = (mode < 0 ? use_fp(nstreams) : mode == 1) &&
+                  (!scratch || scratch_bytes >= fp_scratch(FPW));
   const size_t per_wg = fp ? fp_scratch(FPW) : SLOT;
   const uint32_t res = fp ? cu_count() * fp_per_cu() : resident_groups();
   uint32_t grid = nstreams < res ? nstreams : res;
@@ -2302,6 +2308,14 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
     hipLaunchKernelGGL(zstd_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, codec,
                        (const uint8_t *)d_src, (uint8_t *)d_dst, d_desc, nstreams, d_status, sc);
   return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
+                                     const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                     int32_t *d_status, void *scratch, uint64_t scratch_bytes,
+                                     void *stream) {
+  return strom_decompress_zstd_mode(codec, d_src, d_dst, d_desc, nstreams, d_status, scratch,
+                                    scratch_bytes, stream, -1);
 }
 
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }

@@ -212,6 +212,11 @@ class ArrowScan:
     ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
     # ZSTD groups: 1 / ZSTD_ROUND_DIV of the zstd decoder's resident round
     ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "1"))
+    # the zstd decoder per group launch: None the library's choice by stream
+    # count, 0 one wave per stream (groups smaller than its round then decode
+    # concurrently on their slot streams), 1 frame-parallel
+    ZSTD_MODE = (int(os.environ["STROM_ARROW_ZSTD_MODE"])
+                 if os.environ.get("STROM_ARROW_ZSTD_MODE") else None)
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -550,7 +555,7 @@ class ArrowScan:
                 d_need = torch.from_numpy(need).pin_memory().to(self.device, non_blocking=True)
                 status = torch.empty(len(dsc), dtype=torch.int32, device=self.device)
                 D.decompress_async(self._codec, region, s.dec, d_desc, status, stream=cs,
-                                   lanes=lanes)
+                                   lanes=lanes, zstd_mode=self.ZSTD_MODE)
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]

@@ -13,7 +13,7 @@ from __future__ import annotations
 import ctypes as C
 import struct
 from dataclasses import dataclass
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -193,15 +193,23 @@ def make_descs_arrays(src_off, src_len, dst_off, dst_len) -> np.ndarray:
 
 
 def decompress_async(codec: int, src: torch.Tensor, dst: torch.Tensor, d_desc: torch.Tensor,
-                     status: torch.Tensor, stream=None, lanes: bool = False) -> None:
+                     status: torch.Tensor, stream=None, lanes: bool = False,
+                     zstd_mode: Optional[int] = None) -> None:
     """Device-side descriptors (uint8 view of DESC_DTYPE records) and status:
     no host sync; the caller checks ``status`` on the device.  Bounds are
     the caller's contract (checked by :func:`decompress`).  ``lanes``: the
     lane-group LZ4 decoder whatever the stream count — the faster one for
     literal-heavy streams (a serial parse with few tokens, wide literal
-    copies; profiles/r4/dec/lz4par_chars.json)."""
+    copies; profiles/r4/dec/lz4par_chars.json).  ``zstd_mode``: the zstd
+    decoder for this launch (0 one wave per stream, 1 frame-parallel,
+    None / -1 the library's choice)."""
     n = d_desc.numel() // DESC_DTYPE.itemsize
     if n == 0:
+        return
+    if zstd_mode is not None and codec in (ZSTD, ARROW_ZSTD):
+        check(lib().strom_decompress_zstd_mode(codec, ptr(src), ptr(dst), ptr(d_desc), n,
+                                               ptr(status), None, 0, stream_handle(stream),
+                                               int(zstd_mode)), "decompress")
         return
     fn = lib().strom_decompress_lanes if lanes else lib().strom_decompress
     check(fn(codec, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status), stream_handle(stream)),
