@@ -13,4 +13,7 @@
 #define LZ4PAR_NO_HOST 1
 #define LZ4PAR_LOADU 8
 #define LZ4PAR_WPE_LZ4 6
+// snappy too: 96 VGPRs left it at 2 workgroups per CU (5 waves per SIMD);
+// at 80 (6 small spills) it keeps the third
+#define LZ4PAR_WPE 6
 #include "lz4par.hip"
