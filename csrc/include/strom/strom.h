@@ -398,6 +398,8 @@ int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwords,
 #define STROM_COL_BOOL 11   /* bit-packed values */
 #define STROM_COL_STR32 12  /* utf8/binary: int32 offsets in values, bytes in aux */
 #define STROM_COL_STR64 13  /* large utf8/binary: int64 offsets */
+#define STROM_COL_DEC128 14 /* decimal128: 16-byte two's complement (value x 10^scale);
+                               RANGES bounds are 16-byte pairs */
 /* operators */
 #define STROM_QOP_RANGES 1     /* v in one of nconst inclusive ranges: sorted, disjoint
                                   (lo, hi) pairs of int64 (U64: uint64; floats: double) */

@@ -275,7 +275,10 @@ __global__ __launch_bounds__(256) void emit_rows_kernel(const uint64_t *__restri
     out[pos] = row0 + bit;
     if (W) {
       const uint64_t r = local0 + bit;
-      if (W == 8) ((uint64_t *)pout)[pos] = ((const uint64_t *)pv)[r];
+      if (W == 16) {
+        ((uint64_t *)pout)[2 * pos] = ((const uint64_t *)pv)[2 * r];
+        ((uint64_t *)pout)[2 * pos + 1] = ((const uint64_t *)pv)[2 * r + 1];
+      } else if (W == 8) ((uint64_t *)pout)[pos] = ((const uint64_t *)pv)[r];
       else if (W == 4) ((uint32_t *)pout)[pos] = ((const uint32_t *)pv)[r];
       else if (W == 2) ((uint16_t *)pout)[pos] = ((const uint16_t *)pv)[r];
       else ((uint8_t *)pout)[pos] = pv[r];
@@ -436,6 +439,8 @@ template <> struct CmpOf<double> { typedef double type; };
 
 struct BitT {};   // STROM_COL_BOOL: one bit per row
 template <> struct CmpOf<BitT> { typedef int64_t type; };
+struct Dec128T {};   // STROM_COL_DEC128: 16-byte little-endian two's complement
+template <> struct CmpOf<Dec128T> { typedef __int128 type; };
 
 template <typename T>
 __device__ __forceinline__ typename CmpOf<T>::type qload(const strom_qual_batch &b, uint64_t i) {
@@ -444,6 +449,11 @@ __device__ __forceinline__ typename CmpOf<T>::type qload(const strom_qual_batch 
 template <>
 __device__ __forceinline__ int64_t qload<BitT>(const strom_qual_batch &b, uint64_t i) {
   return (((const uint8_t *)b.values)[i >> 3] >> (i & 7)) & 1;
+}
+template <>
+__device__ __forceinline__ __int128 qload<Dec128T>(const strom_qual_batch &b, uint64_t i) {
+  const uint64_t *p = (const uint64_t *)b.values + 2 * i;   // Arrow buffers: 8-byte aligned
+  return (__int128)(((unsigned __int128)(uint64_t)p[1] << 64) | p[0]);
 }
 
 // sorted disjoint inclusive ranges in LDS: linear for a few, else a binary
@@ -534,7 +544,7 @@ __global__ __launch_bounds__(256) void qual_kernel(strom_col_qual q,
                                                    const uint64_t *__restrict__ or_src, int and_dst,
                                                    unsigned long long *__restrict__ count) {
   typedef typename CmpOf<T>::type CT;
-  extern __shared__ uint32_t qs[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t qs[];
   __shared__ uint32_t wave_cnt[4];
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // constants -> LDS (consts, then the string (start, len) pairs)
@@ -666,6 +676,7 @@ int qual_by_type(const strom_col_qual &q, const strom_qual_batch *bt, uint32_t n
       case STROM_COL_F32: return launch_qual<float, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
       case STROM_COL_F64: return launch_qual<double, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
       case STROM_COL_BOOL: return launch_qual<BitT, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
+      case STROM_COL_DEC128: return launch_qual<Dec128T, K>(q, bt, nb, nw, bm, orv, and_dst, cnt, st);
       default: break;
     }
   }
@@ -740,7 +751,8 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
                                          void *d_pout, uint8_t *d_pvalid, void *stream) {
   if (!nwords || !nbatches) return 0;
   if (!d_bitmap || !d_batches || !d_out || !d_total) return -22;
-  if (d_proj && ((width != 1 && width != 2 && width != 4 && width != 8) || !d_pout)) return -22;
+  if (d_proj && ((width != 1 && width != 2 && width != 4 && width != 8 && width != 16) || !d_pout))
+    return -22;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
   if (nb64 > 0xffffffffull) return -75;
@@ -753,6 +765,9 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
   if (!d_proj)
     hipLaunchKernelGGL(emit_rows_kernel<0>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
                        nbatches, cnt, d_out, nullptr, nullptr, nullptr);
+  else if (width == 16)
+    hipLaunchKernelGGL(emit_rows_kernel<16>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
+                       nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
   else if (width == 8)
     hipLaunchKernelGGL(emit_rows_kernel<8>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
                        nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
@@ -792,7 +807,7 @@ extern "C" int strom_column_qual(const strom_col_qual *q, const strom_qual_batch
   }
   switch (q->op) {
     case STROM_QOP_RANGES: {
-      const uint64_t need = 16ull * q->nconst;
+      const uint64_t need = (q->type == STROM_COL_DEC128 ? 32ull : 16ull) * q->nconst;
       if (str || q->const_bytes < need) return -22;
       return qual_by_type<QK_RANGE>(*q, d_batches, nbatches, nwords, d_bitmap, d_or, and_dst, d_count, st);
     }

@@ -273,6 +273,8 @@ class ArrowScan:
             st = col.storage
             if st == "b1":
                 dneed = (n + 7) // 8
+            elif st == "d16":
+                dneed = n * 16
             elif col.kind in ("utf8", "binary") and col.dictionary is None:
                 dneed = np.where(n > 0, (n + 1) * (8 if col.large else 4), 0)
             else:
@@ -689,6 +691,9 @@ class ArrowScan:
                 nch = sum(int(g.aux_len[:, pcol].sum()) for g in groups)
                 pchars = torch.empty(max(nch, 1), dtype=torch.uint8, device=self.device)
                 poff = torch.empty(max(nrows, 1) + 1, dtype=torch.int64, device=self.device)
+            elif st == "d16":
+                # decimal128: (lo, hi) int64 words per row, value x 10^scale
+                pout = torch.empty((max(nrows, 1), 2), dtype=torch.int64, device=self.device)
             elif st not in _TORCH:
                 raise NotImplementedError(f"projection of {project} ({pmeta.kind}): fixed-width, "
                                           "utf8/binary or dictionary-encoded columns")

@@ -100,9 +100,9 @@ def bitmap_to_rows(bitmap: torch.Tensor, nwords: int, batches: torch.Tensor, out
     if proj is not None:
         if proj_out is None or proj.shape != batches.shape:
             raise ValueError("projection needs proj_out and a table of the same batches")
-        width = proj_out.element_size()
-        if width not in (1, 2, 4, 8):
-            raise ValueError("projected values are 1, 2, 4 or 8 bytes")
+        width = proj_out.element_size() * (proj_out.shape[1] if proj_out.dim() == 2 else 1)
+        if width not in (1, 2, 4, 8, 16):
+            raise ValueError("projected values are 1, 2, 4, 8 or 16 bytes")
         pptr = ptr(proj_out)
         vptr = ptr(proj_valid) if proj_valid is not None else 0
     check(lib().strom_bitmap_to_rows_proj(ptr(bitmap), nwords, ptr(batches), batches.shape[0],

@@ -45,7 +45,7 @@ from ..utils.arrow_ipc import Column
 
 # strom.h: STROM_COL_* storage types, STROM_QOP_* operators, STROM_QUAL_* flags
 COL_CODE = {"i4": 1, "i8": 2, "f4": 3, "f8": 4, "i1": 5, "i2": 6, "u1": 7, "u2": 8, "u4": 9,
-            "u8": 10, "b1": 11}
+            "u8": 10, "b1": 11, "d16": 14}
 COL_STR32, COL_STR64 = 12, 13
 QOP_RANGES, QOP_STR_IN, QOP_STR_PREFIX, QOP_LUT, QOP_VALID, QOP_STR_RANGES = 1, 2, 3, 4, 5, 6
 FLAG_NEGATE, FLAG_NAN = 1, 2
@@ -176,6 +176,11 @@ def _exact(v, col: Column) -> Fraction:
         if math.isnan(v) or math.isinf(v):
             raise OverflowError
         return Fraction(float(v))
+    import decimal as _dec
+    if isinstance(v, _dec.Decimal):
+        if not v.is_finite():
+            raise OverflowError
+        return Fraction(v)
     k = col.kind
     tick = Fraction(86400) if col.unit == "d" else Fraction(1, _TICKS.get(col.unit, 1))
     if hasattr(v, "to_datetime64") or hasattr(v, "to_timedelta64"):   # pandas scalars
@@ -207,6 +212,8 @@ def _exact(v, col: Column) -> Fraction:
 def _int_bounds(dt: str) -> Tuple[int, int]:
     if dt == "b1":
         return 0, 1
+    if dt == "d16":
+        return -(1 << 127), (1 << 127) - 1
     info = np.iinfo(np.dtype(dt))
     return int(info.min), int(info.max)
 
@@ -265,9 +272,11 @@ def _num_ranges(op: str, v, col: Column, dt: str) -> Tuple[List[Tuple], int]:
     else:
         tmin, tmax = _int_bounds(dt)
 
+        scale = Fraction(10) ** col.scale if col.kind == "decimal" else 1
+
         def bound(x, side):
             try:
-                e = _exact(x, col)
+                e = _exact(x, col) * scale
             except OverflowError:               # NaN compares false, +-inf past any int
                 if isinstance(x, (float, np.floating)) and math.isinf(x):
                     return tmax + 1 if x > 0 else tmin - 1
@@ -391,6 +400,11 @@ def _compile_value(p: Pred, col: Column, dt: str, code: int) -> Compiled:
     rs, extra = _num_ranges(base, p.value, col, dt)
     if len(rs) > MAX_RANGES:
         raise ValueError(f"column {col.name}: {len(rs)} disjoint ranges (limit {MAX_RANGES})")
+    if dt == "d16":
+        # 128-bit bounds, (lo, hi) pairs of little-endian two's complement
+        blob = b"".join(int(x).to_bytes(16, "little", signed=True) for r in rs for x in r)
+        return Compiled(code, QOP_RANGES, flags | extra, len(rs), blob or b"\0" * 32,
+                        ranges=np.array(rs, dtype=object).reshape(-1, 2))
     isf = dt in ("f4", "f8")
     cdt = np.float64 if isf else (np.uint64 if dt == "u8" else np.int64)
     arr = np.asarray(rs, dtype=cdt).reshape(-1, 2)
@@ -413,7 +427,7 @@ def compile_pred(p: Pred, col: Column, dictionary=None) -> Compiled:
             raise ValueError(f"column {col.name}: dictionary values needed")
         vals, dvalid = dictionary
         vcol = Column(col.name, col.kind, col.bit_width, col.signed, unit=col.unit, tz=col.tz,
-                      large=col.large)
+                      large=col.large, precision=col.precision, scale=col.scale)
         inner = compile_pred(p, vcol)
         n = len(vals[0]) - 1 if isinstance(vals, tuple) else len(vals)
         hit = evaluate(inner, vals, dvalid, n)
@@ -440,6 +454,12 @@ def evaluate(c: Compiled, values, valid: Optional[np.ndarray], n: int) -> np.nda
     ok = np.ones(n, bool) if valid is None else np.asarray(valid[:n], bool)
     if c.op == QOP_VALID:
         return ~ok if c.flags & FLAG_NEGATE else ok
+    if c.op == QOP_RANGES and c.type == COL_CODE["d16"]:
+        rs = [(int(a), int(b)) for a, b in c.ranges]
+        hit = np.array([any(a <= int(x) <= b for a, b in rs) for x in values[:n]], bool)
+        if c.flags & FLAG_NEGATE:
+            hit = ~hit
+        return hit & ok
     if c.op == QOP_RANGES:
         x = np.asarray(values[:n])
         if x.dtype == bool:

@@ -108,6 +108,8 @@ class Column:
     tz: str = ""               # timestamp time zone ("" = naive)
     large: bool = False        # utf8/binary with 64-bit offsets
     dictionary: Optional[DictEncoding] = None
+    precision: int = 0         # decimal: digits, and the power of ten the stored integer
+    scale: int = 0             # is divided by
 
     @property
     def storage(self) -> str:
@@ -121,6 +123,8 @@ class Column:
             return "i8" if self.large else "i4"
         if self.kind == "bool":
             return "b1"
+        if self.kind == "decimal":
+            return "d16"       # 128-bit two's complement, little-endian
         if self.kind == "float":
             return {16: "f2", 32: "f4", 64: "f8"}[self.bit_width]
         if self.kind in _INTLIKE:
@@ -134,8 +138,8 @@ class Column:
 
 _INTLIKE = ("int", "date", "time", "timestamp", "duration")
 # Schema.fbs Type union ids
-(_TY_INT, _TY_FP, _TY_BIN, _TY_UTF8, _TY_BOOL, _TY_DATE, _TY_TIME, _TY_TS, _TY_DUR,
- _TY_LBIN, _TY_LUTF8) = 2, 3, 4, 5, 6, 8, 9, 10, 18, 19, 20
+(_TY_INT, _TY_FP, _TY_BIN, _TY_UTF8, _TY_BOOL, _TY_DEC, _TY_DATE, _TY_TIME, _TY_TS, _TY_DUR,
+ _TY_LBIN, _TY_LUTF8) = 2, 3, 4, 5, 6, 7, 8, 9, 10, 18, 19, 20
 _TUNIT = ("s", "ms", "us", "ns")       # TimeUnit enum
 # own buffer count per Schema.fbs Type id (None = layout not walkable here)
 _NBUF = {1: 0, 2: 2, 3: 2, 4: 3, 5: 3, 6: 2, 7: 2, 8: 2, 9: 2, 10: 2, 11: 2, 12: 2, 13: 1,
@@ -154,6 +158,12 @@ def _value_type(name: str, nullable: bool, ttype: int, t: Optional[FB]) -> Colum
         return Column(name, "float", bits, True, nullable, supported=bits != 16)
     if ttype == _TY_BOOL:
         return Column(name, "bool", 1, False, nullable)
+    if ttype == _TY_DEC:
+        # Decimal{precision, scale, bitWidth = 128}: decimal128 is scanned,
+        # decimal256 listed only
+        bits = g(2, "i", 128)
+        return Column(name, "decimal", bits, True, nullable, supported=bits == 128,
+                      precision=g(0, "i", 0), scale=g(1, "i", 0))
     if ttype in (_TY_UTF8, _TY_LUTF8, _TY_BIN, _TY_LBIN):
         return Column(name, "utf8" if ttype in (_TY_UTF8, _TY_LUTF8) else "binary", 0, False,
                       nullable, nbuffers=3, large=ttype in (_TY_LBIN, _TY_LUTF8))
@@ -535,6 +545,10 @@ def decode_values(col: Column, length: int, data: bytes, extra: bytes = b""):
         offs = np.frombuffer(data, "<i8" if col.large else "<i4", length + 1) if length else \
             np.zeros(1, np.int64)
         return offs.astype(np.int64), np.frombuffer(extra, np.uint8)
+    if col.kind == "decimal":
+        # the stored 128-bit integers (value x 10^scale) as Python ints
+        return np.array([int.from_bytes(data[16 * i:16 * i + 16], "little", signed=True)
+                         for i in range(length)], dtype=object)
     dt = np.dtype("<" + (Column(col.name, col.kind, col.bit_width, col.signed).storage))
     return np.frombuffer(data, dt, length)
 

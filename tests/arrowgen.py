@@ -4,6 +4,7 @@ parity test and the GPU test)."""
 from __future__ import annotations
 
 import datetime as dt
+import decimal
 
 import numpy as np
 
@@ -37,6 +38,8 @@ def table(n: int = 3000, seed: int = 5):
         "bin": pa.array([x.encode() for x in s], pa.binary()),
         "ls": pa.array(s, pa.large_string()),
         "dict": pa.array([words[k] for k in rng.integers(0, 9, n)], mask=nulls()).dictionary_encode(),
+        "dec": pa.array([decimal.Decimal(int(v)).scaleb(-4) for v in
+                         rng.integers(-10**9, 10**9, n)], pa.decimal128(18, 4), mask=nulls()),
         "idict": pa.DictionaryArray.from_arrays(
             pa.array(rng.integers(0, 20, n).astype(np.int8)),
             pa.array(np.arange(20, dtype=np.int64) * 1000 - 3000)),
@@ -129,6 +132,13 @@ def cases():
          lambda t: rng_(dec(t, "dict"), "ab", "apple")),
         ("dict is_null", P("dict").is_null(), lambda t: pc.is_null(c(t, "dict"))),
         ("idict >", P("idict") > 5000, lambda t: pc.greater(dec(t, "idict"), 5000)),
+        ("dec > ", P("dec") > decimal.Decimal("12.3456"),
+         lambda t: pc.greater(c(t, "dec"), pa.scalar(decimal.Decimal("12.3456"), pa.decimal128(18, 4)))),
+        ("dec between", P("dec").between(-5, 7.25),
+         lambda t: rng_(c(t, "dec"), pa.scalar(decimal.Decimal("-5"), pa.decimal128(18, 4)),
+                        pa.scalar(decimal.Decimal("7.25"), pa.decimal128(18, 4)))),
+        ("dec in", P("dec").isin([decimal.Decimal("0.0001"), 3]),
+         lambda t: isin(c(t, "dec"), [decimal.Decimal("0.0001"), decimal.Decimal("3.0000")])),
         ("or across columns", Or(P("i8") < -100, P("s") == "apple", P("b") == True),  # noqa: E712
          lambda t: pc.or_kleene(pc.or_kleene(pc.less(c(t, "i8"), -100), pc.equal(c(t, "s"), "apple")),
                           pc.equal(c(t, "b"), True))),

@@ -33,6 +33,8 @@ def test_metadata_kinds(arrow_file):
     assert kinds["ls"] == ("utf8", "i8", "") and kinds["bin"] == ("binary", "i4", "")
     assert kinds["dict"] == ("utf8", "i4", "") and m.schema[m.column_index("dict")].dictionary
     assert kinds["idict"] == ("int", "i1", "")
+    assert kinds["dec"] == ("decimal", "d16", "")
+    assert m.schema[m.column_index("dec")].scale == 4
     assert m.schema[m.column_index("ts")].tz == "UTC"
     assert all(c.supported for c in m.schema)
 

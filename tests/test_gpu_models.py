@@ -282,6 +282,16 @@ def test_arrow_scan_predicate_kinds(S, tmp_path, codec):
             want = [col[int(r)].as_py() for r in ids]
             want = [w.encode() if isinstance(w, str) else w for w in want]
             assert all(g == w for g, w, v in zip(got, want, ok) if v), pc_name
+        # decimal128 projection: (lo, hi) words of the scaled integer
+        out = sc.scan_where([P("i8") > 30], project="dec")
+        ids = out.indices.cpu().numpy()
+        w = out.values.cpu().numpy().astype(np.uint64)
+        got = [int(lo) | (int(hi) << 64) for lo, hi in w]
+        got = [g - (1 << 128) if g >> 127 else g for g in got]
+        dcol = tbl.column("dec").combine_chunks()
+        ok = np.asarray(dcol.is_valid())[ids]
+        want = [int(dcol[int(r)].as_py().scaleb(4)) if v else None for r, v in zip(ids, ok)]
+        assert all(g == x for g, x, v in zip(got, want, ok) if v)
         host = sc.host_scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
         assert np.array_equal(sc.scan_where([P("s").startswith("ap"), P("u32") < 1 << 31])
                               .indices.cpu().numpy(), host.indices)
