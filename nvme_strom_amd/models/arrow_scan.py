@@ -285,7 +285,10 @@ class ArrowScan:
                                     ("characters", a.x_off, a.x_len, xneed)):
                 if nd is None:
                     continue
-                short = ~comp & (ln < nd)
+                # a raw buffer shorter than its rows, or an empty one (compressed
+                # or not) for a non-empty batch, would send the kernels past
+                # the bytes the plan reserves for it
+                short = (~comp & (ln < nd)) | ((ln == 0) & (nd > 0))
                 if short.any():
                     b = int(np.flatnonzero(short)[0])
                     raise ValueError(f"column {col.name}, record batch {b}: {what} buffer of "
