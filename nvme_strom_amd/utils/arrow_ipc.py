@@ -470,7 +470,15 @@ def _read(src: "_Src", native: bool = False) -> ArrowFile:
 def _dictionaries(src: "_Src", footer: FB, fbuf: bytes) -> Dict[int, List[DictBatch]]:
     """Footer.dictionaries -> DictionaryBatch messages (Message.fbs
     header_type 2: DictionaryBatch{id, data: RecordBatch, isDelta}).  Only
-    their headers are read here; values are decoded when a scan needs them."""
+    their headers are read here; values are decoded when a scan needs them.
+    The file is input data: a malformed header is a ValueError."""
+    try:
+        return _dictionaries_walk(src, footer, fbuf)
+    except (struct.error, IndexError, UnicodeDecodeError) as e:
+        raise ValueError(f"malformed dictionary batch header: {e}") from None
+
+
+def _dictionaries_walk(src: "_Src", footer: FB, fbuf: bytes) -> Dict[int, List[DictBatch]]:
     start, n = footer.vector(2)
     out: Dict[int, List[DictBatch]] = {}
     for k in range(n):

@@ -119,3 +119,29 @@ def test_compile_exact_bounds():
     assert CP.clauses([("x", 1, 2), ("x", "in", [1]), CP.Or(("x", "==", 1), CP.P("y") > 0)]) == [
         [CP.Pred("x", "between", (1, 2))], [CP.Pred("x", "in", [1])],
         [CP.Pred("x", "==", 1), CP.Pred("y", ">", 0)]]
+
+
+def test_dictionary_headers_malformed(tmp_path):
+    """Corrupted DictionaryBatch headers end in a ValueError (or a file that
+    still parses), never another exception type."""
+    import pyarrow.ipc as ipc
+    from nvme_strom_amd.utils.arrow_ipc import read_metadata
+    tbl = pa.table({"d": pa.array(["x", "y", "z"] * 100).dictionary_encode(),
+                    "i": np.arange(300)})
+    path = str(tmp_path / "d.arrow")
+    with ipc.new_file(path, tbl.schema) as w:
+        w.write_table(tbl)
+    m = read_metadata(path)
+    blk = m.dicts[0][0].buffers[0].offset        # the dictionary batch body
+    raw = bytearray(open(path, "rb").read())
+    rng = np.random.default_rng(4)
+    for trial in range(60):
+        bad = bytearray(raw)
+        pos = int(rng.integers(max(8, blk - 200), blk))
+        bad[pos:pos + 4] = rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        p = str(tmp_path / f"b{trial}.arrow")
+        open(p, "wb").write(bad)
+        try:
+            read_metadata(p, native=False)
+        except ValueError:
+            pass
