@@ -1480,8 +1480,18 @@ struct alignas(16) Ent {                        // a decoded sequence (HBM)
   uint32_t ll, off, lst, ost;                   // ost: output start in the block
 };
 
+// a block of a group, with the frame's Huffman-tree and FSE-table
+// definitions as that block sees them (positions in the input, resolved by
+// the prewalk: a treeless / repeat-mode block rebuilds its tables from
+// them on whatever wave decodes it)
+struct FpDefs {
+  uint32_t hbits, hdesc, hdesc_end;
+  uint32_t have[3], tmode[3], tpos[3], tend[3];
+};
+
 struct FpBlk {
   uint32_t bstart, bend, btype, bsize, blast;
+  FpDefs d;
 };
 
 // the frame's state while its blocks decode on every wave (wave 0's Smem
@@ -1545,48 +1555,100 @@ HD uint32_t sym_resolve(uint32_t v, const uint32_t *rin) {
 // lane 0 of wave 0: the next up to nw block headers of the current frame
 // (parsing the frame header first when one starts).  serial = 1 when a
 // block needs a predecessor's tree / table, or the stream is stored.
+// the definitions block s.bstart.. leaves for its successors: a Huffman
+// description (literals type 2) and the LL / OF / ML table definitions of
+// its sequence section (the table descriptions are walked with fse_norm to
+// find where each ends).  false: a header it cannot follow.
+HD bool prewalk_defs(Smem &s, const Ctx &c, FpDefs &d) {
+  const uint32_t p = s.bstart, end = s.bend, b0 = gbyte(c, p), lt = b0 & 3, sf = (b0 >> 2) & 3;
+  uint32_t q;
+  if (lt <= 1) {
+    const uint32_t hl = (sf & 1) == 0 ? 1 : sf == 1 ? 2 : 3;
+    const uint32_t R = hl == 1 ? b0 >> 3 : hl == 2 ? (b0 >> 4) + (gbyte(c, p + 1) << 4)
+                               : (b0 >> 4) + (gbyte(c, p + 1) << 4) + (gbyte(c, p + 2) << 12);
+    q = p + hl + (lt == 0 ? R : 1);
+  } else {
+    const uint32_t hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5, bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
+    uint64_t h = 0;
+    for (uint32_t j = 0; j < hl; ++j) h |= (uint64_t)gbyte(c, p + j) << (8 * j);
+    const uint32_t C = (uint32_t)(h >> (4 + bits)) & ((1u << bits) - 1);
+    if (lt == 2) {                                 // a new tree: lit_header's hdesc / hdesc_end
+      d.hbits = 1;
+      d.hdesc = p + hl;
+      d.hdesc_end = p + hl + C;
+    } else if (!d.hbits) {
+      return false;                                // treeless with no tree before it
+    }
+    q = p + hl + C;
+  }
+  if (q >= end) return false;
+  const uint32_t n0 = gbyte(c, q);
+  if (n0 == 0) return true;                        // no sequences: no tables
+  q += n0 < 128 ? 1 : n0 < 255 ? 2 : 3;
+  if (q >= end) return false;
+  const uint32_t modes = gbyte(c, q++);
+  for (uint32_t k = 0; k < 3; ++k) {               // LL, OF, ML (seq_header's order)
+    const uint32_t kind = k == 0 ? kLL : k == 1 ? kOF : kML;
+    const uint32_t mode = (modes >> (6 - 2 * k)) & 3;
+    if (mode == 3) {
+      if (!d.have[kind]) return false;
+      continue;
+    }
+    d.tmode[kind] = mode;
+    d.tpos[kind] = q;
+    d.tend[kind] = end;
+    d.have[kind] = 1;
+    if (mode == 1) {
+      ++q;
+    } else if (mode == 2) {
+      FR fr{q, end, 0};
+      uint32_t nsym, al;
+      const uint32_t maxsym = kind == kLL ? 35 : kind == kML ? 52 : 31;
+      if (!fse_norm(c, fr, s.norm, maxsym, kind == kOF ? 8 : 9, nsym, al)) return false;
+      q += fr.bit >> 3;
+    }
+  }
+  return true;
+}
+
+HD void defs_of(FpDefs &d, const Smem &s) {
+  d.hbits = s.hbits ? 1u : 0u;
+  d.hdesc = s.hdesc;
+  d.hdesc_end = s.hdesc_end;
+  d.have[kLL] = s.have_ll;
+  d.have[kOF] = s.have_of;
+  d.have[kML] = s.have_ml;
+  for (uint32_t k = 0; k < 3; ++k) {
+    d.tmode[k] = s.tmode[k];
+    d.tpos[k] = s.tpos[k];
+    d.tend[k] = s.tend[k];
+  }
+}
+
 HD void prewalk(Smem &s, const Ctx &c, FpShared &f, uint32_t nw) {
   f.nblk = 0;
   f.serial = 0;
+  FpDefs d;
+  bool fresh = true;                               // definitions not read yet
   for (uint32_t k = 0; k < nw; ++k) {
     next_block(s, c);
     if (s.err || s.state == kDone) break;
+    if (fresh) {                                   // the frame's (a new frame reset them)
+      defs_of(d, s);
+      fresh = false;
+    }
     FpBlk &b = f.blk[k];
     b.bstart = s.bstart;
     b.bend = s.bend;
     b.btype = s.btype;
     b.bsize = s.bsize;
     b.blast = s.blast;
-    if (s.btype == kComp) {
-      // literal section type + size, then the sequence modes byte
-      const uint32_t p = s.bstart, b0 = gbyte(c, p), lt = b0 & 3, sf = (b0 >> 2) & 3;
-      uint32_t q;
-      if (lt <= 1) {
-        const uint32_t hl = (sf & 1) == 0 ? 1 : sf == 1 ? 2 : 3;
-        const uint32_t R = hl == 1 ? b0 >> 3 : hl == 2 ? (b0 >> 4) + (gbyte(c, p + 1) << 4)
-                                   : (b0 >> 4) + (gbyte(c, p + 1) << 4) + (gbyte(c, p + 2) << 12);
-        q = p + hl + (lt == 0 ? R : 1);
-      } else {
-        const uint32_t hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5, bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
-        uint64_t h = 0;
-        for (uint32_t j = 0; j < hl; ++j) h |= (uint64_t)gbyte(c, p + j) << (8 * j);
-        q = p + hl + ((uint32_t)(h >> (4 + bits)) & ((1u << bits) - 1));
-      }
-      bool dep = lt == 3;                          // treeless literals
-      const uint32_t n0 = gbyte(c, q);
-      const uint32_t mpos = q + (n0 < 128 ? 1 : n0 < 255 ? 2 : 3);
-      if (n0 && q < s.bend) {
-        const uint32_t modes = gbyte(c, mpos);
-        dep |= (modes >> 6) == 3 || ((modes >> 4) & 3) == 3 || ((modes >> 2) & 3) == 3;
-      }
-      // a block that needs a predecessor's tree / table starts the next
-      // group, and a group starting with one runs it alone, serially, on
-      // wave 0 (which holds the definitions)
-      if (dep && k) {
-        f.nblk = k;
-        break;
-      }
-      if (dep) f.serial = 1;
+    b.d = d;
+    if (s.btype == kComp && !prewalk_defs(s, c, d)) {
+      // a header the walk cannot follow: the block runs alone on wave 0,
+      // whose own decode reports the error
+      if (k) break;
+      f.serial = 1;
     }
     f.nblk = k + 1;
     if (s.blast) break;
@@ -1621,8 +1683,19 @@ HD void decode_fp(TM &tm, Smem &s, const Ctx &c, const FpBlk &b, Ent *ent, uint3
     s.ip = b.bstart;
     s.op = 0;                                      // block-relative until it executes
     s.fstart = 0;
-    s.hbits = 0;
-    s.have_ll = s.have_of = s.have_ml = 0;
+    // the definitions this block may refer to (treeless literals,
+    // repeat-mode tables), as the prewalk resolved them
+    s.hbits = b.d.hbits;
+    s.hdesc = b.d.hdesc;
+    s.hdesc_end = b.d.hdesc_end;
+    s.have_ll = b.d.have[kLL];
+    s.have_of = b.d.have[kOF];
+    s.have_ml = b.d.have[kML];
+    for (uint32_t k = 0; k < 3; ++k) {
+      s.tmode[k] = b.d.tmode[k];
+      s.tpos[k] = b.d.tpos[k];
+      s.tend[k] = b.d.tend[k];
+    }
     s.rep[0] = kSym | (0u << 26);
     s.rep[1] = kSym | (1u << 26);
     s.rep[2] = kSym | (2u << 26);
