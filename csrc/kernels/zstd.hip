@@ -2393,6 +2393,9 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
 
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
 
+// frame-parallel workgroups (streams) resident per CU
+extern "C" uint32_t strom_zstd_fp_per_cu(void) { return zs::fp_per_cu(); }
+
 // Decoder choice: -1 by the stream count (default), 0 wave per stream,
 // 1 frame-parallel.  Returns the previous setting.
 extern "C" int strom_zstd_fp_mode(int mode) {

@@ -263,6 +263,7 @@ _SIGS = {
     "strom_zstd_scratch_sizes": (None, [C.c_void_p]),
     "strom_zstd_host_fp_stats": (None, [C.c_void_p]),
     "strom_zstd_fp_mode": (C.c_int, [C.c_int]),
+    "strom_zstd_fp_per_cu": (C.c_uint32, []),
     "strom_decompress_zstd_mode": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
                                              C.c_void_p, C.c_int]),

@@ -320,7 +320,10 @@ class ArrowScan:
             # latency each (A/B, profiles/r3/zstd/arrow_group_div_ab.json:
             # val 11.0-12.8 GB/s at a round, 5.8 at a quarter, 4.2 at an eighth)
             from .. import _native as N
-            rnd = cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
+            if self.ZSTD_MODE == 1:             # frame-parallel: its own round
+                rnd = cus * max(1, int(N.lib().strom_zstd_fp_per_cu()))
+            else:
+                rnd = cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))
             return max(1, rnd // self.ZSTD_ROUND_DIV)
         return self.ROUND_STREAMS_PER_CU * cus
 
@@ -385,11 +388,16 @@ class ArrowScan:
         bounds = []
         a = 0
         firstl, lastl, cuml = first.tolist(), last.tolist(), cum.tolist()
+        # decoder streams per group: at most one resident round (the byte
+        # budget above only approximates it: buffers straddle chunks)
+        rnd_cut = self._round_streams() if ncomp else 0
+        sc = np.concatenate([[0], np.cumsum(real.sum(axis=1))]).tolist()
         for b in range(nb):
             s0, e1 = firstl[a], lastl[b]
             # distinct chunks of batches [a, b]: the first pair counts too
             d = (cuml[e1] - cuml[s0 + 1] + 1) if e1 > s0 else 0
-            if b > a and d > limit:
+            over = rnd_cut and sc[b + 1] - sc[a] > rnd_cut
+            if b > a and (d > limit or over):
                 bounds.append((a, b))
                 a = b
         if nb:
