@@ -388,16 +388,11 @@ class ArrowScan:
         bounds = []
         a = 0
         firstl, lastl, cuml = first.tolist(), last.tolist(), cum.tolist()
-        # decoder streams per group: at most one resident round (the byte
-        # budget above only approximates it: buffers straddle chunks)
-        rnd_cut = self._round_streams() if ncomp else 0
-        sc = np.concatenate([[0], np.cumsum(real.sum(axis=1))]).tolist()
         for b in range(nb):
             s0, e1 = firstl[a], lastl[b]
             # distinct chunks of batches [a, b]: the first pair counts too
             d = (cuml[e1] - cuml[s0 + 1] + 1) if e1 > s0 else 0
-            over = rnd_cut and sc[b + 1] - sc[a] > rnd_cut
-            if b > a and (d > limit or over):
+            if b > a and d > limit:
                 bounds.append((a, b))
                 a = b
         if nb:
