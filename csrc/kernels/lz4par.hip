@@ -93,6 +93,27 @@ static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 // ~100 bytes to fall onto the true token grid on int columns, and a slice
 // whose chain has not merged by its true entry costs a serial fix-up round
 constexpr uint32_t LB = LZ4PAR_LOOKBACK;
+// LZ4: NW speculative walkers per slice instead of one, started WLB,
+// WLB - 1, ... bytes before it (NW = 1: the single chain from LB).  One
+// chain phase-locks on dense LZ4 (text: 3-byte sequences whose offset high
+// byte is 0 read as a token with no literals and a short match, so a chain
+// entering 2 bytes late stays 2 bytes late): 30 % of text slices' chains
+// never met the true one (16 windows x 36 validation rounds, 51 % of the
+// decode's cycles).  Walkers from consecutive bytes start on every phase;
+// they advance lowest position first and merge where they meet, so the
+// steps are those of the distinct positions.  Replay of pyarrow's frames
+// (tools/lz4par_bench.py kinds): text 30 % -> 0 % slices unmatched at
+// 124 steps per slice instead of 189, val 0.35 % -> 0.35 % at 53 instead
+// of 115 (r4 host simulation, profiles/r4/dec/lz4par_walkers.json).
+#ifndef LZ4PAR_WALKERS
+#define LZ4PAR_WALKERS 4
+#endif
+#ifndef LZ4PAR_WLOOKBACK
+#define LZ4PAR_WLOOKBACK 128
+#endif
+constexpr uint32_t NW = LZ4PAR_WALKERS;
+constexpr uint32_t WLB = LZ4PAR_WLOOKBACK;
+static_assert(NW >= 1 && NW <= 8 && WLB >= NW, "walkers");
 #ifndef LZ4PAR_RESTART
 #define LZ4PAR_RESTART 1
 #endif
@@ -114,13 +135,23 @@ enum : uint32_t { kModeBlock = 0, kModeDone = 1 };
 HD constexpr uint32_t WI(uint32_t r) { return r + ((r >> 7) << 2); }
 HD constexpr uint32_t PI(uint32_t e) { return e + (e >> 5); }
 
+// the walkers' marks and exits (LZ4, NW > 1), live from the speculation to
+// the end of validation: they share LDS with the pointer batch, live after
+struct WalkMem {
+  uint32_t bits[NW * (PW / 32)];   // walker j, slice t: bits[j * PW / 32 + SW * t + i]
+  uint32_t ex[NW * NT];            // walker j, slice t: ex[j * NT + t]
+};
+
 struct Smem {
   uint8_t win[WI(PW + PAD) + 4];
-  uint32_t bits[PW / 32];
+  uint32_t bits[PW / 32];  // the chain slice t follows (a walker's, or a fix-up's)
   uint32_t ex[NT];       // exit of slice t's chain
   uint32_t en[NT];       // true entry of slice t
   uint32_t ost[NT];      // output bytes of slice t's true sequences, then their inclusive prefix
-  uint32_t ptr[PI(OB)];
+  union {
+    uint32_t ptr[PI(OB)];
+    WalkMem wk;
+  };
   uint32_t hb[HW];       // run heads of the batch (entries whose pointer fill wrote)
   uint32_t hsum[HS];
   uint8_t ring[HR ? HR : 4];   // output byte at absolute position x: ring[x % HR]
@@ -139,6 +170,8 @@ struct Smem {
   uint32_t minfix;       // snappy: first slice not yet settled
   uint32_t cov;          // snappy: last slice settled by the current round
 };
+
+static_assert(sizeof(WalkMem) <= sizeof(uint32_t) * PI(OB), "walkers fit the pointer batch");
 
 struct Ctx {
   const uint8_t *in;
@@ -304,9 +337,109 @@ HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
   }
 }
 
+// (1') LZ4 speculative walkers of slice t.  Walker slots hold a position
+// and the mask of walker ids that have merged into them; every id keeps its
+// own marks (registers, fully unrolled: no scratch) and exit.  The slice
+// starts on walker 0's chain.
+HD void ph_spec_walk(Smem &s, const Ctx &c, uint32_t t) {
+  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
+  uint32_t wp[NW], wm[NW];
+  uint32_t *wb = s.wk.bits + SW * t;     // walker j's words: wb[j * PW / 32 + i]
+#pragma unroll
+  for (uint32_t w = 0; w < NW; ++w) {
+    const uint32_t back = WLB - w;
+    wp[w] = lo - s.ws > back ? lo - back : s.ws;   // the window start is a true token
+    wm[w] = lo < hi ? 1u << w : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < SW; ++i) wb[w * (PW / 32) + i] = 0;
+  }
+  for (;;) {
+    uint32_t pm = 0xffffffffu;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w)
+      if (wm[w] && wp[w] < pm) pm = wp[w];
+    if (pm >= hi) break;
+    // every walker at pm merges into the first of them
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w)
+      if (wm[w] && wp[w] == pm) m |= wm[w];
+    bool kept = false;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w)
+      if (wm[w] && wp[w] == pm) {
+        wm[w] = kept ? 0u : m;
+        kept = true;
+      }
+    // marks straight to LDS (the slice's words are this thread's): held in
+    // registers they cost 8 VGPRs and the 4th workgroup per CU
+    if (pm >= lo) {
+      const uint32_t r = pm - lo, bit = 1u << (r & 31);
+#pragma unroll
+      for (uint32_t w = 0; w < NW; ++w)
+        if ((m >> w) & 1u) wb[w * (PW / 32) + (r >> 5)] |= bit;
+    }
+    Seq q;
+    parse<false>(s, c, pm, s.bend, q);   // a failed parse: the chain goes on anyway
+    kept = false;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w)
+      if (wm[w] && wp[w] == pm && !kept) {
+        wp[w] = q.next;
+        kept = true;
+      }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < NW; ++j) {
+    uint32_t e = lo;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w)
+      if ((wm[w] >> j) & 1u) e = wp[w];
+    s.wk.ex[j * NT + t] = e;
+    if (j == 0) s.ex[t] = e;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = wb[i];
+}
+
+// The first walker of slice t whose chain holds position e (>= the slice
+// start), or NW: a chain through e is the true one from e on whatever
+// came before, and its earlier marks are never read (counting starts at
+// the entry), so for e past the slice an exit equal to e suffices
+HD uint32_t wv_holder(const Smem &s, uint32_t t, uint32_t e) {
+  const uint32_t hi = slice_hi(s, t);
+  for (uint32_t k = 0; k < NW; ++k) {
+    if (e < hi) {
+      const uint32_t r = e - s.ws;
+      if ((s.wk.bits[k * (PW / 32) + (r >> 5)] >> (r & 31)) & 1u) return k;
+    } else if (s.wk.ex[k * NT + t] == e) {
+      return k;
+    }
+  }
+  return NW;
+}
+
+// walker k's marks and exit become slice t's
+HD void wv_adopt(Smem &s, uint32_t t, uint32_t k) {
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = s.wk.bits[k * (PW / 32) + SW * t + i];
+  s.ex[t] = s.wk.ex[k * NT + t];
+}
+
+// slice t's chain from `ent`, if one of its walkers holds it
+HD bool adopt_walker(Smem &s, uint32_t t, uint32_t ent) {
+  const uint32_t k = wv_holder(s, t, ent);
+  if (k >= NW) return false;
+  wv_adopt(s, t, k);
+  return true;
+}
+
 // (1) speculative chain of slice t
 template <bool SN>
 HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
+  if constexpr (!SN && NW > 1) {
+    ph_spec_walk(s, c, t);
+    return;
+  }
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
   if (lo >= hi) {
@@ -386,6 +519,12 @@ HD uint32_t ph_serial(Smem &s, const Ctx &c, uint32_t f, uint32_t nsl) {
       p = s.ex[t];
       continue;
     }
+    if constexpr (!SN && NW > 1) {
+      if (p < hi && adopt_walker(s, t, p)) {
+        p = s.ex[t];
+        continue;
+      }
+    }
     for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
     Seq q;
     while (p < hi) {
@@ -419,6 +558,67 @@ HD bool serial_worth(const Smem &s, uint32_t f) {
   for (uint32_t i = 0; i < SW * (f + 1); ++i) tok += (uint32_t)__builtin_popcount(s.bits[i]);
   const uint32_t done = s.ex[f] - s.ws, rest = s.wend > s.ex[f] ? s.wend - s.ex[f] : 0;
   return (uint64_t)tok * rest <= (uint64_t)SERIAL_TOKENS * (done ? done : 1);
+}
+
+// (2*) LZ4 walker validation (NW > 1): no re-parse rounds.  Slice t's
+// transition map sends its walker j to the walker of slice t+1 that holds
+// j's exit (NW: none holds it); slice 0's walkers all start at the window
+// start, a true token, so the true chain of slice t is walker
+// (M_{t-1} o ... o M_0)(0) — an inclusive scan of map compositions, log2 NT
+// steps.  The first slice f whose walker comes out "none" re-parses from
+// its (final) entry; its map becomes the constant "the walker of f+1
+// holding my exit" (slices it passes whole, inside one literal run, too),
+// and the scan runs again.  Iterations: misses + 1 (text ~1 per 6 windows,
+// val ~1 per window), against ~36 re-parse rounds per text window before.
+// Maps pack NW + 1 4-bit entries, entry NW being "none" in and out.
+HD uint32_t wv_get(uint32_t m, uint32_t j) { return (m >> (4 * j)) & 15u; }
+
+HD uint32_t wv_const(uint32_t h) {
+  uint32_t m = 0;
+  for (uint32_t j = 0; j <= NW; ++j) m |= h << (4 * j);
+  return m;
+}
+
+// a after b
+HD uint32_t wv_compose(uint32_t a, uint32_t b) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j <= NW; ++j) m |= wv_get(a, wv_get(b, j)) << (4 * j);
+  return m;
+}
+
+// slice t's map (`fixed`: the slice's chain is final, from its re-parse)
+HD uint32_t wv_map(const Smem &s, uint32_t t, uint32_t nsl, bool fixed) {
+  if (t + 1 >= nsl) return wv_const(NW);
+  if (fixed) return wv_const(wv_holder(s, t + 1, s.ex[t]));
+  uint32_t m = NW << (4 * NW);
+  for (uint32_t j = 0; j < NW; ++j) m |= wv_holder(s, t + 1, s.wk.ex[j * NT + t]) << (4 * j);
+  return m;
+}
+
+// slice t re-parses from its final entry
+template <bool SN>
+HD void wv_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
+  const uint32_t hi = slice_hi(s, t);
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
+  uint32_t p = ent;
+  Seq q;
+  while (p < hi) {
+    setbit(s, p);
+    parse<SN>(s, c, p, s.bend, q);
+    p = q.next;
+  }
+  s.ex[t] = p;
+}
+
+// after slice f's re-parse: slice t lies wholly before f's exit (inside one
+// element), so its chain is empty and its exit f's
+HD bool wv_pass(Smem &s, uint32_t t, uint32_t f) {
+  const uint32_t e = s.ex[f];
+  if (t <= f || slice_lo(s, t) >= slice_hi(s, t) || slice_hi(s, t) > e) return false;
+  for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
+  s.ex[t] = e;
+  return true;
 }
 
 // (2') snappy validation: a SETTLED prefix instead of rounds in which every
@@ -894,6 +1094,12 @@ using namespace LZ4P_NS;
 // 80 VGPRs (6 waves per SIMD, 3 workgroups per CU — what round 3 measured
 // 85 -> 115 GB/s with) without spilling; the snappy instantiation keeps the
 // compiler's choice (it would spill there).
+// The 256-thread LZ4 kernel is held at 128 VGPRs (4 waves per SIMD: its
+// LDS allows 4 workgroups per CU); left alone the walkers' validation took
+// it to 149 and one workgroup less.
+#if !defined(LZ4PAR_WPE_LZ4) && LZ4PAR_NT == 256
+#define LZ4PAR_WPE_LZ4 4
+#endif
 #ifdef LZ4PAR_WPE
 #define LZ4PAR_OCC __attribute__((amdgpu_waves_per_eu(LZ4PAR_WPE)))
 #else
@@ -973,6 +1179,54 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
               if (!link) atomicMin(&s.minfix, t);
             }
             __syncthreads();
+          }
+          s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
+          __syncthreads();
+        } else if (NW > 1) {
+          const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+          const uint32_t lane = t & 63, wave = t >> 6;
+          bool fixed = false;
+          uint32_t mine = wv_map(s, t, nsl, false);
+          for (uint32_t r = 1;; ++r) {
+            LP_CNT(kLpNRound);
+            // inclusive scan of the maps: in the wave by shuffles, then
+            // the earlier waves' totals (s.hb is free until the count)
+            uint32_t x = mine;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+              const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+              if (lane >= d) x = wv_compose(x, y);
+            }
+            if (lane == 63) s.hb[wave] = x;
+            if (t == 0) s.minfix = NT;
+            __syncthreads();
+            for (uint32_t v = wave; v-- > 0;) x = wv_compose(x, s.hb[v]);
+            s.ost[t] = x;
+            __syncthreads();
+            const uint32_t w = t == 0 ? 0u : wv_get(s.ost[t - 1], 0);
+            if (t < nsl && !fixed && w >= NW) atomicMin(&s.minfix, t);
+            __syncthreads();
+            const uint32_t f = s.minfix;
+            if (t < nsl && t < f && !fixed) wv_adopt(s, t, w);
+            __syncthreads();
+            if (f >= nsl) break;
+            if (t == f) {
+              wv_fix<SN>(s, c, t, s.ex[t - 1]);
+              fixed = true;
+            }
+            __syncthreads();
+            if (wv_pass(s, t, f)) fixed = true;
+            __syncthreads();
+            if (r >= SERIAL_AFTER) {
+              if (t == 0) s.cov = serial_worth(s, f) ? 1u : 0u;
+              __syncthreads();
+              if (s.cov) {
+                if (t == 0) ph_serial<SN>(s, c, f + 1, nsl);
+                __syncthreads();
+                break;
+              }
+            }
+            if (fixed) mine = wv_map(s, t, nsl, true);
           }
           s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
           __syncthreads();
@@ -1169,6 +1423,38 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
             }
           for (uint32_t t = cov + 1; t < NT; ++t) flag[t] = t >= nsl || sn_link(s, t, s.ex[t - 1]);
           for (uint32_t t = S; t <= cov; ++t) flag[t] = true;
+        }
+        for (uint32_t t = 0; t < NT; ++t) s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
+      } else if (NW > 1) {
+        const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
+        uint32_t mp[NT];
+        for (uint32_t t = 0; t < NT; ++t) {
+          flag[t] = false;                      // fixed
+          mp[t] = wv_map(s, t, nsl, false);
+        }
+        for (uint32_t r = 1;; ++r) {
+          ++rounds;
+          uint32_t x = 0, f = NT;
+          for (uint32_t t = 0; t < NT; ++t) {   // ent[t]: slice t's walker
+            ent[t] = t == 0 ? 0u : wv_get(x, 0);
+            x = t == 0 ? mp[0] : wv_compose(mp[t], x);
+            if (t < nsl && !flag[t] && ent[t] >= NW && f == NT) f = t;
+          }
+          for (uint32_t t = 0; t < nsl && t < f; ++t)
+            if (!flag[t]) wv_adopt(s, t, ent[t]);
+          if (f >= nsl) break;
+          ++fixes;
+          wv_fix<SN>(s, c, f, s.ex[f - 1]);
+          flag[f] = true;
+          for (uint32_t t = f + 1; t < NT; ++t)
+            if (wv_pass(s, t, f)) flag[t] = true;
+          if (r >= SERIAL_AFTER && serial_worth(s, f)) {
+            serial += ph_serial<SN>(s, c, f + 1, nsl);
+            ++serial_windows;
+            break;
+          }
+          for (uint32_t t = 0; t < NT; ++t)
+            if (flag[t]) mp[t] = wv_map(s, t, nsl, true);
         }
         for (uint32_t t = 0; t < NT; ++t) s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
       } else {
