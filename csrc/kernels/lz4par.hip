@@ -114,6 +114,19 @@ constexpr uint32_t LB = LZ4PAR_LOOKBACK;
 constexpr uint32_t NW = LZ4PAR_WALKERS;
 constexpr uint32_t WLB = LZ4PAR_WLOOKBACK;
 static_assert(NW >= 1 && NW <= 8 && WLB >= NW, "walkers");
+// A stream starts with the single chain (int columns merge: ~1.5 rounds a
+// window, and the walkers cost their lockstep: val 110 -> 98 GB/s when
+// always on) and switches to the walkers — that window again, and the
+// stream's later ones — once a window needs WALK_AFTER rounds without the
+// serial walk taking over (text: 36 rounds; a literal-heavy column goes
+// serial at SERIAL_AFTER and stays).  The thresholds keep every window of
+// the bench's 32 val frames single-chain (its worst needs 9 rounds at 64-
+// byte slices, 23 at 32): one switched stream in 16 cost val 7 % of its
+// GB/s, the launch waiting for its slowest workgroups.
+#ifndef LZ4PAR_WALK_AFTER
+#define LZ4PAR_WALK_AFTER (LZ4PAR_NT == 512 ? 24 : 10)
+#endif
+constexpr uint32_t WALK_AFTER = LZ4PAR_WALK_AFTER;
 #ifndef LZ4PAR_RESTART
 #define LZ4PAR_RESTART 1
 #endif
@@ -169,6 +182,7 @@ struct Smem {
   uint32_t expect;       // snappy: the preamble's decoded length (else ~0)
   uint32_t minfix;       // snappy: first slice not yet settled
   uint32_t cov;          // snappy: last slice settled by the current round
+  uint32_t walk;         // LZ4: this stream speculates with walkers (WALK_AFTER)
 };
 
 static_assert(sizeof(WalkMem) <= sizeof(uint32_t) * PI(OB), "walkers fit the pointer batch");
@@ -435,10 +449,12 @@ HD bool adopt_walker(Smem &s, uint32_t t, uint32_t ent) {
 
 // (1) speculative chain of slice t
 template <bool SN>
-HD void ph_spec(Smem &s, const Ctx &c, uint32_t t) {
+HD void ph_spec(Smem &s, const Ctx &c, uint32_t t, bool walk) {
   if constexpr (!SN && NW > 1) {
-    ph_spec_walk(s, c, t);
-    return;
+    if (walk) {
+      ph_spec_walk(s, c, t);
+      return;
+    }
   }
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   for (uint32_t i = 0; i < SW; ++i) s.bits[SW * t + i] = 0;
@@ -509,7 +525,7 @@ HD bool ph_fix(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
 // token, ~44 per such window.  Slices from `f` on get their final entry
 // and exit; a slice whose own chain holds the entry keeps its marks.
 template <bool SN>
-HD uint32_t ph_serial(Smem &s, const Ctx &c, uint32_t f, uint32_t nsl) {
+HD uint32_t ph_serial(Smem &s, const Ctx &c, uint32_t f, uint32_t nsl, bool walk) {
   uint32_t p = s.ex[f - 1], steps = 0;
   for (uint32_t t = f; t < nsl; ++t) {
     const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
@@ -520,7 +536,7 @@ HD uint32_t ph_serial(Smem &s, const Ctx &c, uint32_t f, uint32_t nsl) {
       continue;
     }
     if constexpr (!SN && NW > 1) {
-      if (p < hi && adopt_walker(s, t, p)) {
+      if (walk && p < hi && adopt_walker(s, t, p)) {   // (single chain: no walkers)
         p = s.ex[t];
         continue;
       }
@@ -934,6 +950,7 @@ HD void ph_rawcopy(Smem &s, const Ctx &c, uint32_t t) {
 HD void st_header(Smem &s, const Ctx &c, int codec) {
   s.op = 0;
   s.err = 0;
+  s.walk = 0;
   s.mode = kModeBlock;
   s.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
   s.raw_block = codec == STROM_CODEC_LZ4;
@@ -1151,7 +1168,9 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
         ph_load(s, c, t);
         __syncthreads();
         LP_MARK(kLpLoad);
-        ph_spec<SN>(s, c, t);
+        bool walk = s.walk;
+      respec:
+        ph_spec<SN>(s, c, t, walk);
         __syncthreads();
         LP_MARK(kLpSpec);
         if (SN) {
@@ -1182,7 +1201,7 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           }
           s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
           __syncthreads();
-        } else if (NW > 1) {
+        } else if (NW > 1 && walk) {
           const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
           const uint32_t lane = t & 63, wave = t >> 6;
           bool fixed = false;
@@ -1221,7 +1240,7 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
               if (t == 0) s.cov = serial_worth(s, f) ? 1u : 0u;
               __syncthreads();
               if (s.cov) {
-                if (t == 0) ph_serial<SN>(s, c, f + 1, nsl);
+                if (t == 0) ph_serial<SN>(s, c, f + 1, nsl, true);
                 __syncthreads();
                 break;
               }
@@ -1241,12 +1260,19 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
             if (changed) atomicMin(&s.minfix, t);
             const uint32_t nchg = (uint32_t)__syncthreads_count(changed);
             if (!nchg) break;
+            if (NW > 1 && r == WALK_AFTER) {
+              // this window and the stream's next ones go to the walkers
+              // (every thread has passed its fix: the count's barrier)
+              if (t == 0) s.walk = 1;
+              walk = true;
+              goto respec;
+            }
             if (r >= SERIAL_AFTER) {
               // the frontier slice was just re-parsed from a final entry
               if (t == 0) s.cov = serial_worth(s, s.minfix) ? 1u : 0u;
               __syncthreads();
               if (s.cov) {
-                if (t == 0) ph_serial<SN>(s, c, s.minfix + 1, nsl);
+                if (t == 0) ph_serial<SN>(s, c, s.minfix + 1, nsl, false);
                 __syncthreads();
                 break;
               }
@@ -1385,6 +1411,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
   Held *held = new Held[NT];
   FillPos *fpos = new FillPos[NT];
   uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0, serial = 0, serial_windows = 0;
+  uint32_t walk_windows = 0;
   st_header(s, c, codec);
   for (;;) {
     if (s.mode != kModeDone) st_block(s, c);
@@ -1403,7 +1430,9 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
       ++windows;
       st_window(s, c, ws);
       for (uint32_t t = 0; t < NT; ++t) ph_load(s, c, t);
-      for (uint32_t t = 0; t < NT; ++t) ph_spec<SN>(s, c, t);
+      bool walk = s.walk;
+    respec:
+      for (uint32_t t = 0; t < NT; ++t) ph_spec<SN>(s, c, t, walk);
       if (SN) {
         const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
         for (uint32_t t = 0; t < NT; ++t)
@@ -1425,7 +1454,8 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
           for (uint32_t t = S; t <= cov; ++t) flag[t] = true;
         }
         for (uint32_t t = 0; t < NT; ++t) s.en[t] = t == 0 ? s.ws : s.ex[t - 1];
-      } else if (NW > 1) {
+      } else if (NW > 1 && walk) {
+        ++walk_windows;
         const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
         uint32_t mp[NT];
         for (uint32_t t = 0; t < NT; ++t) {
@@ -1449,7 +1479,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
           for (uint32_t t = f + 1; t < NT; ++t)
             if (wv_pass(s, t, f)) flag[t] = true;
           if (r >= SERIAL_AFTER && serial_worth(s, f)) {
-            serial += ph_serial<SN>(s, c, f + 1, nsl);
+            serial += ph_serial<SN>(s, c, f + 1, nsl, true);
             ++serial_windows;
             break;
           }
@@ -1470,8 +1500,13 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
           }
           fixes += nchg;
           if (!nchg) break;
+          if (NW > 1 && r == WALK_AFTER) {
+            s.walk = 1;
+            walk = true;
+            goto respec;
+          }
           if (r >= SERIAL_AFTER && serial_worth(s, first)) {
-            serial += ph_serial<SN>(s, c, first + 1, nsl);
+            serial += ph_serial<SN>(s, c, first + 1, nsl, false);
             ++serial_windows;
             break;
           }
@@ -1513,6 +1548,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
     stats[3] = dbl;
     stats[4] = serial_windows;
     stats[5] = serial;
+    stats[6] = walk_windows;
   }
   if (!s.err && s.expect != 0xffffffffu && s.op != s.expect) s.err = kErrFormat;
   const int r = s.err ? s.err : (int)s.op;

@@ -143,7 +143,7 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
         raise ValueError("threads: 256 or 512")
     n = fn(codec, src.ctypes.data, len(data), out.ctypes.data, cap, st.ctypes.data)
     stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]),
-                 serial_windows=int(st[4]), serial_steps=int(st[5]))
+                 serial_windows=int(st[4]), serial_steps=int(st[5]), walk_windows=int(st[6]))
     return n, (out[:n].tobytes() if n >= 0 else b""), stats
 
 

@@ -161,6 +161,29 @@ def test_lz4par_arrow_frames_from_pyarrow(kind, threads):
 
 
 @pytest.mark.parametrize("threads", [256, 512])
+def test_lz4par_walkers(threads):
+    """The speculative walkers (lz4par.hip NW, WALK_AFTER): dense text —
+    whose single chains phase-lock — switches to them in its first window
+    and then validates in one scan per window; an int column does not
+    switch (64-byte slices); a literal-heavy column (bench kind ``chars``) keeps the serial
+    walk.  Every output equals the source."""
+    pytest.importorskip("pyarrow")
+    from nvme_strom_amd.tools.lz4par_bench import frames
+    for kind in ("text", "val", "chars"):
+        raws, bufs = frames(kind, 1)
+        st, out, stats = D.lz4par_host(D.ARROW_LZ4, bufs[0], len(raws[0]), threads)
+        assert st == len(raws[0]) and out == raws[0], (kind, stats)
+        if kind == "text":
+            assert stats["walk_windows"] == stats["windows"]
+            assert stats["rounds"] < 2 * stats["windows"] + 24, stats   # + the first window's
+        elif kind == "val":
+            if threads == 256:          # 32-byte slices: some windows switch
+                assert stats["walk_windows"] == 0
+        else:
+            assert stats["serial_windows"] == stats["windows"]
+
+
+@pytest.mark.parametrize("threads", [256, 512])
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "floats", "text", "random", "zeros", "runs"])
 def test_snappy_block_parallel_from_pyarrow(kind, threads):
     """Raw snappy buffers from pyarrow (and our host compressor) decode
