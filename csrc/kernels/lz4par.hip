@@ -94,7 +94,10 @@ static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 // whose chain has not merged by its true entry costs a serial fix-up round
 constexpr uint32_t LB = LZ4PAR_LOOKBACK;
 // LZ4: NW speculative walkers per slice instead of one, started WLB,
-// WLB - 1, ... bytes before it (NW = 1: the single chain from LB).  One
+// WLB - 1, ... bytes before it (NW = 1: the single chain from LB).  WLB
+// 16: the walkers are there for the phases, not for a long run-in (text
+// windows validate in one scan from 8 bytes back; 128 -> 16 took text from
+// 85 to 97 GB/s, profiles/r4/dec/lz4par_walkers_wlb.json).  One
 // chain phase-locks on dense LZ4 (text: 3-byte sequences whose offset high
 // byte is 0 read as a token with no literals and a short match, so a chain
 // entering 2 bytes late stays 2 bytes late): 30 % of text slices' chains
@@ -109,7 +112,7 @@ constexpr uint32_t LB = LZ4PAR_LOOKBACK;
 #define LZ4PAR_WALKERS 4
 #endif
 #ifndef LZ4PAR_WLOOKBACK
-#define LZ4PAR_WLOOKBACK 128
+#define LZ4PAR_WLOOKBACK 16
 #endif
 constexpr uint32_t NW = LZ4PAR_WALKERS;
 constexpr uint32_t WLB = LZ4PAR_WLOOKBACK;
