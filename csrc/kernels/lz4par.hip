@@ -93,6 +93,14 @@ static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 // ~100 bytes to fall onto the true token grid on int columns, and a slice
 // whose chain has not merged by its true entry costs a serial fix-up round
 constexpr uint32_t LB = LZ4PAR_LOOKBACK;
+// snappy's chains (with restarts) meet the true one within ~100 bytes:
+// 512 -> 128 bytes of run-in took 512 streams from 55 / 44 / 39 GB/s
+// (text / val / ids) to 72 / 59 / 40, 2048 streams text 71 -> 84, val
+// 60 -> 71 (profiles/r4/dec/snappy_lookback_ab.json); 64 or 96 no better
+#ifndef LZ4PAR_SN_LOOKBACK
+#define LZ4PAR_SN_LOOKBACK 128
+#endif
+constexpr uint32_t SLB = LZ4PAR_SN_LOOKBACK;
 // LZ4: NW speculative walkers per slice instead of one, started WLB,
 // WLB - 1, ... bytes before it (NW = 1: the single chain from LB).  WLB
 // 16: the walkers are there for the phases, not for a long run-in (text
@@ -465,7 +473,8 @@ HD void ph_spec(Smem &s, const Ctx &c, uint32_t t, bool walk) {
     s.ex[t] = lo;
     return;
   }
-  uint32_t p = lo - s.ws > LB ? lo - LB : s.ws;   // the window start is a true token
+  constexpr uint32_t lb = SN ? SLB : LB;
+  uint32_t p = lo - s.ws > lb ? lo - lb : s.ws;   // the window start is a true token
   Seq q;
   while (p < hi) {
     if (p >= lo) setbit(s, p);
