@@ -16,4 +16,7 @@
 // snappy too: 96 VGPRs left it at 2 workgroups per CU (5 waves per SIMD);
 // at 80 (6 small spills) it keeps the third
 #define LZ4PAR_WPE 6
+// 32-byte slices: a 64-byte snappy run-in (512 streams val 59 -> 61, text 72 -> 74 GB/s,
+// profiles/r4/dec/snappy_lookback_ab512.json)
+#define LZ4PAR_SN_LOOKBACK 64
 #include "lz4par.hip"
