@@ -106,7 +106,7 @@ build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
 # the 512-thread build of the block-parallel decoder WITH its host copy:
 # the CPU tests run its phases thread by thread (tests/test_codecs_cpu.py)
 $(OUT)/libstrom_lz4par512_host.so: csrc/kernels/lz4par.hip csrc/include/strom/strom.h
-	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_NT=512 -DLZ4PAR_LOADU=8 -DLZ4PAR_WPE_LZ4=6 -DLZ4P_NS=lz4p512 -DLZ4PAR_SN_LOOKBACK=64 \
+	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_NT=512 -DLZ4PAR_LOADU=8 -DLZ4PAR_WPE_LZ4=6 -DLZ4P_NS=lz4p512 -DLZ4PAR_SN_LOOKBACK=64 -DLZ4PAR_SN_WLOOKBACK=32 \
 	  -DLZ4PAR_ENTRY=strom_decompress_par512 -shared -o $@ $<
 
 # lz4par geometry variants for A/B timing (tools/lz4par_bench.py --variants):

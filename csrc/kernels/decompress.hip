@@ -891,7 +891,11 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // snappy takes the same block-parallel decoder (its element grammar, round 4)
   const bool par_codec = codec != STROM_CODEC_COPY;
   if (par_codec && (pe ? pv != 0 : nblocks <= 8192)) {
-    if (pv == 512 || (pv != 256 && nblocks <= 3 * device_cus()))
+    // snappy takes the 512-thread build at every count (its walkers, r4:
+    // 2,048 / 8,192 streams text 85 -> 94 / 88 -> 101, val 76 -> 84 /
+    // 79 -> 91, ids 78 -> 85 / 81 -> 91 GB/s, profiles/r4/dec/snappy_final.json)
+    const bool wide = codec == STROM_CODEC_SNAPPY || nblocks <= 3 * device_cus();
+    if (pv == 512 || (pv != 256 && wide))
       return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   }

@@ -138,6 +138,24 @@ static_assert(NW >= 1 && NW <= 8 && WLB >= NW, "walkers");
 #define LZ4PAR_WALK_AFTER (LZ4PAR_NT == 512 ? 24 : 10)
 #endif
 constexpr uint32_t WALK_AFTER = LZ4PAR_WALK_AFTER;
+// Snappy walks from its first window: its single chains meet the true one
+// (restarting at a failed parse) but the settled-prefix rounds still
+// re-walked 1-3 slices a window on int columns; four walkers from
+// SWLB..SWLB-3 bytes back validate every text / val / ids window of the
+// bench frames in one scan with no re-parse (host twin, 8 frames each:
+// ids 488 rounds + 4,584 re-walks -> 136 scans + 0).
+#ifndef LZ4PAR_SN_WALK
+#define LZ4PAR_SN_WALK 1
+#endif
+// GPU A/B (profiles/r4/dec/snappy_walkers_ab.json), 2,048 streams: text /
+// val / ids / chars 84 / 71 / 56 / 315 GB/s with the settled prefix, 85 /
+// 77 / 78 / 314 with walkers from 16 bytes back (32: 84 / 75 / 76; 128:
+// 76 / 66 / 65); the 512-thread build takes 32 (512 streams 71 / 64 / 65).
+#ifndef LZ4PAR_SN_WLOOKBACK
+#define LZ4PAR_SN_WLOOKBACK 16
+#endif
+constexpr bool SN_WALK = LZ4PAR_SN_WALK && NW > 1;
+constexpr uint32_t SWLB = LZ4PAR_SN_WLOOKBACK;
 #ifndef LZ4PAR_RESTART
 #define LZ4PAR_RESTART 1
 #endif
@@ -366,13 +384,14 @@ HD void ph_load(Smem &s, const Ctx &c, uint32_t t) {
 // and the mask of walker ids that have merged into them; every id keeps its
 // own marks (registers, fully unrolled: no scratch) and exit.  The slice
 // starts on walker 0's chain.
+template <bool SN>
 HD void ph_spec_walk(Smem &s, const Ctx &c, uint32_t t) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
   uint32_t wp[NW], wm[NW];
   uint32_t *wb = s.wk.bits + SW * t;     // walker j's words: wb[j * PW / 32 + i]
 #pragma unroll
   for (uint32_t w = 0; w < NW; ++w) {
-    const uint32_t back = WLB - w;
+    const uint32_t back = (SN ? SWLB : WLB) - w;
     wp[w] = lo - s.ws > back ? lo - back : s.ws;   // the window start is a true token
     wm[w] = lo < hi ? 1u << w : 0u;
 #pragma unroll
@@ -405,7 +424,9 @@ HD void ph_spec_walk(Smem &s, const Ctx &c, uint32_t t) {
         if ((m >> w) & 1u) wb[w * (PW / 32) + (r >> 5)] |= bit;
     }
     Seq q;
-    parse<false>(s, c, pm, s.bend, q);   // a failed parse: the chain goes on anyway
+    // a failed parse: an LZ4 chain goes on anyway; a snappy one restarts at
+    // the next byte (a garbage literal tag may claim kilobytes)
+    if (!parse<SN>(s, c, pm, s.bend, q) && SN) q.next = pm + 1;
     kept = false;
 #pragma unroll
     for (uint32_t w = 0; w < NW; ++w)
@@ -461,9 +482,9 @@ HD bool adopt_walker(Smem &s, uint32_t t, uint32_t ent) {
 // (1) speculative chain of slice t
 template <bool SN>
 HD void ph_spec(Smem &s, const Ctx &c, uint32_t t, bool walk) {
-  if constexpr (!SN && NW > 1) {
+  if constexpr (NW > 1) {
     if (walk) {
-      ph_spec_walk(s, c, t);
+      ph_spec_walk<SN>(s, c, t);
       return;
     }
   }
@@ -962,7 +983,7 @@ HD void ph_rawcopy(Smem &s, const Ctx &c, uint32_t t) {
 HD void st_header(Smem &s, const Ctx &c, int codec) {
   s.op = 0;
   s.err = 0;
-  s.walk = 0;
+  s.walk = codec == STROM_CODEC_SNAPPY && SN_WALK;
   s.mode = kModeBlock;
   s.bcs = codec == STROM_CODEC_LZ4_FRAME_BCS;
   s.raw_block = codec == STROM_CODEC_LZ4;
@@ -1129,6 +1150,9 @@ using namespace LZ4P_NS;
 #if !defined(LZ4PAR_WPE_LZ4) && LZ4PAR_NT == 256
 #define LZ4PAR_WPE_LZ4 4
 #endif
+#if !defined(LZ4PAR_WPE) && LZ4PAR_NT == 256
+#define LZ4PAR_WPE 4   // the snappy kernel likewise (140 with its walkers)
+#endif
 #ifdef LZ4PAR_WPE
 #define LZ4PAR_OCC __attribute__((amdgpu_waves_per_eu(LZ4PAR_WPE)))
 #else
@@ -1185,7 +1209,7 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
         ph_spec<SN>(s, c, t, walk);
         __syncthreads();
         LP_MARK(kLpSpec);
-        if (SN) {
+        if (SN && !walk) {
           const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
           if (t == 0) s.minfix = nsl;
           __syncthreads();
@@ -1445,7 +1469,7 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
       bool walk = s.walk;
     respec:
       for (uint32_t t = 0; t < NT; ++t) ph_spec<SN>(s, c, t, walk);
-      if (SN) {
+      if (SN && !walk) {
         const uint32_t nsl = (s.wend - s.ws + SL - 1) / SL;
         for (uint32_t t = 0; t < NT; ++t)
           flag[t] = t == 0 || t >= nsl || sn_link(s, t, s.ex[t - 1]);   // link

@@ -19,4 +19,5 @@
 // 32-byte slices: a 64-byte snappy run-in (512 streams val 59 -> 61, text 72 -> 74 GB/s,
 // profiles/r4/dec/snappy_lookback_ab512.json)
 #define LZ4PAR_SN_LOOKBACK 64
+#define LZ4PAR_SN_WLOOKBACK 32
 #include "lz4par.hip"

@@ -184,6 +184,22 @@ def test_lz4par_walkers(threads):
 
 
 @pytest.mark.parametrize("threads", [256, 512])
+def test_snappy_walkers(threads):
+    """Snappy streams walk from their first window (lz4par.hip SN_WALK):
+    sorted ids, whose settled-prefix validation re-walked ~3 slices a
+    window, validate in one scan per window with no re-parse."""
+    pytest.importorskip("pyarrow")
+    from nvme_strom_amd.tools.lz4par_bench import frames
+    for kind in ("ids", "val", "text"):
+        raws, bufs = frames(kind, 2, codec="snappy")
+        for raw, buf in zip(raws, bufs):
+            st, out, stats = D.lz4par_host(D.SNAPPY, buf, len(raw), threads)
+            assert st == len(raw) and out == raw, (kind, stats)
+            assert stats["walk_windows"] == stats["windows"]
+            assert stats["rounds"] <= stats["windows"] + 4, (kind, stats)
+
+
+@pytest.mark.parametrize("threads", [256, 512])
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "floats", "text", "random", "zeros", "runs"])
 def test_snappy_block_parallel_from_pyarrow(kind, threads):
     """Raw snappy buffers from pyarrow (and our host compressor) decode
