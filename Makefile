@@ -20,6 +20,7 @@ KERNEL_OBJ := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERNEL_SRC))
 TOOLS      := $(patsubst csrc/tools/%.cc,$(OUT)/%,$(wildcard csrc/tools/*.cc))
 
 all: $(OUT)/libstrom.so tools $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so \
+     $(OUT)/libstrom_lz4par512b_host.so \
      $(OUT)/libstrom_zstdprof.so
 
 tools: $(TOOLS)
@@ -38,6 +39,7 @@ $(OBJ)/kernels/%.o: csrc/kernels/%.hip csrc/include/strom/strom.h
 
 # the 512-thread decoder build is lz4par.hip compiled again
 $(OBJ)/kernels/lz4par_nt512.o: csrc/kernels/lz4par.hip
+$(OBJ)/kernels/lz4par_nt512_ob8k.o: csrc/kernels/lz4par.hip
 
 $(OUT)/libstrom.so: $(ENGINE_OBJ) $(KERNEL_OBJ) $(CORE_OBJ)
 	@mkdir -p $(OUT)
@@ -77,6 +79,7 @@ $(OUT)/%: csrc/tools/%.cc $(OUT)/libstrom.so
 
 clean:
 	rm -rf build $(OUT)/libstrom.so $(OUT)/libstrom_decprof.so $(OUT)/libstrom_lz4par512_host.so \
+	  $(OUT)/libstrom_lz4par512b_host.so \
 	  $(OUT)/libstrom_zstdprof.so $(TOOLS)
 
 .PHONY: all tools clean ab
@@ -108,6 +111,11 @@ build/selftest-tsan: $(SELFTEST_SRC) csrc/engine/engine.h
 $(OUT)/libstrom_lz4par512_host.so: csrc/kernels/lz4par.hip csrc/include/strom/strom.h
 	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_NT=512 -DLZ4PAR_LOADU=8 -DLZ4PAR_WPE_LZ4=6 -DLZ4P_NS=lz4p512 -DLZ4PAR_SN_LOOKBACK=64 -DLZ4PAR_SN_WLOOKBACK=32 \
 	  -DLZ4PAR_ENTRY=strom_decompress_par512 -shared -o $@ $<
+
+# ... and of the 8 KiB-batch build (lz4par_nt512_ob8k.hip)
+$(OUT)/libstrom_lz4par512b_host.so: csrc/kernels/lz4par.hip csrc/include/strom/strom.h
+	$(HIPCC) $(HIPFLAGS) -Icsrc/include -DLZ4PAR_NT=512 -DLZ4PAR_LOADU=8 -DLZ4PAR_OB=8192 -DLZ4PAR_WPE_LZ4=4 -DLZ4PAR_WPE=4 -DLZ4P_NS=lz4p512b -DLZ4PAR_SN_LOOKBACK=64 -DLZ4PAR_SN_WLOOKBACK=32 \
+	  -DLZ4PAR_ENTRY=strom_decompress_par512b -shared -o $@ $<
 
 # lz4par geometry variants for A/B timing (tools/lz4par_bench.py --variants):
 # make lz4v LZ4V="name:-DX=1,-DY=2 ..." -> $(OUT)/lz4v/<name>.so (lz4par.hip

@@ -848,6 +848,10 @@ extern "C" int strom_decompress_par512(int codec, const void *d_src, void *d_dst
                                        const strom_decomp_desc *d_desc, uint32_t nstreams,
                                        int32_t *d_status, void *stream);
 
+extern "C" int strom_decompress_par512b(int codec, const void *d_src, void *d_dst,
+                                        const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                        int32_t *d_status, void *stream);
+
 extern "C" int strom_decompress_lanes(int codec, const void *d_src, void *d_dst,
                                       const strom_decomp_desc *d_desc, uint32_t nblocks,
                                       int32_t *d_status, void *stream);
@@ -885,17 +889,21 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
   // shorter per-stream chains (lz4par_nt512.hip; config-5 frames 512: 61 ->
   // 85 GB/s, 768: 86 -> 115; profiles/r3/dec/lz4par_nt_occupancy_ab.json).
   // STROM_DECOMP_PAR=0 forces the lane groups, 1 the block-parallel choice,
-  // 256 / 512 a build.
+  // 256 / 512 / 8192 a build (8192: 512 threads, 8 KiB batches).
   const char *pe = getenv("STROM_DECOMP_PAR");
   const int pv = pe ? atoi(pe) : -1;
   // snappy takes the same block-parallel decoder (its element grammar, round 4)
   const bool par_codec = codec != STROM_CODEC_COPY;
   if (par_codec && (pe ? pv != 0 : nblocks <= 8192)) {
-    // snappy takes the 512-thread build at every count (its walkers, r4:
-    // 2,048 / 8,192 streams text 85 -> 94 / 88 -> 101, val 76 -> 84 /
+    // up to two streams per CU: the 8 KiB-batch build (lz4par_nt512_ob8k.hip)
+    const uint32_t cus = device_cus();
+    const bool pick = pv != 256 && pv != 512 && pv != 8192;   // the library's choice
+    if (pv == 8192 || (pick && nblocks <= 2 * cus))
+      return strom_decompress_par512b(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
+    // snappy takes the 512-thread build at every larger count (its walkers,
+    // r4: 2,048 / 8,192 streams text 85 -> 94 / 88 -> 101, val 76 -> 84 /
     // 79 -> 91, ids 78 -> 85 / 81 -> 91 GB/s, profiles/r4/dec/snappy_final.json)
-    const bool wide = codec == STROM_CODEC_SNAPPY || nblocks <= 3 * device_cus();
-    if (pv == 512 || (pv != 256 && wide))
+    if (pv == 512 || (pick && (codec == STROM_CODEC_SNAPPY || nblocks <= 3 * cus)))
       return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   }

@@ -277,6 +277,8 @@ _SIGS = {
                                        C.c_void_p, C.c_void_p]),
     "strom_decompress_par512": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_void_p, C.c_void_p]),
+    "strom_decompress_par512b": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                        C.c_void_p, C.c_void_p]),
     "strom_decompress_lanes": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
     "strom_file_topology": (C.c_int, [C.c_int, C.c_void_p]),

@@ -115,32 +115,32 @@ def _xxh32(data: bytes, seed: int = 0) -> int:
         return 0
 
 
-_HOST512 = None
+_HOST = {}
 
 
-def lz4par_host(codec: int, data: bytes, cap: int, threads: int = 256):
+def lz4par_host(codec: int, data: bytes, cap: int, threads=256):
     """The block-parallel decoder's phases (csrc/kernels/lz4par.hip) run on
     the CPU, thread by thread: -> (status, output bytes, stats dict).  The
     reference for the GPU kernel's algorithm; ``threads=512`` runs the
-    geometry of the 512-thread build (lz4par_nt512.hip)."""
-    global _HOST512
+    geometry of the 512-thread build (lz4par_nt512.hip), ``"512b"`` that of
+    the 8 KiB-batch build (lz4par_nt512_ob8k.hip)."""
     src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
     out = np.zeros(max(cap, 1), dtype=np.uint8)
     st = np.zeros(8, dtype=np.uint32)
-    if threads == 512:
-        if _HOST512 is None:
-            import ctypes as C
+    if threads in (512, "512b"):
+        if threads not in _HOST:
             import os
-            lib = C.CDLL(os.path.join(os.path.dirname(N.LIB_PATH), "libstrom_lz4par512_host.so"))
+            name = "libstrom_lz4par512_host.so" if threads == 512 else "libstrom_lz4par512b_host.so"
+            lib = C.CDLL(os.path.join(os.path.dirname(N.LIB_PATH), name))
             lib.strom_lz4par_host.restype = C.c_int
             lib.strom_lz4par_host.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p,
                                               C.c_uint32, C.c_void_p]
-            _HOST512 = lib.strom_lz4par_host
-        fn = _HOST512
+            _HOST[threads] = lib.strom_lz4par_host
+        fn = _HOST[threads]
     elif threads == 256:
         fn = N.lib().strom_lz4par_host
     else:
-        raise ValueError("threads: 256 or 512")
+        raise ValueError("threads: 256, 512 or '512b'")
     n = fn(codec, src.ctypes.data, len(data), out.ctypes.data, cap, st.ctypes.data)
     stats = dict(windows=int(st[0]), rounds=int(st[1]), fixes=int(st[2]), doubling=int(st[3]),
                  serial_windows=int(st[4]), serial_steps=int(st[5]), walk_windows=int(st[6]))

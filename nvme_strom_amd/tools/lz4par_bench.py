@@ -110,6 +110,7 @@ def main(argv=None) -> int:
     import os
     decoders = ([("lanes", lib().strom_decompress_lanes)] if a.lanes else []) + \
         [("par", lib().strom_decompress_par), ("par512", lib().strom_decompress_par512),
+         ("par512b", lib().strom_decompress_par512b),
          ("auto", lib().strom_decompress)]
     for v in [x for x in a.variants.split(",") if x]:
         so = C.CDLL(os.path.join(os.path.dirname(os.path.dirname(__file__)), "lib", "lz4v",

@@ -131,7 +131,7 @@ def _ints(kind, n, seed=0):
     return rng.random(n // 8).tobytes()
 
 
-@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("threads", [256, 512, "512b"])
 @pytest.mark.parametrize("kind", ["random", "text", "runs", "zeros", "uniform", "sorted", "floats"])
 @pytest.mark.parametrize("n", [1, 13, 100, 4096, 70000, 300000])
 def test_lz4par_raw_block_matches_host(kind, n, threads):
@@ -144,7 +144,7 @@ def test_lz4par_raw_block_matches_host(kind, n, threads):
     assert st == len(d) and out == d, (st, stats)
 
 
-@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("threads", [256, 512, "512b"])
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "text", "random"])
 def test_lz4par_arrow_frames_from_pyarrow(kind, threads):
     """pyarrow's LZ4 frames (linked 64 KiB blocks: matches reach into the
@@ -160,7 +160,7 @@ def test_lz4par_arrow_frames_from_pyarrow(kind, threads):
     assert st == 5000 and out == d[:5000]
 
 
-@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("threads", [256, 512, "512b"])
 def test_lz4par_walkers(threads):
     """The speculative walkers (lz4par.hip NW, WALK_AFTER): dense text —
     whose single chains phase-lock — switches to them in its first window
@@ -183,7 +183,7 @@ def test_lz4par_walkers(threads):
             assert stats["serial_windows"] == stats["windows"]
 
 
-@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("threads", [256, 512, "512b"])
 def test_snappy_walkers(threads):
     """Snappy streams walk from their first window (lz4par.hip SN_WALK):
     sorted ids, whose settled-prefix validation re-walked ~3 slices a
@@ -199,7 +199,7 @@ def test_snappy_walkers(threads):
             assert stats["rounds"] <= stats["windows"] + 4, (kind, stats)
 
 
-@pytest.mark.parametrize("threads", [256, 512])
+@pytest.mark.parametrize("threads", [256, 512, "512b"])
 @pytest.mark.parametrize("kind", ["uniform", "sorted", "floats", "text", "random", "zeros", "runs"])
 def test_snappy_block_parallel_from_pyarrow(kind, threads):
     """Raw snappy buffers from pyarrow (and our host compressor) decode

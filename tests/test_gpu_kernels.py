@@ -130,16 +130,16 @@ def test_lz4_raw(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, "par256", "par512"])
+@pytest.mark.parametrize("g", [1, 2, 3, 4, 6, 8, 16, 32, "par256", "par512", "par8192"])
 @pytest.mark.parametrize("codec", ["lz4", "snappy"])
 def test_decoder_geometries(dev, monkeypatch, g, codec):
     """Every streams-per-wave variant of the lane-group decoder
     (STROM_DECOMP_G, the block-parallel decoder switched off) decodes the
     same payloads: the fast LZ4 step's pass width differs per geometry (a
     length-15 match nibble must still take the extended-length path);
-    3 / 2 / 6 = the large-ring few-stream geometries; "par256" / "par512" =
-    the block-parallel decoder's two builds (lz4par.hip, lz4par_nt512.hip;
-    LZ4 only)."""
+    3 / 2 / 6 = the large-ring few-stream geometries; "par256" / "par512" /
+    "par8192" = the block-parallel decoder's three builds (lz4par.hip,
+    lz4par_nt512.hip, lz4par_nt512_ob8k.hip)."""
     pa = pytest.importorskip("pyarrow")
     from nvme_strom_amd.ops import decompress as D
     if str(g).startswith("par"):
@@ -170,7 +170,7 @@ def test_snappy(dev, which):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["auto", "lanes", "256", "512"])
+@pytest.mark.parametrize("g", ["auto", "lanes", "256", "512", "8192"])
 def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     """pyarrow's 'lz4' codec = LZ4 frame with linked 64 KiB blocks: matches
     may reach into the previous block (lane groups: the LDS history ring;
@@ -189,7 +189,7 @@ def test_lz4_frame_linked_blocks_from_pyarrow(dev, monkeypatch, g):
     assert outs == pays
 
 
-@pytest.mark.parametrize("g", ["0", "256", "512"])
+@pytest.mark.parametrize("g", ["0", "256", "512", "8192"])
 def test_malformed_streams_report_errors(dev, monkeypatch, g):
     from nvme_strom_amd.ops import decompress as D
     monkeypatch.setenv("STROM_DECOMP_PAR", g)
