@@ -141,6 +141,14 @@ build/zstd_fuzz: csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip csrc/include/stro
 	  -Xarch_host -fno-sanitize-recover=all -fno-omit-frame-pointer \
 	  -o $@ csrc/tests/zstd_fuzz.cc csrc/kernels/zstd.hip
 
+# the block-parallel LZ4 / snappy decoder's host copy, host-only with ASan + UBSan
+build/lz4par_fuzz: csrc/tests/lz4par_fuzz.cc csrc/kernels/lz4par.hip csrc/include/strom/strom.h
+	@mkdir -p build
+	$(HIPCC) -std=c++17 -O1 -g -Icsrc/include --offload-arch=$(ARCH) \
+	  -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
+	  -Xarch_host -fno-sanitize-recover=all -fno-omit-frame-pointer \
+	  -o $@ csrc/tests/lz4par_fuzz.cc csrc/kernels/lz4par.hip
+
 selftest: build/selftest build/selftest-asan build/selftest-tsan
 	STROM_STAT_SHM=0 ./build/selftest && STROM_STAT_SHM=0 ./build/selftest-asan && STROM_STAT_SHM=0 TSAN_OPTIONS=report_signal_unsafe=0 ./build/selftest-tsan
 

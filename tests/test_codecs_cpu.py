@@ -370,6 +370,35 @@ def test_zstd_errors_are_bounded():
         assert st <= len(d)
 
 
+def test_lz4par_fuzz_asan(tmp_path):
+    """Random edits / truncations of pyarrow LZ4 frames and snappy buffers
+    through the block-parallel decoder's phases built host-only with ASan +
+    UBSan (csrc/tests/lz4par_fuzz.cc): the text seeds run on the walkers
+    (LZ4 switches to them, snappy starts on them); seeds decode exactly,
+    mutants end in a clean status within the capacity."""
+    pa = pytest.importorskip("pyarrow")
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "build/lz4par_fuzz"], cwd=root, capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    args = []
+    seeds = [_data("text", 150000, 2), _ints("uniform", 160000, 1), _ints("sorted", 120000, 3)]
+    for i, d in enumerate(seeds):
+        for codec, enc in ((D.ARROW_LZ4, lambda x: D.arrow_lz4_buffer(
+                x, pa.compress(x, codec="lz4", asbytes=True))),
+                           (D.SNAPPY, lambda x: pa.compress(x, codec="snappy", asbytes=True))):
+            (tmp_path / f"{i}_{codec}.bin").write_bytes(enc(d))
+            (tmp_path / f"{i}_{codec}.raw").write_bytes(d)
+            args += [str(codec), str(tmp_path / f"{i}_{codec}.bin"),
+                     str(tmp_path / f"{i}_{codec}.raw")]
+    r = subprocess.run([os.path.join(root, "build", "lz4par_fuzz"), "150"] + args,
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert "6 seeds ok" in r.stdout
+
+
 def test_zstd_fuzz_asan(tmp_path):
     """8k random edits / truncations of real zstd frames through the
     decoder's phases built host-only with ASan + UBSan
