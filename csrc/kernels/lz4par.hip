@@ -138,6 +138,13 @@ static_assert(NW >= 1 && NW <= 8 && WLB >= NW, "walkers");
 #define LZ4PAR_WALK_AFTER (LZ4PAR_NT == 512 ? 24 : 10)
 #endif
 constexpr uint32_t WALK_AFTER = LZ4PAR_WALK_AFTER;
+// ... or already after WALK_EARLY rounds when an eighth of the slices
+// re-parsed in the last one and the serial walk would not take over (a
+// phase-locked text window; an int column re-parses a slice or two)
+#ifndef LZ4PAR_WALK_EARLY
+#define LZ4PAR_WALK_EARLY 2
+#endif
+constexpr uint32_t WALK_EARLY = LZ4PAR_WALK_EARLY;
 // Snappy walks from its first window: its single chains meet the true one
 // (restarting at a failed parse) but the settled-prefix rounds still
 // re-walked 1-3 slices a window on int columns; four walkers from
@@ -1296,12 +1303,22 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
             if (changed) atomicMin(&s.minfix, t);
             const uint32_t nchg = (uint32_t)__syncthreads_count(changed);
             if (!nchg) break;
-            if (NW > 1 && r == WALK_AFTER) {
+            if (NW > 1 && (r == WALK_AFTER || (r == WALK_EARLY && nchg >= NT / 8))) {
               // this window and the stream's next ones go to the walkers
-              // (every thread has passed its fix: the count's barrier)
-              if (t == 0) s.walk = 1;
-              walk = true;
-              goto respec;
+              // (every thread has passed its fix: the count's barrier);
+              // early only when the serial walk would not take over
+              bool go = r == WALK_AFTER;
+              if (!go) {
+                if (t == 0) s.cov = serial_worth(s, s.minfix) ? 1u : 0u;
+                __syncthreads();
+                go = !s.cov;
+                __syncthreads();
+              }
+              if (go) {
+                if (t == 0) s.walk = 1;
+                walk = true;
+                goto respec;
+              }
             }
             if (r >= SERIAL_AFTER) {
               // the frontier slice was just re-parsed from a final entry
@@ -1536,7 +1553,8 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
           }
           fixes += nchg;
           if (!nchg) break;
-          if (NW > 1 && r == WALK_AFTER) {
+          if (NW > 1 && (r == WALK_AFTER || (r == WALK_EARLY && nchg >= NT / 8 &&
+                                             !serial_worth(s, first)))) {
             s.walk = 1;
             walk = true;
             goto respec;
