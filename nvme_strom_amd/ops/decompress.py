@@ -11,6 +11,7 @@ produce test data and serve as CPU references.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import struct
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
@@ -29,6 +30,10 @@ LZ4_FRAME_BCS = 5
 ARROW_LZ4 = 6          # Arrow IPC buffer: i64 length prefix (-1 = raw) + LZ4 frame
 ZSTD = 7               # Zstandard frame(s), RFC 8878 (csrc/kernels/zstd.hip)
 ARROW_ZSTD = 8         # Arrow IPC buffer: i64 length prefix (-1 = raw) + zstd frame
+
+# decompress(): a stream whose compressed size is at least this share of its
+# capacity goes to the lane decoder
+LANES_RATIO = 0.9
 
 DESC_DTYPE = np.dtype([("src_off", "<u8"), ("dst_off", "<u8"), ("src_len", "<u4"),
                        ("dst_len", "<u4")])
@@ -232,8 +237,28 @@ def decompress(codec: int, src: torch.Tensor, dst: torch.Tensor, descs: np.ndarr
         raise ValueError("descriptor source out of range")
     if int((descs["dst_off"] + descs["dst_len"]).max()) > dst.numel():
         raise ValueError("descriptor destination out of range")
-    d_desc = torch.from_numpy(descs.view(np.uint8).copy()).to(src.device)
+    # streams stored at >= LANES_RATIO of their capacity (literal runs, a
+    # token per few hundred bytes) take the lane decoder, the rest the
+    # library's choice — the Arrow scan's per-buffer routing
+    # (models/arrow_scan.py; profiles/r4/dec/lz4par_final.json chars, 2,048
+    # streams: LZ4 lanes 173 vs block-parallel 108 GB/s, snappy 402 vs 316).
+    # A decoder forced with STROM_DECOMP_PAR takes every stream.
+    if codec in (LZ4, LZ4_FRAME, LZ4_FRAME_BCS, ARROW_LZ4, SNAPPY) and \
+            os.environ.get("STROM_DECOMP_PAR") is None:
+        lit = descs["src_len"].astype(np.float64) >= LANES_RATIO * descs["dst_len"]
+    else:
+        lit = np.zeros(len(descs), dtype=bool)
     status = torch.empty(len(descs), dtype=torch.int32, device=src.device)
-    check(lib().strom_decompress(codec, ptr(src), ptr(dst), ptr(d_desc), len(descs), ptr(status),
-                                 stream_handle(stream)), "decompress")
+    for mask, fn in ((~lit, lib().strom_decompress), (lit, lib().strom_decompress_lanes)):
+        idx = np.nonzero(mask)[0]
+        if not len(idx):
+            continue
+        part = descs if len(idx) == len(descs) else descs[idx]
+        d_desc = torch.from_numpy(part.view(np.uint8).copy()).to(src.device)
+        st = status if len(idx) == len(descs) else \
+            torch.empty(len(idx), dtype=torch.int32, device=src.device)
+        check(fn(codec, ptr(src), ptr(dst), ptr(d_desc), len(idx), ptr(st),
+                 stream_handle(stream)), "decompress")
+        if st is not status:
+            status[torch.from_numpy(idx).to(src.device)] = st
     return status.cpu().numpy()

@@ -116,6 +116,38 @@ def _run(codec, streams, sizes, dev):
     return st, [out[int(do):int(do) + n] for do, n in zip(doffs, sizes)]
 
 
+@pytest.mark.parametrize("codec", ["lz4", "snappy"])
+def test_mixed_literal_heavy_routing(dev, monkeypatch, codec):
+    """decompress() sends streams stored at >= LANES_RATIO of their size to
+    the lane decoder and the rest to the library's choice, two launches:
+    interleaved incompressible and text streams come back in order with
+    their own statuses (a short capacity on one of each kind)."""
+    monkeypatch.delenv("STROM_DECOMP_PAR", raising=False)
+    from nvme_strom_amd.ops import decompress as D
+    rng = np.random.default_rng(11)
+    words = [b"select", b"from", b"where", b"gpu", b"hbm"]
+    pays = []
+    for i in range(24):
+        if i % 3 == 0:
+            pays.append(rng.integers(0, 256, 20000 + 97 * i, dtype=np.uint8).tobytes())
+        else:
+            pays.append(b" ".join(words[j] for j in rng.integers(0, 5, 9000 + 13 * i)))
+    enc = D.lz4_compress if codec == "lz4" else D.snappy_compress
+    comp = [enc(p) for p in pays]
+    assert any(len(c) >= D.LANES_RATIO * len(p) for c, p in zip(comp, pays))
+    assert any(len(c) < D.LANES_RATIO * len(p) for c, p in zip(comp, pays))
+    sizes = [len(p) for p in pays]
+    sizes[3] -= 1                       # literal-heavy, one byte short
+    sizes[4] -= 1                       # compressible, one byte short
+    cid = D.LZ4 if codec == "lz4" else D.SNAPPY
+    st, outs = _run(cid, comp, sizes, dev)
+    for i, p in enumerate(pays):
+        if i in (3, 4):
+            assert st[i] < 0, (i, st[i])
+        else:
+            assert st[i] == len(p) and outs[i] == p, (i, st[i])
+
+
 @pytest.mark.parametrize("which", ["ours", "pyarrow"])
 def test_lz4_raw(dev, which):
     from nvme_strom_amd.ops import decompress as D
