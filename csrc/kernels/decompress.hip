@@ -903,7 +903,14 @@ extern "C" int strom_decompress(int codec, const void *d_src, void *d_dst,
     // snappy takes the 512-thread build at every larger count (its walkers,
     // r4: 2,048 / 8,192 streams text 85 -> 94 / 88 -> 101, val 76 -> 84 /
     // 79 -> 91, ids 78 -> 85 / 81 -> 91 GB/s, profiles/r4/dec/snappy_final.json)
-    if (pv == 512 || (pick && (codec == STROM_CODEC_SNAPPY || nblocks <= 3 * cus)))
+    // LZ4 from 12 streams per CU too: text / ids / val at 3,072 streams 116 /
+    // 111 / 110 against 99 / 102 / 110 GB/s (8,192: 120 / 115 / 113 against
+    // 102 / 105 / 112; profiles/r4/dec/lz4par_many_streams.json); between
+    // 3 and 12 per CU the 256-thread build keeps val (2,048: 110 vs 104).
+    // Literal-heavy streams (utf8 characters) lose on it (8,192: 74 vs 110)
+    // and go to the lane decoder from decompress() and the Arrow scan.
+    if (pv == 512 ||
+        (pick && (codec == STROM_CODEC_SNAPPY || nblocks <= 3 * cus || nblocks >= 12 * cus)))
       return strom_decompress_par512(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
     return strom_decompress_par(codec, d_src, d_dst, d_desc, nblocks, d_status, stream);
   }
