@@ -119,7 +119,8 @@ $(OUT)/libstrom_lz4par512b_host.so: csrc/kernels/lz4par.hip csrc/include/strom/s
 
 # lz4par geometry variants for A/B timing (tools/lz4par_bench.py --variants):
 # make lz4v LZ4V="name:-DX=1,-DY=2 ..." -> $(OUT)/lz4v/<name>.so (lz4par.hip
-# with those macros: LZ4PAR_PW / _OB / _HR / _LOOKBACK / _DBL / _RES)
+# with those macros: LZ4PAR_NT / _PW / _OB / _HR / _LOOKBACK / _WALKERS / _WLOOKBACK /
+# _WALK_AFTER / _WALK_EARLY / _SN_WALK / _SN_LOOKBACK / _SN_WLOOKBACK / _WPE / _WPE_LZ4)
 LZ4V ?= base:-DLZ4PAR_HR=0
 lz4v:
 	@rm -rf $(OUT)/lz4v && mkdir -p $(OUT)/lz4v
