@@ -412,6 +412,7 @@ class IoEngine {
   struct Worker;
  private:
   std::vector<std::unique_ptr<Worker>> workers_;
+  std::mutex prof_mu_;            // prof(): the workers' counter baselines
   std::atomic<uint32_t> rr_{0};
 };
 
@@ -469,7 +470,7 @@ class Ingest {
   bool init();
   int launch_grid();
   int start_locked();
-  void write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len);
+  bool write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len);
 
   int device_;
   uint32_t nslots_ = 0, grid_ = 0;
@@ -484,6 +485,7 @@ class Ingest {
   std::atomic<uint64_t> state_{0};
   bool launched_ = false;              // under mu_
   std::atomic<bool> dead_{false};
+  std::atomic<bool> gone_{false};     // shutdown() saw the grid exit
   uint64_t nr_launch_ = 0;
 };
 

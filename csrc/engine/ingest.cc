@@ -185,21 +185,32 @@ void Ingest::post_runs(Run *runs, size_t nruns, uint32_t piece) {
     if (!r.ok) continue;
     r.first = s + 1;
     for (uint32_t off = 0; off < r.len; off += piece, ++s, ++r.n)
-      write_desc(s, (const char *)r.src + off, r.dst + off, std::min(piece, r.len - off));
+      if (!write_desc(s, (const char *)r.src + off, r.dst + off, std::min(piece, r.len - off))) {
+        // the grid is gone (shutdown): this and the later runs take the
+        // caller's SDMA fallback; their reservations are never served
+        for (size_t j = i; j < nruns; ++j) runs[j].ok = false;
+        return;
+      }
   }
 }
 
-void Ingest::write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len) {
+bool Ingest::write_desc(uint64_t s, const void *src, uint64_t dst, uint32_t len) {
   const uint32_t k = (uint32_t)(s % nslots_);
   // the slot's previous occupant (s - nslots) must be done: in-flight
-  // requests are bounded by the workers' staging, far below nslots
+  // requests are bounded by the workers' staging, far below nslots.  A
+  // poster that reserved before shutdown() and finds the grid gone would
+  // spin here forever: gone_ ends the wait.
   if (s >= nslots_)
-    while (__atomic_load_n(&done_[k], __ATOMIC_ACQUIRE) < s - nslots_ + 1) _mm_pause();
+    while (__atomic_load_n(&done_[k], __ATOMIC_ACQUIRE) < s - nslots_ + 1) {
+      if (gone_.load(std::memory_order_acquire)) return false;
+      _mm_pause();
+    }
   IngestDesc *d = (IngestDesc *)ring_ + k;
   d->src = (uint64_t)src;
   d->dst = dst;
   d->len_tag = len;
   __atomic_store_n(&d->seq, s + 1, __ATOMIC_RELEASE);
+  return true;
 }
 
 bool Ingest::is_done(uint64_t seq) const {
@@ -226,8 +237,16 @@ void Ingest::idle() {
 }
 
 void Ingest::shutdown() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    dead_.store(true);                 // no new reservations from here on
+  }
+  // a poster that passed the dead_ check and reserved while the grid was
+  // running gets its descriptors served before the grid is told to stop
+  // (bounded: at exit a reservation may never be retired)
+  const uint64_t drain_end = mono_ns() + 200000000ull;
+  while ((state_.load() >> 1) != 0 && (state_.load() & 1) && mono_ns() < drain_end) _mm_pause();
   std::lock_guard<std::mutex> g(mu_);
-  dead_.store(true);
   state_.fetch_and(~1ull);
   __atomic_store_n(stop_, 1, __ATOMIC_SEQ_CST);
   if (launched_) {
@@ -237,6 +256,7 @@ void Ingest::shutdown() {
       _mm_pause();
     launched_ = false;
   }
+  gone_.store(true, std::memory_order_release);
 }
 
 }  // namespace strom

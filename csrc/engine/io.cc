@@ -316,15 +316,23 @@ struct IoEngine::Worker {
   uint32_t lh_io[STROM_HIST_BUCKETS] = {}, lh_copy[STROM_HIST_BUCKETS] = {};
   uint64_t lh_io_mask = 0, lh_copy_mask = 0;
 
-  // ---- attribution (config io_prof), read racily by IoEngine::prof
+  // ---- attribution (config io_prof).  Single writer (this worker):
+  // relaxed load + store, no RMW on the hot path; IoEngine::prof reads them
+  // concurrently and "resets" by moving its own baseline (prof_base_*,
+  // guarded by IoEngine::prof_mu_), never by writing the worker's counters.
   bool prof_on = false;
   uint64_t prof_t = 0;
-  uint64_t prof_cyc[kProfPhases] = {};
-  uint64_t prof_cnt[kProfCounts] = {};
+  std::atomic<uint64_t> prof_cyc[kProfPhases] = {};
+  std::atomic<uint64_t> prof_cnt[kProfCounts] = {};
+  uint64_t prof_base_cyc[kProfPhases] = {};
+  uint64_t prof_base_cnt[kProfCounts] = {};
+  static void bump(std::atomic<uint64_t> &c, uint64_t d) {
+    c.store(c.load(std::memory_order_relaxed) + d, std::memory_order_relaxed);
+  }
   void lap(int k) {
     if (__builtin_expect(prof_on, 0)) {
       const uint64_t t = tsc_now();
-      prof_cyc[k] += t - prof_t;
+      bump(prof_cyc[k], t - prof_t);
       prof_t = t;
     }
   }
@@ -405,8 +413,8 @@ struct IoEngine::Worker {
       }
       i = j;
     }
-    prof_cnt[PC_REQ] += n;
-    ++prof_cnt[PC_BATCH];
+    bump(prof_cnt[PC_REQ], n);
+    bump(prof_cnt[PC_BATCH], 1);
     fin.clear();
     lap(PF_FINISH);
   }
@@ -649,7 +657,7 @@ struct IoEngine::Worker {
         }
         if (run.ok) {
           ndesc += run.n;
-          prof_cnt[PC_DESC] += run.n;
+          bump(prof_cnt[PC_DESC], run.n);
         }
       }
       i = k;
@@ -869,7 +877,7 @@ struct IoEngine::Worker {
         if (q.empty() && quiet) {
           if (stop) break;
           sleeping = true;
-          ++prof_cnt[PC_SLEEP];
+          bump(prof_cnt[PC_SLEEP], 1);
           cv.wait(g, [&] { return stop || !q.empty(); });
           sleeping = false;
           lap(PF_IDLE);
@@ -894,7 +902,7 @@ struct IoEngine::Worker {
       lap(PF_START);
       if (use_ring && ring.pending()) {
         ring.enter(0);
-        ++prof_cnt[PC_ENTER];
+        bump(prof_cnt[PC_ENTER], 1);
         lap(PF_SUBMIT);
       }
       const bool drained = lpos == local.size();
@@ -912,7 +920,7 @@ struct IoEngine::Worker {
           reap_fake();
         } else {
           ring.enter(1);
-          ++prof_cnt[PC_ENTER];
+          bump(prof_cnt[PC_ENTER], 1);
           lap(PF_WAIT);
           reap();
         }
@@ -954,14 +962,17 @@ int IoEngine::prof(uint64_t *out, int nout, bool reset) {
   memset(out, 0, sizeof(uint64_t) * need);
   out[0] = workers_.size();
   out[1] = tsc_khz();
+  std::lock_guard<std::mutex> lk(prof_mu_);
   for (auto &w : workers_) {
     for (int k = 0; k < kProfPhases; ++k) {
-      out[2 + k] += w->prof_cyc[k];
-      if (reset) w->prof_cyc[k] = 0;
+      const uint64_t v = w->prof_cyc[k].load(std::memory_order_relaxed);
+      out[2 + k] += v - w->prof_base_cyc[k];
+      if (reset) w->prof_base_cyc[k] = v;
     }
     for (int k = 0; k < kProfCounts; ++k) {
-      out[2 + kProfPhases + k] += w->prof_cnt[k];
-      if (reset) w->prof_cnt[k] = 0;
+      const uint64_t v = w->prof_cnt[k].load(std::memory_order_relaxed);
+      out[2 + kProfPhases + k] += v - w->prof_base_cnt[k];
+      if (reset) w->prof_base_cnt[k] = v;
     }
   }
   CallerProf &cp = caller_prof();

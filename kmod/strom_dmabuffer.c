@@ -185,8 +185,20 @@ struct strom_dbuf_map *strom_dma_buffer_map(struct file *filp, struct device *de
 		b->cap_maps = cap;
 	}
 	m = dbuf_map_new(b, dev, false);
-	if (!m)
+	if (!m) {
+		/* Page-by-page maps stay until the buffer is released.  Under
+		 * swiotlb every page holds a bounce slot for that long, so the
+		 * buffers a controller can serve at once are bounded by the
+		 * bounce pool (64 MiB by default): a raid0 route over several
+		 * members maps the buffer once per member.  Said in the log,
+		 * since SSD2RAM then fails with -EIO, not at allocation. */
+		pr_notice("nvme-strom: dma buffer %zu bytes: 4 MiB segment map refused, mapping %d pages one by one\n",
+			  (size_t)b->length, b->nsegs * SEG_PAGES);
 		m = dbuf_map_new(b, dev, true);
+		if (!m)
+			pr_warn("nvme-strom: dma buffer %zu bytes: page-by-page map failed (bounce pool exhausted?)\n",
+				(size_t)b->length);
+	}
 	if (m)
 		b->maps[b->nmaps++] = m;
 out:

@@ -139,6 +139,7 @@ void kshim_might_sleep(const char *file, int line);
 void kshim_printk(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 #define pr_info(...) kshim_printk(__VA_ARGS__)
 #define pr_notice(...) kshim_printk(__VA_ARGS__)
+#define pr_warn(...) kshim_printk(__VA_ARGS__)
 #define cmpxchg(p, o, n) __sync_val_compare_and_swap(p, o, n)
 #define uid_eq(a, b) ((a).val == (b).val)
 #define MKDEV(ma, mi) (((ma) << 20) | (mi))

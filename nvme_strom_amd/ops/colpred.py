@@ -245,6 +245,30 @@ def _merge(rs: List[Tuple], adjacent_int: bool) -> List[Tuple]:
     return [tuple(r) for r in out]
 
 
+def _dec_float_bound(x: float, side: str, scale: Fraction, tmin: int, tmax: int) -> int:
+    """Bound on the unscaled integer u of a decimal column compared with a
+    float constant the way pyarrow.compute does it: the column is cast to
+    float64, so u qualifies iff float64(u / 10^scale) <op> x (float() of a
+    Fraction rounds correctly, as the cast does for |u| < 2^53).  That map
+    is monotone in u, so the bound is the first u whose float passes
+    (``>=`` / ``>``), or the one before it (``<`` / ``<=``), found by
+    bisection over the storage range (float spacing can exceed 10^-scale,
+    so several u round onto x)."""
+    strict = side in (">", "<=")               # first u with fl(u) > x, else >= x
+
+    def ok(u: int) -> bool:
+        f = float(Fraction(u) / scale)
+        return f > x if strict else f >= x
+    lo, hi = tmin - 1, tmax + 1                # ok(lo) taken false, ok(hi) true
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if ok(mid):
+            hi = mid
+        else:
+            lo = mid
+    return hi if side in (">", ">=") else hi - 1
+
+
 def _num_ranges(op: str, v, col: Column, dt: str) -> Tuple[List[Tuple], int]:
     """(ranges in the compare domain, extra flags) of a numeric predicate
     (op already stripped of its negation)."""
@@ -275,6 +299,8 @@ def _num_ranges(op: str, v, col: Column, dt: str) -> Tuple[List[Tuple], int]:
         scale = Fraction(10) ** col.scale if col.kind == "decimal" else 1
 
         def bound(x, side):
+            if col.kind == "decimal" and isinstance(x, (float, np.floating)) and math.isfinite(x):
+                return _dec_float_bound(float(x), side, scale, tmin, tmax)
             try:
                 e = _exact(x, col) * scale
             except OverflowError:               # NaN compares false, +-inf past any int

@@ -21,6 +21,11 @@ def table(n: int = 3000, seed: int = 5):
              "cherry", "cherries", "日本語", "日本", "zz" * 13, "prefix-" + "x" * 30]
     s = [words[k] for k in rng.integers(0, len(words), n)]
     ts0 = np.datetime64("2024-01-01T00:00:00", "us").astype(np.int64)
+    # decimal(18, 4) unscaled values; a fifth of them near 1.1 / 2.5, so float
+    # constants (compared as float64, like pyarrow) select something
+    dv = rng.integers(-10**9, 10**9, n)
+    near = rng.random(n) < 0.2
+    dv[near] = rng.choice([11000, 10999, 11001, -11000, 25000], int(near.sum()))
     cols = {
         "i8": pa.array(rng.integers(-128, 128, n).astype(np.int8), mask=nulls()),
         "u32": pa.array(rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)),
@@ -38,8 +43,8 @@ def table(n: int = 3000, seed: int = 5):
         "bin": pa.array([x.encode() for x in s], pa.binary()),
         "ls": pa.array(s, pa.large_string()),
         "dict": pa.array([words[k] for k in rng.integers(0, 9, n)], mask=nulls()).dictionary_encode(),
-        "dec": pa.array([decimal.Decimal(int(v)).scaleb(-4) for v in
-                         rng.integers(-10**9, 10**9, n)], pa.decimal128(18, 4), mask=nulls()),
+        "dec": pa.array([decimal.Decimal(int(v)).scaleb(-4) for v in dv], pa.decimal128(18, 4),
+                        mask=nulls()),
         "idict": pa.DictionaryArray.from_arrays(
             pa.array(rng.integers(0, 20, n).astype(np.int8)),
             pa.array(np.arange(20, dtype=np.int64) * 1000 - 3000)),
@@ -139,6 +144,14 @@ def cases():
                         pa.scalar(decimal.Decimal("7.25"), pa.decimal128(18, 4)))),
         ("dec in", P("dec").isin([decimal.Decimal("0.0001"), 3]),
          lambda t: isin(c(t, "dec"), [decimal.Decimal("0.0001"), decimal.Decimal("3.0000")])),
+        # float constants on a decimal column: compared in float64, as pyarrow does
+        ("dec == 1.1", P("dec") == 1.1, lambda t: pc.equal(c(t, "dec"), 1.1)),
+        ("dec >= 1.1", P("dec") >= 1.1, lambda t: pc.greater_equal(c(t, "dec"), 1.1)),
+        ("dec < 1.1", P("dec") < 1.1, lambda t: pc.less(c(t, "dec"), 1.1)),
+        ("dec > 2.5", P("dec") > 2.5, lambda t: pc.greater(c(t, "dec"), 2.5)),
+        ("dec in floats", P("dec").isin([1.1, 2.5]),
+         lambda t: pc.and_(pc.is_in(c(t, "dec"), value_set=pa.array([1.1, 2.5])),
+                           pc.is_valid(c(t, "dec")))),
         ("or across columns", Or(P("i8") < -100, P("s") == "apple", P("b") == True),  # noqa: E712
          lambda t: pc.or_kleene(pc.or_kleene(pc.less(c(t, "i8"), -100), pc.equal(c(t, "s"), "apple")),
                           pc.equal(c(t, "b"), True))),

@@ -10,6 +10,7 @@
 #   zpmc       two PMC passes (issue / wait / LDS / memory mix) over zstd_bench val + x
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
+#   zatrace    kernel trace of the Arrow ZSTD scan per group size (ingest grid vs decoder)
 #   mtests     model-level GPU tests only (PG / Arrow / multi-rank scans)
 #   smoke      __graft_entry__.smoke()
 #   bench      python bench.py (default flagship config)
@@ -73,6 +74,14 @@ for phase in "$@"; do
                  --no-lz4 --iters 1) || exit 1
           done ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
+    zatrace) # kernel trace of the Arrow ZSTD scan at ZATRACE_DIVS group sizes: ingest grid vs decoder concurrency
+          for dv in ${ZATRACE_DIVS:-1 4}; do
+            (cd /tmp && STROM_ARROW_ZSTD_DIV=$dv step zatrace_d$dv 300 rocprofv3 --kernel-trace --stats --output-format csv \
+              -d "$OUT/zatrace_d$dv" -o trace -- python3 -m nvme_strom_amd.tools.arrow_bench --codec zstd --columns val \
+              --no-qual2 --no-strings --reps 2 --out "$OUT/zatrace_d$dv.json") || exit 1
+            python -m nvme_strom_amd.tools.overlap_trace $(find "$OUT/zatrace_d$dv" -name '*kernel_trace.csv' | head -1) \
+              --side zstd --md "$OUT/zatrace_d${dv}_summary.md" > "$OUT/zatrace_d${dv}_summary.txt" 2>&1 || exit 1
+          done ;;
     ztrace) (cd /tmp && step ztrace 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ztrace" -o trace \
               -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds val,x --levels 1 --streams 2048 --no-lz4) ;;
     par) step par 300 python -u -m nvme_strom_amd.tools.kbench --only par --out "$OUT/par.json" ;;
