@@ -285,6 +285,17 @@ def main() -> int:
         ioctl_p50 = float(np.percentile(S.ioctl_latency(buf.handle, 0, fd, offs)[50:], 50)) / 1e3
         costs = S.host_costs(fd)
 
+    # the storage's own sequential rate in this run: host-only io_uring
+    # O_DIRECT reads of the same shard, the engine's request size, ring
+    # count and depth, each ring over its own run of the file (no GPU, no
+    # engine) — so value / storage says how much of the storage the load
+    # path delivers.  All ranks read at once, as their loads do.
+    mreq = int(S.config_get("max_request"))
+    nw, qd = int(S.config_get("workers")), int(S.config_get("queue_depth"))
+    if world > 1:
+        dist.barrier()
+    _, seq_gib = S.raw_read_rate(fd, mreq, max(64, 2 * W // mreq), threads=nw,
+                                 qd=min(256, max(1, qd)), sequential=True)
     # VFS control: pread -> pinned -> HtoD, same window
     S.evict_file(fd)
     vt = vfs_control(path, 0, W, buf.tensor, segment_sz=a.segment_mib << 20, nr_segments=a.depth)
@@ -293,8 +304,10 @@ def main() -> int:
     if world > 1:
         p50, p99, p50_py, ioctl_p50 = allreduce([p50, p99, p50_py, ioctl_p50], dist.ReduceOp.MAX)
         vfs_total = allreduce([vfs], dist.ReduceOp.SUM)[0]
+        seq_total = allreduce([seq_gib], dist.ReduceOp.SUM)[0]
     else:
         vfs_total = vfs
+        seq_total = seq_gib
     ver = 1.0 if verified else 0.0
     hist = S.stat_hist()
     ing = S.ingest_info(local_dev)
@@ -312,6 +325,11 @@ def main() -> int:
         "vs_baseline": round(value / vfs_total, 3) if vfs_total > 0 else None,
         "baseline": "VFS control (pread->pinned->HtoD, nvme_test -f methodology) on the same box",
         "vfs_control_GiBps": round(vfs_total, 3),
+        "storage_seq_GiBps": round(seq_total, 3),
+        "of_storage": round(value / seq_total, 3) if seq_total > 0 else None,
+        "storage_seq_note": (f"host-only io_uring O_DIRECT sequential read of the same shard, "
+                             f"{mreq >> 10} KiB requests, {nw} rings x QD {qd}, disjoint run per "
+                             "ring, all ranks at once, same run"),
         "p50_4k_lat_us": round(p50, 2),
         "p99_4k_lat_us": round(p99, 2),
         "p50_4k_lat_python_us": round(p50_py, 2),

@@ -260,9 +260,11 @@ HD void code_base(uint32_t kind, uint32_t c, uint32_t &base, uint32_t &add) {
 // ------------------------------------------------------------- input
 HD uint32_t gbyte(const Ctx &c, uint32_t p) { return p < c.len ? c.in[p] : 0u; }
 
-HD const uint8_t *sbytes(const Smem &s) { return (const uint8_t *)&s; }
+template <class S>
+HD const uint8_t *sbytes(const S &s) { return (const uint8_t *)&s; }
 
-HD uint32_t wbyte(const Smem &s, const Win &w, const Ctx &c, uint32_t p) {
+template <class S>
+HD uint32_t wbyte(const S &s, const Win &w, const Ctx &c, uint32_t p) {
   const uint32_t r = p - w.lo;
   return r < w.n ? sbytes(s)[w.off + r] : gbyte(c, p);
 }
@@ -284,7 +286,8 @@ HD bool br_init(BR &b, const Ctx &c, uint32_t beg, uint32_t len) {
   return true;
 }
 
-HD void br_fill(BR &b, const Smem &s, const Win &w, const Ctx &c) {
+template <class S>
+HD void br_fill(BR &b, const S &s, const Win &w, const Ctx &c) {
   const int32_t nb = b.nbits > 0 ? b.nbits : 0;
   int32_t base = nb - 57;
   base = base > 0 ? (base + 7) & ~7 : 0;    // >= 50 readable bits after a fill
@@ -307,7 +310,8 @@ HD void br_fill(BR &b, const Smem &s, const Win &w, const Ctx &c) {
 
 // the next k (<= 32) bits without consuming them; past the stream start
 // the bits read as zeros (the caller sees nbits < 0 afterwards)
-HD uint32_t br_peek(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k) {
+template <class S>
+HD uint32_t br_peek(BR &b, const S &s, const Win &w, const Ctx &c, uint32_t k) {
   if (b.nbits - (int32_t)k < b.cbase && b.cbase != 0) br_fill(b, s, w, c);
   const int32_t lo = b.nbits - (int32_t)k - b.cbase;
   const uint64_t m = (1ull << k) - 1;
@@ -316,7 +320,8 @@ HD uint32_t br_peek(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k
   return (uint32_t)((b.cont << (-lo)) & m);
 }
 
-HD uint32_t br_read(BR &b, const Smem &s, const Win &w, const Ctx &c, uint32_t k) {
+template <class S>
+HD uint32_t br_read(BR &b, const S &s, const Win &w, const Ctx &c, uint32_t k) {
   if (k == 0) return 0;
   const uint32_t v = br_peek(b, s, w, c, k);
   b.nbits -= (int32_t)k;
@@ -349,7 +354,8 @@ HD uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t sh) {
 #endif
 }
 
-HD void br_wfill(BR &b, const Smem &s, const Win &w) {
+template <class S>
+HD void br_wfill(BR &b, const S &s, const Win &w) {
   const int32_t nb = b.nbits > 0 ? b.nbits : 0;
   const int32_t base = (nb - 57) & ~7;             // floor to a byte: 57..64 bits readable
   int32_t r = (int32_t)(b.beg - w.lo) + (base >> 3);
@@ -373,7 +379,8 @@ HD void br_wfill(BR &b, const Smem &s, const Win &w) {
   b.cbase = base;
 }
 
-HD void br_need(BR &b, const Smem &s, const Win &w, uint32_t k) {
+template <class S>
+HD void br_need(BR &b, const S &s, const Win &w, uint32_t k) {
   if (b.nbits - (int32_t)k < b.cbase) br_wfill(b, s, w);
 }
 
@@ -521,7 +528,8 @@ HD void fse_predef(Smem &s, SeqEnt *tab, uint32_t kind, uint32_t &al) {
 
 // ------------------------------------------------------------- Huffman
 // Huffman tree description (RFC 8878 4.2.1) -> weights hw[0..nw)
-HD bool huf_weights(Smem &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &used,
+template <class S>
+HD bool huf_weights(S &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &used,
                     uint32_t &nw) {
   if (p >= end) return ZF(false);
   const uint32_t hb = gbyte(c, p);
@@ -573,7 +581,8 @@ HD bool huf_weights(Smem &s, const Ctx &c, uint32_t p, uint32_t end, uint32_t &u
 
 // decode table: entries ordered by weight, then symbol; a weight-w symbol
 // covers 2^(w-1) entries and has code length hbits + 1 - w
-HD bool huf_build(Smem &s, uint32_t nw) {
+template <class S>
+HD bool huf_build(S &s, uint32_t nw) {
   uint32_t total = 0;
   for (uint32_t i = 0; i < nw; ++i) {
     const uint32_t w = s.hw[i];
@@ -611,7 +620,8 @@ HD bool huf_build(Smem &s, uint32_t nw) {
 }
 
 // ------------------------------------------------------------- lane 0: headers
-HD void stream_init(Smem &s, const Ctx &c, int codec) {
+template <class S>
+HD void stream_init(S &s, const Ctx &c, int codec) {
   s.err = 0;
   s.op = 0;
   s.ip = 0;
@@ -644,7 +654,8 @@ HD void stream_init(Smem &s, const Ctx &c, int codec) {
 
 // Parse frame headers (skipping skippable frames) and the next block
 // header.  Sets s.state = kDone at the end of the input.
-HD void next_block(Smem &s, const Ctx &c) {
+template <class S>
+HD void next_block(S &s, const Ctx &c) {
   if (s.state == kStored) {        // Arrow buffer stored uncompressed
     s.state = kBlock;
     s.btype = kRaw;
@@ -747,7 +758,8 @@ HD void next_block(Smem &s, const Ctx &c) {
 
 // after a block: advance; at the end of a frame skip the checksum and
 // check the content size
-HD void end_block(Smem &s, const Ctx &c) {
+template <class S>
+HD void end_block(S &s, const Ctx &c) {
   s.ip = s.bend;
   if (!s.blast) return;
   if (s.cksum) {
@@ -763,7 +775,8 @@ HD void end_block(Smem &s, const Ctx &c) {
   s.state = kFrame;                // the next frame, or the end of the input
 }
 
-HD bool lit_header(Smem &s, const Ctx &c) {
+template <class S>
+HD bool lit_header(S &s, const Ctx &c) {
   const uint32_t p = s.ip, end = s.bend;
   const uint32_t b0 = gbyte(c, p), type = b0 & 3, sf = (b0 >> 2) & 3;
   s.lit_used = 0;
@@ -1559,7 +1572,8 @@ HD uint32_t sym_resolve(uint32_t v, const uint32_t *rin) {
 // description (literals type 2) and the LL / OF / ML table definitions of
 // its sequence section (the table descriptions are walked with fse_norm to
 // find where each ends).  false: a header it cannot follow.
-HD bool prewalk_defs(Smem &s, const Ctx &c, FpDefs &d) {
+template <class S>
+HD bool prewalk_defs(S &s, const Ctx &c, FpDefs &d) {
   const uint32_t p = s.bstart, end = s.bend, b0 = gbyte(c, p), lt = b0 & 3, sf = (b0 >> 2) & 3;
   uint32_t q;
   if (lt <= 1) {
@@ -1611,7 +1625,8 @@ HD bool prewalk_defs(Smem &s, const Ctx &c, FpDefs &d) {
   return true;
 }
 
-HD void defs_of(FpDefs &d, const Smem &s) {
+template <class S>
+HD void defs_of(FpDefs &d, const S &s) {
   d.hbits = s.hbits ? 1u : 0u;
   d.hdesc = s.hdesc;
   d.hdesc_end = s.hdesc_end;
@@ -2186,6 +2201,834 @@ struct HostGroup {
   }
 };
 
+// ------------------------------------------------------------- lane-parallel
+// The decoders above run a block's serial entropy stages on a whole wave:
+// 64 lanes compute the same values, one symbol / sequence at a time, so a
+// stream's latency is ~1,000 cycles per sequence and the chip fills only
+// with thousands of streams (profiles/r4/zstd: 2,048 val streams at 34.8
+// GB/s, VALU-issue-bound).  The lane-parallel ("LP") decoder gives every
+// BLOCK its own lanes instead: LPB blocks share a wave, a block's four
+// Huffman literal streams decode on four of its lanes and its sequence
+// bitstream on one, each lane walking its own tables and input window in
+// LDS.  Three launches:
+//   walk     one lane per stream: frame + block headers, every block's
+//            literal / sequence counts and the Huffman-tree / FSE-table
+//            definitions it may refer to (treeless / repeat-mode blocks
+//            rebuild them on their own lanes); blocks go to one list,
+//            entries are allocated from a pool
+//   entropy  LPB blocks per wave (all of a column's blocks at once, in one
+//            or two resident rounds): literals decode straight into the
+//            stream's OUTPUT buffer, packed at its tail, and sequences into
+//            16-byte entries (repeat offsets symbolic, as the frame-parallel
+//            decoder's)
+//   exec     one workgroup per stream, blocks in order: exec_fp's batches
+//            over the entries, gathers split from stores (a literal's tail
+//            position is never below its output position — the in-place
+//            decompression argument — but a batch may write where a later
+//            byte of the same batch reads), symbolic offsets resolved and
+//            every distance checked
+// Any stream the walk cannot take (several frames, a stored Arrow buffer,
+// a header it cannot follow, pool exhausted) or whose LP decode reports an
+// error is decoded again by the serial decoder (run()) in the exec launch,
+// so statuses and errors are the serial decoder's.
+#ifndef ZS_LPB
+#define ZS_LPB 8
+#endif
+constexpr uint32_t LPB = ZS_LPB;              // blocks per wave
+constexpr uint32_t LPL = NT / LPB;            // lanes per block: >= 4 (one per literal stream)
+static_assert(NT % LPB == 0 && LPL >= 4, "LP lanes");
+constexpr uint32_t LP_LSYM = 128;             // literal symbols per stream per round
+constexpr uint32_t LP_LWIN = 256;             // its input window (one dword per lane)
+constexpr uint32_t LP_SEQN = 64;              // sequences per round
+constexpr uint32_t LP_SWIN = 768;             // its input window (three dwords per lane)
+static_assert(LP_LSYM * 11 / 8 + 24 <= LP_LWIN && LP_SEQN * 89 / 8 + 24 <= LP_SWIN, "LP windows");
+static_assert(LP_LWIN == 4 * NT && LP_SWIN % (4 * NT) == 0, "LP window loads");
+
+// compact FSE entry (4 bytes, a third of the LDS the 8-byte SeqEnt takes):
+// code | bits << 8 | next state base << 16; the code's baseline and extra
+// bits come from code_base()
+HD uint32_t lp_ent(uint32_t code, uint32_t nb, uint32_t next) { return code | nb << 8 | next << 16; }
+
+HD bool fse_build4(uint32_t *tab, const int16_t *norm, uint32_t nsym, uint32_t al,
+                   uint16_t *snext) {
+  const uint32_t size = 1u << al, mask = size - 1;
+  uint32_t high = size - 1;
+  for (uint32_t s = 0; s < nsym; ++s) {
+    if (norm[s] == -1) {
+      tab[high--] = s;
+      snext[s] = 1;
+    } else {
+      snext[s] = (uint16_t)norm[s];
+    }
+  }
+  const uint32_t step = (size >> 1) + (size >> 3) + 3;
+  uint32_t pos = 0;
+  for (uint32_t s = 0; s < nsym; ++s)
+    for (int32_t i = 0; i < norm[s]; ++i) {
+      tab[pos] = s;
+      do pos = (pos + step) & mask;
+      while (pos > high);
+    }
+  if (pos != 0) return ZF(false);
+  for (uint32_t u = 0; u < size; ++u) {
+    const uint32_t s = tab[u] & 255;
+    const uint32_t nx = snext[s]++;
+    const uint32_t nb = al - hibit(nx);
+    tab[u] = lp_ent(s, nb, (nx << nb) - size);
+  }
+  return true;
+}
+
+// seq_table with compact entries (the same modes and saved definitions)
+template <class S>
+HD bool seq_table4(S &s, const Ctx &c, uint32_t mode, uint32_t kind, uint32_t &p, uint32_t end,
+                   uint32_t *tab, uint32_t &al, uint32_t &have) {
+  const uint32_t maxsym = kind == kLL ? 35 : kind == kML ? 52 : 31;
+  const uint32_t maxal = kind == kOF ? 8 : 9;
+  const bool repeat = mode == 3;
+  if (repeat && !have) return ZF(false);
+  const uint32_t m = repeat ? s.tmode[kind] : mode;
+  const uint32_t q0 = repeat ? s.tpos[kind] : p;
+  const uint32_t qend = repeat ? s.tend[kind] : end;
+  uint32_t q = q0;
+  if (m == 0) {
+    const int8_t *src = kind == kLL ? kNormLL : kind == kML ? kNormML : kNormOF;
+    const uint32_t n = kind == kLL ? 36 : kind == kML ? 53 : 29;
+    for (uint32_t i = 0; i < n; ++i) s.norm[i] = src[i];
+    al = kind == kOF ? 5 : 6;
+    fse_build4(tab, s.norm, n, al, s.snext);
+  } else if (m == 1) {
+    if (q >= qend) return ZF(false);
+    const uint32_t sym = gbyte(c, q++);
+    if (sym > maxsym) return ZF(false);
+    tab[0] = lp_ent(sym, 0, 0);
+    al = 0;
+  } else {
+    FR f{q, qend, 0};
+    uint32_t nsym;
+    if (!fse_norm(c, f, s.norm, maxsym, maxal, nsym, al)) return ZF(false);
+    if (!fse_build4(tab, s.norm, nsym, al, s.snext)) return ZF(false);
+    q += f.bit >> 3;
+  }
+  if (!repeat) {
+    s.tmode[kind] = m;
+    s.tpos[kind] = q0;
+    s.tend[kind] = end;
+    p = q;
+  }
+  have = 1;
+  return true;
+}
+
+// ---- global records (the pool: header, streams, blocks, fallback slots, entries)
+struct LpHdr {
+  uint32_t nblk;             // blocks listed (may pass the capacity: those streams fall back)
+  uint32_t lp_done;          // streams the LP path decoded (the rest: the serial decoder)
+  uint64_t ent_used;         // entry bytes allocated
+};
+
+enum : uint32_t { kLpDecode = 0, kLpSerial = 1 };
+
+struct LpStream {
+  uint32_t first, nblk, mode, fcs_set, fcs, cksum, ck_pos, pad;
+  int64_t expect;
+};
+
+struct alignas(16) LpBlock {
+  // walk
+  uint32_t stream, bstart, bend, btype, bsize, blast, active, lit_off;
+  FpDefs d;
+  uint64_t ent_off;
+  // entropy
+  uint32_t lit_kind, lit_n, lit_base, lit_rle, nseq, nent, bout;
+  uint32_t rep[3];
+  int32_t err;
+};
+
+// the walk's per-lane state: what stream_init / next_block / prewalk_defs use
+struct LpWalk {
+  int32_t err;
+  uint32_t op, ip, state;
+  int64_t expect;
+  uint32_t hbits, hdesc, hdesc_end, ck_need, ck_pos, fcs_set, fcs, cksum, fstart;
+  uint32_t rep[3];
+  uint32_t have_ll, have_of, have_ml, tmode[3], tpos[3], tend[3];
+  uint32_t bstart, bend, btype, bsize, blast;
+  int16_t norm[64];
+};
+
+// a compressed block's regenerated literal count (R), the literal section's
+// type and its sequence count, from the two section headers
+HD bool lp_sizes(const Ctx &c, uint32_t p, uint32_t end, uint32_t &R, uint32_t &lt,
+                 uint32_t &nseq) {
+  if (p >= end) return false;
+  const uint32_t b0 = gbyte(c, p), sf = (b0 >> 2) & 3;
+  lt = b0 & 3;
+  uint32_t q;
+  if (lt <= 1) {
+    const uint32_t hl = (sf & 1) == 0 ? 1 : sf == 1 ? 2 : 3;
+    R = hl == 1 ? b0 >> 3 : hl == 2 ? (b0 >> 4) + (gbyte(c, p + 1) << 4)
+                          : (b0 >> 4) + (gbyte(c, p + 1) << 4) + (gbyte(c, p + 2) << 12);
+    q = p + hl + (lt == 0 ? R : 1);
+  } else {
+    const uint32_t hl = sf <= 1 ? 3 : sf == 2 ? 4 : 5, bits = sf <= 1 ? 10 : sf == 2 ? 14 : 18;
+    uint64_t h = 0;
+    for (uint32_t j = 0; j < hl; ++j) h |= (uint64_t)gbyte(c, p + j) << (8 * j);
+    R = (uint32_t)(h >> 4) & ((1u << bits) - 1);
+    q = p + hl + ((uint32_t)(h >> (4 + bits)) & ((1u << bits) - 1));
+  }
+  if (R > MAXB || q >= end) return false;
+  const uint32_t n0 = gbyte(c, q);
+  nseq = n0 < 128 ? n0 : n0 < 255 ? ((n0 - 128) << 8) + gbyte(c, q + 1)
+                                  : gbyte(c, q + 1) + (gbyte(c, q + 2) << 8) + 0x7F00;
+  return nseq <= kMaxSeq;
+}
+
+// One stream's headers.  rec == nullptr: count (blocks, literal bytes
+// packed at the output's tail, entries); else fill rec[0..nblk).  false:
+// the LP path does not take the stream (the serial decoder will).
+// lit_start: where the tail-packed literal regions begin (cap - the first
+// pass's lits); ent_base: the stream's entries in the pool.
+HD bool lp_walk(LpWalk &s, const Ctx &c, int codec, uint32_t stream, LpBlock *rec,
+                uint32_t lit_start, uint64_t ent_base, uint32_t &nblk, uint32_t &lits,
+                uint32_t &nent, LpStream &st) {
+  stream_init(s, c, codec);
+  if (s.err || s.state == kStored) return false;
+  nblk = lits = nent = 0;
+  uint32_t frames = 0, pos = lit_start;      // tail packing cursor
+  FpDefs d{};
+  bool fresh = true;
+  for (;;) {
+    if (s.state == kFrame) {
+      if (s.ip == c.len) break;              // end of the input
+      if (++frames > 1) return false;        // several frames: the serial decoder
+    }
+    next_block(s, c);
+    if (s.err) return false;
+    if (s.state == kDone) break;
+    if (fresh) {
+      defs_of(d, s);
+      fresh = false;
+    }
+    uint32_t R = 0, lt = 0, nseq = 0;
+    LpBlock b{};
+    b.stream = stream;
+    b.bstart = s.bstart;
+    b.bend = s.bend;
+    b.btype = s.btype;
+    b.bsize = s.bsize;
+    b.blast = s.blast;
+    b.d = d;
+    if (s.btype == kComp) {
+      if (!lp_sizes(c, s.bstart, s.bend, R, lt, nseq) || !prewalk_defs(s, c, d)) return false;
+      const uint32_t lr = lt >= 2 ? R : 0;   // Huffman literals: a region at the tail
+      if (lr > c.cap - lits) return false;
+      lits += lr;
+      b.active = 1;
+      b.lit_off = pos;
+      pos += lr;
+      b.ent_off = ent_base + (uint64_t)nent * sizeof(Ent);
+      nent += nseq + 1;                      // + the trailing literals
+    }
+    if (rec) rec[nblk] = b;
+    ++nblk;
+    s.ip = s.bend;
+    if (s.blast) {                           // end_block without its output checks
+      st.cksum = s.cksum;
+      if (s.cksum) {
+        if (s.ip + 4 > c.len) return false;
+        st.ck_pos = s.ip;
+        s.ip += 4;
+      }
+      st.fcs_set = s.fcs_set;
+      st.fcs = s.fcs;
+      s.state = kFrame;
+    }
+  }
+  if (frames != 1 || !nblk || s.state != kFrame) return false;
+  st.expect = s.expect;
+  return true;
+}
+
+// ---- entropy: LPB blocks per wave
+struct alignas(16) LpB {
+  union {                                    // the block's tables (one section at a time)
+    struct {
+      uint8_t hsym[2048];
+      uint8_t hlen[2048];
+    };
+    struct {
+      uint32_t tll[512];
+      uint32_t tml[512];
+      uint32_t tof[256];
+    };
+  };
+  union {
+    struct {                                 // building a table
+      SeqEnt hwt[64];
+      uint8_t hw[256];
+      int16_t norm[64];
+      uint16_t snext[64];
+      uint32_t wrank[16];
+    };
+    alignas(4) uint8_t lwin[4][LP_LWIN];    // literal streams' windows
+    alignas(4) uint8_t swin[LP_SWIN];       // the sequence bitstream's window
+  };
+  BR lbr[4];
+  BR sbr;
+  uint32_t lcnt[4], lout[4], lwlo[4], lrn[4];
+  uint32_t swlo, act, lact;                  // act: decoding; lact: bit j = stream j has symbols left
+  // lit_header / seq_header state (their field names)
+  uint32_t ip, bend, op, lit_used, lit_direct, lit_n, lit_kind, lit_base, lit_rle;
+  uint32_t hdesc, hdesc_end, hbits, nls;
+  uint32_t tmode[3], tpos[3], tend[3], have_ll, have_of, have_ml;
+  uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
+  uint32_t rep[3], lit, out, nent;
+  int32_t err;
+  uint32_t len, cap;
+  const uint8_t *in;
+  uint8_t *litp;                             // the block's literal region (in the output)
+  Ent *ent;
+};
+
+struct LpWave {
+  LpB b[LPB];
+};
+
+HD Ctx lp_ctx(const LpB &s) { return Ctx{s.in, nullptr, nullptr, s.len, s.cap}; }
+
+// (0) block b's lane 0: load its record, literal section header + tree
+HD void lp_begin(LpB &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const uint8_t *src,
+                 uint8_t *dst, const strom_decomp_desc *desc, uint8_t *pool) {
+  s.act = 0;
+  s.lact = 0;
+  s.err = 0;
+  if (k >= nlist) return;
+  const LpBlock &r = blk[k];
+  if (!r.active) return;
+  const strom_decomp_desc dd = desc[r.stream];
+  s.in = src + dd.src_off;
+  s.len = dd.src_len;
+  s.cap = dd.dst_len;
+  s.litp = dst + dd.dst_off + r.lit_off;
+  s.ent = (Ent *)(pool + r.ent_off);
+  s.ip = r.bstart;
+  s.bend = r.bend;
+  s.op = 0;
+  s.hbits = r.d.hbits;
+  s.hdesc = r.d.hdesc;
+  s.hdesc_end = r.d.hdesc_end;
+  s.have_ll = r.d.have[kLL];
+  s.have_of = r.d.have[kOF];
+  s.have_ml = r.d.have[kML];
+  for (uint32_t j = 0; j < 3; ++j) {
+    s.tmode[j] = r.d.tmode[j];
+    s.tpos[j] = r.d.tpos[j];
+    s.tend[j] = r.d.tend[j];
+    s.rep[j] = kSym | (j << 26);
+  }
+  s.act = 1;
+  const Ctx c = lp_ctx(s);
+  if (!lit_header(s, c)) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  s.lit_direct = 0;
+  if (s.lit_kind == kLitScratch)
+    for (uint32_t j = 0; j < s.nls; ++j)
+      if (s.lcnt[j]) s.lact |= 1u << j;
+}
+
+// (1) literal windows of every stream with symbols left: one dword per lane
+// each, aligned in the input (bytes outside it read as 0)
+HD uint32_t lp_ld32(const uint8_t *in, uint32_t len, uint32_t p) {
+  if (p < len && len - p >= 4) return *(const uint32_t *)(in + p);
+  uint32_t v = 0;
+  for (uint32_t j = 0; j < 4; ++j) v |= (p + j < len ? (uint32_t)in[p + j] : 0u) << (8 * j);
+  return v;
+}
+
+// a window origin moved down to a dword boundary of the input (the caller
+// asked win_lo for 4 bytes less, so the window still reaches as high); below
+// the input it wraps and reads as 0
+HD uint32_t lp_align_lo(const uint8_t *in, uint32_t lo) {
+  return lo - (uint32_t)(((uintptr_t)in + lo) & 3);
+}
+
+HD void lp_lit_windows(LpWave &W, uint32_t t) {
+  for (uint32_t w = 0; w < 4 * LPB; ++w) {
+    LpB &s = W.b[w / 4];
+    const uint32_t j = w % 4;
+    if (!(s.lact >> j & 1)) continue;
+    ((uint32_t *)s.lwin[j])[t] = lp_ld32(s.in, s.len, s.lwlo[j] + 4 * t);
+  }
+}
+
+HD void lp_seq_windows(LpWave &W, uint32_t t) {
+  for (uint32_t b = 0; b < LPB; ++b) {
+    LpB &s = W.b[b];
+    if (!s.act || s.err || s.seq_done >= s.nseq) continue;
+#pragma unroll
+    for (uint32_t k = 0; k < LP_SWIN / (4 * NT); ++k)
+      ((uint32_t *)s.swin)[t + k * NT] = lp_ld32(s.in, s.len, s.swlo + 4 * (t + k * NT));
+  }
+}
+
+// (1) up to LP_LSYM symbols of literal stream j, straight into the block's
+// literal region (four per container check, as lit_chunk)
+HD void lp_lit_chunk(LpB &s, uint32_t j) {
+  const uint32_t left = s.lcnt[j];
+  BR b = s.lbr[j];
+  const Win w{(uint32_t)offsetof(LpB, lwin) + j * LP_LWIN, s.lwlo[j], LP_LWIN};
+  const uint32_t n = left < LP_LSYM ? left : LP_LSYM, mb = s.hbits;
+  uint8_t *dst = s.litp + s.lout[j];
+  const uint32_t nf = n & ~3u;
+  for (uint32_t k = 0; k < nf; k += 4) {
+    br_need(b, s, w, 4 * mb);
+    uint32_t word = 0;
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t lo = (uint32_t)(b.nbits - (int32_t)mb - b.cbase) & 63;
+      const uint32_t x = ubfe((uint32_t)(b.cont >> lo), 0, mb);
+      b.nbits -= (int32_t)s.hlen[x];
+      word |= (uint32_t)s.hsym[x] << (8 * g);
+    }
+    uint8_t *o = dst + k;
+    if (((uintptr_t)o & 3) == 0) {
+      *(uint32_t *)o = word;
+    } else {
+      o[0] = (uint8_t)word;
+      o[1] = (uint8_t)(word >> 8);
+      o[2] = (uint8_t)(word >> 16);
+      o[3] = (uint8_t)(word >> 24);
+    }
+  }
+  if (nf < n) {
+    br_need(b, s, w, 4 * mb);
+#pragma unroll
+    for (uint32_t g = 0; g < 4; ++g) {
+      const uint32_t lo = (uint32_t)(b.nbits - (int32_t)mb - b.cbase) & 63;
+      const uint32_t x = ubfe((uint32_t)(b.cont >> lo), 0, mb);
+      if (nf + g < n) {
+        b.nbits -= (int32_t)s.hlen[x];
+        dst[nf + g] = s.hsym[x];
+      }
+    }
+  }
+  s.lout[j] += n;
+  s.lcnt[j] = left - n;
+  s.lbr[j] = b;
+  if (left == n) {
+    if (b.nbits != 0) s.err = ZF(kErrFormat);   // a stream ends exactly
+    s.lact &= ~(1u << j);
+  }
+}
+
+// (2) lane 0 of a block: the sequence section header (compact tables)
+HD void lp_seq_header(LpB &s) {
+  if (!s.act || s.err) return;
+  const Ctx c = lp_ctx(s);
+  uint32_t p = s.ip;
+  const uint32_t end = s.bend;
+  s.seq_done = 0;
+  s.lit = 0;
+  s.out = 0;
+  s.nent = 0;
+  if (p >= end) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  const uint32_t b0 = gbyte(c, p);
+  uint32_t n;
+  if (b0 == 0) {
+    s.nseq = 0;
+    if (p + 1 != end) s.err = ZF(kErrFormat);
+    return;
+  }
+  if (b0 < 128) {
+    n = b0;
+    p += 1;
+  } else if (b0 < 255) {
+    n = ((b0 - 128) << 8) + gbyte(c, p + 1);
+    p += 2;
+  } else {
+    n = gbyte(c, p + 1) + (gbyte(c, p + 2) << 8) + 0x7F00;
+    p += 3;
+  }
+  s.nseq = n;
+  if (p >= end || n > kMaxSeq) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  const uint32_t modes = gbyte(c, p++);
+  if ((modes & 3) || !seq_table4(s, c, modes >> 6, kLL, p, end, s.tll, s.al_ll, s.have_ll) ||
+      !seq_table4(s, c, (modes >> 4) & 3, kOF, p, end, s.tof, s.al_of, s.have_of) ||
+      !seq_table4(s, c, (modes >> 2) & 3, kML, p, end, s.tml, s.al_ml, s.have_ml) ||
+      p >= end || !br_init(s.sbr, c, p, end - p)) {
+    s.err = ZF(kErrFormat);
+    return;
+  }
+  const Win w{0, 0, 0};
+  s.st_ll = br_read(s.sbr, s, w, c, s.al_ll);
+  s.st_of = br_read(s.sbr, s, w, c, s.al_of);
+  s.st_ml = br_read(s.sbr, s, w, c, s.al_ml);
+  if (s.sbr.nbits < 0) s.err = ZF(kErrFormat);
+}
+
+// (2) lane 0 of a block: up to LP_SEQN sequences into its entries — seq_chunk
+// with symbolic repeat offsets, one lane per block instead of a whole wave
+HD void lp_seq_chunk(LpB &s) {
+  const uint32_t left = s.nseq - s.seq_done;
+  const uint32_t m = left < LP_SEQN ? left : LP_SEQN;
+  BR b = s.sbr;
+  const Win w{(uint32_t)offsetof(LpB, swin), s.swlo, LP_SWIN};
+  uint32_t sll = s.st_ll, sof = s.st_of, sml = s.st_ml;
+  uint32_t r0 = s.rep[0], r1 = s.rep[1], r2 = s.rep[2];
+  uint32_t n = s.nent, out = s.out, lit = s.lit;
+  bool bad = false;
+  Ent *ent = s.ent;
+  for (uint32_t i = 0; i < m; ++i) {
+    const bool more = i + 1 < left;           // the block's last sequence reads no state bits
+    const uint32_t eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
+    uint32_t ob, oa, mb, ma, lb, la;
+    code_base(kOF, eo & 255, ob, oa);
+    code_base(kML, em & 255, mb, ma);
+    code_base(kLL, el & 255, lb, la);
+    br_need(b, s, w, 47);
+    const uint64_t x1 = br_take(b, oa + ma);
+    const uint32_t ml = mb + ubfe((uint32_t)x1, 0, ma);
+    const uint32_t ofv = ob + ubfe((uint32_t)(x1 >> ma), 0, oa);
+    const uint32_t onb = (eo >> 8) & 255, mnb = (em >> 8) & 255, lnb = (el >> 8) & 255;
+    br_need(b, s, w, 42);
+    const uint32_t nst = more ? lnb + mnb + onb : 0;
+    const uint64_t x2 = br_take(b, la + nst);
+    const uint32_t ll = lb + ubfe((uint32_t)(x2 >> nst), 0, la);
+    if (more) {
+      const uint32_t y = (uint32_t)x2;
+      sof = (eo >> 16) + ubfe(y, 0, onb);
+      sml = (em >> 16) + ubfe(y, onb, mnb);
+      sll = (el >> 16) + ubfe(y, onb + mnb, lnb);
+    }
+    uint32_t off = r0;
+    if (ofv != 1 || ll == 0) {
+      const bool isnew = ofv > 3;
+      const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
+      const uint32_t rep01 = k == 1 ? r1 : r0;
+      const uint32_t rep012 = k == 2 ? r2 : rep01;
+      const uint32_t rep = k == 3 ? (is_sym(r0) ? r0 + 1 : r0 - 1) : rep012;
+      off = isnew ? ofv - 3 : rep;
+      bad |= isnew && is_sym(off);
+      const bool shift2 = isnew || k >= 2;
+      r2 = shift2 ? r1 : r2;
+      r1 = r0;
+      r0 = off;
+    }
+    Ent e;
+    e.ll = ll;
+    e.off = off;
+    e.lst = lit;
+    e.ost = out;
+    ent[n++] = e;
+    lit += ll;
+    out += ll + ml;
+  }
+  int32_t err = 0;
+  if (lit > s.lit_n || out > MAXB) err = ZF(kErrFormat);
+  else if (bad) err = ZF(kErrDistance);
+  s.seq_done += m;
+  s.sbr = b;
+  s.st_ll = sll;
+  s.st_of = sof;
+  s.st_ml = sml;
+  s.rep[0] = r0;
+  s.rep[1] = r1;
+  s.rep[2] = r2;
+  s.nent = n;
+  s.out = out;
+  s.lit = lit;
+  if (err) s.err = err;
+}
+
+// (3) lane 0 of a block: trailing literals, checks, the record's results
+HD void lp_end(LpB &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
+  if (k >= nlist) return;
+  LpBlock &r = blk[k];
+  if (!r.active) {
+    r.err = 0;
+    r.bout = r.bsize;
+    r.nent = 0;
+    r.nseq = 0;
+    return;
+  }
+  if (!s.err && s.nseq && s.sbr.nbits != 0) s.err = ZF(kErrFormat);
+  if (!s.err) {
+    const uint32_t rest = s.lit_n - s.lit;   // lit <= lit_n (lp_seq_chunk's check)
+    if (rest) {
+      Ent e;
+      e.ll = rest;
+      e.off = 0;
+      e.lst = s.lit;
+      e.ost = s.out;
+      s.ent[s.nent++] = e;
+      s.out += rest;
+      s.lit += rest;
+    }
+    if (s.out > MAXB) s.err = ZF(kErrFormat);
+  }
+  r.err = s.err;
+  r.lit_kind = s.lit_kind;
+  r.lit_n = s.lit_n;
+  r.lit_base = s.lit_base;
+  r.lit_rle = s.lit_rle;
+  r.nseq = s.nseq;
+  r.nent = s.nent;
+  r.bout = s.out;
+  for (uint32_t j = 0; j < 3; ++j) r.rep[j] = s.rep[j];
+}
+
+// One wave's group of LPB blocks (list entries k0 ..): the phases with the
+// team's barriers between them (the kernel: one wave; the CPU: lanes one
+// after another).
+template <class TM>
+HD void lp_entropy_group(TM &tm, LpWave &W, LpBlock *blk, uint32_t k0, uint32_t nlist,
+                         const uint8_t *src, uint8_t *dst, const strom_decomp_desc *desc,
+                         uint8_t *pool) {
+  tm.each([&](uint32_t t) {
+    if (t % LPL == 0) lp_begin(W.b[t / LPL], blk, k0 + t / LPL, nlist, src, dst, desc, pool);
+  });
+  tm.sync();
+  // literal rounds: window origins, cooperative window loads, LP_LSYM
+  // symbols per stream
+  for (;;) {
+    const bool more = tm.any([&](uint32_t t) {
+      LpB &s = W.b[t / LPL];
+      const uint32_t j = t % LPL;
+      if (j < 4 && s.err) s.lact = 0;
+      return j < 4 && (s.lact >> j & 1);
+    });
+    if (!more) break;
+    tm.each([&](uint32_t t) {
+      LpB &s = W.b[t / LPL];
+      const uint32_t j = t % LPL;
+      if (j < 4 && (s.lact >> j & 1)) s.lwlo[j] = lp_align_lo(s.in, win_lo(s.lbr[j], LP_LWIN - 4));
+    });
+    tm.sync();
+    tm.each([&](uint32_t t) { lp_lit_windows(W, t); });
+    tm.sync();
+    tm.each([&](uint32_t t) {
+      LpB &s = W.b[t / LPL];
+      const uint32_t j = t % LPL;
+      if (j < 4 && (s.lact >> j & 1)) lp_lit_chunk(s, j);
+    });
+    tm.sync();
+  }
+  tm.each([&](uint32_t t) {
+    if (t % LPL == 0) lp_seq_header(W.b[t / LPL]);
+  });
+  tm.sync();
+  for (;;) {
+    const bool more = tm.any([&](uint32_t t) {
+      const LpB &s = W.b[t / LPL];
+      return t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq;
+    });
+    if (!more) break;
+    tm.each([&](uint32_t t) {
+      LpB &s = W.b[t / LPL];
+      if (t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq)
+        s.swlo = lp_align_lo(s.in, win_lo(s.sbr, LP_SWIN - 4));
+    });
+    tm.sync();
+    tm.each([&](uint32_t t) { lp_seq_windows(W, t); });
+    tm.sync();
+    tm.each([&](uint32_t t) {
+      LpB &s = W.b[t / LPL];
+      if (t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq) lp_seq_chunk(s);
+    });
+    tm.sync();
+  }
+  tm.each([&](uint32_t t) {
+    if (t % LPL == 0) lp_end(W.b[t / LPL], blk, k0 + t / LPL, nlist);
+  });
+  tm.fence();
+  tm.sync();
+}
+
+// (exec) a block of an LP stream: exec_fp's batches with the gathers split
+// from the stores (the literals sit in the output buffer)
+HD void gx_gather(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn, uint32_t nb) {
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * tn + t;
+    if (e >= nb) break;
+    const uint32_t v = gptr(sm, e), x = v & ~kTag;
+    uint8_t y;
+    if (v & kLit)
+      y = s.lit_kind == kLitInput ? c.in[s.lit_base + x]
+        : s.lit_kind == kLitRle ? (uint8_t)s.lit_rle : c.lit[x];
+    else
+      y = c.out[x];
+    gptr(sm, e) = y;
+  }
+}
+
+HD void gx_store(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn, uint32_t b0,
+                 uint32_t nb) {
+  uint8_t *o = c.out + s.op + b0;
+  for (uint32_t k = 0; k < EPT; ++k) {
+    const uint32_t e = k * tn + t;
+    if (e >= nb) break;
+    o[e] = (uint8_t)gptr(sm, e);
+  }
+}
+
+template <class TM>
+HD void exec_lp(TM &tm, Smem *sm, FpFrame &s0, const Ctx &c, const Ent *ent, uint32_t nent,
+                uint32_t bout) {
+  Smem &s = sm[0];
+  const uint32_t tn = tm.size(), gob = tn * EPT;
+  tm.one([&] {
+    s.op = s0.op;
+    if ((uint64_t)s0.op + bout > c.cap) s.err = kErrOverflow;
+  });
+  tm.sync();
+  if (s.err) return;
+  if (s.btype != kComp) {
+    tm.each([&](uint32_t t) {
+      uint8_t *o = c.out + s.op;
+      if (s.btype == kRle) {
+        const uint8_t v = (uint8_t)gbyte(c, s.bstart);
+        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = v;
+      } else {
+        const uint8_t *in = c.in + s.bstart;
+        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = in[i];
+      }
+    });
+  } else {
+    const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
+    const uint32_t fpos = s0.op - s0.fstart;
+    const uint32_t gseq = tn / NT * SEQN;
+    for (uint32_t i0 = 0; i0 < nent; i0 += gseq) {
+      const uint32_t m = nent - i0 < gseq ? nent - i0 : gseq;
+      const uint32_t base = ent[i0].ost;
+      const uint32_t end = (i0 + m < nent ? ent[i0 + m].ost : bout) - base;
+      tm.each([&](uint32_t t) {
+        bool bad = false;
+        for (uint32_t i = t; i < m; i += tn) {
+          const Ent e = ent[i0 + i];
+          const uint32_t off = sym_resolve(e.off, rin);
+          const bool has_match = (i0 + i + 1 < nent ? ent[i0 + i + 1].ost : bout) - e.ost > e.ll;
+          bad |= has_match && off - 1 >= fpos + e.ost + e.ll;
+          Smem &q = sm[i / SEQN];
+          q.sll[i % SEQN] = e.ll;
+          q.soff[i % SEQN] = off;
+          q.lst[i % SEQN] = e.lst;
+          q.ost[i % SEQN] = e.ost - base;
+        }
+        if (bad) s.err = ZF(kErrDistance);
+      });
+      tm.sync();
+      if (s.err) return;
+      const GChunk gc{sm, m, end};
+      for (uint32_t b0 = 0; b0 < end; b0 += gob) {
+        const uint32_t nb = end - b0 < gob ? end - b0 : gob;
+        tm.each([&](uint32_t t) { gx_fill(s, gc, t, b0, nb); });
+        tm.sync();
+        while (tm.any([&](uint32_t t) { return gx_double(sm, t, tn, nb); })) {
+        }
+        tm.each([&](uint32_t t) { gx_gather(s, sm, c, t, tn, nb); });
+        tm.sync();
+        tm.each([&](uint32_t t) { gx_store(s, sm, c, t, tn, b0, nb); });
+        tm.fence();
+        tm.sync();
+      }
+      tm.one([&] { s.op += end; });
+      tm.sync();
+    }
+  }
+  tm.fence();
+  tm.sync();
+  tm.one([&] {
+    s0.op += bout;
+    if (s.btype == kComp && s.nseq) {
+      const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
+      s0.rep[0] = sym_resolve(s.rep[0], rin);
+      s0.rep[1] = sym_resolve(s.rep[1], rin);
+      s0.rep[2] = sym_resolve(s.rep[2], rin);
+    }
+  });
+  tm.sync();
+}
+
+// (exec) one stream: its blocks in order, then the frame's checks; any
+// error (or a stream the walk refused) -> the serial decoder, whose status
+// is the stream's.  Returns the status.
+template <class G>
+HD int32_t lp_exec_stream(G &g, Smem *sm, FpFrame &fr, const LpStream &st, const LpBlock *blk,
+                          const uint8_t *pool, const Ctx &c, uint8_t *slot, int codec,
+                          bool &lp_used) {
+  bool ok = st.mode == kLpDecode;
+  for (uint32_t k = 0; ok && k < st.nblk; ++k)
+    if (blk[st.first + k].err) ok = false;
+  if (ok) {
+    g.all([&](auto &tm) {
+      tm.one([&] {
+        fr.op = 0;
+        fr.fstart = 0;
+        fr.rep[0] = 1;
+        fr.rep[1] = 4;
+        fr.rep[2] = 8;
+        sm[0].err = 0;
+      });
+      tm.sync();
+    });
+    g.sync_all();
+    for (uint32_t k = 0; k < st.nblk; ++k) {
+      const LpBlock &b = blk[st.first + k];
+      g.all([&](auto &tm) {
+        tm.one([&] {
+          Smem &s = sm[0];
+          s.btype = b.btype;
+          s.bstart = b.bstart;
+          s.bsize = b.bsize;
+          s.nseq = b.nseq;
+          s.lit_kind = b.lit_kind;
+          s.lit_n = b.lit_n;
+          s.lit_base = b.lit_base;
+          s.lit_rle = b.lit_rle;
+          s.rep[0] = b.rep[0];
+          s.rep[1] = b.rep[1];
+          s.rep[2] = b.rep[2];
+        });
+        tm.sync();
+        const Ctx cb{c.in, c.out, c.out + b.lit_off, c.len, c.cap};
+        exec_lp(tm, sm, fr, cb, (const Ent *)(pool + b.ent_off), b.nent, b.bout);
+      });
+      g.sync_all();
+      if (sm[0].err) break;
+    }
+    g.wave(0, [&](auto &tm) {
+      tm.one([&] {
+        Smem &s = sm[0];
+        if (!s.err && st.fcs_set && fr.op != st.fcs) s.err = ZF(kErrFormat);
+        if (!s.err && st.expect >= 0 && (int64_t)fr.op != st.expect) s.err = ZF(kErrFormat);
+        s.op = fr.op;
+        s.fstart = 0;
+        s.ck_pos = st.ck_pos;
+      });
+      tm.sync();
+      if (!sm[0].err && st.cksum) verify_frame(tm, sm[0], c);
+    });
+    g.sync_all();
+    ok = !sm[0].err;
+  }
+  lp_used = ok;
+  if (!ok) {
+    const Ctx cs{c.in, c.out, slot, c.len, c.cap};
+    g.wave(0, [&](auto &tm) { run(tm, sm[0], cs, codec); });
+    g.sync_all();
+  }
+  return sm[0].err ? sm[0].err : (int32_t)sm[0].op;
+}
+
 // frame-parallel scratch per workgroup: NW literal slots, then NW - 1
 // entry buffers
 HD constexpr size_t fp_scratch(uint32_t nw) {
@@ -2240,6 +3083,155 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(ZS_WPE)
   tm.flush();
 }
 
+// ---- lane-parallel launches
+// pool layout: LpHdr | LpStream[n] | LpBlock[blk_cap] | exec fallback slots | entries
+struct LpLayout {
+  size_t streams, blocks, slots, ents, total;
+  uint32_t blk_cap, nslot;
+  uint64_t ent_cap;
+};
+
+HD size_t lp_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+HD LpLayout lp_layout(uint32_t n, uint32_t blk_cap, uint32_t nslot, uint64_t ent_cap) {
+  LpLayout l;
+  l.blk_cap = blk_cap;
+  l.nslot = nslot;
+  l.ent_cap = ent_cap;
+  l.streams = 256;
+  l.blocks = lp_up(l.streams + (size_t)n * sizeof(LpStream), 256);
+  l.slots = lp_up(l.blocks + (size_t)blk_cap * sizeof(LpBlock), 256);
+  l.ents = lp_up(l.slots + (size_t)nslot * SLOT, 256);
+  l.total = l.ents + (size_t)ent_cap;
+  return l;
+}
+
+// one stream's walk: the stream record, its blocks listed and its entries
+// allocated (two passes over its headers: count, then fill)
+// A: atomics policy (device atomics, or plain adds on the CPU)
+template <class A>
+HD void lp_walk_stream(LpWalk &ws, const Ctx &c, int codec, uint32_t i, uint8_t *pool,
+                       const LpLayout &l) {
+  LpHdr &h = *(LpHdr *)pool;
+  LpStream *st = (LpStream *)(pool + l.streams);
+  LpBlock *blk = (LpBlock *)(pool + l.blocks);
+  LpStream s{};
+  s.mode = kLpSerial;
+  s.expect = -1;
+  uint32_t nblk, lits, nent;
+  if (lp_walk(ws, c, codec, i, nullptr, 0, 0, nblk, lits, nent, s)) {
+    const uint32_t first = A::add32(&h.nblk, nblk);
+    const uint64_t need = (uint64_t)nent * sizeof(Ent);
+    const uint64_t eoff = need ? A::add64(&h.ent_used, need) : 0;
+    const bool fits = first < l.blk_cap && nblk <= l.blk_cap - first && eoff <= l.ent_cap &&
+                      need <= l.ent_cap - eoff;
+    uint32_t n2, l2, e2;
+    if (fits && lp_walk(ws, c, codec, i, blk + first, c.cap - lits, eoff, n2, l2, e2, s) &&
+        n2 == nblk) {
+      s.first = first;
+      s.nblk = nblk;
+      s.mode = kLpDecode;
+    } else {
+      // listed blocks of a stream the serial decoder takes: idle in the
+      // entropy launch
+      for (uint32_t k = first; k < l.blk_cap && k - first < nblk; ++k) {
+        blk[k] = LpBlock{};
+        blk[k].stream = i;
+      }
+      s.mode = kLpSerial;
+    }
+  }
+  st[i] = s;
+}
+
+struct LpDevAtom {
+  static __device__ uint32_t add32(uint32_t *p, uint32_t v) { return atomicAdd(p, v); }
+  static __device__ uint64_t add64(uint64_t *p, uint64_t v) {
+    return (uint64_t)atomicAdd((unsigned long long *)p, (unsigned long long)v);
+  }
+};
+
+struct LpHostAtom {
+  static uint32_t add32(uint32_t *p, uint32_t v) {
+    const uint32_t o = *p;
+    *p = o + v;
+    return o;
+  }
+  static uint64_t add64(uint64_t *p, uint64_t v) {
+    const uint64_t o = *p;
+    *p = o + v;
+    return o;
+  }
+};
+
+constexpr uint32_t LP_WALK_T = 64;
+
+__global__ void __launch_bounds__(LP_WALK_T) zstd_lp_walk(int codec, const uint8_t *src,
+                                                          const strom_decomp_desc *desc, uint32_t n,
+                                                          uint8_t *pool, LpLayout l) {
+  __shared__ LpWalk ws[LP_WALK_T];
+  const uint32_t i = blockIdx.x * LP_WALK_T + threadIdx.x;
+  if (i >= n) return;
+  const strom_decomp_desc d = desc[i];
+  const Ctx c{src + d.src_off, nullptr, nullptr, d.src_len, d.dst_len};
+  lp_walk_stream<LpDevAtom>(ws[threadIdx.x], c, codec, i, pool, l);
+}
+
+__global__ void __launch_bounds__(NT) zstd_lp_entropy(const uint8_t *src, uint8_t *dst,
+                                                      const strom_decomp_desc *desc, uint8_t *pool,
+                                                      LpLayout l) {
+  __shared__ LpWave W;
+  const uint32_t nb = *(const volatile uint32_t *)pool;
+  const uint32_t nlist = nb < l.blk_cap ? nb : l.blk_cap;
+  LpBlock *blk = (LpBlock *)(pool + l.blocks);
+  DevTeam tm;
+  for (uint32_t k0 = blockIdx.x * LPB; k0 < nlist; k0 += gridDim.x * LPB)
+    lp_entropy_group(tm, W, blk, k0, nlist, src, dst, desc, pool + l.ents);
+}
+
+__global__ void __launch_bounds__(NT * FPW) zstd_lp_exec(int codec, const uint8_t *src, uint8_t *dst,
+                                                         const strom_decomp_desc *desc, uint32_t n,
+                                                         int32_t *status, uint8_t *pool, LpLayout l) {
+  __shared__ Smem sm[FPW];
+  __shared__ FpFrame fr;
+  DevGroup g;
+  const LpStream *st = (const LpStream *)(pool + l.streams);
+  const LpBlock *blk = (const LpBlock *)(pool + l.blocks);
+  uint8_t *slot = pool + l.slots + (size_t)(blockIdx.x % l.nslot) * SLOT;
+  for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+    const strom_decomp_desc d = desc[b];
+    const Ctx c{src + d.src_off, dst + d.dst_off, slot, d.src_len, d.dst_len};
+    bool used;
+    const int32_t r = lp_exec_stream(g, sm, fr, st[b], blk, pool + l.ents, c, slot, codec, used);
+    if (threadIdx.x == 0) {
+      status[b] = r;
+      if (used) atomicAdd(&((LpHdr *)pool)->lp_done, 1u);
+    }
+    __syncthreads();
+  }
+}
+
+// LP launch geometry
+uint32_t lp_entropy_per_cu() {
+  const uint32_t per = (160u << 10) / (uint32_t)sizeof(LpWave);
+  return per ? (per > 8 ? 8 : per) : 1;
+}
+
+uint32_t lp_exec_per_cu() {
+  const uint32_t per = (160u << 10) / (uint32_t)(FPW * sizeof(Smem) + sizeof(FpFrame));
+  return per ? per : 1;
+}
+
+double lp_ent_factor() {
+  static double f = 0;
+  if (f == 0) {
+    const char *e = getenv("STROM_ZSTD_LP_ENT");
+    f = e ? atof(e) : 0;
+    if (!(f > 0)) f = 3.0;
+  }
+  return f;
+}
+
 // literal scratch per (device, stream): launches on one stream are ordered,
 // concurrent launches on different streams never share a slot
 std::mutex g_mu;
@@ -2248,7 +3240,17 @@ struct Scratch {
   size_t bytes = 0;
   uint64_t used = 0;         // LRU stamp
 };
-std::map<std::pair<int, void *>, Scratch> g_scratch;
+// key: (device, stream, tag) — tag 0 the wave / frame-parallel decoders'
+// literal slots, 1 the lane-parallel decoder's pool
+struct ScratchKey {
+  int dev;
+  void *stream;
+  int tag;
+  bool operator<(const ScratchKey &o) const {
+    return dev != o.dev ? dev < o.dev : stream != o.stream ? stream < o.stream : tag < o.tag;
+  }
+};
+std::map<ScratchKey, Scratch> g_scratch;
 uint64_t g_scratch_clock = 0;
 constexpr size_t kScratchKeep = 8;   // streams with a cached buffer
 
@@ -2256,10 +3258,10 @@ constexpr size_t kScratchKeep = 8;   // streams with a cached buffer
 // strom_zstd_release) by another thread frees a buffer only with hipFree /
 // hipStreamSynchronize, which wait for work already QUEUED — so the launch
 // that uses the pointer must be queued before the lock drops.
-uint8_t *scratch_for(void *stream, size_t bytes) {
+uint8_t *scratch_for(void *stream, size_t bytes, int tag = 0) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  auto it = g_scratch.find({dev, stream});
+  auto it = g_scratch.find(ScratchKey{dev, stream, tag});
   if (it == g_scratch.end()) {
     // bound the cache: a caller cycling through many streams would
     // otherwise keep up to ~290 MiB per stream; the least recently used
@@ -2271,7 +3273,7 @@ uint8_t *scratch_for(void *stream, size_t bytes) {
       if (lru->second.p) (void)hipFree(lru->second.p);
       g_scratch.erase(lru);
     }
-    it = g_scratch.emplace(std::make_pair(dev, stream), Scratch{}).first;
+    it = g_scratch.emplace(ScratchKey{dev, stream, tag}, Scratch{}).first;
   }
   Scratch &e = it->second;
   e.used = ++g_scratch_clock;
@@ -2419,7 +3421,7 @@ extern "C" int strom_zstd_release(void) {
   int rc = 0;
   for (auto &kv : zs::g_scratch) {
     if (!kv.second.p) continue;
-    if (hipStreamSynchronize((hipStream_t)kv.first.second) != hipSuccess) rc = -5;
+    if (hipStreamSynchronize((hipStream_t)kv.first.stream) != hipSuccess) rc = -5;
     if (hipFree(kv.second.p) != hipSuccess) rc = -5;
   }
   zs::g_scratch.clear();
@@ -2478,4 +3480,114 @@ extern "C" int strom_zstd_host(int codec, const uint8_t *src, uint32_t src_len, 
   const Ctx c{src, dst, lit.get(), src_len, cap};
   run(tm, *s, c, codec);
   return s->err ? s->err : (int32_t)s->op;
+}
+
+// Lane-parallel zstd decode (see the "lane-parallel" section): walk, entropy
+// and exec launches on `stream`.  dst_bytes: the decoded capacity of all
+// streams together (sizes the entry pool: STROM_ZSTD_LP_ENT x dst_bytes;
+// streams that do not fit are decoded by the serial decoder in the exec
+// launch).  The pool is library-kept per (device, stream).
+extern "C" int strom_decompress_zstd_lp(int codec, const void *d_src, void *d_dst,
+                                        const strom_decomp_desc *d_desc, uint32_t nstreams,
+                                        int32_t *d_status, uint64_t dst_bytes, void *stream) {
+  using namespace zs;
+  if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  if (!nstreams) return 0;
+  const uint32_t cus = cu_count();
+  uint32_t xgrid = cus * lp_exec_per_cu();
+  if (xgrid > nstreams) xgrid = nstreams;
+  const uint64_t bc = dst_bytes / 32768 + 4ull * nstreams + 64;
+  const uint32_t blk_cap = bc > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bc;
+  const uint64_t ent_cap = lp_up((uint64_t)(lp_ent_factor() * (double)dst_bytes) + (1 << 20), 256);
+  const LpLayout l = lp_layout(nstreams, blk_cap, xgrid, ent_cap);
+  std::lock_guard<std::mutex> g(g_mu);          // held through the launches (scratch_for)
+  uint8_t *pool = scratch_for(stream, l.total, 1);
+  if (!pool) return -12;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(pool, 0, sizeof(LpHdr), s) != hipSuccess) return -5;
+  hipLaunchKernelGGL(zstd_lp_walk, dim3((nstreams + LP_WALK_T - 1) / LP_WALK_T), dim3(LP_WALK_T), 0, s,
+                     codec, (const uint8_t *)d_src, d_desc, nstreams, pool, l);
+  // enough waves for every listed block in one or two resident rounds
+  const uint64_t want = (blk_cap + LPB - 1) / LPB;
+  uint32_t egrid = cus * lp_entropy_per_cu();
+  if (egrid > want) egrid = (uint32_t)want;
+  hipLaunchKernelGGL(zstd_lp_entropy, dim3(egrid), dim3(NT), 0, s, (const uint8_t *)d_src,
+                     (uint8_t *)d_dst, d_desc, pool, l);
+  hipLaunchKernelGGL(zstd_lp_exec, dim3(xgrid), dim3(NT * FPW), 0, s, codec, (const uint8_t *)d_src,
+                     (uint8_t *)d_dst, d_desc, nstreams, d_status, pool, l);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+// The last LP launch's counters on `stream` (synchronizes it): {blocks
+// listed, streams the LP path decoded, entry bytes used, pool bytes}.
+extern "C" int strom_zstd_lp_last(void *stream, uint64_t *out) {
+  using namespace zs;
+  std::lock_guard<std::mutex> g(g_mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -5;
+  auto it = g_scratch.find(ScratchKey{dev, stream, 1});
+  if (it == g_scratch.end() || !it->second.p) return -2;
+  LpHdr h{};
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess ||
+      hipMemcpy(&h, it->second.p, sizeof h, hipMemcpyDeviceToHost) != hipSuccess)
+    return -5;
+  out[0] = h.nblk;
+  out[1] = h.lp_done;
+  out[2] = h.ent_used;
+  out[3] = it->second.bytes;
+  return 0;
+}
+
+// LP geometry: {LDS bytes per entropy wave, blocks per wave, entropy waves
+// per CU, exec workgroups per CU}
+extern "C" void strom_zstd_lp_info(uint32_t *out) {
+  out[0] = (uint32_t)sizeof(zs::LpWave);
+  out[1] = zs::LPB;
+  out[2] = zs::lp_entropy_per_cu();
+  out[3] = zs::lp_exec_per_cu();
+}
+
+// The LP decoder's three phases on the CPU (host buffers): every stream
+// walked, the block list's groups entropy-decoded lane by lane, every
+// stream executed — the algorithm's reference for the kernels.  status[i]:
+// decoded bytes or an error; returns the number of streams the LP path
+// decoded (the rest went to the serial decoder: refused by the walk, or an
+// LP error).
+extern "C" int strom_zstd_host_lp(int codec, const uint8_t *src, const strom_decomp_desc *desc,
+                                  uint32_t n, uint8_t *dst, int32_t *status, double ent_factor) {
+  using namespace zs;
+  if (codec != STROM_CODEC_ZSTD && codec != STROM_CODEC_ARROW_ZSTD) return -22;
+  if (!n) return 0;
+  uint64_t dst_bytes = 0;
+  for (uint32_t i = 0; i < n; ++i) dst_bytes += desc[i].dst_len;
+  const uint64_t bc = dst_bytes / 32768 + 4ull * n + 64;
+  const uint64_t ent_cap = lp_up((uint64_t)((ent_factor > 0 ? ent_factor : 3.0) * (double)dst_bytes) + 4096, 256);
+  const LpLayout l = lp_layout(n, (uint32_t)bc, 1, ent_cap);
+  std::unique_ptr<uint8_t[]> pool(new uint8_t[l.total]());
+  std::unique_ptr<LpWalk> ws(new LpWalk());
+  for (uint32_t i = 0; i < n; ++i) {
+    const Ctx c{src + desc[i].src_off, nullptr, nullptr, desc[i].src_len, desc[i].dst_len};
+    lp_walk_stream<LpHostAtom>(*ws, c, codec, i, pool.get(), l);
+  }
+  const LpHdr &h = *(const LpHdr *)pool.get();
+  const uint32_t nlist = h.nblk < l.blk_cap ? h.nblk : l.blk_cap;
+  LpBlock *blk = (LpBlock *)(pool.get() + l.blocks);
+  std::unique_ptr<LpWave> W(new LpWave());
+  HostTeam tm;
+  for (uint32_t k0 = 0; k0 < nlist; k0 += LPB)
+    lp_entropy_group(tm, *W, blk, k0, nlist, src, dst, desc, pool.get() + l.ents);
+  std::unique_ptr<Smem[]> sm(new Smem[FPW]());
+  FpFrame fr{};
+  HostGroup g;
+  g.nw = FPW;
+  const LpStream *st = (const LpStream *)(pool.get() + l.streams);
+  uint8_t *slot = pool.get() + l.slots;
+  int taken = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const Ctx c{src + desc[i].src_off, dst + desc[i].dst_off, slot, desc[i].src_len, desc[i].dst_len};
+    bool used;
+    status[i] = lp_exec_stream(g, sm.get(), fr, st[i], blk, pool.get() + l.ents, c, slot, codec, used);
+    taken += used;
+  }
+  return taken;
 }

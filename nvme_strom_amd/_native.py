@@ -270,6 +270,12 @@ _SIGS = {
     "strom_decompress_zstd": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                         C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "strom_zstd_lds_bytes": (C.c_uint32, []),
+    "strom_decompress_zstd_lp": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "strom_zstd_lp_info": (None, [C.c_void_p]),
+    "strom_zstd_lp_last": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "strom_zstd_host_lp": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                     C.c_void_p, C.c_double]),
     "strom_zstd_release": (C.c_int, []),
     "strom_lz4par_host": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                     C.c_void_p]),

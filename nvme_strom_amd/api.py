@@ -505,7 +505,8 @@ def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
                   sequential: bool = False, buffered: bool = False) -> tuple:
     """Storage ceiling for one block size with no engine in the way:
     ``threads`` io_uring rings ``qd`` deep, O_DIRECT reads into host memory
-    at random aligned offsets (or in file order through a shared cursor);
+    at random aligned offsets, or ``sequential``: each ring reads its own
+    disjoint run of the file in order (no cursor shared between rings);
     ``buffered`` reads through the page cache instead.  Returns (IOPS, GiB/s)."""
     iops, gibps = C.c_double(), C.c_double()
     _check(N.lib().strom_raw_read_rate(fd, block, nreq, threads, qd,

@@ -152,7 +152,29 @@ def lz4par_host(codec: int, data: bytes, cap: int, threads=256):
     return n, (out[:n].tobytes() if n >= 0 else b""), stats
 
 
-def zstd_host(codec: int, data: bytes, cap: int, fp: int = 0):
+ZSTD_LP = 2      # zstd_mode: the lane-parallel decoder (zstd.hip "lane-parallel")
+
+
+def zstd_host_lp(codec: int, bufs, caps, ent_factor: float = 0.0):
+    """The lane-parallel zstd decoder's phases on the CPU over several
+    streams at once (walk, entropy groups lane by lane, executions):
+    -> (statuses, outputs, streams the LP path took)."""
+    n = len(bufs)
+    src = np.frombuffer(b"".join(bufs) + b"\0", dtype=np.uint8)
+    d = np.zeros(n, dtype=DESC_DTYPE)
+    so = np.cumsum([0] + [len(b) for b in bufs])[:-1]
+    do = np.cumsum([0] + list(caps))[:-1]
+    d[DESC_DTYPE.names[0]], d[DESC_DTYPE.names[1]] = so, do
+    d[DESC_DTYPE.names[2]], d[DESC_DTYPE.names[3]] = [len(b) for b in bufs], caps
+    out = np.zeros(max(int(sum(caps)), 1), dtype=np.uint8)
+    st = np.zeros(n, dtype=np.int32)
+    taken = N.lib().strom_zstd_host_lp(codec, src.ctypes.data, d.ctypes.data, n, out.ctypes.data,
+                                       st.ctypes.data, float(ent_factor))
+    outs = [out[o:o + s].tobytes() if s >= 0 else b"" for o, s in zip(do, st.tolist())]
+    return st.tolist(), outs, taken
+
+
+def zstd_host(codec: int, data: bytes, cap: int, fp: int = 0, lp: bool = False):
     """The zstd kernel's phases run lane by lane on the CPU
     (csrc/kernels/zstd.hip): -> (status, output bytes).  The reference for
     the GPU decoder; status = decoded bytes or <0 (-1 malformed,
@@ -161,6 +183,9 @@ def zstd_host(codec: int, data: bytes, cap: int, fp: int = 0):
     waves one after another)."""
     src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, dtype=np.uint8)
     out = np.zeros(max(cap, 1), dtype=np.uint8)
+    if lp:
+        st, outs, _ = zstd_host_lp(codec, [bytes(data)], [cap])
+        return st[0], outs[0]
     if fp:
         n = N.lib().strom_zstd_host_fp(codec, src.ctypes.data, len(data), out.ctypes.data, cap, fp)
     else:
@@ -207,9 +232,15 @@ def decompress_async(codec: int, src: torch.Tensor, dst: torch.Tensor, d_desc: t
     literal-heavy streams (a serial parse with few tokens, wide literal
     copies; profiles/r4/dec/lz4par_chars.json).  ``zstd_mode``: the zstd
     decoder for this launch (0 one wave per stream, 1 frame-parallel,
-    None / -1 the library's choice)."""
+    2 lane-parallel, None / -1 the library's choice)."""
     n = d_desc.numel() // DESC_DTYPE.itemsize
     if n == 0:
+        return
+    if zstd_mode == ZSTD_LP and codec in (ZSTD, ARROW_ZSTD):
+        # the entry pool is sized from the decoded capacity (dst)
+        check(lib().strom_decompress_zstd_lp(codec, ptr(src), ptr(dst), ptr(d_desc), n,
+                                             ptr(status), dst.numel(), stream_handle(stream)),
+              "decompress")
         return
     if zstd_mode is not None and codec in (ZSTD, ARROW_ZSTD):
         check(lib().strom_decompress_zstd_mode(codec, ptr(src), ptr(dst), ptr(d_desc), n,

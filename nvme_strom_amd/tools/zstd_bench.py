@@ -94,7 +94,8 @@ def main(argv=None) -> int:
                     help="comma list of lib/zv/<name>.so geometry builds (make zv) timed too")
     ap.add_argument("--modes", default="auto,wave,fp",
                     help="zstd decoder choice per row: auto (by stream count), wave (one wave "
-                         "per stream), fp (frame-parallel: a frame's blocks on a workgroup's waves)")
+                         "per stream), fp (frame-parallel: a frame's blocks on a workgroup's "
+                         "waves), lp (lane-parallel: blocks' entropy stages on lanes)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import torch
@@ -138,7 +139,7 @@ def main(argv=None) -> int:
                 runs = [(vn, vf, md) for vn, vf in (variants if codec == "zstd" else variants[:1])
                         for md in (a.modes.split(",") if codec == "zstd" and vf is None else ["auto"])]
                 for vname, vfn, mode in runs:
-                    lib().strom_zstd_fp_mode({"auto": -1, "wave": 0, "fp": 1}[mode])
+                    lib().strom_zstd_fp_mode({"auto": -1, "wave": 0, "fp": 1, "lp": -1}[mode])
                     times = []
                     ok = True
                     for it in range(a.iters + 1):
@@ -147,7 +148,11 @@ def main(argv=None) -> int:
                         e0 = torch.cuda.Event(enable_timing=True)
                         e1 = torch.cuda.Event(enable_timing=True)
                         e0.record()
-                        if vfn is None:
+                        if vfn is None and mode == "lp":
+                            rc = lib().strom_decompress_zstd_lp(cid, ptr(src), ptr(dst),
+                                                                ptr(d_desc), n, ptr(status),
+                                                                dst.numel(), None)
+                        elif vfn is None:
                             rc = lib().strom_decompress(cid, ptr(src), ptr(dst), ptr(d_desc), n,
                                                         ptr(status), None)
                         else:
@@ -169,6 +174,12 @@ def main(argv=None) -> int:
                     row[pre + "GBps"] = round(n * rawlen / med / 1e9, 2)
                     row[pre + "ms"] = round(med * 1e3, 3)
                     row[pre + "verified"] = ok
+                    if mode == "lp" and vfn is None:
+                        # streams the lane-parallel path decoded itself (not the serial fallback)
+                        cnt = np.zeros(4, np.uint64)
+                        lib().strom_zstd_lp_last(None, cnt.ctypes.data)
+                        row["lp_blocks"], row["lp_streams"] = int(cnt[0]), int(cnt[1])
+                        row["lp_entry_bytes"] = int(cnt[2])
                 if a.prof and codec == "zstd":
                     row["phases"] = prof(cid, n, src, dst, d_desc, status)
                 _log(json.dumps(row))

@@ -445,3 +445,62 @@ def test_zstd_content_checksum(n):
     assert D.zstd_host(D.ZSTD, z, len(d)) == (len(d), d)
     bad = z[:-1] + bytes([z[-1] ^ 0x01])
     assert D.zstd_host(D.ZSTD, bad, len(d))[0] == -5
+
+
+# ------------------------------------------------------- zstd lane-parallel
+@pytest.mark.parametrize("level", [-5, 1, 3, 9, 19])
+def test_zstd_host_lane_parallel_matches_pyarrow(level):
+    """The lane-parallel decoder's phases (walk per stream; entropy stages
+    of LPB blocks per wave, a lane per literal stream / sequence bitstream,
+    literals packed at the output's tail; executions in block order) over
+    every payload at once: each decodes exactly, and on the LP path itself
+    (no serial fallback) — raw / RLE / compressed blocks, treeless
+    literals, repeat-mode tables and symbolic repeat offsets included."""
+    pa = pytest.importorskip("pyarrow")
+    codec = pa.Codec("zstd", compression_level=level)
+    pl = _zstd_payloads()
+    bufs = [codec.compress(d, asbytes=True) for d in pl.values()]
+    st, outs, taken = D.zstd_host_lp(D.ZSTD, bufs, [len(d) for d in pl.values()])
+    for (kind, d), s, o in zip(pl.items(), st, outs):
+        assert s == len(d) and o == d, (kind, s)
+    assert taken == len(bufs)
+
+
+def test_zstd_host_lane_parallel_arrow_fallbacks_and_errors():
+    """Streams the walk refuses (a stored Arrow buffer, several frames, a
+    dictionary) and broken ones go to the serial decoder inside the exec
+    phase: the statuses and outputs equal the serial decoder's, mutants
+    included; an entry pool too small for every stream sends the rest to
+    the serial decoder, still exact."""
+    pa = pytest.importorskip("pyarrow")
+    d = _ints("uniform", 512 << 10, 12)
+    frame = pa.Codec("zstd").compress(d, asbytes=True)
+    a, b = _data("text", 70000, 13), _data("runs", 90000, 14)
+    skip = struct.pack("<II", 0x184D2A53, 5) + b"12345"
+    two = pa.Codec("zstd").compress(a, asbytes=True) + skip + \
+        pa.Codec("zstd", compression_level=7).compress(b, asbytes=True)
+    st, outs, taken = D.zstd_host_lp(D.ARROW_ZSTD, [D.arrow_zstd_buffer(d, frame),
+                                                    b"\xff" * 8 + d[:5000]], [len(d), 5000])
+    assert st == [len(d), 5000] and outs == [d, d[:5000]] and taken == 1
+    st, outs, taken = D.zstd_host_lp(D.ZSTD, [two, frame, frame, frame[: len(frame) // 2]],
+                                     [len(a) + len(b), len(d), len(d) - 1, len(d)])
+    assert st[:3] == [len(a) + len(b), len(d), -2] and outs[:2] == [a + b, d]
+    assert st[3] < 0 and taken == 1
+    # pool exhaustion: some streams fall back, all exact
+    bufs = [frame] * 6
+    st, outs, taken = D.zstd_host_lp(D.ZSTD, bufs, [len(d)] * 6, ent_factor=0.6)
+    assert st == [len(d)] * 6 and all(o == d for o in outs) and 0 < taken < 6
+    # mutants: the LP statuses / outputs are the serial decoder's
+    rng = np.random.default_rng(21)
+    for src, cap in ((frame, len(d)), (pa.Codec("zstd", compression_level=3).compress(
+            _data("text", 200000, 15), asbytes=True), 200000)):
+        muts = []
+        for _ in range(120):
+            m = bytearray(src)
+            for _ in range(int(rng.integers(1, 6))):
+                m[int(rng.integers(4, len(m)))] = int(rng.integers(0, 256))
+            muts.append(bytes(m))
+        st, outs, _ = D.zstd_host_lp(D.ZSTD, muts, [cap] * len(muts))
+        for m, s, o in zip(muts, st, outs):
+            ss, so = D.zstd_host(D.ZSTD, m, cap)
+            assert (s, o) == (ss, so)
