@@ -108,67 +108,253 @@ uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno, uint32_t page_
   return (uint16_t)((x % 65535u) + 1);
 }
 
-// ---- MVCC visibility of heap tuples (HeapTupleSatisfiesMVCC, simplified):
-// hint bits first, then the commit log (pg_xact layout: 2 bits per xid,
-// 0 in progress / 1 committed / 2 aborted / 3 sub-committed), then the
-// snapshot (visible: committed and xid < xmin, or xid < xmax and not in xip).
+// ---- MVCC visibility of heap tuples: HeapTupleSatisfiesMVCC
+// (src/backend/access/heap/heapam_visibility.c), with the inputs it reads
+// from shared memory and the SLRUs supplied by the caller (strom_pg_mvcc):
+// hint bits, pg_xact, pg_subtrans (sub-committed xids follow their parent;
+// XidInMVCCSnapshot maps to the topmost xid when the snapshot's subxip
+// overflowed), pg_multixact (a locker-only xmax deletes nothing; otherwise
+// the update member decides) and the scanning transaction's own xids with
+// its command id.  Transaction ids compare modulo 2^32 (TransactionIdPrecedes).
+// What it cannot decide — a combo command id (backend-local), a log window
+// that does not cover an xid — is reported, never guessed.
 namespace {
-constexpr uint16_t kXminCommitted = 0x0100, kXminInvalid = 0x0200, kXmaxCommitted = 0x0400,
-                   kXmaxInvalid = 0x0800, kXmaxLockOnly = 0x0080;
-struct Snap {
-  uint32_t xmin, xmax;
-  const uint32_t *xip;
-  uint32_t nxip;
-  const uint8_t *clog;
-  uint64_t nclog;      // xids covered by clog
+constexpr uint16_t kXmaxKeyshrLock = 0x0010, kComboCid = 0x0020, kXmaxExclLock = 0x0040,
+                   kXmaxLockOnly = 0x0080, kXminCommitted = 0x0100, kXminInvalid = 0x0200,
+                   kXmaxCommitted = 0x0400, kXmaxInvalid = 0x0800, kXmaxIsMulti = 0x1000;
+constexpr uint16_t kLockMask = kXmaxKeyshrLock | kXmaxExclLock;
+
+struct Vis {
+  const strom_pg_mvcc &m;
+  bool undecided = false;
 };
-int xid_status(const Snap &s, uint32_t xid) {
-  if (xid < 3) return xid == 0 ? 2 : 1;            // invalid / bootstrap, frozen
-  if (!s.clog || xid >= s.nclog) return 0;           // unknown: in progress
-  return (s.clog[xid >> 2] >> ((xid & 3) * 2)) & 3;
+
+bool xid_normal(uint32_t x) { return x >= 3; }
+bool xid_precedes(uint32_t a, uint32_t b) {       // TransactionIdPrecedes
+  if (!xid_normal(a) || !xid_normal(b)) return a < b;
+  return (int32_t)(a - b) < 0;
 }
-bool in_snapshot(const Snap &s, uint32_t xid) {
-  if (xid < 3 || xid < s.xmin) return true;
-  if (xid >= s.xmax) return false;
-  for (uint32_t i = 0; i < s.nxip; ++i)
-    if (s.xip[i] == xid) return false;
+
+int clog_status(Vis &v, uint32_t xid) {          // -1: outside the window
+  const uint64_t k = (uint32_t)(xid - v.m.clog_base);
+  if (!v.m.clog || k >= v.m.clog_n) return -1;
+  return (v.m.clog[k >> 2] >> ((k & 3) * 2)) & 3;
+}
+
+bool subtrans_parent(Vis &v, uint32_t xid, uint32_t &parent) {
+  const uint32_t k = xid - v.m.subtrans_base;
+  if (!v.m.subtrans || k >= v.m.subtrans_n) return false;
+  parent = v.m.subtrans[k];
   return true;
 }
-bool mvcc_visible(const Snap &s, const uint8_t *tup) {
+
+bool did_commit(Vis &v, uint32_t xid) {           // TransactionIdDidCommit
+  for (int depth = 0; depth < 1024; ++depth) {
+    if (!xid_normal(xid)) return xid == 1 || xid == 2;   // bootstrap / frozen; invalid never
+    const int st = clog_status(v, xid);
+    if (st < 0) {
+      v.undecided = true;
+      return false;
+    }
+    if (st != 3) return st == 1;
+    // sub-committed: its parent decides; one older than every snapshot's
+    // xmin whose parent never committed has crashed
+    if (xid_precedes(xid, v.m.xmin)) return false;
+    uint32_t p;
+    if (!subtrans_parent(v, xid, p)) {
+      v.undecided = true;
+      return false;
+    }
+    if (p == 0) return false;
+    xid = p;
+  }
+  v.undecided = true;
+  return false;
+}
+
+bool in_list(const uint32_t *a, uint32_t n, uint32_t x) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (a[i] == x) return true;
+  return false;
+}
+
+bool is_current(Vis &v, uint32_t xid) {           // TransactionIdIsCurrentTransactionId
+  return xid_normal(xid) && in_list(v.m.curxids, v.m.ncurxids, xid);
+}
+
+bool xid_in_snapshot(Vis &v, uint32_t xid) {     // XidInMVCCSnapshot: still running for us
+  if (xid_precedes(xid, v.m.xmin)) return false;
+  if (!xid_precedes(xid, v.m.xmax)) return true;
+  if (!v.m.suboverflowed) {
+    if (in_list(v.m.subxip, v.m.nsubxip, xid)) return true;
+  } else {
+    // SubTransGetTopmostTransaction
+    uint32_t top = xid, p = xid;
+    for (int depth = 0; depth < 1024 && p; ++depth) {
+      top = p;
+      if (xid_precedes(p, v.m.xmin)) break;
+      uint32_t q;
+      if (!subtrans_parent(v, p, q)) {
+        v.undecided = true;
+        return true;
+      }
+      if (q && !xid_precedes(q, p)) {                 // a corrupt entry
+        v.undecided = true;
+        return true;
+      }
+      p = q;
+    }
+    xid = top;
+    if (xid_precedes(xid, v.m.xmin)) return false;
+  }
+  return in_list(v.m.xip, v.m.nxip, xid);
+}
+
+bool locked_only(uint16_t mask) {                 // HEAP_XMAX_IS_LOCKED_ONLY
+  return (mask & kXmaxLockOnly) || (mask & (kXmaxIsMulti | kLockMask)) == kXmaxExclLock;
+}
+
+// MultiXactIdGetUpdateXid: the member whose status is an update (at most
+// one); 0 when every member only locks
+uint32_t multi_update_xid(Vis &v, uint32_t multi) {
+  const uint32_t k = multi - v.m.mx_base;
+  if (!v.m.mx_offsets || k >= v.m.mx_n || !v.m.mx_members) {
+    v.undecided = true;
+    return 0;
+  }
+  const uint32_t off = v.m.mx_offsets[k], n = v.m.mx_offsets[k + 1] - off;
+  if (n > 65536) {
+    v.undecided = true;
+    return 0;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t mem = (uint32_t)(off + i - v.m.mxm_base);
+    if (mem >= v.m.mxm_n) {
+      v.undecided = true;
+      return 0;
+    }
+    const uint64_t group = mem / 4, page = group / 409, within = mem % 4;
+    const uint8_t *g = v.m.mx_members + page * 8192 + (group % 409) * 20;
+    const uint32_t status = g[within];
+    if (status > 3) return rd32(g + 4 + 4 * within);  // NoKeyUpdate / Update
+  }
+  return 0;
+}
+
+// a command id of the scanning transaction's own tuple; false: a combo
+// command id (its mapping lives in that backend only)
+bool own_cid(Vis &v, uint16_t mask, const uint8_t *tup, uint32_t &cid) {
+  if (mask & kComboCid) {
+    v.undecided = true;
+    return false;
+  }
+  cid = rd32(tup + 8);
+  return true;
+}
+
+int tuple_visible(Vis &v, const uint8_t *tup) {
   const uint32_t xmin = rd32(tup), xmax = rd32(tup + 4);
   const uint16_t mask = (uint16_t)(tup[20] | (tup[21] << 8));
-  const bool frozen = (mask & (kXminCommitted | kXminInvalid)) == (kXminCommitted | kXminInvalid);
-  if (!frozen) {
-    if (mask & kXminInvalid) return false;
-    const bool committed = (mask & kXminCommitted) || xid_status(s, xmin) == 1;
-    if (!committed || !in_snapshot(s, xmin)) return false;
+#define UND(r) (v.undecided ? -1 : (r))
+  if (!(mask & kXminCommitted)) {
+    if (mask & kXminInvalid) return 0;
+    if (is_current(v, xmin)) {
+      uint32_t cid;
+      if (!own_cid(v, mask, tup, cid)) return -1;
+      if (cid >= v.m.curcid) return 0;             // inserted after the scan started
+      if (mask & kXmaxInvalid) return 1;
+      if (locked_only(mask)) return 1;
+      if (mask & kXmaxIsMulti) {
+        const uint32_t up = multi_update_xid(v, xmax);
+        if (v.undecided) return -1;
+        if (!is_current(v, up)) return 1;          // the updating subxact aborted
+        return cid >= v.m.curcid ? 1 : 0;          // t_cid is the cmax here (no combo)
+      }
+      if (!is_current(v, xmax)) return 1;          // the deleting subxact aborted
+      return cid >= v.m.curcid ? 1 : 0;
+    }
+    if (xid_in_snapshot(v, xmin)) return UND(0);
+    if (!did_commit(v, xmin)) return UND(0);       // aborted or crashed
+  } else if ((mask & (kXminCommitted | kXminInvalid)) != (kXminCommitted | kXminInvalid) &&
+             xid_in_snapshot(v, xmin)) {
+    return UND(0);                                 // committed, but not for this snapshot
   }
-  if ((mask & kXmaxInvalid) || xmax == 0 || (mask & kXmaxLockOnly)) return true;
-  const bool deleted = (mask & kXmaxCommitted) || xid_status(s, xmax) == 1;
-  return !(deleted && in_snapshot(s, xmax));
+  if (v.undecided) return -1;
+  // the inserting transaction is visible; now the deleter
+  if (mask & kXmaxInvalid) return 1;
+  if (locked_only(mask)) return 1;
+  if (mask & kXmaxIsMulti) {
+    const uint32_t up = multi_update_xid(v, xmax);
+    if (v.undecided) return -1;
+    if (!up) return 1;
+    if (is_current(v, up)) {
+      uint32_t cid;
+      if (!own_cid(v, mask, tup, cid)) return -1;
+      return cid >= v.m.curcid ? 1 : 0;
+    }
+    if (xid_in_snapshot(v, up)) return UND(1);
+    return UND(did_commit(v, up) ? 0 : 1);
+  }
+  if (!(mask & kXmaxCommitted)) {
+    if (is_current(v, xmax)) {
+      uint32_t cid;
+      if (!own_cid(v, mask, tup, cid)) return -1;
+      return cid >= v.m.curcid ? 1 : 0;
+    }
+    if (xid_in_snapshot(v, xmax)) return UND(1);
+    return UND(did_commit(v, xmax) ? 0 : 1);
+  }
+  return UND(xid_in_snapshot(v, xmax) ? 1 : 0);
+#undef UND
 }
 }  // namespace
 
-long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
-                             const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
-                             uint64_t clog_xids) {
+int strom_pg_tuple_visible(const void *tuple_header, const strom_pg_mvcc *m) {
+  Vis v{*m};
+  return tuple_visible(v, (const uint8_t *)tuple_header);
+}
+
+long strom_pg_apply_mvcc(void *page, uint32_t page_sz, const strom_pg_mvcc *m, uint16_t *recheck,
+                         uint32_t cap, uint32_t *nrecheck) {
   uint8_t *p = (uint8_t *)page;
+  if (nrecheck) *nrecheck = 0;
   const uint16_t lower = (uint16_t)(p[12] | (p[13] << 8)), flags = (uint16_t)(p[10] | (p[11] << 8));
   if (lower < 24 || lower > page_sz) return -22;
   if (flags & 0x0004) return 0;                      // PD_ALL_VISIBLE: nothing to check
-  const Snap s{snap_xmin, snap_xmax, xip, nxip, clog, clog_xids};
   long removed = 0;
+  uint32_t nr = 0;
   for (uint32_t i = 0; i < (uint32_t)(lower - 24) / 4; ++i) {
     uint8_t *lpp = p + 24 + 4 * i;
     uint32_t lp = rd32(lpp);
     const uint32_t off = lp & 0x7fff, fl = (lp >> 15) & 3, len = lp >> 17;
     if (fl != 1 || len < 23 || off < 24 || off + len > page_sz) continue;
-    if (mvcc_visible(s, p + off)) continue;
+    Vis v{*m};
+    const int r = tuple_visible(v, p + off);
+    if (r > 0) continue;
+    if (r < 0) {                                     // kept for a recheck
+      if (recheck && nr < cap) recheck[nr] = (uint16_t)(i + 1);
+      ++nr;
+      continue;
+    }
     lp &= ~(3u << 15);                               // LP_UNUSED, as the reference marks them
     memcpy(lpp, &lp, 4);
     ++removed;
   }
+  if (nrecheck) *nrecheck = nr;
   return removed;
+}
+
+long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
+                             const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
+                             uint64_t clog_xids) {
+  strom_pg_mvcc m{};
+  m.xmin = snap_xmin;
+  m.xmax = snap_xmax;
+  m.xip = xip;
+  m.nxip = nxip;
+  m.clog = clog;
+  m.clog_n = clog_xids;
+  return strom_pg_apply_mvcc(page, page_sz, &m, nullptr, 0, nullptr);
 }
 
 uint64_t strom_atomic_fetch_add_u64(uint64_t *addr, uint64_t v) {

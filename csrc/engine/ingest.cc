@@ -95,10 +95,37 @@ bool Ingest::init() {
   int prio_least = 0, prio_greatest = 0;
   if (config().ingest_prio && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess)
     prio_greatest = 0;
-  if (hipMalloc(&next_, 64) != hipSuccess ||
-      hipStreamCreateWithPriority((hipStream_t *)&stream_, hipStreamNonBlocking,
-                                  config().ingest_prio ? prio_greatest : 0) != hipSuccess ||
-      hipEventCreateWithFlags((hipEvent_t *)&end_ev_, hipEventDisableTiming) != hipSuccess) {
+  if (hipMalloc(&next_, 64) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  // The grid needs a hardware queue of its own: a kernel queued behind it
+  // on a shared queue waits until the grid goes idle, and a grid relaunch
+  // waits behind that kernel (round 5 trace: Arrow ZSTD decodes on the
+  // grid's queue ran only between reads, profiles/r5/zstd_arrow).  HIP
+  // hands normal-priority streams GPU_MAX_HW_QUEUES (4) queues round-robin,
+  // so a process with more streams aliases them; a CU-masked stream always
+  // gets a new queue (tools/probe/hwq_probe.py), so the grid's stream is one
+  // with every CU in its mask.  ingest_prio=1: a greatest-priority stream
+  // instead (the first one of its priority also gets its own queue).
+  bool made = false;
+  if (!config().ingest_prio) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_) == hipSuccess &&
+        cus > 0 && cus <= 1024) {
+      uint32_t mask[32] = {0};
+      for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+      made = hipExtStreamCreateWithCUMask((hipStream_t *)&stream_, (uint32_t)((cus + 31) / 32),
+                                          mask) == hipSuccess;
+      if (!made) (void)hipGetLastError();
+    }
+  }
+  if (!made && hipStreamCreateWithPriority((hipStream_t *)&stream_, hipStreamNonBlocking,
+                                           config().ingest_prio ? prio_greatest : 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (hipEventCreateWithFlags((hipEvent_t *)&end_ev_, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }

@@ -292,6 +292,44 @@ uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
 long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
                              const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
                              uint64_t clog_xids);
+/* The full HeapTupleSatisfiesMVCC inputs (heapam_visibility.c): snapshot
+ * (xmin, xmax, xip, subxip / suboverflowed), the scanning transaction's own
+ * xids and command id, and windows of the SLRU logs — pg_xact (2 bits per
+ * xid from clog_base), pg_subtrans (parent xid per xid from subtrans_base),
+ * pg_multixact offsets (member offset per multixact from mx_base, n + 1
+ * entries: the last is the next offset) and members (PostgreSQL's page
+ * layout: 409 groups of 4 flag bytes + 4 xids per 8 KiB page, from member
+ * offset mxm_base).  Transaction ids compare modulo 2^32. */
+struct strom_pg_mvcc {
+	uint32_t xmin, xmax;
+	const uint32_t *xip;
+	uint32_t nxip;
+	uint32_t suboverflowed;
+	const uint32_t *subxip;
+	uint32_t nsubxip;
+	uint32_t curcid;
+	const uint32_t *curxids;  /* the scanning transaction: top xid + its subxacts */
+	uint32_t ncurxids;
+	uint32_t clog_base;
+	const uint8_t *clog;
+	uint64_t clog_n;
+	const uint32_t *subtrans;
+	uint32_t subtrans_base, subtrans_n;
+	const uint32_t *mx_offsets;
+	uint32_t mx_base, mx_n;
+	const uint8_t *mx_members;
+	uint64_t mxm_n;
+	uint32_t mxm_base, pad;
+};
+/* The same in-place marking with the full rules; tuples the inputs cannot
+ * decide (a combo command id of the scanning transaction, an xid / multixact
+ * outside the log windows) are kept and their line numbers (1-based)
+ * written to recheck[] (up to cap), *nrecheck = their count.  Returns the
+ * tuples removed, or -22 for a page that is not a heap page. */
+long strom_pg_apply_mvcc(void *page, uint32_t page_sz, const struct strom_pg_mvcc *m,
+                         uint16_t *recheck, uint32_t cap, uint32_t *nrecheck);
+/* one tuple header: 1 visible, 0 not, -1 undecided */
+int strom_pg_tuple_visible(const void *tuple_header, const struct strom_pg_mvcc *m);
 /* fetch-and-add on shared memory (cross-process scan cursors) */
 uint64_t strom_atomic_fetch_add_u64(uint64_t *addr, uint64_t v);
 int strom_atomic_cas_u64(uint64_t *addr, uint64_t expect, uint64_t desired);

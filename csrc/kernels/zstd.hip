@@ -2249,6 +2249,19 @@ static_assert(LP_LWIN == 4 * NT && LP_SWIN % (4 * NT) == 0, "LP window loads");
 // bits come from code_base()
 HD uint32_t lp_ent(uint32_t code, uint32_t nb, uint32_t next) { return code | nb << 8 | next << 16; }
 
+// The LP phases keep their input / output pointers in LDS (per block), so
+// the compiler no longer sees that they are global: accesses would become
+// FLAT, and a flat op counts in lgkmcnt too — every LDS table lookup would
+// then wait for the previous literal / entry store.  The hot loops go
+// through these global-address-space views instead.
+#ifdef __HIP_DEVICE_COMPILE__
+#define ZG __attribute__((address_space(1)))
+#else
+#define ZG
+#endif
+template <class T>
+HD ZG T *zg(T *p) { return (ZG T *)p; }
+
 HD bool fse_build4(uint32_t *tab, const int16_t *norm, uint32_t nsym, uint32_t al,
                    uint16_t *snext) {
   const uint32_t size = 1u << al, mask = size - 1;
@@ -2542,9 +2555,10 @@ HD void lp_begin(LpB &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const u
 // (1) literal windows of every stream with symbols left: one dword per lane
 // each, aligned in the input (bytes outside it read as 0)
 HD uint32_t lp_ld32(const uint8_t *in, uint32_t len, uint32_t p) {
-  if (p < len && len - p >= 4) return *(const uint32_t *)(in + p);
+  const ZG uint8_t *g = zg(in);
+  if (p < len && len - p >= 4) return *(const ZG uint32_t *)(g + p);
   uint32_t v = 0;
-  for (uint32_t j = 0; j < 4; ++j) v |= (p + j < len ? (uint32_t)in[p + j] : 0u) << (8 * j);
+  for (uint32_t j = 0; j < 4; ++j) v |= (p + j < len ? (uint32_t)g[p + j] : 0u) << (8 * j);
   return v;
 }
 
@@ -2555,23 +2569,79 @@ HD uint32_t lp_align_lo(const uint8_t *in, uint32_t lo) {
   return lo - (uint32_t)(((uintptr_t)in + lo) & 3);
 }
 
-HD void lp_lit_windows(LpWave &W, uint32_t t) {
-  for (uint32_t w = 0; w < 4 * LPB; ++w) {
-    LpB &s = W.b[w / 4];
-    const uint32_t j = w % 4;
-    if (!(s.lact >> j & 1)) continue;
-    ((uint32_t *)s.lwin[j])[t] = lp_ld32(s.in, s.len, s.lwlo[j] + 4 * t);
+// Every window dword of the round is LOADED before any is stored: one
+// load per window with its LDS store behind it serialized the round on
+// global-memory latency (a wait per window: 32 / 24 round trips per round,
+// most of the entropy launch — r5 trace).  Inactive windows load from
+// `safe` (any valid global dword); dwords that reach past either end of
+// the input take the guarded byte path afterwards (a stream's first /
+// last window only).
+template <uint32_t NWIN, uint32_t PER, class F>
+HD void lp_windows(const uint32_t *safe, uint32_t t, F win) {
+  uint32_t v[NWIN * PER];
+  uint64_t slow = 0;
+  static_assert(NWIN * PER <= 64, "window dwords per lane");
+#pragma unroll
+  for (uint32_t w = 0; w < NWIN; ++w) {
+    const uint8_t *in;
+    uint32_t len, lo;
+    uint8_t *dst;
+    const bool on = win(w, in, len, lo, dst);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t p = lo + 4 * (t + k * NT);
+      const bool fast = on && p < len && len - p >= 4;
+      const ZG uint32_t *a = fast ? (const ZG uint32_t *)(zg(in) + p) : zg(safe);
+      v[w * PER + k] = *a;
+      if (on && !fast) slow |= 1ull << (w * PER + k);
+    }
+  }
+  if (slow) {
+#pragma unroll
+    for (uint32_t w = 0; w < NWIN; ++w) {
+      const uint8_t *in;
+      uint32_t len, lo;
+      uint8_t *dst;
+      win(w, in, len, lo, dst);
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (slow >> (w * PER + k) & 1) v[w * PER + k] = lp_ld32(in, len, lo + 4 * (t + k * NT));
+    }
+  }
+#pragma unroll
+  for (uint32_t w = 0; w < NWIN; ++w) {
+    const uint8_t *in;
+    uint32_t len, lo;
+    uint8_t *dst;
+    if (!win(w, in, len, lo, dst)) continue;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) ((uint32_t *)dst)[t + k * NT] = v[w * PER + k];
   }
 }
 
-HD void lp_seq_windows(LpWave &W, uint32_t t) {
-  for (uint32_t b = 0; b < LPB; ++b) {
-    LpB &s = W.b[b];
-    if (!s.act || s.err || s.seq_done >= s.nseq) continue;
-#pragma unroll
-    for (uint32_t k = 0; k < LP_SWIN / (4 * NT); ++k)
-      ((uint32_t *)s.swin)[t + k * NT] = lp_ld32(s.in, s.len, s.swlo + 4 * (t + k * NT));
-  }
+HD void lp_lit_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
+  lp_windows<4 * LPB, LP_LWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in, uint32_t &len,
+                                                       uint32_t &lo, uint8_t *&dst) {
+    LpB &s = W.b[w / 4];
+    const uint32_t j = w % 4;
+    in = s.in;
+    len = s.len;
+    lo = s.lwlo[j];
+    dst = s.lwin[j];
+    return (s.lact >> j & 1) != 0;
+  });
+}
+
+HD void lp_seq_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
+  lp_windows<LPB, LP_SWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in, uint32_t &len,
+                                                   uint32_t &lo, uint8_t *&dst) {
+    LpB &s = W.b[w];
+    in = s.in;
+    len = s.len;
+    lo = s.swlo;
+    dst = s.swin;
+    return s.act && !s.err && s.seq_done < s.nseq;
+  });
 }
 
 // (1) up to LP_LSYM symbols of literal stream j, straight into the block's
@@ -2581,7 +2651,7 @@ HD void lp_lit_chunk(LpB &s, uint32_t j) {
   BR b = s.lbr[j];
   const Win w{(uint32_t)offsetof(LpB, lwin) + j * LP_LWIN, s.lwlo[j], LP_LWIN};
   const uint32_t n = left < LP_LSYM ? left : LP_LSYM, mb = s.hbits;
-  uint8_t *dst = s.litp + s.lout[j];
+  ZG uint8_t *dst = zg(s.litp) + s.lout[j];
   const uint32_t nf = n & ~3u;
   for (uint32_t k = 0; k < nf; k += 4) {
     br_need(b, s, w, 4 * mb);
@@ -2593,9 +2663,9 @@ HD void lp_lit_chunk(LpB &s, uint32_t j) {
       b.nbits -= (int32_t)s.hlen[x];
       word |= (uint32_t)s.hsym[x] << (8 * g);
     }
-    uint8_t *o = dst + k;
+    ZG uint8_t *o = dst + k;
     if (((uintptr_t)o & 3) == 0) {
-      *(uint32_t *)o = word;
+      *(ZG uint32_t *)o = word;
     } else {
       o[0] = (uint8_t)word;
       o[1] = (uint8_t)(word >> 8);
@@ -2686,7 +2756,7 @@ HD void lp_seq_chunk(LpB &s) {
   uint32_t r0 = s.rep[0], r1 = s.rep[1], r2 = s.rep[2];
   uint32_t n = s.nent, out = s.out, lit = s.lit;
   bool bad = false;
-  Ent *ent = s.ent;
+  ZG Ent *ent = zg(s.ent);
   for (uint32_t i = 0; i < m; ++i) {
     const bool more = i + 1 < left;           // the block's last sequence reads no state bits
     const uint32_t eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
@@ -2723,12 +2793,11 @@ HD void lp_seq_chunk(LpB &s) {
       r1 = r0;
       r0 = off;
     }
-    Ent e;
+    ZG Ent &e = ent[n++];
     e.ll = ll;
     e.off = off;
     e.lst = lit;
     e.ost = out;
-    ent[n++] = e;
     lit += ll;
     out += ll + ml;
   }
@@ -2813,7 +2882,7 @@ HD void lp_entropy_group(TM &tm, LpWave &W, LpBlock *blk, uint32_t k0, uint32_t 
       if (j < 4 && (s.lact >> j & 1)) s.lwlo[j] = lp_align_lo(s.in, win_lo(s.lbr[j], LP_LWIN - 4));
     });
     tm.sync();
-    tm.each([&](uint32_t t) { lp_lit_windows(W, t); });
+    tm.each([&](uint32_t t) { lp_lit_windows(W, t, (const uint32_t *)desc); });
     tm.sync();
     tm.each([&](uint32_t t) {
       LpB &s = W.b[t / LPL];
@@ -2838,7 +2907,7 @@ HD void lp_entropy_group(TM &tm, LpWave &W, LpBlock *blk, uint32_t k0, uint32_t 
         s.swlo = lp_align_lo(s.in, win_lo(s.sbr, LP_SWIN - 4));
     });
     tm.sync();
-    tm.each([&](uint32_t t) { lp_seq_windows(W, t); });
+    tm.each([&](uint32_t t) { lp_seq_windows(W, t, (const uint32_t *)desc); });
     tm.sync();
     tm.each([&](uint32_t t) {
       LpB &s = W.b[t / LPL];
@@ -2853,180 +2922,221 @@ HD void lp_entropy_group(TM &tm, LpWave &W, LpBlock *blk, uint32_t k0, uint32_t 
   tm.sync();
 }
 
-// (exec) a block of an LP stream: exec_fp's batches with the gathers split
-// from the stores (the literals sit in the output buffer)
-HD void gx_gather(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn, uint32_t nb) {
-  for (uint32_t k = 0; k < EPT; ++k) {
-    const uint32_t e = k * tn + t;
+// (exec) One workgroup of LPX_T lanes per stream, blocks in order.  Its
+// own LDS (25 KB, six workgroups per CU; the Smem-based exec_fp needs four
+// Smem): a chunk of up to LPX_SEQ entries at a time, its output in batches
+// of LPX_OB bytes — a source pointer per byte (literal index / stored
+// output / earlier byte of the batch), pointer doubling, then every byte
+// GATHERED before any is STORED: the block's literals sit in the output
+// buffer's tail, never below the position they are copied to, but a batch
+// may write where a later byte of the same batch reads.
+constexpr uint32_t LPX_T = 256;
+constexpr uint32_t LPX_EPT = 16;
+constexpr uint32_t LPX_OB = LPX_T * LPX_EPT;    // output bytes per batch
+constexpr uint32_t LPX_SEQ = 512;               // entries per chunk
+HD constexpr uint32_t PX(uint32_t e) { return e + e / LPX_EPT; }   // bank skew, as PI
+
+struct LpX {
+  uint32_t ptr[PX(LPX_OB)];
+  uint32_t sll[LPX_SEQ], soff[LPX_SEQ], lst[LPX_SEQ], ost[LPX_SEQ + 1];
+  // frame: output position, repeat offsets; block: its record's fields
+  uint32_t op, rep[3];
+  uint32_t brep[3], btype, bstart, bsize, nseq, lit_kind, lit_n, lit_base, lit_rle;
+  uint32_t m, end;                              // the chunk: entries, output bytes
+  int32_t err;
+};
+
+HD uint32_t lpx_entry_of(const LpX &x, uint32_t pos) {   // ost strictly increases
+  uint32_t lo = 0, hi = x.m;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (x.ost[mid] <= pos) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+HD void lpx_fill(LpX &x, uint32_t t, uint32_t b0, uint32_t nb) {
+  const uint32_t abs0 = x.op, e0 = t * LPX_EPT;
+  if (e0 >= nb) return;
+  uint32_t i = lpx_entry_of(x, b0 + e0);
+  uint32_t start = x.ost[i], next = x.ost[i + 1];
+  uint32_t ll = x.sll[i], off = x.soff[i], lst = x.lst[i];
+  for (uint32_t k = 0; k < LPX_EPT; ++k) {
+    const uint32_t e = e0 + k;
     if (e >= nb) break;
-    const uint32_t v = gptr(sm, e), x = v & ~kTag;
-    uint8_t y;
+    const uint32_t pos = b0 + e;
+    while (pos >= next) {
+      ++i;
+      start = next;
+      next = x.ost[i + 1];
+      ll = x.sll[i];
+      off = x.soff[i];
+      lst = x.lst[i];
+    }
+    const uint32_t r = pos - start;
+    uint32_t v;
+    if (r < ll) {
+      v = kLit | (lst + r);
+    } else {
+      const uint32_t src = abs0 + pos - off;
+      v = src < abs0 + b0 ? (kHist | src) : src - abs0 - b0;
+    }
+    x.ptr[PX(e)] = v;
+  }
+}
+
+HD bool lpx_double(LpX &x, uint32_t t, uint32_t nb) {
+  bool more = false;
+  for (uint32_t k = 0; k < LPX_EPT; ++k) {
+    const uint32_t e = k * LPX_T + t;
+    if (e >= nb) break;
+    const uint32_t v = x.ptr[PX(e)];
+    if (v & kTag) continue;
+    const uint32_t y = x.ptr[PX(v)];
+    x.ptr[PX(e)] = y;
+    more |= !(y & kTag);
+  }
+  return more;
+}
+
+HD void lpx_gather(LpX &x, const Ctx &c, const uint8_t *lit, uint32_t t, uint32_t nb) {
+  for (uint32_t k = 0; k < LPX_EPT; ++k) {
+    const uint32_t e = k * LPX_T + t;
+    if (e >= nb) break;
+    const uint32_t v = x.ptr[PX(e)], a = v & ~kTag;
+    uint32_t y;
     if (v & kLit)
-      y = s.lit_kind == kLitInput ? c.in[s.lit_base + x]
-        : s.lit_kind == kLitRle ? (uint8_t)s.lit_rle : c.lit[x];
+      y = x.lit_kind == kLitInput ? c.in[x.lit_base + a] : x.lit_kind == kLitRle ? x.lit_rle : lit[a];
     else
-      y = c.out[x];
-    gptr(sm, e) = y;
+      y = c.out[a];
+    x.ptr[PX(e)] = y;
   }
 }
 
-HD void gx_store(const Smem &s, Smem *sm, const Ctx &c, uint32_t t, uint32_t tn, uint32_t b0,
-                 uint32_t nb) {
-  uint8_t *o = c.out + s.op + b0;
-  for (uint32_t k = 0; k < EPT; ++k) {
-    const uint32_t e = k * tn + t;
+HD void lpx_store(const LpX &x, const Ctx &c, uint32_t t, uint32_t b0, uint32_t nb) {
+  uint8_t *o = c.out + x.op + b0;
+  for (uint32_t k = 0; k < LPX_EPT; ++k) {
+    const uint32_t e = k * LPX_T + t;
     if (e >= nb) break;
-    o[e] = (uint8_t)gptr(sm, e);
+    o[e] = (uint8_t)x.ptr[PX(e)];
   }
 }
 
+// one block of the stream at x.op (the frame state advances)
 template <class TM>
-HD void exec_lp(TM &tm, Smem *sm, FpFrame &s0, const Ctx &c, const Ent *ent, uint32_t nent,
-                uint32_t bout) {
-  Smem &s = sm[0];
-  const uint32_t tn = tm.size(), gob = tn * EPT;
+HD void lpx_block(TM &tm, LpX &x, const Ctx &c, const LpBlock &b, const Ent *ent) {
   tm.one([&] {
-    s.op = s0.op;
-    if ((uint64_t)s0.op + bout > c.cap) s.err = kErrOverflow;
+    x.btype = b.btype;
+    x.bstart = b.bstart;
+    x.bsize = b.bsize;
+    x.nseq = b.nseq;
+    x.lit_kind = b.lit_kind;
+    x.lit_n = b.lit_n;
+    x.lit_base = b.lit_base;
+    x.lit_rle = b.lit_rle;
+    for (uint32_t j = 0; j < 3; ++j) x.brep[j] = b.rep[j];
+    if ((uint64_t)x.op + b.bout > c.cap) x.err = kErrOverflow;
   });
   tm.sync();
-  if (s.err) return;
-  if (s.btype != kComp) {
+  if (x.err) return;
+  const uint32_t tn = tm.size(), nent = b.nent, bout = b.bout;
+  if (x.btype != kComp) {
     tm.each([&](uint32_t t) {
-      uint8_t *o = c.out + s.op;
-      if (s.btype == kRle) {
-        const uint8_t v = (uint8_t)gbyte(c, s.bstart);
-        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = v;
+      uint8_t *o = c.out + x.op;
+      if (x.btype == kRle) {
+        const uint8_t v = (uint8_t)gbyte(c, x.bstart);
+        for (uint32_t i = t; i < x.bsize; i += tn) o[i] = v;
       } else {
-        const uint8_t *in = c.in + s.bstart;
-        for (uint32_t i = t; i < s.bsize; i += tn) o[i] = in[i];
+        const uint8_t *in = c.in + x.bstart;
+        for (uint32_t i = t; i < x.bsize; i += tn) o[i] = in[i];
       }
     });
   } else {
-    const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
-    const uint32_t fpos = s0.op - s0.fstart;
-    const uint32_t gseq = tn / NT * SEQN;
-    for (uint32_t i0 = 0; i0 < nent; i0 += gseq) {
-      const uint32_t m = nent - i0 < gseq ? nent - i0 : gseq;
+    const uint8_t *lit = c.out + b.lit_off;
+    const uint32_t fpos = x.op;                  // one frame per LP stream: it starts at 0
+    for (uint32_t i0 = 0; i0 < nent; i0 += LPX_SEQ) {
+      const uint32_t m = nent - i0 < LPX_SEQ ? nent - i0 : LPX_SEQ;
       const uint32_t base = ent[i0].ost;
       const uint32_t end = (i0 + m < nent ? ent[i0 + m].ost : bout) - base;
       tm.each([&](uint32_t t) {
+        const uint32_t rin[3] = {x.rep[0], x.rep[1], x.rep[2]};
         bool bad = false;
         for (uint32_t i = t; i < m; i += tn) {
           const Ent e = ent[i0 + i];
           const uint32_t off = sym_resolve(e.off, rin);
+          // a match reaches back at most to the frame start; the trailing
+          // literals entry has no match
           const bool has_match = (i0 + i + 1 < nent ? ent[i0 + i + 1].ost : bout) - e.ost > e.ll;
           bad |= has_match && off - 1 >= fpos + e.ost + e.ll;
-          Smem &q = sm[i / SEQN];
-          q.sll[i % SEQN] = e.ll;
-          q.soff[i % SEQN] = off;
-          q.lst[i % SEQN] = e.lst;
-          q.ost[i % SEQN] = e.ost - base;
+          x.sll[i] = e.ll;
+          x.soff[i] = off;
+          x.lst[i] = e.lst;
+          x.ost[i] = e.ost - base;
         }
-        if (bad) s.err = ZF(kErrDistance);
+        if (t == 0) {
+          x.ost[m] = end;
+          x.m = m;
+        }
+        if (bad) x.err = ZF(kErrDistance);
       });
       tm.sync();
-      if (s.err) return;
-      const GChunk gc{sm, m, end};
-      for (uint32_t b0 = 0; b0 < end; b0 += gob) {
-        const uint32_t nb = end - b0 < gob ? end - b0 : gob;
-        tm.each([&](uint32_t t) { gx_fill(s, gc, t, b0, nb); });
+      if (x.err) return;
+      for (uint32_t b0 = 0; b0 < end; b0 += LPX_OB) {
+        const uint32_t nb = end - b0 < LPX_OB ? end - b0 : LPX_OB;
+        tm.each([&](uint32_t t) { lpx_fill(x, t, b0, nb); });
         tm.sync();
-        while (tm.any([&](uint32_t t) { return gx_double(sm, t, tn, nb); })) {
+        while (tm.any([&](uint32_t t) { return lpx_double(x, t, nb); })) {
         }
-        tm.each([&](uint32_t t) { gx_gather(s, sm, c, t, tn, nb); });
+        tm.each([&](uint32_t t) { lpx_gather(x, c, lit, t, nb); });
         tm.sync();
-        tm.each([&](uint32_t t) { gx_store(s, sm, c, t, tn, b0, nb); });
+        tm.each([&](uint32_t t) { lpx_store(x, c, t, b0, nb); });
         tm.fence();
         tm.sync();
       }
-      tm.one([&] { s.op += end; });
+      tm.one([&] { x.op += end; });
       tm.sync();
     }
   }
   tm.fence();
   tm.sync();
   tm.one([&] {
-    s0.op += bout;
-    if (s.btype == kComp && s.nseq) {
-      const uint32_t rin[3] = {s0.rep[0], s0.rep[1], s0.rep[2]};
-      s0.rep[0] = sym_resolve(s.rep[0], rin);
-      s0.rep[1] = sym_resolve(s.rep[1], rin);
-      s0.rep[2] = sym_resolve(s.rep[2], rin);
+    if (x.btype != kComp) x.op += x.bsize;
+    if (x.btype == kComp && x.nseq) {
+      const uint32_t rin[3] = {x.rep[0], x.rep[1], x.rep[2]};
+      for (uint32_t j = 0; j < 3; ++j) x.rep[j] = sym_resolve(x.brep[j], rin);
     }
   });
   tm.sync();
 }
 
-// (exec) one stream: its blocks in order, then the frame's checks; any
-// error (or a stream the walk refused) -> the serial decoder, whose status
-// is the stream's.  Returns the status.
-template <class G>
-HD int32_t lp_exec_stream(G &g, Smem *sm, FpFrame &fr, const LpStream &st, const LpBlock *blk,
-                          const uint8_t *pool, const Ctx &c, uint8_t *slot, int codec,
-                          bool &lp_used) {
-  bool ok = st.mode == kLpDecode;
-  for (uint32_t k = 0; ok && k < st.nblk; ++k)
-    if (blk[st.first + k].err) ok = false;
-  if (ok) {
-    g.all([&](auto &tm) {
-      tm.one([&] {
-        fr.op = 0;
-        fr.fstart = 0;
-        fr.rep[0] = 1;
-        fr.rep[1] = 4;
-        fr.rep[2] = 8;
-        sm[0].err = 0;
-      });
-      tm.sync();
-    });
-    g.sync_all();
-    for (uint32_t k = 0; k < st.nblk; ++k) {
-      const LpBlock &b = blk[st.first + k];
-      g.all([&](auto &tm) {
-        tm.one([&] {
-          Smem &s = sm[0];
-          s.btype = b.btype;
-          s.bstart = b.bstart;
-          s.bsize = b.bsize;
-          s.nseq = b.nseq;
-          s.lit_kind = b.lit_kind;
-          s.lit_n = b.lit_n;
-          s.lit_base = b.lit_base;
-          s.lit_rle = b.lit_rle;
-          s.rep[0] = b.rep[0];
-          s.rep[1] = b.rep[1];
-          s.rep[2] = b.rep[2];
-        });
-        tm.sync();
-        const Ctx cb{c.in, c.out, c.out + b.lit_off, c.len, c.cap};
-        exec_lp(tm, sm, fr, cb, (const Ent *)(pool + b.ent_off), b.nent, b.bout);
-      });
-      g.sync_all();
-      if (sm[0].err) break;
-    }
-    g.wave(0, [&](auto &tm) {
-      tm.one([&] {
-        Smem &s = sm[0];
-        if (!s.err && st.fcs_set && fr.op != st.fcs) s.err = ZF(kErrFormat);
-        if (!s.err && st.expect >= 0 && (int64_t)fr.op != st.expect) s.err = ZF(kErrFormat);
-        s.op = fr.op;
-        s.fstart = 0;
-        s.ck_pos = st.ck_pos;
-      });
-      tm.sync();
-      if (!sm[0].err && st.cksum) verify_frame(tm, sm[0], c);
-    });
-    g.sync_all();
-    ok = !sm[0].err;
+// (exec) one stream: its blocks in order, then the frame's checks.
+// Returns the status, or kLpRedo when the serial decoder has to decode the
+// stream (refused by the walk, or any LP error: it then reports the error
+// the serial decoder finds).
+constexpr int32_t kLpRedo = INT32_MIN;
+
+template <class TM>
+HD int32_t lp_exec_stream(TM &tm, LpX &x, const LpStream &st, const LpBlock *blk,
+                          const uint8_t *pool, const Ctx &c) {
+  if (st.mode != kLpDecode) return kLpRedo;
+  for (uint32_t k = 0; k < st.nblk; ++k)
+    if (blk[st.first + k].err) return kLpRedo;
+  tm.one([&] {
+    x.op = 0;
+    x.rep[0] = 1;
+    x.rep[1] = 4;
+    x.rep[2] = 8;
+    x.err = 0;
+  });
+  tm.sync();
+  for (uint32_t k = 0; k < st.nblk && !x.err; ++k) {
+    const LpBlock &b = blk[st.first + k];
+    lpx_block(tm, x, c, b, (const Ent *)(pool + b.ent_off));
   }
-  lp_used = ok;
-  if (!ok) {
-    const Ctx cs{c.in, c.out, slot, c.len, c.cap};
-    g.wave(0, [&](auto &tm) { run(tm, sm[0], cs, codec); });
-    g.sync_all();
-  }
-  return sm[0].err ? sm[0].err : (int32_t)sm[0].op;
+  if (x.err || (st.fcs_set && x.op != st.fcs) || (st.expect >= 0 && (int64_t)x.op != st.expect))
+    return kLpRedo;
+  return (int32_t)x.op;
 }
 
 // frame-parallel scratch per workgroup: NW literal slots, then NW - 1
@@ -3127,7 +3237,7 @@ HD void lp_walk_stream(LpWalk &ws, const Ctx &c, int codec, uint32_t i, uint8_t 
                       need <= l.ent_cap - eoff;
     uint32_t n2, l2, e2;
     if (fits && lp_walk(ws, c, codec, i, blk + first, c.cap - lits, eoff, n2, l2, e2, s) &&
-        n2 == nblk) {
+        n2 == nblk && !s.cksum) {              // a content checksum: the serial decoder verifies it
       s.first = first;
       s.nblk = nblk;
       s.mode = kLpDecode;
@@ -3189,24 +3299,39 @@ __global__ void __launch_bounds__(NT) zstd_lp_entropy(const uint8_t *src, uint8_
     lp_entropy_group(tm, W, blk, k0, nlist, src, dst, desc, pool + l.ents);
 }
 
-__global__ void __launch_bounds__(NT * FPW) zstd_lp_exec(int codec, const uint8_t *src, uint8_t *dst,
-                                                         const strom_decomp_desc *desc, uint32_t n,
-                                                         int32_t *status, uint8_t *pool, LpLayout l) {
-  __shared__ Smem sm[FPW];
-  __shared__ FpFrame fr;
-  DevGroup g;
+__global__ void __launch_bounds__(LPX_T) zstd_lp_exec(const uint8_t *src, uint8_t *dst,
+                                                      const strom_decomp_desc *desc, uint32_t n,
+                                                      int32_t *status, uint8_t *pool, LpLayout l) {
+  __shared__ LpX x;
+  DevTeam tm;
   const LpStream *st = (const LpStream *)(pool + l.streams);
   const LpBlock *blk = (const LpBlock *)(pool + l.blocks);
-  uint8_t *slot = pool + l.slots + (size_t)(blockIdx.x % l.nslot) * SLOT;
   for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
     const strom_decomp_desc d = desc[b];
-    const Ctx c{src + d.src_off, dst + d.dst_off, slot, d.src_len, d.dst_len};
-    bool used;
-    const int32_t r = lp_exec_stream(g, sm, fr, st[b], blk, pool + l.ents, c, slot, codec, used);
+    const Ctx c{src + d.src_off, dst + d.dst_off, nullptr, d.src_len, d.dst_len};
+    const int32_t r = lp_exec_stream(tm, x, st[b], blk, pool + l.ents, c);
     if (threadIdx.x == 0) {
       status[b] = r;
-      if (used) atomicAdd(&((LpHdr *)pool)->lp_done, 1u);
+      if (r != kLpRedo) atomicAdd(&((LpHdr *)pool)->lp_done, 1u);
     }
+    __syncthreads();
+  }
+}
+
+// the streams the LP path handed back (status kLpRedo): the serial decoder,
+// one wave each, a literal slot per workgroup
+__global__ void __launch_bounds__(NT) zstd_lp_serial(int codec, const uint8_t *src, uint8_t *dst,
+                                                     const strom_decomp_desc *desc, uint32_t n,
+                                                     int32_t *status, uint8_t *pool, LpLayout l) {
+  __shared__ Smem s;
+  DevTeam tm;
+  uint8_t *lit = pool + l.slots + (size_t)blockIdx.x * SLOT;
+  for (uint32_t b = blockIdx.x; b < n; b += gridDim.x) {
+    if (status[b] != kLpRedo) continue;
+    const strom_decomp_desc d = desc[b];
+    const Ctx c{src + d.src_off, dst + d.dst_off, lit, d.src_len, d.dst_len};
+    run(tm, s, c, codec);
+    if (threadIdx.x == 0) status[b] = s.err ? s.err : (int32_t)s.op;
     __syncthreads();
   }
 }
@@ -3218,8 +3343,8 @@ uint32_t lp_entropy_per_cu() {
 }
 
 uint32_t lp_exec_per_cu() {
-  const uint32_t per = (160u << 10) / (uint32_t)(FPW * sizeof(Smem) + sizeof(FpFrame));
-  return per ? per : 1;
+  const uint32_t per = (160u << 10) / (uint32_t)sizeof(LpX);
+  return per ? (per > 8 ? 8 : per) : 1;
 }
 
 double lp_ent_factor() {
@@ -3496,10 +3621,13 @@ extern "C" int strom_decompress_zstd_lp(int codec, const void *d_src, void *d_ds
   const uint32_t cus = cu_count();
   uint32_t xgrid = cus * lp_exec_per_cu();
   if (xgrid > nstreams) xgrid = nstreams;
+  // the serial fallback's workgroups (each a 128 KiB literal slot)
+  uint32_t sgrid = cus * 2;
+  if (sgrid > nstreams) sgrid = nstreams;
   const uint64_t bc = dst_bytes / 32768 + 4ull * nstreams + 64;
   const uint32_t blk_cap = bc > 0x7fffffffull ? 0x7fffffffu : (uint32_t)bc;
   const uint64_t ent_cap = lp_up((uint64_t)(lp_ent_factor() * (double)dst_bytes) + (1 << 20), 256);
-  const LpLayout l = lp_layout(nstreams, blk_cap, xgrid, ent_cap);
+  const LpLayout l = lp_layout(nstreams, blk_cap, sgrid, ent_cap);
   std::lock_guard<std::mutex> g(g_mu);          // held through the launches (scratch_for)
   uint8_t *pool = scratch_for(stream, l.total, 1);
   if (!pool) return -12;
@@ -3513,7 +3641,9 @@ extern "C" int strom_decompress_zstd_lp(int codec, const void *d_src, void *d_ds
   if (egrid > want) egrid = (uint32_t)want;
   hipLaunchKernelGGL(zstd_lp_entropy, dim3(egrid), dim3(NT), 0, s, (const uint8_t *)d_src,
                      (uint8_t *)d_dst, d_desc, pool, l);
-  hipLaunchKernelGGL(zstd_lp_exec, dim3(xgrid), dim3(NT * FPW), 0, s, codec, (const uint8_t *)d_src,
+  hipLaunchKernelGGL(zstd_lp_exec, dim3(xgrid), dim3(LPX_T), 0, s, (const uint8_t *)d_src,
+                     (uint8_t *)d_dst, d_desc, nstreams, d_status, pool, l);
+  hipLaunchKernelGGL(zstd_lp_serial, dim3(sgrid), dim3(NT), 0, s, codec, (const uint8_t *)d_src,
                      (uint8_t *)d_dst, d_desc, nstreams, d_status, pool, l);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -3576,18 +3706,26 @@ extern "C" int strom_zstd_host_lp(int codec, const uint8_t *src, const strom_dec
   HostTeam tm;
   for (uint32_t k0 = 0; k0 < nlist; k0 += LPB)
     lp_entropy_group(tm, *W, blk, k0, nlist, src, dst, desc, pool.get() + l.ents);
-  std::unique_ptr<Smem[]> sm(new Smem[FPW]());
-  FpFrame fr{};
-  HostGroup g;
-  g.nw = FPW;
+  std::unique_ptr<LpX> x(new LpX());
+  std::unique_ptr<Smem> sm(new Smem());
+  HostTeam tx;
+  tx.n = LPX_T;
+  HostTeam t1;
   const LpStream *st = (const LpStream *)(pool.get() + l.streams);
   uint8_t *slot = pool.get() + l.slots;
   int taken = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    const Ctx c{src + desc[i].src_off, dst + desc[i].dst_off, slot, desc[i].src_len, desc[i].dst_len};
-    bool used;
-    status[i] = lp_exec_stream(g, sm.get(), fr, st[i], blk, pool.get() + l.ents, c, slot, codec, used);
-    taken += used;
+    const Ctx c{src + desc[i].src_off, dst + desc[i].dst_off, nullptr, desc[i].src_len,
+                desc[i].dst_len};
+    status[i] = lp_exec_stream(tx, *x, st[i], blk, pool.get() + l.ents, c);
+    taken += status[i] != kLpRedo;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (status[i] != kLpRedo) continue;
+    const Ctx c{src + desc[i].src_off, dst + desc[i].dst_off, slot, desc[i].src_len,
+                desc[i].dst_len};
+    run(t1, *sm, c, codec);
+    status[i] = sm->err ? sm->err : (int32_t)sm->op;
   }
   return taken;
 }

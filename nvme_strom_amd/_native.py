@@ -131,6 +131,18 @@ class HeapScanArgs(C.Structure):
                 ("blkno_base", C.c_uint32), ("blknos", C.c_void_p)]
 
 
+class PgMvcc(C.Structure):
+    """strom_pg_mvcc (strom.h): snapshot, own transaction and SLRU windows."""
+    _fields_ = [("xmin", C.c_uint32), ("xmax", C.c_uint32), ("xip", C.c_void_p),
+                ("nxip", C.c_uint32), ("suboverflowed", C.c_uint32), ("subxip", C.c_void_p),
+                ("nsubxip", C.c_uint32), ("curcid", C.c_uint32), ("curxids", C.c_void_p),
+                ("ncurxids", C.c_uint32), ("clog_base", C.c_uint32), ("clog", C.c_void_p),
+                ("clog_n", C.c_uint64), ("subtrans", C.c_void_p), ("subtrans_base", C.c_uint32),
+                ("subtrans_n", C.c_uint32), ("mx_offsets", C.c_void_p), ("mx_base", C.c_uint32),
+                ("mx_n", C.c_uint32), ("mx_members", C.c_void_p), ("mxm_n", C.c_uint64),
+                ("mxm_base", C.c_uint32), ("pad", C.c_uint32)]
+
+
 HEAP_MAX_ATTS = 64
 HEAP_MAX_QUALS = 8
 
@@ -206,6 +218,9 @@ _SIGS = {
     "strom_snappy_compress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
     "strom_snappy_decompress_host": (C.c_long, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
     "strom_pg_checksum_host": (C.c_uint16, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "strom_pg_apply_mvcc": (C.c_long, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                       C.c_uint32, C.c_void_p]),
+    "strom_pg_tuple_visible": (C.c_int, [C.c_void_p, C.c_void_p]),
     "strom_pg_apply_snapshot": (C.c_long, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "strom_atomic_fetch_add_u64": (C.c_uint64, [C.c_void_p, C.c_uint64]),

@@ -48,7 +48,7 @@ from .. import api
 from ..ops.heapscan import PAGE_RECHECK, heap_project, heap_scan, heap_scan2
 from ..tensor import FileReader, HbmBuffer, host_buffer
 from ..utils import pgmvcc, pgpage
-from ..utils.pgmvcc import CommitLog, Snapshot
+from ..utils.pgmvcc import CommitLog, MultiXact, Snapshot, SubTrans
 
 BLCKSZ = 8192
 RELSEG_SIZE = 131072          # blocks per segment file (1 GiB)
@@ -68,6 +68,10 @@ class ScanConfig:
     # check); without one, the GPU applies hint bits / PD_ALL_VISIBLE
     snapshot: Optional[Snapshot] = None
     clog: Optional[CommitLog] = None
+    # the rest of HeapTupleSatisfiesMVCC's inputs: pg_subtrans (sub-committed
+    # xids, overflowed snapshots) and pg_multixact (multixact xmax)
+    subtrans: Optional[SubTrans] = None
+    multixact: Optional[MultiXact] = None
 
     def validate(self) -> None:
         if self.chunk_size % BLCKSZ or self.buffer_size % self.chunk_size:
@@ -544,7 +548,7 @@ class HeapRelationScan:
                     res, landed = readers[seg].submit(hb, slot * cfg.chunk_size, ids,
                                                       wb=wbs[slot])
                 if len(cpu_ids):
-                    st.removed += self._checked_pages(readers[seg].fd, cpu_ids, cpu_bufs[slot])
+                    st.removed += self._checked_pages(readers[seg].fd, cpu_ids, cpu_bufs[slot], st)
                     st.nr_checked += len(cpu_ids)
                     at = slot * cfg.chunk_size + len(ids) * BLCKSZ
                     nb = len(cpu_ids) * BLCKSZ
@@ -561,9 +565,11 @@ class HeapRelationScan:
         st.chunk_items = found
         return st
 
-    def _checked_pages(self, fd: int, blocks: np.ndarray, stage: torch.Tensor) -> int:
+    def _checked_pages(self, fd: int, blocks: np.ndarray, stage: torch.Tensor,
+                       st: "ScanResult") -> int:
         """Buffer-manager path: read each block through the page cache and
-        mark the tuples the snapshot must not see as unused."""
+        mark the tuples the snapshot must not see as unused (blocks with
+        tuples the inputs cannot decide go to ``st.recheck_blocks``)."""
         arr = stage.numpy() if stage.device.type == "cpu" else stage.cpu().numpy()
         removed = 0
         for j, b in enumerate(blocks.tolist()):
@@ -571,8 +577,13 @@ class HeapRelationScan:
             got = os.preadv(fd, [memoryview(page)], (b % self.rel.relseg_size) * BLCKSZ)
             if got < BLCKSZ:
                 page[got:] = 0
+            rc: List[int] = []
             removed += pgmvcc.apply_snapshot(page, self.cfg.snapshot, self.cfg.clog,
-                                             b if self.cfg.verify_checksum else None)
+                                             b if self.cfg.verify_checksum else None,
+                                             subtrans=self.cfg.subtrans,
+                                             multi=self.cfg.multixact, recheck=rc)
+            if rc:
+                st.recheck_blocks.append(int(b))
         return removed
 
     def _consume(self, item, hb, readers, found, st: ScanResult) -> None:
@@ -721,8 +732,13 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                         got = os.preadv(fd, [memoryview(page)], (b % rel.relseg_size) * BLCKSZ)
                         if got < BLCKSZ:
                             page[got:] = 0
+                        rc: List[int] = []
                         st.removed += pgmvcc.apply_snapshot(page, cfg.snapshot, cfg.clog,
-                                                            b if cfg.verify_checksum else None)
+                                                            b if cfg.verify_checksum else None,
+                                                            subtrans=cfg.subtrans,
+                                                            multi=cfg.multixact, recheck=rc)
+                        if rc:
+                            st.recheck_blocks.append(int(b))
                     st.nr_checked += len(cpu_ids)
                     blocks_here = np.concatenate([ids, cpu_ids]).astype(np.int64)
                     # block numbers feed the checksum: scan page by page

@@ -116,7 +116,13 @@ def main(argv=None) -> int:
                                              C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         so.strom_zstd_lds_bytes.restype = C.c_uint32
         res.setdefault("variant_lds_bytes", {})[v] = int(so.strom_zstd_lds_bytes())
-        variants.append((v, so.strom_decompress_zstd))
+        if hasattr(so, "strom_decompress_zstd_lp"):
+            so.strom_decompress_zstd_lp.restype = C.c_int
+            so.strom_decompress_zstd_lp.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                    C.c_uint32, C.c_void_p, C.c_uint64,
+                                                    C.c_void_p]
+            so.strom_zstd_lp_last.argtypes = [C.c_void_p, C.c_void_p]
+        variants.append((v, so))
     for kind in a.kinds.split(","):
         for codec, level in cases:
             raws, bufs = frames(kind, a.distinct, codec, level)
@@ -136,8 +142,12 @@ def main(argv=None) -> int:
                 status = torch.empty(n, dtype=torch.int32, device=dev)
                 row = dict(kind=kind, codec=codec, level=level if codec == "zstd" else None,
                            streams=n, bytes=n * rawlen, ratio=round(ratio, 3))
+                # a variant build runs in lp mode when lp is asked for (its
+                # LP geometry is what differs), else in auto
                 runs = [(vn, vf, md) for vn, vf in (variants if codec == "zstd" else variants[:1])
-                        for md in (a.modes.split(",") if codec == "zstd" and vf is None else ["auto"])]
+                        for md in (a.modes.split(",") if codec == "zstd" and vf is None else
+                                   (["lp"] if "lp" in a.modes.split(",") and codec == "zstd"
+                                    else ["auto"]))]
                 for vname, vfn, mode in runs:
                     lib().strom_zstd_fp_mode({"auto": -1, "wave": 0, "fp": 1, "lp": -1}[mode])
                     times = []
@@ -155,9 +165,12 @@ def main(argv=None) -> int:
                         elif vfn is None:
                             rc = lib().strom_decompress(cid, ptr(src), ptr(dst), ptr(d_desc), n,
                                                         ptr(status), None)
+                        elif mode == "lp":
+                            rc = vfn.strom_decompress_zstd_lp(cid, ptr(src), ptr(dst), ptr(d_desc),
+                                                              n, ptr(status), dst.numel(), None)
                         else:
-                            rc = vfn(cid, ptr(src), ptr(dst), ptr(d_desc), n, ptr(status),
-                                     None, 0, None)
+                            rc = vfn.strom_decompress_zstd(cid, ptr(src), ptr(dst), ptr(d_desc), n,
+                                                           ptr(status), None, 0, None)
                         check(rc, codec)
                         e1.record()
                         torch.cuda.synchronize()
@@ -174,12 +187,11 @@ def main(argv=None) -> int:
                     row[pre + "GBps"] = round(n * rawlen / med / 1e9, 2)
                     row[pre + "ms"] = round(med * 1e3, 3)
                     row[pre + "verified"] = ok
-                    if mode == "lp" and vfn is None:
+                    if mode == "lp":
                         # streams the lane-parallel path decoded itself (not the serial fallback)
                         cnt = np.zeros(4, np.uint64)
-                        lib().strom_zstd_lp_last(None, cnt.ctypes.data)
-                        row["lp_blocks"], row["lp_streams"] = int(cnt[0]), int(cnt[1])
-                        row["lp_entry_bytes"] = int(cnt[2])
+                        (vfn or lib()).strom_zstd_lp_last(None, cnt.ctypes.data)
+                        row[pre + "lp_blocks"], row[pre + "lp_streams"] = int(cnt[0]), int(cnt[1])
                 if a.prof and codec == "zstd":
                     row["phases"] = prof(cid, n, src, dst, d_desc, status)
                 _log(json.dumps(row))

@@ -35,22 +35,10 @@ def test_vm_roundtrip_multi_page(tmp_path):
 
 
 def _model_visible(xmin, xmax, mask, snap, clog):
-    """Independent model of the MVCC rules the native check applies."""
-    def st(x):
-        return clog.status(x)
-
-    def sees(x):
-        return snap.sees(x)
-    frozen = (mask & (XMIN_C | XMIN_I)) == (XMIN_C | XMIN_I)
-    if not frozen:
-        if mask & XMIN_I:
-            return False
-        if not (mask & XMIN_C or st(xmin) == 1) or not sees(xmin):
-            return False
-    if mask & XMAX_I or xmax == 0 or mask & 0x0080:
-        return True
-    deleted = bool(mask & XMAX_C) or st(xmax) == 1
-    return not (deleted and sees(xmax))
+    """The independent Python transcription (pgmvcc.model_visible); an
+    undecidable tuple (None) is kept."""
+    r = pgmvcc.model_visible(xmin, xmax, mask, 0, snap, clog)
+    return True if r is None else r
 
 
 def _case_tuples(rng, n, clog):
@@ -222,3 +210,177 @@ def test_heap_scan_pool_keyed_and_released(tmp_path, monkeypatch):
     del h3
     gc.collect()
     assert freed == ["A", "B", "C"]
+
+
+# ------------------------------------------------ HeapTupleSatisfiesMVCC parity
+from nvme_strom_amd.utils.pgmvcc import (HEAP_COMBOCID, HEAP_XMAX_EXCL_LOCK, HEAP_XMAX_INVALID,  # noqa: E402
+                                         HEAP_XMAX_IS_MULTI, HEAP_XMAX_LOCK_ONLY, HEAP_XMIN_COMMITTED,
+                                         HEAP_XMIN_INVALID, MX_FOR_SHARE, MX_FOR_UPDATE, MX_UPDATE,
+                                         MultiXact, SubTrans, XACT_ABORTED, XACT_COMMITTED,
+                                         XACT_IN_PROGRESS, XACT_SUBCOMMITTED)
+
+W = 1 << 32
+
+
+def _hdr(xmin, xmax, mask, cid=0):
+    return struct.pack("<IIIHHHHHB", xmin % W, xmax % W, cid, 0, 0, 0, 1, mask, 24)
+
+
+def _both(xmin, xmax, mask, snap, clog, sub=None, mx=None, cid=0):
+    nat = pgmvcc.native_visible(_hdr(xmin, xmax, mask, cid), snap, clog, sub, mx)
+    mod = pgmvcc.model_visible(xmin % W, xmax % W, mask, cid, snap, clog, sub, mx)
+    assert nat == mod, (xmin, xmax, hex(mask), cid, nat, mod)
+    return nat
+
+
+def test_mvcc_wraparound_snapshot():
+    """A snapshot straddling the 2^32 wrap: ids compare modulo 2^32
+    (TransactionIdPrecedes), so an xid just before the wrap precedes one
+    just after it, and the commit-log window wraps with them."""
+    base = W - 1000
+    clog = CommitLog(4000, base=base)
+    for x in range(base, base + 4000):
+        clog.set(x % W, XACT_COMMITTED)
+    snap = Snapshot(xmin=(W - 10) % W, xmax=20, xip=[W - 5, 7])
+    old, running, after, late = W - 50, W - 5, 5, 30
+    assert _both(old, 0, HEAP_XMAX_INVALID, snap, clog) is True      # before xmin
+    assert _both(running, 0, HEAP_XMAX_INVALID, snap, clog) is False  # in xip
+    assert _both(after, 0, HEAP_XMAX_INVALID, snap, clog) is True     # past the wrap, < xmax
+    assert _both(7, 0, HEAP_XMAX_INVALID, snap, clog) is False        # in xip past the wrap
+    assert _both(late, 0, HEAP_XMAX_INVALID, snap, clog) is False     # >= xmax
+    # deleted by a committed xid before the wrap: gone; by one >= xmax: still there
+    assert _both(old, W - 40, 0, snap, clog) is False
+    assert _both(old, late, 0, snap, clog) is True
+    # the old unsigned compare would call W - 50 >= xmax (20) and hide it
+    assert pgmvcc.xid_precedes(W - 50, 20)
+
+
+def test_mvcc_multixact_lockers_and_updaters():
+    clog = CommitLog(2000)
+    for x in range(3, 2000):
+        clog.set(x, XACT_COMMITTED)
+    clog.set(500, XACT_ABORTED)
+    clog.set(600, XACT_IN_PROGRESS)
+    mx = MultiXact(base=10)
+    lockers = mx.add([(300, MX_FOR_SHARE), (301, MX_FOR_UPDATE)])
+    upd_commit = mx.add([(300, MX_FOR_SHARE), (400, MX_UPDATE)])
+    upd_abort = mx.add([(301, MX_FOR_SHARE), (500, MX_UPDATE)])
+    upd_running = mx.add([(600, MX_UPDATE)])
+    snap = Snapshot(xmin=650, xmax=700, xip=[])
+    m = HEAP_XMIN_COMMITTED | HEAP_XMAX_IS_MULTI
+    assert _both(100, lockers, m, snap, clog, mx=mx) is True          # lockers delete nothing
+    assert _both(100, lockers, m | HEAP_XMAX_LOCK_ONLY, snap, clog, mx=mx) is True
+    assert _both(100, upd_commit, m, snap, clog, mx=mx) is False      # committed update
+    assert _both(100, upd_abort, m, snap, clog, mx=mx) is True        # aborted update
+    snap2 = Snapshot(xmin=590, xmax=700, xip=[600])
+    assert _both(100, upd_running, m, snap2, clog, mx=mx) is True     # updater still running
+    # an xmax that is a multixact looked up in pg_xact would be nonsense: a
+    # multi outside the window is undecided, not guessed
+    assert _both(100, 999, m, snap, clog, mx=mx) is None
+    # a pre-9.3 exclusive lock without IS_MULTI is a lock too
+    assert _both(100, 400, HEAP_XMIN_COMMITTED | HEAP_XMAX_EXCL_LOCK, snap, clog) is True
+
+
+def test_mvcc_subtransactions():
+    """Sub-committed xids follow their parent (pg_subtrans); with an
+    overflowed subxip the snapshot maps a subxid to its top-level xid."""
+    clog = CommitLog(2000)
+    sub = SubTrans(2000)
+    clog.set(100, XACT_COMMITTED)
+    clog.set(101, XACT_SUBCOMMITTED)
+    sub.set(101, 100)                       # child of a committed parent
+    clog.set(200, XACT_ABORTED)
+    clog.set(201, XACT_SUBCOMMITTED)
+    sub.set(201, 200)                       # child of an aborted parent
+    clog.set(300, XACT_IN_PROGRESS)
+    clog.set(301, XACT_SUBCOMMITTED)
+    sub.set(301, 300)                       # child of a running parent
+    snap = Snapshot(xmin=50, xmax=400, xip=[300], subxip=[301])
+    mi = HEAP_XMAX_INVALID
+    assert _both(101, 0, mi, snap, clog, sub) is True
+    assert _both(201, 0, mi, snap, clog, sub) is False
+    assert _both(301, 0, mi, snap, clog, sub) is False
+    over = Snapshot(xmin=50, xmax=400, xip=[300], suboverflowed=True)
+    assert _both(301, 0, mi, over, clog, sub) is False   # via its top-level xid
+    assert _both(101, 0, mi, over, clog, sub) is True
+    # without pg_subtrans a sub-committed xid cannot be decided
+    assert _both(101, 0, mi, snap, clog, None) is None
+    # deleted by a sub-committed child of a committed parent: gone
+    assert _both(100, 101, 0, snap, clog, sub) is False
+    assert _both(100, 201, 0, snap, clog, sub) is True
+
+
+def test_mvcc_own_transaction():
+    """The scanning transaction's own inserts / deletes by command id; a
+    combo command id (inserted and deleted by it) is undecidable here."""
+    clog = CommitLog(1000)
+    for x in range(3, 1000):
+        clog.set(x, XACT_COMMITTED)
+    clog.set(700, XACT_IN_PROGRESS)
+    clog.set(701, XACT_SUBCOMMITTED)
+    snap = Snapshot(xmin=690, xmax=710, xip=[700], curxids=[700, 701], curcid=5)
+    mi = HEAP_XMAX_INVALID
+    assert _both(700, 0, mi, snap, clog, cid=3) is True        # inserted before the scan
+    assert _both(701, 0, mi, snap, clog, cid=4) is True        # by its subtransaction
+    assert _both(700, 0, mi, snap, clog, cid=5) is False       # inserted at / after it
+    assert _both(100, 700, HEAP_XMIN_COMMITTED, snap, clog, cid=2) is False   # deleted before
+    assert _both(100, 700, HEAP_XMIN_COMMITTED, snap, clog, cid=9) is True    # deleted after
+    assert _both(700, 700, HEAP_COMBOCID, snap, clog, cid=1) is None
+    # own insert, deleted by another (aborted) subtransaction not in curxids
+    assert _both(700, 702, 0, snap, clog, cid=1) is True
+
+
+def test_mvcc_native_equals_model_randomized():
+    """Thousands of random headers — hint bits, multixacts, subtransactions,
+    own xids, a window across the wrap — native == model, also through a
+    page (removed + recheck line numbers)."""
+    rng = np.random.default_rng(77)
+    base = W - 3000
+    n = 6000
+    clog = CommitLog(n, base=base)
+    sub = SubTrans(n, base=base)
+    xs = [(base + i) % W for i in range(3, n)]
+    for x in xs:
+        st = int(rng.choice([XACT_COMMITTED] * 4 + [XACT_ABORTED, XACT_IN_PROGRESS,
+                                                     XACT_SUBCOMMITTED]))
+        clog.set(x, st)
+        if st == XACT_SUBCOMMITTED or rng.random() < 0.2:
+            sub.set(x, (x - int(rng.integers(1, 40))) % W)
+    mx = MultiXact(base=W - 20)
+    multis = [mx.add([(int(rng.choice(xs)), int(rng.integers(0, 6)))
+                      for _ in range(int(rng.integers(1, 4)))]) for _ in range(60)]
+    pick = lambda: int(rng.choice(xs))   # noqa: E731
+    for trial in range(6):
+        xmin = (base + int(rng.integers(1000, 3000))) % W
+        xmax = (xmin + int(rng.integers(10, 2500))) % W
+        xip = sorted({(xmin + int(rng.integers(0, 10))) % W for _ in range(5)})
+        snap = Snapshot(xmin=xmin, xmax=xmax, xip=xip,
+                        subxip=[pick() for _ in range(5)], suboverflowed=bool(trial % 2),
+                        curxids=[pick(), pick()], curcid=int(rng.integers(0, 10)))
+        for _ in range(500):
+            ismulti = rng.random() < 0.2
+            xmax_v = int(rng.choice(multis)) if ismulti else int(rng.choice([0] + xs))
+            mask = int(rng.choice([0, HEAP_XMIN_COMMITTED, HEAP_XMIN_INVALID,
+                                   HEAP_XMIN_COMMITTED | HEAP_XMIN_INVALID]))
+            mask |= int(rng.choice([0, HEAP_XMAX_INVALID, 0x0400, HEAP_XMAX_LOCK_ONLY,
+                                    HEAP_XMAX_EXCL_LOCK]))
+            mask |= HEAP_XMAX_IS_MULTI if ismulti else 0
+            mask |= HEAP_COMBOCID if rng.random() < 0.05 else 0
+            xmin_v = int(rng.choice(snap.curxids)) if rng.random() < 0.1 else pick()
+            _both(xmin_v, xmax_v, mask, snap, clog, sub, mx, cid=int(rng.integers(0, 10)))
+        # a page: removed and recheck lists against the model
+        cases = []
+        for i in range(120):
+            ismulti = rng.random() < 0.2
+            xmax_v = int(rng.choice(multis)) if ismulti else int(rng.choice([0] + xs))
+            mask = int(rng.choice([0, HEAP_XMIN_COMMITTED])) | (HEAP_XMAX_IS_MULTI if ismulti else 0)
+            cases.append((i, pick(), xmax_v, mask))
+        tuples = [pgpage.tuple_bytes(struct.pack("<q", i), infomask=m, xmin=a, xmax=b)
+                  for i, a, b, m in cases]
+        page = np.frombuffer(bytearray(pgpage.build_page(tuples, with_checksum=False)),
+                             np.uint8).copy()
+        rc = []
+        removed = pgmvcc.apply_snapshot(page, snap, clog, subtrans=sub, multi=mx, recheck=rc)
+        want = [pgmvcc.model_visible(a, b, m, 0, snap, clog, sub, mx) for i, a, b, m in cases]
+        assert removed == sum(1 for w in want if w is False)
+        assert rc == [i + 1 for i, w in enumerate(want) if w is None]
