@@ -284,6 +284,7 @@ def main() -> int:
         offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
         ioctl_p50 = float(np.percentile(S.ioctl_latency(buf.handle, 0, fd, offs)[50:], 50)) / 1e3
         costs = S.host_costs(fd)
+        costs.update({"engine_" + k: v for k, v in S.engine_costs(buf.handle, fd).items()})
 
     # the storage's own sequential rate in this run: host-only io_uring
     # O_DIRECT reads of the same shard, the engine's request size, ring

@@ -958,6 +958,43 @@ int strom_host_costs(int fd, uint64_t *out, int n) {
   return 0;
 }
 
+// The engine's own per-request host steps on the synchronous 4 KiB path,
+// ns per call (what the "lookup" / "complete" phases are made of):
+//   0 gpu_registry().get(handle)   1 validate (HIP buffer id of the range)
+//   2 open_file (fstat + cache)    3 completion bookkeeping (histograms,
+//   counters, mapping in-flight count) — finish_request and the stats adds
+int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
+  using namespace strom;
+  if (n <= 0 || fd < 0) return -EINVAL;
+  auto bench = [&](auto &&fn) {
+    const uint64_t t0 = mono_ns();
+    for (int i = 0; i < n; ++i) fn();
+    return (mono_ns() - t0) / (uint64_t)n;
+  };
+  volatile uint64_t sink = 0;
+  auto g = gpu_registry().get(handle);
+  if (!g) return -ENOENT;
+  out[0] = bench([&] { sink += (uint64_t)(gpu_registry().get(handle) != nullptr); });
+  out[1] = bench([&] { sink += (uint64_t)gpu_registry().validate(g); });
+  int err = 0;
+  out[2] = bench([&] { sink += (uint64_t)(engine().open_file(fd, &err) != nullptr); });
+  out[3] = bench([&] {
+    Stats &st = stats();
+    st.copy_ns.add(1000);
+    st.nr_debug[0].fetch_add(1, std::memory_order_relaxed);
+    st.inflight_inc();
+    g->inflight.fetch_add(1);
+    long status = 0;
+    IoReq r;
+    r.gmap = g.get();
+    r.status_out = &status;
+    r.t_submit_tsc = tsc_now();
+    finish_request(r, 0);
+    sink += (uint64_t)status;
+  });
+  return 0;
+}
+
 // SSD2RAM destinations: mmap a DMA-buffer fd through the engine so the
 // range sits in the registry's address index (no VMA query per request).
 // Kernel provider: a plain mmap of the kernel's buffer fd.

@@ -538,14 +538,15 @@ class Engine {
   int stripe_close(int sfd);
   struct StripeSet;
 
+  // the per-file cache (fstat-validated): classification, descriptors, map
+  std::shared_ptr<OpenFile> open_file(int fd, int *err);
+
  private:
   int check_file(strom_check_file *a);
   int memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a);
   int memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a);
   int memcpy_wait(strom_memcpy_wait *a);
   int memcpy_wait_timed(strom_memcpy_wait_timed *a);
-
-  std::shared_ptr<OpenFile> open_file(int fd, int *err);
 
   std::shared_ptr<StripeSet> stripe(int fd);
 

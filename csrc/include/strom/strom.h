@@ -65,6 +65,9 @@ int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t 
  * latency breakdown: {clock_gettime, rdtsc, fstat(fd), mincore 1 page of fd,
  * bare syscall, mutex lock+unlock, condvar notify} -> out[7]. */
 int strom_host_costs(int fd, uint64_t *out, int n);
+/* the engine's own steps of a synchronous read (registry lookup, freed-range
+ * check, file cache, completion bookkeeping), ns per call */
+int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n);
 
 /* Storage ceiling for a block size, no engine: `threads` io_uring rings,
  * each `qd` deep, O_DIRECT reads of `block` bytes at random aligned

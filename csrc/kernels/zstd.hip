@@ -2207,19 +2207,20 @@ struct HostGroup {
 // stream's latency is ~1,000 cycles per sequence and the chip fills only
 // with thousands of streams (profiles/r4/zstd: 2,048 val streams at 34.8
 // GB/s, VALU-issue-bound).  The lane-parallel ("LP") decoder gives every
-// BLOCK its own lanes instead: LPB blocks share a wave, a block's four
+// BLOCK its own lanes instead: several blocks share a wave, a block's four
 // Huffman literal streams decode on four of its lanes and its sequence
 // bitstream on one, each lane walking its own tables and input window in
-// LDS.  Three launches:
+// LDS.  Launches:
 //   walk     one lane per stream: frame + block headers, every block's
 //            literal / sequence counts and the Huffman-tree / FSE-table
 //            definitions it may refer to (treeless / repeat-mode blocks
 //            rebuild them on their own lanes); blocks go to one list,
 //            entries are allocated from a pool
-//   entropy  LPB blocks per wave (all of a column's blocks at once, in one
+//   lit      LPLB blocks per wave (all of a column's blocks at once, in one
 //            or two resident rounds): literals decode straight into the
-//            stream's OUTPUT buffer, packed at its tail, and sequences into
-//            16-byte entries (repeat offsets symbolic, as the frame-parallel
+//            stream's OUTPUT buffer, packed at its tail
+//   seq      LPSB blocks per wave, one lane each: sequences into 16-byte
+//            entries (repeat offsets symbolic, as the frame-parallel
 //            decoder's)
 //   exec     one workgroup per stream, blocks in order: exec_fp's batches
 //            over the entries, gathers split from stores (a literal's tail
@@ -2234,9 +2235,6 @@ struct HostGroup {
 #ifndef ZS_LPB
 #define ZS_LPB 8
 #endif
-constexpr uint32_t LPB = ZS_LPB;              // blocks per wave
-constexpr uint32_t LPL = NT / LPB;            // lanes per block: >= 4 (one per literal stream)
-static_assert(NT % LPB == 0 && LPL >= 4, "LP lanes");
 constexpr uint32_t LP_LSYM = 128;             // literal symbols per stream per round
 constexpr uint32_t LP_LWIN = 256;             // its input window (one dword per lane)
 constexpr uint32_t LP_SEQN = 64;              // sequences per round
@@ -2353,7 +2351,7 @@ struct alignas(16) LpBlock {
   FpDefs d;
   uint64_t ent_off;
   // entropy
-  uint32_t lit_kind, lit_n, lit_base, lit_rle, nseq, nent, bout;
+  uint32_t lit_kind, lit_n, lit_base, lit_rle, sip, nseq, nent, bout;
   uint32_t rep[3];
   int32_t err;
 };
@@ -2463,56 +2461,82 @@ HD bool lp_walk(LpWalk &s, const Ctx &c, int codec, uint32_t stream, LpBlock *re
   return true;
 }
 
-// ---- entropy: LPB blocks per wave
-struct alignas(16) LpB {
-  union {                                    // the block's tables (one section at a time)
-    struct {
-      uint8_t hsym[2048];
-      uint8_t hlen[2048];
-    };
-    struct {
-      uint32_t tll[512];
-      uint32_t tml[512];
-      uint32_t tof[256];
-    };
-  };
+// ---- entropy: two launches, literal sections then sequence sections, each
+// with its own per-block LDS (a block's Huffman table, or its three FSE
+// tables) and blocks per wave — the sequence launch keeps 4 waves per CU,
+// one per SIMD, where one launch for both held 3.
+// literals: LPLB blocks per wave, 64 / LPLB lanes each (one per stream)
+#ifndef ZS_LPLB
+#define ZS_LPLB ZS_LPB
+#endif
+#ifndef ZS_LPSB
+#define ZS_LPSB 6
+#endif
+constexpr uint32_t LPLB = ZS_LPLB;
+constexpr uint32_t LPLL = NT / LPLB;
+static_assert(NT % LPLB == 0 && LPLL >= 4, "LP literal lanes");
+constexpr uint32_t LPSB = ZS_LPSB;            // sequences: blocks per wave, block b on lane b
+static_assert(LPSB >= 1 && LPSB <= NT, "LP sequence lanes");
+
+struct alignas(16) LpL {                      // a block's literal section
+  uint8_t hsym[2048];
+  uint8_t hlen[2048];
   union {
-    struct {                                 // building a table
+    struct {                                  // building the Huffman table
       SeqEnt hwt[64];
       uint8_t hw[256];
       int16_t norm[64];
       uint16_t snext[64];
       uint32_t wrank[16];
     };
-    alignas(4) uint8_t lwin[4][LP_LWIN];    // literal streams' windows
-    alignas(4) uint8_t swin[LP_SWIN];       // the sequence bitstream's window
+    alignas(4) uint8_t lwin[4][LP_LWIN];     // the four streams' windows
   };
   BR lbr[4];
-  BR sbr;
   uint32_t lcnt[4], lout[4], lwlo[4], lrn[4];
-  uint32_t swlo, act, lact;                  // act: decoding; lact: bit j = stream j has symbols left
-  // lit_header / seq_header state (their field names)
+  uint32_t act, lact;                         // decoding; bit j = stream j has symbols left
+  // lit_header's state (its field names)
   uint32_t ip, bend, op, lit_used, lit_direct, lit_n, lit_kind, lit_base, lit_rle;
   uint32_t hdesc, hdesc_end, hbits, nls;
-  uint32_t tmode[3], tpos[3], tend[3], have_ll, have_of, have_ml;
-  uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
-  uint32_t rep[3], lit, out, nent;
   int32_t err;
   uint32_t len, cap;
   const uint8_t *in;
-  uint8_t *litp;                             // the block's literal region (in the output)
+  uint8_t *litp;                              // the block's literal region (in the output)
+};
+
+struct alignas(16) LpS {                      // a block's sequence section
+  uint32_t tll[512];
+  uint32_t tml[512];
+  uint32_t tof[256];
+  union {
+    struct {                                  // building an FSE table
+      int16_t norm[64];
+      uint16_t snext[64];
+    };
+    alignas(4) uint8_t swin[LP_SWIN];        // the bitstream's window
+  };
+  BR sbr;
+  uint32_t swlo, act;
+  uint32_t tmode[3], tpos[3], tend[3], have_ll, have_of, have_ml;
+  uint32_t nseq, seq_done, st_ll, st_of, st_ml, al_ll, al_of, al_ml;
+  uint32_t rep[3], lit, out, nent, lit_n, sip, bend;
+  int32_t err;
+  uint32_t len;
+  const uint8_t *in;
   Ent *ent;
 };
 
-struct LpWave {
-  LpB b[LPB];
+struct LpLWave {
+  LpL b[LPLB];
 };
 
-HD Ctx lp_ctx(const LpB &s) { return Ctx{s.in, nullptr, nullptr, s.len, s.cap}; }
+struct LpSWave {
+  uint32_t ctab[36 + 53];                     // LL / ML code -> base | extra bits << 24
+  LpS b[LPSB];
+};
 
-// (0) block b's lane 0: load its record, literal section header + tree
-HD void lp_begin(LpB &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const uint8_t *src,
-                 uint8_t *dst, const strom_decomp_desc *desc, uint8_t *pool) {
+// (L0) a block's lane 0: its record, literal section header + tree
+HD void lp_lit_begin(LpL &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const uint8_t *src,
+                     uint8_t *dst, const strom_decomp_desc *desc) {
   s.act = 0;
   s.lact = 0;
   s.err = 0;
@@ -2524,24 +2548,14 @@ HD void lp_begin(LpB &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const u
   s.len = dd.src_len;
   s.cap = dd.dst_len;
   s.litp = dst + dd.dst_off + r.lit_off;
-  s.ent = (Ent *)(pool + r.ent_off);
   s.ip = r.bstart;
   s.bend = r.bend;
   s.op = 0;
   s.hbits = r.d.hbits;
   s.hdesc = r.d.hdesc;
   s.hdesc_end = r.d.hdesc_end;
-  s.have_ll = r.d.have[kLL];
-  s.have_of = r.d.have[kOF];
-  s.have_ml = r.d.have[kML];
-  for (uint32_t j = 0; j < 3; ++j) {
-    s.tmode[j] = r.d.tmode[j];
-    s.tpos[j] = r.d.tpos[j];
-    s.tend[j] = r.d.tend[j];
-    s.rep[j] = kSym | (j << 26);
-  }
   s.act = 1;
-  const Ctx c = lp_ctx(s);
+  const Ctx c{s.in, nullptr, nullptr, s.len, s.cap};
   if (!lit_header(s, c)) {
     s.err = ZF(kErrFormat);
     return;
@@ -2550,6 +2564,18 @@ HD void lp_begin(LpB &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const u
   if (s.lit_kind == kLitScratch)
     for (uint32_t j = 0; j < s.nls; ++j)
       if (s.lcnt[j]) s.lact |= 1u << j;
+}
+
+// (L) the block's results: its literal section, where its sequences start
+HD void lp_lit_end(const LpL &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
+  if (k >= nlist || !blk[k].active) return;
+  LpBlock &r = blk[k];
+  r.err = s.err;
+  r.lit_kind = s.lit_kind;
+  r.lit_n = s.lit_n;
+  r.lit_base = s.lit_base;
+  r.lit_rle = s.lit_rle;
+  r.sip = s.ip;                               // where the sequence section starts
 }
 
 // (1) literal windows of every stream with symbols left: one dword per lane
@@ -2619,10 +2645,10 @@ HD void lp_windows(const uint32_t *safe, uint32_t t, F win) {
   }
 }
 
-HD void lp_lit_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
-  lp_windows<4 * LPB, LP_LWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in, uint32_t &len,
-                                                       uint32_t &lo, uint8_t *&dst) {
-    LpB &s = W.b[w / 4];
+HD void lp_lit_windows(LpLWave &W, uint32_t t, const uint32_t *safe) {
+  lp_windows<4 * LPLB, LP_LWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in,
+                                                        uint32_t &len, uint32_t &lo, uint8_t *&dst) {
+    LpL &s = W.b[w / 4];
     const uint32_t j = w % 4;
     in = s.in;
     len = s.len;
@@ -2632,10 +2658,10 @@ HD void lp_lit_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
   });
 }
 
-HD void lp_seq_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
-  lp_windows<LPB, LP_SWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in, uint32_t &len,
-                                                   uint32_t &lo, uint8_t *&dst) {
-    LpB &s = W.b[w];
+HD void lp_seq_windows(LpSWave &W, uint32_t t, const uint32_t *safe) {
+  lp_windows<LPSB, LP_SWIN / (4 * NT)>(safe, t, [&](uint32_t w, const uint8_t *&in, uint32_t &len,
+                                                    uint32_t &lo, uint8_t *&dst) {
+    LpS &s = W.b[w];
     in = s.in;
     len = s.len;
     lo = s.swlo;
@@ -2646,10 +2672,10 @@ HD void lp_seq_windows(LpWave &W, uint32_t t, const uint32_t *safe) {
 
 // (1) up to LP_LSYM symbols of literal stream j, straight into the block's
 // literal region (four per container check, as lit_chunk)
-HD void lp_lit_chunk(LpB &s, uint32_t j) {
+HD void lp_lit_chunk(LpL &s, uint32_t j) {
   const uint32_t left = s.lcnt[j];
   BR b = s.lbr[j];
-  const Win w{(uint32_t)offsetof(LpB, lwin) + j * LP_LWIN, s.lwlo[j], LP_LWIN};
+  const Win w{(uint32_t)offsetof(LpL, lwin) + j * LP_LWIN, s.lwlo[j], LP_LWIN};
   const uint32_t n = left < LP_LSYM ? left : LP_LSYM, mb = s.hbits;
   ZG uint8_t *dst = zg(s.litp) + s.lout[j];
   const uint32_t nf = n & ~3u;
@@ -2694,16 +2720,77 @@ HD void lp_lit_chunk(LpB &s, uint32_t j) {
   }
 }
 
-// (2) lane 0 of a block: the sequence section header (compact tables)
-HD void lp_seq_header(LpB &s) {
-  if (!s.act || s.err) return;
-  const Ctx c = lp_ctx(s);
-  uint32_t p = s.ip;
+// the literal launch's wave: LPLB blocks' literal sections
+template <class TM>
+HD void lp_lit_group(TM &tm, LpLWave &W, LpBlock *blk, uint32_t k0, uint32_t nlist,
+                     const uint8_t *src, uint8_t *dst, const strom_decomp_desc *desc) {
+  tm.each([&](uint32_t t) {
+    if (t % LPLL == 0) lp_lit_begin(W.b[t / LPLL], blk, k0 + t / LPLL, nlist, src, dst, desc);
+  });
+  tm.sync();
+  for (;;) {
+    const bool more = tm.any([&](uint32_t t) {
+      LpL &s = W.b[t / LPLL];
+      const uint32_t j = t % LPLL;
+      if (j < 4 && s.err) s.lact = 0;
+      return j < 4 && (s.lact >> j & 1);
+    });
+    if (!more) break;
+    tm.each([&](uint32_t t) {
+      LpL &s = W.b[t / LPLL];
+      const uint32_t j = t % LPLL;
+      if (j < 4 && (s.lact >> j & 1)) s.lwlo[j] = lp_align_lo(s.in, win_lo(s.lbr[j], LP_LWIN - 4));
+    });
+    tm.sync();
+    tm.each([&](uint32_t t) { lp_lit_windows(W, t, (const uint32_t *)desc); });
+    tm.sync();
+    tm.each([&](uint32_t t) {
+      LpL &s = W.b[t / LPLL];
+      const uint32_t j = t % LPLL;
+      if (j < 4 && (s.lact >> j & 1)) lp_lit_chunk(s, j);
+    });
+    tm.sync();
+  }
+  tm.each([&](uint32_t t) {
+    if (t % LPLL == 0) lp_lit_end(W.b[t / LPLL], blk, k0 + t / LPLL, nlist);
+  });
+  tm.fence();
+  tm.sync();
+}
+
+// (S0) block b's lane: the sequence section header (compact tables), from
+// where the literal launch left it
+HD void lp_seq_begin(LpS &s, const LpBlock *blk, uint32_t k, uint32_t nlist, const uint8_t *src,
+                     const strom_decomp_desc *desc, uint8_t *pool) {
+  s.act = 0;
+  s.err = 0;
+  if (k >= nlist) return;
+  const LpBlock &r = blk[k];
+  if (!r.active || r.err) return;
+  const strom_decomp_desc dd = desc[r.stream];
+  s.in = src + dd.src_off;
+  s.len = dd.src_len;
+  s.ent = (Ent *)(pool + r.ent_off);
+  s.lit_n = r.lit_n;
+  s.bend = r.bend;
+  s.have_ll = r.d.have[kLL];
+  s.have_of = r.d.have[kOF];
+  s.have_ml = r.d.have[kML];
+  for (uint32_t j = 0; j < 3; ++j) {
+    s.tmode[j] = r.d.tmode[j];
+    s.tpos[j] = r.d.tpos[j];
+    s.tend[j] = r.d.tend[j];
+    s.rep[j] = kSym | (j << 26);
+  }
+  s.act = 1;
+  const Ctx c{s.in, nullptr, nullptr, s.len, 0};
+  uint32_t p = r.sip;                         // after the literal section
   const uint32_t end = s.bend;
   s.seq_done = 0;
   s.lit = 0;
   s.out = 0;
   s.nent = 0;
+  s.nseq = 0;
   if (p >= end) {
     s.err = ZF(kErrFormat);
     return;
@@ -2711,7 +2798,6 @@ HD void lp_seq_header(LpB &s) {
   const uint32_t b0 = gbyte(c, p);
   uint32_t n;
   if (b0 == 0) {
-    s.nseq = 0;
     if (p + 1 != end) s.err = ZF(kErrFormat);
     return;
   }
@@ -2745,13 +2831,14 @@ HD void lp_seq_header(LpB &s) {
   if (s.sbr.nbits < 0) s.err = ZF(kErrFormat);
 }
 
-// (2) lane 0 of a block: up to LP_SEQN sequences into its entries — seq_chunk
-// with symbolic repeat offsets, one lane per block instead of a whole wave
-HD void lp_seq_chunk(LpB &s) {
+// (S) a block's lane: up to LP_SEQN sequences into its entries — seq_chunk
+// with symbolic repeat offsets on one lane: the LL / ML baselines from the
+// wave's code table, the repeat-offset update as selects
+HD void lp_seq_chunk(LpS &s, const uint32_t *ctab) {
   const uint32_t left = s.nseq - s.seq_done;
   const uint32_t m = left < LP_SEQN ? left : LP_SEQN;
   BR b = s.sbr;
-  const Win w{(uint32_t)offsetof(LpB, swin), s.swlo, LP_SWIN};
+  const Win w{(uint32_t)offsetof(LpS, swin), s.swlo, LP_SWIN};
   uint32_t sll = s.st_ll, sof = s.st_of, sml = s.st_ml;
   uint32_t r0 = s.rep[0], r1 = s.rep[1], r2 = s.rep[2];
   uint32_t n = s.nent, out = s.out, lit = s.lit;
@@ -2760,10 +2847,9 @@ HD void lp_seq_chunk(LpB &s) {
   for (uint32_t i = 0; i < m; ++i) {
     const bool more = i + 1 < left;           // the block's last sequence reads no state bits
     const uint32_t eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
-    uint32_t ob, oa, mb, ma, lb, la;
-    code_base(kOF, eo & 255, ob, oa);
-    code_base(kML, em & 255, mb, ma);
-    code_base(kLL, el & 255, lb, la);
+    const uint32_t cm = ctab[36 + (em & 255)], cl = ctab[el & 255];
+    const uint32_t oa = eo & 255, ob = 1u << oa;
+    const uint32_t ma = cm >> 24, mb = cm & 0xFFFFFF, la = cl >> 24, lb = cl & 0xFFFFFF;
     br_need(b, s, w, 47);
     const uint64_t x1 = br_take(b, oa + ma);
     const uint32_t ml = mb + ubfe((uint32_t)x1, 0, ma);
@@ -2773,26 +2859,25 @@ HD void lp_seq_chunk(LpB &s) {
     const uint32_t nst = more ? lnb + mnb + onb : 0;
     const uint64_t x2 = br_take(b, la + nst);
     const uint32_t ll = lb + ubfe((uint32_t)(x2 >> nst), 0, la);
-    if (more) {
-      const uint32_t y = (uint32_t)x2;
-      sof = (eo >> 16) + ubfe(y, 0, onb);
-      sml = (em >> 16) + ubfe(y, onb, mnb);
-      sll = (el >> 16) + ubfe(y, onb + mnb, lnb);
-    }
-    uint32_t off = r0;
-    if (ofv != 1 || ll == 0) {
-      const bool isnew = ofv > 3;
-      const uint32_t k = ofv - 1 + (ll == 0 ? 1 : 0);
-      const uint32_t rep01 = k == 1 ? r1 : r0;
-      const uint32_t rep012 = k == 2 ? r2 : rep01;
-      const uint32_t rep = k == 3 ? (is_sym(r0) ? r0 + 1 : r0 - 1) : rep012;
-      off = isnew ? ofv - 3 : rep;
-      bad |= isnew && is_sym(off);
-      const bool shift2 = isnew || k >= 2;
-      r2 = shift2 ? r1 : r2;
-      r1 = r0;
-      r0 = off;
-    }
+    const uint32_t y = (uint32_t)x2;
+    sof = (eo >> 16) + ubfe(y, 0, onb);
+    sml = (em >> 16) + ubfe(y, onb, mnb);
+    sll = (el >> 16) + ubfe(y, onb + mnb, lnb);
+    // repeat offsets (RFC 8878 3.1.2.5), as selects: "plain" is the first
+    // repeat offset after literals (nothing changes); k = 1, 2 the second /
+    // third, k = 3 the first minus one (symbolic: + 1 on the symbol's k)
+    const bool isnew = ofv > 3;
+    const bool plain = ofv == 1 && ll != 0;
+    const uint32_t k = ofv - 1 + (ll == 0 ? 1u : 0u);
+    const uint32_t r0m1 = is_sym(r0) ? r0 + 1 : r0 - 1;
+    const uint32_t rep = k == 1 ? r1 : k == 2 ? r2 : r0m1;
+    const uint32_t off = plain ? r0 : isnew ? ofv - 3 : rep;
+    bad |= isnew && is_sym(off);
+    const uint32_t n2 = plain ? r2 : (isnew || k >= 2) ? r1 : r2;
+    const uint32_t n1 = plain ? r1 : r0;
+    r2 = n2;
+    r1 = n1;
+    r0 = off;
     ZG Ent &e = ent[n++];
     e.ll = ll;
     e.off = off;
@@ -2818,8 +2903,8 @@ HD void lp_seq_chunk(LpB &s) {
   if (err) s.err = err;
 }
 
-// (3) lane 0 of a block: trailing literals, checks, the record's results
-HD void lp_end(LpB &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
+// (S) a block's lane: trailing literals, checks, the record's results
+HD void lp_seq_end(LpS &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
   if (k >= nlist) return;
   LpBlock &r = blk[k];
   if (!r.active) {
@@ -2829,9 +2914,10 @@ HD void lp_end(LpB &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
     r.nseq = 0;
     return;
   }
+  if (r.err) return;                          // the literal launch's
   if (!s.err && s.nseq && s.sbr.nbits != 0) s.err = ZF(kErrFormat);
   if (!s.err) {
-    const uint32_t rest = s.lit_n - s.lit;   // lit <= lit_n (lp_seq_chunk's check)
+    const uint32_t rest = s.lit_n - s.lit;    // lit <= lit_n (lp_seq_chunk's check)
     if (rest) {
       Ent e;
       e.ll = rest;
@@ -2845,78 +2931,50 @@ HD void lp_end(LpB &s, LpBlock *blk, uint32_t k, uint32_t nlist) {
     if (s.out > MAXB) s.err = ZF(kErrFormat);
   }
   r.err = s.err;
-  r.lit_kind = s.lit_kind;
-  r.lit_n = s.lit_n;
-  r.lit_base = s.lit_base;
-  r.lit_rle = s.lit_rle;
   r.nseq = s.nseq;
   r.nent = s.nent;
   r.bout = s.out;
   for (uint32_t j = 0; j < 3; ++j) r.rep[j] = s.rep[j];
 }
 
-// One wave's group of LPB blocks (list entries k0 ..): the phases with the
-// team's barriers between them (the kernel: one wave; the CPU: lanes one
-// after another).
+// the sequence launch's wave: LPSB blocks' sequence sections
 template <class TM>
-HD void lp_entropy_group(TM &tm, LpWave &W, LpBlock *blk, uint32_t k0, uint32_t nlist,
-                         const uint8_t *src, uint8_t *dst, const strom_decomp_desc *desc,
-                         uint8_t *pool) {
+HD void lp_seq_group(TM &tm, LpSWave &W, LpBlock *blk, uint32_t k0, uint32_t nlist,
+                     const uint8_t *src, const strom_decomp_desc *desc, uint8_t *pool) {
   tm.each([&](uint32_t t) {
-    if (t % LPL == 0) lp_begin(W.b[t / LPL], blk, k0 + t / LPL, nlist, src, dst, desc, pool);
-  });
-  tm.sync();
-  // literal rounds: window origins, cooperative window loads, LP_LSYM
-  // symbols per stream
-  for (;;) {
-    const bool more = tm.any([&](uint32_t t) {
-      LpB &s = W.b[t / LPL];
-      const uint32_t j = t % LPL;
-      if (j < 4 && s.err) s.lact = 0;
-      return j < 4 && (s.lact >> j & 1);
-    });
-    if (!more) break;
-    tm.each([&](uint32_t t) {
-      LpB &s = W.b[t / LPL];
-      const uint32_t j = t % LPL;
-      if (j < 4 && (s.lact >> j & 1)) s.lwlo[j] = lp_align_lo(s.in, win_lo(s.lbr[j], LP_LWIN - 4));
-    });
-    tm.sync();
-    tm.each([&](uint32_t t) { lp_lit_windows(W, t, (const uint32_t *)desc); });
-    tm.sync();
-    tm.each([&](uint32_t t) {
-      LpB &s = W.b[t / LPL];
-      const uint32_t j = t % LPL;
-      if (j < 4 && (s.lact >> j & 1)) lp_lit_chunk(s, j);
-    });
-    tm.sync();
-  }
-  tm.each([&](uint32_t t) {
-    if (t % LPL == 0) lp_seq_header(W.b[t / LPL]);
+    for (uint32_t c = t; c < 36 + 53; c += tm.size()) {
+      uint32_t base, add;
+      code_base(c < 36 ? kLL : kML, c < 36 ? c : c - 36, base, add);
+      W.ctab[c] = base | add << 24;
+    }
+    if (t < LPSB) lp_seq_begin(W.b[t], blk, k0 + t, nlist, src, desc, pool);
   });
   tm.sync();
   for (;;) {
     const bool more = tm.any([&](uint32_t t) {
-      const LpB &s = W.b[t / LPL];
-      return t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq;
+      if (t >= LPSB) return false;
+      const LpS &s = W.b[t];
+      return s.act && !s.err && s.seq_done < s.nseq;
     });
     if (!more) break;
     tm.each([&](uint32_t t) {
-      LpB &s = W.b[t / LPL];
-      if (t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq)
+      if (t >= LPSB) return;
+      LpS &s = W.b[t];
+      if (s.act && !s.err && s.seq_done < s.nseq)
         s.swlo = lp_align_lo(s.in, win_lo(s.sbr, LP_SWIN - 4));
     });
     tm.sync();
     tm.each([&](uint32_t t) { lp_seq_windows(W, t, (const uint32_t *)desc); });
     tm.sync();
     tm.each([&](uint32_t t) {
-      LpB &s = W.b[t / LPL];
-      if (t % LPL == 0 && s.act && !s.err && s.seq_done < s.nseq) lp_seq_chunk(s);
+      if (t >= LPSB) return;
+      LpS &s = W.b[t];
+      if (s.act && !s.err && s.seq_done < s.nseq) lp_seq_chunk(s, W.ctab);
     });
     tm.sync();
   }
   tm.each([&](uint32_t t) {
-    if (t % LPL == 0) lp_end(W.b[t / LPL], blk, k0 + t / LPL, nlist);
+    if (t < LPSB) lp_seq_end(W.b[t], blk, k0 + t, nlist);
   });
   tm.fence();
   tm.sync();
@@ -3287,16 +3345,27 @@ __global__ void __launch_bounds__(LP_WALK_T) zstd_lp_walk(int codec, const uint8
   lp_walk_stream<LpDevAtom>(ws[threadIdx.x], c, codec, i, pool, l);
 }
 
-__global__ void __launch_bounds__(NT) zstd_lp_entropy(const uint8_t *src, uint8_t *dst,
-                                                      const strom_decomp_desc *desc, uint8_t *pool,
-                                                      LpLayout l) {
-  __shared__ LpWave W;
+__global__ void __launch_bounds__(NT) zstd_lp_lit(const uint8_t *src, uint8_t *dst,
+                                                  const strom_decomp_desc *desc, uint8_t *pool,
+                                                  LpLayout l) {
+  __shared__ LpLWave W;
   const uint32_t nb = *(const volatile uint32_t *)pool;
   const uint32_t nlist = nb < l.blk_cap ? nb : l.blk_cap;
   LpBlock *blk = (LpBlock *)(pool + l.blocks);
   DevTeam tm;
-  for (uint32_t k0 = blockIdx.x * LPB; k0 < nlist; k0 += gridDim.x * LPB)
-    lp_entropy_group(tm, W, blk, k0, nlist, src, dst, desc, pool + l.ents);
+  for (uint32_t k0 = blockIdx.x * LPLB; k0 < nlist; k0 += gridDim.x * LPLB)
+    lp_lit_group(tm, W, blk, k0, nlist, src, dst, desc);
+}
+
+__global__ void __launch_bounds__(NT) zstd_lp_seq(const uint8_t *src, const strom_decomp_desc *desc,
+                                                  uint8_t *pool, LpLayout l) {
+  __shared__ LpSWave W;
+  const uint32_t nb = *(const volatile uint32_t *)pool;
+  const uint32_t nlist = nb < l.blk_cap ? nb : l.blk_cap;
+  LpBlock *blk = (LpBlock *)(pool + l.blocks);
+  DevTeam tm;
+  for (uint32_t k0 = blockIdx.x * LPSB; k0 < nlist; k0 += gridDim.x * LPSB)
+    lp_seq_group(tm, W, blk, k0, nlist, src, desc, pool + l.ents);
 }
 
 __global__ void __launch_bounds__(LPX_T) zstd_lp_exec(const uint8_t *src, uint8_t *dst,
@@ -3337,8 +3406,13 @@ __global__ void __launch_bounds__(NT) zstd_lp_serial(int codec, const uint8_t *s
 }
 
 // LP launch geometry
-uint32_t lp_entropy_per_cu() {
-  const uint32_t per = (160u << 10) / (uint32_t)sizeof(LpWave);
+uint32_t lp_lit_per_cu() {
+  const uint32_t per = (160u << 10) / (uint32_t)sizeof(LpLWave);
+  return per ? (per > 8 ? 8 : per) : 1;
+}
+
+uint32_t lp_seq_per_cu() {
+  const uint32_t per = (160u << 10) / (uint32_t)sizeof(LpSWave);
   return per ? (per > 8 ? 8 : per) : 1;
 }
 
@@ -3636,11 +3710,13 @@ extern "C" int strom_decompress_zstd_lp(int codec, const void *d_src, void *d_ds
   hipLaunchKernelGGL(zstd_lp_walk, dim3((nstreams + LP_WALK_T - 1) / LP_WALK_T), dim3(LP_WALK_T), 0, s,
                      codec, (const uint8_t *)d_src, d_desc, nstreams, pool, l);
   // enough waves for every listed block in one or two resident rounds
-  const uint64_t want = (blk_cap + LPB - 1) / LPB;
-  uint32_t egrid = cus * lp_entropy_per_cu();
-  if (egrid > want) egrid = (uint32_t)want;
-  hipLaunchKernelGGL(zstd_lp_entropy, dim3(egrid), dim3(NT), 0, s, (const uint8_t *)d_src,
+  uint32_t lgrid = cus * lp_lit_per_cu(), sgrid2 = cus * lp_seq_per_cu();
+  if (lgrid > (blk_cap + LPLB - 1) / LPLB) lgrid = (blk_cap + LPLB - 1) / LPLB;
+  if (sgrid2 > (blk_cap + LPSB - 1) / LPSB) sgrid2 = (blk_cap + LPSB - 1) / LPSB;
+  hipLaunchKernelGGL(zstd_lp_lit, dim3(lgrid), dim3(NT), 0, s, (const uint8_t *)d_src,
                      (uint8_t *)d_dst, d_desc, pool, l);
+  hipLaunchKernelGGL(zstd_lp_seq, dim3(sgrid2), dim3(NT), 0, s, (const uint8_t *)d_src, d_desc,
+                     pool, l);
   hipLaunchKernelGGL(zstd_lp_exec, dim3(xgrid), dim3(LPX_T), 0, s, (const uint8_t *)d_src,
                      (uint8_t *)d_dst, d_desc, nstreams, d_status, pool, l);
   hipLaunchKernelGGL(zstd_lp_serial, dim3(sgrid), dim3(NT), 0, s, codec, (const uint8_t *)d_src,
@@ -3668,13 +3744,18 @@ extern "C" int strom_zstd_lp_last(void *stream, uint64_t *out) {
   return 0;
 }
 
-// LP geometry: {LDS bytes per entropy wave, blocks per wave, entropy waves
-// per CU, exec workgroups per CU}
+// LP geometry: {LDS bytes per sequence wave, its blocks, its waves per CU,
+// exec workgroups per CU, LDS bytes per literal wave, its blocks, its waves
+// per CU, 0}
 extern "C" void strom_zstd_lp_info(uint32_t *out) {
-  out[0] = (uint32_t)sizeof(zs::LpWave);
-  out[1] = zs::LPB;
-  out[2] = zs::lp_entropy_per_cu();
+  out[0] = (uint32_t)sizeof(zs::LpSWave);
+  out[1] = zs::LPSB;
+  out[2] = zs::lp_seq_per_cu();
   out[3] = zs::lp_exec_per_cu();
+  out[4] = (uint32_t)sizeof(zs::LpLWave);
+  out[5] = zs::LPLB;
+  out[6] = zs::lp_lit_per_cu();
+  out[7] = 0;
 }
 
 // The LP decoder's three phases on the CPU (host buffers): every stream
@@ -3702,10 +3783,12 @@ extern "C" int strom_zstd_host_lp(int codec, const uint8_t *src, const strom_dec
   const LpHdr &h = *(const LpHdr *)pool.get();
   const uint32_t nlist = h.nblk < l.blk_cap ? h.nblk : l.blk_cap;
   LpBlock *blk = (LpBlock *)(pool.get() + l.blocks);
-  std::unique_ptr<LpWave> W(new LpWave());
+  std::unique_ptr<LpLWave> WL(new LpLWave());
+  std::unique_ptr<LpSWave> WS(new LpSWave());
   HostTeam tm;
-  for (uint32_t k0 = 0; k0 < nlist; k0 += LPB)
-    lp_entropy_group(tm, *W, blk, k0, nlist, src, dst, desc, pool.get() + l.ents);
+  for (uint32_t k0 = 0; k0 < nlist; k0 += LPLB) lp_lit_group(tm, *WL, blk, k0, nlist, src, dst, desc);
+  for (uint32_t k0 = 0; k0 < nlist; k0 += LPSB)
+    lp_seq_group(tm, *WS, blk, k0, nlist, src, desc, pool.get() + l.ents);
   std::unique_ptr<LpX> x(new LpX());
   std::unique_ptr<Smem> sm(new Smem());
   HostTeam tx;

@@ -201,6 +201,7 @@ _SIGS = {
     "strom_gpu_detached": (C.c_long, []),
     "strom_gpu_bar_bytes": (C.c_long, [C.c_ulong]),
     "strom_host_costs": (C.c_int, [C.c_int, C.c_void_p, C.c_int]),
+    "strom_engine_costs": (C.c_int, [C.c_ulong, C.c_int, C.c_void_p, C.c_int]),
     "strom_config_set": (C.c_int, [C.c_char_p, C.c_char_p]),
     "strom_config_get": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "strom_engine_reset": (C.c_int, []),

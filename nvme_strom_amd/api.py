@@ -177,6 +177,16 @@ def host_costs(fd: int, n: int = 20000) -> dict:
     return {k: int(v) for k, v in zip(HOST_COSTS, out)}
 
 
+ENGINE_COSTS = ("registry_get", "validate", "open_file", "completion")
+
+
+def engine_costs(handle: int, fd: int, n: int = 20000) -> dict:
+    """ns per call of the engine's own steps on the synchronous 4 KiB path."""
+    out = np.zeros(len(ENGINE_COSTS), dtype=np.uint64)
+    _check(N.lib().strom_engine_costs(handle, fd, out.ctypes.data, n), "engine_costs")
+    return {k: int(v) for k, v in zip(ENGINE_COSTS, out)}
+
+
 def resident_bytes(fd: int, offset: int = 0, length: int = 1 << 62) -> int:
     return _check(N.lib().strom_resident_bytes(fd, offset, length), "resident_bytes")
 

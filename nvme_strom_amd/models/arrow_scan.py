@@ -212,11 +212,13 @@ class ArrowScan:
     ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
     # ZSTD groups: 1 / ZSTD_ROUND_DIV of the zstd decoder's resident round
     ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "1"))
-    # the zstd decoder per group launch: None the library's choice by stream
-    # count, 0 one wave per stream (groups smaller than its round then decode
-    # concurrently on their slot streams), 1 frame-parallel
+    # the zstd decoder per group launch: 2 lane-parallel (default: the
+    # blocks' entropy stages on the lanes of a wave, so a group's decode
+    # takes about one block's latency, not one stream's), None the wave /
+    # frame-parallel choice by stream count, 0 one wave per stream, 1
+    # frame-parallel
     ZSTD_MODE = (int(os.environ["STROM_ARROW_ZSTD_MODE"])
-                 if os.environ.get("STROM_ARROW_ZSTD_MODE") else None)
+                 if os.environ.get("STROM_ARROW_ZSTD_MODE") else 2)
 
     def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
                  slot_bytes: int = 256 << 20, nslots: int = 3,
@@ -320,7 +322,13 @@ class ArrowScan:
             # latency each (A/B, profiles/r3/zstd/arrow_group_div_ab.json:
             # val 11.0-12.8 GB/s at a round, 5.8 at a quarter, 4.2 at an eighth)
             from .. import _native as N
-            if self.ZSTD_MODE == 1:             # frame-parallel: its own round
+            if self.ZSTD_MODE == 2:
+                # lane-parallel: a group of about one resident round of its
+                # entropy waves' blocks (config-5 buffers: 4 blocks each)
+                info = np.zeros(8, np.uint32)
+                N.lib().strom_zstd_lp_info(info.ctypes.data)
+                rnd = cus * int(info[2]) * int(info[1]) // 4
+            elif self.ZSTD_MODE == 1:             # frame-parallel: its own round
                 rnd = cus * max(1, int(N.lib().strom_zstd_fp_per_cu()))
             else:
                 rnd = cus * max(1, (160 << 10) // int(N.lib().strom_zstd_lds_bytes()))

@@ -26,6 +26,7 @@
 #   dist       multi-rank Arrow / PG scans: 1 rank (RCCL) and 2 gloo ranks (DIST_ARGS)
 #   overlap    load <-> side-stream collective overlap test + bench (both grid priorities)
 #   otrace     rocprofv3 kernel trace of overlap_bench + grid/side concurrency summary
+#   odtrace    the same with the zstd decoder as the side work (LDS co-residency)
 #   benchtests bench.py contract tests (tests/test_gpu_bench.py)
 #   ram        SSD2RAM (ssd2ram_test, 1 MiB units) vs the raw ceiling
 #   decprof    decoder cycle profile per code path (libstrom_decprof.so)
@@ -108,10 +109,18 @@ for phase in "$@"; do
             --master-port 29562 -m nvme_strom_amd.tools.dist_scan_bench ${DIST_ARGS:---rows 134217728} --reps 3 \
             --backend gloo --out "$OUT/dist2_gloo.json" ;;
     overlap) step otests 300 python -u -m pytest tests/test_gpu_overlap.py -m gpu -x -v --timeout 200 --timeout-method thread
-             step overlap 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 --gather-reps ${OV_REPS:-8} \
+             step overlap 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 --calibrate \
                --n 2,8 --out "$OUT/overlap.json"
+             step overlap_dec 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 512 --steps 6 --calibrate \
+               --side decode --n 2 --out "$OUT/overlap_dec.json"
              STROM_INGEST_PRIO=1 step overlap_prio 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 \
                --gather-reps ${OV_REPS:-8} --n 2,8 --out "$OUT/overlap_prio.json" ;;
+    odtrace) # the ingest grid next to the LDS-heavy zstd decoder: kernel trace + concurrency summary
+            (cd /tmp && step odtrace 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/odtrace" -o trace \
+              -- python3 -m nvme_strom_amd.tools.overlap_bench --side decode --calibrate --n 2 --modes overlap --window-mib 512 --steps 6 \
+                 --out "$OUT/odtrace.json") && \
+            python -m nvme_strom_amd.tools.overlap_trace $(find "$OUT/odtrace" -name '*kernel_trace.csv' | head -1) \
+              --side zstd --md "$OUT/odtrace_summary.md" ;;
     otrace) (cd /tmp && step otrace 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/otrace" -o trace \
               -- python3 -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 8 --gather-reps ${OV_REPS:-8} --n 8 --modes overlap) && \
             python -m nvme_strom_amd.tools.overlap_trace $(find "$OUT/otrace" -name '*kernel_trace.csv' | head -1) \
