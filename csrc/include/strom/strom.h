@@ -265,6 +265,30 @@ struct strom_heap_qual {
  * cannot decide it, the tuple is not emitted and its page is flagged
  * STROM_PAGE_RECHECK for the host to re-evaluate. */
 #define STROM_PAGE_RECHECK     8u
+#define STROM_QUAL_TEXT_IN      8  /* varlena bytes == one of nconst constants */
+#define STROM_QUAL_NUMERIC_RANGE 9 /* lo <= v <= hi, v a PostgreSQL numeric */
+#define STROM_QUAL2_FALSE 0x80   /* strom_heap_qual2.flags: the qual is constant false */
+/* A qualifier of a program (strom_heap_scan2_args.prog): quals with the
+ * same clause id are ORed and contiguous, clauses are ANDed (CNF); any
+ * number of either.  Constants live in a device pool:
+ *   TEXT_EQ / TEXT_PREFIX  nconst bytes at coff (any length)
+ *   INT_IN                 nconst int64 at coff (any count)
+ *   TEXT_IN                nconst (uint32 offset, uint32 length) at coff
+ *   NUMERIC_RANGE          constants at pool offsets lo and hi: uint16 kind
+ *                          (0 finite, 1 NaN, 2 +inf, 3 -inf), uint16 sign
+ *                          (0 / 1 negative), int16 weight, uint16 ndigits,
+ *                          int16 base-10000 digits (no leading / trailing 0s)
+ * flags (NUMERIC_RANGE): 1 no lower bound, 2 no upper bound, 4 lower
+ * strict, 8 upper strict. */
+struct strom_heap_qual2 {
+	int16_t attno;
+	uint8_t kind;
+	uint8_t flags;
+	uint32_t clause;
+	uint32_t nconst;
+	uint32_t coff;
+	int64_t lo, hi;
+};
 struct strom_heap_scan2_args {
 	struct strom_heap_scan_args base;     /* base.attr_off must be -1 */
 	struct strom_heap_tupdesc desc;
@@ -272,6 +296,11 @@ struct strom_heap_scan2_args {
 	                                         except for IS_NULL */
 	struct strom_heap_qual quals[STROM_HEAP_MAX_QUALS];
 	uint32_t *recheck_count;              /* device, optional: undecidable tuples */
+	/* program mode (prog != NULL; quals / nquals unused): nprog quals in
+	 * device memory, their constants in cpool (cpool_len bytes) */
+	const struct strom_heap_qual2 *prog;
+	const uint8_t *cpool;
+	uint32_t nprog, cpool_len;
 };
 int strom_heap_scan2(const struct strom_heap_scan2_args *a, void *stream);
 /* Projection of one attribute of the tuples `items` (page << 16 | lineno,
@@ -284,6 +313,13 @@ int strom_heap_project(const void *pages, uint32_t page_sz, const uint32_t *item
                        const uint32_t *d_count, uint32_t cap,
                        const struct strom_heap_tupdesc *desc, int attno, int as_float,
                        uint64_t *values, uint8_t *valid, void *stream);
+/* several attributes in one deform walk per tuple: values / valid are
+ * [ncol][cap], column j as float64 when bit j of float_mask is set */
+int strom_heap_project_n(const void *pages, uint32_t page_sz, const uint32_t *items,
+                         const uint32_t *d_count, uint32_t cap,
+                         const struct strom_heap_tupdesc *desc, const int32_t *attnos,
+                         uint32_t ncol, uint64_t float_mask, uint64_t *values, uint8_t *valid,
+                         void *stream);
 uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
                                 uint32_t page_sz);
 /* Per-tuple MVCC check of a heap page against a snapshot (xmin, xmax,

@@ -320,6 +320,216 @@ __device__ __forceinline__ int eval_quals(const strom_heap_scan2_args &g, const 
   return verdict;
 }
 
+// ---- qualifier programs (strom_heap_qual2): CNF over any number of quals,
+// constants in a device pool.  Three-valued like SQL's quals over values
+// the GPU cannot read (compressed / TOAST varlena): a clause with no true
+// qual and an undecidable one is undecidable; the tuple is dropped by a
+// false clause, else undecidable (page flagged for a host recheck) if any
+// clause is.
+__device__ __forceinline__ uint32_t pool_u32(const uint8_t *p, uint32_t o) {
+  return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) |
+         ((uint32_t)p[o + 3] << 24);
+}
+__device__ __forceinline__ uint32_t pool_u16(const uint8_t *p, uint32_t o) {
+  return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8);
+}
+
+// A PostgreSQL numeric (numeric.c on-disk: NumericShort / NumericLong /
+// special values) or a pool constant in the same normalized terms.
+struct Num {
+  uint32_t kind;     // 0 finite, 1 NaN, 2 +inf, 3 -inf
+  uint32_t neg;
+  int32_t weight;    // digits[0] x 10000^weight
+  uint32_t nd;       // digits
+  const uint8_t *dig;  // int16 little-endian base-10000 digits
+};
+
+__device__ __forceinline__ bool num_of_datum(const uint8_t *t, const Att &a, Num &n) {
+  const uint32_t len = a.len - a.hdr;
+  const uint8_t *d = t + a.off + a.hdr;
+  if (len < 2) return false;
+  const uint32_t h = (uint32_t)d[0] | ((uint32_t)d[1] << 8);
+  n.kind = 0;
+  n.neg = 0;
+  if ((h & 0xC000) == 0xC000) {               // NUMERIC_SPECIAL
+    const uint32_t sp = h & 0xF000;
+    n.kind = sp == 0xC000 ? 1 : sp == 0xD000 ? 2 : sp == 0xF000 ? 3 : 9;
+    n.nd = 0;
+    return n.kind != 9;
+  }
+  if ((h & 0xC000) == 0x8000) {               // NUMERIC_SHORT
+    n.neg = (h & 0x2000) != 0;
+    n.weight = (h & 0x0040) ? (int32_t)(h | ~0x3Fu) : (int32_t)(h & 0x3F);
+    n.nd = (len - 2) / 2;
+    n.dig = d + 2;
+    return ((len - 2) & 1) == 0;
+  }
+  if (len < 4) return false;                  // NumericLong
+  n.neg = (h & 0xC000) == 0x4000;
+  n.weight = (int16_t)((uint32_t)d[2] | ((uint32_t)d[3] << 8));
+  n.nd = (len - 4) / 2;
+  n.dig = d + 4;
+  return ((len - 4) & 1) == 0;
+}
+
+__device__ __forceinline__ Num num_of_pool(const uint8_t *p, uint32_t o) {
+  Num n;
+  n.kind = pool_u16(p, o);
+  n.neg = pool_u16(p, o + 2);
+  n.weight = (int16_t)pool_u16(p, o + 4);
+  n.nd = pool_u16(p, o + 6);
+  n.dig = p + o + 8;
+  return n;
+}
+
+__device__ __forceinline__ int32_t num_digit(const Num &n, uint32_t i) {
+  return (int16_t)((uint32_t)n.dig[2 * i] | ((uint32_t)n.dig[2 * i + 1] << 8));
+}
+
+// cmp_abs_common (numeric.c): |a| vs |b|
+__device__ __forceinline__ int num_cmp_abs(const Num &a, const Num &b) {
+  uint32_t i1 = 0, i2 = 0;
+  int32_t w1 = a.weight, w2 = b.weight;
+  while (w1 > w2 && i1 < a.nd) {
+    if (num_digit(a, i1++) != 0) return 1;
+    --w1;
+  }
+  while (w2 > w1 && i2 < b.nd) {
+    if (num_digit(b, i2++) != 0) return -1;
+    --w2;
+  }
+  if (w1 == w2) {
+    while (i1 < a.nd && i2 < b.nd) {
+      const int32_t d = num_digit(a, i1++) - num_digit(b, i2++);
+      if (d) return d > 0 ? 1 : -1;
+    }
+  }
+  while (i1 < a.nd)
+    if (num_digit(a, i1++) != 0) return 1;
+  while (i2 < b.nd)
+    if (num_digit(b, i2++) != 0) return -1;
+  return 0;
+}
+
+__device__ __forceinline__ bool num_zero(const Num &n) {
+  for (uint32_t i = 0; i < n.nd; ++i)
+    if (num_digit(n, i)) return false;
+  return true;
+}
+
+// cmp_numerics: NaN equals NaN and sorts above everything, +inf above every
+// finite value, -inf below; finite values by sign, then magnitude
+__device__ __forceinline__ int num_cmp(const Num &a, const Num &b) {
+  auto rank = [](const Num &n) { return n.kind == 1 ? 3 : n.kind == 2 ? 2 : n.kind == 3 ? 0 : 1; };
+  const int ra = rank(a), rb = rank(b);
+  if (ra != rb) return ra < rb ? -1 : 1;
+  if (ra != 1) return 0;
+  const bool za = num_zero(a), zb = num_zero(b);
+  if (za || zb) {
+    if (za && zb) return 0;
+    if (za) return b.neg ? 1 : -1;
+    return a.neg ? -1 : 1;
+  }
+  if (a.neg != b.neg) return a.neg ? -1 : 1;
+  const int m = num_cmp_abs(a, b);
+  return a.neg ? -m : m;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t *x, const uint8_t *y, uint32_t n) {
+  for (uint32_t k = 0; k < n; ++k)
+    if (x[k] != y[k]) return false;
+  return true;
+}
+
+// one qual of a program on attribute a: 1 true, 0 false, 2 undecidable
+__device__ __forceinline__ int eval_qual2(const strom_heap_qual2 &q, const uint8_t *pool,
+                                          const uint8_t *t, const Att &a) {
+  if (q.flags & STROM_QUAL2_FALSE) return 0;
+  if (q.kind == STROM_QUAL_IS_NULL) return a.null ? 1 : 0;
+  if (a.null) return 0;
+  switch (q.kind) {
+    case STROM_QUAL_NOT_NULL:
+      return 1;
+    case STROM_QUAL_INT_RANGE: {
+      const int64_t v = att_int(t, a);
+      return v >= q.lo && v <= q.hi;
+    }
+    case STROM_QUAL_INT_IN: {
+      const int64_t v = att_int(t, a);
+      for (uint32_t k = 0; k < q.nconst; ++k) {
+        const int64_t c = (int64_t)((uint64_t)pool_u32(pool, q.coff + 8 * k) |
+                                    ((uint64_t)pool_u32(pool, q.coff + 8 * k + 4) << 32));
+        if (v == c) return 1;
+      }
+      return 0;
+    }
+    case STROM_QUAL_FLOAT_RANGE: {
+      const double v = att_float(t, a);
+      return pg_le(__longlong_as_double(q.lo), v) && pg_le(v, __longlong_as_double(q.hi));
+    }
+    case STROM_QUAL_TEXT_EQ:
+    case STROM_QUAL_TEXT_PREFIX:
+    case STROM_QUAL_TEXT_IN: {
+      if (a.ext) return 2;
+      const uint32_t n = a.len - a.hdr;
+      const uint8_t *v = t + a.off + a.hdr;
+      if (q.kind == STROM_QUAL_TEXT_EQ) return n == q.nconst && bytes_eq(v, pool + q.coff, n);
+      if (q.kind == STROM_QUAL_TEXT_PREFIX) return n >= q.nconst && bytes_eq(v, pool + q.coff, q.nconst);
+      for (uint32_t k = 0; k < q.nconst; ++k) {
+        const uint32_t co = pool_u32(pool, q.coff + 8 * k), cl = pool_u32(pool, q.coff + 8 * k + 4);
+        if (n == cl && bytes_eq(v, pool + co, n)) return 1;
+      }
+      return 0;
+    }
+    case STROM_QUAL_NUMERIC_RANGE: {
+      if (a.ext) return 2;
+      Num v;
+      if (!num_of_datum(t, a, v)) return 0;
+      if (!(q.flags & 1)) {
+        const int c = num_cmp(v, num_of_pool(pool, (uint32_t)q.lo));
+        if (c < 0 || (c == 0 && (q.flags & 4))) return 0;
+      }
+      if (!(q.flags & 2)) {
+        const int c = num_cmp(v, num_of_pool(pool, (uint32_t)q.hi));
+        if (c > 0 || (c == 0 && (q.flags & 8))) return 0;
+      }
+      return 1;
+    }
+    default:
+      return 0;
+  }
+}
+
+// the program over one tuple: 1 keep, 0 drop, 2 undecidable
+__device__ __forceinline__ int eval_prog(const strom_heap_scan2_args &g, const uint8_t *t,
+                                         uint32_t tlen) {
+  Deform s = deform_init(t, tlen);
+  Att a;
+  int last = -1;
+  int verdict = 1;
+  uint32_t qi = 0;
+  while (qi < g.nprog) {
+    const uint32_t cl = g.prog[qi].clause;
+    int cv = 0;                                 // the clause: 0 false, 1 true, 2 unknown
+    for (; qi < g.nprog && g.prog[qi].clause == cl; ++qi) {
+      if (cv == 1) continue;                     // decided: skip the clause's rest
+      const strom_heap_qual2 &q = g.prog[qi];
+      if (q.attno != last) {
+        if ((uint32_t)q.attno < s.next) s = deform_init(t, tlen);   // walk again from the start
+        a = deform_to(g.desc, s, (uint32_t)q.attno);
+        last = q.attno;
+      }
+      if (s.bad) return 0;
+      const int r = eval_qual2(q, g.cpool, t, a);
+      if (r == 1) cv = 1;
+      else if (r == 2) cv = 2;
+    }
+    if (cv == 0) return 0;
+    if (cv == 2) verdict = 2;
+  }
+  return verdict;
+}
+
 // 1 keep, 0 drop, 2 undecidable (GEN: a text qual met a compressed value)
 template <bool GEN>
 __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const uint8_t *pg,
@@ -336,7 +546,7 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
     if (!(infomask & kXminCommitted)) return false;
     if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return false;
   }
-  if (GEN) return g.nquals ? eval_quals(g, pg + off, len) : 1;
+  if (GEN) return g.prog ? eval_prog(g, pg + off, len) : g.nquals ? eval_quals(g, pg + off, len) : 1;
   if (a.attr_off < 0) return true;
   const uint32_t at = hoff + (uint32_t)a.attr_off;
   if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return false;
@@ -511,30 +721,45 @@ int heap_scan_launch(const strom_heap_scan2_args &g, bool gen, void *stream) {
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-// one thread per selected item: deform its tuple from the page in HBM
+// the projected columns: ascending attribute numbers, each with its output
+// column (values / valid are [ncol][cap]) and float flag
+struct ProjSpec {
+  uint32_t n;
+  uint64_t fmask;                               // bit j: column j as float64
+  uint8_t att[STROM_HEAP_MAX_ATTS], slot[STROM_HEAP_MAX_ATTS];
+};
+
+// one thread per selected item: deform its tuple once from the page in HBM,
+// every projected attribute on the way
 __global__ __launch_bounds__(256) void heap_project_kernel(const uint8_t *pages, uint32_t page_sz,
                                                            const uint32_t *items, const uint32_t *d_count,
                                                            uint32_t cap, strom_heap_tupdesc desc,
-                                                           uint32_t attno, int as_float,
-                                                           uint64_t *values, uint8_t *valid) {
+                                                           ProjSpec ps, uint64_t *values, uint8_t *valid) {
   const uint32_t n = min(*d_count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t it = items[i], pg = it >> 16, lineno = it & 0xffff;
     const uint8_t *page = pages + (uint64_t)pg * page_sz;
-    uint64_t v = 0;
-    uint8_t ok = 0;
     const uint32_t lower = lds_u32a(page, 12) & 0xffff;
+    bool tup = false;
+    uint32_t off = 0, len = 0;
     if (lineno >= 1 && kSizeOfPageHeader + 4 * lineno <= lower) {
       const uint32_t lp = lds_u32a(page, kSizeOfPageHeader + 4 * (lineno - 1));
-      const uint32_t off = lp & 0x7fff, len = lp >> 17;
-      if (len >= 23 && off >= kSizeOfPageHeader && off + len <= page_sz && !(off & 1)) {
-        Deform s = deform_init(page + off, len);
+      off = lp & 0x7fff;
+      len = lp >> 17;
+      tup = len >= 23 && off >= kSizeOfPageHeader && off + len <= page_sz && !(off & 1);
+    }
+    Deform s = deform_init(page + off, tup ? len : 0);
+    for (uint32_t j = 0; j < ps.n; ++j) {
+      const uint32_t attno = ps.att[j], slot = ps.slot[j];
+      uint64_t v = 0;
+      uint8_t ok = 0;
+      if (tup) {
         const Att a = deform_to(desc, s, attno);
         if (!s.bad && !a.null) {
           if (desc.attlen[attno] < 0) {   // varlena / cstring: where its bytes are
             v = ((uint64_t)((uint64_t)pg * page_sz + off + a.off + a.hdr) << 32) | (a.len - a.hdr);
             ok = a.ext ? 2 : 1;
-          } else if (as_float) {
+          } else if ((ps.fmask >> slot) & 1) {
             v = (uint64_t)__double_as_longlong(att_float(page + off, a));
             ok = 1;
           } else {
@@ -543,9 +768,9 @@ __global__ __launch_bounds__(256) void heap_project_kernel(const uint8_t *pages,
           }
         }
       }
+      values[(size_t)slot * cap + i] = v;
+      if (valid) valid[(size_t)slot * cap + i] = ok;
     }
-    values[i] = v;
-    if (valid) valid[i] = ok;
   }
 }
 
@@ -559,14 +784,66 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   return heap_scan_launch(g, false, stream);
 }
 
+// host-side check of a program (a copy in host memory, as uploaded): every
+// qual's kind fits its attribute, constants inside the pool, clauses contiguous
+extern "C" int strom_heap_prog_check(const strom_heap_tupdesc *d, const strom_heap_qual2 *prog,
+                                     uint32_t n, uint32_t pool_len) {
+  uint32_t seen_last = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const strom_heap_qual2 &x = prog[i];
+    if (x.attno < 0 || x.attno >= d->natts) return -22;
+    if (i && x.clause != prog[i - 1].clause) {
+      for (uint32_t j = 0; j < i; ++j)       // a clause id may not come back
+        if (prog[j].clause == x.clause) return -22;
+    }
+    seen_last = x.clause;
+    const int len = d->attlen[x.attno];
+    const uint64_t end = (uint64_t)x.coff;
+    switch (x.kind) {
+      case STROM_QUAL_INT_RANGE:
+        if (len != 1 && len != 2 && len != 4 && len != 8) return -22;
+        break;
+      case STROM_QUAL_INT_IN:
+        if (len != 1 && len != 2 && len != 4 && len != 8) return -22;
+        if (end + 8ull * x.nconst > pool_len) return -22;
+        break;
+      case STROM_QUAL_FLOAT_RANGE:
+        if (len != 4 && len != 8) return -22;
+        break;
+      case STROM_QUAL_TEXT_EQ:
+      case STROM_QUAL_TEXT_PREFIX:
+        if (len != -1 || end + x.nconst > pool_len) return -22;
+        break;
+      case STROM_QUAL_TEXT_IN:
+        if (len != -1 || end + 8ull * x.nconst > pool_len) return -22;
+        break;
+      case STROM_QUAL_NUMERIC_RANGE:
+        if (len != -1) return -22;
+        if (!(x.flags & 1) && ((uint64_t)x.lo + 8 > pool_len || x.lo < 0)) return -22;
+        if (!(x.flags & 2) && ((uint64_t)x.hi + 8 > pool_len || x.hi < 0)) return -22;
+        break;
+      case STROM_QUAL_IS_NULL:
+      case STROM_QUAL_NOT_NULL:
+        break;
+      default:
+        return -22;
+    }
+  }
+  (void)seen_last;
+  return 0;
+}
+
 extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   if (!g || g->base.attr_off >= 0) return -22;
-  if (g->nquals < 0 || g->nquals > STROM_HEAP_MAX_QUALS) return -22;
   if (g->desc.natts < 1 || g->desc.natts > STROM_HEAP_MAX_ATTS) return -22;
   for (int i = 0; i < g->desc.natts; ++i) {
     const int al = g->desc.attalign[i], len = g->desc.attlen[i];
     if ((al != 1 && al != 2 && al != 4 && al != 8) || len == 0 || len < -2) return -22;
   }
+  // a program was checked by the caller against its host copy
+  // (strom_heap_prog_check); it lives in device memory here
+  if (g->prog) return heap_scan_launch(*g, true, stream);
+  if (g->nquals < 0 || g->nquals > STROM_HEAP_MAX_QUALS) return -22;
   int last = -1;
   for (int q = 0; q < g->nquals; ++q) {
     const strom_heap_qual &x = g->quals[q];
@@ -596,19 +873,48 @@ extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   return heap_scan_launch(*g, true, stream);
 }
 
+extern "C" int strom_heap_project_n(const void *pages, uint32_t page_sz, const uint32_t *items,
+                                    const uint32_t *d_count, uint32_t cap,
+                                    const strom_heap_tupdesc *desc, const int32_t *attnos,
+                                    uint32_t ncol, uint64_t float_mask, uint64_t *values,
+                                    uint8_t *valid, void *stream) {
+  if (!pages || !items || !d_count || !desc || !values || !attnos) return -22;
+  if (desc->natts < 1 || desc->natts > STROM_HEAP_MAX_ATTS) return -22;
+  if (ncol < 1 || ncol > STROM_HEAP_MAX_ATTS) return -22;
+  if (page_sz < 1024 || (page_sz & 1023) || page_sz > 32768) return -22;
+  ProjSpec ps;
+  __builtin_memset(&ps, 0, sizeof ps);
+  ps.n = ncol;
+  ps.fmask = float_mask;
+  for (uint32_t j = 0; j < ncol; ++j) {
+    const int32_t k = attnos[j];
+    if (k < 0 || k >= desc->natts) return -22;
+    const int len = desc->attlen[k];
+    if (((float_mask >> j) & 1) && len != 4 && len != 8) return -22;
+    ps.att[j] = (uint8_t)k;
+    ps.slot[j] = (uint8_t)j;
+  }
+  // ascending attributes: one forward deform walk per tuple
+  for (uint32_t j = 1; j < ncol; ++j)
+    for (uint32_t i = j; i > 0 && ps.att[i - 1] > ps.att[i]; --i) {
+      std::swap(ps.att[i - 1], ps.att[i]);
+      std::swap(ps.slot[i - 1], ps.slot[i]);
+    }
+  for (uint32_t j = 1; j < ncol; ++j)
+    if (ps.att[j] == ps.att[j - 1]) return -22;
+  if (cap == 0) return 0;
+  const uint32_t grid = std::min<uint32_t>((cap + 255) / 256, 4096);
+  hipLaunchKernelGGL(heap_project_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t *)pages, page_sz, items, d_count, cap, *desc, ps, values, valid);
+  return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
 extern "C" int strom_heap_project(const void *pages, uint32_t page_sz, const uint32_t *items,
                                   const uint32_t *d_count, uint32_t cap,
                                   const strom_heap_tupdesc *desc, int attno, int as_float,
                                   uint64_t *values, uint8_t *valid, void *stream) {
-  if (!pages || !items || !d_count || !desc || !values) return -22;
-  if (attno < 0 || attno >= desc->natts || desc->natts > STROM_HEAP_MAX_ATTS) return -22;
-  if (page_sz < 1024 || (page_sz & 1023) || page_sz > 32768) return -22;
-  const int len = desc->attlen[attno];
-  if (as_float && len != 4 && len != 8) return -22;
-  if (cap == 0) return 0;
-  const uint32_t grid = std::min<uint32_t>((cap + 255) / 256, 4096);
-  hipLaunchKernelGGL(heap_project_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                     (const uint8_t *)pages, page_sz, items, d_count, cap, *desc, (uint32_t)attno,
-                     as_float, values, valid);
-  return hipGetLastError() == hipSuccess ? 0 : -5;
+  if (!desc) return -22;
+  const int32_t k = attno;
+  return strom_heap_project_n(pages, page_sz, items, d_count, cap, desc, &k, 1, as_float ? 1 : 0,
+                              values, valid, stream);
 }

@@ -158,9 +158,18 @@ class HeapQual(C.Structure):
                 ("cbytes", C.c_uint8 * 32)]
 
 
+class HeapQual2(C.Structure):
+    """strom_heap_qual2: one qualifier of a CNF program (constants in a pool)."""
+    _fields_ = [("attno", C.c_int16), ("kind", C.c_uint8), ("flags", C.c_uint8),
+                ("clause", C.c_uint32), ("nconst", C.c_uint32), ("coff", C.c_uint32),
+                ("lo", C.c_int64), ("hi", C.c_int64)]
+
+
 class HeapScan2Args(C.Structure):
     _fields_ = [("base", HeapScanArgs), ("desc", HeapTupDesc), ("nquals", C.c_int32),
-                ("quals", HeapQual * HEAP_MAX_QUALS), ("recheck_count", C.c_void_p)]
+                ("quals", HeapQual * HEAP_MAX_QUALS), ("recheck_count", C.c_void_p),
+                ("prog", C.c_void_p), ("cpool", C.c_void_p), ("nprog", C.c_uint32),
+                ("cpool_len", C.c_uint32)]
 
 
 class DecompDesc(C.Structure):
@@ -242,9 +251,14 @@ _SIGS = {
     "strom_fill_pattern": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     "strom_heap_scan": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p]),
     "strom_heap_scan2": (C.c_int, [C.POINTER(HeapScan2Args), C.c_void_p]),
+    "strom_heap_prog_check": (C.c_int, [C.POINTER(HeapTupDesc), C.c_void_p, C.c_uint32,
+                                        C.c_uint32]),
     "strom_heap_project": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.POINTER(HeapTupDesc), C.c_int, C.c_int, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
+    "strom_heap_project_n": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.POINTER(HeapTupDesc), C.c_void_p, C.c_uint32,
+                                       C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
     "strom_decompress": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                    C.c_void_p, C.c_void_p]),
     "strom_column_filter": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_double,

@@ -45,9 +45,9 @@ import numpy as np
 import torch
 
 from .. import api
-from ..ops.heapscan import PAGE_RECHECK, heap_project, heap_scan, heap_scan2
+from ..ops.heapscan import PAGE_RECHECK, Program, heap_project_many, heap_scan, heap_scan2
 from ..tensor import FileReader, HbmBuffer, host_buffer
-from ..utils import pgmvcc, pgpage
+from ..utils import pgmvcc, pgpage, pgtuple
 from ..utils.pgmvcc import CommitLog, MultiXact, Snapshot, SubTrans
 
 BLCKSZ = 8192
@@ -337,6 +337,9 @@ class ScanResult:
     # blocks holding tuples a text qualifier could not decide on the GPU
     # (compressed / TOAST values): the executor re-evaluates those blocks
     recheck_blocks: List[int] = field(default_factory=list)
+    # every projected column: {name: (values, valid)} as values / valid
+    # (a numeric column's values are decimal.Decimal)
+    columns: Dict[str, tuple] = field(default_factory=dict)
 
     @property
     def ntuples(self) -> int:
@@ -389,9 +392,10 @@ class HeapRelationScan:
                  hi: int = (1 << 63) - 1, desc=None, quals=None, project=None):
         """``attr_off``..``hi``: the fixed-offset int predicate of the round-1
         kernel.  ``desc`` (utils.pgtuple.TupleDesc) + ``quals`` (a list of
-        pgtuple.Qual, ANDed) + optional ``project`` column: every tuple is
-        deformed on the GPU and the qualifier list evaluated there, as the
-        reference's ExecScan does on the CPU (pgsql/nvme_strom.c:1137-1143)."""
+        pgtuple.Qual, ANDed, and pgtuple.Or clauses: CNF) + optional
+        ``project`` column or list of columns: every tuple is deformed on the
+        GPU and the qualifier list evaluated there, as the reference's
+        ExecScan does on the CPU (pgsql/nvme_strom.c:1137-1143)."""
         self.rel = rel
         self.cfg = cfg or ScanConfig()
         self.cfg.validate()
@@ -402,6 +406,10 @@ class HeapRelationScan:
         if desc is not None and attr_off >= 0:
             raise ValueError("a fixed-offset predicate and a qualifier list are exclusive")
         self.desc, self.quals, self.project = desc, list(quals or []), project
+        self._cols = ([] if project is None else [project] if isinstance(project, (str, int))
+                      else list(project))
+        # compiled once per scan object (checked and uploaded per chunk)
+        self._prog = Program(desc, self.quals) if desc is not None else None
         # idle participant resources (session, HBM ring, readers, pinned
         # write-back buffers), reused by later runs: allocating and pinning
         # them per run cost more than the scan of a GiB-sized relation.
@@ -505,14 +513,19 @@ class HeapRelationScan:
         chunks = sorted((c for r in results for c in r.chunk_items), key=lambda c: c[0])
         items = np.concatenate([c[1] for c in chunks]) if chunks else np.zeros(0, np.uint64)
         out = ScanResult(items, seconds=time.perf_counter() - t0, workers=workers)
-        if self.project is not None:
-            vals = [c[2] for c in chunks]
-            if vals and isinstance(vals[0], list):
-                out.values = [v for part in vals for v in part]
+        for j, col in enumerate(self._cols):
+            vals = [c[2][j] for c in chunks]
+            if not vals:
+                values = [] if self.desc.attlen[self.desc.attno(col)] < 0 else np.zeros(0)
+            elif isinstance(vals[0], list):
+                values = [v for part in vals for v in part]
             else:
-                out.values = np.concatenate(vals) if vals else np.zeros(0)
-            out.valid = (np.concatenate([c[3] for c in chunks]) if chunks
-                         else np.zeros(0, np.uint8))
+                values = np.concatenate(vals)
+            valid = (np.concatenate([c[3][j] for c in chunks]) if chunks
+                     else np.zeros(0, np.uint8))
+            out.columns[col] = (values, valid)
+        if self._cols and not isinstance(self.project, (list, tuple)):
+            out.values, out.valid = out.columns[self._cols[0]]
         out.merge(results)
         return out
 
@@ -599,7 +612,7 @@ class HeapRelationScan:
         skip = self.cfg.skip_invisible and self.cfg.snapshot is None
         general = self.desc is not None
         if general:
-            r = heap_scan2(pages, self.desc, self.quals, BLCKSZ,
+            r = heap_scan2(pages, self.desc, self._prog, BLCKSZ,
                            verify_checksum=self.cfg.verify_checksum, skip_invisible=skip,
                            blknos=blk)
         else:
@@ -614,23 +627,30 @@ class HeapRelationScan:
         lineno = (it & 0xFFFF).astype(np.uint64)
         blocks = landed.astype(np.uint64)[page_idx]
         ptrs = (blocks << np.uint64(16)) | lineno
-        vals = valid = None
-        if general and self.project is not None:
+        vals, valid = [], []
+        if general and self._cols:
+            # every projected column in one deform walk per tuple
             cnt = torch.tensor([r.count], dtype=torch.int32, device=pages.device)
-            v, ok = heap_project(pages, r.items, cnt, self.desc, self.project, BLCKSZ,
-                                 cap=max(r.count, 1))
-            v, ok = v[:r.count][perm], ok[:r.count][perm]
-            valid = ok.cpu().numpy()
-            if self.desc.attlen[self.desc.attno(self.project)] < 0:
-                vals = _gather_varlena(pages, v, ok)
-            else:
-                vals = v.cpu().numpy()
+            got = heap_project_many(pages, r.items, cnt, self.desc, self._cols, BLCKSZ,
+                                    cap=max(r.count, 1))
+            for col in self._cols:
+                v, ok = got[col]
+                v, ok = v[:r.count][perm], ok[:r.count][perm]
+                valid.append(ok.cpu().numpy())
+                k = self.desc.attno(col)
+                if self.desc.attlen[k] < 0:
+                    b = _gather_varlena(pages, v, ok)
+                    if self.desc.kinds[k] == "numeric":
+                        b = [pgtuple.numeric_value(x) if f == 1 else x
+                             for x, f in zip(b, valid[-1].tolist())]
+                    vals.append(b)
+                else:
+                    vals.append(v.cpu().numpy())
         if n > 1 and bool((landed[1:] < landed[:-1]).any()):
             o = np.argsort(ptrs, kind="stable")  # page-cache chunks landed at the tail
             ptrs = ptrs[o]
-            if valid is not None:
-                valid = valid[o]
-                vals = [vals[j] for j in o] if isinstance(vals, list) else vals[o]
+            valid = [x[o] for x in valid]
+            vals = [[x[j] for j in o] if isinstance(x, list) else x[o] for x in vals]
         found.append((int(landed.min()) if n else 0, ptrs, vals, valid))
         status = r.page_status.cpu().numpy()
         if general:
@@ -680,10 +700,11 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
     """Reference-shaped path: SSD2RAM into a NUMA DMA buffer, host tuple walk
     (with ``desc`` / ``quals`` / ``project``: the host deformer,
     utils.pgtuple.host_scan2)."""
-    from ..utils import pgtuple
     cfg = cfg or ScanConfig()
     general = desc is not None
-    vals_out, valid_out = [], []
+    cols = [] if project is None else [project] if isinstance(project, (str, int)) else list(project)
+    vals_out = [[] for _ in cols]
+    valid_out = [[] for _ in cols]
 
     def walk(raw, blkno):
         """(item ids, statuses) of pages ``raw`` starting at block ``blkno``"""
@@ -691,12 +712,11 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
             return pgpage.host_scan(raw, BLCKSZ, skip, attr_off, attr_width, lo, hi,
                                     cfg.verify_checksum, blkno)
         its, stt, pv = pgtuple.host_scan2(raw, desc, quals or [], BLCKSZ, skip,
-                                          cfg.verify_checksum, blkno, project)
-        if project is not None:
-            k = desc.attno(project)
-            for v in pv:
-                valid_out.append(0 if v is None else 2 if v is pgtuple.EXT else 1)
-                vals_out.append(b"" if v is None or v is pgtuple.EXT else v)
+                                          cfg.verify_checksum, blkno, cols or None)
+        for row in pv if cols else ():
+            for j, v in enumerate(row):
+                valid_out[j].append(0 if v is None else 2 if v is pgtuple.EXT else 1)
+                vals_out[j].append(b"" if v is None or v is pgtuple.EXT else v)
         for j, x in enumerate(stt):
             if x & pgtuple.PAGE_RECHECK:
                 st.recheck_blocks.append(blkno + j)
@@ -760,14 +780,17 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                 os.close(fd)
     order = np.argsort(np.array(items, dtype=np.uint64), kind="stable")
     st.items = np.array(items, dtype=np.uint64)[order]
-    if general and project is not None:
-        k = desc.attno(project)
-        st.valid = np.array(valid_out, dtype=np.uint8)[order]
+    for j, col in enumerate(cols if general else ()):
+        k = desc.attno(col)
+        valid = np.array(valid_out[j], dtype=np.uint8)[order]
         if desc.attlen[k] < 0:
-            st.values = [vals_out[j] for j in order]
+            values = [vals_out[j][i] for i in order]
         else:
             dt = np.float64 if desc.kinds[k] == "float" else np.int64
-            st.values = np.array([0 if isinstance(v, bytes) else v for v in vals_out], dtype=dt)[order]
+            values = np.array([0 if isinstance(v, bytes) else v for v in vals_out[j]], dtype=dt)[order]
+        st.columns[col] = (values, valid)
+    if cols and not isinstance(project, (list, tuple)):
+        st.values, st.valid = st.columns[cols[0]]
     st.recheck_blocks.sort()
     st.seconds = time.perf_counter() - t0
     return st

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import struct
 from dataclasses import dataclass
 from typing import Optional
 
@@ -72,8 +73,10 @@ def tupdesc_struct(desc) -> N.HeapTupDesc:
 
 
 def qual_structs(desc, quals) -> list:
-    """ctypes strom_heap_qual list (sorted by attribute) of pgtuple.Qual."""
-    import struct
+    """ctypes strom_heap_qual list (sorted by attribute) of pgtuple.Qual:
+    the fixed-size form (<= 8 ANDed quals, <= 32 constant bytes); heap_scan2
+    compiles a Program instead."""
+    import math
     out = []
     for q in quals:
         k = desc.attno(q.col)
@@ -92,11 +95,12 @@ def qual_structs(desc, quals) -> list:
                 s.hi = struct.unpack("<q", struct.pack("<d", float(args[1])))[0]
             elif kind == "int":
                 s.kind = 1
-                s.lo, s.hi = int(args[0]), int(args[1])
+                # exact: a fractional lower bound rounds up, an upper one down
+                s.lo, s.hi = math.ceil(_exact(args[0])), math.floor(_exact(args[1]))
             else:
                 raise ValueError(f"range qual on a {desc.types[k]} column")
         elif op == "in":
-            vals = [int(v) for v in args[0]]
+            vals = [int(v) for v in args[0] if _exact(v) == int(_exact(v))]
             if kind != "int" or len(vals) > 4:
                 raise ValueError("IN lists take up to 4 values of an int column")
             s.kind, s.nconst = 7, len(vals)
@@ -117,6 +121,182 @@ def qual_structs(desc, quals) -> list:
     return out
 
 
+QUAL_TEXT_IN, QUAL_NUMERIC_RANGE = 8, 9
+QUAL2_FALSE = 0x80
+_INT_LIMITS = {1: (-(1 << 7), (1 << 7) - 1), 2: (-(1 << 15), (1 << 15) - 1),
+               4: (-(1 << 31), (1 << 31) - 1), 8: (-(1 << 63), (1 << 63) - 1)}
+
+
+class Program:
+    """A qualifier list compiled for strom_heap_scan2's program mode: one
+    strom_heap_qual2 per leaf qualifier, clause ids for the CNF (a ``Qual``
+    is a clause of its own, an ``Or`` one clause of several), and the
+    constant pool (IN lists and text of any size, numeric constants)."""
+
+    def __init__(self, desc, quals):
+        import math
+        from ..utils import pgtuple as T
+        self.pool = bytearray()
+        self.quals: list = []
+
+        def const(b: bytes) -> int:
+            while len(self.pool) % 8:
+                self.pool.append(0)
+            o = len(self.pool)
+            self.pool += b
+            return o
+
+        def num_const(v) -> int:
+            kind, neg, weight, digits, _ = T.numeric_parts(v)
+            return const(struct.pack("<HHhH", kind, neg, weight, len(digits)) +
+                         struct.pack(f"<{len(digits)}h", *digits))
+
+        def emit(k, kind, clause, nconst=0, coff=0, lo=0, hi=0, flags=0):
+            q = N.HeapQual2()
+            q.attno, q.kind, q.flags, q.clause = k, kind, flags, clause
+            q.nconst, q.coff, q.lo, q.hi = nconst, coff, lo, hi
+            self.quals.append(q)
+
+        def never(k, clause):
+            # a constant-false qual (false for NULLs and unreadable values too)
+            emit(k, 4, clause, flags=QUAL2_FALSE)
+
+        for ci, clause in enumerate(T.clauses(quals)):
+            for q in clause:
+                k = desc.attno(q.col)
+                kind, L = desc.kinds[k], desc.attlen[k]
+                op, args = q.op, q.args
+                if op == "isnull":
+                    emit(k, 3, ci)
+                elif op == "notnull":
+                    emit(k, 4, ci)
+                elif op in ("text_eq", "prefix", "text_in"):
+                    if L != -1 or kind not in ("text",):
+                        raise ValueError(f"{op} on a {desc.types[k]} column")
+                    if op == "text_in":
+                        vals = [T._b(c) for c in args[0]]
+                        offs = [const(v) for v in vals]
+                        table = b"".join(struct.pack("<II", o, len(v)) for o, v in zip(offs, vals))
+                        emit(k, QUAL_TEXT_IN, ci, nconst=len(vals), coff=const(table))
+                    else:
+                        c = T._b(args[0])
+                        emit(k, 5 if op == "text_eq" else 6, ci, nconst=len(c), coff=const(c))
+                elif kind == "numeric":
+                    if op == "in":
+                        for c in args[0]:
+                            o = num_const(c)
+                            emit(k, QUAL_NUMERIC_RANGE, ci, lo=o, hi=o)
+                        if not args[0]:
+                            never(k, ci)
+                        continue
+                    lo = hi = None
+                    flags = 0
+                    if op == "between":
+                        lo, hi = args
+                    elif op == "eq":
+                        lo = hi = args[0]
+                    elif op in ("lt", "le"):
+                        hi = args[0]
+                        flags |= 1 | (8 if op == "lt" else 0)
+                    elif op in ("gt", "ge"):
+                        lo = args[0]
+                        flags |= 2 | (4 if op == "gt" else 0)
+                    else:
+                        raise ValueError(f"{op} on a numeric column")
+                    emit(k, QUAL_NUMERIC_RANGE, ci, flags=flags,
+                         lo=num_const(lo) if lo is not None else 0,
+                         hi=num_const(hi) if hi is not None else 0)
+                elif kind == "float":
+                    if op == "in":
+                        for c in args[0]:
+                            emit(k, 2, ci, lo=_fbits(c), hi=_fbits(c))
+                        if not args[0]:
+                            never(k, ci)
+                        continue
+                    lo, hi = -math.inf, math.inf
+                    if op == "between":
+                        lo, hi = float(args[0]), float(args[1])
+                    elif op == "eq":
+                        lo = hi = float(args[0])
+                    elif op == "le":
+                        hi = float(args[0])
+                    elif op == "lt":
+                        hi = math.nextafter(float(args[0]), -math.inf)
+                    elif op == "ge":
+                        lo = float(args[0])
+                    elif op == "gt":
+                        lo = math.nextafter(float(args[0]), math.inf)
+                    else:
+                        raise ValueError(f"{op} on a float column")
+                    emit(k, 2, ci, lo=_fbits(lo), hi=_fbits(hi))
+                elif kind == "int" and L in _INT_LIMITS:
+                    tmin, tmax = _INT_LIMITS[L]
+                    if op == "in":
+                        vals = sorted({int(c) for c in args[0]
+                                       if _exact(c) == int(_exact(c)) and tmin <= int(c) <= tmax})
+                        if not vals:
+                            never(k, ci)
+                            continue
+                        emit(k, 7, ci, nconst=len(vals),
+                             coff=const(struct.pack(f"<{len(vals)}q", *vals)))
+                        continue
+                    # exact bounds on the integers: a fractional lower bound
+                    # rounds up, an upper one down; clamped to the type
+                    lo, hi = tmin, tmax
+                    d = _exact
+                    if op == "between":
+                        lo, hi = math.ceil(d(args[0])), math.floor(d(args[1]))
+                    elif op == "eq":
+                        lo, hi = math.ceil(d(args[0])), math.floor(d(args[0]))
+                    elif op == "le":
+                        hi = math.floor(d(args[0]))
+                    elif op == "lt":
+                        hi = math.ceil(d(args[0])) - 1
+                    elif op == "ge":
+                        lo = math.ceil(d(args[0]))
+                    elif op == "gt":
+                        lo = math.floor(d(args[0])) + 1
+                    else:
+                        raise ValueError(f"{op} on an int column")
+                    lo, hi = max(lo, tmin), min(hi, tmax)
+                    if lo > hi:
+                        never(k, ci)
+                    else:
+                        emit(k, 1, ci, lo=lo, hi=hi)
+                else:
+                    raise ValueError(f"{op} on a {desc.types[k]} column")
+        # clauses by their first attribute, quals by attribute inside a
+        # clause: the device deforms each tuple forward, walking again from
+        # the start only when a clause goes back to an earlier attribute
+        groups: dict = {}
+        for q in self.quals:
+            groups.setdefault(q.clause, []).append(q)
+        order = sorted(groups.values(), key=lambda g: min(q.attno for q in g))
+        self.quals = []
+        for ci, g in enumerate(order):
+            for q in sorted(g, key=lambda q: q.attno):
+                q.clause = ci
+                self.quals.append(q)
+        if not self.pool:
+            self.pool = bytearray(8)
+
+    def arrays(self):
+        """(program bytes, pool bytes) for upload."""
+        raw = b"".join(bytes(q) for q in self.quals)
+        return raw, bytes(self.pool)
+
+
+def _exact(x):
+    """The exact value of an int / float / Decimal constant (a float's binary
+    value, as Python's int-vs-float comparisons use)."""
+    from decimal import Decimal
+    return x if isinstance(x, Decimal) else Decimal(x)
+
+
+def _fbits(x: float) -> int:
+    return struct.unpack("<q", struct.pack("<d", float(x)))[0]
+
+
 @dataclass
 class HeapScan2Result(HeapScanResult):
     recheck: int = 0                     # undecidable tuples (pages flagged PAGE_RECHECK)
@@ -128,7 +308,8 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
                blknos: Optional[torch.Tensor] = None, stream=None,
                sync: bool = True) -> HeapScan2Result:
     """Scan ``pages`` deforming every tuple with ``desc`` (utils.pgtuple) and
-    keeping the ones that pass every qualifier of ``quals`` (ANDed).
+    keeping the ones ``quals`` selects: a list of ``pgtuple.Qual`` (ANDed)
+    and ``pgtuple.Or`` clauses (CNF), or a compiled ``Program``.
     ``sync=False`` leaves ``count`` / ``recheck`` as device tensors (no host
     read)."""
     require_cuda(pages, "pages")
@@ -149,10 +330,26 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
                             page_status=ptr(status), blkno_base=blkno_base,
                             blknos=ptr(blknos) if blknos is not None else None)
     g.desc = tupdesc_struct(desc)
-    qs = qual_structs(desc, quals)
-    g.nquals = len(qs)
-    for i, q in enumerate(qs):
-        g.quals[i] = q
+    # the qualifier list as a program (CNF, any number of quals and
+    # constants) in device memory, checked on its host copy first
+    prog = quals if isinstance(quals, Program) else Program(desc, quals)
+    raw, pool = prog.arrays()
+    if prog.quals:
+        hp = np.frombuffer(raw, np.uint8)
+        check(lib().strom_heap_prog_check(C.byref(g.desc), hp.ctypes.data, len(prog.quals),
+                                          len(pool)), "heap_scan2 program")
+        # uploaded on the scan's stream (ordered before the kernel; their
+        # memory is reused only after it), and kept by the result
+        ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.current_stream(dev)
+        with torch.cuda.stream(ts):
+            d_prog = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+            d_pool = torch.frombuffer(bytearray(pool), dtype=torch.uint8).to(dev)
+        g.prog, g.cpool = ptr(d_prog), ptr(d_pool)
+        g.nprog, g.cpool_len = len(prog.quals), len(pool)
+        keep = [d_prog, d_pool]
+    else:
+        keep = []
+    g.nquals = 0
     g.recheck_count = ptr(cnt) + 4
     if npages:
         cnt[1].zero_()
@@ -160,6 +357,7 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
     if not sync:
         r = HeapScan2Result(items, cnt[0:1], status[:npages])
         r.recheck = cnt[1:2]
+        r.keep = keep
         return r
     c = cnt.cpu().tolist()
     r = HeapScan2Result(items, min(c[0], cap), status[:npages])
@@ -187,3 +385,30 @@ def heap_project(pages: torch.Tensor, items: torch.Tensor, count: torch.Tensor, 
     if as_float:
         vals = vals.view(torch.float64)
     return vals[:n], valid[:n]
+
+
+def heap_project_many(pages: torch.Tensor, items: torch.Tensor, count: torch.Tensor, desc, cols,
+                      page_sz: int = 8192, cap: Optional[int] = None, stream=None) -> dict:
+    """Several attributes of the tuples ``items`` names, in one deform walk
+    per tuple: {column: (values, valid)} as heap_project returns them."""
+    require_cuda(pages, "pages")
+    cols = list(cols)
+    ks = [desc.attno(c) for c in cols]
+    if len(set(ks)) != len(ks):
+        raise ValueError("a column is projected twice")
+    n = int(cap if cap is not None else items.numel())
+    dev = pages.device
+    m = max(n, 1)
+    vals = torch.empty((len(cols), m), dtype=torch.int64, device=dev)
+    valid = torch.empty((len(cols), m), dtype=torch.uint8, device=dev)
+    fmask = sum(1 << j for j, k in enumerate(ks) if desc.kinds[k] == "float")
+    att = (C.c_int32 * len(ks))(*ks)
+    d = tupdesc_struct(desc)
+    check(lib().strom_heap_project_n(ptr(pages), page_sz, ptr(items), ptr(count), n, C.byref(d),
+                                     C.addressof(att), len(ks), fmask, ptr(vals), ptr(valid),
+                                     stream_handle(stream)), "heap_project_n")
+    out = {}
+    for j, c in enumerate(cols):
+        v = vals[j, :n]
+        out[c] = (v.view(torch.float64) if (fmask >> j) & 1 else v, valid[j, :n])
+    return out

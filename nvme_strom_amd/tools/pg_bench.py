@@ -126,7 +126,14 @@ def main(argv=None) -> int:
         t_pages = len(tmpl2) // 8192
         qsets = {"quals1": [T.Qual("a", "between", (-200_000, 300_000))],
                  "quals2": [T.Qual("a", "between", (-500_000, 200_000)),
-                            T.Qual("b", "between", (0.1, 0.6))]}
+                            T.Qual("b", "between", (0.1, 0.6))],
+                 # CNF: three OR-groups over int / IN-list / text-IN (with a
+                 # constant past 32 bytes) / float / null tests
+                 "cnf3": [T.Or(T.Qual("a", "between", (-500_000, 300_000)),
+                               T.Qual("c", "in", (list(range(1, 12)),))),
+                          T.Or(T.Qual("name", "text_in", (["k17", "k3", "k42", "x" * 40],)),
+                               T.Qual("b", "between", (0.1, 0.9))),
+                          T.Or(T.Qual("e", "between", (-1.0, 1.0)), T.Qual("tail", "isnull"))]}
         ccfg = pg_scan.ScanConfig(verify_checksum=False, chunk_size=best["chunk_mib"] << 20,
                                   buffer_size=8 * best["chunk_mib"] << 20)
         for name, qs in qsets.items():
@@ -155,11 +162,15 @@ def main(argv=None) -> int:
             med = float(np.median(times))
             row = dict(GBps=round(n2 / med / 1e9, 2), ms=[round(t * 1e3, 1) for t in times],
                        cold_ms=round(cold * 1e3, 1), workers=best["workers"],
-                       chunk_mib=best["chunk_mib"], quals=len(qs), selected=int(len(out.items)),
+                       chunk_mib=best["chunk_mib"], quals=sum(len(c) for c in T.clauses(qs)),
+                       clauses=len(qs), selected=int(len(out.items)),
                        relation_bytes=n2, verified=bool(ok),
                        of_single_predicate=round(n2 / med / 1e9 / best["GBps"], 3))
             res["runs"][f"gpu_{name}"] = row
             _log("gpu", name, row)
+        q1 = res["runs"].get("gpu_quals1")
+        if q1 and q1["GBps"]:
+            res["runs"]["gpu_cnf3"]["of_quals1"] = round(res["runs"]["gpu_cnf3"]["GBps"] / q1["GBps"], 3)
         for p in rel2.segments + one2.segments:
             try:
                 os.unlink(p)

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import struct
 from dataclasses import dataclass, field
+from decimal import Decimal, localcontext
 from typing import Any, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -39,7 +40,7 @@ PG_TYPES = {
     "date": (4, 4, "int"), "time": (8, 8, "int"), "timestamp": (8, 8, "int"),
     "timestamptz": (8, 8, "int"), "float4": (4, 4, "float"), "float8": (8, 8, "float"),
     "text": (-1, 4, "text"), "varchar": (-1, 4, "text"), "bpchar": (-1, 4, "text"),
-    "bytea": (-1, 4, "text"), "numeric": (-1, 4, "text"), "jsonb": (-1, 4, "text"),
+    "bytea": (-1, 4, "text"), "numeric": (-1, 4, "numeric"), "jsonb": (-1, 4, "text"),
     "name": (64, 1, "bytes"), "cstring": (-2, 1, "text"),
 }
 
@@ -111,6 +112,83 @@ class TupleDesc:
         return out
 
 
+# ---- numeric (src/backend/utils/adt/numeric.c on-disk form): base-10000
+# digits, NumericShort when the display scale and weight fit, else
+# NumericLong; NaN / +-Infinity as special headers
+NBASE = 10000
+
+
+def numeric_parts(v) -> Tuple[int, int, int, List[int], int]:
+    """(kind 0 finite / 1 NaN / 2 +inf / 3 -inf, negative, weight, digits,
+    dscale) of a Decimal / int / float / str, digits with no leading or
+    trailing zero groups (zero: no digits, weight 0)."""
+    d = v if isinstance(v, Decimal) else Decimal(str(v))
+    if d.is_nan():
+        return 1, 0, 0, [], 0
+    if d.is_infinite():
+        return (2 if d > 0 else 3), 0, 0, [], 0
+    sign, digits, exp = d.as_tuple()
+    dscale = max(0, -exp)
+    coef = int("".join(map(str, digits))) if digits else 0
+    k = (dscale + 3) // 4
+    n = coef * 10 ** (4 * k + exp)
+    groups: List[int] = []
+    while n:
+        groups.insert(0, n % NBASE)
+        n //= NBASE
+    if not groups:
+        return 0, 0, 0, [], dscale
+    weight = len(groups) - 1 - k
+    while groups and groups[-1] == 0:
+        groups.pop()
+    return 0, int(sign), weight, groups, dscale
+
+
+def numeric_bytes(v) -> bytes:
+    """The numeric's varlena payload (without the varlena header)."""
+    kind, neg, weight, digits, dscale = numeric_parts(v)
+    if kind:
+        return struct.pack("<H", {1: 0xC000, 2: 0xD000, 3: 0xF000}[kind])
+    body = struct.pack(f"<{len(digits)}h", *digits)
+    if dscale <= 0x3F and -64 <= weight <= 63:
+        h = 0x8000 | (0x2000 if neg else 0) | (dscale << 7) | (0x40 if weight < 0 else 0) | \
+            (weight & 0x3F)
+        return struct.pack("<H", h) + body
+    return struct.pack("<Hh", (0x4000 if neg else 0) | (dscale & 0x3FFF), weight) + body
+
+
+def numeric_value(raw: bytes) -> Decimal:
+    """A numeric's varlena payload back to a Decimal."""
+    h, = struct.unpack_from("<H", raw, 0)
+    if h & 0xC000 == 0xC000:
+        sp = h & 0xF000
+        return Decimal({0xC000: "NaN", 0xD000: "Infinity", 0xF000: "-Infinity"}[sp])
+    if h & 0xC000 == 0x8000:
+        neg = bool(h & 0x2000)
+        weight = (h | ~0x3F) if h & 0x40 else h & 0x3F
+        body = raw[2:]
+    else:
+        neg = (h & 0xC000) == 0x4000
+        weight, = struct.unpack_from("<h", raw, 2)
+        body = raw[4:]
+    digits = struct.unpack(f"<{len(body) // 2}h", body[:len(body) // 2 * 2])
+    with localcontext() as ctx:
+        ctx.prec = 4 * len(digits) + 8
+        val = sum((Decimal(d) * (Decimal(NBASE) ** (weight - i)) for i, d in enumerate(digits)),
+                  Decimal(0))
+        return -val if neg else +val
+
+
+def numeric_key(v) -> Tuple[int, Decimal]:
+    """PostgreSQL's numeric order: -inf < finite < +inf < NaN (NaN = NaN)."""
+    d = v if isinstance(v, Decimal) else Decimal(str(v))
+    if d.is_nan():
+        return (3, Decimal(0))
+    if d.is_infinite():
+        return (2 if d > 0 else 0, Decimal(0))
+    return (1, d)
+
+
 def _datum(v: Any, L: int, kind: str, al: int, off: int) -> Tuple[int, bytes]:
     """(aligned offset, bytes) of a non-null attribute stored at ``off``."""
     if L > 0:
@@ -133,7 +211,10 @@ def _datum(v: Any, L: int, kind: str, al: int, off: int) -> Tuple[int, bytes]:
         off = _align(off, al)
         n = 4 + 4 + len(v.payload)
         return off, struct.pack("<I", (n << 2) | 2) + struct.pack("<I", 1000) + v.payload
-    raw = v.encode() if isinstance(v, str) else bytes(v)
+    if kind == "numeric":
+        raw = numeric_bytes(v)
+    else:
+        raw = v.encode() if isinstance(v, str) else bytes(v)
     if len(raw) + 1 <= 0x7F:                 # VARATT_CAN_MAKE_SHORT: no alignment
         return off, bytes([((len(raw) + 1) << 1) | 1]) + raw
     off = _align(off, al)
@@ -219,6 +300,8 @@ def deform(tup: bytes, desc: TupleDesc) -> List[Any]:
             else:
                 n = b >> 1
                 out.append(bytes(tup[off + 1:off + n]))
+            if kind == "numeric" and out[-1] is not EXT:
+                out[-1] = numeric_value(out[-1])
             if off + n > len(tup):
                 raise ValueError("varlena past the tuple end")
             off += n
@@ -229,27 +312,55 @@ def deform(tup: bytes, desc: TupleDesc) -> List[Any]:
     return out
 
 
+def _b(x) -> bytes:
+    return x.encode() if isinstance(x, str) else bytes(x)
+
+
 @dataclass
 class Qual:
-    """One qualifier: ``op`` in between / eq / in / isnull / notnull /
-    text_eq / prefix, over column ``col`` (name or 0-based attno)."""
+    """One qualifier over column ``col`` (name or 0-based attno): ``op`` in
+    between (inclusive) / eq / lt / le / gt / ge / in / isnull / notnull on
+    int, float and numeric columns; text_eq / prefix / text_in on varlena
+    text.  A qualifier list is ANDed; ``Or(...)`` groups qualifiers into one
+    ORed clause (conjunctive normal form)."""
     col: Any
     op: str
     args: tuple = ()
 
     def test(self, v: Any, kind: str) -> Optional[bool]:
-        """True / False, or None when undecidable (EXT under a text op)."""
+        """True / False, or None when undecidable (EXT under a text or
+        numeric op)."""
         if self.op == "isnull":
             return v is None
         if v is None:
             return False
         if self.op == "notnull":
             return True
-        if self.op in ("text_eq", "prefix"):
+        if self.op in ("text_eq", "prefix", "text_in"):
             if v is EXT:
                 return None
-            c = self.args[0].encode() if isinstance(self.args[0], str) else bytes(self.args[0])
+            if self.op == "text_in":
+                return v in {_b(c) for c in self.args[0]}
+            c = _b(self.args[0])
             return v == c if self.op == "text_eq" else v.startswith(c)
+        if kind == "numeric":
+            if self.op == "in" and not self.args[0]:
+                return False                     # constant false, whatever v is
+            if v is EXT:
+                return None
+            k = numeric_key(v)
+            if self.op == "in":
+                return any(k == numeric_key(c) for c in self.args[0])
+            if self.op == "between":
+                return numeric_key(self.args[0]) <= k <= numeric_key(self.args[1])
+            c = numeric_key(self.args[0])
+            return {"eq": k == c, "lt": k < c, "le": k <= c, "gt": k > c, "ge": k >= c}[self.op]
+        if self.op in ("lt", "le", "gt", "ge"):
+            c = self.args[0]
+            if kind == "float":
+                return {"lt": not _pg_le(c, v), "le": _pg_le(v, c), "gt": not _pg_le(v, c),
+                        "ge": _pg_le(c, v)}[self.op]
+            return {"lt": v < c, "le": v <= c, "gt": v > c, "ge": v >= c}[self.op]
         if self.op == "between":
             lo, hi = self.args
             if kind == "float":
@@ -258,8 +369,27 @@ class Qual:
         if self.op == "eq":
             return v == self.args[0] if kind != "float" else (_pg_le(self.args[0], v) and _pg_le(v, self.args[0]))
         if self.op == "in":
+            if kind == "float":
+                return any(_pg_le(c, v) and _pg_le(v, c) for c in self.args[0])
             return v in self.args[0]
         raise ValueError(self.op)
+
+
+class Or:
+    """An ORed clause of qualifiers in a qualifier list (CNF)."""
+
+    def __init__(self, *quals: Qual):
+        if not quals:
+            raise ValueError("empty Or")
+        self.quals = list(quals)
+
+    def __repr__(self) -> str:
+        return "Or(" + ", ".join(map(repr, self.quals)) + ")"
+
+
+def clauses(quals) -> List[List[Qual]]:
+    """A qualifier list as CNF clauses (each a list of ORed Quals)."""
+    return [q.quals if isinstance(q, Or) else [q] for q in quals]
 
 
 def _pg_le(x: float, y: float) -> bool:
@@ -274,9 +404,12 @@ def host_scan2(data: bytes, desc: TupleDesc, quals: Sequence[Qual], page_sz: int
                skip_invisible: bool = False, verify_checksum: bool = False,
                blkno_base: int = 0, project=None) -> Tuple[List[int], List[int], list]:
     """Reference scan with a qualifier list: (sorted item ids page<<16|lineno,
-    per-page status incl. PAGE_RECHECK, projected values of the items)."""
+    per-page status incl. PAGE_RECHECK, projected values of the items: one
+    value per item, a tuple of values when ``project`` lists columns)."""
     items, status, proj = [], [], []
-    pj = desc.attno(project) if project is not None else None
+    many = isinstance(project, (list, tuple))
+    pj = ([desc.attno(c) for c in project] if many else
+          desc.attno(project) if project is not None else None)
     for pg in range(len(data) // page_sz):
         page = data[pg * page_sz:(pg + 1) * page_sz]
         _, st = pgpage.host_scan(page, page_sz, False, verify_checksum=verify_checksum,
@@ -300,19 +433,29 @@ def host_scan2(data: bytes, desc: TupleDesc, quals: Sequence[Qual], page_sz: int
                 vals = deform(tup, desc)
             except (ValueError, KeyError, IndexError):
                 continue
+            # CNF, three-valued: a clause is true if any of its quals is,
+            # unknown if none is but one is undecidable (EXT), else false
             verdict = True
-            for q in quals:
-                k = desc.attno(q.col)
-                r = q.test(vals[k], desc.kinds[k])
-                if r is False:
+            for cl in clauses(quals):
+                cv = False
+                for q in cl:
+                    k = desc.attno(q.col)
+                    r = q.test(vals[k], desc.kinds[k])
+                    if r is True:
+                        cv = True
+                        break
+                    if r is None:
+                        cv = None
+                if cv is False:
                     verdict = False
                     break
-                if r is None:
+                if cv is None:
                     verdict = None
             if verdict is None:
                 st |= PAGE_RECHECK
             elif verdict:
-                found.append((i + 1, vals[pj] if pj is not None else None))
+                found.append((i + 1, tuple(vals[k] for k in pj) if many else
+                              vals[pj] if pj is not None else None))
         status.append(st)
         for lineno, v in found:
             items.append((pg << 16) | lineno)

@@ -1,4 +1,5 @@
 """Tuple builder / deformer (utils.pgtuple) against PostgreSQL's on-disk rules."""
+import collections
 import struct
 
 import numpy as np
@@ -109,3 +110,104 @@ def test_cpu_scan_with_qualifier_list(strom, tmp_path):
         else:
             assert [v if ok == 1 else None for v, ok in zip(r.values, r.valid)] == \
                 [v if isinstance(v, bytes) else None for v in vals]
+
+
+# ---- qualifier programs: numeric, CNF, constants of any size
+def test_numeric_roundtrip_and_order():
+    """numeric's on-disk form (NumericShort / NumericLong / specials) round-
+    trips through the tuple deformer, and the order is PostgreSQL's
+    (-inf < finite < +inf < NaN, NaN = NaN)."""
+    import decimal
+    D = decimal.Decimal
+    desc = T.TupleDesc.of([("v", "numeric")])
+    vals = [D("0"), D("1"), D("-1"), D("12345.678"), D("-0.00005"), D("1e-300"), D("NaN"),
+            D("Infinity"), D("-Infinity"), D("123456789012345678901234567890.123456789"),
+            D("99999999999999999999.5")]
+    for v in vals:
+        got = T.deform(T.heap_tuple([v], desc), desc)[0]
+        assert (got.is_nan() and v.is_nan()) or got == v, (v, got)
+    keys = sorted(vals, key=T.numeric_key)
+    assert keys[0] == D("-Infinity") and keys[-1].is_nan() and keys[-2] == D("Infinity")
+
+
+def test_program_compiles_cnf_and_exact_int_bounds():
+    """Quals -> program: one clause per Qual / Or, constants in the pool;
+    int bounds exact (a fractional lower bound rounds up, an upper one down,
+    a fractional equality selects nothing, bounds clamp to the type) —
+    ADVICE r4: the host twin and the device agree."""
+    import ctypes as C
+    from nvme_strom_amd.ops import heapscan as H
+    desc, _ = heapgen.numeric_rel(10)
+    qs = [T.Qual("x", "between", (1.5, 3)), T.Or(T.Qual("s", "eq", (2.5,)), T.Qual("x", "lt", (10**30,))),
+          T.Qual("tag", "text_in", (["a" * 100, "b"],)), T.Qual("amt", "ge", (3,))]
+    p = H.Program(desc, qs)
+    cl = [q.clause for q in p.quals]
+    assert cl == sorted(cl) and sorted(collections.Counter(cl).values()) == [1, 1, 1, 2]
+    # clauses by first attribute (amt, tag, x, x|s), quals by attribute inside
+    assert [q.attno for q in p.quals] == [1, 2, 3, 3, 6]
+    x_between, x_lt, s_eq = p.quals[2], p.quals[3], p.quals[4]
+    assert x_between.clause != x_lt.clause == s_eq.clause
+    assert (x_between.lo, x_between.hi) == (2, 3)
+    assert s_eq.flags & H.QUAL2_FALSE                         # s == 2.5: never
+    assert x_lt.hi == (1 << 63) - 1                          # clamped to int8
+    raw, pool = p.arrays()
+    hp = np.frombuffer(raw, np.uint8)
+    d = H.tupdesc_struct(desc)
+    assert H.lib().strom_heap_prog_check(C.byref(d), hp.ctypes.data, len(p.quals), len(pool)) == 0
+    assert H.lib().strom_heap_prog_check(C.byref(d), hp.ctypes.data, len(p.quals), 8) < 0
+    # the host twin on the same fractional bounds
+    assert T.Qual("x", "between", (1.5, 3)).test(1, "int") is False
+    assert T.Qual("s", "eq", (2.5,)).test(2, "int") is False
+
+
+def _brute(rows, desc, qs):
+    """Independent CNF evaluation straight from the Python row values."""
+    out = []
+    for i, r in enumerate(rows):
+        verdict = True
+        for cl in T.clauses(qs):
+            cv = False
+            for q in cl:
+                k = desc.attno(q.col)
+                v = r[k]
+                v = T.EXT if isinstance(v, (T.Toast, T.Compressed)) else (
+                    T._b(v) if desc.kinds[k] == "text" and v is not None else v)
+                t = q.test(v, desc.kinds[k])
+                if t is True:
+                    cv = True
+                    break
+                if t is None:
+                    cv = None
+            if cv is False:
+                verdict = False
+                break
+            if cv is None:
+                verdict = None
+        out.append(verdict)
+    return out
+
+
+def test_host_scan2_cnf_matches_brute_force():
+    """The host twin's CNF over deformed tuples equals a brute-force
+    evaluation of the same quals over the Python row values (numeric,
+    text IN / long constants, NULLs, TOAST / compressed -> undecidable)."""
+    desc, rows = heapgen.numeric_rel(1500, seed=3)
+    data = T.build_pages(rows, desc)
+    rng = np.random.default_rng(8)
+    for _ in range(25):
+        qs = heapgen.random_cnf(rng, int(rng.integers(1, 12)))
+        items, status, _ = T.host_scan2(data, desc, qs)
+        want = _brute(rows, desc, qs)
+        # rows -> (page, lineno) in insertion order
+        ids, pg, ln, used = [], 0, 0, 24
+        for r in rows:
+            t = T.heap_tuple(r, desc)
+            need = ((len(t) + 7) & ~7) + 4
+            if ln and used + need > 8192:
+                pg, ln, used = pg + 1, 0, 24
+            ln += 1
+            used += need
+            ids.append((pg << 16) | ln)
+        assert items == [i for i, w in zip(ids, want) if w is True]
+        rech = {i >> 16 for i, w in zip(ids, want) if w is None}
+        assert {p for p, s in enumerate(status) if s & T.PAGE_RECHECK} == rech
