@@ -107,6 +107,29 @@ void engine_reset() {
 Engine::Engine() { io_ = std::make_unique<IoEngine>(config()); }
 Engine::~Engine() { io_.reset(); }
 
+const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *err) {
+  static thread_local struct {
+    int fd = -1;
+    const Engine *eng = nullptr;
+    std::shared_ptr<OpenFile> f;
+  } tl;
+  static const std::shared_ptr<OpenFile> none;
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    *err = -errno;
+    return none;
+  }
+  const OpenFile *c = tl.f.get();
+  if (tl.fd == fd && tl.eng == this && c && c->dev == st.st_dev && c->ino == st.st_ino &&
+      c->vsize == st.st_size && c->ctim.tv_sec == st.st_ctim.tv_sec &&
+      c->ctim.tv_nsec == st.st_ctim.tv_nsec)
+    return tl.f;
+  tl.f = open_file(fd, err);
+  tl.fd = tl.f ? fd : -1;
+  tl.eng = this;
+  return tl.f ? tl.f : none;
+}
+
 std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
   struct stat st;
   if (fstat(fd, &st) != 0) {
@@ -464,12 +487,12 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
                         uint64_t len) {
   if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
   if (fd >= kStripeFdBase) return -EAGAIN;  // stripe sets: the planner routes members
-  auto gmap = gpu_registry().get(handle);
+  const auto &gmap = gpu_registry().get_cached(handle);
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
   if (strom_core_check_range(gmap->map_length - gmap->map_offset, offset, len)) return -ERANGE;
   int err = 0;
-  auto f = open_file(fd, &err);
+  const auto &f = open_file_cached(fd, &err);
   if (!f) return err;
   phase_mark(0);
   const uint64_t size = (uint64_t)f->fc.size;
@@ -963,6 +986,9 @@ int strom_host_costs(int fd, uint64_t *out, int n) {
 //   0 gpu_registry().get(handle)   1 validate (HIP buffer id of the range)
 //   2 open_file (fstat + cache)    3 completion bookkeeping (histograms,
 //   counters, mapping in-flight count) — finish_request and the stats adds
+//   4 / 5 the per-thread cached forms of 0 / 2 (pread_sync uses them)
+//   6 a 4 KiB BAR store + posted HDP flush   7 the first locked instruction
+//   after it (0 / 0 without a BAR mapping)
 int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   using namespace strom;
   if (n <= 0 || fd < 0) return -EINVAL;
@@ -992,6 +1018,28 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
     finish_request(r, 0);
     sink += (uint64_t)status;
   });
+  out[4] = bench([&] { sink += (uint64_t)(gpu_registry().get_cached(handle) != nullptr); });
+  out[5] = bench([&] { sink += (uint64_t)(engine().open_file_cached(fd, &err) != nullptr); });
+  // a 4 KiB store through the BAR with its (posted) HDP flush, then the
+  // first locked instruction after it: is the write's drain paid there?
+  out[6] = out[7] = 0;
+  if (g->bar && g->length >= 4096) {
+    alignas(64) static uint8_t src[4096];
+    std::atomic<uint64_t> ctr{0};
+    uint64_t store = 0, lock = 0;
+    for (int i = 0; i < n; ++i) {
+      const uint64_t t0 = mono_ns();
+      g->bar_write(g->va, src, 4096, true);
+      const uint64_t t1 = mono_ns();
+      ctr.fetch_add(1);
+      const uint64_t t2 = mono_ns();
+      store += t1 - t0;
+      lock += t2 - t1;
+    }
+    out[6] = store / (uint64_t)n;
+    out[7] = lock / (uint64_t)n;
+    sink += ctr.load();
+  }
   return 0;
 }
 

@@ -246,6 +246,11 @@ class GpuRegistry {
   int list(strom_list_gpu_memory *out);
   int info(strom_info_gpu_memory *out);
   std::shared_ptr<GpuMapping> get(unsigned long handle);
+  // get() through a per-thread one-entry cache, valid while no mapping was
+  // added, removed or detached since (the generation): the synchronous
+  // small-read path then takes no lock and makes no geteuid() call.  The
+  // reference stays valid until this thread's next get_cached().
+  const std::shared_ptr<GpuMapping> &get_cached(unsigned long handle);
   // 0 while the allocation that was mapped still backs the range; else the
   // mapping is detached (like the reference's free callback,
   // kmod/pmemmap.c:150-208) and -ENOENT returned
@@ -257,6 +262,7 @@ class GpuRegistry {
   std::map<unsigned long, std::shared_ptr<GpuMapping>> maps_;
   unsigned long next_ = 0x5350000000000000ul;  // 'S','P' tag + counter
   std::atomic<uint64_t> detached_{0};
+  std::atomic<uint64_t> gen_{1};
 };
 
 GpuRegistry &gpu_registry();
@@ -540,6 +546,11 @@ class Engine {
 
   // the per-file cache (fstat-validated): classification, descriptors, map
   std::shared_ptr<OpenFile> open_file(int fd, int *err);
+  // open_file() for the synchronous small-read path: the fstat stays (the
+  // descriptor's identity), the lock, map lookup and reference count go
+  // when this thread's last file is still the same (device, inode, ctime,
+  // size).  The reference stays valid until this thread's next call.
+  const std::shared_ptr<OpenFile> &open_file_cached(int fd, int *err);
 
  private:
   int check_file(strom_check_file *a);

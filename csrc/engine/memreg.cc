@@ -130,6 +130,7 @@ int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memor
     std::lock_guard<std::mutex> g(mu_);
     m->handle = ++next_;
     maps_.emplace(m->handle, m);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
   }
   out->handle = m->handle;
   out->gpu_page_sz = (uint32_t)STROM_GPU_BOUND_SIZE;
@@ -137,6 +138,22 @@ int GpuRegistry::map(uint64_t va, size_t len, int dmabuf_fd, strom_map_gpu_memor
   STROM_LOG(1, "map va=%#lx len=%zu dev=%d handle=%#lx", (unsigned long)va, len, device,
             m->handle);
   return 0;
+}
+
+const std::shared_ptr<GpuMapping> &GpuRegistry::get_cached(unsigned long handle) {
+  static thread_local struct {
+    unsigned long handle = 0;
+    uint64_t gen = 0;
+    std::shared_ptr<GpuMapping> m;
+  } tl;
+  // the generation is read before the lookup: a change racing with it
+  // leaves the entry one generation old, so the next call looks up again
+  const uint64_t gen = gen_.load(std::memory_order_acquire);
+  if (tl.handle == handle && tl.gen == gen && tl.m) return tl.m;
+  tl.m = get(handle);
+  tl.handle = handle;
+  tl.gen = gen;
+  return tl.m;
 }
 
 std::shared_ptr<GpuMapping> GpuRegistry::get(unsigned long handle) {
@@ -162,6 +179,7 @@ int GpuRegistry::validate(const std::shared_ptr<GpuMapping> &m) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = maps_.find(m->handle);
     if (it != maps_.end() && it->second == m) maps_.erase(it);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
   }
   m->detached = true;
   detached_.fetch_add(1);
@@ -179,6 +197,7 @@ int GpuRegistry::unmap(unsigned long handle) {
     if (it->second->owner != geteuid()) return -EACCES;
     m = it->second;
     maps_.erase(it);
+    gen_.fetch_add(1, std::memory_order_acq_rel);
   }
   // wait for in-flight DMA targeting the range (free-callback semantics);
   // completions notify only while someone drains

@@ -83,6 +83,22 @@ constexpr uint32_t KW = OB / 4 / NT + 1; // output dwords a thread holds per bat
 constexpr uint32_t EPT = OB / NT;        // batch entries a thread expands (contiguous)
 constexpr uint32_t HW = OB / 32;         // run-head bitmap words
 constexpr uint32_t HS = (HW + 31) / 32;  // summary words (bit w: head word w not empty)
+// The pointer fill's unit of work: UB compressed bytes of a slice (CP per
+// slice).  The count records where each unit's first sequence starts and
+// its output offset; a batch's fill then runs on every thread whose unit
+// meets it, not only on the ~OB / (output per slice) threads whose slices
+// do (round 4: the fill was 0.27-0.48 of thread 0's cycles).
+#ifndef LZ4PAR_UB
+#define LZ4PAR_UB 16
+#endif
+constexpr uint32_t UB = LZ4PAR_UB < SL ? LZ4PAR_UB : SL;
+constexpr uint32_t CP = SL / UB;
+constexpr uint32_t kCkNone = 0xffu;      // checkpoint: no sequence starts in the unit
+#ifndef LZ4PAR_HOPS
+#define LZ4PAR_HOPS 1
+#endif
+constexpr uint32_t HOPS = LZ4PAR_HOPS;   // chain steps per entry per doubling round
+static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 #ifndef LZ4PAR_LOOKBACK
@@ -193,9 +209,16 @@ struct WalkMem {
 
 struct Smem {
   uint8_t win[WI(PW + PAD) + 4];
-  uint32_t bits[PW / 32];  // the chain slice t follows (a walker's, or a fix-up's)
+  union {
+    struct {
+      uint32_t bits[PW / 32];  // the chain slice t follows (a walker's, or a fix-up's)
+      uint32_t en[NT];         // true entry of slice t
+    };
+    // from the count on: unit u's first sequence, (output offset in its
+    // slice << 8) | (input offset in its slice), or kCkNone
+    uint32_t ck[NT * CP];
+  };
   uint32_t ex[NT];       // exit of slice t's chain
-  uint32_t en[NT];       // true entry of slice t
   uint32_t ost[NT];      // output bytes of slice t's true sequences, then their inclusive prefix
   union {
     uint32_t ptr[PI(OB)];
@@ -730,15 +753,21 @@ HD uint32_t sn_settle(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   return j - 1;
 }
 
-// (3) output bytes of slice t's true sequences (errors set s.err)
+// (3) output bytes of slice t's true sequences from its entry `ent` (read
+// from s.en before a barrier: the checkpoints overwrite it) and the
+// checkpoint of each of its fill units (errors set s.err)
 template <bool SN>
-HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
+HD void ph_count(Smem &s, const Ctx &c, uint32_t t, uint32_t ent) {
   const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
-  uint32_t o = 0;
+  uint32_t o = 0, j = 0;
   if (lo < hi) {
-    uint32_t p = s.en[t];
+    uint32_t p = ent;
     Seq q;
     while (p < hi) {
+      // p is the first sequence of every unit whose start it has reached
+      // (an output offset past 24 bits merges the slice's later units)
+      for (; j < CP && p >= lo + j * UB; ++j)
+        s.ck[t * CP + j] = o < (1u << 24) ? (o << 8) | (p - lo) : kCkNone;
       if (!parse<SN>(s, c, p, s.bend, q)) {
         s.err = kErrFormat;
         break;
@@ -752,6 +781,7 @@ HD void ph_count(Smem &s, const Ctx &c, uint32_t t) {
       p = q.next;
     }
   }
+  for (; j < CP; ++j) s.ck[t * CP + j] = kCkNone;
   s.ost[t] = o;
   if (t < HW) s.hb[t] = 0;
   if (t < HS) s.hsum[t] = 0;
@@ -781,59 +811,63 @@ HD void head(Smem &s, uint32_t e, uint32_t v) {
 #endif
 }
 
-// where slice t's walk resumes in the next batch: its first sequence not
-// completely before the batch (set per window, advanced by ph_fill)
-struct FillPos {
-  uint32_t p, o;
-};
-
-HD void ph_fill_init(const Smem &s, uint32_t t, FillPos &f) {
-  f.p = s.en[t];
-  f.o = t ? s.ost[t - 1] : 0;
-}
-
+// (4a) thread t fills for units t, t + NT, ...: consecutive units (one
+// slice's, then the next slice's) on consecutive threads, so the ~OB /
+// (output per unit) units a batch meets spread over as many threads.  A
+// unit longer than a batch is walked again from its start by the next one.
 template <bool SN>
-HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0, FillPos &f) {
-  const uint32_t lo = slice_lo(s, t), hi = slice_hi(s, t);
-  if (lo >= hi) return;
-  const uint32_t o1 = s.ost[t], o0 = t ? s.ost[t - 1] : 0;
+HD void ph_fill(Smem &s, const Ctx &c, uint32_t t, uint32_t b0) {
   const uint32_t b1 = b0 + OB;
-  if (o1 <= b0 || o0 >= b1) return;
   const uint32_t opw = s.op;             // output position of the window start
-  uint32_t p = f.p, o = f.o;
-  Seq q;
-  while (p < hi && o < b1) {
-    parse<SN>(s, c, p, s.bend, q);       // checked by ph_count
-    const uint32_t le = o + q.lit;
-    if (le > b0 && q.lit) {
-      const uint32_t x0 = o > b0 ? o : b0;
-      head(s, x0 - b0, kLit | (q.lit0 + (x0 - o)));
-    }
-    o = le;
-    if (SN ? q.mlen != 0 : !q.last) {
-      const uint32_t me = o + q.mlen;
-      if (me > b0 && o < b1) {
-        if ((uint64_t)q.off > (uint64_t)opw + o) {
-          s.err = kErrDistance;
-          return;
-        }
-        const uint32_t x0 = o > b0 ? o : b0, x1 = me < b1 ? me : b1;
-        // source of byte x: absolute opw + x - off; inside the batch (index
-        // x - off - b0) from x = b0 + off on, stored history before
-        const uint32_t xs = b0 + q.off;
-        if (x0 < xs) {
-          head(s, x0 - b0, kHist | (opw + x0 - q.off));
-          if (xs < x1) head(s, xs - b0, 0);
-        } else {
-          head(s, x0 - b0, x0 - q.off - b0);
-        }
+  for (uint32_t k = 0; k < CP; ++k) {
+    const uint32_t u = t + k * NT, sl = u / CP, j = u % CP;
+    const uint32_t v = s.ck[u];
+    if ((v & 0xff) == kCkNone) continue;
+    const uint32_t base = sl ? s.ost[sl - 1] : 0, lo = slice_lo(s, sl);
+    uint32_t o = base + (v >> 8);
+    if (o >= b1) continue;
+    // the unit ends where the slice's next unit with a sequence starts
+    uint32_t oend = s.ost[sl], pend = slice_hi(s, sl);
+    for (uint32_t i = j + 1; i < CP; ++i) {
+      const uint32_t w = s.ck[sl * CP + i];
+      if ((w & 0xff) != kCkNone) {
+        oend = base + (w >> 8);
+        pend = lo + (w & 0xff);
+        break;
       }
-      o = me;
     }
-    p = q.next;
-    if (o <= b1) {                       // done with it: the next batch starts later
-      f.p = p;
-      f.o = o;
+    if (oend <= b0) continue;
+    uint32_t p = lo + (v & 0xff);
+    Seq q;
+    while (p < pend && o < b1) {
+      parse<SN>(s, c, p, s.bend, q);     // checked by ph_count
+      const uint32_t le = o + q.lit;
+      if (le > b0 && q.lit) {
+        const uint32_t x0 = o > b0 ? o : b0;
+        head(s, x0 - b0, kLit | (q.lit0 + (x0 - o)));
+      }
+      o = le;
+      if (SN ? q.mlen != 0 : !q.last) {
+        const uint32_t me = o + q.mlen;
+        if (me > b0 && o < b1) {
+          if ((uint64_t)q.off > (uint64_t)opw + o) {
+            s.err = kErrDistance;
+            return;
+          }
+          const uint32_t x0 = o > b0 ? o : b0, x1 = me < b1 ? me : b1;
+          // source of byte x: absolute opw + x - off; inside the batch (index
+          // x - off - b0) from x = b0 + off on, stored history before
+          const uint32_t xs = b0 + q.off;
+          if (x0 < xs) {
+            head(s, x0 - b0, kHist | (opw + x0 - q.off));
+            if (xs < x1) head(s, xs - b0, 0);
+          } else {
+            head(s, x0 - b0, x0 - q.off - b0);
+          }
+        }
+        o = me;
+      }
+      p = q.next;
     }
   }
 }
@@ -867,7 +901,18 @@ HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
       cur = e;
       base = s.ptr[PI(e)];
     } else {
-      s.ptr[PI(e)] = base + (e - cur);
+      // a match run whose source is inside the batch starts off = cur -
+      // base bytes after it; past off bytes the run copies itself
+      // (overlapping match: RLE-like runs), so byte e also equals the
+      // source byte (e - cur) mod off — one step to a byte before the run
+      // instead of a chain through the run that pointer doubling would
+      // need log2(run / off) rounds for
+      uint32_t d = e - cur;
+      if (!(base & kTag) && base < cur) {
+        const uint32_t off = cur - base;
+        if (d >= off) d = off == 1 ? 0 : d % off;
+      }
+      s.ptr[PI(e)] = base + d;
     }
   }
 }
@@ -883,8 +928,14 @@ HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
     const uint32_t v = s.ptr[PI(e)];
     if (!(v & kTag)) {
       // v < e always (a match reads backwards); the bound only keeps a
-      // corrupt table inside the array
-      const uint32_t w = v < e ? s.ptr[PI(v)] : kLit;
+      // corrupt table inside the array.  HOPS > 1 follows the chain further
+      // within the round (any value read is a valid pointer of the byte:
+      // they only move towards the root), trading LDS latency for rounds.
+      uint32_t w = v < e ? s.ptr[PI(v)] : kLit;
+      for (uint32_t k = 1; k < HOPS && !(w & kTag); ++k) {
+        const uint32_t x = w;
+        w = x < e ? s.ptr[PI(x)] : kLit;
+      }
       s.ptr[PI(e)] = w;
       more |= !(w & kTag);
     }
@@ -1333,7 +1384,11 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           }
         }
         LP_MARK(kLpValid);
-        ph_count<SN>(s, c, t);
+        {
+          const uint32_t ent = s.en[t];
+          __syncthreads();
+          ph_count<SN>(s, c, t, ent);
+        }
         for (uint32_t dd = 1; dd < NT; dd <<= 1) {
           __syncthreads();
           const uint32_t v = ph_scan_read(s, t, dd);
@@ -1349,12 +1404,10 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
         LP_MARK(kLpScan);
         if (s.err) break;
         const uint32_t total = s.total;
-        FillPos fpos;
-        ph_fill_init(s, t, fpos);
         for (uint32_t b0 = 0; b0 < total; b0 += OB) {
           LP_CNT(kLpNBatch);
           const uint32_t nb = total - b0 < OB ? total - b0 : OB;
-          ph_fill<SN>(s, c, t, b0, fpos);
+          ph_fill<SN>(s, c, t, b0);
           __syncthreads();
           LP_MARK(kLpFill);
           if (s.err) break;
@@ -1454,7 +1507,8 @@ template <bool SN>
 int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, uint32_t cap,
                 uint32_t *stats) {
   using namespace LZ4P_NS;
-  static_assert(NT != 256 || PW != 16384 || OB != 4096 || HR != 0 || sizeof(Smem) <= 40 * 1024,
+  static_assert(NT != 256 || PW != 16384 || OB != 4096 || HR != 0 || UB != 16 ||
+                    sizeof(Smem) <= 40 * 1024,
                 "default geometry: four workgroups per CU (160 KiB LDS)");
   Smem *sp = new Smem;
   Smem &s = *sp;
@@ -1462,7 +1516,6 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
   uint32_t ent[NT];
   bool flag[NT];
   Held *held = new Held[NT];
-  FillPos *fpos = new FillPos[NT];
   uint32_t rounds = 0, fixes = 0, windows = 0, dbl = 0, serial = 0, serial_windows = 0;
   uint32_t walk_windows = 0;
   st_header(s, c, codec);
@@ -1566,7 +1619,8 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
           }
         }
       }
-      for (uint32_t t = 0; t < NT; ++t) ph_count<SN>(s, c, t);
+      for (uint32_t t = 0; t < NT; ++t) ent[t] = s.en[t];
+      for (uint32_t t = 0; t < NT; ++t) ph_count<SN>(s, c, t, ent[t]);
       for (uint32_t dd = 1; dd < NT; dd <<= 1) {
         for (uint32_t t = 0; t < NT; ++t) ent[t] = ph_scan_read(s, t, dd);
         for (uint32_t t = 0; t < NT; ++t) ph_scan_write(s, t, ent[t]);
@@ -1574,10 +1628,9 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
       s.total = s.ost[NT - 1];
       if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
       if (s.err) break;
-      for (uint32_t t = 0; t < NT; ++t) ph_fill_init(s, t, fpos[t]);
       for (uint32_t b0 = 0; b0 < s.total; b0 += OB) {
         const uint32_t nb = s.total - b0 < OB ? s.total - b0 : OB;
-        for (uint32_t t = 0; t < NT; ++t) ph_fill<SN>(s, c, t, b0, fpos[t]);
+        for (uint32_t t = 0; t < NT; ++t) ph_fill<SN>(s, c, t, b0);
         if (s.err) break;
         for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
         bool any;
@@ -1608,7 +1661,6 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
   const int r = s.err ? s.err : (int)s.op;
   delete sp;
   delete[] held;
-  delete[] fpos;
   return r;
 }
 }  // namespace

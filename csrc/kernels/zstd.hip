@@ -2233,7 +2233,7 @@ struct HostGroup {
 // error is decoded again by the serial decoder (run()) in the exec launch,
 // so statuses and errors are the serial decoder's.
 #ifndef ZS_LPB
-#define ZS_LPB 8
+#define ZS_LPB 4
 #endif
 constexpr uint32_t LP_LSYM = 128;             // literal symbols per stream per round
 constexpr uint32_t LP_LWIN = 256;             // its input window (one dword per lane)

@@ -177,7 +177,8 @@ def host_costs(fd: int, n: int = 20000) -> dict:
     return {k: int(v) for k, v in zip(HOST_COSTS, out)}
 
 
-ENGINE_COSTS = ("registry_get", "validate", "open_file", "completion")
+ENGINE_COSTS = ("registry_get", "validate", "open_file", "completion", "registry_get_cached",
+                "open_file_cached", "bar_store_4k", "lock_after_bar_store")
 
 
 def engine_costs(handle: int, fd: int, n: int = 20000) -> dict:
@@ -512,15 +513,19 @@ def pread_raw_latency(fd: int, file_offs, length: int = 4096) -> np.ndarray:
 
 
 def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
-                  sequential: bool = False, buffered: bool = False) -> tuple:
+                  sequential: bool = False, buffered: bool = False,
+                  fixed: bool = False) -> tuple:
     """Storage ceiling for one block size with no engine in the way:
     ``threads`` io_uring rings ``qd`` deep, O_DIRECT reads into host memory
     at random aligned offsets, or ``sequential``: each ring reads its own
     disjoint run of the file in order (no cursor shared between rings);
-    ``buffered`` reads through the page cache instead.  Returns (IOPS, GiB/s)."""
+    ``buffered`` reads through the page cache instead; ``fixed``: into
+    2 MiB-page buffers registered with the ring (READ_FIXED, as the
+    engine's pinned staging).  Returns (IOPS, GiB/s)."""
     iops, gibps = C.c_double(), C.c_double()
     _check(N.lib().strom_raw_read_rate(fd, block, nreq, threads, qd,
-                                       int(sequential) | (2 if buffered else 0),
+                                       int(sequential) | (2 if buffered else 0) |
+                                       (4 if fixed else 0),
                                        C.byref(iops), C.byref(gibps)), "raw_read_rate")
     return iops.value, gibps.value
 

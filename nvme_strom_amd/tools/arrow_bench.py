@@ -242,7 +242,7 @@ def main(argv=None) -> int:
                 runs.append(dt)
                 if r == 0:
                     cold_bd = dict(open_s=round(t_open, 4),
-                                   **{k: round(v, 4) for k, v in out.seconds.items()})
+                                   **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.seconds.items()})
                 _log(f"{label}{' cold' if r == 0 else ''}: {out.selected} rows, "
                      f"{dt * 1e3:.1f} ms, groups {out.groups}, "
                      f"{out.column_bytes / dt / 1e9:.1f} GB/s column, {out.seconds}")
@@ -261,7 +261,7 @@ def main(argv=None) -> int:
             column_GBps=round(out.column_bytes / med / 1e9, 2),
             column_GBps_cold=round(out.column_bytes / runs[0] / 1e9, 2),
             file_GBps=round(out.bytes_read / med / 1e9, 2),
-            last_breakdown_s={k: round(v, 4) for k, v in out.seconds.items()},
+            last_breakdown_s={k: (round(v, 4) if isinstance(v, float) else v) for k, v in out.seconds.items()},
             cold_breakdown_s=cold_bd)
         if cpu_s == cpu_s:
             row.update(cpu_ms=round(cpu_s * 1e3, 1),

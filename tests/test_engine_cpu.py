@@ -420,3 +420,38 @@ def test_coalesce_knob(strom):
     finally:
         strom.configure(coalesce=1)
     assert strom.config_get("coalesce") == "1"
+
+
+def test_pread_gpu_per_thread_caches(strom, rand_file):
+    """The synchronous path's per-thread mapping / file caches: an unmapped
+    handle fails at once, a new mapping is seen, a descriptor number reused
+    for another file reads the new file, and a file that grew is re-sized."""
+    path, data = rand_file(16 * 4096)
+    path2, data2 = rand_file(32 * 4096)
+    keep, hbm = _host_target(4 * 4096)
+    fd = _open(path)
+    try:
+        m = strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes)
+        strom.pread_gpu_latency(m.handle, 0, fd, np.array([3 * 4096], dtype=np.uint64))
+        assert np.array_equal(hbm[:4096], data[3 * 4096:4 * 4096])
+        h = m.handle
+        strom.unmap_gpu_memory(h)
+        with pytest.raises(strom.StromError) as e:
+            strom.pread_gpu_latency(h, 0, fd, np.array([0], dtype=np.uint64))
+        assert e.value.errno == errno.ENOENT
+        m = strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes)
+        # the same descriptor number, another file
+        fd2 = os.open(path2, os.O_RDONLY)
+        os.dup2(fd2, fd)
+        os.close(fd2)
+        strom.pread_gpu_latency(m.handle, 4096, fd, np.array([20 * 4096], dtype=np.uint64))
+        assert np.array_equal(hbm[4096:8192], data2[20 * 4096:21 * 4096])
+        # the file grows: a read past the old size succeeds
+        extra = np.random.default_rng(5).integers(0, 256, 8 * 4096, dtype=np.uint8)
+        with open(path2, "ab") as f:
+            f.write(extra.tobytes())
+        strom.pread_gpu_latency(m.handle, 0, fd, np.array([33 * 4096], dtype=np.uint64))
+        assert np.array_equal(hbm[:4096], extra[4096:8192])
+        strom.unmap_gpu_memory(m.handle)
+    finally:
+        os.close(fd)
