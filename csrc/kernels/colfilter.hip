@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "strom/strom.h"
 
@@ -683,6 +686,33 @@ int qual_by_type(const strom_col_qual &q, const strom_qual_batch *bt, uint32_t n
   return -22;
 }
 
+
+// Block-count scratch of the emit launches, kept per (device, stream) and
+// grown on demand.  Stream-ordered reuse on one stream is safe; hipMallocAsync
+// / hipFreeAsync were not free: the host blocked in them until the stream's
+// queued work had drained (r5 Arrow ZSTD timeline: group k+1's emit waited
+// ~20 ms for its own decode, so the next group's launches queued late).
+std::mutex g_cs_mu;
+std::map<std::pair<int, void *>, std::pair<void *, size_t>> g_cs;
+
+// under g_cs_mu, held by the caller through its launches
+void *col_scratch(hipStream_t st, size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  auto &e = g_cs[{dev, (void *)st}];
+  if (e.second < bytes) {
+    // the old buffer may still be read by this stream's queued launches
+    if (e.first && (hipStreamSynchronize(st) != hipSuccess || hipFree(e.first) != hipSuccess))
+      return nullptr;
+    e = {nullptr, 0};
+    const size_t want = bytes < (64u << 10) ? (64u << 10) : bytes;
+    void *p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+    e = {p, want};
+  }
+  return e.first;
+}
+
 }  // namespace
 
 extern "C" int strom_column_filter(int type, const void *d_values, const uint8_t *d_valid,
@@ -701,8 +731,7 @@ extern "C" int strom_column_filter(int type, const void *d_values, const uint8_t
 }
 
 // d_out needs room for every selected row; d_count receives the total.
-// Scratch for the block counts is carved from the tail of d_out's capacity
-// by the caller contract: we allocate it here with hipMallocAsync instead.
+// The block counts live in the library-kept per-stream scratch (col_scratch).
 extern "C" int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n, uint32_t *d_out,
                                        uint64_t *d_count, void *stream) {
   if (!n) return 0;
@@ -710,13 +739,13 @@ extern "C" int strom_bitmap_to_indices(const uint64_t *d_bitmap, uint64_t n, uin
   hipStream_t st = (hipStream_t)stream;
   uint64_t words = (n + 63) / 64;
   uint32_t nb = (uint32_t)((words + kWordsPerBlock - 1) / kWordsPerBlock);
-  uint32_t *cnt = nullptr;
-  if (hipMallocAsync((void **)&cnt, sizeof(uint32_t) * nb, st) != hipSuccess) return -12;
+  std::lock_guard<std::mutex> g(g_cs_mu);
+  uint32_t *cnt = (uint32_t *)col_scratch(st, sizeof(uint32_t) * nb);
+  if (!cnt) return -12;
   hipLaunchKernelGGL(block_popc_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, words, cnt);
   hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
                      (unsigned long long *)d_count);
   hipLaunchKernelGGL(emit_indices_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, words, n, cnt, d_out);
-  (void)hipFreeAsync(cnt, st);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -757,8 +786,9 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
   const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
   if (nb64 > 0xffffffffull) return -75;
   const uint32_t nb = (uint32_t)nb64;
-  uint64_t *cnt = nullptr;
-  if (hipMallocAsync((void **)&cnt, sizeof(uint64_t) * nb, st) != hipSuccess) return -12;
+  std::lock_guard<std::mutex> g(g_cs_mu);
+  uint64_t *cnt = (uint64_t *)col_scratch(st, sizeof(uint64_t) * nb);
+  if (!cnt) return -12;
   hipLaunchKernelGGL(block_popc64_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, cnt);
   hipLaunchKernelGGL(scan_blocks_cursor_kernel, dim3(1), dim3(1024), 0, st, cnt, nb,
                      (unsigned long long *)d_total);
@@ -780,7 +810,6 @@ extern "C" int strom_bitmap_to_rows_proj(const uint64_t *d_bitmap, uint64_t nwor
   else
     hipLaunchKernelGGL(emit_rows_kernel<1>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, d_batches,
                        nbatches, cnt, d_out, d_proj, d_pout, d_pvalid);
-  (void)hipFreeAsync(cnt, st);
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
@@ -855,8 +884,9 @@ extern "C" int strom_bitmap_to_rows_str(const uint64_t *d_bitmap, uint64_t nword
   const uint64_t nb64 = (nwords + kWordsPerBlock - 1) / kWordsPerBlock;
   if (nb64 > 0xffffffffull) return -75;
   const uint32_t nb = (uint32_t)nb64;
-  uint64_t *cnt = nullptr;
-  if (hipMallocAsync((void **)&cnt, sizeof(uint64_t) * 2 * nb, st) != hipSuccess) return -12;
+  std::lock_guard<std::mutex> g(g_cs_mu);
+  uint64_t *cnt = (uint64_t *)col_scratch(st, sizeof(uint64_t) * 2 * nb);
+  if (!cnt) return -12;
   uint64_t *ccnt = cnt + nb;
   hipLaunchKernelGGL(block_popc64_kernel, dim3(nb), dim3(256), 0, st, d_bitmap, nwords, cnt);
   if (owidth == 4)
@@ -875,7 +905,6 @@ extern "C" int strom_bitmap_to_rows_str(const uint64_t *d_bitmap, uint64_t nword
   else
     hipLaunchKernelGGL(emit_str_kernel<int64_t>, dim3(nb), dim3(256), 0, st, d_bitmap, nwords,
                        d_strtab, nbatches, cnt, ccnt, d_out, d_poff, d_pchars, d_pvalid);
-  (void)hipFreeAsync(cnt, st);
   (void)d_batches;
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }

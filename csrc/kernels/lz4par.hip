@@ -94,10 +94,15 @@ constexpr uint32_t HS = (HW + 31) / 32;  // summary words (bit w: head word w no
 constexpr uint32_t UB = LZ4PAR_UB < SL ? LZ4PAR_UB : SL;
 constexpr uint32_t CP = SL / UB;
 constexpr uint32_t kCkNone = 0xffu;      // checkpoint: no sequence starts in the unit
+// Chain steps per entry per doubling round: 3 cut the host twin's rounds
+// per stream from 662 to ~350 (text) and took 2,048 streams from 119 / 124
+// / 114 GB/s (text / val / ids, one hop) to 133 / 136 / 125, snappy 111 /
+// 105 / 97 to 126 / 115 / 107; 4 hops lose again on text / ids (LDS
+// latency per round), profiles/r5/lz4par/lz4par_hops_ab_r5j.json
 #ifndef LZ4PAR_HOPS
-#define LZ4PAR_HOPS 1
+#define LZ4PAR_HOPS 3
 #endif
-constexpr uint32_t HOPS = LZ4PAR_HOPS;   // chain steps per entry per doubling round
+constexpr uint32_t HOPS = LZ4PAR_HOPS;
 static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");

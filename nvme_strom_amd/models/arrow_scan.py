@@ -603,6 +603,7 @@ class ArrowScan:
                 # status = decoded bytes; short or failed -> error count
                 s.err += ((status < d_need) | (status < 0)).sum()
                 s.keep += [d_desc, d_need, status]
+                state["marks"].append((k, "decode_queued", time.perf_counter()))
             # one batch table per referenced column, uploaded once per group
             tabs: Dict[int, torch.Tensor] = {}
 
@@ -633,6 +634,7 @@ class ArrowScan:
                     else:
                         qual_batched(cq, table(col), g.words, s.bitmap, cnt, stream=cs,
                                      or_src=s.bm2, and_dst=True)
+            state["marks"].append((k, "quals_queued", time.perf_counter()))
             # emit tables: the strom_filter_batch prefix of the qual tables
             any_col = spec[0][0][0]
             d_rows = table(any_col)[:, :BATCH_FIELDS].contiguous()
