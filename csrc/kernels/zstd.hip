@@ -2243,16 +2243,9 @@ static_assert(LP_LSYM * 11 / 8 + 24 <= LP_LWIN && LP_SEQN * 89 / 8 + 24 <= LP_SW
 static_assert(LP_LWIN == 4 * NT && LP_SWIN % (4 * NT) == 0, "LP window loads");
 
 // compact FSE entry (4 bytes, a third of the LDS the 8-byte SeqEnt takes):
-// code | extra bits << 6 | state bits << 11 | next state base << 16.  The
-// code's extra-bit count rides in the entry so that the sequence loop's
-// state chain (entry -> bits consumed -> next states) never waits for the
-// baseline lookup (the wave's code table), which only the decoded values need
-HD uint32_t lp_ent(uint32_t code, uint32_t nb, uint32_t next, uint32_t kind) {
-  uint32_t base, add;
-  code_base(kind, code, base, add);
-  (void)base;
-  return code | add << 6 | nb << 11 | next << 16;
-}
+// code | bits << 8 | next state base << 16; the code's baseline and extra
+// bits come from code_base()
+HD uint32_t lp_ent(uint32_t code, uint32_t nb, uint32_t next) { return code | nb << 8 | next << 16; }
 
 // The LP phases keep their input / output pointers in LDS (per block), so
 // the compiler no longer sees that they are global: accesses would become
@@ -2268,7 +2261,7 @@ template <class T>
 HD ZG T *zg(T *p) { return (ZG T *)p; }
 
 HD bool fse_build4(uint32_t *tab, const int16_t *norm, uint32_t nsym, uint32_t al,
-                   uint16_t *snext, uint32_t kind) {
+                   uint16_t *snext) {
   const uint32_t size = 1u << al, mask = size - 1;
   uint32_t high = size - 1;
   for (uint32_t s = 0; s < nsym; ++s) {
@@ -2292,7 +2285,7 @@ HD bool fse_build4(uint32_t *tab, const int16_t *norm, uint32_t nsym, uint32_t a
     const uint32_t s = tab[u] & 255;
     const uint32_t nx = snext[s]++;
     const uint32_t nb = al - hibit(nx);
-    tab[u] = lp_ent(s, nb, (nx << nb) - size, kind);
+    tab[u] = lp_ent(s, nb, (nx << nb) - size);
   }
   return true;
 }
@@ -2314,18 +2307,18 @@ HD bool seq_table4(S &s, const Ctx &c, uint32_t mode, uint32_t kind, uint32_t &p
     const uint32_t n = kind == kLL ? 36 : kind == kML ? 53 : 29;
     for (uint32_t i = 0; i < n; ++i) s.norm[i] = src[i];
     al = kind == kOF ? 5 : 6;
-    fse_build4(tab, s.norm, n, al, s.snext, kind);
+    fse_build4(tab, s.norm, n, al, s.snext);
   } else if (m == 1) {
     if (q >= qend) return ZF(false);
     const uint32_t sym = gbyte(c, q++);
     if (sym > maxsym) return ZF(false);
-    tab[0] = lp_ent(sym, 0, 0, kind);
+    tab[0] = lp_ent(sym, 0, 0);
     al = 0;
   } else {
     FR f{q, qend, 0};
     uint32_t nsym;
     if (!fse_norm(c, f, s.norm, maxsym, maxal, nsym, al)) return ZF(false);
-    if (!fse_build4(tab, s.norm, nsym, al, s.snext, kind)) return ZF(false);
+    if (!fse_build4(tab, s.norm, nsym, al, s.snext)) return ZF(false);
     q += f.bit >> 3;
   }
   if (!repeat) {
@@ -2854,15 +2847,14 @@ HD void lp_seq_chunk(LpS &s, const uint32_t *ctab) {
   for (uint32_t i = 0; i < m; ++i) {
     const bool more = i + 1 < left;           // the block's last sequence reads no state bits
     const uint32_t eo = s.tof[sof], em = s.tml[sml], el = s.tll[sll];
-    // baselines: off the state chain (lp_ent carries the extra-bit counts)
-    const uint32_t mb = ctab[36 + (em & 63)] & 0xFFFFFF, lb = ctab[el & 63] & 0xFFFFFF;
-    const uint32_t oa = ubfe(eo, 6, 5), ob = 1u << oa;
-    const uint32_t ma = ubfe(em, 6, 5), la = ubfe(el, 6, 5);
+    const uint32_t cm = ctab[36 + (em & 255)], cl = ctab[el & 255];
+    const uint32_t oa = eo & 255, ob = 1u << oa;
+    const uint32_t ma = cm >> 24, mb = cm & 0xFFFFFF, la = cl >> 24, lb = cl & 0xFFFFFF;
     br_need(b, s, w, 47);
     const uint64_t x1 = br_take(b, oa + ma);
     const uint32_t ml = mb + ubfe((uint32_t)x1, 0, ma);
     const uint32_t ofv = ob + ubfe((uint32_t)(x1 >> ma), 0, oa);
-    const uint32_t onb = ubfe(eo, 11, 5), mnb = ubfe(em, 11, 5), lnb = ubfe(el, 11, 5);
+    const uint32_t onb = (eo >> 8) & 255, mnb = (em >> 8) & 255, lnb = (el >> 8) & 255;
     br_need(b, s, w, 42);
     const uint32_t nst = more ? lnb + mnb + onb : 0;
     const uint64_t x2 = br_take(b, la + nst);

@@ -179,6 +179,8 @@ def main(argv=None) -> int:
     ap.add_argument("--dir", default="/tmp/strom_arrow")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--slot-mib", type=int, default=256)
+    ap.add_argument("--chunk-kib", type=int, default=64,
+                    help="the scan's read chunk (buffers are read as whole chunks)")
     ap.add_argument("--nslots", type=int, default=3,
                     help="HBM slots of the scan's ring (reads in flight: nslots - 1 groups)")
     ap.add_argument("--columns", default="val,x")
@@ -209,7 +211,7 @@ def main(argv=None) -> int:
     if a.qual2:
         specs.append(("qual2", [("val", 100_000, 599_999), ("x", 0.25, 0.75)], "id"))
     res = dict(file_bytes=fsize, rows=a.rows, batch_rows=a.batch_rows, codec=("lz4_frame" if a.codec == "lz4" else "zstd") + " (pyarrow)",
-               slot_mib=a.slot_mib, nslots=a.nslots, reps=a.reps, columns={})
+               slot_mib=a.slot_mib, nslots=a.nslots, chunk_kib=a.chunk_kib, reps=a.reps, columns={})
     fd = os.open(path, os.O_RDONLY)
     cols_np = {}
     # once per process: the first scan also loads the decoder/filter code
@@ -237,7 +239,8 @@ def main(argv=None) -> int:
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
                 if sc is None:                  # cold: open + plan + allocate
-                    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20, nslots=a.nslots)
+                    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20, nslots=a.nslots,
+                                   chunk_sz=a.chunk_kib << 10)
                     t_open = time.perf_counter() - t1
                 out = sc.scan_where(quals, project=proj)
                 dt = time.perf_counter() - t1
