@@ -987,8 +987,9 @@ int strom_host_costs(int fd, uint64_t *out, int n) {
 //   2 open_file (fstat + cache)    3 completion bookkeeping (histograms,
 //   counters, mapping in-flight count) — finish_request and the stats adds
 //   4 / 5 the per-thread cached forms of 0 / 2 (pread_sync uses them)
-//   6 a 4 KiB BAR store + posted HDP flush   7 the first locked instruction
-//   after it (0 / 0 without a BAR mapping)
+//   6 a 4 KiB BAR store (memcpy) + posted HDP flush   7 the first locked
+//   instruction after it   8 / 9 the same with whole-line non-temporal
+//   stores (config bar_nt); 0 without a BAR mapping
 int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   using namespace strom;
   if (n <= 0 || fd < 0) return -EINVAL;
@@ -1022,22 +1023,24 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   out[5] = bench([&] { sink += (uint64_t)(engine().open_file_cached(fd, &err) != nullptr); });
   // a 4 KiB store through the BAR with its (posted) HDP flush, then the
   // first locked instruction after it: is the write's drain paid there?
-  out[6] = out[7] = 0;
+  out[6] = out[7] = out[8] = out[9] = 0;
   if (g->bar && g->length >= 4096) {
     alignas(64) static uint8_t src[4096];
     std::atomic<uint64_t> ctr{0};
-    uint64_t store = 0, lock = 0;
-    for (int i = 0; i < n; ++i) {
-      const uint64_t t0 = mono_ns();
-      g->bar_write(g->va, src, 4096, true);
-      const uint64_t t1 = mono_ns();
-      ctr.fetch_add(1);
-      const uint64_t t2 = mono_ns();
-      store += t1 - t0;
-      lock += t2 - t1;
+    for (int mode = 0; mode < 2; ++mode) {
+      uint64_t store = 0, lock = 0;
+      for (int i = 0; i < n; ++i) {
+        const uint64_t t0 = mono_ns();
+        g->bar_write_mode(g->va, src, 4096, mode);
+        const uint64_t t1 = mono_ns();
+        ctr.fetch_add(1);
+        const uint64_t t2 = mono_ns();
+        store += t1 - t0;
+        lock += t2 - t1;
+      }
+      out[6 + 2 * mode] = store / (uint64_t)n;
+      out[7 + 2 * mode] = lock / (uint64_t)n;
     }
-    out[6] = store / (uint64_t)n;
-    out[7] = lock / (uint64_t)n;
     sink += ctr.load();
   }
   return 0;

@@ -78,6 +78,8 @@ struct Config {
                                  // pinning); falls back to READ when the
                                  // kernel or RLIMIT_MEMLOCK refuses
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
+  int bar_nt = 0;                // BAR stores: 1 whole-line non-temporal (AVX-512 /
+                                 // AVX2), 0 memcpy
   uint32_t ingest_min = 0;       // worker requests below this go staging -> BAR by
                                  // CPU stores even when the ingest grid runs
   bool io_prof = false;          // per-worker phase attribution (strom_io_prof)
@@ -226,6 +228,7 @@ struct GpuMapping {
   // false when the range is not BAR-mapped.  Ends with a read-back that
   // flushes the posted writes, so the data is in HBM when this returns.
   bool bar_write(uint64_t dst, const void *src, size_t len, bool flush = true) const;
+  bool bar_write_mode(uint64_t dst, const void *src, size_t len, int mode) const;
   // make CPU stores through the BAR (ending at `last`) visible to shaders:
   // sfence, then an HDP flush (write + read back the flush register, as
   // the runtime does for CPU-written kernargs in VRAM); without the

@@ -58,10 +58,52 @@ namespace strom {
 // ------------------------------------------------------- GPU registry
 GpuMapping::~GpuMapping() { hip::bar_unmap(bar, bar_len); }
 
+// Copy into write-combining BAR memory with whole-line (64-byte)
+// non-temporal stores, so every WC buffer leaves the core as one full-line
+// PCIe write (config bar_nt; memcpy's store mix is the default).
+__attribute__((target("avx512f"))) static void bar_copy_nt512(uint8_t *d, const uint8_t *s,
+                                                              size_t n) {
+  size_t i = 0;
+  for (; i + 64 <= n; i += 64)
+    _mm512_stream_si512((__m512i *)(d + i), _mm512_loadu_si512((const void *)(s + i)));
+  if (i < n) memcpy(d + i, s + i, n - i);
+}
+
+__attribute__((target("avx2"))) static void bar_copy_nt256(uint8_t *d, const uint8_t *s,
+                                                           size_t n) {
+  size_t i = 0;
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256((__m256i *)(d + i), _mm256_loadu_si256((const __m256i *)(s + i)));
+  if (i < n) memcpy(d + i, s + i, n - i);
+}
+
+void bar_copy(uint8_t *d, const void *src, size_t n, int mode) {
+  static const int have512 = __builtin_cpu_supports("avx512f") ? 1 : 0;
+  static const int have256 = __builtin_cpu_supports("avx2") ? 1 : 0;
+  const uint8_t *s = (const uint8_t *)src;
+  // 64-byte aligned destinations only: a line split over two WC buffers
+  // gains nothing
+  if (mode && !((uintptr_t)d & 63)) {
+    if (have512) return bar_copy_nt512(d, s, n);
+    if (have256) return bar_copy_nt256(d, s, n);
+  }
+  memcpy(d, s, n);
+}
+
+// one BAR store of len bytes with the given copy mode and its HDP flush
+// (strom_engine_costs A/B)
+bool GpuMapping::bar_write_mode(uint64_t dst, const void *src, size_t len, int mode) const {
+  if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
+  uint8_t *p = bar + (dst - bar_va);
+  bar_copy(p, src, len, mode);
+  bar_flush(p + ((len - 1) & ~(size_t)3));
+  return true;
+}
+
 bool GpuMapping::bar_write(uint64_t dst, const void *src, size_t len, bool flush) const {
   if (!bar || len == 0 || dst < bar_va || dst + len > bar_va + bar_len) return false;
   uint8_t *p = bar + (dst - bar_va);
-  memcpy(p, src, len);
+  bar_copy(p, src, len, config().bar_nt);
   phase_mark(4);
   if (flush) bar_flush(p + ((len - 1) & ~(size_t)3));
   phase_mark(5);

@@ -178,7 +178,8 @@ def host_costs(fd: int, n: int = 20000) -> dict:
 
 
 ENGINE_COSTS = ("registry_get", "validate", "open_file", "completion", "registry_get_cached",
-                "open_file_cached", "bar_store_4k", "lock_after_bar_store")
+                "open_file_cached", "bar_store_4k", "lock_after_bar_store", "bar_store_4k_nt",
+                "lock_after_bar_store_nt")
 
 
 def engine_costs(handle: int, fd: int, n: int = 20000) -> dict:
