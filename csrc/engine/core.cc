@@ -34,7 +34,7 @@ Config Config::from_env() {
   Config c;
   static const char *keys[] = {"backend", "workers", "queue_depth", "max_request",
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
-                               "bar_map", "bar_max", "bar_nt", "coalesce", "trace",
+                               "bar_map", "bar_max", "bar_nt", "inline_plain", "coalesce", "trace",
                                "ingest", "ingest_grid", "ingest_piece", "ingest_min", "ingest_prio", "hdp_sync",
                                "fixed_bufs", "io_prof",
                                "strict", "direct_io",
@@ -113,6 +113,7 @@ int Config::set(const std::string &k, const std::string &v) {
     bar_max = (uint32_t)n;
     return 0;
   }
+  if (k == "inline_plain") { inline_plain = parse_bool(v); return 0; }
   if (k == "bar_nt") {
     if (!num_ok) { bar_nt = parse_bool(v) ? 1 : 0; return 0; }
     if (n < 0 || n > 1) return -EINVAL;
@@ -159,6 +160,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;
   else if (k == "bar_nt") v = bar_nt;
+  else if (k == "inline_plain") v = inline_plain;
   else if (k == "strict") v = strict;
   else if (k == "direct_io") v = direct_io;
   else if (k == "pgcache_probe") v = pgcache_probe;

@@ -80,6 +80,8 @@ struct Config {
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
   int bar_nt = 0;                // BAR stores: 1 whole-line non-temporal (AVX-512 /
                                  // AVX2), 0 memcpy
+  bool inline_plain = false;     // synchronous reads bound for the BAR land in plain
+                                 // (unpinned) memory: CPU stores need no pinning
   uint32_t ingest_min = 0;       // worker requests below this go staging -> BAR by
                                  // CPU stores even when the ingest grid runs
   bool io_prof = false;          // per-worker phase attribution (strom_io_prof)

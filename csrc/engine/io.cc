@@ -1013,6 +1013,8 @@ IoEngine::~IoEngine() {
 struct InlineCtx {
   uint8_t *buf = nullptr;
   size_t cap = 0;
+  uint8_t *plain = nullptr;      // config inline_plain: unpinned bounce for BAR stores
+  size_t plain_cap = 0;
   int dev = -1;
   hipStream_t st = nullptr;
   hipEvent_t ev = nullptr;
@@ -1045,16 +1047,31 @@ void IoEngine::run_inline(IoReq &r) {
     c.cap = cap;
   }
   const int rfd = config().backend == BackendKind::kCache && r.fd_buffered >= 0 ? r.fd_buffered : r.fd;
-  long got = frc ? frc : pread_full(rfd, c.buf, len, r.off);
+  // a read the CPU will store through the BAR needs no pinned bounce
+  const bool to_bar = r.len <= config().bar_max && r.gmap && r.gmap->bar;
+  uint8_t *rb = c.buf;
+  if (to_bar && config().inline_plain) {
+    if (c.plain_cap < r.len) {
+      free(c.plain);
+      c.plain_cap = 0;
+      const size_t cap = std::max<size_t>(r.len, 64u << 10);
+      c.plain = posix_memalign((void **)&c.plain, 4096, cap) == 0 ? c.plain : nullptr;
+      if (c.plain) c.plain_cap = cap;
+    }
+    if (c.plain) rb = c.plain;
+  }
+  long got = frc ? frc : pread_full(rfd, rb, len, r.off);
   uint64_t t1 = mono_ns();
   if (tl_phase) tl_phase[3] = t1;
   stats().io_ns.add(t1 - t0);
-  long status = finalize_read(r, c.buf, len, got);
+  long status = finalize_read(r, rb, len, got);
   Ingest *ing = nullptr;
   uint64_t first = 0;
   uint32_t nseq = 0;
-  if (status == 0 && r.len <= config().bar_max && r.gmap &&
-      r.gmap->bar_write(r.gpu_dst, c.buf, r.len)) {
+  const bool bar_ok = status == 0 && to_bar && r.gmap->bar_write(r.gpu_dst, rb, r.len);
+  // the other paths below read the pinned bounce
+  if (!bar_ok && status == 0 && rb != c.buf) memcpy(c.buf, rb, r.len);
+  if (bar_ok) {
     stats().copy_ns.add(mono_ns() - t1);
     stats().nr_debug[0].fetch_add(1, std::memory_order_relaxed);
   } else if (status == 0 && ing_ok && r.gmap && (ing = Ingest::get(r.device)) &&
