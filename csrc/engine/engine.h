@@ -78,8 +78,11 @@ struct Config {
                                  // pinning); falls back to READ when the
                                  // kernel or RLIMIT_MEMLOCK refuses
   uint32_t bar_max = 256u << 10; // requests up to this go staging -> BAR by CPU
-  int bar_nt = 0;                // BAR stores: 1 whole-line non-temporal (AVX-512 /
-                                 // AVX2), 0 memcpy
+  int bar_nt = 1;                // BAR stores: 1 whole-line non-temporal (AVX-512 /
+                                 // AVX2), 0 memcpy.  QD1 4 KiB: the drain paid at
+                                 // the next locked instruction 554 -> 382 ns, p50
+                                 // 5.04 -> 4.16 us on storage, 1.62 -> 1.44 engine-only
+                                 // (profiles/r5/qd1/qd1_ab_r5p.json)
   bool inline_plain = false;     // synchronous reads bound for the BAR land in plain
                                  // (unpinned) memory: CPU stores need no pinning
   uint32_t ingest_min = 0;       // worker requests below this go staging -> BAR by

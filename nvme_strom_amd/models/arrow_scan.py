@@ -213,7 +213,10 @@ class ArrowScan:
     # profiles/r3/arrow_group_policy_ab/.)
     ROUND_STREAMS_PER_CU = int(os.environ.get("STROM_ARROW_ROUND_PER_CU", "3"))
     # ZSTD groups: 1 / ZSTD_ROUND_DIV of the zstd decoder's resident round
-    ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "1"))
+    # (lane-parallel decoder: 2, four groups for config 5's val — its
+    # decode latency is per block, so a group's decode overlaps the next
+    # groups' reads; 4+ groups lose to the reads' interleaving)
+    ZSTD_ROUND_DIV = int(os.environ.get("STROM_ARROW_ZSTD_DIV", "2"))
     # the zstd decoder per group launch: 2 lane-parallel (default: the
     # blocks' entropy stages on the lanes of a wave, so a group's decode
     # takes about one block's latency, not one stream's), None the wave /
@@ -222,16 +225,22 @@ class ArrowScan:
     ZSTD_MODE = (int(os.environ["STROM_ARROW_ZSTD_MODE"])
                  if os.environ.get("STROM_ARROW_ZSTD_MODE") else 2)
 
-    def __init__(self, path: str, device=None, chunk_sz: int = 64 << 10,
-                 slot_bytes: int = 256 << 20, nslots: int = 3,
+    def __init__(self, path: str, device=None, chunk_sz: Optional[int] = None,
+                 slot_bytes: int = 256 << 20, nslots: Optional[int] = None,
                  max_slot_bytes: int = 4 << 30):
+        """``chunk_sz`` / ``nslots`` default by the file's codec: LZ4 64 KiB
+        chunks, 3 slots; ZSTD 16 KiB chunks (a buffer is read as whole
+        chunks: 600 -> 500 MB read for config 5's ``val``) and 4 slots, so
+        the reads of every one of its groups are in flight behind the first
+        (profiles/r5/zstd_arrow/group_ab/)."""
         self.path = path
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self.meta: ArrowFile = read_metadata(path)
-        self.chunk_sz = chunk_sz
+        zstd = set(self.meta.codecs) - {None} == {"zstd"}
+        self.chunk_sz = chunk_sz if chunk_sz else ((16 << 10) if zstd else (64 << 10))
         self.slot_bytes = slot_bytes
         self.max_slot_bytes = max(slot_bytes, max_slot_bytes)
-        self.nslots = max(2, nslots)
+        self.nslots = max(2, nslots if nslots else (4 if zstd else 3))
         self.reader: Optional[FileReader] = None
         self._slots: List[_Slot] = []
         self._wbs: List[Optional[torch.Tensor]] = []
@@ -755,7 +764,9 @@ class ArrowScan:
                            offsets=torch.zeros(1, dtype=torch.int64, device=self.device)
                            if pstrings else None)
         self._ensure_slots(groups)
-        self.emit_stream = torch.cuda.Stream(device=self.device)
+        # one emit stream per scan object (its library-kept scratch follows it)
+        if getattr(self, "emit_stream", None) is None:
+            self.emit_stream = torch.cuda.Stream(device=self.device)
         z = lambda: torch.zeros(1, dtype=torch.int64, device=self.device)
         state = dict(out=out, cursor=z(), count=z(), err=z(), wait_s=0.0, bytes_read=0,
                      column_bytes=0, pout=pout, pvalid=pvalid, pchars=pchars, poff=poff,

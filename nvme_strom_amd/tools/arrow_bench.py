@@ -179,9 +179,9 @@ def main(argv=None) -> int:
     ap.add_argument("--dir", default="/tmp/strom_arrow")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--slot-mib", type=int, default=256)
-    ap.add_argument("--chunk-kib", type=int, default=64,
-                    help="the scan's read chunk (buffers are read as whole chunks)")
-    ap.add_argument("--nslots", type=int, default=3,
+    ap.add_argument("--chunk-kib", type=int, default=0,
+                    help="the scan's read chunk (buffers are read as whole chunks; 0: by codec)")
+    ap.add_argument("--nslots", type=int, default=0,
                     help="HBM slots of the scan's ring (reads in flight: nslots - 1 groups)")
     ap.add_argument("--columns", default="val,x")
     ap.add_argument("--codec", default="lz4", choices=["lz4", "zstd"],
@@ -239,8 +239,8 @@ def main(argv=None) -> int:
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
                 if sc is None:                  # cold: open + plan + allocate
-                    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20, nslots=a.nslots,
-                                   chunk_sz=a.chunk_kib << 10)
+                    sc = ArrowScan(path, "cuda", slot_bytes=a.slot_mib << 20, nslots=a.nslots or None,
+                                   chunk_sz=(a.chunk_kib << 10) or None)
                     t_open = time.perf_counter() - t1
                 out = sc.scan_where(quals, project=proj)
                 dt = time.perf_counter() - t1
