@@ -63,9 +63,10 @@ struct Config {
   bool ingest = true;            // staged reads reach HBM through the GPU ingest
                                  // grid (ingest.hip) instead of SDMA copies
   int ingest_grid = 16;          // workgroups of the ingest grid (CUs it holds)
-  int ingest_prio = 0;           // 1: the grid's stream is created at the
-                                 // greatest priority (a hardware queue of its
-                                 // own, not shared with normal-priority streams)
+  int ingest_prio = 1;           // 1: the grid's stream is a greatest-priority
+                                 // non-blocking one (a hardware queue of its own);
+                                 // 0: a CU-masked stream (its own queue too, but
+                                 // blocking: it synchronizes with the NULL stream)
   uint32_t ingest_piece = 256u << 10;  // bytes per ingest descriptor
   int hdp_sync = 2;              // HDP flush after CPU stores through the BAR:
                                  // 0 posted; 1 read back after every write; 2 read

@@ -106,8 +106,14 @@ bool Ingest::init() {
   // hands normal-priority streams GPU_MAX_HW_QUEUES (4) queues round-robin,
   // so a process with more streams aliases them; a CU-masked stream always
   // gets a new queue (tools/probe/hwq_probe.py), so the grid's stream is one
-  // with every CU in its mask.  ingest_prio=1: a greatest-priority stream
-  // instead (the first one of its priority also gets its own queue).
+  // with every CU in its mask.  ingest_prio=1 (default): a greatest-priority
+  // non-blocking stream instead — the first one of its priority also gets a
+  // queue of its own, and unlike the CU-masked stream (created blocking:
+  // there is no flags argument) it does not synchronize with the NULL
+  // stream.  A blocking grid stream made every NULL-stream launch or event
+  // (PyTorch's default stream) wait for the persistent grid to go idle: the
+  // Arrow ZSTD decodes, queued behind a wait on the default stream, started
+  // only after all reads (r5q trace, profiles/r5/zstd_arrow).
   bool made = false;
   if (!config().ingest_prio) {
     int cus = 0;

@@ -584,9 +584,12 @@ class ArrowScan:
         state["marks"].append((k, "landed", t1))
         region = self._hbm.tensor[s.off:s.off + len(g.ids) * self.chunk_sz]
         # write-back copies of page-cache chunks (FileReader.submit without a
-        # BAR) were queued on the current stream
+        # BAR) were queued on the current stream; only then wait for it (a
+        # wait on the default stream also waits for whatever blocking
+        # streams hold)
         cs = s.stream
-        cs.wait_stream(torch.cuda.current_stream(self.device))
+        if res.nr_ram:
+            cs.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(cs):
             if res.nr_ram and not np.array_equal(landed, g.ids.astype(np.uint32)):
                 # page-cache chunks landed at the tail: restore chunk order

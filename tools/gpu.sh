@@ -10,6 +10,8 @@
 #   zpmc       two PMC passes (issue / wait / LDS / memory mix) over zstd_bench val + x
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
+#   zlibs      zstd decoder builds A/B (lib/zv/*.so, ZLIBS)
+#   zgroups    Arrow ZSTD scan group count / read chunk / slots A/B (ZGROUPS)
 #   zatrace    kernel trace of the Arrow ZSTD scan per group size (ingest grid vs decoder)
 #   mtests     model-level GPU tests only (PG / Arrow / multi-rank scans)
 #   smoke      __graft_entry__.smoke()
@@ -24,7 +26,7 @@
 #   esweep     engine-only sweep (backend=cache) with per-worker attribution
 #   lz4par     block-parallel LZ4 decoder by stream count (LZ4PAR_STREAMS / _KINDS / _ARGS)
 #   dist       multi-rank Arrow / PG scans: 1 rank (RCCL) and 2 gloo ranks (DIST_ARGS)
-#   overlap    load <-> side-stream collective overlap test + bench (both grid priorities)
+#   overlap    load <-> side-stream collective overlap test + bench (priority and CU-masked grid streams)
 #   otrace     rocprofv3 kernel trace of overlap_bench + grid/side concurrency summary
 #   odtrace    the same with the zstd decoder as the side work (LDS co-residency)
 #   benchtests bench.py contract tests (tests/test_gpu_bench.py)
@@ -75,6 +77,16 @@ for phase in "$@"; do
                  --no-lz4 --iters 1) || exit 1
           done ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
+    zlibs) # same-process A/B of zstd decoder builds in nvme_strom_amd/lib/zv/ (ZLIBS=a,b ZSTREAMS=...)
+          step zlibs 400 python -u -m nvme_strom_amd.tools.zstd_bench --libs ${ZLIBS:?ZLIBS} --kinds val,ids,x,text \
+            --levels 1 --streams ${ZSTREAMS:-2048} --no-lz4 --out "$OUT/zlibs.json" ;;
+    zgroups) # Arrow ZSTD scan: group count x read chunk x slots, arms in one call (ZGROUPS="div:chunk_kib:nslots ...")
+          for arm in ${ZGROUPS:-1:64:3 2:16:4 1:16:3}; do
+            IFS=: read -r dv ck ns <<< "$arm"
+            STROM_ARROW_ZSTD_DIV=$dv step zg_${dv}_${ck}_${ns} 300 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd \
+              --columns val --no-strings --reps ${ZREPS:-7} --chunk-kib $ck --nslots $ns --slot-mib 1024 \
+              --out "$OUT/zg_${dv}_${ck}_${ns}.json"
+          done ;;
     zatrace) # kernel trace of the Arrow ZSTD scan at ZATRACE_DIVS group sizes: ingest grid vs decoder concurrency
           for dv in ${ZATRACE_DIVS:-1 4}; do
             (cd /tmp && STROM_ARROW_ZSTD_DIV=$dv step zatrace_d$dv 300 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -113,8 +125,8 @@ for phase in "$@"; do
                --n 2,8 --out "$OUT/overlap.json"
              step overlap_dec 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 512 --steps 6 --calibrate \
                --side decode --n 2 --out "$OUT/overlap_dec.json"
-             STROM_INGEST_PRIO=1 step overlap_prio 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 \
-               --gather-reps ${OV_REPS:-8} --n 2,8 --out "$OUT/overlap_prio.json" ;;
+             STROM_INGEST_PRIO=0 step overlap_cumask 300 python -u -m nvme_strom_amd.tools.overlap_bench --window-mib 256 --steps 12 \
+               --gather-reps ${OV_REPS:-8} --n 2,8 --out "$OUT/overlap_cumask.json" ;;
     odtrace) # the ingest grid next to the LDS-heavy zstd decoder: kernel trace + concurrency summary
             (cd /tmp && step odtrace 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/odtrace" -o trace \
               -- python3 -m nvme_strom_amd.tools.overlap_bench --side decode --calibrate --n 2 --modes overlap --window-mib 512 --steps 6 \
