@@ -77,7 +77,7 @@ __attribute__((target("avx2"))) static void bar_copy_nt256(uint8_t *d, const uin
   if (i < n) memcpy(d + i, s + i, n - i);
 }
 
-void bar_copy(uint8_t *d, const void *src, size_t n, int mode) {
+static void bar_copy(uint8_t *d, const void *src, size_t n, int mode) {
   static const int have512 = __builtin_cpu_supports("avx512f") ? 1 : 0;
   static const int have256 = __builtin_cpu_supports("avx2") ? 1 : 0;
   const uint8_t *s = (const uint8_t *)src;

@@ -176,14 +176,13 @@ def main(argv=None) -> int:
                 kw["buffered"] = a.engine_only
                 evict(fd)
                 riops, rgib = S.raw_read_rate(fd, B, nraw, sequential=True, **kw)
-                if not a.engine_only:
-                    # registered 2 MiB-page buffers (READ_FIXED, as the
-                    # engine's pinned staging): the better one is the ceiling
-                    evict(fd)
-                    fi, fg = S.raw_read_rate(fd, B, nraw, sequential=True, fixed=True, **kw)
-                    row.update(raw_plain_GiBps=round(rgib, 2), raw_fixed_GiBps=round(fg, 2))
-                    if fg > rgib:
-                        riops, rgib = fi, fg
+                # registered 2 MiB-page buffers (READ_FIXED, as the engine's
+                # pinned staging): the better one is the ceiling
+                evict(fd)
+                fi, fg = S.raw_read_rate(fd, B, nraw, sequential=True, fixed=True, **kw)
+                row.update(raw_plain_GiBps=round(rgib, 2), raw_fixed_GiBps=round(fg, 2))
+                if fg > rgib:
+                    riops, rgib = fi, fg
                 evict(fd)
                 _, rgib_rand = S.raw_read_rate(fd, B, nraw, **kw)
                 row.update(raw_iops=round(riops), raw_GiBps=round(rgib, 2),
