@@ -211,3 +211,18 @@ def test_host_scan2_cnf_matches_brute_force():
         assert items == [i for i, w in zip(ids, want) if w is True]
         rech = {i >> 16 for i, w in zip(ids, want) if w is None}
         assert {p for p, s in enumerate(status) if s & T.PAGE_RECHECK} == rech
+
+
+def test_program_rejects_kind_mismatches():
+    """A qual whose op does not fit its column's type is refused at compile
+    time (the device never sees it)."""
+    from nvme_strom_amd.ops import heapscan as H
+    desc, _ = heapgen.numeric_rel(4)
+    for q in (T.Qual("amt", "prefix", ("1",)), T.Qual("tag", "between", (1, 2)),
+              T.Qual("x", "text_eq", ("a",)), T.Qual("f", "text_in", (["a"],)),
+              T.Qual("amt", "frobnicate", (1,))):
+        with pytest.raises(ValueError):
+            H.Program(desc, [q])
+    # an empty IN is constant false, also under an Or
+    p = H.Program(desc, [T.Or(T.Qual("amt", "in", ([],)), T.Qual("x", "in", ([],)))])
+    assert all(q.flags & H.QUAL2_FALSE for q in p.quals)
