@@ -1024,8 +1024,12 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   // a 4 KiB store through the BAR with its (posted) HDP flush, then the
   // first locked instruction after it: is the write's drain paid there?
   out[6] = out[7] = out[8] = out[9] = 0;
-  if (g->bar && g->length >= 4096) {
-    alignas(64) static uint8_t src[4096];
+  if (g->bar && g->length >= 4096 && g->va >= g->bar_va && g->va + 4096 <= g->bar_va + g->bar_len) {
+    // the probe stores over the mapping's first 4 KiB: keep them and put
+    // them back afterwards (one slow BAR read)
+    alignas(64) static thread_local uint8_t keep[4096], src[4096];
+    memcpy(keep, g->bar + (g->va - g->bar_va), 4096);
+    memcpy(src, keep, 4096);
     std::atomic<uint64_t> ctr{0};
     for (int mode = 0; mode < 2; ++mode) {
       uint64_t store = 0, lock = 0;
@@ -1041,6 +1045,7 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
       out[6 + 2 * mode] = store / (uint64_t)n;
       out[7 + 2 * mode] = lock / (uint64_t)n;
     }
+    g->bar_write(g->va, keep, 4096, true);
     sink += ctr.load();
   }
   return 0;
