@@ -103,17 +103,6 @@ constexpr uint32_t kCkNone = 0xffu;      // checkpoint: no sequence starts in th
 #define LZ4PAR_HOPS 3
 #endif
 constexpr uint32_t HOPS = LZ4PAR_HOPS;
-// A/B switches (tools/lz4par_bench.py --variants): expansion follows
-// chains inside the thread's own entries; doubling skips entries known to
-// be roots (a register mask) instead of re-reading them every round
-#ifndef LZ4PAR_XCHAIN
-#define LZ4PAR_XCHAIN 0
-#endif
-#ifndef LZ4PAR_PEND
-#define LZ4PAR_PEND 0
-#endif
-constexpr bool XCHAIN = LZ4PAR_XCHAIN;
-constexpr bool PEND = LZ4PAR_PEND;
 static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
@@ -916,18 +905,6 @@ HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
     if ((hm >> i) & 1u) {
       cur = e;
       base = s.ptr[PI(e)];
-    } else if (XCHAIN) {
-      uint32_t d = e - cur;
-      if (!(base & kTag) && base < cur) {
-        const uint32_t off = cur - base;
-        if (d >= off) d = off == 1 ? 0 : d % off;
-      }
-      uint32_t v = base + d;
-      // a source among this thread's own earlier entries is expanded
-      // already: follow it now (heads keep their value — a later thread's
-      // run may start from one)
-      while (!(v & kTag) && v >= e0 && v < e) v = s.ptr[PI(v)];
-      s.ptr[PI(e)] = v;
     } else {
       // a match run whose source is inside the batch starts off = cur -
       // base bytes after it; past off bytes the run copies itself
@@ -947,15 +924,13 @@ HD void ph_expand(Smem &s, uint32_t t, uint32_t nb) {
 
 // (4b) one pointer-doubling round over the batch; true while any pointer
 // still points inside the batch
-HD bool ph_double(Smem &s, uint32_t t, uint32_t nb, uint32_t &pend) {
+HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
   // in order, each replacement visible to the thread's later entries (a
   // chain through this thread's entries collapses within the round;
   // reading all entries before writing any measured 30 % slower)
   bool more = false;
-  for (uint32_t k0 = 0, e = t; e < nb; ++k0, e += NT) {
-    if (PEND && !((pend >> k0) & 1u)) continue;
+  for (uint32_t e = t; e < nb; e += NT) {
     const uint32_t v = s.ptr[PI(e)];
-    if (PEND && (v & kTag)) pend &= ~(1u << k0);
     if (!(v & kTag)) {
       // v < e always (a match reads backwards); the bound only keeps a
       // corrupt table inside the array.  HOPS > 1 follows the chain further
@@ -968,7 +943,6 @@ HD bool ph_double(Smem &s, uint32_t t, uint32_t nb, uint32_t &pend) {
       }
       s.ptr[PI(e)] = w;
       more |= !(w & kTag);
-      if (PEND && (w & kTag)) pend &= ~(1u << k0);
     }
   }
   return more;
@@ -1446,10 +1420,9 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           __syncthreads();
           LP_MARK(kLpExpand);
           bool more;
-          uint32_t pend = ~0u;
           do {
             LP_CNT(kLpNDouble);
-            more = ph_double(s, t, nb, pend);
+            more = ph_double(s, t, nb);
           } while (__syncthreads_or(more));
           LP_MARK(kLpDouble);
           Held h;
@@ -1666,12 +1639,10 @@ int lz4par_host(int codec, const uint8_t *src, uint32_t src_len, uint8_t *dst, u
         if (s.err) break;
         for (uint32_t t = 0; t < NT; ++t) ph_expand(s, t, nb);
         bool any;
-        uint32_t pend[NT];
-        for (uint32_t t = 0; t < NT; ++t) pend[t] = ~0u;
         do {
           ++dbl;
           any = false;
-          for (uint32_t t = 0; t < NT; ++t) any |= ph_double(s, t, nb, pend[t]);
+          for (uint32_t t = 0; t < NT; ++t) any |= ph_double(s, t, nb);
         } while (any);
         for (uint32_t t = 0; t < NT; ++t) ph_resolve(s, c, t, b0, nb, held[t]);
         for (uint32_t t = 0; t < NT; ++t) ph_write(s, c, t, b0, nb, held[t]);
