@@ -335,7 +335,7 @@ HD uint32_t br_read(BR &b, const S &s, const Win &w, const Ctx &c, uint32_t k) {
 // stream (cbase < 0, those bits zeroed), so an extraction is one shift and
 // mask with no branch; the fill offset is clamped into the window so that
 // even a corrupt stream cannot read outside it.  br_need(k) makes k <= 56
-// bits available, br_look / br_get64 then extract them.
+// bits available, br_take then extracts them.
 // bits [off, off + w) of v, w <= 31, off + w <= 32; w = 0 gives 0
 HD uint32_t ubfe(uint32_t v, uint32_t off, uint32_t w) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -382,17 +382,6 @@ HD void br_wfill(BR &b, const S &s, const Win &w) {
 template <class S>
 HD void br_need(BR &b, const S &s, const Win &w, uint32_t k) {
   if (b.nbits - (int32_t)k < b.cbase) br_wfill(b, s, w);
-}
-
-HD uint32_t br_look(const BR &b, uint32_t k) {   // after br_need(>= k); k = 0 gives 0
-  const uint32_t lo = (uint32_t)(b.nbits - (int32_t)k - b.cbase) & 63;
-  return (uint32_t)((b.cont >> lo) & ((1ull << k) - 1));
-}
-
-HD uint64_t br_get64(BR &b, uint32_t k) {        // k <= 56, after br_need(>= k)
-  const uint32_t lo = (uint32_t)(b.nbits - (int32_t)k - b.cbase) & 63;
-  b.nbits -= (int32_t)k;
-  return (b.cont >> lo) & ((1ull << k) - 1);
 }
 
 // consume k bits (after br_need(>= k)) and return the container shifted
