@@ -99,10 +99,6 @@ constexpr uint32_t kCkNone = 0xffu;      // checkpoint: no sequence starts in th
 // / 114 GB/s (text / val / ids, one hop) to 133 / 136 / 125, snappy 111 /
 // 105 / 97 to 126 / 115 / 107; 4 hops lose again on text / ids (LDS
 // latency per round), profiles/r5/lz4par/lz4par_hops_ab_r5j.json
-#ifndef LZ4PAR_HW2
-#define LZ4PAR_HW2 0
-#endif
-constexpr bool HW2 = LZ4PAR_HW2;   // history dwords in the resolve (A/B)
 #ifndef LZ4PAR_HOPS
 #define LZ4PAR_HOPS 3
 #endif
@@ -965,24 +961,6 @@ HD uint8_t hist_byte(const Ctx &c, uint32_t pos) {
 #endif
 }
 
-// the four stored bytes at [pos, pos + 4): one or two aligned dword loads
-// (L1-bypassing, as hist_byte)
-HD uint32_t hist_word(const Ctx &c, uint32_t pos) {
-#ifdef __HIP_DEVICE_COMPILE__
-  const uintptr_t a = (uintptr_t)(c.out + pos);
-  const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-  const uint32_t sh = 8 * (uint32_t)(a & 3);
-  const uint32_t d0 = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (!sh) return d0;
-  const uint32_t d1 = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_amdgcn_alignbit(d1, d0, sh);
-#else
-  uint32_t v;
-  memcpy(&v, c.out + pos, 4);
-  return v;
-#endif
-}
-
 HD uint8_t resolve(const Smem &s, const Ctx &c, uint32_t v) {
   if (v & kLit) return inb(s, c, v & ~kLit);
   return hist_byte(c, v & ~kHist);
@@ -1004,22 +982,6 @@ HD void ph_resolve(const Smem &s, const Ctx &c, uint32_t t, uint32_t b0, uint32_
     const uint32_t k = t + j * NT;
     uint32_t w = 0;
     if (k < nw) {
-      if (HW2) {
-        // four consecutive bytes of stored history (a match's run): two
-        // aligned dword loads instead of four
-        const int32_t e0 = (int32_t)(4 * k) - (int32_t)mis;
-        if (e0 >= 0 && (uint32_t)e0 + 4 <= nb) {
-          const uint32_t v0 = s.ptr[PI(e0)];
-          if ((v0 & kTag) == kHist && s.ptr[PI(e0 + 3)] == v0 + 3 && s.ptr[PI(e0 + 1)] == v0 + 1 &&
-              s.ptr[PI(e0 + 2)] == v0 + 2) {
-            const uint32_t hp = v0 & ~kHist;
-            if (!(HR && bs - hp <= HR)) {
-              h.w[j] = hist_word(c, hp);
-              continue;
-            }
-          }
-        }
-      }
       for (uint32_t b = 0; b < 4; ++b) {
         const int32_t e = (int32_t)(4 * k + b) - (int32_t)mis;
         if (e < 0 || (uint32_t)e >= nb) continue;
