@@ -385,3 +385,52 @@ def test_stripe_set_to_hbm(S, tmp_path):
         torch.cuda.synchronize()
         assert t.numel() == size
         assert V.crc32c(t) == S.crc32c_host(data.tobytes())
+
+
+def test_default_stream_runs_while_grid_reads(S, tmp_path):
+    """Work on PyTorch's default stream, and a side stream ordered after it
+    by an event (as the Arrow scan's decode streams are), goes through while
+    a large read is still landing through the persistent ingest grid — the
+    grid never holds other streams' work until it goes idle."""
+    import time
+    from nvme_strom_amd.tensor import FileReader, HbmBuffer
+    S.configure(ingest=1)
+    n = 1 << 30
+    p = str(tmp_path / "big.bin")
+    with open(p, "wb") as f:
+        blk = np.random.default_rng(31).integers(0, 256, size=64 << 20, dtype=np.uint8).tobytes()
+        for _ in range(n // len(blk)):
+            f.write(blk)
+    hb = HbmBuffer(n, "cuda")
+    chunk = 1 << 20
+    r = FileReader(p, chunk_sz=chunk, max_chunks=n // chunk)
+    try:
+        S.evict_file(r.fd)
+        x = torch.ones(1 << 20, device="cuda")
+        side = torch.cuda.Stream()
+        y = x * 2                               # kernel code loaded before timing
+        with torch.cuda.stream(side):
+            z = x * 3
+        torch.cuda.synchronize()
+        res, _ = r.submit(hb, 0, np.arange(n // chunk, dtype=np.uint32))
+        time.sleep(0.002)                       # the grid is resident now
+        t0 = time.perf_counter()
+        y = x * 2                               # default stream
+        # a side stream ordered after the default stream (an event recorded
+        # on it), as the Arrow scan's decode streams were
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            z = x * 3
+        side.synchronize()
+        torch.cuda.current_stream().synchronize()
+        t1 = time.perf_counter()
+        r.finish(res)
+        t2 = time.perf_counter()
+        assert float(y[0]) == 2.0 and float(z[0]) == 3.0
+        # the rest of a 1 GiB read takes tens of ms; the default stream
+        # came back long before it landed
+        assert t2 - t0 > 0.01, (t1 - t0, t2 - t0)
+        assert (t1 - t0) < 0.3 * (t2 - t0), (t1 - t0, t2 - t0)
+    finally:
+        r.close()
+        hb.close()
