@@ -109,11 +109,10 @@ bool Ingest::init() {
   // with every CU in its mask.  ingest_prio=1 (default): a greatest-priority
   // non-blocking stream instead — the first one of its priority also gets a
   // queue of its own, and unlike the CU-masked stream (created blocking:
-  // there is no flags argument) it does not synchronize with the NULL
-  // stream.  A blocking grid stream made every NULL-stream launch or event
-  // (PyTorch's default stream) wait for the persistent grid to go idle: the
-  // Arrow ZSTD decodes, queued behind a wait on the default stream, started
-  // only after all reads (r5q trace, profiles/r5/zstd_arrow).
+  // there is no flags argument) it is not ordered with the NULL stream by
+  // HIP's rules.  (Round 5 A/B: once the Arrow scan stopped ordering its
+  // decode streams after the default stream, both kinds overlap its decodes
+  // with the reads, profiles/r5/zstd_arrow/grid_stream_ab.)
   bool made = false;
   if (!config().ingest_prio) {
     int cus = 0;
