@@ -692,25 +692,46 @@ int qual_by_type(const strom_col_qual &q, const strom_qual_batch *bt, uint32_t n
 // / hipFreeAsync were not free: the host blocked in them until the stream's
 // queued work had drained (r5 Arrow ZSTD timeline: group k+1's emit waited
 // ~20 ms for its own decode, so the next group's launches queued late).
+struct ColScratch {
+  void *p = nullptr;
+  size_t bytes = 0;
+  uint64_t used = 0;                  // LRU clock
+};
 std::mutex g_cs_mu;
-std::map<std::pair<int, void *>, std::pair<void *, size_t>> g_cs;
+std::map<std::pair<int, void *>, ColScratch> g_cs;
+uint64_t g_cs_clock = 0;
+constexpr size_t kColScratchKeep = 64;   // streams kept (a caller cycling through
+                                         // more evicts the least recently used)
 
 // under g_cs_mu, held by the caller through its launches
 void *col_scratch(hipStream_t st, size_t bytes) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  auto &e = g_cs[{dev, (void *)st}];
-  if (e.second < bytes) {
+  const std::pair<int, void *> key{dev, (void *)st};
+  if (!g_cs.count(key) && g_cs.size() >= kColScratchKeep) {
+    auto lru = g_cs.begin();
+    for (auto j = g_cs.begin(); j != g_cs.end(); ++j)
+      if (j->second.used < lru->second.used) lru = j;
+    // its stream may still read it (hipFree waits for the device's work)
+    if (lru->second.p) (void)hipFree(lru->second.p);
+    g_cs.erase(lru);
+  }
+  ColScratch &c = g_cs[key];
+  c.used = ++g_cs_clock;
+  auto &e = c;
+  if (e.bytes < bytes) {
     // the old buffer may still be read by this stream's queued launches
-    if (e.first && (hipStreamSynchronize(st) != hipSuccess || hipFree(e.first) != hipSuccess))
+    if (e.p && (hipStreamSynchronize(st) != hipSuccess || hipFree(e.p) != hipSuccess))
       return nullptr;
-    e = {nullptr, 0};
+    e.p = nullptr;
+    e.bytes = 0;
     const size_t want = bytes < (64u << 10) ? (64u << 10) : bytes;
     void *p = nullptr;
     if (hipMalloc(&p, want) != hipSuccess) return nullptr;
-    e = {p, want};
+    e.p = p;
+    e.bytes = want;
   }
-  return e.first;
+  return e.p;
 }
 
 }  // namespace
