@@ -485,11 +485,27 @@ class ArrowScan:
         g.has_valid = pres[:, :, 1].any(axis=0)
 
     # --------------------------------------------------------- pipeline
+    # HBM for the slot ring beyond nslots (a slot per group up to this):
+    # with a slot of its own a group's read never waits for an earlier
+    # group's decode to free one (r5 timeline: date_ts group 4 was submitted
+    # 12 ms late, behind group 0's decode, and held groups 2-3's launches)
+    MAX_RING_BYTES = 8 << 30
+    MAX_SLOTS = 16
+
+    def _slot_count(self, groups: List[_Group], nbytes: int) -> int:
+        """Slots of the HBM ring: one per group while they fit MAX_RING_BYTES
+        / MAX_SLOTS, never fewer than nslots (or than the groups).  The
+        read-ahead stays nslots - 1 groups either way."""
+        n = len(groups)
+        fit = max(1, min(self.MAX_SLOTS, self.MAX_RING_BYTES // max(nbytes, 1)))
+        return max(1, min(n, max(self.nslots, fit)))
+
     def _ensure_slots(self, groups: List[_Group]) -> None:
         nbytes = max(len(g.ids) for g in groups) * self.chunk_sz
         dec = max(max(g.dec_bytes for g in groups), 64)
         words = max(max(g.words for g in groups), 1)
-        if self._slots and len(self._slots) >= min(self.nslots, len(groups)) and (
+        want_slots = self._slot_count(groups, nbytes)
+        if self._slots and len(self._slots) >= want_slots and (
                 self._slots[0].cap >= nbytes and
                             self._slots[0].dec.numel() >= dec and
                             self._slots[0].bitmap.numel() >= words):
@@ -498,7 +514,7 @@ class ArrowScan:
         # one registered HBM ring for every slot: one MAP (dma-buf export +
         # BAR mapping) per scan object instead of one per slot (cold cost);
         # no more slots than groups
-        nsl = max(1, min(self.nslots, len(groups)))
+        nsl = want_slots
         self._hbm = HbmBuffer(nbytes * nsl, self.device)
         for k in range(nsl):
             sl = _Slot(k * nbytes, nbytes,
@@ -776,7 +792,7 @@ class ArrowScan:
                      ccursor=z(), owidth=8 if pstrings and pmeta.large else 4, marks=[])
         t_alloc = time.perf_counter()
         # depth nslots - 1 of reads ahead of the group being computed
-        ahead = max(1, len(self._slots) - 1)
+        ahead = max(1, min(self.nslots, len(self._slots)) - 1)
         for k in range(min(ahead, len(groups))):
             self._submit(k, groups[k])
             state["marks"].append((k, "submitted", time.perf_counter()))
