@@ -17,6 +17,7 @@
 #include <sys/ioctl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/syscall.h>
 #include <sys/sysmacros.h>
 #include <unistd.h>
 #include <x86intrin.h>
@@ -491,10 +492,12 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
   if (strom_core_check_range(gmap->map_length - gmap->map_offset, offset, len)) return -ERANGE;
+  // phases of this path: "lookup" the mapping, "plan" the file (fstat +
+  // the per-thread cache)
+  phase_mark(0);
   int err = 0;
   const auto &f = open_file_cached(fd, &err);
   if (!f) return err;
-  phase_mark(0);
   const uint64_t size = (uint64_t)f->fc.size;
   if (file_off >= size) return -ERANGE;
   phase_mark(1);
@@ -978,6 +981,20 @@ int strom_host_costs(int fd, uint64_t *out, int n) {
   out[5] = bench([&] { std::lock_guard<std::mutex> g(mu); sink += 1; });
   std::condition_variable cv;
   out[6] = bench([&] { cv.notify_all(); });
+  // descriptor identity without a stat: kcmp(KCMP_FILE) of the descriptor
+  // against a dup of it (0 when the call is refused, e.g. by a seccomp
+  // filter); statx asking only for the inode number
+  const int d = fcntl(fd, F_DUPFD_CLOEXEC, 0);
+  const pid_t me = getpid();
+  out[7] = d < 0 || syscall(SYS_kcmp, me, me, 0 /* KCMP_FILE */, fd, d) != 0
+               ? 0
+               : bench([&] { sink += (uint64_t)syscall(SYS_kcmp, me, me, 0, fd, d); });
+  if (d >= 0) close(d);
+  struct statx sx;
+  out[8] = bench([&] {
+    statx(fd, "", AT_EMPTY_PATH | AT_STATX_DONT_SYNC, STATX_INO, &sx);
+    sink += sx.stx_ino;
+  });
   return 0;
 }
 

@@ -167,7 +167,8 @@ def io_prof(reset: bool = False) -> dict:
                 busy_ns_per_req=round(sum(v for k, v in ns.items() if k != "idle") / req, 1))
 
 
-HOST_COSTS = ("clock_gettime", "rdtsc", "fstat", "mincore", "syscall", "mutex", "cv_notify")
+HOST_COSTS = ("clock_gettime", "rdtsc", "fstat", "mincore", "syscall", "mutex", "cv_notify",
+              "kcmp_file", "statx_ino")
 
 
 def host_costs(fd: int, n: int = 20000) -> dict:
