@@ -145,3 +145,22 @@ def test_dictionary_headers_malformed(tmp_path):
             read_metadata(p, native=False)
         except ValueError:
             pass
+
+
+def test_scan_geometry_defaults_and_slots(arrow_file):
+    """Codec-dependent defaults (ZSTD: 16 KiB chunks, 4 slots; else 64 KiB, 3)
+    and the slot ring: one slot per group while it fits, never fewer than
+    nslots, never more than the groups or MAX_SLOTS."""
+    import torch
+    from nvme_strom_amd.models.arrow_scan import ArrowScan
+    path, _ = arrow_file
+    sc = ArrowScan(path, torch.device("cpu"))
+    zstd = set(sc.meta.codecs) - {None} == {"zstd"}
+    assert sc.chunk_sz == (16 << 10 if zstd else 64 << 10)
+    assert sc.nslots == (4 if zstd else 3)
+    g = [object()] * 40
+    assert sc._slot_count(g[:2], 1 << 20) == 2                 # never more than the groups
+    assert sc._slot_count(g[:10], 1 << 20) == 10               # a slot per group
+    assert sc._slot_count(g, 1 << 20) == ArrowScan.MAX_SLOTS
+    assert sc._slot_count(g, 4 << 30) == sc.nslots             # the byte cap, floored at nslots
+    assert ArrowScan(path, torch.device("cpu"), chunk_sz=8192, nslots=5).chunk_sz == 8192
