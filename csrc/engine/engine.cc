@@ -108,27 +108,71 @@ void engine_reset() {
 Engine::Engine() { io_ = std::make_unique<IoEngine>(config()); }
 Engine::~Engine() { io_.reset(); }
 
-const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *err) {
-  static thread_local struct {
-    int fd = -1;
-    const Engine *eng = nullptr;
-    std::shared_ptr<OpenFile> f;
-  } tl;
+// kcmp(KCMP_FILE) of the caller's descriptor against a dup of it taken
+// when the file was last checked: the same open file description means the
+// same file, without a stat (122 vs 215 ns on the pool boxes,
+// host_costs_ns).  -1 unknown, 0 refused here (seccomp / no CONFIG_KCMP), 1 usable.
+static std::atomic<int> g_kcmp{-1};
+
+static bool same_description(int fd, int dup) {
+  const pid_t me = getpid();
+  const long r = syscall(SYS_kcmp, me, me, 0 /* KCMP_FILE */, fd, dup);
+  if (r < 0 && g_kcmp.load(std::memory_order_relaxed) != 1) g_kcmp.store(0);
+  return r == 0;
+}
+
+struct TlFile {
+  int fd = -1;
+  int dup = -1;                        // the caller's description, kept for kcmp
+  const void *eng = nullptr;
+  std::shared_ptr<Engine::OpenFile> f;
+  ~TlFile() {
+    if (dup >= 0) close(dup);
+  }
+};
+static thread_local TlFile tl_file;
+
+void Engine::forget_cached_file() {
+  tl_file.f.reset();
+  tl_file.fd = -1;
+}
+
+const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *err, bool *fast) {
+  TlFile &tl = tl_file;
   static const std::shared_ptr<OpenFile> none;
+  if (fast) *fast = false;
+  // fast path: the same descriptor still names the same open file
+  // description (its size may have moved: callers redo a read that looks
+  // past the end or comes back short with forget_cached_file())
+  if (tl.fd == fd && tl.eng == this && tl.f && tl.dup >= 0 && g_kcmp.load(std::memory_order_relaxed) != 0 &&
+      same_description(fd, tl.dup)) {
+    g_kcmp.store(1, std::memory_order_relaxed);
+    if (fast) *fast = true;
+    return tl.f;
+  }
   struct stat st;
   if (fstat(fd, &st) != 0) {
     *err = -errno;
     return none;
   }
   const OpenFile *c = tl.f.get();
-  if (tl.fd == fd && tl.eng == this && c && c->dev == st.st_dev && c->ino == st.st_ino &&
-      c->vsize == st.st_size && c->ctim.tv_sec == st.st_ctim.tv_sec &&
-      c->ctim.tv_nsec == st.st_ctim.tv_nsec)
-    return tl.f;
-  tl.f = open_file(fd, err);
-  tl.fd = tl.f ? fd : -1;
-  tl.eng = this;
-  return tl.f ? tl.f : none;
+  const bool same = tl.fd == fd && tl.eng == this && c && c->dev == st.st_dev && c->ino == st.st_ino &&
+                    c->vsize == st.st_size && c->ctim.tv_sec == st.st_ctim.tv_sec &&
+                    c->ctim.tv_nsec == st.st_ctim.tv_nsec;
+  if (!same) {
+    tl.f = open_file(fd, err);
+    tl.eng = this;
+    if (!tl.f) {
+      tl.fd = -1;
+      return none;
+    }
+  }
+  if (tl.fd != fd || tl.dup < 0 || !same) {
+    if (tl.dup >= 0) close(tl.dup);
+    tl.dup = g_kcmp.load(std::memory_order_relaxed) != 0 ? fcntl(fd, F_DUPFD_CLOEXEC, 0) : -1;
+  }
+  tl.fd = fd;
+  return tl.f;
 }
 
 std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
@@ -496,10 +540,16 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   // the per-thread cache)
   phase_mark(0);
   int err = 0;
-  const auto &f = open_file_cached(fd, &err);
+  bool fast = false;
+  const auto &f = open_file_cached(fd, &err, &fast);
   if (!f) return err;
   const uint64_t size = (uint64_t)f->fc.size;
-  if (file_off >= size) return -ERANGE;
+  if (file_off >= size) {
+    if (!fast) return -ERANGE;
+    // the size came from the cache: check it once more with a stat
+    forget_cached_file();
+    return pread_sync(handle, offset, fd, file_off, len);
+  }
   phase_mark(1);
   long status = 0;
   IoReq r;
@@ -520,6 +570,12 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   stats().nr_setup_prps.fetch_add(1, std::memory_order_relaxed);
   phase_mark(2);
   io_->run_inline(r);
+  if (status == -EIO && fast) {
+    // short against the cached size: the file may have shrunk — redo the
+    // read with the size checked by a stat
+    forget_cached_file();
+    return pread_sync(handle, offset, fd, file_off, len);
+  }
   if (status) return status;
   return (long)len;
 }

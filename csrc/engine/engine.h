@@ -555,11 +555,15 @@ class Engine {
 
   // the per-file cache (fstat-validated): classification, descriptors, map
   std::shared_ptr<OpenFile> open_file(int fd, int *err);
-  // open_file() for the synchronous small-read path: the fstat stays (the
-  // descriptor's identity), the lock, map lookup and reference count go
-  // when this thread's last file is still the same (device, inode, ctime,
-  // size).  The reference stays valid until this thread's next call.
-  const std::shared_ptr<OpenFile> &open_file_cached(int fd, int *err);
+  // open_file() for the synchronous small-read path: when this thread's
+  // last descriptor still names the same open file description (kcmp
+  // against a dup of it; *fast set — the cached size may be stale) or, where
+  // kcmp is refused, the same (device, inode, ctime, size) by an fstat, the
+  // cached entry is returned without the lock, map lookup or reference
+  // count.  The reference stays valid until this thread's next call.
+  const std::shared_ptr<OpenFile> &open_file_cached(int fd, int *err, bool *fast = nullptr);
+  // drop this thread's cached file (the next open_file_cached stats again)
+  void forget_cached_file();
 
  private:
   int check_file(strom_check_file *a);

@@ -452,6 +452,13 @@ def test_pread_gpu_per_thread_caches(strom, rand_file):
             f.write(extra.tobytes())
         strom.pread_gpu_latency(m.handle, 0, fd, np.array([33 * 4096], dtype=np.uint64))
         assert np.array_equal(hbm[:4096], extra[4096:8192])
+        # ... and shrinks: past the new end is out of range, inside it reads
+        os.truncate(path2, 10 * 4096)
+        with pytest.raises(strom.StromError) as e:
+            strom.pread_gpu_latency(m.handle, 0, fd, np.array([20 * 4096], dtype=np.uint64))
+        assert e.value.errno == errno.ERANGE
+        strom.pread_gpu_latency(m.handle, 0, fd, np.array([5 * 4096], dtype=np.uint64))
+        assert np.array_equal(hbm[:4096], data2[5 * 4096:6 * 4096])
         strom.unmap_gpu_memory(m.handle)
     finally:
         os.close(fd)
