@@ -105,7 +105,11 @@ void engine_reset() {
   g_engine = nullptr;
 }
 
-Engine::Engine() { io_ = std::make_unique<IoEngine>(config()); }
+// every engine instance gets a new number: per-thread caches keyed by it
+// never hand a reset engine (new configuration) an entry of the old one
+static std::atomic<uint64_t> g_engine_gen{0};
+
+Engine::Engine() : gen_(g_engine_gen.fetch_add(1) + 1) { io_ = std::make_unique<IoEngine>(config()); }
 Engine::~Engine() { io_.reset(); }
 
 // kcmp(KCMP_FILE) of the caller's descriptor against a dup of it taken
@@ -124,7 +128,7 @@ static bool same_description(int fd, int dup) {
 struct TlFile {
   int fd = -1;
   int dup = -1;                        // the caller's description, kept for kcmp
-  const void *eng = nullptr;
+  uint64_t eng = 0;                    // Engine::gen_ of the entry
   std::shared_ptr<Engine::OpenFile> f;
   ~TlFile() {
     if (dup >= 0) close(dup);
@@ -144,7 +148,7 @@ const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *e
   // fast path: the same descriptor still names the same open file
   // description (its size may have moved: callers redo a read that looks
   // past the end or comes back short with forget_cached_file())
-  if (tl.fd == fd && tl.eng == this && tl.f && tl.dup >= 0 && g_kcmp.load(std::memory_order_relaxed) != 0 &&
+  if (tl.fd == fd && tl.eng == gen_ && tl.f && tl.dup >= 0 && g_kcmp.load(std::memory_order_relaxed) != 0 &&
       same_description(fd, tl.dup)) {
     g_kcmp.store(1, std::memory_order_relaxed);
     if (fast) *fast = true;
@@ -156,12 +160,12 @@ const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *e
     return none;
   }
   const OpenFile *c = tl.f.get();
-  const bool same = tl.fd == fd && tl.eng == this && c && c->dev == st.st_dev && c->ino == st.st_ino &&
+  const bool same = tl.fd == fd && tl.eng == gen_ && c && c->dev == st.st_dev && c->ino == st.st_ino &&
                     c->vsize == st.st_size && c->ctim.tv_sec == st.st_ctim.tv_sec &&
                     c->ctim.tv_nsec == st.st_ctim.tv_nsec;
   if (!same) {
     tl.f = open_file(fd, err);
-    tl.eng = this;
+    tl.eng = gen_;
     if (!tl.f) {
       tl.fd = -1;
       return none;

@@ -535,6 +535,7 @@ uint64_t buffer_id(uint64_t va);
 // -------------------------------------------------------------- engine
 class Engine {
  public:
+  const uint64_t gen_;           // instance number (per-thread caches key on it)
   Engine();
   ~Engine();
   int ioctl(int session, unsigned long cmd, void *arg);
