@@ -299,10 +299,16 @@ struct strom_heap_scan2_args {
 	/* program mode (prog != NULL; quals / nquals unused): nprog quals in
 	 * device memory, their constants in cpool (cpool_len bytes) */
 	const struct strom_heap_qual2 *prog;
-	const uint8_t *cpool;
+	const uint8_t *cpool;                 /* 8-aligned constants, cpool_len % 8 == 0 */
 	uint32_t nprog, cpool_len;
 };
 int strom_heap_scan2(const struct strom_heap_scan2_args *a, void *stream);
+/* Checks a program and its pool (host copies of what prog / cpool hold)
+ * before a launch: kinds against the attributes, contiguous clauses, every
+ * constant (IN tables and the text entries they name, numeric digits)
+ * inside the pool.  0 or -EINVAL. */
+int strom_heap_prog_check(const struct strom_heap_tupdesc *d, const struct strom_heap_qual2 *prog,
+			  uint32_t n, const uint8_t *pool, uint32_t pool_len);
 /* Projection of one attribute of the tuples `items` (page << 16 | lineno,
  * as strom_heap_scan writes them) names: values[i] (8 bytes: the int
  * sign-extended, float4 widened to double, varlena: (offset in pages <<

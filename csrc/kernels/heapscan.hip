@@ -326,12 +326,16 @@ __device__ __forceinline__ int eval_quals(const strom_heap_scan2_args &g, const 
 // qual and an undecidable one is undecidable; the tuple is dropped by a
 // false clause, else undecidable (page flagged for a host recheck) if any
 // clause is.
-__device__ __forceinline__ uint32_t pool_u32(const uint8_t *p, uint32_t o) {
-  return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) |
-         ((uint32_t)p[o + 3] << 24);
+// The pool through the constant address space (never written while the
+// kernel runs): wave-uniform dword reads are scalar loads.  Every constant
+// starts 8-aligned and the pool is padded to 8 bytes (ops/heapscan.Program).
+typedef const __attribute__((address_space(4))) uint8_t cu8;
+typedef const __attribute__((address_space(4))) uint32_t cu32;
+__device__ __forceinline__ uint32_t pool_u32(cu8 *p, uint32_t o) {   // o % 4 == 0
+  return *(cu32 *)(p + o);
 }
-__device__ __forceinline__ uint32_t pool_u16(const uint8_t *p, uint32_t o) {
-  return (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8);
+__device__ __forceinline__ uint32_t pool_u16(cu8 *p, uint32_t o) {   // o % 2 == 0
+  return (pool_u32(p, o & ~3u) >> ((o & 2) * 8)) & 0xffff;
 }
 
 // A PostgreSQL numeric (numeric.c on-disk: NumericShort / NumericLong /
@@ -372,13 +376,13 @@ __device__ __forceinline__ bool num_of_datum(const uint8_t *t, const Att &a, Num
   return ((len - 4) & 1) == 0;
 }
 
-__device__ __forceinline__ Num num_of_pool(const uint8_t *p, uint32_t o) {
+__device__ __forceinline__ Num num_of_pool(cu8 *p, uint32_t o) {
   Num n;
   n.kind = pool_u16(p, o);
   n.neg = pool_u16(p, o + 2);
   n.weight = (int16_t)pool_u16(p, o + 4);
   n.nd = pool_u16(p, o + 6);
-  n.dig = p + o + 8;
+  n.dig = (const uint8_t *)(p + o + 8);
   return n;
 }
 
@@ -435,14 +439,19 @@ __device__ __forceinline__ int num_cmp(const Num &a, const Num &b) {
   return a.neg ? -m : m;
 }
 
-__device__ __forceinline__ bool bytes_eq(const uint8_t *x, const uint8_t *y, uint32_t n) {
-  for (uint32_t k = 0; k < n; ++k)
-    if (x[k] != y[k]) return false;
+// n bytes of a tuple vs a pool constant (8-aligned, read a dword at a time)
+__device__ __forceinline__ bool bytes_eq(const uint8_t *x, cu8 *y, uint32_t n) {
+  for (uint32_t k = 0; k < n; k += 4) {
+    const uint32_t w = *(cu32 *)(y + k);
+    const uint32_t m = n - k;
+    for (uint32_t b = 0; b < 4 && b < m; ++b)
+      if (x[k + b] != ((w >> (8 * b)) & 0xff)) return false;
+  }
   return true;
 }
 
 // one qual of a program on attribute a: 1 true, 0 false, 2 undecidable
-__device__ __forceinline__ int eval_qual2(const strom_heap_qual2 &q, const uint8_t *pool,
+__device__ __forceinline__ int eval_qual2(const strom_heap_qual2 &q, cu8 *pool,
                                           const uint8_t *t, const Att &a) {
   if (q.flags & STROM_QUAL2_FALSE) return 0;
   if (q.kind == STROM_QUAL_IS_NULL) return a.null ? 1 : 0;
@@ -500,38 +509,76 @@ __device__ __forceinline__ int eval_qual2(const strom_heap_qual2 &q, const uint8
   }
 }
 
-// the program over one tuple: 1 keep, 0 drop, 2 undecidable
+// the program over one tuple: 1 keep, 0 drop, 2 undecidable.  The loop
+// over quals stays uniform across the wave (a decided lane only stops
+// evaluating; the wave leaves when every lane has decided), and the program
+// is read through the constant address space, so its entries are scalar
+// loads (profiles/r5/heap/prog_kbench.md)
 __device__ __forceinline__ int eval_prog(const strom_heap_scan2_args &g, const uint8_t *t,
                                          uint32_t tlen) {
   Deform s = deform_init(t, tlen);
   Att a;
+  a.off = a.len = a.hdr = 0;
+  a.null = true;
+  a.ext = false;
   int last = -1;
-  int verdict = 1;
+  int verdict = s.bad ? 0 : 1;
+  bool live = verdict != 0;
+  // the program through the constant address space: it is never written
+  // while the kernel runs, so its wave-uniform reads become scalar loads
+  // (a generic pointer next to the kernel's own stores gets per-lane vector
+  // loads: ~20% of the scan's time on a one-qual program)
+  typedef const __attribute__((address_space(4))) strom_heap_qual2 cqual2;
+  cqual2 *prog = (cqual2 *)g.prog;
+  const uint32_t n = g.nprog;
   uint32_t qi = 0;
-  while (qi < g.nprog) {
-    const uint32_t cl = g.prog[qi].clause;
+  while (qi < n) {
+    const uint32_t cl = prog[qi].clause;
     int cv = 0;                                 // the clause: 0 false, 1 true, 2 unknown
-    for (; qi < g.nprog && g.prog[qi].clause == cl; ++qi) {
-      if (cv == 1) continue;                     // decided: skip the clause's rest
-      const strom_heap_qual2 &q = g.prog[qi];
+    for (; qi < n && prog[qi].clause == cl; ++qi) {
+      strom_heap_qual2 q;
+      q.attno = prog[qi].attno;
+      q.kind = prog[qi].kind;
+      q.flags = prog[qi].flags;
+      q.clause = cl;
+      q.nconst = prog[qi].nconst;
+      q.coff = prog[qi].coff;
+      q.lo = prog[qi].lo;
+      q.hi = prog[qi].hi;
+      if (!live || cv == 1) continue;           // decided: skip the clause's rest
       if (q.attno != last) {
         if ((uint32_t)q.attno < s.next) s = deform_init(t, tlen);   // walk again from the start
         a = deform_to(g.desc, s, (uint32_t)q.attno);
         last = q.attno;
       }
-      if (s.bad) return 0;
-      const int r = eval_qual2(q, g.cpool, t, a);
+      if (s.bad) {
+        live = false;
+        verdict = 0;
+        continue;
+      }
+      const int r = eval_qual2(q, (cu8 *)g.cpool, t, a);
       if (r == 1) cv = 1;
       else if (r == 2) cv = 2;
     }
-    if (cv == 0) return 0;
-    if (cv == 2) verdict = 2;
+    if (live) {
+      if (cv == 0) {
+        live = false;
+        verdict = 0;
+      } else if (cv == 2) {
+        verdict = 2;
+      }
+    }
+    if (!__ballot(live)) break;                 // every lane decided
   }
   return verdict;
 }
 
-// 1 keep, 0 drop, 2 undecidable (GEN: a text qual met a compressed value)
-template <bool GEN>
+// 1 keep, 0 drop, 2 undecidable (GEN: a text qual met a compressed value).
+// GEN 0: the fixed int attribute of strom_heap_scan; 1: the fixed-size AND
+// list (quals in the kernel arguments: scalar loads, early exit); 2: a
+// program in device memory.  Separate instances: the program evaluator's
+// registers and code stay out of the other two.
+template <int GEN>
 __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const uint8_t *pg,
                                           uint32_t lp, bool all_visible) {
   const strom_heap_scan_args &a = g.base;
@@ -546,7 +593,8 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
     if (!(infomask & kXminCommitted)) return false;
     if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return false;
   }
-  if (GEN) return g.prog ? eval_prog(g, pg + off, len) : g.nquals ? eval_quals(g, pg + off, len) : 1;
+  if (GEN == 2) return eval_prog(g, pg + off, len);
+  if (GEN == 1) return g.nquals ? eval_quals(g, pg + off, len) : 1;
   if (a.attr_off < 0) return true;
   const uint32_t at = hoff + (uint32_t)a.attr_off;
   if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return false;
@@ -568,7 +616,7 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
 // row "dequeue" — 2.1 TB/s).
 constexpr int kPerWave = 8;
 
-template <int PAGE, bool GEN>
+template <int PAGE, int GEN>
 __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan2_args g, uint32_t maxchunks,
                                                         uint32_t ppw) {
   const strom_heap_scan_args &a = g.base;
@@ -684,7 +732,7 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan2_args g,
 #undef STROM_HS_ISSUE
 }
 
-int heap_scan_launch(const strom_heap_scan2_args &g, bool gen, void *stream) {
+int heap_scan_launch(const strom_heap_scan2_args &g, int gen, void *stream) {
   const strom_heap_scan_args *a = &g.base;
   if (!a->pages || !a->out_count) return -22;
   if (a->page_sz < 1024 || (a->page_sz & 1023) || a->page_sz > 32768) return -22;
@@ -707,16 +755,15 @@ int heap_scan_launch(const strom_heap_scan2_args &g, bool gen, void *stream) {
   uint32_t grid = (a->npages + kWaves * ppw - 1) / (kWaves * ppw);
   const uint32_t cap = 256u * (per_cu ? per_cu : 1u) * 2u;
   if (grid > cap) grid = cap;
+  auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, g, maxchunks, ppw); };
   if (a->page_sz == 8192) {
-    if (gen)
-      hipLaunchKernelGGL((heap_scan_kernel<8192, true>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
-    else
-      hipLaunchKernelGGL((heap_scan_kernel<8192, false>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+    if (gen == 2) launch(heap_scan_kernel<8192, 2>);
+    else if (gen == 1) launch(heap_scan_kernel<8192, 1>);
+    else launch(heap_scan_kernel<8192, 0>);
   } else {
-    if (gen)
-      hipLaunchKernelGGL((heap_scan_kernel<0, true>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
-    else
-      hipLaunchKernelGGL((heap_scan_kernel<0, false>), dim3(grid), dim3(256), lds, st, g, maxchunks, ppw);
+    if (gen == 2) launch(heap_scan_kernel<0, 2>);
+    else if (gen == 1) launch(heap_scan_kernel<0, 1>);
+    else launch(heap_scan_kernel<0, 0>);
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -781,46 +828,62 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   strom_heap_scan2_args g;
   __builtin_memset(&g, 0, sizeof g);
   g.base = *a;
-  return heap_scan_launch(g, false, stream);
+  return heap_scan_launch(g, 0, stream);
 }
 
-// host-side check of a program (a copy in host memory, as uploaded): every
-// qual's kind fits its attribute, constants inside the pool, clauses contiguous
+// host-side check of a program and its pool (copies in host memory, as
+// uploaded): every qual's kind fits its attribute, clauses contiguous, every
+// constant the device reads inside the pool — IN tables, text, numeric
+// headers and their digits, the text entries an IN table names — and
+// 8-aligned (the device reads the pool a dword at a time)
 extern "C" int strom_heap_prog_check(const strom_heap_tupdesc *d, const strom_heap_qual2 *prog,
-                                     uint32_t n, uint32_t pool_len) {
-  uint32_t seen_last = 0;
+                                     uint32_t n, const uint8_t *pool, uint32_t pool_len) {
+  if (!d || (n && !prog) || !pool || (pool_len & 7)) return -22;
+  auto u32 = [&](uint64_t o) {
+    return (uint32_t)pool[o] | ((uint32_t)pool[o + 1] << 8) | ((uint32_t)pool[o + 2] << 16) |
+           ((uint32_t)pool[o + 3] << 24);
+  };
+  auto num_ok = [&](int64_t o) {              // header (kind, neg, weight, ndigits) + digits
+    if (o < 0 || (o & 7) || (uint64_t)o + 8 > pool_len) return false;
+    const uint32_t nd = (uint32_t)pool[o + 6] | ((uint32_t)pool[o + 7] << 8);
+    return (uint64_t)o + 8 + 2ull * nd <= pool_len;
+  };
   for (uint32_t i = 0; i < n; ++i) {
     const strom_heap_qual2 &x = prog[i];
     if (x.attno < 0 || x.attno >= d->natts) return -22;
+    if (x.coff & 7) return -22;
     if (i && x.clause != prog[i - 1].clause) {
       for (uint32_t j = 0; j < i; ++j)       // a clause id may not come back
         if (prog[j].clause == x.clause) return -22;
     }
-    seen_last = x.clause;
     const int len = d->attlen[x.attno];
-    const uint64_t end = (uint64_t)x.coff;
+    const uint64_t at = (uint64_t)x.coff;
     switch (x.kind) {
       case STROM_QUAL_INT_RANGE:
         if (len != 1 && len != 2 && len != 4 && len != 8) return -22;
         break;
       case STROM_QUAL_INT_IN:
         if (len != 1 && len != 2 && len != 4 && len != 8) return -22;
-        if (end + 8ull * x.nconst > pool_len) return -22;
+        if (at + 8ull * x.nconst > pool_len) return -22;
         break;
       case STROM_QUAL_FLOAT_RANGE:
         if (len != 4 && len != 8) return -22;
         break;
       case STROM_QUAL_TEXT_EQ:
       case STROM_QUAL_TEXT_PREFIX:
-        if (len != -1 || end + x.nconst > pool_len) return -22;
+        if (len != -1 || at + x.nconst > pool_len) return -22;
         break;
       case STROM_QUAL_TEXT_IN:
-        if (len != -1 || end + 8ull * x.nconst > pool_len) return -22;
+        if (len != -1 || at + 8ull * x.nconst > pool_len) return -22;
+        for (uint32_t k = 0; k < x.nconst; ++k) {
+          const uint64_t co = u32(at + 8 * k), cl = u32(at + 8 * k + 4);
+          if ((co & 7) || co + cl > pool_len) return -22;
+        }
         break;
       case STROM_QUAL_NUMERIC_RANGE:
         if (len != -1) return -22;
-        if (!(x.flags & 1) && ((uint64_t)x.lo + 8 > pool_len || x.lo < 0)) return -22;
-        if (!(x.flags & 2) && ((uint64_t)x.hi + 8 > pool_len || x.hi < 0)) return -22;
+        if (!(x.flags & 1) && !num_ok(x.lo)) return -22;
+        if (!(x.flags & 2) && !num_ok(x.hi)) return -22;
         break;
       case STROM_QUAL_IS_NULL:
       case STROM_QUAL_NOT_NULL:
@@ -829,7 +892,6 @@ extern "C" int strom_heap_prog_check(const strom_heap_tupdesc *d, const strom_he
         return -22;
     }
   }
-  (void)seen_last;
   return 0;
 }
 
@@ -842,7 +904,7 @@ extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   }
   // a program was checked by the caller against its host copy
   // (strom_heap_prog_check); it lives in device memory here
-  if (g->prog) return heap_scan_launch(*g, true, stream);
+  if (g->prog) return heap_scan_launch(*g, 2, stream);
   if (g->nquals < 0 || g->nquals > STROM_HEAP_MAX_QUALS) return -22;
   int last = -1;
   for (int q = 0; q < g->nquals; ++q) {
@@ -870,7 +932,7 @@ extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
         return -22;
     }
   }
-  return heap_scan_launch(*g, true, stream);
+  return heap_scan_launch(*g, 1, stream);
 }
 
 extern "C" int strom_heap_project_n(const void *pages, uint32_t page_sz, const uint32_t *items,

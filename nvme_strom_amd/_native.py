@@ -252,7 +252,7 @@ _SIGS = {
     "strom_heap_scan": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p]),
     "strom_heap_scan2": (C.c_int, [C.POINTER(HeapScan2Args), C.c_void_p]),
     "strom_heap_prog_check": (C.c_int, [C.POINTER(HeapTupDesc), C.c_void_p, C.c_uint32,
-                                        C.c_uint32]),
+                                        C.c_char_p, C.c_uint32]),
     "strom_heap_project": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32,
                                      C.POINTER(HeapTupDesc), C.c_int, C.c_int, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),

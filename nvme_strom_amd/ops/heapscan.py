@@ -277,8 +277,34 @@ class Program:
             for q in sorted(g, key=lambda q: q.attno):
                 q.clause = ci
                 self.quals.append(q)
-        if not self.pool:
-            self.pool = bytearray(8)
+        # the device reads the pool a dword at a time: padded to 8 bytes
+        while not self.pool or len(self.pool) % 8:
+            self.pool.append(0)
+
+    def fixed(self):
+        """The program as strom_heap_scan2's fixed-size AND list (the quals
+        ride in the kernel arguments: scalar loads and an early exit per
+        tuple), or None when it needs the program mode: an OR, more than
+        HEAP_MAX_QUALS quals, a kind or constant the fixed form lacks."""
+        qs = self.quals
+        if len(qs) > N.HEAP_MAX_QUALS or len({q.clause for q in qs}) != len(qs):
+            return None
+        out = []
+        for q in qs:
+            if q.flags or q.kind not in (1, 2, 3, 4, 5, 6, 7):
+                return None
+            s = N.HeapQual()
+            s.attno, s.kind, s.lo, s.hi = q.attno, q.kind, q.lo, q.hi
+            if q.kind in (5, 6, 7):
+                n = q.nconst * (8 if q.kind == 7 else 1)
+                if q.nconst > (4 if q.kind == 7 else 32):
+                    return None
+                s.nconst = q.nconst
+                C.memmove(C.addressof(s.cbytes), bytes(self.pool[q.coff:q.coff + n]), n)
+            out.append(s)
+        if any(b.attno < a.attno for a, b in zip(out, out[1:])):
+            return None
+        return out
 
     def arrays(self):
         """(program bytes, pool bytes) for upload."""
@@ -306,12 +332,12 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
                verify_checksum: bool = False, skip_invisible: bool = False,
                blkno_base: int = 0, out_cap: Optional[int] = None,
                blknos: Optional[torch.Tensor] = None, stream=None,
-               sync: bool = True) -> HeapScan2Result:
+               sync: bool = True, program: bool = False) -> HeapScan2Result:
     """Scan ``pages`` deforming every tuple with ``desc`` (utils.pgtuple) and
     keeping the ones ``quals`` selects: a list of ``pgtuple.Qual`` (ANDed)
     and ``pgtuple.Or`` clauses (CNF), or a compiled ``Program``.
     ``sync=False`` leaves ``count`` / ``recheck`` as device tensors (no host
-    read)."""
+    read); ``program=True`` runs the program mode even for a plain AND list."""
     require_cuda(pages, "pages")
     pages = pages.view(torch.uint8)
     if pages.numel() % page_sz:
@@ -331,13 +357,21 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
                             blknos=ptr(blknos) if blknos is not None else None)
     g.desc = tupdesc_struct(desc)
     # the qualifier list as a program (CNF, any number of quals and
-    # constants) in device memory, checked on its host copy first
+    # constants) in device memory, checked on its host copy first; a plain
+    # AND list of the fixed form's kinds goes in the arguments instead
     prog = quals if isinstance(quals, Program) else Program(desc, quals)
     raw, pool = prog.arrays()
-    if prog.quals:
+    fx = prog.fixed() if prog.quals and not program else None
+    keep = []
+    if fx is not None:
+        # a plain AND list: the fixed-size form in the kernel arguments
+        g.nquals = len(fx)
+        for i, q in enumerate(fx):
+            g.quals[i] = q
+    elif prog.quals:
         hp = np.frombuffer(raw, np.uint8)
         check(lib().strom_heap_prog_check(C.byref(g.desc), hp.ctypes.data, len(prog.quals),
-                                          len(pool)), "heap_scan2 program")
+                                          pool, len(pool)), "heap_scan2 program")
         # uploaded on the scan's stream (ordered before the kernel; their
         # memory is reused only after it), and kept by the result
         ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.current_stream(dev)
@@ -347,9 +381,6 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
         g.prog, g.cpool = ptr(d_prog), ptr(d_pool)
         g.nprog, g.cpool_len = len(prog.quals), len(pool)
         keep = [d_prog, d_pool]
-    else:
-        keep = []
-    g.nquals = 0
     g.recheck_count = ptr(cnt) + 4
     if npages:
         cnt[1].zero_()

@@ -98,6 +98,15 @@ def main(argv=None):
                                                         T.Qual("tail", "between", (0, 50))])):
             log(name, timed(lambda: heap_scan2(pages, desc, qs, verify_checksum=True,
                                                skip_invisible=True)), nb)
+            # the same list through the program mode (device-memory CNF)
+            log(name.replace("heap_scan2_", "heap_scan2_prog_"),
+                timed(lambda: heap_scan2(pages, desc, qs, verify_checksum=True,
+                                         skip_invisible=True, program=True)), nb)
+        # a CNF only the program mode takes: (a in range OR c IS NULL) AND b < 0.6
+        cnf = [T.Or(T.Qual("a", "between", (-200_000, 300_000)), T.Qual("c", "isnull")),
+               T.Qual("b", "lt", (0.6,))]
+        log("heap_scan2_prog_cnf2", timed(lambda: heap_scan2(pages, desc, cnf, verify_checksum=True,
+                                                             skip_invisible=True)), nb)
         del pages
     rng = np.random.default_rng(1)
     words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]

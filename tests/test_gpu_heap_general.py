@@ -22,13 +22,16 @@ def rel():
     return data, pages
 
 
+@pytest.mark.parametrize("program", [False, True])
 @pytest.mark.parametrize("qi", range(len(heapgen.QUAL_SETS)))
-def test_scan2_matches_host(rel, qi):
+def test_scan2_matches_host(rel, qi, program):
+    """Both kernels: the fixed AND list in the arguments (when the list fits
+    it) and the device-memory program."""
     from nvme_strom_amd.ops import heapscan as H
     data, pages = rel
     qs = heapgen.QUAL_SETS[qi]
     want, wstatus, _ = T.host_scan2(data, heapgen.DESC, qs, verify_checksum=True)
-    r = H.heap_scan2(pages, heapgen.DESC, qs, verify_checksum=True)
+    r = H.heap_scan2(pages, heapgen.DESC, qs, verify_checksum=True, program=program)
     got = r.sorted_items().tolist()
     assert got == want
     st = r.page_status.cpu().numpy().tolist()

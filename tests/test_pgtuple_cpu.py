@@ -153,8 +153,24 @@ def test_program_compiles_cnf_and_exact_int_bounds():
     raw, pool = p.arrays()
     hp = np.frombuffer(raw, np.uint8)
     d = H.tupdesc_struct(desc)
-    assert H.lib().strom_heap_prog_check(C.byref(d), hp.ctypes.data, len(p.quals), len(pool)) == 0
-    assert H.lib().strom_heap_prog_check(C.byref(d), hp.ctypes.data, len(p.quals), 8) < 0
+    chk = H.lib().strom_heap_prog_check
+    assert len(pool) % 8 == 0
+    assert chk(C.byref(d), hp.ctypes.data, len(p.quals), pool, len(pool)) == 0
+    assert chk(C.byref(d), hp.ctypes.data, len(p.quals), pool, 8) < 0
+    assert chk(C.byref(d), hp.ctypes.data, len(p.quals), pool, len(pool) - 4) < 0   # unpadded
+    # a text IN entry naming bytes past the pool's end
+    tin = next(q for q in p.quals if q.kind == H.QUAL_TEXT_IN)
+    bad = bytearray(pool)
+    struct.pack_into("<I", bad, tin.coff + 4, len(pool) + 1)
+    assert chk(C.byref(d), hp.ctypes.data, len(p.quals), bytes(bad), len(pool)) < 0
+    # a numeric constant whose digit count runs past the pool's end
+    pn = H.Program(desc, [T.Qual("amt", "ge", (3,))])
+    raw2, pool2 = pn.arrays()
+    h2 = np.frombuffer(raw2, np.uint8)
+    assert chk(C.byref(d), h2.ctypes.data, 1, pool2, len(pool2)) == 0
+    bad = bytearray(pool2)
+    struct.pack_into("<H", bad, pn.quals[0].lo + 6, 999)
+    assert chk(C.byref(d), h2.ctypes.data, 1, bytes(bad), len(pool2)) < 0
     # the host twin on the same fractional bounds
     assert T.Qual("x", "between", (1.5, 3)).test(1, "int") is False
     assert T.Qual("s", "eq", (2.5,)).test(2, "int") is False
@@ -226,3 +242,29 @@ def test_program_rejects_kind_mismatches():
     # an empty IN is constant false, also under an Or
     p = H.Program(desc, [T.Or(T.Qual("amt", "in", ([],)), T.Qual("x", "in", ([],)))])
     assert all(q.flags & H.QUAL2_FALSE for q in p.quals)
+
+
+def test_program_fixed_form():
+    """A plain AND list of the fixed form's kinds goes in the kernel
+    arguments (sorted by attribute, constants copied out of the pool); an OR,
+    a numeric range, a constant-false qual, a long text constant or more than
+    HEAP_MAX_QUALS quals keep the program mode."""
+    import ctypes as C
+    from nvme_strom_amd import _native as N
+    from nvme_strom_amd.ops import heapscan as H
+    desc, _ = heapgen.numeric_rel(4)
+    fx = H.Program(desc, [T.Qual("x", "in", ([3, 1, 2],)), T.Qual("tag", "text_eq", ("abc",)),
+                          T.Qual("f", "between", (0.5, 1.5))]).fixed()
+    assert fx is not None and [q.attno for q in fx] == sorted(q.attno for q in fx)
+    kinds = {q.kind: q for q in fx}
+    assert set(kinds) == {2, 5, 7}
+    assert kinds[7].nconst == 3 and bytes(kinds[7].cbytes)[:24] == struct.pack("<3q", 1, 2, 3)
+    assert kinds[5].nconst == 3 and bytes(kinds[5].cbytes)[:3] == b"abc"
+    assert C.sizeof(N.HeapQual) == 56
+    for qs in ([T.Or(T.Qual("x", "eq", (1,)), T.Qual("s", "eq", (2,)))],
+               [T.Qual("amt", "ge", (3,))],
+               [T.Qual("s", "eq", (2.5,))],
+               [T.Qual("tag", "text_eq", ("a" * 33,))],
+               [T.Qual("x", "in", (list(range(5)),))],
+               [T.Qual("x", "ge", (i,)) for i in range(N.HEAP_MAX_QUALS + 1)]):
+        assert H.Program(desc, qs).fixed() is None, qs
