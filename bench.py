@@ -282,13 +282,23 @@ def main() -> int:
     p50_py = float(np.percentile(lat_py, 50))
     # where the 4 KiB latency goes (native phase stamps, this rank's medians)
     # and its floor: a bare O_DIRECT pread of the same offsets into host RAM
-    phases, raw_p50 = {}, float("nan")
+    phases, raw_p50, paired = {}, float("nan"), {}
     if a.lat_samples:
         S.evict_file(fd)
         offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
         phases = S.phase_breakdown(S.pread_gpu_phases(buf.handle, 0, fd, offs)[50:])
         S.evict_file(fd)
         raw_p50 = float(np.percentile(S.pread_raw_latency(fd, offs)[50:], 50)) / 1e3
+        # the same comparison interleaved read by read (storage drift cancels)
+        S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=2 * (min(a.lat_samples, 1000) + 50)) * 4096
+        pe, pr = (x[50:].astype(np.float64) / 1e3 for x in S.pread_pair_latency(buf.handle, 0, fd, offs))
+        paired = {"engine_p50_us": round(float(np.median(pe)), 2),
+                  "raw_p50_us": round(float(np.median(pr)), 2),
+                  "overhead_p50_us": round(float(np.median(pe - pr)), 2),
+                  "pairs": int(len(pe)),
+                  "note": "raw O_DIRECT pread and pread_gpu alternated read by read, "
+                          "order flipped every pair; overhead = median of pairwise differences"}
 
     # the same QD1 reads through the v0.6 ioctl pair (SSD2GPU + WAIT: task
     # table, residency probe, planner), and the host primitive costs below both
@@ -378,6 +388,7 @@ def main() -> int:
         "latency_reduction": "max over ranks (worst rank)",
         "ingest_grid": ing,
         "p50_4k_phases_us": phases,
+        "qd1_paired": paired,
         "verified_crc32c": bool(ver == 1.0),
         "avg_request_kib": round(0.5 * agg["nr_blocks"] / agg["nr_submit"], 1) if agg["nr_submit"] else 0,
         "ram_chunks": agg["nr_ram"],

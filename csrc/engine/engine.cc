@@ -1015,6 +1015,45 @@ int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t 
   return rc;
 }
 
+// QD1 engine vs raw floor at the same moment: read pairs interleaved (raw
+// O_DIRECT pread into host memory, then strom_pread_gpu into HBM; the order
+// flips every pair), each read at its own offset (offs[2i], offs[2i+1]), so
+// storage drift over the probe hits both sides alike.
+int strom_pread_pair_lat(int session, unsigned long handle, size_t offset, int fd,
+                         const uint64_t *file_offs, uint32_t npairs, uint64_t len,
+                         uint64_t *ns_engine, uint64_t *ns_raw) {
+  if (len == 0 || (len & 4095)) return -EINVAL;
+  char path[64];
+  snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+  int d = open(path, O_RDONLY | O_DIRECT | O_CLOEXEC);
+  if (d < 0) return -errno;
+  void *buf = nullptr;
+  if (posix_memalign(&buf, 4096, len) != 0) {
+    close(d);
+    return -ENOMEM;
+  }
+  int rc = 0;
+  for (uint32_t i = 0; i < npairs && rc == 0; ++i) {
+    for (int side = 0; side < 2 && rc == 0; ++side) {
+      const bool raw = (side == 0) == ((i & 1) == 0);
+      const uint64_t off = file_offs[2 * i + (raw ? 0 : 1)];
+      const uint64_t t0 = mono_ns();
+      if (raw) {
+        const ssize_t got = pread(d, buf, len, (off_t)off);
+        ns_raw[i] = mono_ns() - t0;
+        if (got < 0) rc = -errno;
+      } else {
+        const long r = strom_pread_gpu(session, handle, offset, fd, off, len);
+        ns_engine[i] = mono_ns() - t0;
+        if (r < 0) rc = (int)r;
+      }
+    }
+  }
+  free(buf);
+  close(d);
+  return rc;
+}
+
 // Host primitive costs on this machine (ns per call, mean of n): what the
 // 4 KiB latency path is made of below the engine's own logic.
 //   0 clock_gettime(MONOTONIC)  1 rdtsc  2 fstat  3 mincore(1 page)

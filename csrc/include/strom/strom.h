@@ -60,6 +60,11 @@ int strom_pread_gpu_phases(int session, unsigned long handle, size_t offset, int
  * into aligned host memory (no engine, no HBM), ns per read. */
 int strom_pread_raw_lat(int fd, const uint64_t *file_offs, uint32_t n, uint64_t len,
                         uint64_t *ns_out);
+/* QD1 pairs, interleaved: a raw O_DIRECT pread (offs[2i]) and a
+ * strom_pread_gpu (offs[2i+1]) per pair, order flipped every pair; ns each. */
+int strom_pread_pair_lat(int session, unsigned long handle, size_t offset, int fd,
+			 const uint64_t *file_offs, uint32_t npairs, uint64_t len,
+			 uint64_t *ns_engine, uint64_t *ns_raw);
 
 /* Host primitive costs (ns per call, mean of n) on this machine, for the
  * latency breakdown: {clock_gettime, rdtsc, fstat(fd), mincore 1 page of fd,

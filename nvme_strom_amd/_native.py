@@ -197,6 +197,8 @@ _SIGS = {
     "strom_pread_gpu_phases": (C.c_int, [C.c_int, C.c_ulong, C.c_size_t, C.c_int, C.c_void_p,
                                          C.c_uint32, C.c_uint64, C.c_void_p]),
     "strom_pread_raw_lat": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p]),
+    "strom_pread_pair_lat": (C.c_int, [C.c_int, C.c_ulong, C.c_size_t, C.c_int, C.c_void_p,
+                                       C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]),
     "strom_raw_read_rate": (C.c_int, [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "strom_export_dmabuf": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_int),

@@ -514,6 +514,23 @@ def pread_raw_latency(fd: int, file_offs, length: int = 4096) -> np.ndarray:
     return out
 
 
+def pread_pair_latency(handle: int, offset: int, fd: int, file_offs, length: int = 4096,
+                       sess: Optional[Session] = None) -> tuple:
+    """QD1 engine read vs the raw floor at the same moment: pairs of a raw
+    O_DIRECT pread (file_offs[2i]) and a pread_gpu (file_offs[2i+1]),
+    interleaved, the order flipped every pair.  -> (engine ns, raw ns) per
+    pair; their pairwise difference is the engine's cost over the storage
+    with the storage's drift cancelled."""
+    s = sess or session()
+    offs = np.ascontiguousarray(file_offs, dtype=np.uint64)
+    n = len(offs) // 2
+    eng = np.zeros(n, dtype=np.uint64)
+    raw = np.zeros(n, dtype=np.uint64)
+    _check(s.lib.strom_pread_pair_lat(s.sid, handle, offset, fd, offs.ctypes.data, n, length,
+                                      eng.ctypes.data, raw.ctypes.data), "pread_pair_lat")
+    return eng, raw
+
+
 def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
                   sequential: bool = False, buffered: bool = False,
                   fixed: bool = False) -> tuple:

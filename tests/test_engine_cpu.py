@@ -407,6 +407,11 @@ def test_pread_gpu_phase_probe(strom, rand_file):
             assert list(bd) == list(strom.PHASES) and bd["wait"] is not None
             raw = strom.pread_raw_latency(fd, offs)
             assert raw.shape == (5,) and (raw > 0).all()
+            # interleaved pairs: the engine read of each pair lands its own
+            # offset (offs[2i + 1]); the last one is in hbm
+            pe, pr = strom.pread_pair_latency(m.handle, 0, fd, np.array([2, 7, 11, 4], dtype=np.uint64) * 4096)
+            assert pe.shape == pr.shape == (2,) and (pe > 0).all() and (pr > 0).all()
+            assert np.array_equal(hbm[:4096], data[4 * 4096:5 * 4096])
     finally:
         os.close(fd)
 
