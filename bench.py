@@ -299,6 +299,19 @@ def main() -> int:
                   "pairs": int(len(pe)),
                   "note": "raw O_DIRECT pread and pread_gpu alternated read by read, "
                           "order flipped every pair; overhead = median of pairwise differences"}
+        # the same through a registered file (S.RegisteredFile: the descriptor
+        # resolved once, no per-read kcmp / fstat)
+        with S.RegisteredFile(fd) as rf:
+            S.evict_file(fd)
+            offs = rng.integers(0, F // 4096, size=2 * (min(a.lat_samples, 1000) + 50)) * 4096
+            pe, pr = (x[50:].astype(np.float64) / 1e3 for x in S.pread_pair_latency(buf.handle, 0, rf.fd, offs))
+            paired["registered"] = {"engine_p50_us": round(float(np.median(pe)), 2),
+                                    "raw_p50_us": round(float(np.median(pr)), 2),
+                                    "overhead_p50_us": round(float(np.median(pe - pr)), 2)}
+            S.evict_file(fd)
+            offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
+            paired["registered"]["phases_us"] = S.phase_breakdown(
+                S.pread_gpu_phases(buf.handle, 0, rf.fd, offs)[50:])
 
     # the same QD1 reads through the v0.6 ioctl pair (SSD2GPU + WAIT: task
     # table, residency probe, planner), and the host primitive costs below both

@@ -179,7 +179,72 @@ const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *e
   return tl.f;
 }
 
+struct TlReg {
+  int rfd = -1;
+  uint64_t eng = 0, ver = 0;
+  std::shared_ptr<Engine::OpenFile> f;
+};
+static thread_local TlReg tl_reg;
+
+const std::shared_ptr<Engine::OpenFile> &Engine::registered(int rfd) {
+  TlReg &tl = tl_reg;
+  if (tl.rfd == rfd && tl.eng == gen_ && tl.ver == reg_ver_.load(std::memory_order_acquire))
+    return tl.f;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  const uint32_t i = (uint32_t)(rfd - kRegFdBase);
+  tl.f = is_registered_id(rfd) && i < reg_.size() ? reg_[i] : nullptr;
+  tl.rfd = rfd;
+  tl.eng = gen_;
+  tl.ver = reg_ver_.load(std::memory_order_relaxed);   // under the lock: matches tl.f
+  return tl.f;
+}
+
+int Engine::register_file(int fd) {
+  if (fd >= kRegFdBase) return -EINVAL;      // an id or a stripe set
+  int err = 0;
+  auto f = open_file(fd, &err);
+  if (!f) return err ? err : -EBADF;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  size_t i = 0;
+  while (i < reg_.size() && reg_[i]) ++i;
+  if (i >= (size_t)kRegMax) return -EMFILE;
+  if (i == reg_.size()) reg_.emplace_back();
+  reg_[i] = std::move(f);
+  reg_ver_.fetch_add(1, std::memory_order_release);
+  return kRegFdBase + (int)i;
+}
+
+int Engine::unregister_file(int rfd) {
+  std::lock_guard<std::mutex> g(reg_mu_);
+  const uint32_t i = (uint32_t)(rfd - kRegFdBase);
+  if (!is_registered_id(rfd) || i >= reg_.size() || !reg_[i]) return -EBADF;
+  reg_[i].reset();
+  reg_ver_.fetch_add(1, std::memory_order_release);
+  return 0;
+}
+
+void Engine::refresh_registered(int rfd) {
+  std::shared_ptr<OpenFile> f = registered(rfd);
+  if (!f) return;
+  int err = 0;
+  // the engine's own descriptor: open_file re-reads size and ctime in place,
+  // or hands back a new entry (the file was replaced under its inode)
+  auto nf = open_file(f->fd_buffered, &err);
+  if (!nf || nf == f) return;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  const uint32_t i = (uint32_t)(rfd - kRegFdBase);
+  if (i < reg_.size() && reg_[i] == f) {
+    reg_[i] = nf;
+    reg_ver_.fetch_add(1, std::memory_order_release);
+  }
+}
+
 std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
+  if (is_registered_id(fd)) {
+    std::shared_ptr<OpenFile> f = registered(fd);
+    if (!f) *err = -EBADF;
+    return f;
+  }
   struct stat st;
   if (fstat(fd, &st) != 0) {
     *err = -errno;
@@ -354,8 +419,14 @@ int Engine::check_file(strom_check_file *a) {
     return 0;
   }
   FileClass fc;
-  int rc = classify_file(a->fdesc, &fc, config().strict);
-  if (rc) return rc;
+  if (is_registered_id(a->fdesc)) {
+    const auto &f = registered(a->fdesc);
+    if (!f) return -EBADF;
+    fc = f->fc;
+  } else {
+    int rc = classify_file(a->fdesc, &fc, config().strict);
+    if (rc) return rc;
+  }
   a->numa_node_id = fc.numa_node;
   a->support_dma64 = fc.dma64 ? 1 : 0;
   return 0;
@@ -533,26 +604,32 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
 }
 
 long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off,
-                        uint64_t len) {
+                        uint64_t len, bool checked) {
   if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
   if (fd >= kStripeFdBase) return -EAGAIN;  // stripe sets: the planner routes members
   const auto &gmap = gpu_registry().get_cached(handle);
   if (!gmap) return -ENOENT;
   if (int v = gpu_registry().validate(gmap)) return v;
   if (strom_core_check_range(gmap->map_length - gmap->map_offset, offset, len)) return -ERANGE;
-  // phases of this path: "lookup" the mapping, "plan" the file (fstat +
-  // the per-thread cache)
+  // phases of this path: "lookup" the mapping, "plan" the file (the
+  // per-thread caches: a registered file's entry, or a kcmp / fstat check)
   phase_mark(0);
   int err = 0;
   bool fast = false;
-  const auto &f = open_file_cached(fd, &err, &fast);
-  if (!f) return err;
+  const bool reg = is_registered_id(fd);
+  const auto &f = reg ? registered(fd) : open_file_cached(fd, &err, &fast);
+  if (!f) return reg ? -EBADF : err;
+  fast |= reg;                              // the size is a cached one
+  auto recheck = [&] {
+    // the size came from a cache: check it once more with a stat
+    if (reg) refresh_registered(fd);
+    else forget_cached_file();
+    return pread_sync(handle, offset, fd, file_off, len, true);
+  };
   const uint64_t size = (uint64_t)f->fc.size;
   if (file_off >= size) {
-    if (!fast) return -ERANGE;
-    // the size came from the cache: check it once more with a stat
-    forget_cached_file();
-    return pread_sync(handle, offset, fd, file_off, len);
+    if (!fast || checked) return -ERANGE;
+    return recheck();
   }
   phase_mark(1);
   long status = 0;
@@ -574,11 +651,10 @@ long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t fi
   stats().nr_setup_prps.fetch_add(1, std::memory_order_relaxed);
   phase_mark(2);
   io_->run_inline(r);
-  if (status == -EIO && fast) {
+  if (status == -EIO && fast && !checked) {
     // short against the cached size: the file may have shrunk — redo the
     // read with the size checked by a stat
-    forget_cached_file();
-    return pread_sync(handle, offset, fd, file_off, len);
+    return recheck();
   }
   if (status) return status;
   return (long)len;
@@ -1197,6 +1273,9 @@ int strom_stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size) 
 }
 
 int strom_stripe_close(int sfd) { return engine().stripe_close(sfd); }
+
+int strom_register_file(int fd) { return engine().register_file(fd); }
+int strom_unregister_file(int rfd) { return engine().unregister_file(rfd); }
 
 int strom_file_topology(int fd, strom_file_topo *out) {
   if (!out) return -EFAULT;

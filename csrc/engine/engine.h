@@ -543,7 +543,9 @@ class Engine {
   // the caller's thread: no task, no residency probe (O_DIRECT reads see
   // dirty page-cache data: the kernel writes the range back first).  The
   // 4 KiB latency path of strom_pread_gpu.  -EAGAIN: use the task path.
-  long pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off, uint64_t len);
+  // `checked`: the file's size was just re-read (no second retry).
+  long pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off, uint64_t len,
+                  bool checked = false);
   IoEngine &io() { return *io_; }
   struct OpenFile;
   // Stripe sets (PAR2 without md): a logical file striped in `unit`-byte
@@ -566,6 +568,19 @@ class Engine {
   // drop this thread's cached file (the next open_file_cached stats again)
   void forget_cached_file();
 
+  // Registered files (io_uring's IORING_REGISTER_FILES, for this engine):
+  // register_file() resolves a descriptor once and returns an id
+  // (kRegFdBase + slot) accepted wherever a file descriptor is.  The engine
+  // reads through its own descriptors of the file, so an id needs no
+  // per-read identity check (no fstat, no kcmp: the caller may even close
+  // its descriptor); only a read past the cached size or a short one
+  // re-reads the size.  Ids end with unregister_file() or an engine reset.
+  int register_file(int fd);
+  int unregister_file(int rfd);
+  // the registered file of rfd (nullptr: none); per-thread cache validated
+  // by one atomic load of the table's version
+  const std::shared_ptr<OpenFile> &registered(int rfd);
+
  private:
   int check_file(strom_check_file *a);
   int memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a);
@@ -574,14 +589,23 @@ class Engine {
   int memcpy_wait_timed(strom_memcpy_wait_timed *a);
 
   std::shared_ptr<StripeSet> stripe(int fd);
+  // re-read a registered file's size (open_file on the engine's descriptor)
+  void refresh_registered(int rfd);
 
   std::unique_ptr<IoEngine> io_;
   std::mutex files_mu_;
   std::map<std::pair<dev_t, ino_t>, std::shared_ptr<OpenFile>> files_;
+  std::mutex reg_mu_;
+  std::vector<std::shared_ptr<OpenFile>> reg_;   // slot i: id kRegFdBase + i
+  std::atomic<uint64_t> reg_ver_{0};             // bumped by every (un)registration
 };
 
 // pseudo descriptors of stripe sets: far above any real fd
 constexpr int kStripeFdBase = 0x7f000000;
+// ids of registered files: below the stripe sets, above any real fd
+constexpr int kRegFdBase = 0x7e000000;
+constexpr int kRegMax = 4096;
+inline bool is_registered_id(int fd) { return fd >= kRegFdBase && fd < kRegFdBase + kRegMax; }
 
 Engine &engine();
 void engine_reset();

@@ -94,6 +94,13 @@ int strom_export_dmabuf(uint64_t va, uint64_t len, int *fd, uint64_t *offset);
  * when a member is too short.  Userspace provider only. */
 int strom_stripe_open(const int *fds, uint32_t n, uint32_t unit, uint64_t size);
 int strom_stripe_close(int sfd);
+/* Registered file (as io_uring's registered files): the descriptor is
+ * resolved once; the returned id is accepted wherever a file descriptor is
+ * and skips the per-read identity check (fstat / kcmp).  The engine reads
+ * through descriptors of its own: the caller may close fd.  An id lives
+ * until strom_unregister_file() or an engine reset (-EBADF after). */
+int strom_register_file(int fd);
+int strom_unregister_file(int rfd);
 
 /* SSD2RAM destinations: mmap (MAP_SHARED, read/write) `length` bytes of an
  * ALLOC_DMA_BUFFER fd through the engine, so the range is found in the

@@ -209,6 +209,8 @@ _SIGS = {
     "strom_dmabuf_gc": (C.c_int, []),
     "strom_stripe_open": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
     "strom_stripe_close": (C.c_int, [C.c_int]),
+    "strom_register_file": (C.c_int, [C.c_int]),
+    "strom_unregister_file": (C.c_int, [C.c_int]),
     "strom_gpu_detached": (C.c_long, []),
     "strom_gpu_bar_bytes": (C.c_long, [C.c_ulong]),
     "strom_host_costs": (C.c_int, [C.c_int, C.c_void_p, C.c_int]),

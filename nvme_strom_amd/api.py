@@ -377,6 +377,42 @@ class StripeSet:
         self.close()
 
 
+class RegisteredFile:
+    """A file registered with the engine (io_uring's registered files): the
+    descriptor (or path) is resolved once and ``fd`` is an id the engine
+    accepts wherever it takes a file descriptor (pread_gpu, CHECK_FILE,
+    MEMCPY_SSD2GPU / SSD2RAM, the latency probes).  Reads by id skip the
+    per-read identity check of a plain descriptor (kcmp or fstat): the
+    engine reads through descriptors of its own, so closing the caller's
+    descriptor does not end the registration; ``close()`` does."""
+
+    def __init__(self, f):
+        own = None
+        if not isinstance(f, int):
+            own = fd = os.open(f, os.O_RDONLY)
+        else:
+            fd = f
+        try:
+            rc = N.lib().strom_register_file(fd)
+        finally:
+            if own is not None:
+                os.close(own)
+        if rc < 0:
+            raise StromError(-rc, "strom_register_file")
+        self.fd = rc
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            N.lib().strom_unregister_file(self.fd)
+            self.fd = -1
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def write_striped(paths, data, unit: int = 1 << 20) -> int:
     """Write ``data`` (bytes-like) as a stripe set over ``paths``; returns
     the logical size (test and benchmark helper)."""

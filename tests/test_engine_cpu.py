@@ -432,7 +432,7 @@ def test_pread_gpu_per_thread_caches(strom, rand_file):
     handle fails at once, a new mapping is seen, a descriptor number reused
     for another file reads the new file, and a file that grew is re-sized."""
     path, data = rand_file(16 * 4096)
-    path2, data2 = rand_file(32 * 4096)
+    path2, data2 = rand_file(32 * 4096, seed=1, name="other.bin")
     keep, hbm = _host_target(4 * 4096)
     fd = _open(path)
     try:
@@ -467,3 +467,61 @@ def test_pread_gpu_per_thread_caches(strom, rand_file):
         strom.unmap_gpu_memory(m.handle)
     finally:
         os.close(fd)
+
+
+def test_registered_file(strom, rand_file):
+    """A registered file's id reads like its descriptor (pread_gpu, CHECK_FILE,
+    SSD2GPU), keeps reading after the caller closes its descriptor and after
+    the number is reused for another file, follows growth and shrinkage, and
+    ends with unregister (-EBADF after)."""
+    path, data = rand_file(16 * 4096)
+    path2, data2 = rand_file(8 * 4096, seed=3, name="other.bin")
+    keep, hbm = _host_target(4 * 4096)
+    fd = _open(path)
+    rf = strom.RegisteredFile(fd)
+    assert rf.fd >= 0x7E000000
+    with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+        strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([3 * 4096], dtype=np.uint64))
+        assert np.array_equal(hbm[:4096], data[3 * 4096:4 * 4096])
+        # the caller's descriptor closed, its number reused for another file
+        os.close(fd)
+        fd2 = os.open(path2, os.O_RDONLY)
+        try:
+            strom.pread_gpu_latency(m.handle, 4096, rf.fd, np.array([9 * 4096], dtype=np.uint64))
+            assert np.array_equal(hbm[4096:8192], data[9 * 4096:10 * 4096])
+            # the task path and CHECK_FILE take the id too
+            ids = np.array([12, 13], dtype=np.uint32)
+            wb = np.zeros(2 * 4096, dtype=np.uint8)
+            t = strom.memcpy_ssd2gpu(m.handle, 0, rf.fd, ids, 4096, wb_buffer=wb.ctypes.data)
+            strom.memcpy_wait(t.dma_task_id)
+            for k, c in enumerate(ids.tolist()):
+                got = hbm[k * 4096:(k + 1) * 4096] if k < t.nr_ssd else wb[k * 4096:(k + 1) * 4096]
+                assert np.array_equal(got, data[c * 4096:(c + 1) * 4096])
+            strom.check_file(rf.fd)
+            # two ids, interleaved on one thread
+            with strom.RegisteredFile(path2) as rf2:
+                for k in (1, 7, 2):
+                    strom.pread_gpu_latency(m.handle, 0, rf2.fd, np.array([k * 4096], dtype=np.uint64))
+                    assert np.array_equal(hbm[:4096], data2[k * 4096:(k + 1) * 4096])
+                    strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([k * 4096], dtype=np.uint64))
+                    assert np.array_equal(hbm[:4096], data[k * 4096:(k + 1) * 4096])
+            # growth: a read past the registered size re-reads it
+            extra = np.random.default_rng(6).integers(0, 256, 4 * 4096, dtype=np.uint8)
+            with open(path, "ab") as f:
+                f.write(extra.tobytes())
+            strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([17 * 4096], dtype=np.uint64))
+            assert np.array_equal(hbm[:4096], extra[4096:8192])
+            # shrinkage: past the new end is out of range
+            os.truncate(path, 6 * 4096)
+            with pytest.raises(strom.StromError) as e:
+                strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([10 * 4096], dtype=np.uint64))
+            assert e.value.errno == errno.ERANGE
+            strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([5 * 4096], dtype=np.uint64))
+            assert np.array_equal(hbm[:4096], data[5 * 4096:6 * 4096])
+            rf.close()
+            with pytest.raises(strom.StromError) as e:
+                strom.pread_gpu_latency(m.handle, 0, rf.fd if rf.fd >= 0 else 0x7E000000,
+                                        np.array([0], dtype=np.uint64))
+            assert e.value.errno == errno.EBADF
+        finally:
+            os.close(fd2)
