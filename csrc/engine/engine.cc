@@ -1099,8 +1099,14 @@ int strom_pread_pair_lat(int session, unsigned long handle, size_t offset, int f
                          const uint64_t *file_offs, uint32_t npairs, uint64_t len,
                          uint64_t *ns_engine, uint64_t *ns_raw) {
   if (len == 0 || (len & 4095)) return -EINVAL;
+  int real = fd;                     // the raw side needs a real descriptor
+  if (is_registered_id(fd)) {
+    const auto &f = engine().registered(fd);
+    if (!f) return -EBADF;
+    real = f->fd_buffered;
+  }
   char path[64];
-  snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+  snprintf(path, sizeof path, "/proc/self/fd/%d", real);
   int d = open(path, O_RDONLY | O_DIRECT | O_CLOEXEC);
   if (d < 0) return -errno;
   void *buf = nullptr;

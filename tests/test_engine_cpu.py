@@ -498,6 +498,9 @@ def test_registered_file(strom, rand_file):
                 got = hbm[k * 4096:(k + 1) * 4096] if k < t.nr_ssd else wb[k * 4096:(k + 1) * 4096]
                 assert np.array_equal(got, data[c * 4096:(c + 1) * 4096])
             strom.check_file(rf.fd)
+            pe, pr = strom.pread_pair_latency(m.handle, 0, rf.fd, np.array([2, 4], dtype=np.uint64) * 4096)
+            assert (pe > 0).all() and (pr > 0).all()
+            assert np.array_equal(hbm[:4096], data[4 * 4096:5 * 4096])
             # two ids, interleaved on one thread
             with strom.RegisteredFile(path2) as rf2:
                 for k in (1, 7, 2):
