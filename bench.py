@@ -258,16 +258,50 @@ def main() -> int:
     gather_ok = verified if fan else None
     buf = ld.bufs[last % len(ld.bufs)]
 
-    # p50/p99 latency of single 4 KiB reads into HBM (QD1, O_DIRECT path),
-    # timed in the engine's native loop (the reference's C-tool vantage);
-    # the same probe through the Python binding is reported alongside
-    lat = lat_py = np.array([float("nan")])
-    if a.lat_samples:
+    # QD1 4 KiB reads into HBM (O_DIRECT path), timed in the engine's native
+    # loop (the reference's C-tool vantage).  The headline reads go through a
+    # registered file (RegisteredFile: the descriptor resolved once, as the
+    # reference's module holds the file for an ioctl) and alternate read by
+    # read with raw O_DIRECT preads of other offsets (order flipped every
+    # pair), so the storage floor they are compared with is the same
+    # moment's.  A plain descriptor's numbers (a kcmp identity check per
+    # read) and the Python-binding probe are reported alongside.
+    nan = float("nan")
+    lat = lat_plain = lat_py = np.array([nan])
+    phases, phases_plain, paired, raw_p50, floor = {}, {}, {}, nan, nan
+
+    def pair(rfd, n):
         S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=2 * (n + 50)) * 4096
+        pe, pr = (x[50:].astype(np.float64) / 1e3 for x in S.pread_pair_latency(buf.handle, 0, rfd, offs))
+        return pe, pr, {"engine_p50_us": round(float(np.median(pe)), 2),
+                        "raw_p50_us": round(float(np.median(pr)), 2),
+                        "overhead_p50_us": round(float(np.median(pe - pr)), 2),
+                        "pairs": int(len(pe))}
+
+    def phase_split(rfd, n):
+        S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=n + 50) * 4096
+        return S.phase_breakdown(S.pread_gpu_phases(buf.handle, 0, rfd, offs)[50:])
+
+    if a.lat_samples:
         rng = np.random.default_rng(rank)
-        offs = rng.integers(0, F // 4096, size=a.lat_samples + 50) * 4096
         S.stat_hist(reset=True)
-        lat = S.pread_gpu_latency(buf.handle, 0, fd, offs)[50:] / 1e3
+        with S.RegisteredFile(fd) as rf:
+            lat, pr, paired = pair(rf.fd, a.lat_samples)
+            floor = float(np.median(pr))
+            paired["note"] = ("registered file; raw O_DIRECT pread and pread_gpu alternated read "
+                              "by read, order flipped every pair; overhead = median of pairwise "
+                              "differences")
+            phases = phase_split(rf.fd, min(a.lat_samples, 1000))
+        _, _, paired["plain_descriptor"] = pair(fd, min(a.lat_samples, 1000))
+        phases_plain = phase_split(fd, min(a.lat_samples, 1000))
+        S.evict_file(fd)
+        offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
+        lat_plain = S.pread_gpu_latency(buf.handle, 0, fd, offs)[50:] / 1e3
+        # the floor in a pass of its own (the round-4 vantage)
+        S.evict_file(fd)
+        raw_p50 = float(np.percentile(S.pread_raw_latency(fd, offs)[50:], 50)) / 1e3
         S.evict_file(fd)
         offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 500) + 50) * 4096
         py = []
@@ -279,39 +313,8 @@ def main() -> int:
                 py.append((t2 - t1) / 1e3)
         lat_py = np.array(py)
     p50, p99 = float(np.percentile(lat, 50)), float(np.percentile(lat, 99))
+    p50_plain = float(np.percentile(lat_plain, 50))
     p50_py = float(np.percentile(lat_py, 50))
-    # where the 4 KiB latency goes (native phase stamps, this rank's medians)
-    # and its floor: a bare O_DIRECT pread of the same offsets into host RAM
-    phases, raw_p50, paired = {}, float("nan"), {}
-    if a.lat_samples:
-        S.evict_file(fd)
-        offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
-        phases = S.phase_breakdown(S.pread_gpu_phases(buf.handle, 0, fd, offs)[50:])
-        S.evict_file(fd)
-        raw_p50 = float(np.percentile(S.pread_raw_latency(fd, offs)[50:], 50)) / 1e3
-        # the same comparison interleaved read by read (storage drift cancels)
-        S.evict_file(fd)
-        offs = rng.integers(0, F // 4096, size=2 * (min(a.lat_samples, 1000) + 50)) * 4096
-        pe, pr = (x[50:].astype(np.float64) / 1e3 for x in S.pread_pair_latency(buf.handle, 0, fd, offs))
-        paired = {"engine_p50_us": round(float(np.median(pe)), 2),
-                  "raw_p50_us": round(float(np.median(pr)), 2),
-                  "overhead_p50_us": round(float(np.median(pe - pr)), 2),
-                  "pairs": int(len(pe)),
-                  "note": "raw O_DIRECT pread and pread_gpu alternated read by read, "
-                          "order flipped every pair; overhead = median of pairwise differences"}
-        # the same through a registered file (S.RegisteredFile: the descriptor
-        # resolved once, no per-read kcmp / fstat)
-        with S.RegisteredFile(fd) as rf:
-            S.evict_file(fd)
-            offs = rng.integers(0, F // 4096, size=2 * (min(a.lat_samples, 1000) + 50)) * 4096
-            pe, pr = (x[50:].astype(np.float64) / 1e3 for x in S.pread_pair_latency(buf.handle, 0, rf.fd, offs))
-            paired["registered"] = {"engine_p50_us": round(float(np.median(pe)), 2),
-                                    "raw_p50_us": round(float(np.median(pr)), 2),
-                                    "overhead_p50_us": round(float(np.median(pe - pr)), 2)}
-            S.evict_file(fd)
-            offs = rng.integers(0, F // 4096, size=min(a.lat_samples, 1000) + 50) * 4096
-            paired["registered"]["phases_us"] = S.phase_breakdown(
-                S.pread_gpu_phases(buf.handle, 0, rf.fd, offs)[50:])
 
     # the same QD1 reads through the v0.6 ioctl pair (SSD2GPU + WAIT: task
     # table, residency probe, planner), and the host primitive costs below both
@@ -339,7 +342,8 @@ def main() -> int:
     vfs = W / vt / (1 << 30)
     # worst rank for latencies, sum of ranks for the control's throughput
     if world > 1:
-        p50, p99, p50_py, ioctl_p50 = allreduce([p50, p99, p50_py, ioctl_p50], dist.ReduceOp.MAX)
+        p50, p99, p50_py, ioctl_p50, p50_plain, floor = allreduce(
+            [p50, p99, p50_py, ioctl_p50, p50_plain, floor], dist.ReduceOp.MAX)
         vfs_total = allreduce([vfs], dist.ReduceOp.SUM)[0]
         seq_total = allreduce([seq_gib], dist.ReduceOp.SUM)[0]
         seq_modes = dict(zip(seq_modes, allreduce(list(seq_modes.values()), dist.ReduceOp.SUM)))
@@ -373,11 +377,16 @@ def main() -> int:
         "p50_4k_lat_us": round(p50, 2),
         "p99_4k_lat_us": round(p99, 2),
         "p50_4k_lat_python_us": round(p50_py, 2),
+        "p50_4k_lat_plain_fd_us": round(p50_plain, 2),
+        "p50_4k_lat_note": ("p50/p99: QD1 4 KiB pread_gpu through a registered file, alternated "
+                            "read by read with raw O_DIRECT preads (storage_4k_p50_us is their "
+                            "median: the floor at the same moment); plain_fd: a plain "
+                            "descriptor, native loop; raw_odirect: the floor in a pass of its own"),
         "p50_4k_lat_ioctl_us": round(ioctl_p50, 2),
         "host_costs_ns": costs,
         "engine_io_p50_us": round(S.hist_percentile(hist["io_ns"], 50) / 1e3, 2),
         "raw_odirect_4k_p50_us": round(raw_p50, 2),
-        "storage_4k_p50_us": round(raw_p50, 2),
+        "storage_4k_p50_us": round(floor, 2),
         "storage": {
             "fs_type": fstype,
             "dir": a.dir,
@@ -401,6 +410,7 @@ def main() -> int:
         "latency_reduction": "max over ranks (worst rank)",
         "ingest_grid": ing,
         "p50_4k_phases_us": phases,
+        "p50_4k_phases_plain_fd_us": phases_plain,
         "qd1_paired": paired,
         "verified_crc32c": bool(ver == 1.0),
         "avg_request_kib": round(0.5 * agg["nr_blocks"] / agg["nr_submit"], 1) if agg["nr_submit"] else 0,
