@@ -527,24 +527,29 @@ __device__ __forceinline__ int eval_prog(const strom_heap_scan2_args &g, const u
   // the program through the constant address space: it is never written
   // while the kernel runs, so its wave-uniform reads become scalar loads
   // (a generic pointer next to the kernel's own stores gets per-lane vector
-  // loads: ~20% of the scan's time on a one-qual program)
-  typedef const __attribute__((address_space(4))) strom_heap_qual2 cqual2;
-  cqual2 *prog = (cqual2 *)g.prog;
+  // loads).  One 32-byte s_load per qual, the next one issued before the
+  // current qual is evaluated.
+  typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+  typedef const __attribute__((address_space(4))) u32x8 cq8;
+  static_assert(sizeof(strom_heap_qual2) == 32, "one s_load_dwordx8 per qual");
+  cq8 *prog = (cq8 *)g.prog;
   const uint32_t n = g.nprog;
   uint32_t qi = 0;
+  u32x8 w = prog[0];                            // n >= 1 (program mode)
   while (qi < n) {
-    const uint32_t cl = prog[qi].clause;
+    const uint32_t cl = w[1];
     int cv = 0;                                 // the clause: 0 false, 1 true, 2 unknown
-    for (; qi < n && prog[qi].clause == cl; ++qi) {
+    do {
       strom_heap_qual2 q;
-      q.attno = prog[qi].attno;
-      q.kind = prog[qi].kind;
-      q.flags = prog[qi].flags;
+      q.attno = (int16_t)(w[0] & 0xffff);
+      q.kind = (uint8_t)(w[0] >> 16);
+      q.flags = (uint8_t)(w[0] >> 24);
       q.clause = cl;
-      q.nconst = prog[qi].nconst;
-      q.coff = prog[qi].coff;
-      q.lo = prog[qi].lo;
-      q.hi = prog[qi].hi;
+      q.nconst = w[2];
+      q.coff = w[3];
+      q.lo = (int64_t)((uint64_t)w[4] | ((uint64_t)w[5] << 32));
+      q.hi = (int64_t)((uint64_t)w[6] | ((uint64_t)w[7] << 32));
+      if (++qi < n) w = prog[qi];
       if (!live || cv == 1) continue;           // decided: skip the clause's rest
       if (q.attno != last) {
         if ((uint32_t)q.attno < s.next) s = deform_init(t, tlen);   // walk again from the start
@@ -559,7 +564,7 @@ __device__ __forceinline__ int eval_prog(const strom_heap_scan2_args &g, const u
       const int r = eval_qual2(q, (cu8 *)g.cpool, t, a);
       if (r == 1) cv = 1;
       else if (r == 2) cv = 2;
-    }
+    } while (qi < n && w[1] == cl);
     if (live) {
       if (cv == 0) {
         live = false;
@@ -904,7 +909,10 @@ extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   }
   // a program was checked by the caller against its host copy
   // (strom_heap_prog_check); it lives in device memory here
-  if (g->prog) return heap_scan_launch(*g, 2, stream);
+  if (g->prog) {
+    if (!g->nprog || !g->cpool || (g->cpool_len & 7)) return -22;   // the kernel reads prog[0]
+    return heap_scan_launch(*g, 2, stream);
+  }
   if (g->nquals < 0 || g->nquals > STROM_HEAP_MAX_QUALS) return -22;
   int last = -1;
   for (int q = 0; q < g->nquals; ++q) {

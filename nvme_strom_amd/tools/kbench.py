@@ -81,7 +81,7 @@ def main(argv=None):
         del pages
         # tuple descriptor + qualifier lists (strom_heap_scan2): 10 columns
         # with NULLs, short / long / TOASTed text before the predicated ones
-        from nvme_strom_amd.ops.heapscan import heap_scan2
+        from nvme_strom_amd.ops.heapscan import Program, heap_scan2
         from nvme_strom_amd.utils import pgtuple as T
         desc, rows = T.synthetic(4000, seed=2)
         tmpl = T.build_pages(rows, desc)
@@ -96,16 +96,19 @@ def main(argv=None):
                                                         T.Qual("d", "notnull"),
                                                         T.Qual("e", "between", (-0.5, 0.5)),
                                                         T.Qual("tail", "between", (0, 50))])):
-            log(name, timed(lambda: heap_scan2(pages, desc, qs, verify_checksum=True,
+            # compiled once, as a scan plan is (the program mode uploads it once)
+            P = Program(desc, qs)
+            log(name, timed(lambda: heap_scan2(pages, desc, P, verify_checksum=True,
                                                skip_invisible=True)), nb)
             # the same list through the program mode (device-memory CNF)
             log(name.replace("heap_scan2_", "heap_scan2_prog_"),
-                timed(lambda: heap_scan2(pages, desc, qs, verify_checksum=True,
+                timed(lambda: heap_scan2(pages, desc, P, verify_checksum=True,
                                          skip_invisible=True, program=True)), nb)
         # a CNF only the program mode takes: (a in range OR c IS NULL) AND b < 0.6
         cnf = [T.Or(T.Qual("a", "between", (-200_000, 300_000)), T.Qual("c", "isnull")),
                T.Qual("b", "lt", (0.6,))]
-        log("heap_scan2_prog_cnf2", timed(lambda: heap_scan2(pages, desc, cnf, verify_checksum=True,
+        P = Program(desc, cnf)
+        log("heap_scan2_prog_cnf2", timed(lambda: heap_scan2(pages, desc, P, verify_checksum=True,
                                                              skip_invisible=True)), nb)
         del pages
     rng = np.random.default_rng(1)
