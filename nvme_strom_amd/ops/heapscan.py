@@ -281,6 +281,8 @@ class Program:
         while not self.pool or len(self.pool) % 8:
             self.pool.append(0)
         self._dev: dict = {}
+        self._checked: set = set()        # tuple descriptors the program passed
+        self._arrays = None
 
     def device_arrays(self, dev, stream) -> tuple:
         """(program, pool) as device tensors on ``dev``: uploaded once (on
@@ -324,9 +326,11 @@ class Program:
         return out
 
     def arrays(self):
-        """(program bytes, pool bytes) for upload."""
-        raw = b"".join(bytes(q) for q in self.quals)
-        return raw, bytes(self.pool)
+        """(program bytes, pool bytes) for upload (a program is not changed
+        after compilation: built once)."""
+        if self._arrays is None:
+            self._arrays = (b"".join(bytes(q) for q in self.quals), bytes(self.pool))
+        return self._arrays
 
 
 def _exact(x):
@@ -386,9 +390,13 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
         for i, q in enumerate(fx):
             g.quals[i] = q
     elif prog.quals:
-        hp = np.frombuffer(raw, np.uint8)
-        check(lib().strom_heap_prog_check(C.byref(g.desc), hp.ctypes.data, len(prog.quals),
-                                          pool, len(pool)), "heap_scan2 program")
+        # checked once per program and tuple descriptor
+        dkey = bytes(g.desc)
+        if dkey not in prog._checked:
+            hp = np.frombuffer(raw, np.uint8)
+            check(lib().strom_heap_prog_check(C.byref(g.desc), hp.ctypes.data, len(prog.quals),
+                                              pool, len(pool)), "heap_scan2 program")
+            prog._checked.add(dkey)
         # uploaded once per program and device (complete before any launch
         # reads it), kept by the program and by the result
         ts = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.current_stream(dev)
