@@ -9,6 +9,7 @@
 //   - snappy raw format: greedy compressor + safe decoder.
 #include <errno.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <cstdint>
 #include <vector>
@@ -341,6 +342,62 @@ long strom_pg_apply_mvcc(void *page, uint32_t page_sz, const strom_pg_mvcc *m, u
     ++removed;
   }
   if (nrecheck) *nrecheck = nr;
+  return removed;
+}
+
+// The buffer-manager leg of the reference's chunk loader
+// (pgsql/nvme_strom.c:896-940: ReadBuffer, per-tuple visibility, copy into
+// the chunk) for the blocks a scan checks on the host: one pread per run of
+// consecutive blocks, the checksum ReadBuffer would verify, then the
+// in-place LP_UNUSED marking.  A page that is not a heap page is left as
+// read (the scan kernel reports its header).
+long strom_pg_read_check_pages(int fd, const uint32_t *blocks, uint32_t n, uint32_t relseg_blocks,
+                               uint32_t page_sz, void *stage, const strom_pg_mvcc *m,
+                               int verify_checksum, uint8_t *recheck_flags) {
+  if ((n && (!blocks || !stage)) || !m || page_sz < 1024 || (page_sz & 1023)) return -EINVAL;
+  uint8_t *out = (uint8_t *)stage;
+  long removed = 0;
+  std::vector<uint16_t> rc(page_sz / 4);
+  for (uint32_t i = 0; i < n;) {
+    // a run of blocks consecutive in the file: one read
+    uint32_t j = i + 1;
+    const uint64_t b0 = relseg_blocks ? blocks[i] % relseg_blocks : blocks[i];
+    while (j < n && blocks[j] == blocks[j - 1] + 1 &&
+           (relseg_blocks ? blocks[j] % relseg_blocks : blocks[j]) == b0 + (j - i))
+      ++j;
+    const size_t want = (size_t)(j - i) * page_sz;
+    size_t got = 0;
+    while (got < want) {
+      const ssize_t r = pread(fd, out + (size_t)i * page_sz + got, want - got,
+                              (off_t)(b0 * page_sz + got));
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        return -errno;
+      }
+      if (r == 0) break;
+      got += (size_t)r;
+    }
+    memset(out + (size_t)i * page_sz + got, 0, want - got);
+    for (uint32_t k = i; k < j; ++k) {
+      uint8_t *p = out + (size_t)k * page_sz;
+      bool ck_ok = false;
+      if (verify_checksum) {
+        const uint16_t stored = (uint16_t)(p[8] | (p[9] << 8));
+        ck_ok = strom_pg_checksum_host(p, blocks[k], page_sz) == stored;
+      }
+      uint32_t nr = 0;
+      const long r = strom_pg_apply_mvcc(p, page_sz, m, rc.data(), (uint32_t)rc.size(), &nr);
+      if (recheck_flags) recheck_flags[k] = r >= 0 && nr ? 1 : 0;
+      if (r <= 0) continue;
+      removed += r;
+      if (ck_ok) {
+        const uint16_t c = strom_pg_checksum_host(p, blocks[k], page_sz);
+        p[8] = (uint8_t)c;
+        p[9] = (uint8_t)(c >> 8);
+      }
+    }
+    i = j;
+  }
   return removed;
 }
 

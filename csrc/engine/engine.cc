@@ -145,10 +145,11 @@ const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *e
   TlFile &tl = tl_file;
   static const std::shared_ptr<OpenFile> none;
   if (fast) *fast = false;
-  // fast path: the same descriptor still names the same open file
-  // description (its size may have moved: callers redo a read that looks
-  // past the end or comes back short with forget_cached_file())
-  if (tl.fd == fd && tl.eng == gen_ && tl.f && tl.dup >= 0 && g_kcmp.load(std::memory_order_relaxed) != 0 &&
+  // fast path (config fd_kcmp): the same descriptor still names the same
+  // open file description (its size may have moved: callers redo a read
+  // that looks past the end or comes back short with forget_cached_file())
+  const bool use_kcmp = config().fd_kcmp && g_kcmp.load(std::memory_order_relaxed) != 0;
+  if (use_kcmp && tl.fd == fd && tl.eng == gen_ && tl.f && tl.dup >= 0 &&
       same_description(fd, tl.dup)) {
     g_kcmp.store(1, std::memory_order_relaxed);
     if (fast) *fast = true;
@@ -171,9 +172,14 @@ const std::shared_ptr<Engine::OpenFile> &Engine::open_file_cached(int fd, int *e
       return none;
     }
   }
-  if (tl.fd != fd || tl.dup < 0 || !same) {
+  if (!use_kcmp) {
+    // no dup of the caller's descriptor is kept (a close of one would drop
+    // the process's record locks on the file): identity by fstat each call
     if (tl.dup >= 0) close(tl.dup);
-    tl.dup = g_kcmp.load(std::memory_order_relaxed) != 0 ? fcntl(fd, F_DUPFD_CLOEXEC, 0) : -1;
+    tl.dup = -1;
+  } else if (tl.fd != fd || tl.dup < 0 || !same) {
+    if (tl.dup >= 0) close(tl.dup);
+    tl.dup = fcntl(fd, F_DUPFD_CLOEXEC, 0);
   }
   tl.fd = fd;
   return tl.f;
@@ -237,6 +243,11 @@ void Engine::refresh_registered(int rfd) {
     reg_[i] = nf;
     reg_ver_.fetch_add(1, std::memory_order_release);
   }
+}
+
+std::shared_ptr<Engine::OpenFile> Engine::task_file(int fd, int *err) {
+  if (is_registered_id(fd)) refresh_registered(fd);   // one fstat on the engine's descriptor
+  return open_file(fd, err);
 }
 
 std::shared_ptr<Engine::OpenFile> Engine::open_file(int fd, int *err) {
@@ -420,8 +431,9 @@ int Engine::check_file(strom_check_file *a) {
   }
   FileClass fc;
   if (is_registered_id(a->fdesc)) {
-    const auto &f = registered(a->fdesc);
-    if (!f) return -EBADF;
+    int err = 0;
+    const auto f = task_file(a->fdesc, &err);
+    if (!f) return err ? err : -EBADF;
     fc = f->fc;
   } else {
     int rc = classify_file(a->fdesc, &fc, config().strict);
@@ -520,7 +532,7 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   std::shared_ptr<OpenFile> f;
   if (!ss) {
     if (a->file_desc >= kStripeFdBase) return -EBADF;
-    f = open_file(a->file_desc, &err);
+    f = task_file(a->file_desc, &err);
     if (!f) return err;
   }
 
@@ -675,7 +687,7 @@ int Engine::memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a) {
   std::shared_ptr<OpenFile> f;
   if (!ss) {
     if (a->file_desc >= kStripeFdBase) return -EBADF;
-    f = open_file(a->file_desc, &err);
+    f = task_file(a->file_desc, &err);
     if (!f) return err;
   }
 

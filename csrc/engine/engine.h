@@ -89,6 +89,14 @@ struct Config {
   uint32_t ingest_min = 0;       // worker requests below this go staging -> BAR by
                                  // CPU stores even when the ingest grid runs
   bool io_prof = false;          // per-worker phase attribution (strom_io_prof)
+  bool fd_kcmp = false;          // synchronous reads on a plain descriptor: keep a
+                                 // dup of it and check identity with kcmp (~90 ns
+                                 // below an fstat).  Opt-in: closing that dup when
+                                 // the thread moves to another file drops the
+                                 // process's fcntl record locks on the file, and
+                                 // while held it keeps flock locks and an unlinked
+                                 // file's space alive; registered
+                                 // files (strom_register_file) skip both costs
   bool strict = false;           // reference CHECK_FILE rules only
   bool direct_io = true;         // O_DIRECT reads of uncached chunks
   bool pgcache_probe = true;     // residency scoring (mincore)
@@ -591,6 +599,11 @@ class Engine {
   std::shared_ptr<StripeSet> stripe(int fd);
   // re-read a registered file's size (open_file on the engine's descriptor)
   void refresh_registered(int rfd);
+  // the file of an asynchronous task (MEMCPY_SSD2GPU / SSD2RAM / CHECK_FILE):
+  // a registered id's size is re-read first — such a task cannot redo a
+  // read after it returned, so a grown or shrunk file (a PostgreSQL segment)
+  // must be planned with its size now, not the one cached at registration
+  std::shared_ptr<OpenFile> task_file(int fd, int *err);
 
   std::unique_ptr<IoEngine> io_;
   std::mutex files_mu_;

@@ -213,6 +213,36 @@ int strom_verify_equal(const void *d_a, const void *d_b, uint64_t nbytes,
 int strom_fill_pattern(void *d_buf, uint64_t nbytes, uint32_t pattern,
                        void *stream);
 
+/* The full HeapTupleSatisfiesMVCC inputs (heapam_visibility.c): snapshot
+ * (xmin, xmax, xip, subxip / suboverflowed), the scanning transaction's own
+ * xids and command id, and windows of the SLRU logs — pg_xact (2 bits per
+ * xid from clog_base), pg_subtrans (parent xid per xid from subtrans_base),
+ * pg_multixact offsets (member offset per multixact from mx_base, n + 1
+ * entries: the last is the next offset) and members (PostgreSQL's page
+ * layout: 409 groups of 4 flag bytes + 4 xids per 8 KiB page, from member
+ * offset mxm_base).  Transaction ids compare modulo 2^32. */
+struct strom_pg_mvcc {
+	uint32_t xmin, xmax;
+	const uint32_t *xip;
+	uint32_t nxip;
+	uint32_t suboverflowed;
+	const uint32_t *subxip;
+	uint32_t nsubxip;
+	uint32_t curcid;
+	const uint32_t *curxids;  /* the scanning transaction: top xid + its subxacts */
+	uint32_t ncurxids;
+	uint32_t clog_base;
+	const uint8_t *clog;
+	uint64_t clog_n;
+	const uint32_t *subtrans;
+	uint32_t subtrans_base, subtrans_n;
+	const uint32_t *mx_offsets;
+	uint32_t mx_base, mx_n;
+	const uint8_t *mx_members;
+	uint64_t mxm_n;
+	uint32_t mxm_base, pad;
+};
+
 /* PostgreSQL heap pages (8 KiB by default). */
 struct strom_heap_scan_args {
 	const void *pages;       /* device: npages * page_sz bytes */
@@ -313,8 +343,38 @@ struct strom_heap_scan2_args {
 	const struct strom_heap_qual2 *prog;
 	const uint8_t *cpool;                 /* 8-aligned constants, cpool_len % 8 == 0 */
 	uint32_t nprog, cpool_len;
+	/* Snapshot visibility on the device (mvcc_on != 0): every LP_NORMAL
+	 * tuple of a page that is not PD_ALL_VISIBLE — and, with mvcc_pages,
+	 * whose byte is nonzero (the visibility map said "not all-visible") — is
+	 * checked with HeapTupleSatisfiesMVCC's rules (strom_pg_tuple_visible's,
+	 * pgsql/nvme_strom.c:907-936 runs them per buffer-manager tuple).  An
+	 * invisible tuple is dropped and counted in mvcc_removed[0]; one the
+	 * inputs cannot decide (combo cid, an xid / multixact outside the
+	 * windows) is kept, as the host check keeps it, and its page flagged
+	 * STROM_PAGE_RECHECK.  mvcc's pointers are DEVICE memory, and xip /
+	 * subxip / curxids must be sorted ascending (binary-searched). */
+	struct strom_pg_mvcc mvcc;
+	const uint8_t *mvcc_pages;            /* device, optional: per page */
+	uint32_t *mvcc_removed;               /* device, optional: u32[1] */
+	uint32_t mvcc_on, mvcc_pad;
 };
 int strom_heap_scan2(const struct strom_heap_scan2_args *a, void *stream);
+/* strom_heap_scan (the fixed-offset int predicate) with the device snapshot
+ * check above; m holds device pointers (NULL m: hint bits only). */
+int strom_heap_scan_mvcc(const struct strom_heap_scan_args *a, const struct strom_pg_mvcc *m,
+                         const uint8_t *mvcc_pages, uint32_t *mvcc_removed,
+                         uint32_t *recheck_count, void *stream);
+/* The host ("buffer manager") path for blocks checked on the CPU: each
+ * block blocks[i] is read (pread of page_sz bytes at (block % relseg_blocks)
+ * * page_sz; relseg_blocks 0: no modulo) into stage + i * page_sz, a short
+ * read zero-filled; with verify_checksum its checksum is tested first and,
+ * when valid, re-stamped after the edit (as ReadBuffer + a hint-bit write);
+ * then the tuples m hides are marked LP_UNUSED.  recheck_flags[i] (optional)
+ * = 1 when the block holds tuples the inputs cannot decide.  Returns the
+ * tuples removed, or -errno of a failed read. */
+long strom_pg_read_check_pages(int fd, const uint32_t *blocks, uint32_t n, uint32_t relseg_blocks,
+                               uint32_t page_sz, void *stage, const struct strom_pg_mvcc *m,
+                               int verify_checksum, uint8_t *recheck_flags);
 /* Checks a program and its pool (host copies of what prog / cpool hold)
  * before a launch: kinds against the attributes, contiguous clauses, every
  * constant (IN tables and the text entries they name, numeric digits)
@@ -349,35 +409,6 @@ uint16_t strom_pg_checksum_host(const void *page, uint32_t blkno,
 long strom_pg_apply_snapshot(void *page, uint32_t page_sz, uint32_t snap_xmin, uint32_t snap_xmax,
                              const uint32_t *xip, uint32_t nxip, const uint8_t *clog,
                              uint64_t clog_xids);
-/* The full HeapTupleSatisfiesMVCC inputs (heapam_visibility.c): snapshot
- * (xmin, xmax, xip, subxip / suboverflowed), the scanning transaction's own
- * xids and command id, and windows of the SLRU logs — pg_xact (2 bits per
- * xid from clog_base), pg_subtrans (parent xid per xid from subtrans_base),
- * pg_multixact offsets (member offset per multixact from mx_base, n + 1
- * entries: the last is the next offset) and members (PostgreSQL's page
- * layout: 409 groups of 4 flag bytes + 4 xids per 8 KiB page, from member
- * offset mxm_base).  Transaction ids compare modulo 2^32. */
-struct strom_pg_mvcc {
-	uint32_t xmin, xmax;
-	const uint32_t *xip;
-	uint32_t nxip;
-	uint32_t suboverflowed;
-	const uint32_t *subxip;
-	uint32_t nsubxip;
-	uint32_t curcid;
-	const uint32_t *curxids;  /* the scanning transaction: top xid + its subxacts */
-	uint32_t ncurxids;
-	uint32_t clog_base;
-	const uint8_t *clog;
-	uint64_t clog_n;
-	const uint32_t *subtrans;
-	uint32_t subtrans_base, subtrans_n;
-	const uint32_t *mx_offsets;
-	uint32_t mx_base, mx_n;
-	const uint8_t *mx_members;
-	uint64_t mxm_n;
-	uint32_t mxm_base, pad;
-};
 /* The same in-place marking with the full rules; tuples the inputs cannot
  * decide (a combo command id of the scanning transaction, an xid / multixact
  * outside the log windows) are kept and their line numbers (1-based)
@@ -429,6 +460,9 @@ int strom_decompress_zstd_mode(int codec, const void *d_src, void *d_dst,
 /* decoder choice for strom_decompress_zstd: -1 by stream count (default),
  * 0 / 1 forced; returns the previous setting */
 int strom_zstd_fp_mode(int mode);
+/* buffers kept per (device, stream) by the zstd decoders (literal slots,
+ * lane-parallel entry pools) */
+uint32_t strom_zstd_scratch_keep(void);
 /* free the library-kept zstd scratch (after the streams' last decodes) */
 int strom_zstd_release(void);
 /* the same decode on the CPU (the kernel's phases lane by lane) */

@@ -578,31 +578,236 @@ __device__ __forceinline__ int eval_prog(const strom_heap_scan2_args &g, const u
   return verdict;
 }
 
-// 1 keep, 0 drop, 2 undecidable (GEN: a text qual met a compressed value).
+// ---- snapshot visibility: HeapTupleSatisfiesMVCC on the device.
+// The reference hands every tuple of a block that is not all-visible to
+// HeapTupleSatisfiesVisibility on the CPU (pgsql/nvme_strom.c:907-936);
+// here each lane decides its own tuple from the header in the LDS page
+// image, with the snapshot in the kernel arguments (scalar loads) and the
+// SLRU windows — pg_xact, pg_subtrans, pg_multixact — in HBM, shared by
+// every wave (L2-resident: a scan's tuples name few distinct xids).  The
+// rules and their order are those of the host check (codecs.cc
+// tuple_visible); the xid lists are sorted on upload and binary-searched.
+// Three-valued like the qualifier programs: 1 visible, 0 not, -1 the inputs
+// cannot decide (combo command id, an xid outside a window).
+constexpr uint32_t kXmaxKeyshrLock = 0x0010, kComboCid = 0x0020, kXmaxExclLock = 0x0040,
+                   kXminInvalid = 0x0200, kXmaxCommitted = 0x0400, kXmaxIsMulti = 0x1000;
+
+struct MvccCtx {
+  const strom_pg_mvcc &m;
+  bool und;
+};
+
+__device__ __forceinline__ bool mv_normal(uint32_t x) { return x >= 3; }
+__device__ __forceinline__ bool mv_precedes(uint32_t a, uint32_t b) {   // TransactionIdPrecedes
+  if (!mv_normal(a) || !mv_normal(b)) return a < b;
+  return (int32_t)(a - b) < 0;
+}
+
+// membership in an ascending uint32 list (n may be 0)
+__device__ __forceinline__ bool mv_has(const uint32_t *s, uint32_t n, uint32_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint32_t v = s[mid];
+    if (v == x) return true;
+    if (v < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return false;
+}
+
+__device__ __forceinline__ int mv_clog(MvccCtx &c, uint32_t xid) {   // -1: outside the window
+  const uint64_t k = (uint32_t)(xid - c.m.clog_base);
+  if (!c.m.clog || k >= c.m.clog_n) return -1;
+  return (c.m.clog[k >> 2] >> ((k & 3) * 2)) & 3;
+}
+
+__device__ __forceinline__ bool mv_parent(MvccCtx &c, uint32_t xid, uint32_t &p) {
+  const uint32_t k = xid - c.m.subtrans_base;
+  if (!c.m.subtrans || k >= c.m.subtrans_n) return false;
+  p = c.m.subtrans[k];
+  return true;
+}
+
+__device__ bool mv_did_commit(MvccCtx &c, uint32_t xid) {        // TransactionIdDidCommit
+  for (int depth = 0; depth < 1024; ++depth) {
+    if (!mv_normal(xid)) return xid == 1 || xid == 2;
+    const int st = mv_clog(c, xid);
+    if (st < 0) {
+      c.und = true;
+      return false;
+    }
+    if (st != 3) return st == 1;
+    if (mv_precedes(xid, c.m.xmin)) return false;   // sub-committed, parent crashed
+    uint32_t p;
+    if (!mv_parent(c, xid, p)) {
+      c.und = true;
+      return false;
+    }
+    if (p == 0) return false;
+    xid = p;
+  }
+  c.und = true;
+  return false;
+}
+
+__device__ __forceinline__ bool mv_current(MvccCtx &c, uint32_t xid) {
+  return mv_normal(xid) && mv_has(c.m.curxids, c.m.ncurxids, xid);
+}
+
+__device__ bool mv_in_snapshot(MvccCtx &c, uint32_t xid) {       // XidInMVCCSnapshot
+  if (mv_precedes(xid, c.m.xmin)) return false;
+  if (!mv_precedes(xid, c.m.xmax)) return true;
+  if (!c.m.suboverflowed) {
+    if (mv_has(c.m.subxip, c.m.nsubxip, xid)) return true;
+  } else {
+    uint32_t top = xid, p = xid;                    // SubTransGetTopmostTransaction
+    for (int depth = 0; depth < 1024 && p; ++depth) {
+      top = p;
+      if (mv_precedes(p, c.m.xmin)) break;
+      uint32_t q;
+      if (!mv_parent(c, p, q) || (q && !mv_precedes(q, p))) {
+        c.und = true;
+        return true;
+      }
+      p = q;
+    }
+    xid = top;
+    if (mv_precedes(xid, c.m.xmin)) return false;
+  }
+  return mv_has(c.m.xip, c.m.nxip, xid);
+}
+
+__device__ __forceinline__ bool mv_locked_only(uint32_t mask) {   // HEAP_XMAX_IS_LOCKED_ONLY
+  return (mask & kXmaxLockOnly) ||
+         (mask & (kXmaxIsMulti | kXmaxKeyshrLock | kXmaxExclLock)) == kXmaxExclLock;
+}
+
+// MultiXactIdGetUpdateXid over PostgreSQL's member page layout (409 groups
+// of 4 status bytes + 4 xids per 8 KiB page); 0 when every member locks
+__device__ uint32_t mv_update_xid(MvccCtx &c, uint32_t multi) {
+  const uint32_t k = multi - c.m.mx_base;
+  if (!c.m.mx_offsets || k >= c.m.mx_n || !c.m.mx_members) {
+    c.und = true;
+    return 0;
+  }
+  const uint32_t off = c.m.mx_offsets[k], n = c.m.mx_offsets[k + 1] - off;
+  if (n > 65536) {
+    c.und = true;
+    return 0;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t mem = (uint32_t)(off + i - c.m.mxm_base);
+    if (mem >= c.m.mxm_n) {
+      c.und = true;
+      return 0;
+    }
+    const uint64_t group = mem / 4, page = group / 409, within = mem % 4;
+    const uint8_t *grp = c.m.mx_members + page * 8192 + (group % 409) * 20;
+    if (grp[within] > 3) {                          // NoKeyUpdate / Update
+      const uint8_t *x = grp + 4 + 4 * within;
+      return (uint32_t)x[0] | ((uint32_t)x[1] << 8) | ((uint32_t)x[2] << 16) |
+             ((uint32_t)x[3] << 24);
+    }
+  }
+  return 0;
+}
+
+// the tuple at t (LDS page image), infomask already read
+__device__ int mvcc_visible(const strom_pg_mvcc &m, const uint8_t *t, uint32_t mask) {
+  MvccCtx c{m, false};
+  const uint32_t xmin = lds_u32(t, 0), xmax = lds_u32(t, 4);
+  // the scanning transaction's own command id; a combo cid is backend-local
+  auto own_cid = [&](uint32_t &cid) {
+    if (mask & kComboCid) return false;
+    cid = lds_u32(t, 8);
+    return true;
+  };
+#define MV_UND(r) (c.und ? -1 : (r))
+  if (!(mask & kXminCommitted)) {
+    if (mask & kXminInvalid) return 0;
+    if (mv_current(c, xmin)) {
+      uint32_t cid;
+      if (!own_cid(cid)) return -1;
+      if (cid >= m.curcid) return 0;              // inserted after the scan started
+      if ((mask & kXmaxInvalid) || mv_locked_only(mask)) return 1;
+      if (mask & kXmaxIsMulti) {
+        const uint32_t up = mv_update_xid(c, xmax);
+        if (c.und) return -1;
+        if (!mv_current(c, up)) return 1;          // the updating subxact aborted
+        return cid >= m.curcid ? 1 : 0;
+      }
+      if (!mv_current(c, xmax)) return 1;          // the deleting subxact aborted
+      return cid >= m.curcid ? 1 : 0;
+    }
+    if (mv_in_snapshot(c, xmin)) return MV_UND(0);
+    if (!mv_did_commit(c, xmin)) return MV_UND(0);
+  } else if ((mask & (kXminCommitted | kXminInvalid)) != (kXminCommitted | kXminInvalid) &&
+             mv_in_snapshot(c, xmin)) {
+    return MV_UND(0);                              // committed, not for this snapshot
+  }
+  if (c.und) return -1;
+  if ((mask & kXmaxInvalid) || mv_locked_only(mask)) return 1;
+  if (mask & kXmaxIsMulti) {
+    const uint32_t up = mv_update_xid(c, xmax);
+    if (c.und) return -1;
+    if (!up) return 1;
+    if (mv_current(c, up)) {
+      uint32_t cid;
+      if (!own_cid(cid)) return -1;
+      return cid >= m.curcid ? 1 : 0;
+    }
+    if (mv_in_snapshot(c, up)) return MV_UND(1);
+    return MV_UND(mv_did_commit(c, up) ? 0 : 1);
+  }
+  if (!(mask & kXmaxCommitted)) {
+    if (mv_current(c, xmax)) {
+      uint32_t cid;
+      if (!own_cid(cid)) return -1;
+      return cid >= m.curcid ? 1 : 0;
+    }
+    if (mv_in_snapshot(c, xmax)) return MV_UND(1);
+    return MV_UND(mv_did_commit(c, xmax) ? 0 : 1);
+  }
+  return MV_UND(mv_in_snapshot(c, xmax) ? 1 : 0);
+#undef MV_UND
+}
+
+// Bits: 1 keep, 2 undecidable here (a text qual met a compressed value, or
+// the snapshot check could not decide: the page is flagged for a host
+// recheck), 4 removed by the snapshot check.  3 = kept AND flagged: an
+// undecided visibility keeps the tuple, as the host check does.
 // GEN 0: the fixed int attribute of strom_heap_scan; 1: the fixed-size AND
 // list (quals in the kernel arguments: scalar loads, early exit); 2: a
-// program in device memory.  Separate instances: the program evaluator's
-// registers and code stay out of the other two.
-template <int GEN>
+// program in device memory.  MV: the snapshot check on pages `check` marks.
+// Separate instances: the program evaluator's and the snapshot check's
+// registers and code stay out of the others.
+template <int GEN, bool MV>
 __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const uint8_t *pg,
-                                          uint32_t lp, bool all_visible) {
+                                          uint32_t lp, bool all_visible, bool check) {
   const strom_heap_scan_args &a = g.base;
   const uint32_t off = lp & 0x7fff, flags = (lp >> 15) & 3, len = lp >> 17;
   if (flags != kLpNormal || len < 23 || off < kSizeOfPageHeader || off + len > a.page_sz ||
       (off & 1))
-    return false;
+    return 0;
   const uint32_t w20 = lds_u32(pg, off + 20);  // t_infomask (16) | t_hoff (8) | bits
   const uint32_t infomask = w20 & 0xffff, hoff = (w20 >> 16) & 0xff;
   if ((a.flags & STROM_HEAP_SKIP_INVISIBLE) && !all_visible) {
     // no clog here: only hint bits that prove visibility count
-    if (!(infomask & kXminCommitted)) return false;
-    if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return false;
+    if (!(infomask & kXminCommitted)) return 0;
+    if (!(infomask & (kXmaxInvalid | kXmaxLockOnly))) return 0;
   }
-  if (GEN == 2) return eval_prog(g, pg + off, len);
-  if (GEN == 1) return g.nquals ? eval_quals(g, pg + off, len) : 1;
-  if (a.attr_off < 0) return true;
+  int und = 0;
+  if (MV && check) {
+    const int v = mvcc_visible(g.mvcc, pg + off, infomask);
+    if (v == 0) return 4;
+    if (v < 0) und = 2;
+  }
+  if (GEN == 2) return eval_prog(g, pg + off, len) | und;
+  if (GEN == 1) return (g.nquals ? eval_quals(g, pg + off, len) : 1) | und;
+  if (a.attr_off < 0) return 1 | und;
   const uint32_t at = hoff + (uint32_t)a.attr_off;
-  if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return false;
+  if ((infomask & kHeapHasNull) || at + (uint32_t)a.attr_width > len) return und;
   int64_t v;
   if (a.attr_width == 8) {
     const uint64_t lo = lds_u32(pg, off + at), hi = lds_u32(pg, off + at + 4);
@@ -610,7 +815,7 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
   } else {
     v = (int32_t)lds_u32(pg, off + at);
   }
-  return v >= a.lo && v <= a.hi;
+  return (v >= a.lo && v <= a.hi ? 1 : 0) | und;
 }
 
 // PAGE = page size known at compile time (0: a.page_sz at run time).  Each
@@ -621,7 +826,7 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
 // row "dequeue" — 2.1 TB/s).
 constexpr int kPerWave = 8;
 
-template <int PAGE, int GEN>
+template <int PAGE, int GEN, bool MV>
 __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan2_args g, uint32_t maxchunks,
                                                         uint32_t ppw) {
   const strom_heap_scan_args &a = g.base;
@@ -679,24 +884,30 @@ __global__ __launch_bounds__(256) void heap_scan_kernel(strom_heap_scan2_args g,
         uint32_t status = page_status(a, mypage, h, pg, lane);
         if (status == 0) {
           const bool all_visible = (h.flags & kPdAllVisible) != 0;
+          // the snapshot check: pages that are not PD_ALL_VISIBLE and that
+          // the visibility map (mvcc_pages) did not route around it
+          const bool check = MV && !all_visible && (!g.mvcc_pages || g.mvcc_pages[pg]);
           const uint32_t nitems = (h.lower - kSizeOfPageHeader) / 4;
           nchunks = (nitems + 63) / 64;
-          uint32_t recheck = 0;
+          uint32_t recheck = 0, removed = 0;
           for (uint32_t c = 0; c < nchunks; ++c) {
             const uint32_t i = c * 64 + lane;
             const int keep =
                 i < nitems
-                    ? tuple_keep<GEN>(g, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i), all_visible)
+                    ? tuple_keep<GEN, MV>(g, mypage, lds_u32a(mypage, kSizeOfPageHeader + 4 * i),
+                                          all_visible, check)
                     : 0;
-            const uint64_t m = __ballot(keep == 1);
+            const uint64_t m = __ballot(keep & 1);
             if (lane == 0) masks[j * maxchunks + c] = m;
             count += __popcll(m);
-            if (GEN) recheck += __popcll(__ballot(keep == 2));
+            if (GEN || MV) recheck += __popcll(__ballot(keep & 2));
+            if (MV) removed += __popcll(__ballot(keep & 4));
           }
-          if (GEN && recheck) {
+          if ((GEN || MV) && recheck) {
             status |= STROM_PAGE_RECHECK;
             if (lane == 0 && g.recheck_count) atomicAdd(g.recheck_count, recheck);
           }
+          if (MV && removed && lane == 0 && g.mvcc_removed) atomicAdd(g.mvcc_removed, removed);
         }
         if (lane == 0 && a.page_status) a.page_status[pg] = status;
       }
@@ -761,14 +972,27 @@ int heap_scan_launch(const strom_heap_scan2_args &g, int gen, void *stream) {
   const uint32_t cap = 256u * (per_cu ? per_cu : 1u) * 2u;
   if (grid > cap) grid = cap;
   auto launch = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, g, maxchunks, ppw); };
+  const bool mv = g.mvcc_on != 0;
   if (a->page_sz == 8192) {
-    if (gen == 2) launch(heap_scan_kernel<8192, 2>);
-    else if (gen == 1) launch(heap_scan_kernel<8192, 1>);
-    else launch(heap_scan_kernel<8192, 0>);
+    if (mv) {
+      if (gen == 2) launch(heap_scan_kernel<8192, 2, true>);
+      else if (gen == 1) launch(heap_scan_kernel<8192, 1, true>);
+      else launch(heap_scan_kernel<8192, 0, true>);
+    } else {
+      if (gen == 2) launch(heap_scan_kernel<8192, 2, false>);
+      else if (gen == 1) launch(heap_scan_kernel<8192, 1, false>);
+      else launch(heap_scan_kernel<8192, 0, false>);
+    }
   } else {
-    if (gen == 2) launch(heap_scan_kernel<0, 2>);
-    else if (gen == 1) launch(heap_scan_kernel<0, 1>);
-    else launch(heap_scan_kernel<0, 0>);
+    if (mv) {
+      if (gen == 2) launch(heap_scan_kernel<0, 2, true>);
+      else if (gen == 1) launch(heap_scan_kernel<0, 1, true>);
+      else launch(heap_scan_kernel<0, 0, true>);
+    } else {
+      if (gen == 2) launch(heap_scan_kernel<0, 2, false>);
+      else if (gen == 1) launch(heap_scan_kernel<0, 1, false>);
+      else launch(heap_scan_kernel<0, 0, false>);
+    }
   }
   return hipGetLastError() == hipSuccess ? 0 : -5;
 }
@@ -833,6 +1057,33 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
   strom_heap_scan2_args g;
   __builtin_memset(&g, 0, sizeof g);
   g.base = *a;
+  return heap_scan_launch(g, 0, stream);
+}
+
+// the snapshot inputs' shape (their contents are device memory): windows
+// within what the index arithmetic covers, lists present when counted
+static int mvcc_check(const strom_pg_mvcc &m) {
+  if ((m.nxip && !m.xip) || (m.nsubxip && !m.subxip) || (m.ncurxids && !m.curxids)) return -22;
+  if (m.clog_n > (1ull << 32)) return -22;
+  if (m.mx_n && (!m.mx_offsets || !m.mx_members)) return -22;
+  return 0;
+}
+
+extern "C" int strom_heap_scan_mvcc(const strom_heap_scan_args *a, const strom_pg_mvcc *m,
+                                    const uint8_t *mvcc_pages, uint32_t *mvcc_removed,
+                                    uint32_t *recheck_count, void *stream) {
+  if (!a) return -22;
+  strom_heap_scan2_args g;
+  __builtin_memset(&g, 0, sizeof g);
+  g.base = *a;
+  g.recheck_count = recheck_count;
+  if (m) {
+    if (mvcc_check(*m)) return -22;
+    g.mvcc = *m;
+    g.mvcc_on = 1;
+    g.mvcc_pages = mvcc_pages;
+    g.mvcc_removed = mvcc_removed;
+  }
   return heap_scan_launch(g, 0, stream);
 }
 
@@ -902,6 +1153,7 @@ extern "C" int strom_heap_prog_check(const strom_heap_tupdesc *d, const strom_he
 
 extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   if (!g || g->base.attr_off >= 0) return -22;
+  if (g->mvcc_on && mvcc_check(g->mvcc)) return -22;
   if (g->desc.natts < 1 || g->desc.natts > STROM_HEAP_MAX_ATTS) return -22;
   for (int i = 0; i < g->desc.natts; ++i) {
     const int al = g->desc.attalign[i], len = g->desc.attlen[i];

@@ -3583,6 +3583,11 @@ extern "C" int strom_decompress_zstd(int codec, const void *d_src, void *d_dst,
 
 extern "C" uint32_t strom_zstd_lds_bytes(void) { return (uint32_t)sizeof(zs::Smem); }
 
+// (device, stream) buffers the library keeps (literal slots, LP entry
+// pools): a caller decoding on more streams than this in turn evicts a
+// pool per decode
+extern "C" uint32_t strom_zstd_scratch_keep(void) { return (uint32_t)zs::kScratchKeep; }
+
 // frame-parallel workgroups (streams) resident per CU
 extern "C" uint32_t strom_zstd_fp_per_cu(void) { return zs::fp_per_cu(); }
 

@@ -169,7 +169,8 @@ class HeapScan2Args(C.Structure):
     _fields_ = [("base", HeapScanArgs), ("desc", HeapTupDesc), ("nquals", C.c_int32),
                 ("quals", HeapQual * HEAP_MAX_QUALS), ("recheck_count", C.c_void_p),
                 ("prog", C.c_void_p), ("cpool", C.c_void_p), ("nprog", C.c_uint32),
-                ("cpool_len", C.c_uint32)]
+                ("cpool_len", C.c_uint32), ("mvcc", PgMvcc), ("mvcc_pages", C.c_void_p),
+                ("mvcc_removed", C.c_void_p), ("mvcc_on", C.c_uint32), ("mvcc_pad", C.c_uint32)]
 
 
 class DecompDesc(C.Structure):
@@ -235,6 +236,11 @@ _SIGS = {
     "strom_pg_apply_mvcc": (C.c_long, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                        C.c_uint32, C.c_void_p]),
     "strom_pg_tuple_visible": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "strom_pg_read_check_pages": (C.c_long, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
+                                             C.c_void_p]),
+    "strom_heap_scan_mvcc": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p]),
     "strom_pg_apply_snapshot": (C.c_long, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "strom_atomic_fetch_add_u64": (C.c_uint64, [C.c_void_p, C.c_uint64]),
@@ -297,6 +303,7 @@ _SIGS = {
     "strom_zstd_scratch_sizes": (None, [C.c_void_p]),
     "strom_zstd_host_fp_stats": (None, [C.c_void_p]),
     "strom_zstd_fp_mode": (C.c_int, [C.c_int]),
+    "strom_zstd_scratch_keep": (C.c_uint32, []),
     "strom_zstd_fp_per_cu": (C.c_uint32, []),
     "strom_decompress_zstd_mode": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,

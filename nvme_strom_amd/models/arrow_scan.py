@@ -491,20 +491,43 @@ class ArrowScan:
     # 12 ms late, behind group 0's decode, and held groups 2-3's launches)
     MAX_RING_BYTES = 8 << 30
     MAX_SLOTS = 16
+    # HBM for everything a slot holds: its compressed ring share, its decode
+    # buffer and (ZSTD lane-parallel) the entry pool the library keeps for
+    # its stream (only the ring was counted)
+    MAX_SLOT_HBM = 48 << 30
 
-    def _slot_count(self, groups: List[_Group], nbytes: int) -> int:
+    def _lp_pool_bytes(self, dec: int) -> int:
+        """The LP decoder's entry pool for a decode of ``dec`` bytes
+        (zstd.hip strom_decompress_zstd_lp: STROM_ZSTD_LP_ENT x dst + block
+        and stream tables), 0 for other decoders."""
+        if getattr(self, "_codec", None) != D.ARROW_ZSTD or self.ZSTD_MODE != 2:
+            return 0
+        f = float(os.environ.get("STROM_ZSTD_LP_ENT") or 0) or 3.0
+        return int(f * dec) + (1 << 20) + dec // 32768 * 64
+
+    def _slot_count(self, groups: List[_Group], nbytes: int, dec: int = 0) -> int:
         """Slots of the HBM ring: one per group while they fit MAX_RING_BYTES
-        / MAX_SLOTS, never fewer than nslots (or than the groups).  The
-        read-ahead stays nslots - 1 groups either way."""
+        / MAX_SLOTS and, with their decode buffers and LP pools, MAX_SLOT_HBM;
+        never fewer than nslots (or than the groups).  ZSTD lane-parallel
+        slots are also capped by the pools the library keeps per stream
+        (strom_zstd_scratch_keep): one more slot would evict another slot's
+        pool every decode — a hipFree that waits for the device, and a
+        multi-GB hipMalloc.  The read-ahead stays nslots - 1 groups."""
         n = len(groups)
-        fit = max(1, min(self.MAX_SLOTS, self.MAX_RING_BYTES // max(nbytes, 1)))
-        return max(1, min(n, max(self.nslots, fit)))
+        per_slot = nbytes + dec + self._lp_pool_bytes(dec)
+        fit = max(1, min(self.MAX_SLOTS, self.MAX_RING_BYTES // max(nbytes, 1),
+                         self.MAX_SLOT_HBM // max(per_slot, 1)))
+        want = max(1, min(n, max(self.nslots, fit)))
+        if self._lp_pool_bytes(dec):
+            from .. import _native as N
+            want = min(want, max(1, int(N.lib().strom_zstd_scratch_keep())))
+        return want
 
     def _ensure_slots(self, groups: List[_Group]) -> None:
         nbytes = max(len(g.ids) for g in groups) * self.chunk_sz
         dec = max(max(g.dec_bytes for g in groups), 64)
         words = max(max(g.words for g in groups), 1)
-        want_slots = self._slot_count(groups, nbytes)
+        want_slots = self._slot_count(groups, nbytes, dec)
         if self._slots and len(self._slots) >= want_slots and (
                 self._slots[0].cap >= nbytes and
                             self._slots[0].dec.numel() >= dec and

@@ -14,10 +14,14 @@ Reference map (pgsql/nvme_strom.c):
     threshold and cost model (:502-580)             -> :func:`plan_scan`
   * chunk ring + load + tuple iteration (:852-1123) -> :class:`HeapRelationScan`
   * visibility-map routing (:870-940): with a snapshot, all-visible blocks
-    go to DMA unchecked, the others are read through the host ("buffer
-    manager") and every tuple is checked against the snapshot + commit log,
-    invisible ones marked unused, before the chunk is scanned
-    (utils/pgmvcc.py, native strom_pg_apply_snapshot)
+    are taken unchecked and every tuple of the others is checked against
+    the snapshot, pg_xact, pg_subtrans and pg_multixact.  The reference reads
+    those blocks through the buffer manager and checks them on the CPU; here
+    every block is read SSD->HBM and the scan kernel runs the check
+    (ScanConfig.mvcc_device, heapscan.hip mvcc_visible) for the pages the VM
+    flags, so a relation that is not all-visible scans at the same rate.
+    ``mvcc_device=False`` keeps the reference's split (native
+    strom_pg_read_check_pages: pread + checksum + in-place LP_UNUSED)
   * ExecReScanNVMEStrom cursor reset (:1168-1176)  -> :meth:`ParallelCursor.rescan`;
     the reference persists no scan state, :class:`ResumableScan` adds
     block-range checkpoints so an interrupted scan resumes where it stopped
@@ -45,7 +49,8 @@ import numpy as np
 import torch
 
 from .. import api
-from ..ops.heapscan import PAGE_RECHECK, Program, heap_project_many, heap_scan, heap_scan2
+from ..ops.heapscan import (PAGE_RECHECK, DeviceMvcc, Program, heap_project_many, heap_scan,
+                            heap_scan2)
 from ..tensor import FileReader, HbmBuffer, host_buffer
 from ..utils import pgmvcc, pgpage, pgtuple
 from ..utils.pgmvcc import CommitLog, MultiXact, Snapshot, SubTrans
@@ -72,6 +77,12 @@ class ScanConfig:
     # xids, overflowed snapshots) and pg_multixact (multixact xmax)
     subtrans: Optional[SubTrans] = None
     multixact: Optional[MultiXact] = None
+    # where the snapshot check runs: True (default) on the GPU — every block
+    # is read SSD->HBM and the scan kernel checks the tuples of the blocks
+    # the VM does not call all-visible (ops.heapscan.DeviceMvcc); False: the
+    # reference's split, those blocks read and checked on the host
+    # (native strom_pg_read_check_pages) and copied in after the DMA blocks
+    mvcc_device: bool = True
 
     def validate(self) -> None:
         if self.chunk_size % BLCKSZ or self.buffer_size % self.chunk_size:
@@ -422,9 +433,12 @@ class HeapRelationScan:
         self._finalizer = weakref.finalize(self, HeapRelationScan._drain, self._pool,
                                            self._pool_lock)
 
+    def _host_mvcc(self) -> bool:
+        return self.cfg.snapshot is not None and not self.cfg.mvcc_device
+
     def _pool_key(self) -> tuple:
         c = self.cfg
-        return (c.buffer_size, c.chunk_size, c.snapshot is not None, str(self.device))
+        return (c.buffer_size, c.chunk_size, self._host_mvcc(), str(self.device))
 
     def _acquire(self) -> tuple:
         key = self._pool_key()
@@ -450,7 +464,7 @@ class HeapRelationScan:
         wbs = [host_buffer(cfg.chunk_size) for _ in range(nslots)]
         # checked-path pages (MVCC mode) are staged here, then copied to HBM
         # right after the chunk's DMA blocks
-        cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if cfg.snapshot is not None else []
+        cpu_bufs = [host_buffer(cfg.chunk_size) for _ in range(nslots)] if self._host_mvcc() else []
         return sess, hb, readers, wbs, cpu_bufs
 
     def _release(self, rs: tuple) -> None:
@@ -492,6 +506,11 @@ class HeapRelationScan:
         b0, b1 = _block_range(blocks, self.rel.nblocks)
         if cursor is None:
             cursor = ParallelCursor(b1, start=b0)
+        # the snapshot check's inputs, uploaded once per run for every
+        # participant's launches (they may change between runs)
+        c = self.cfg
+        self._dmvcc = (DeviceMvcc(c.snapshot, c.clog, c.subtrans, c.multixact, self.device)
+                       if c.snapshot is not None and c.mvcc_device else None)
         results: List[ScanResult] = []
         errors: List[BaseException] = []
         t0 = time.perf_counter()
@@ -531,7 +550,7 @@ class HeapRelationScan:
 
     def _participant(self, cursor) -> ScanResult:
         cfg = self.cfg
-        mvcc = cfg.snapshot is not None
+        mvcc = self._host_mvcc()          # the host leg of the VM split
         per_chunk = cfg.chunk_size // BLCKSZ
         nslots = cfg.buffer_size // cfg.chunk_size
         rs = self._acquire()
@@ -580,23 +599,16 @@ class HeapRelationScan:
 
     def _checked_pages(self, fd: int, blocks: np.ndarray, stage: torch.Tensor,
                        st: "ScanResult") -> int:
-        """Buffer-manager path: read each block through the page cache and
-        mark the tuples the snapshot must not see as unused (blocks with
-        tuples the inputs cannot decide go to ``st.recheck_blocks``)."""
+        """Buffer-manager path (``mvcc_device=False``, and the host recheck
+        leg): read the blocks and mark the tuples the snapshot must not see
+        as unused, natively (blocks with tuples the inputs cannot decide go
+        to ``st.recheck_blocks``)."""
         arr = stage.numpy() if stage.device.type == "cpu" else stage.cpu().numpy()
-        removed = 0
-        for j, b in enumerate(blocks.tolist()):
-            page = arr[j * BLCKSZ:(j + 1) * BLCKSZ]
-            got = os.preadv(fd, [memoryview(page)], (b % self.rel.relseg_size) * BLCKSZ)
-            if got < BLCKSZ:
-                page[got:] = 0
-            rc: List[int] = []
-            removed += pgmvcc.apply_snapshot(page, self.cfg.snapshot, self.cfg.clog,
-                                             b if self.cfg.verify_checksum else None,
-                                             subtrans=self.cfg.subtrans,
-                                             multi=self.cfg.multixact, recheck=rc)
-            if rc:
-                st.recheck_blocks.append(int(b))
+        c = self.cfg
+        removed, rc = pgmvcc.read_check_pages(fd, blocks, arr, c.snapshot, c.clog,
+                                              self.rel.relseg_size, c.verify_checksum,
+                                              c.subtrans, c.multixact, BLCKSZ)
+        st.recheck_blocks += [int(b) for b in blocks[rc.astype(bool)]]
         return removed
 
     def _consume(self, item, hb, readers, found, st: ScanResult) -> None:
@@ -607,17 +619,28 @@ class HeapRelationScan:
         n = len(landed)
         pages = hb.tensor[slot * self.cfg.chunk_size: slot * self.cfg.chunk_size + n * BLCKSZ]
         blk = torch.from_numpy(landed.astype(np.int64).astype(np.uint32).view(np.int32)).to(pages.device)
-        # MVCC mode: visibility is settled (all-visible blocks unchecked, the
-        # rest filtered against the snapshot): every LP_NORMAL tuple counts
+        # MVCC mode: visibility is the snapshot's (all-visible blocks
+        # unchecked, the rest checked on the device or already filtered on
+        # the host): no hint-bit rule
         skip = self.cfg.skip_invisible and self.cfg.snapshot is None
         general = self.desc is not None
+        dm = getattr(self, "_dmvcc", None)
+        chk = None
+        if dm is not None:
+            # the VM's verdict per landed block: 1 = check its tuples
+            vm = self.rel.vm
+            chk = (np.ones(n, np.uint8) if vm is None
+                   else ((vm[landed.astype(np.int64)] & pgmvcc.VM_ALL_VISIBLE) == 0).astype(np.uint8))
+            st.nr_checked += int(chk.sum())
         if general:
             r = heap_scan2(pages, self.desc, self._prog, BLCKSZ,
                            verify_checksum=self.cfg.verify_checksum, skip_invisible=skip,
-                           blknos=blk)
+                           blknos=blk, mvcc=dm, mvcc_pages=chk)
         else:
             r = heap_scan(pages, BLCKSZ, verify_checksum=self.cfg.verify_checksum,
-                          skip_invisible=skip, blknos=blk, **self.pred)
+                          skip_invisible=skip, blknos=blk, mvcc=dm, mvcc_pages=chk,
+                          **self.pred)
+        st.removed += int(r.removed)
         # the kernel reserves output per workgroup (arbitrary order across
         # workgroups): sort the chunk's items on the GPU (page order) before
         # the copy, so chunks only need ordering by their first block
@@ -653,7 +676,7 @@ class HeapRelationScan:
             vals = [[x[j] for j in o] if isinstance(x, list) else x[o] for x in vals]
         found.append((int(landed.min()) if n else 0, ptrs, vals, valid))
         status = r.page_status.cpu().numpy()
-        if general:
+        if general or dm is not None:
             st.recheck_blocks += [int(landed[j]) for j in np.nonzero(status & PAGE_RECHECK)[0]]
         st.pages += n
         st.bad_pages += int(((status & 3) != 0).sum())
@@ -746,19 +769,15 @@ def cpu_scan(rel: Relation, cfg: Optional[ScanConfig] = None, attr_off: int = -1
                         r = api.memcpy_ssd2ram(buf.address, fd, ids, BLCKSZ, rel.relseg_size)
                         api.memcpy_wait(r.dma_task_id)
                         st.add_io(r)
-                    for j, b in enumerate(cpu_ids.tolist()):
-                        # buffer-manager path: page cache read + snapshot check
-                        page = buf.array[(len(ids) + j) * BLCKSZ:(len(ids) + j + 1) * BLCKSZ]
-                        got = os.preadv(fd, [memoryview(page)], (b % rel.relseg_size) * BLCKSZ)
-                        if got < BLCKSZ:
-                            page[got:] = 0
-                        rc: List[int] = []
-                        st.removed += pgmvcc.apply_snapshot(page, cfg.snapshot, cfg.clog,
-                                                            b if cfg.verify_checksum else None,
-                                                            subtrans=cfg.subtrans,
-                                                            multi=cfg.multixact, recheck=rc)
-                        if rc:
-                            st.recheck_blocks.append(int(b))
+                    if len(cpu_ids):
+                        # buffer-manager path: page cache read + snapshot
+                        # check (native), after the DMA'd blocks
+                        stage = buf.array[len(ids) * BLCKSZ:(len(ids) + len(cpu_ids)) * BLCKSZ]
+                        rm, rc = pgmvcc.read_check_pages(fd, cpu_ids, stage, cfg.snapshot, cfg.clog,
+                                                         rel.relseg_size, cfg.verify_checksum,
+                                                         cfg.subtrans, cfg.multixact, BLCKSZ)
+                        st.removed += rm
+                        st.recheck_blocks += [int(b) for b in cpu_ids[rc.astype(bool)]]
                     st.nr_checked += len(cpu_ids)
                     blocks_here = np.concatenate([ids, cpu_ids]).astype(np.int64)
                     # block numbers feed the checksum: scan page by page

@@ -24,18 +24,83 @@ class HeapScanResult:
     items: torch.Tensor        # int32 (page << 16 | lineno), unordered
     count: int
     page_status: torch.Tensor  # int32 per page (PAGE_* bits)
+    # snapshot mode (mvcc=): tuples the device check removed; tuples it could
+    # not decide (kept, their pages flagged PAGE_RECHECK) add to ``recheck``
+    removed: int = 0
+    recheck: int = 0
 
     def sorted_items(self) -> np.ndarray:
         return np.sort(self.items[:self.count].cpu().numpy().view(np.uint32))
+
+
+class DeviceMvcc:
+    """HeapTupleSatisfiesMVCC's inputs in HBM for the scan kernels' snapshot
+    check: the snapshot (xip / subxip / the scanning transaction's xids,
+    sorted for the device's binary search), and the pg_xact, pg_subtrans and
+    pg_multixact windows (utils.pgmvcc objects).  Uploaded once — a scan
+    builds one per run and every chunk's launch reads it — and kept alive by
+    this object; ``struct`` is the strom_pg_mvcc of device pointers."""
+
+    def __init__(self, snap, clog=None, subtrans=None, multi=None, device="cuda"):
+        dev = torch.device(device)
+        self.device = dev
+        self._keep = []
+        m = N.PgMvcc()
+
+        def up(a: np.ndarray):
+            a = np.ascontiguousarray(a)
+            if a.size == 0:
+                return None
+            t = torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(dev)
+            self._keep.append(t)
+            return ptr(t)
+
+        def xids(v):
+            return np.unique(np.asarray([int(x) & 0xFFFFFFFF for x in v], dtype=np.uint32))
+        m.xmin, m.xmax = snap.xmin & 0xFFFFFFFF, snap.xmax & 0xFFFFFFFF
+        xip, sub, cur = xids(snap.xip), xids(snap.subxip), xids(snap.curxids)
+        m.xip, m.nxip = up(xip), len(xip)
+        m.subxip, m.nsubxip = up(sub), len(sub)
+        m.curxids, m.ncurxids = up(cur), len(cur)
+        m.suboverflowed = int(bool(snap.suboverflowed))
+        m.curcid = snap.curcid
+        if clog is not None:
+            m.clog, m.clog_n, m.clog_base = up(clog.bits), clog.nxids, clog.base
+        if subtrans is not None:
+            m.subtrans, m.subtrans_n = up(subtrans.parent), len(subtrans.parent)
+            m.subtrans_base = subtrans.base
+        if multi is not None:
+            off, mem = multi.offsets_array(), multi.members_pages()
+            m.mx_offsets, m.mx_base, m.mx_n = up(off), multi.base, len(off) - 1
+            m.mx_members, m.mxm_n, m.mxm_base = up(mem), len(multi.members), multi.members_base
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
+        self.struct = m
+
+
+def _mvcc_pages(mvcc_pages, npages: int, dev):
+    """The per-page check flags as a device uint8 tensor (None: every page
+    that is not PD_ALL_VISIBLE is checked)."""
+    if mvcc_pages is None:
+        return None
+    t = mvcc_pages if isinstance(mvcc_pages, torch.Tensor) else torch.from_numpy(
+        np.ascontiguousarray(np.asarray(mvcc_pages, dtype=np.uint8)))
+    t = t.to(device=dev, dtype=torch.uint8)
+    if t.numel() < npages:
+        raise ValueError(f"mvcc_pages has {t.numel()} entries for {npages} pages")
+    return t
 
 
 def heap_scan(pages: torch.Tensor, page_sz: int = 8192, verify_checksum: bool = False,
               skip_invisible: bool = False, attr_off: int = -1, attr_width: int = 4,
               lo: int = -(1 << 63), hi: int = (1 << 63) - 1, blkno_base: int = 0,
               out_cap: Optional[int] = None, blknos: Optional[torch.Tensor] = None,
-              stream=None) -> HeapScanResult:
+              stream=None, mvcc: Optional[DeviceMvcc] = None, mvcc_pages=None) -> HeapScanResult:
     """Scan ``pages`` (uint8, npages*page_sz) for visible LP_NORMAL tuples,
-    optionally filtered by lo <= int column at ``attr_off`` (after t_hoff) <= hi."""
+    optionally filtered by lo <= int column at ``attr_off`` (after t_hoff) <= hi.
+    ``mvcc`` (a DeviceMvcc): every tuple of a page that is not PD_ALL_VISIBLE
+    (and whose ``mvcc_pages`` flag, when given, is nonzero) is checked
+    against the snapshot on the device."""
     require_cuda(pages, "pages")
     pages = pages.view(torch.uint8)
     if pages.numel() % page_sz:
@@ -43,17 +108,23 @@ def heap_scan(pages: torch.Tensor, page_sz: int = 8192, verify_checksum: bool = 
     npages = pages.numel() // page_sz
     cap = out_cap if out_cap is not None else npages * (page_sz // 28 + 1)
     items = torch.empty(max(cap, 1), dtype=torch.int32, device=pages.device)
-    count = torch.zeros(1, dtype=torch.int32, device=pages.device)
+    cnt = torch.zeros(3, dtype=torch.int32, device=pages.device)   # count, recheck, removed
     status = torch.empty(max(npages, 1), dtype=torch.int32, device=pages.device)
     flags = (VERIFY_CHECKSUM if verify_checksum else 0) | (SKIP_INVISIBLE if skip_invisible else 0)
     a = N.HeapScanArgs(pages=ptr(pages), npages=npages, page_sz=page_sz, flags=flags,
                        attr_off=attr_off, attr_width=attr_width, lo=lo, hi=hi,
-                       out_items=ptr(items), out_cap=cap, out_count=ptr(count),
+                       out_items=ptr(items), out_cap=cap, out_count=ptr(cnt),
                        page_status=ptr(status), blkno_base=blkno_base,
                        blknos=ptr(blknos) if blknos is not None else None)
-    check(lib().strom_heap_scan(C.byref(a), stream_handle(stream)), "heap_scan")
-    n = int(count.item())
-    return HeapScanResult(items, min(n, cap), status[:npages])
+    if mvcc is None:
+        check(lib().strom_heap_scan(C.byref(a), stream_handle(stream)), "heap_scan")
+    else:
+        mp = _mvcc_pages(mvcc_pages, npages, pages.device)
+        check(lib().strom_heap_scan_mvcc(C.byref(a), C.byref(mvcc.struct),
+                                         ptr(mp) if mp is not None else None, ptr(cnt) + 8,
+                                         ptr(cnt) + 4, stream_handle(stream)), "heap_scan_mvcc")
+    c = cnt.cpu().tolist()
+    return HeapScanResult(items, min(c[0], cap), status[:npages], removed=c[2], recheck=c[1])
 
 
 # ------------------------------------------------- tuple descriptor + quals
@@ -346,19 +417,22 @@ def _fbits(x: float) -> int:
 
 @dataclass
 class HeapScan2Result(HeapScanResult):
-    recheck: int = 0                     # undecidable tuples (pages flagged PAGE_RECHECK)
+    pass                                 # recheck: undecidable tuples (pages flagged PAGE_RECHECK)
 
 
 def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
                verify_checksum: bool = False, skip_invisible: bool = False,
                blkno_base: int = 0, out_cap: Optional[int] = None,
                blknos: Optional[torch.Tensor] = None, stream=None,
-               sync: bool = True, program: bool = False) -> HeapScan2Result:
+               sync: bool = True, program: bool = False,
+               mvcc: Optional[DeviceMvcc] = None, mvcc_pages=None) -> HeapScan2Result:
     """Scan ``pages`` deforming every tuple with ``desc`` (utils.pgtuple) and
     keeping the ones ``quals`` selects: a list of ``pgtuple.Qual`` (ANDed)
     and ``pgtuple.Or`` clauses (CNF), or a compiled ``Program``.
-    ``sync=False`` leaves ``count`` / ``recheck`` as device tensors (no host
-    read); ``program=True`` runs the program mode even for a plain AND list."""
+    ``sync=False`` leaves ``count`` / ``recheck`` / ``removed`` as device
+    tensors (no host read); ``program=True`` runs the program mode even for a
+    plain AND list; ``mvcc`` / ``mvcc_pages``: the snapshot check, as in
+    :func:`heap_scan`."""
     require_cuda(pages, "pages")
     pages = pages.view(torch.uint8)
     if pages.numel() % page_sz:
@@ -367,7 +441,7 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
     cap = out_cap if out_cap is not None else npages * (page_sz // 28 + 1)
     dev = pages.device
     items = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int32, device=dev)      # [count, recheck]
+    cnt = torch.zeros(3, dtype=torch.int32, device=dev)      # [count, recheck, removed]
     status = torch.empty(max(npages, 1), dtype=torch.int32, device=dev)
     flags = (VERIFY_CHECKSUM if verify_checksum else 0) | (SKIP_INVISIBLE if skip_invisible else 0)
     g = N.HeapScan2Args()
@@ -405,18 +479,21 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
         g.nprog, g.cpool_len = len(prog.quals), len(pool)
         keep = [d_prog, d_pool]
     g.recheck_count = ptr(cnt) + 4
-    if npages:
-        cnt[1].zero_()
+    if mvcc is not None:
+        mp = _mvcc_pages(mvcc_pages, npages, dev)
+        g.mvcc, g.mvcc_on = mvcc.struct, 1
+        g.mvcc_pages = ptr(mp) if mp is not None else None
+        g.mvcc_removed = ptr(cnt) + 8
+        keep = keep + [mp, mvcc]
     check(lib().strom_heap_scan2(C.byref(g), stream_handle(stream)), "heap_scan2")
     if not sync:
         r = HeapScan2Result(items, cnt[0:1], status[:npages])
         r.recheck = cnt[1:2]
+        r.removed = cnt[2:3]
         r.keep = keep
         return r
     c = cnt.cpu().tolist()
-    r = HeapScan2Result(items, min(c[0], cap), status[:npages])
-    r.recheck = c[1]
-    return r
+    return HeapScan2Result(items, min(c[0], cap), status[:npages], removed=c[2], recheck=c[1])
 
 
 def heap_project(pages: torch.Tensor, items: torch.Tensor, count: torch.Tensor, desc, col,

@@ -34,6 +34,118 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _evict_paths(paths) -> None:
+    import nvme_strom_amd as S
+    for p in paths:
+        fd = os.open(p, os.O_RDONLY)
+        S.evict_file(fd)
+        os.close(fd)
+
+
+def snapshot_template(npages: int, per_page: int, nav_frac: float, seed: int = 1):
+    """A bulk-loaded relation's pages as a snapshot sees them: rows without
+    hint bits (nobody has read them since the load), inserted by committed,
+    aborted and still-running transactions, some deleted by committed or
+    running ones.  A fraction ``nav_frac`` of the pages is NOT all-visible
+    (the others carry PD_ALL_VISIBLE and their VM bit, rows from old
+    committed xids).  Returns (pages, VM bits, snapshot, clog)."""
+    from nvme_strom_amd.utils import pgpage
+    from nvme_strom_amd.utils.pgmvcc import (CommitLog, Snapshot, XACT_ABORTED, XACT_COMMITTED,
+                                             XACT_IN_PROGRESS)
+    rng = np.random.default_rng(seed)
+    clog = CommitLog(1 << 16, base=0)
+    for x in range(3, 1 << 16):
+        clog.set(x, XACT_COMMITTED)
+    for x in rng.choice(np.arange(2000, 60000), 3000, replace=False).tolist():
+        clog.set(x, XACT_ABORTED)
+    running = sorted(rng.choice(np.arange(50000, 60000), 40, replace=False).tolist())
+    for x in running:
+        clog.set(x, XACT_IN_PROGRESS)
+    snap = Snapshot(xmin=50000, xmax=60000, xip=running)
+    nav = np.zeros(npages, bool)
+    nav[rng.permutation(npages)[:int(round(nav_frac * npages))]] = True
+    vals = rng.integers(-5000, 5000, npages * per_page)
+    pages = []
+    for p in range(npages):
+        row = vals[p * per_page:(p + 1) * per_page].tolist()
+        if nav[p]:
+            xmin = rng.integers(1000, 62000, per_page).tolist()
+            dele = rng.random(per_page) < 0.1
+            xmax = np.where(dele, rng.integers(1000, 62000, per_page), 0).tolist()
+            masks = [0 if d else pgpage.HEAP_XMAX_INVALID for d in dele.tolist()]
+            ts = [pgpage.tuple_bytes(np.int64(v).tobytes(), infomask=m, xmin=int(x0), xmax=int(x1))
+                  for v, m, x0, x1 in zip(row, masks, xmin, xmax)]
+            pages.append(pgpage.build_page(ts, with_checksum=False))
+        else:
+            ts = [pgpage.tuple_bytes(np.int64(v).tobytes(), infomask=pgpage.HEAP_XMAX_INVALID,
+                                     xmin=int(x0)) for v, x0 in zip(row, rng.integers(3, 1000, per_page))]
+            pages.append(pgpage.build_page(ts, with_checksum=False, all_visible=True))
+    return b"".join(pages), ~nav, snap, clog
+
+
+def snapshot_rows(a, best, res, evict_paths) -> None:
+    """The snapshot rows: one relation per fraction of pages
+    that are not all-visible (0 / 25 / 100 %), scanned with a snapshot
+    through the device check (default) and through the host leg
+    (mvcc_device=False, the reference's split) in the same call, both
+    verified against cpu_scan of the template; rates are warm medians, as
+    for the plain rows, and ``of_all_visible`` divides by the 0 % row."""
+    from nvme_strom_amd.models import pg_scan
+    per_page = 150
+    tp = min(a.template_pages, 2048)
+    pred = dict(attr_off=0, attr_width=8, lo=-100, hi=2500)
+    rows = {}
+    for frac in (0.0, 0.25, 1.0):
+        t0 = time.time()
+        tmpl, av, snap, clog = snapshot_template(tp, per_page, frac)
+        reps = max(1, int(a.gib * (1 << 30)) // len(tmpl))
+        path = os.path.join(a.dir, "16390")
+        rel = pg_scan.Relation.write(path, tmpl * reps, all_visible=np.tile(av, reps))
+        one = pg_scan.Relation.write(os.path.join(a.dir, "16391"), tmpl, all_visible=av)
+        _log(f"snapshot relation nav={frac} {rel.nblocks} blocks in {time.time() - t0:.1f}s")
+        nbytes = rel.nblocks * 8192
+        base = dict(verify_checksum=False, chunk_size=best["chunk_mib"] << 20,
+                    buffer_size=8 * best["chunk_mib"] << 20, snapshot=snap, clog=clog)
+        ref = pg_scan.cpu_scan(one, pg_scan.ScanConfig(**base), **pred)
+        for mode, dev in (("device", True), ("host", False)):
+            if mode == "host" and frac == 0.0:
+                continue                  # nothing to check: the same path as the device row
+            cfg = pg_scan.ScanConfig(mvcc_device=dev, **base)
+            times = []
+            with pg_scan.HeapRelationScan(rel, cfg, "cuda", **pred) as g:
+                evict_paths(rel.segments)
+                out = g.run(best["workers"])            # cold, discarded
+                for _ in range(a.reps):
+                    evict_paths(rel.segments)
+                    t1 = time.perf_counter()
+                    out = g.run(best["workers"])
+                    times.append(time.perf_counter() - t1)
+            blk = (out.items >> np.uint64(16)).astype(np.int64)
+            ok = (len(out.items) == len(ref.items) * reps
+                  and np.array_equal(out.items[blk < tp], ref.items)
+                  and out.removed == ref.removed * reps and out.pages == rel.nblocks)
+            med = float(np.median(times))
+            row = dict(GBps=round(nbytes / med / 1e9, 2), ms=[round(t * 1e3, 1) for t in times],
+                       not_all_visible=frac, nr_checked=int(out.nr_checked),
+                       removed=int(out.removed), selected=int(len(out.items)),
+                       relation_bytes=nbytes, workers=best["workers"],
+                       chunk_mib=best["chunk_mib"], verified=bool(ok))
+            rows[f"snap_{mode}_nav{int(frac * 100)}"] = row
+            _log("snapshot", mode, frac, row)
+        for p in rel.segments + one.segments + [rel.segments[0] + "_vm", one.segments[0] + "_vm"]:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+    allvis = rows["snap_device_nav0"]["GBps"]
+    for k, r in rows.items():
+        r["of_all_visible"] = round(r["GBps"] / allvis, 3) if allvis else None
+    res["runs"].update(rows)
+    res["snapshot_nav100_of_all_visible"] = rows["snap_device_nav100"]["of_all_visible"]
+    res["snapshot_device_over_host_nav100"] = round(
+        rows["snap_device_nav100"]["GBps"] / max(rows["snap_host_nav100"]["GBps"], 1e-9), 2)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=2.0, help="relation size")
@@ -47,6 +159,10 @@ def main(argv=None) -> int:
     ap.add_argument("--dir", default="/tmp/strom_pg")
     ap.add_argument("--no-quals", dest="quals", action="store_false",
                     help="skip the qualifier-list rows (10-column relation)")
+    ap.add_argument("--no-snapshot", dest="snapshot", action="store_false",
+                    help="skip the snapshot rows (0 / 25 / 100 %% of pages not all-visible)")
+    ap.add_argument("--snapshot-only", action="store_true",
+                    help="only the snapshot rows (and the plain scan they are compared with)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     import nvme_strom_amd as S
@@ -112,10 +228,12 @@ def main(argv=None) -> int:
             best = row
     res["gpu_best_GBps"] = best["GBps"]            # best configuration's warm median
     res["gpu_best_cold_ms"] = best["cold_ms"]
+    if a.snapshot:
+        snapshot_rows(a, best, res, evict_paths=_evict_paths)
     # qualifier lists over a 10-column relation of the same size (NULLs,
     # short / long / TOASTed text before the predicated columns): every tuple
     # deformed on the GPU (strom_heap_scan2), at the best configuration above
-    if a.quals:
+    if a.quals and not a.snapshot_only:
         from nvme_strom_amd.utils import pgtuple as T
         desc, rows = T.synthetic(a.template_pages * 56, seed=4)
         tmpl2 = T.build_pages(rows, desc, with_checksum=False)

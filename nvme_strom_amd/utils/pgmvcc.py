@@ -433,3 +433,28 @@ def apply_snapshot(page: np.ndarray, snap: Snapshot, clog: Optional[CommitLog],
         c = checksum(page.tobytes(), blkno)
         page[8], page[9] = c & 0xFF, c >> 8
     return int(rc)
+
+
+def read_check_pages(fd: int, blocks: np.ndarray, stage: np.ndarray, snap: Snapshot,
+                     clog: Optional[CommitLog], relseg_blocks: int = 0,
+                     verify_checksum: bool = False, subtrans: Optional[SubTrans] = None,
+                     multi: Optional[MultiXact] = None, blcksz: int = BLCKSZ
+                     ) -> Tuple[int, np.ndarray]:
+    """The host ("buffer manager") leg for blocks checked on the CPU, native
+    (strom_pg_read_check_pages): each block is read into ``stage`` (writable
+    uint8, len(blocks) * blcksz, page i at i * blcksz), its checksum verified
+    first with ``verify_checksum``, and the tuples ``snap`` must not see
+    marked LP_UNUSED.  Returns (tuples removed, per-block recheck flags)."""
+    blocks = np.ascontiguousarray(np.asarray(blocks, dtype=np.uint32))
+    n = len(blocks)
+    if stage.dtype != np.uint8 or stage.size < n * blcksz or not stage.flags.c_contiguous:
+        raise ValueError("stage must be a contiguous uint8 array of len(blocks) pages")
+    m, keep = mvcc_struct(snap, clog, subtrans, multi)
+    flags = np.zeros(max(n, 1), dtype=np.uint8)
+    import ctypes as C
+    r = N.lib().strom_pg_read_check_pages(fd, blocks.ctypes.data if n else None, n, relseg_blocks,
+                                          blcksz, stage.ctypes.data, C.byref(m),
+                                          1 if verify_checksum else 0, flags.ctypes.data)
+    if r < 0:
+        raise OSError(-r, os.strerror(-r))
+    return int(r), flags[:n]

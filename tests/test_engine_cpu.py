@@ -512,12 +512,25 @@ def test_registered_file(strom, rand_file):
             extra = np.random.default_rng(6).integers(0, 256, 4 * 4096, dtype=np.uint8)
             with open(path, "ab") as f:
                 f.write(extra.tobytes())
+            # ... and so does the task path (it planned with the
+            # size cached at registration, -ERANGE past the old end)
+            ids = np.array([16, 18], dtype=np.uint32)
+            t = strom.memcpy_ssd2gpu(m.handle, 0, rf.fd, ids, 4096, wb_buffer=wb.ctypes.data)
+            strom.memcpy_wait(t.dma_task_id)
+            for k, c in enumerate(ids.tolist()):            # rewritten to the landing order
+                got = hbm[k * 4096:(k + 1) * 4096] if k < t.nr_ssd else wb[k * 4096:(k + 1) * 4096]
+                assert np.array_equal(got, extra[(c - 16) * 4096:(c - 15) * 4096])
             strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([17 * 4096], dtype=np.uint64))
             assert np.array_equal(hbm[:4096], extra[4096:8192])
             # shrinkage: past the new end is out of range
             os.truncate(path, 6 * 4096)
             with pytest.raises(strom.StromError) as e:
                 strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([10 * 4096], dtype=np.uint64))
+            assert e.value.errno == errno.ERANGE
+            # the task path refuses at planning time, not with a late -EIO
+            with pytest.raises(strom.StromError) as e:
+                strom.memcpy_ssd2gpu(m.handle, 0, rf.fd, np.array([8], dtype=np.uint32), 4096,
+                                     wb_buffer=wb.ctypes.data)
             assert e.value.errno == errno.ERANGE
             strom.pread_gpu_latency(m.handle, 0, rf.fd, np.array([5 * 4096], dtype=np.uint64))
             assert np.array_equal(hbm[:4096], data[5 * 4096:6 * 4096])
@@ -528,3 +541,33 @@ def test_registered_file(strom, rand_file):
             assert e.value.errno == errno.EBADF
         finally:
             os.close(fd2)
+
+
+def test_plain_descriptor_keeps_record_locks(strom, rand_file, tmp_path):
+    """a thread alternating synchronous reads over two plain
+    descriptors must not drop the process's fcntl record locks (closing ANY
+    descriptor of a file releases them): by default no dup of the caller's
+    descriptor is kept or closed.  A child process checks the lock."""
+    import fcntl
+    import subprocess
+    import sys
+    pa, _ = rand_file(8 * 4096)
+    pb, _ = rand_file(8 * 4096, seed=2, name="b.bin")
+    keep, hbm = _host_target(4096)
+    fa, fb = _open(pa), _open(pb)
+    lk = os.open(pa, os.O_RDWR)
+    probe = ("import fcntl, os, sys\nfd = os.open(sys.argv[1], os.O_RDWR)\n"
+             "try:\n    fcntl.lockf(fd, fcntl.LOCK_EX | fcntl.LOCK_NB)\n    print('got')\n"
+             "except OSError:\n    print('held')\n")
+    try:
+        fcntl.lockf(lk, fcntl.LOCK_EX)
+        with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+            for k in range(4):
+                for fd in (fa, fb, lk):
+                    strom.pread_gpu_latency(m.handle, 0, fd, np.array([k * 4096], dtype=np.uint64))
+        out = subprocess.run([sys.executable, "-c", probe, pa], capture_output=True, text=True,
+                             timeout=60).stdout.strip()
+        assert out == "held"
+    finally:
+        for fd in (fa, fb, lk):
+            os.close(fd)

@@ -384,3 +384,36 @@ def test_mvcc_native_equals_model_randomized():
         want = [pgmvcc.model_visible(a, b, m, 0, snap, clog, sub, mx) for i, a, b, m in cases]
         assert removed == sum(1 for w in want if w is False)
         assert rc == [i + 1 for i, w in enumerate(want) if w is None]
+
+
+def test_read_check_pages_native_equals_per_tuple(tmp_path):
+    """The host leg in native code (strom_pg_read_check_pages): pread of the
+    blocks (runs across a segment's modulo), checksum verified then re-stamped
+    after the edit, tuples removed and recheck flags — against the per-tuple
+    native check and the Python model."""
+    import mvccgen
+    w = mvccgen.World(seed=3, n=3000)
+    snap = w.snapshot(1)
+    data, cases = w.pages(snap, 6, per_page=120)
+    p = tmp_path / "rel"
+    p.write_bytes(data)
+    exp = w.expect(snap, cases, [True] * 6)
+    for (keep, removed, rc), cs in zip(exp, cases):      # native == model
+        for i, (a, b, m, c) in enumerate(cs):
+            mod = pgmvcc.model_visible(a % W, b % W, m, c, snap, w.clog, w.sub, w.mx)
+            assert (mod is False) == ((i + 1) not in keep)
+    blocks = np.array([4, 5, 0, 1, 2], dtype=np.uint32)   # 6 blocks per "segment": 4,5 | 0,1,2
+    stage = np.zeros(len(blocks) * 8192, np.uint8)
+    fd = os.open(p, os.O_RDONLY)
+    try:
+        removed, rc = pgmvcc.read_check_pages(fd, blocks, stage, snap, w.clog, relseg_blocks=6,
+                                              verify_checksum=True, subtrans=w.sub, multi=w.mx)
+    finally:
+        os.close(fd)
+    assert removed == sum(exp[b][1] for b in blocks)
+    assert rc.tolist() == [int(exp[b][2]) for b in blocks]
+    for j, b in enumerate(blocks.tolist()):
+        page = stage[j * 8192:(j + 1) * 8192].tobytes()
+        items, status = pgpage.host_scan(page, 8192, verify_checksum=True, blkno_base=b)
+        assert status == [0]                               # re-stamped checksum still valid
+        assert [i & 0xFFFF for i in items] == exp[b][0]
