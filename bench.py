@@ -132,6 +132,8 @@ def main() -> int:
     ap.add_argument("--fanout", choices=["allgather", "broadcast", "none"], default="allgather")
     ap.add_argument("--dir", default=os.environ.get("STROM_BENCH_DIR", "/tmp/strom_bench"))
     ap.add_argument("--keep", action="store_true", help="keep shard files")
+    ap.add_argument("--no-verify-each", dest="verify_each", action="store_false",
+                    help="N > 1: skip the per-step device CRC of every gathered slice")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process group backend (nccl = RCCL; gloo rehearses the multi-rank "
                          "path with several ranks on one GPU, collectives staged via the host)")
@@ -206,8 +208,21 @@ def main() -> int:
     fan = mode != "none"
     # the loader: window i of this rank's shard into HBM buffer i % 2 while
     # the side stream fans out window i-1 (status word + RCCL all-gather)
+    # N > 1: every step's gathered shards are delivered to a consumer on the
+    # loader's consumer stream (on_gathered, after the step's gather, while
+    # the next window loads) and every slice is CRC-checked on the device
+    # against its source rank's CRC of the window as it landed
+    # (verify_each) — inside the timed loop: the check's device time is
+    # reported (per_rank.slice_check_ms_per_rank)
+    delivered = {"steps": 0, "bytes": 0}
+
+    def consume(g):
+        delivered["steps"] += 1
+        delivered["bytes"] += g.tensor.numel()
+
     ld = ShardedLoader(path, W, dev, mode=mode, segment_sz=a.segment_mib << 20,
-                       chunk_sz=a.chunk, depth=a.depth)
+                       chunk_sz=a.chunk, depth=a.depth, out_ring=2,
+                       on_gathered=consume if fan else None, verify_each=fan and a.verify_each)
     nwin = ld.nwin
 
     # the storage's own sequential rate (below), once before the timed loop
@@ -231,6 +246,9 @@ def main() -> int:
     ld.stats = type(ld.stats)()
     ld.gather_seconds()
     ld.gather_s = 0.0
+    ld.crc_seconds()
+    ld.crc_s = 0.0
+    delivered.update(steps=0, bytes=0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -405,7 +423,9 @@ def main() -> int:
         "rccl": {"world_size": dist.get_world_size() if world > 1 else 1,
                  "backend": dist.get_backend() if world > 1 else None,
                  "collective": mode, "staged_via_host": ld.staged,
-                 "allgather_verified": gather_ok},
+                 "allgather_verified": gather_ok,
+                 "delivered_steps": delivered["steps"], "delivered_bytes": delivered["bytes"],
+                 "per_step_slice_check": bool(fan and a.verify_each)},
         "per_rank": per_rank,
         "latency_reduction": "max over ranks (worst rank)",
         "ingest_grid": ing,

@@ -356,14 +356,20 @@ struct strom_heap_scan2_args {
 	struct strom_pg_mvcc mvcc;
 	const uint8_t *mvcc_pages;            /* device, optional: per page */
 	uint32_t *mvcc_removed;               /* device, optional: u32[1] */
-	uint32_t mvcc_on, mvcc_pad;
+	uint32_t mvcc_on;
+	/* optional: bit k set when xid mvcc.xmin + k is running for the
+	 * snapshot (in xip, or in subxip unless suboverflowed), k < running_bits
+	 * = xmax - xmin: XidInMVCCSnapshot's list searches become one load */
+	uint32_t mvcc_running_bits;
+	const uint32_t *mvcc_running;
 };
 int strom_heap_scan2(const struct strom_heap_scan2_args *a, void *stream);
 /* strom_heap_scan (the fixed-offset int predicate) with the device snapshot
  * check above; m holds device pointers (NULL m: hint bits only). */
 int strom_heap_scan_mvcc(const struct strom_heap_scan_args *a, const struct strom_pg_mvcc *m,
                          const uint8_t *mvcc_pages, uint32_t *mvcc_removed,
-                         uint32_t *recheck_count, void *stream);
+                         uint32_t *recheck_count, const uint32_t *running,
+                         uint32_t running_bits, void *stream);
 /* The host ("buffer manager") path for blocks checked on the CPU: each
  * block blocks[i] is read (pread of page_sz bytes at (block % relseg_blocks)
  * * page_sz; relseg_blocks 0: no modulo) into stage + i * page_sz, a short

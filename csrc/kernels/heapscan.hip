@@ -594,6 +594,8 @@ constexpr uint32_t kXmaxKeyshrLock = 0x0010, kComboCid = 0x0020, kXmaxExclLock =
 
 struct MvccCtx {
   const strom_pg_mvcc &m;
+  const uint32_t *run;        // running-xid bitmap from m.xmin (or null)
+  uint32_t run_bits;
   bool und;
 };
 
@@ -655,9 +657,16 @@ __device__ __forceinline__ bool mv_current(MvccCtx &c, uint32_t xid) {
   return mv_normal(xid) && mv_has(c.m.curxids, c.m.ncurxids, xid);
 }
 
+__device__ __forceinline__ bool mv_running_bit(const MvccCtx &c, uint32_t xid) {
+  const uint32_t k = xid - c.m.xmin;                // xmin <= xid < xmax here
+  return (c.run[k >> 5] >> (k & 31)) & 1;
+}
+
 __device__ bool mv_in_snapshot(MvccCtx &c, uint32_t xid) {       // XidInMVCCSnapshot
   if (mv_precedes(xid, c.m.xmin)) return false;
   if (!mv_precedes(xid, c.m.xmax)) return true;
+  // the bitmap holds xip (+ subxip when not overflowed) over [xmin, xmax)
+  if (c.run && !c.m.suboverflowed && xid - c.m.xmin < c.run_bits) return mv_running_bit(c, xid);
   if (!c.m.suboverflowed) {
     if (mv_has(c.m.subxip, c.m.nsubxip, xid)) return true;
   } else {
@@ -674,6 +683,7 @@ __device__ bool mv_in_snapshot(MvccCtx &c, uint32_t xid) {       // XidInMVCCSna
     }
     xid = top;
     if (mv_precedes(xid, c.m.xmin)) return false;
+    if (c.run && xid - c.m.xmin < c.run_bits) return mv_running_bit(c, xid);
   }
   return mv_has(c.m.xip, c.m.nxip, xid);
 }
@@ -714,8 +724,9 @@ __device__ uint32_t mv_update_xid(MvccCtx &c, uint32_t multi) {
 }
 
 // the tuple at t (LDS page image), infomask already read
-__device__ int mvcc_visible(const strom_pg_mvcc &m, const uint8_t *t, uint32_t mask) {
-  MvccCtx c{m, false};
+__device__ int mvcc_visible(const strom_heap_scan2_args &g, const uint8_t *t, uint32_t mask) {
+  const strom_pg_mvcc &m = g.mvcc;
+  MvccCtx c{m, g.mvcc_running, g.mvcc_running_bits, false};
   const uint32_t xmin = lds_u32(t, 0), xmax = lds_u32(t, 4);
   // the scanning transaction's own command id; a combo cid is backend-local
   auto own_cid = [&](uint32_t &cid) {
@@ -799,7 +810,7 @@ __device__ __forceinline__ int tuple_keep(const strom_heap_scan2_args &g, const 
   }
   int und = 0;
   if (MV && check) {
-    const int v = mvcc_visible(g.mvcc, pg + off, infomask);
+    const int v = mvcc_visible(g, pg + off, infomask);
     if (v == 0) return 4;
     if (v < 0) und = 2;
   }
@@ -1062,8 +1073,9 @@ extern "C" int strom_heap_scan(const strom_heap_scan_args *a, void *stream) {
 
 // the snapshot inputs' shape (their contents are device memory): windows
 // within what the index arithmetic covers, lists present when counted
-static int mvcc_check(const strom_pg_mvcc &m) {
+static int mvcc_check(const strom_pg_mvcc &m, uint32_t running_bits = 0) {
   if ((m.nxip && !m.xip) || (m.nsubxip && !m.subxip) || (m.ncurxids && !m.curxids)) return -22;
+  if (running_bits > m.xmax - m.xmin) return -22;   // the bitmap covers [xmin, xmax) at most
   if (m.clog_n > (1ull << 32)) return -22;
   if (m.mx_n && (!m.mx_offsets || !m.mx_members)) return -22;
   return 0;
@@ -1071,18 +1083,21 @@ static int mvcc_check(const strom_pg_mvcc &m) {
 
 extern "C" int strom_heap_scan_mvcc(const strom_heap_scan_args *a, const strom_pg_mvcc *m,
                                     const uint8_t *mvcc_pages, uint32_t *mvcc_removed,
-                                    uint32_t *recheck_count, void *stream) {
+                                    uint32_t *recheck_count, const uint32_t *running,
+                                    uint32_t running_bits, void *stream) {
   if (!a) return -22;
   strom_heap_scan2_args g;
   __builtin_memset(&g, 0, sizeof g);
   g.base = *a;
   g.recheck_count = recheck_count;
   if (m) {
-    if (mvcc_check(*m)) return -22;
+    if (mvcc_check(*m, running ? running_bits : 0)) return -22;
     g.mvcc = *m;
     g.mvcc_on = 1;
     g.mvcc_pages = mvcc_pages;
     g.mvcc_removed = mvcc_removed;
+    g.mvcc_running = running;
+    g.mvcc_running_bits = running ? running_bits : 0;
   }
   return heap_scan_launch(g, 0, stream);
 }
@@ -1153,7 +1168,7 @@ extern "C" int strom_heap_prog_check(const strom_heap_tupdesc *d, const strom_he
 
 extern "C" int strom_heap_scan2(const strom_heap_scan2_args *g, void *stream) {
   if (!g || g->base.attr_off >= 0) return -22;
-  if (g->mvcc_on && mvcc_check(g->mvcc)) return -22;
+  if (g->mvcc_on && mvcc_check(g->mvcc, g->mvcc_running ? g->mvcc_running_bits : 0)) return -22;
   if (g->desc.natts < 1 || g->desc.natts > STROM_HEAP_MAX_ATTS) return -22;
   for (int i = 0; i < g->desc.natts; ++i) {
     const int al = g->desc.attalign[i], len = g->desc.attlen[i];

@@ -170,7 +170,8 @@ class HeapScan2Args(C.Structure):
                 ("quals", HeapQual * HEAP_MAX_QUALS), ("recheck_count", C.c_void_p),
                 ("prog", C.c_void_p), ("cpool", C.c_void_p), ("nprog", C.c_uint32),
                 ("cpool_len", C.c_uint32), ("mvcc", PgMvcc), ("mvcc_pages", C.c_void_p),
-                ("mvcc_removed", C.c_void_p), ("mvcc_on", C.c_uint32), ("mvcc_pad", C.c_uint32)]
+                ("mvcc_removed", C.c_void_p), ("mvcc_on", C.c_uint32),
+                ("mvcc_running_bits", C.c_uint32), ("mvcc_running", C.c_void_p)]
 
 
 class DecompDesc(C.Structure):
@@ -240,7 +241,8 @@ _SIGS = {
                                              C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
                                              C.c_void_p]),
     "strom_heap_scan_mvcc": (C.c_int, [C.POINTER(HeapScanArgs), C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_void_p, C.c_void_p]),
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.c_void_p]),
     "strom_pg_apply_snapshot": (C.c_long, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint64]),
     "strom_atomic_fetch_add_u64": (C.c_uint64, [C.c_void_p, C.c_uint64]),

@@ -39,7 +39,10 @@ class DeviceMvcc:
     sorted for the device's binary search), and the pg_xact, pg_subtrans and
     pg_multixact windows (utils.pgmvcc objects).  Uploaded once — a scan
     builds one per run and every chunk's launch reads it — and kept alive by
-    this object; ``struct`` is the strom_pg_mvcc of device pointers."""
+    this object; ``struct`` is the strom_pg_mvcc of device pointers, plus
+    the running-xid bitmap over [xmin, xmax) (``running``)."""
+
+    RUNNING_MAX_BITS = 1 << 23
 
     def __init__(self, snap, clog=None, subtrans=None, multi=None, device="cuda"):
         dev = torch.device(device)
@@ -73,6 +76,19 @@ class DeviceMvcc:
             off, mem = multi.offsets_array(), multi.members_pages()
             m.mx_offsets, m.mx_base, m.mx_n = up(off), multi.base, len(off) - 1
             m.mx_members, m.mxm_n, m.mxm_base = up(mem), len(multi.members), multi.members_base
+        # XidInMVCCSnapshot's list searches as one bit test: xip (and subxip
+        # unless the snapshot overflowed) over [xmin, xmax), up to 2^23 xids
+        span = (m.xmax - m.xmin) & 0xFFFFFFFF
+        self.running, self.running_bits = None, 0
+        if 0 < span <= self.RUNNING_MAX_BITS:
+            bm = np.zeros((span + 31) // 32, dtype=np.uint32)
+            members = [xip] if snap.suboverflowed else [xip, sub]
+            for arr in members:
+                k = (arr.astype(np.int64) - m.xmin) & 0xFFFFFFFF
+                k = k[k < span]
+                np.bitwise_or.at(bm, k >> 5, (np.uint32(1) << (k & 31).astype(np.uint32)))
+            self._run_t = torch.from_numpy(bm.view(np.uint8).copy()).to(dev)
+            self.running, self.running_bits = ptr(self._run_t), span
         if dev.type == "cuda":
             torch.cuda.current_stream(dev).synchronize()
         self.struct = m
@@ -122,7 +138,8 @@ def heap_scan(pages: torch.Tensor, page_sz: int = 8192, verify_checksum: bool = 
         mp = _mvcc_pages(mvcc_pages, npages, pages.device)
         check(lib().strom_heap_scan_mvcc(C.byref(a), C.byref(mvcc.struct),
                                          ptr(mp) if mp is not None else None, ptr(cnt) + 8,
-                                         ptr(cnt) + 4, stream_handle(stream)), "heap_scan_mvcc")
+                                         ptr(cnt) + 4, mvcc.running, mvcc.running_bits,
+                                         stream_handle(stream)), "heap_scan_mvcc")
     c = cnt.cpu().tolist()
     return HeapScanResult(items, min(c[0], cap), status[:npages], removed=c[2], recheck=c[1])
 
@@ -484,6 +501,7 @@ def heap_scan2(pages: torch.Tensor, desc, quals, page_sz: int = 8192,
         g.mvcc, g.mvcc_on = mvcc.struct, 1
         g.mvcc_pages = ptr(mp) if mp is not None else None
         g.mvcc_removed = ptr(cnt) + 8
+        g.mvcc_running, g.mvcc_running_bits = mvcc.running, mvcc.running_bits
         keep = keep + [mp, mvcc]
     check(lib().strom_heap_scan2(C.byref(g), stream_handle(stream)), "heap_scan2")
     if not sync:

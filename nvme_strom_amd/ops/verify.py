@@ -42,6 +42,21 @@ def crc32c(buf: torch.Tensor, nbytes: int | None = None, chunk: int = 1 << 16,
     return int(out.cpu().numpy().view(np.uint32)[0])
 
 
+def crc32c_into(buf: torch.Tensor, out: torch.Tensor, chunk: int = 1 << 16,
+                stream=None) -> None:
+    """CRC32C of the whole buffer written to ``out`` (a one-element device
+    int32 tensor, u32 bit pattern) on ``stream``: no host read, for checks
+    that stay on the device (parallel/fanout.py's per-step slice check)."""
+    buf = as_u8(buf)
+    n = buf.numel()
+    if n == 0:
+        out.zero_()
+        return
+    per = crc32c_chunks(buf, chunk, n, stream=stream)
+    check(lib().strom_crc32c_combine(ptr(per), per.numel(), chunk, n, ptr(out),
+                                     stream_handle(stream)), "crc32c_combine")
+
+
 def u32(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy().view(np.uint32)
 

@@ -33,7 +33,8 @@ def timed(fn, iters=5):
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=1.0)
-    ap.add_argument("--only", default="crc,scatter,verify,heap,lz4,snappy,filter")
+    ap.add_argument("--only", default="crc,scatter,verify,heap,lz4,snappy,filter",
+                    help="also: mvcc (snapshot check), par (LZ4 decoders by stream count)")
     ap.add_argument("--out", default="")
     a = ap.parse_args(argv)
     only = set(a.only.split(","))
@@ -111,6 +112,8 @@ def main(argv=None):
         log("heap_scan2_prog_cnf2", timed(lambda: heap_scan2(pages, desc, P, verify_checksum=True,
                                                              skip_invisible=True)), nb)
         del pages
+    if "mvcc" in only:
+        _mvcc_rows(n, dev, log)
     rng = np.random.default_rng(1)
     words = [b"select", b"from", b"where", b"gpu", b"hbm", b"nvme", b"strom"]
     datasets = {
@@ -180,6 +183,42 @@ def main(argv=None):
         with open(a.out, "w") as f:
             f.write(js)
     print(js)
+
+
+def _mvcc_rows(n, dev, log):
+    """The heap scan's snapshot check (heapscan.hip mvcc_visible) on
+    HBM-resident pages of a bulk-loaded relation (no hint bits; committed,
+    aborted and running inserters, 10 % deleted: tools.pg_bench
+    snapshot_template), every page checked, against the same pages with
+    the check off and with the hint-bit rule; and with a qualifier list."""
+    from nvme_strom_amd.ops.heapscan import DeviceMvcc, Program, heap_scan, heap_scan2
+    from nvme_strom_amd.tools.pg_bench import snapshot_template
+    from nvme_strom_amd.utils import pgtuple as T
+    tp = 2048
+    tmpl, _, snap, clog = snapshot_template(tp, 150, 1.0)
+    reps = max(1, min(n // len(tmpl), 0xFFFF // tp))
+    pages = torch.from_numpy(np.frombuffer(tmpl * reps, dtype=np.uint8).copy()).to(dev)
+    nb = pages.numel()
+    dm = DeviceMvcc(snap, clog, device=dev)
+    log("heap_scan_all", timed(lambda: heap_scan(pages)), nb)
+    log("heap_scan_hints", timed(lambda: heap_scan(pages, skip_invisible=True)), nb)
+    log("heap_scan_mvcc", timed(lambda: heap_scan(pages, mvcc=dm)), nb)
+    log("heap_scan_mvcc_filter", timed(lambda: heap_scan(pages, mvcc=dm, attr_off=0, attr_width=8,
+                                                         lo=-100, hi=2500)), nb)
+    desc = T.TupleDesc.of([("v", "int8")])
+    P = Program(desc, [T.Qual("v", "between", (-100, 2500))])
+    log("heap_scan2_mvcc_1qual", timed(lambda: heap_scan2(pages, desc, P, mvcc=dm)), nb)
+    r = heap_scan(pages, mvcc=dm)
+    log_counts = dict(selected=r.count, removed=r.removed, recheck=r.recheck)
+    print("mvcc counts", log_counts, file=sys.stderr, flush=True)
+    del pages
+    # a bulk-loaded relation: one inserting transaction per page (its rows'
+    # commit-log lookups hit one line), the usual shape after COPY
+    tmpl, _, snap, clog = snapshot_template(tp, 150, 1.0, seed=2, page_xid=True)
+    pages = torch.from_numpy(np.frombuffer(tmpl * reps, dtype=np.uint8).copy()).to(dev)
+    dm = DeviceMvcc(snap, clog, device=dev)
+    log("heap_scan_mvcc_page_xid", timed(lambda: heap_scan(pages, mvcc=dm)), nb)
+    del pages
 
 
 def _par_rows(D, dev, log):

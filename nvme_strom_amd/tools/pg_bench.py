@@ -42,13 +42,16 @@ def _evict_paths(paths) -> None:
         os.close(fd)
 
 
-def snapshot_template(npages: int, per_page: int, nav_frac: float, seed: int = 1):
+def snapshot_template(npages: int, per_page: int, nav_frac: float, seed: int = 1,
+                      page_xid: bool = False):
     """A bulk-loaded relation's pages as a snapshot sees them: rows without
     hint bits (nobody has read them since the load), inserted by committed,
     aborted and still-running transactions, some deleted by committed or
     running ones.  A fraction ``nav_frac`` of the pages is NOT all-visible
     (the others carry PD_ALL_VISIBLE and their VM bit, rows from old
-    committed xids).  Returns (pages, VM bits, snapshot, clog)."""
+    committed xids).  ``page_xid``: every not-all-visible page was filled
+    by one transaction (a COPY / bulk INSERT: one xmin per page) instead of
+    a random inserter per row.  Returns (pages, VM bits, snapshot, clog)."""
     from nvme_strom_amd.utils import pgpage
     from nvme_strom_amd.utils.pgmvcc import (CommitLog, Snapshot, XACT_ABORTED, XACT_COMMITTED,
                                              XACT_IN_PROGRESS)
@@ -69,7 +72,8 @@ def snapshot_template(npages: int, per_page: int, nav_frac: float, seed: int = 1
     for p in range(npages):
         row = vals[p * per_page:(p + 1) * per_page].tolist()
         if nav[p]:
-            xmin = rng.integers(1000, 62000, per_page).tolist()
+            xmin = (np.full(per_page, rng.integers(1000, 62000)) if page_xid
+                    else rng.integers(1000, 62000, per_page)).tolist()
             dele = rng.random(per_page) < 0.1
             xmax = np.where(dele, rng.integers(1000, 62000, per_page), 0).tolist()
             masks = [0 if d else pgpage.HEAP_XMAX_INVALID for d in dele.tolist()]

@@ -36,6 +36,9 @@ def test_bench_two_ranks_self_launch_gloo(tmp_path):
     assert out["verified_crc32c"] is True
     assert len(out["per_rank"]["load_GiBps_per_rank"]) == 2
     assert out["config"]["parallelism"] == "dp2+allgather"
+    # every timed step's gathered shards delivered and slice-checked
+    assert out["rccl"]["delivered_steps"] == 2 and out["rccl"]["per_step_slice_check"] is True
+    assert out["per_rank"]["delivered_steps_per_rank"] == [2, 2]
 
 
 @pytest.mark.gpu

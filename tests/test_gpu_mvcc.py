@@ -34,14 +34,21 @@ def _check(r, exp, npages):
     assert [bool(s & 8) for s in status.tolist()] == [e[2] for e in exp]
 
 
+@pytest.mark.parametrize("bitmap", [True, False], ids=["bitmap", "search"])
 @pytest.mark.parametrize("trial", range(6))
-def test_device_mvcc_equals_native_randomized(world, trial):
+def test_device_mvcc_equals_native_randomized(world, trial, bitmap, monkeypatch):
+    """Both XidInMVCCSnapshot forms on the device: the running-xid bitmap
+    over [xmin, xmax) and the sorted-list binary search (snapshots too wide
+    for a bitmap)."""
     from nvme_strom_amd.ops import heapscan as H
+    if not bitmap:
+        monkeypatch.setattr(H.DeviceMvcc, "RUNNING_MAX_BITS", 0)
     snap = world.snapshot(trial)
     npages = 12
     data, cases = world.pages(snap, npages, per_page=200, all_visible_every=5)
     pages = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
     dm = H.DeviceMvcc(snap, world.clog, world.sub, world.mx)
+    assert (dm.running is not None) == bitmap
     # PD_ALL_VISIBLE pages (0, 5, 10) are never checked
     exp = world.expect(snap, cases, [p % 5 != 0 for p in range(npages)])
     r = H.heap_scan(pages, verify_checksum=True, mvcc=dm)

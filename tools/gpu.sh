@@ -8,6 +8,8 @@
 #   zbench     zstd decoder GB/s by column kind / level / stream count (+ LZ4 rows)
 #   zprof      zstd decoder phase profile (libstrom_zstdprof.so) by column kind
 #   zpmc       two PMC passes (issue / wait / LDS / memory mix) over zstd_bench val + x
+#   lppmc      the same over the LP zstd kernels only (--modes lp), summarized (pmc_summary)
+#   mvpmc      two PMC passes over the heap scan with / without the snapshot check (kbench mvcc)
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
 #   zlibs      zstd decoder builds A/B (lib/zv/*.so, ZLIBS)
@@ -76,6 +78,25 @@ for phase in "$@"; do
               -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,x} --levels 1 --streams ${ZSTREAMS:-2048} --modes ${ZMODES:-auto} \
                  --no-lz4 --iters 1) || exit 1
           done ;;
+    lppmc) n=0 # the LP zstd decoder's kernels (walk / lit / seq / exec / serial): two PMC passes
+          for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+            n=$((n + 1))
+            (cd /tmp && step lppmc$n 120 rocprofv3 --pmc $pass --kernel-include-regex zstd_lp --output-format csv \
+              -d "$OUT/lppmc$n" -o pmc -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,ids,text} \
+                 --levels 1 --streams ${ZSTREAMS:-2048} --modes lp --no-lz4 --iters 1) || exit 1
+          done
+          step lppmcsum 60 python3 -m nvme_strom_amd.tools.pmc_summary "$OUT"/lppmc1 "$OUT"/lppmc2 \
+            --out "$OUT/lppmc_summary.json" ;;
+    mvpmc) n=0 # the heap scan's snapshot-check instance vs the plain one: two PMC passes over kbench mvcc
+          for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+            n=$((n + 1))
+            (cd /tmp && step mvpmc$n 120 rocprofv3 --pmc $pass --kernel-include-regex heap_scan --output-format csv \
+              -d "$OUT/mvpmc$n" -o pmc -- python3 -m nvme_strom_amd.tools.kbench --gib 0.5 --only mvcc) || exit 1
+          done
+          step mvpmcsum 60 python3 -m nvme_strom_amd.tools.pmc_summary "$OUT"/mvpmc1 "$OUT"/mvpmc2 \
+            --out "$OUT/mvpmc_summary.json" ;;
     zarrow) step zarrow 400 python -u -m nvme_strom_amd.tools.arrow_bench --codec zstd --out "$OUT/arrow_zstd.json" ;;
     zlibs) # same-process A/B of zstd decoder builds in nvme_strom_amd/lib/zv/ (ZLIBS=a,b ZSTREAMS=...)
           step zlibs 400 python -u -m nvme_strom_amd.tools.zstd_bench --libs ${ZLIBS:?ZLIBS} --kinds val,ids,x,text \
