@@ -615,6 +615,69 @@ int Engine::memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a) {
   return 0;
 }
 
+int Engine::memcpy_extents(int session, strom_memcpy_ssd2gpu_extents *a) {
+  a->dma_task_id = 0;
+  a->nr_dma_submit = a->nr_dma_blocks = 0;
+  a->bytes_read = a->gap_bytes = a->dst_bytes = 0;
+  if (a->nr_extents && !a->extents) return -EFAULT;
+  if (a->nr_extents > (1u << 24) || (a->flags & ~STROM_EXTENTS_PLAN_ONLY)) return -EINVAL;
+  int err = 0;
+  auto ss = stripe(a->file_desc);
+  std::shared_ptr<OpenFile> f;
+  if (!ss) {
+    if (a->file_desc >= kStripeFdBase) return -EBADF;
+    f = task_file(a->file_desc, &err);
+    if (!f) return err;
+  }
+  PlanParams pp;
+  pp.file_size = ss ? ss->size : (uint64_t)f->fc.size;
+  pp.max_request = config().max_request;
+  if (ss) {
+    pp.raid0 = &ss->geo;
+    pp.bmap = stripe_ident_bmap;
+  }
+  const bool plan_only = a->flags & STROM_EXTENTS_PLAN_ONLY;
+  std::shared_ptr<GpuMapping> gmap;
+  if (!plan_only) {
+    gmap = gpu_registry().get(a->handle);
+    if (!gmap) return -ENOENT;
+    if (int v = gpu_registry().validate(gmap)) return v;
+  }
+  ChunkPlan plan;
+  uint64_t dst_bytes = 0, read_bytes = 0;
+  int rc = plan_xfer(pp, a->extents, a->nr_extents, a->gap_max, !plan_only, &plan, &dst_bytes,
+                     &read_bytes);
+  if (rc) return rc;
+  uint64_t want = 0;
+  for (uint32_t i = 0; i < a->nr_extents; ++i) want += a->extents[i].len;
+  a->dst_bytes = dst_bytes;
+  a->bytes_read = read_bytes;
+  a->gap_bytes = read_bytes - want;
+  if (plan_only) return 0;
+  if (strom_core_check_range(gmap->map_length - gmap->map_offset, a->offset, dst_bytes))
+    return -ERANGE;
+  Task *t = tasks().create(session);
+  t->gmap = gmap;
+  const bool host_dest = gmap->device < 0;  // emulated GPU memory (CPU tests)
+  std::vector<IoReq> reqs;
+  build_requests(t, plan, f ? f->fd_direct : -1, f ? f->fd_buffered : -1, pp.file_size,
+                 gmap.get(), gmap->va + a->offset, host_dest, &reqs, ss.get());
+  const uint64_t t0 = tsc_now();
+  if (reqs.size() == 1 && (reqs[0].len <= config().inline_max || tl_sync_call))
+    io_->run_inline(reqs[0]);
+  else if (!reqs.empty())
+    io_->submit(reqs);
+  stats().nr_submit_dma.fetch_add(reqs.size(), std::memory_order_relaxed);
+  stats().clk_submit_dma.fetch_add(tsc_now() - t0, std::memory_order_relaxed);
+  t->frozen = true;
+  const uint64_t id = t->id;
+  tasks().put(t, 0);
+  a->dma_task_id = id;
+  a->nr_dma_submit = plan.nr_submit;
+  a->nr_dma_blocks = plan.nr_blocks;
+  return 0;
+}
+
 long Engine::pread_sync(unsigned long handle, size_t offset, int fd, uint64_t file_off,
                         uint64_t len, bool checked) {
   if (len > (16u << 20)) return -EAGAIN;     // big reads fan out over the workers
@@ -767,6 +830,7 @@ const char *cmd_name(unsigned long cmd) {
     case STROM_IOCTL__MEMCPY_SSD2RAM: return "strom:MEMCPY_SSD2RAM";
     case STROM_IOCTL__MEMCPY_WAIT: return "strom:MEMCPY_WAIT";
     case STROM_IOCTL__MEMCPY_WAIT_TIMED: return "strom:MEMCPY_WAIT_TIMED";
+    case STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS: return "strom:MEMCPY_SSD2GPU_EXTENTS";
     default: return "strom:ioctl";
   }
 }
@@ -814,6 +878,8 @@ int Engine::ioctl(int session, unsigned long cmd, void *arg) {
       return memcpy_ssd2gpu(session, (strom_memcpy_ssd2gpu *)arg);
     case STROM_IOCTL__MEMCPY_SSD2RAM:
       return memcpy_ssd2ram(session, (strom_memcpy_ssd2ram *)arg);
+    case STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS:
+      return memcpy_extents(session, (strom_memcpy_ssd2gpu_extents *)arg);
     case STROM_IOCTL__MEMCPY_WAIT:
       return memcpy_wait((strom_memcpy_wait *)arg);
     case STROM_IOCTL__MEMCPY_WAIT_TIMED:

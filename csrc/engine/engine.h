@@ -399,6 +399,8 @@ struct PlanParams {
 };
 
 int plan_chunks(const PlanParams &p, ChunkPlan *out);
+int plan_xfer(const PlanParams &p, strom_file_extent *x, uint32_t n, uint32_t gap_max,
+              bool planner, ChunkPlan *out, uint64_t *dst_bytes, uint64_t *read_bytes);
 
 // ------------------------------------------------------------ I/O engine
 struct IoReq {
@@ -592,6 +594,7 @@ class Engine {
  private:
   int check_file(strom_check_file *a);
   int memcpy_ssd2gpu(int session, strom_memcpy_ssd2gpu *a);
+  int memcpy_extents(int session, strom_memcpy_ssd2gpu_extents *a);
   int memcpy_ssd2ram(int session, strom_memcpy_ssd2ram *a);
   int memcpy_wait(strom_memcpy_wait *a);
   int memcpy_wait_timed(strom_memcpy_wait_timed *a);

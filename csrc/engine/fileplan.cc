@@ -322,4 +322,40 @@ int plan_chunks(const PlanParams &p, ChunkPlan *out) {
   return 0;
 }
 
+// Exact extent reads (MEMCPY_SSD2GPU_EXTENTS): the shared core lays the
+// extents out in runs and feeds them to the same merge rules; no residency
+// routing (every byte from storage, O_DIRECT being coherent with dirty
+// pages).  planner == false: layout only.
+int plan_xfer(const PlanParams &p, strom_file_extent *x, uint32_t n, uint32_t gap_max,
+              bool planner, ChunkPlan *out, uint64_t *dst_bytes, uint64_t *read_bytes) {
+  static_assert(sizeof(strom_file_extent) == sizeof(strom_xfer_extent), "extent layout");
+  static_assert(offsetof(strom_file_extent, dst_off) == offsetof(strom_xfer_extent, dst_off) &&
+                offsetof(strom_file_extent, len) == offsetof(strom_xfer_extent, len), "extent layout");
+  out->ssd.clear();
+  out->ram_fpos.clear();
+  out->ram_dest.clear();
+  out->ids_out.clear();
+  out->nr_ram = out->nr_ssd = out->nr_submit = out->nr_blocks = 0;
+  strom_planner pl;
+  memset(&pl, 0, sizeof pl);
+  pl.max_req = std::max<uint32_t>(p.max_request, 4096);
+  pl.file_contig = true;
+  pl.blkbits = 12;
+  pl.raid0 = p.bmap ? p.raid0 : nullptr;
+  pl.part_start_sect = p.bmap ? p.part_start_sect : 0;
+  pl.bmap = p.bmap ? p.bmap : ident_bmap;
+  pl.bmap_ctx = p.bmap_ctx;
+  pl.submit = plan_submit;
+  pl.submit_ctx = out;
+  strom_core_planner_init(&pl);
+  int rc = strom_core_plan_xfer(planner ? &pl : nullptr, (strom_xfer_extent *)x, n, gap_max,
+                                p.file_size, dst_bytes, read_bytes);
+  if (!rc && planner) rc = strom_core_plan_flush(&pl);
+  if (rc) return rc;
+  out->nr_submit = pl.nr_submit;
+  out->nr_blocks = (uint32_t)pl.nr_sectors;
+  out->nr_ssd = (uint32_t)out->ssd.size();
+  return 0;
+}
+
 }  // namespace strom

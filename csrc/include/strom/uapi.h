@@ -17,7 +17,7 @@
  *     scatter lists point at the GPU BAR);
  *   - the fake backend used by the CPU test-suite.
  *
- * MI355X additions use fresh request numbers (0x86, 0x93, 0x9a) so that a
+ * MI355X additions use fresh request numbers (0x86, 0x87, 0x93, 0x94, 0x9a) so that a
  * reference-era binary never reaches them by accident.
  */
 #ifndef STROM_UAPI_H
@@ -56,6 +56,7 @@ typedef uint64_t strom_u64;
 #define STROM_IOCTL__MEMCPY_WAIT_TIMED  _IO(STROM_IOC_MAGIC, 0x93)
 #define STROM_IOCTL__STAT_HIST          _IO(STROM_IOC_MAGIC, 0x9a)
 #define STROM_IOCTL__SET_ROUTE          _IO(STROM_IOC_MAGIC, 0x87)
+#define STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS _IO(STROM_IOC_MAGIC, 0x94)
 
 /* Kernel provider entry points.  /proc keeps v0.6 compatibility; /dev is
  * what the MI355X kmod registers as a misc device. */
@@ -135,6 +136,43 @@ struct strom_memcpy_ssd2gpu {
 	unsigned int  relseg_sz;     /* in:  chunks per segment file, 0 = none */
 	strom_u32 __user *chunk_ids; /* in/out: rewritten to landing order */
 	char __user  *wb_buffer;     /* in:  page-cache chunks land at its tail */
+};
+
+/* ---- MEMCPY_SSD2GPU_EXTENTS (MI355X) --------------------------------
+ * Exact reads of a list of byte ranges (an Arrow scan's column buffers)
+ * instead of fixed-size chunk ids: extents sorted by file offset and
+ * disjoint; each is widened to whole 4 KiB pages, and an extent starting
+ * within gap_max bytes of the previous one's last page is read in the same
+ * run (the hole with it).  Runs land back to back from `offset`, an extent
+ * at the same distance from its run's start as in the file: dst_off says
+ * where.  Runs split into requests of at most the provider's request size.
+ * Every byte comes from storage (O_DIRECT / NVMe READ after the range's
+ * dirty page-cache pages were written back): no reordering.  bytes_read =
+ * the extents' bytes + gap_bytes (holes and page padding).  flags
+ * STROM_EXTENTS_PLAN_ONLY: fill the outputs, read nothing (handle unused):
+ * how a caller sizes its destination. */
+#define STROM_EXTENTS_PLAN_ONLY 1u
+struct strom_file_extent {
+	strom_u64 file_off;          /* in */
+	strom_u64 dst_off;           /* out: bytes from `offset` */
+	strom_u32 len;               /* in */
+	strom_u32 reserved;
+};
+
+struct strom_memcpy_ssd2gpu_extents {
+	unsigned long dma_task_id;   /* out */
+	unsigned int  nr_dma_submit; /* out: storage requests issued */
+	unsigned int  nr_dma_blocks; /* out: 512-B sectors requested */
+	strom_u64     bytes_read;    /* out */
+	strom_u64     gap_bytes;     /* out: bytes_read - the extents' bytes */
+	strom_u64     dst_bytes;     /* out: destination span used from offset */
+	unsigned long handle;        /* in:  GPU mapping */
+	size_t        offset;        /* in:  byte offset inside the mapping */
+	int           file_desc;     /* in */
+	unsigned int  nr_extents;    /* in */
+	unsigned int  gap_max;       /* in:  bytes of hole worth reading through */
+	unsigned int  flags;         /* in:  STROM_EXTENTS_* */
+	struct strom_file_extent __user *extents;  /* in/out */
 };
 
 /* ---- MEMCPY_WAIT ---------------------------------------------------- */
@@ -283,6 +321,10 @@ STROM_ASSERT(sizeof(struct strom_stat_info) == 168, "StatInfo");
 STROM_ASSERT(offsetof(struct strom_stat_info, tsc) == 8, "Stat.tsc");
 STROM_ASSERT(offsetof(struct strom_stat_info, nr_debug1) == 104, "Stat.dbg1");
 STROM_ASSERT(sizeof(struct strom_set_route) == 2648, "SetRoute");
+STROM_ASSERT(sizeof(struct strom_file_extent) == 24, "FileExtent");
+STROM_ASSERT(sizeof(struct strom_memcpy_ssd2gpu_extents) == 80, "SsdToGpuExtents");
+STROM_ASSERT(offsetof(struct strom_memcpy_ssd2gpu_extents, handle) == 40, "S2GX.handle");
+STROM_ASSERT(offsetof(struct strom_memcpy_ssd2gpu_extents, extents) == 72, "S2GX.ext");
 STROM_ASSERT(offsetof(struct strom_set_route, zone_devs) == 344, "Route.devs");
 STROM_ASSERT(STROM_IOCTL__CHECK_FILE == 0x5380, "code");
 STROM_ASSERT(STROM_IOCTL__MEMCPY_SSD2GPU == 0x5390, "code");

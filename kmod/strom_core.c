@@ -176,6 +176,84 @@ int strom_core_plan_range(struct strom_planner *p, sc_u64 fpos, sc_u32 len, sc_u
 	return 0;
 }
 
+/* ---- exact extent reads -------------------------------------------------------------- */
+/* one run [a, b) at destination d: the pages before EOF, in planner pieces
+ * that fit plan_range's 32-bit length */
+static int xfer_run(struct strom_planner *p, sc_u64 a, sc_u64 b, sc_u64 d, sc_u64 isize,
+		    sc_u64 *read_bytes)
+{
+	const sc_u64 eof = (isize + STROM_CORE_PAGE - 1) & ~(sc_u64)(STROM_CORE_PAGE - 1);
+	const sc_u64 end = b < eof ? b : eof;
+	sc_u64 o;
+	int rc;
+
+	if (end <= a)
+		return 0;
+	*read_bytes += end - a;
+	for (o = a; p && o < end; o += 1u << 30) {
+		const sc_u64 piece = end - o < (1u << 30) ? end - o : (1u << 30);
+
+		rc = strom_core_plan_range(p, o, (sc_u32)piece, d + (o - a));
+		if (rc)
+			return rc;
+	}
+	return 0;
+}
+
+int strom_core_plan_xfer(struct strom_planner *p, struct strom_xfer_extent *x, sc_u32 n,
+			 sc_u32 gap_max, sc_u64 isize, sc_u64 *dst_bytes, sc_u64 *read_bytes)
+{
+	const sc_u64 mask = STROM_CORE_PAGE - 1;
+	sc_u64 run_a = 0, run_b = 0, run_d = 0, d = 0, prev_end = 0;
+	bool open = false;
+	sc_u32 i;
+	int rc;
+
+	*dst_bytes = *read_bytes = 0;
+	if (n && !x)
+		return -EINVAL;
+	for (i = 0; i < n; i++) {
+		const sc_u64 o = x[i].file_off, e = o + x[i].len;
+		sc_u64 a, b;
+
+		if (!x[i].len) {                     /* nothing to read */
+			x[i].dst_off = 0;
+			continue;
+		}
+		if (e < o || e > isize)
+			return -ERANGE;
+		if (o < prev_end)
+			return -EINVAL;              /* sorted and disjoint */
+		prev_end = e;
+		a = o & ~mask;
+		b = (e + mask) & ~mask;
+		if (open && a <= run_b + gap_max) {
+			if (b > run_b)
+				run_b = b;           /* sorted: a >= run_a */
+		} else {
+			if (open) {
+				rc = xfer_run(p, run_a, run_b, run_d, isize, read_bytes);
+				if (rc)
+					return rc;
+				d = run_d + (run_b - run_a);
+			}
+			run_a = a;
+			run_b = b;
+			run_d = d;
+			open = true;
+		}
+		x[i].dst_off = run_d + (o - run_a);
+	}
+	if (open) {
+		rc = xfer_run(p, run_a, run_b, run_d, isize, read_bytes);
+		if (rc)
+			return rc;
+		d = run_d + (run_b - run_a);
+	}
+	*dst_bytes = d;
+	return 0;
+}
+
 /* ---- bus addresses + PRPs ----------------------------------------------------------- */
 int strom_core_sg_lookup(struct strom_sgmap *m, sc_u64 off, sc_u64 *addr, sc_u64 *contig)
 {

@@ -145,6 +145,29 @@ void strom_core_planner_init(struct strom_planner *p);
 int strom_core_plan_range(struct strom_planner *p, sc_u64 fpos, sc_u32 len, sc_u64 dest);
 int strom_core_plan_flush(struct strom_planner *p);
 
+/* ---- exact extent reads (MEMCPY_SSD2GPU_EXTENTS) ----------------------------
+ * Layout-identical to uapi.h struct strom_file_extent (both providers assert
+ * it): the caller's (file_off, len) in, dst_off out. */
+struct strom_xfer_extent {
+	sc_u64 file_off;
+	sc_u64 dst_off;
+	sc_u32 len;
+	sc_u32 reserved;
+};
+/* n extents, sorted by file offset and disjoint, each ending at or before
+ * isize, laid out for page-granular reads: an extent is widened to whole
+ * 4 KiB pages; one whose first page starts at most gap_max bytes past the
+ * current run's last page joins that run (the hole is read too), otherwise
+ * it starts a new run.  Runs land back to back from destination 0, every
+ * extent at the same distance from its run's start as in the file
+ * (x[i].dst_off; 0 for an empty extent).  With a planner, every run goes to
+ * strom_core_plan_range (its merge rules split it into requests; the caller
+ * flushes); pages wholly past isize are not read.  *dst_bytes: destination
+ * span; *read_bytes: bytes the requests read.  0, -EINVAL (unsorted or
+ * overlapping), -ERANGE (past isize) or the planner's error. */
+int strom_core_plan_xfer(struct strom_planner *p, struct strom_xfer_extent *x, sc_u32 n,
+			 sc_u32 gap_max, sc_u64 isize, sc_u64 *dst_bytes, sc_u64 *read_bytes);
+
 /* ---- bus addresses + PRPs ---------------------------------------------------- */
 /* A dma-buf sg table flattened once at attach: segment k covers bytes
  * [start[k], start[k] + len[k]) of the buffer at bus address addr[k].

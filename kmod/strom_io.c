@@ -529,6 +529,112 @@ out_free:
 	return rc;
 }
 
+_Static_assert(sizeof(struct strom_file_extent) == sizeof(struct strom_xfer_extent) &&
+	       offsetof(struct strom_file_extent, dst_off) == offsetof(struct strom_xfer_extent, dst_off) &&
+	       offsetof(struct strom_file_extent, len) == offsetof(struct strom_xfer_extent, len),
+	       "uapi extent == core extent");
+
+/* MEMCPY_SSD2GPU_EXTENTS: exact byte ranges (an Arrow scan's buffers), laid
+ * out and merged by the shared core (strom_core_plan_xfer); every byte by
+ * NVMe READ into HBM after the span's dirty page-cache pages were written
+ * back (the chunk path's coherence rule, without a page-cache leg) */
+int strom_memcpy_ssd2gpu_extents(struct strom_session *s,
+				 struct strom_memcpy_ssd2gpu_extents __user *uarg)
+{
+	struct strom_memcpy_ssd2gpu_extents k;
+	struct strom_xfer_extent *x = NULL;
+	struct strom_gpumap *gmap = NULL;
+	struct copy_ctx c = {};
+	u64 dst_bytes = 0, read_bytes = 0, want = 0;
+	struct file *filp;
+	loff_t isize;
+	u32 i;
+	int rc;
+
+	if (copy_from_user(&k, uarg, sizeof(k)))
+		return -EFAULT;
+	if (k.nr_extents > STROM_MAX_CHUNKS || (k.flags & ~STROM_EXTENTS_PLAN_ONLY))
+		return -EINVAL;
+	rc = open_source(k.file_desc, &filp, &c.vol);
+	if (rc)
+		return rc;
+	x = kvmalloc_array(k.nr_extents ? k.nr_extents : 1, sizeof(*x), GFP_KERNEL);
+	if (!x || copy_from_user(x, k.extents, (size_t)k.nr_extents * sizeof(*x))) {
+		rc = x ? -EFAULT : -ENOMEM;
+		goto out_src;
+	}
+	isize = i_size_read(file_inode(filp));
+	/* the layout first: the destination it needs, nothing submitted */
+	rc = strom_core_plan_xfer(NULL, x, k.nr_extents, k.gap_max, isize, &dst_bytes, &read_bytes);
+	if (rc)
+		goto out_src;
+	for (i = 0; i < k.nr_extents; i++)
+		want += x[i].len;
+	k.dst_bytes = dst_bytes;
+	k.bytes_read = read_bytes;
+	k.gap_bytes = read_bytes - want;
+	k.dma_task_id = 0;
+	k.nr_dma_submit = k.nr_dma_blocks = 0;
+	if (k.flags & STROM_EXTENTS_PLAN_ONLY)
+		goto out_copy;
+	gmap = strom_gpumap_get(k.handle);
+	if (!gmap) {
+		rc = -ENOENT;
+		goto out_src;
+	}
+	rc = strom_core_check_dest(gmap->length, gmap->dmabuf_off, k.offset, dst_bytes);
+	if (!rc && read_bytes) {
+		/* the extents' span: dirty pages reach the device before it is read */
+		for (i = 0; i < k.nr_extents && !x[i].len; i++)
+			;
+		rc = filemap_write_and_wait_range(filp->f_mapping, x[i].file_off,
+						  x[k.nr_extents - 1].file_off + x[k.nr_extents - 1].len);
+	}
+	if (rc) {
+		strom_gpumap_put(gmap);
+		goto out_src;
+	}
+	c.t = strom_task_create(s, filp, gmap);   /* task owns filp + gmap refs */
+	if (!c.t) {
+		strom_gpumap_put(gmap);
+		rc = -ENOMEM;
+		goto out_src;
+	}
+	c.t->vol = c.vol;
+	c.gmap = gmap;
+	c.gpu_base = gmap->dmabuf_off + k.offset;
+	ctx_init(&c, filp);
+	rc = strom_core_plan_xfer(&c.pl, x, k.nr_extents, k.gap_max, isize, &dst_bytes, &read_bytes);
+	if (!rc)
+		rc = strom_core_plan_flush(&c.pl);
+	c.t->frozen = true;
+	k.dma_task_id = c.t->id;
+	strom_task_put(c.t, rc);
+	if (rc) {
+		long st;
+
+		strom_task_wait_session(s, k.dma_task_id, &st, MAX_SCHEDULE_TIMEOUT);
+		goto out_free;
+	}
+	k.nr_dma_submit = c.pl.nr_submit;
+	k.nr_dma_blocks = (u32)c.pl.nr_sectors;
+	goto out_copy_free;
+out_copy:
+	fput(filp);
+	strom_volume_put(c.vol);
+out_copy_free:
+	if (copy_to_user(uarg, &k, offsetof(struct strom_memcpy_ssd2gpu_extents, handle)) ||
+	    copy_to_user(k.extents, x, (size_t)k.nr_extents * sizeof(*x)))
+		rc = -EFAULT;
+	goto out_free;
+out_src:
+	fput(filp);
+	strom_volume_put(c.vol);
+out_free:
+	kvfree(x);
+	return rc;
+}
+
 int strom_memcpy_ssd2ram(struct strom_session *s, struct strom_memcpy_ssd2ram __user *uarg)
 {
 	struct strom_memcpy_ssd2ram k;

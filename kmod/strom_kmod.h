@@ -211,6 +211,8 @@ int strom_memcpy_ssd2gpu(struct strom_session *s,
 			 struct strom_memcpy_ssd2gpu __user *uarg);
 int strom_memcpy_ssd2ram(struct strom_session *s,
 			 struct strom_memcpy_ssd2ram __user *uarg);
+int strom_memcpy_ssd2gpu_extents(struct strom_session *s,
+				 struct strom_memcpy_ssd2gpu_extents __user *uarg);
 
 /* ---- DMA buffers (anon inode) -------------------------------------------- */
 int strom_alloc_dma_buffer(struct strom_alloc_dma_buffer *arg);

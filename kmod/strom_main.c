@@ -108,6 +108,8 @@ static long strom_ioctl(struct file *filp, unsigned int cmd, unsigned long arg)
 		return strom_memcpy_ssd2gpu(s, uarg);
 	case STROM_IOCTL__MEMCPY_SSD2RAM:
 		return strom_memcpy_ssd2ram(s, uarg);
+	case STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS:
+		return strom_memcpy_ssd2gpu_extents(s, uarg);
 	case STROM_IOCTL__MEMCPY_WAIT: {
 		COPY_IN(struct strom_memcpy_wait);
 		rc = strom_task_wait_session(s, karg.dma_task_id, &karg.status,

@@ -1122,7 +1122,93 @@ static int scn_concurrent_sessions(void)
 }
 
 /* ------------------------------------------------------------ driver */
+/* MEMCPY_SSD2GPU_EXTENTS on a fragmented file: every extent's bytes at its
+ * dst_off (a dirty page inside one written back first and read by DMA),
+ * bytes_read = extents + gap bytes = the sectors requested, errors for
+ * unsorted and past-EOF extents, a plan-only call reading nothing */
+static int scn_extents(void)
+{
+	struct world w;
+	struct strom_memcpy_ssd2gpu_extents a = { 0 };
+	struct strom_file_extent x[64], y[2];
+	u64 pos = 777, want = 0;
+	u32 i, n = 0, s = 99;
+	unsigned long h;
+	struct fmodel f;
+	int fd, db;
+	long st;
+	u8 *hbm;
+
+	up(&w, 9, 256);
+	f = new_file(w.fs, 8ull << 20, 17, frag_map(2048, 100, 5, 40));
+	fd = ksim_file_open(f.fi, 1);
+	db = ksim_dmabuf_new(16ull << 20, 7, 3);
+	hbm = ksim_dmabuf_mem(db);
+	h = map_dmabuf(w.dev, db, 0, 16ull << 20);
+	CHECK(h);
+	while (n < 64 && pos < (8ull << 20) - 200000) {
+		x[n].file_off = pos;
+		x[n].len = 1 + rnd(&s) % 150000;
+		x[n].dst_off = 0;
+		x[n].reserved = 0;
+		pos += x[n].len + (rnd(&s) % 3 ? rnd(&s) % 20000 : 200000 + rnd(&s) % 100000);
+		pos = (pos + 7) & ~7ull;
+		want += x[n].len;
+		n++;
+	}
+	{   /* a dirty page inside extent 3 */
+		u8 nb[64];
+		const u64 at = x[3].file_off + 10;
+
+		memset(nb, 0x3c, sizeof(nb));
+		ksim_file_write(f.fi, at, nb, sizeof(nb));
+		memcpy(f.data + at, nb, sizeof(nb));
+	}
+	a.file_desc = fd;
+	a.nr_extents = n;
+	a.gap_max = 16384;
+	a.extents = x;
+	a.flags = STROM_EXTENTS_PLAN_ONLY;
+	CHECK_EQ(ksim_ioctl(w.dev, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a), 0);
+	CHECK_EQ(a.dma_task_id, 0);
+	CHECK_EQ(a.bytes_read, want + a.gap_bytes);
+	CHECK(a.dst_bytes <= (16ull << 20) - 65536);
+	a.flags = 0;
+	a.handle = h;
+	a.offset = 65536;
+	CHECK_EQ(ksim_ioctl(w.dev, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a), 0);
+	CHECK(a.dma_task_id != 0);
+	CHECK_EQ(wait_task(w.dev, a.dma_task_id, &st), 0);
+	CHECK_EQ(st, 0);
+	CHECK_EQ((u64)a.nr_dma_blocks * 512, a.bytes_read);
+	CHECK(a.nr_dma_submit >= 1);
+	for (i = 0; i < n; i++) {
+		if (memcmp(hbm + 65536 + x[i].dst_off, f.data + x[i].file_off, x[i].len)) {
+			fprintf(stderr, "[%s] extent %u differs\n", g_scn, i);
+			g_failures++;
+			return 1;
+		}
+	}
+	CHECK_EQ(ksim_pc_get(f.fi, (x[3].file_off + 10) >> 12), 1);   /* written back */
+	/* unsorted, then past EOF */
+	y[0] = x[5];
+	y[1] = x[2];
+	a.extents = y;
+	a.nr_extents = 2;
+	CHECK_EQ(ksim_ioctl(w.dev, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a), -EINVAL);
+	y[0].file_off = (8ull << 20) - 100;
+	y[0].len = 200;
+	a.nr_extents = 1;
+	CHECK_EQ(ksim_ioctl(w.dev, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a), -ERANGE);
+	CHECK_EQ(unmap(w.dev, h), 0);
+	ksim_close(fd);
+	ksim_close(db);
+	free(f.data);
+	return down(&w);
+}
+
 static const struct { const char *name; int (*fn)(void); } scenarios[] = {
+	{ "extents", scn_extents },
 	{ "ssd2gpu_landing", scn_ssd2gpu_landing },
 	{ "relseg_eof", scn_relseg_eof },
 	{ "ssd2ram", scn_ssd2ram },

@@ -33,6 +33,7 @@ MEMCPY_SSD2GPU = _IO("S", 0x90)
 MEMCPY_SSD2RAM = _IO("S", 0x91)
 MEMCPY_WAIT = _IO("S", 0x92)
 MEMCPY_WAIT_TIMED = _IO("S", 0x93)
+MEMCPY_SSD2GPU_EXTENTS = _IO("S", 0x94)
 STAT_INFO = _IO("S", 0x99)
 STAT_HIST = _IO("S", 0x9A)
 
@@ -86,6 +87,18 @@ class MemCopySsdToGpu(C.Structure):
                 ("offset", C.c_size_t), ("file_desc", C.c_int), ("nr_chunks", C.c_uint),
                 ("chunk_sz", C.c_uint), ("relseg_sz", C.c_uint),
                 ("chunk_ids", C.POINTER(C.c_uint32)), ("wb_buffer", C.c_void_p)]
+
+
+class MemCopySsdToGpuExtents(C.Structure):
+    """strom_memcpy_ssd2gpu_extents (uapi.h): exact byte-range reads."""
+    _fields_ = [("dma_task_id", C.c_ulong), ("nr_dma_submit", C.c_uint),
+                ("nr_dma_blocks", C.c_uint), ("bytes_read", C.c_uint64),
+                ("gap_bytes", C.c_uint64), ("dst_bytes", C.c_uint64), ("handle", C.c_ulong),
+                ("offset", C.c_size_t), ("file_desc", C.c_int), ("nr_extents", C.c_uint),
+                ("gap_max", C.c_uint), ("flags", C.c_uint), ("extents", C.c_void_p)]
+
+
+EXTENTS_PLAN_ONLY = 1
 
 
 class MemCopyWait(C.Structure):

@@ -468,6 +468,59 @@ def memcpy_ssd2gpu(handle: int, offset: int, fd: int, chunk_ids: np.ndarray, chu
     return CopyResult(a.dma_task_id, a.nr_ram2gpu, a.nr_ssd2gpu, a.nr_dma_submit, a.nr_dma_blocks)
 
 
+# strom_file_extent records (uapi.h): file_off / len in, dst_off out
+EXTENT_DTYPE = np.dtype([("file_off", "<u8"), ("dst_off", "<u8"), ("len", "<u4"),
+                         ("reserved", "<u4")])
+
+
+@dataclass
+class ExtentResult:
+    dma_task_id: int
+    nr_dma_submit: int
+    nr_dma_blocks: int
+    bytes_read: int       # storage bytes the requests read
+    gap_bytes: int        # bytes_read - the extents' bytes (holes + page padding)
+    dst_bytes: int        # destination span used from the offset
+    dst_off: np.ndarray   # uint64 per extent: where it landed, from the offset
+
+    @property
+    def avg_request_bytes(self) -> float:
+        return 512.0 * self.nr_dma_blocks / self.nr_dma_submit if self.nr_dma_submit else 0.0
+
+
+def extents_array(file_off, length) -> np.ndarray:
+    """strom_file_extent records of (file offset, length) pairs."""
+    off = np.asarray(file_off, dtype=np.uint64).reshape(-1)
+    ln = np.asarray(length, dtype=np.uint64).reshape(-1)
+    if off.shape != ln.shape:
+        raise ValueError("file_off and length differ in length")
+    if len(ln) and int(ln.max()) > 0xFFFFFFFF:
+        raise ValueError("an extent longer than 4 GiB")
+    x = np.zeros(len(off), dtype=EXTENT_DTYPE)
+    x["file_off"], x["len"] = off, ln.astype(np.uint32)
+    return x
+
+
+def memcpy_ssd2gpu_extents(handle: int, offset: int, fd: int, extents: np.ndarray,
+                           gap_max: int = 64 << 10, plan_only: bool = False,
+                           sess: Optional[Session] = None) -> ExtentResult:
+    """Issue MEMCPY_SSD2GPU_EXTENTS (uapi.h): read the byte ranges of
+    ``extents`` (EXTENT_DTYPE, sorted by file offset, disjoint; its dst_off
+    column is filled in place) into the mapping at ``offset``, holes of at
+    most ``gap_max`` bytes read through.  ``plan_only``: the layout without
+    reading (``handle`` unused) — the destination size is ``dst_bytes``."""
+    if not (isinstance(extents, np.ndarray) and extents.dtype == EXTENT_DTYPE
+            and extents.flags.c_contiguous):
+        raise TypeError("extents must be a contiguous EXTENT_DTYPE array (dst_off written in place)")
+    a = N.MemCopySsdToGpuExtents(handle=handle, offset=offset, file_desc=fd,
+                                 nr_extents=len(extents), gap_max=int(gap_max),
+                                 flags=N.EXTENTS_PLAN_ONLY if plan_only else 0,
+                                 extents=extents.ctypes.data if len(extents) else None)
+    (sess or session()).ioctl(N.MEMCPY_SSD2GPU_EXTENTS, a, "MEMCPY_SSD2GPU_EXTENTS")
+    return ExtentResult(a.dma_task_id, a.nr_dma_submit, a.nr_dma_blocks, a.bytes_read,
+                        a.gap_bytes, a.dst_bytes, extents["dst_off"])
+
+
 def memcpy_ssd2ram(dest_addr: int, fd: int, chunk_ids, chunk_sz: int, relseg_sz: int = 0,
                    sess: Optional[Session] = None) -> CopyResult:
     ids = _ids_array(chunk_ids)

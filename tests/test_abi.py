@@ -14,6 +14,8 @@ EXPECTED_SIZES = {
     N.CheckFile: 12, N.MapGpuMemory: 32, N.UnmapGpuMemory: 8, N.ListGpuMemory: 16,
     N.InfoGpuMemory: 56, N.MemCopySsdToGpu: 72, N.MemCopyWait: 16, N.MemCopySsdToRam: 56,
     N.AllocDMABuffer: 16, N.StatInfo: 168,
+    # MI355X extension (uapi.h static assertions pin the C side)
+    N.MemCopySsdToGpuExtents: 80,
 }
 
 EXPECTED_OFFSETS = [
@@ -25,7 +27,15 @@ EXPECTED_OFFSETS = [
     (N.MemCopySsdToGpu, "wb_buffer", 64),
     (N.MemCopySsdToRam, "dest_uaddr", 24), (N.MemCopySsdToRam, "chunk_ids", 48),
     (N.StatInfo, "tsc", 8), (N.StatInfo, "nr_debug1", 104),
+    (N.MemCopySsdToGpuExtents, "handle", 40), (N.MemCopySsdToGpuExtents, "extents", 72),
 ]
+
+
+def test_extent_record_layout():
+    from nvme_strom_amd.api import EXTENT_DTYPE
+    assert EXTENT_DTYPE.itemsize == 24
+    assert [EXTENT_DTYPE.fields[k][1] for k in ("file_off", "dst_off", "len")] == [0, 8, 16]
+    assert N.MEMCPY_SSD2GPU_EXTENTS == 0x5394
 
 
 @pytest.mark.parametrize("cls,size", list(EXPECTED_SIZES.items()), ids=lambda x: getattr(x, "__name__", str(x)))
