@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import math
 import struct
 from dataclasses import dataclass
 from typing import Optional
@@ -183,12 +184,14 @@ def qual_structs(desc, quals) -> list:
                 s.hi = struct.unpack("<q", struct.pack("<d", float(args[1])))[0]
             elif kind == "int":
                 s.kind = 1
-                # exact: a fractional lower bound rounds up, an upper one down
-                s.lo, s.hi = math.ceil(_exact(args[0])), math.floor(_exact(args[1]))
+                # exact: a fractional lower bound rounds up, an upper one
+                # down; non-finite bounds clamp (an empty range: lo > hi)
+                b = _int_bounds("between", args, -(1 << 63), (1 << 63) - 1)
+                s.lo, s.hi = b if b is not None else (1, 0)
             else:
                 raise ValueError(f"range qual on a {desc.types[k]} column")
         elif op == "in":
-            vals = [int(v) for v in args[0] if _exact(v) == int(_exact(v))]
+            vals = [int(v) for v in args[0] if _is_int_value(v)]
             if kind != "int" or len(vals) > 4:
                 raise ValueError("IN lists take up to 4 values of an int column")
             s.kind, s.nconst = 7, len(vals)
@@ -320,37 +323,19 @@ class Program:
                 elif kind == "int" and L in _INT_LIMITS:
                     tmin, tmax = _INT_LIMITS[L]
                     if op == "in":
-                        vals = sorted({int(c) for c in args[0]
-                                       if _exact(c) == int(_exact(c)) and tmin <= int(c) <= tmax})
+                        vals = sorted({int(c) for c in args[0] if _is_int_value(c)
+                                       and tmin <= int(c) <= tmax})
                         if not vals:
                             never(k, ci)
                             continue
                         emit(k, 7, ci, nconst=len(vals),
                              coff=const(struct.pack(f"<{len(vals)}q", *vals)))
                         continue
-                    # exact bounds on the integers: a fractional lower bound
-                    # rounds up, an upper one down; clamped to the type
-                    lo, hi = tmin, tmax
-                    d = _exact
-                    if op == "between":
-                        lo, hi = math.ceil(d(args[0])), math.floor(d(args[1]))
-                    elif op == "eq":
-                        lo, hi = math.ceil(d(args[0])), math.floor(d(args[0]))
-                    elif op == "le":
-                        hi = math.floor(d(args[0]))
-                    elif op == "lt":
-                        hi = math.ceil(d(args[0])) - 1
-                    elif op == "ge":
-                        lo = math.ceil(d(args[0]))
-                    elif op == "gt":
-                        lo = math.floor(d(args[0])) + 1
-                    else:
-                        raise ValueError(f"{op} on an int column")
-                    lo, hi = max(lo, tmin), min(hi, tmax)
-                    if lo > hi:
+                    b = _int_bounds(op, args, tmin, tmax)
+                    if b is None:
                         never(k, ci)
                     else:
-                        emit(k, 1, ci, lo=lo, hi=hi)
+                        emit(k, 1, ci, lo=b[0], hi=b[1])
                 else:
                     raise ValueError(f"{op} on a {desc.types[k]} column")
         # clauses by their first attribute, quals by attribute inside a
@@ -419,6 +404,51 @@ class Program:
         if self._arrays is None:
             self._arrays = (b"".join(bytes(q) for q in self.quals), bytes(self.pool))
         return self._arrays
+
+
+def _is_int_value(c) -> bool:
+    """A constant equal to some integer (NaN and the infinities are not)."""
+    d = _exact(c)
+    return d.is_finite() and d == int(d)
+
+
+def _int_bounds(op: str, args, tmin: int, tmax: int):
+    """Exact [lo, hi] of an int qualifier on a column of range [tmin, tmax]
+    (a fractional lower bound rounds up, an upper one down; clamped to the
+    type), or None when nothing qualifies.  Non-finite constants compare as
+    PostgreSQL / IEEE do: -inf below and +inf above every integer, NaN
+    (equal to nothing, ordered by nothing here) never true."""
+    from decimal import Decimal
+    d = [_exact(a) for a in args]
+    if any(x.is_nan() for x in d):
+        return None
+
+    def lo_of(x: Decimal, strict: bool) -> int:
+        if x.is_infinite():
+            return tmin if x < 0 else tmax + 1
+        return math.floor(x) + 1 if strict else math.ceil(x)
+
+    def hi_of(x: Decimal, strict: bool) -> int:
+        if x.is_infinite():
+            return tmin - 1 if x < 0 else tmax
+        return math.ceil(x) - 1 if strict else math.floor(x)
+    lo, hi = tmin, tmax
+    if op == "between":
+        lo, hi = lo_of(d[0], False), hi_of(d[1], False)
+    elif op == "eq":
+        lo, hi = lo_of(d[0], False), hi_of(d[0], False)
+    elif op == "le":
+        hi = hi_of(d[0], False)
+    elif op == "lt":
+        hi = hi_of(d[0], True)
+    elif op == "ge":
+        lo = lo_of(d[0], False)
+    elif op == "gt":
+        lo = lo_of(d[0], True)
+    else:
+        raise ValueError(f"{op} on an int column")
+    lo, hi = max(lo, tmin), min(hi, tmax)
+    return None if lo > hi else (lo, hi)
 
 
 def _exact(x):

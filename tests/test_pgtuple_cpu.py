@@ -268,3 +268,36 @@ def test_program_fixed_form():
                [T.Qual("x", "in", (list(range(5)),))],
                [T.Qual("x", "ge", (i,)) for i in range(N.HEAP_MAX_QUALS + 1)]):
         assert H.Program(desc, qs).fixed() is None, qs
+
+
+def test_program_non_finite_int_constants():
+    """inf / -inf / NaN constants against an int column compile
+    to the range they mean (the type's limits, or a constant-false qual)
+    instead of raising; IN lists drop them.  The host twin agrees."""
+    from nvme_strom_amd.ops.heapscan import QUAL2_FALSE, Program
+    from nvme_strom_amd.utils import pgtuple as T
+    desc = T.TupleDesc.of([("a", "int4")])
+    inf, nan = float("inf"), float("nan")
+    lim = (-(1 << 31), (1 << 31) - 1)
+
+    def one(q):
+        p = Program(desc, [q])
+        assert len(p.quals) == 1
+        x = p.quals[0]
+        return None if x.flags & QUAL2_FALSE else (x.kind, x.lo, x.hi, x.nconst)
+    assert one(T.Qual("a", "lt", (inf,))) == (1, lim[0], lim[1], 0)
+    assert one(T.Qual("a", "le", (-inf,))) is None
+    assert one(T.Qual("a", "gt", (-inf,))) == (1, lim[0], lim[1], 0)
+    assert one(T.Qual("a", "ge", (inf,))) is None
+    assert one(T.Qual("a", "between", (-inf, 5.5))) == (1, lim[0], 5, 0)
+    assert one(T.Qual("a", "between", (nan, 5))) is None
+    assert one(T.Qual("a", "eq", (nan,))) is None
+    assert one(T.Qual("a", "eq", (inf,))) is None
+    assert one(T.Qual("a", "in", ([nan, inf, 3, 4.0, 4.5],))) == (7, 0, 0, 2)
+    # the host evaluation of the same quals over a few values
+    rows = [(v,) for v in (lim[0], -7, 0, 5, lim[1])]
+    data = T.build_pages(rows, desc)
+    for q, want in ((T.Qual("a", "lt", (inf,)), 5), (T.Qual("a", "le", (-inf,)), 0),
+                    (T.Qual("a", "between", (-inf, 5.5)), 4), (T.Qual("a", "eq", (nan,)), 0)):
+        items, _, _ = T.host_scan2(data, desc, [q])
+        assert len(items) == want, (q, items)
