@@ -473,7 +473,7 @@ struct IoEngine::Worker {
     const size_t small = std::min<size_t>((size_t)cfg.queue_depth * 4, budget / cfg.max_request);
     const size_t by_bytes = std::min<size_t>(cfg.staging_bytes / cfg.max_request, 256);
     return (int)std::min<size_t>(256, std::max<size_t>({(size_t)cfg.staging_slots, small, by_bytes,
-                                                        (size_t)cfg.queue_depth}));
+                                                        cfg.stage_by_bytes ? (size_t)cfg.queue_depth : 0}));
   }
   // the staging bytes requests may hold at once: the slots' bytes up to the
   // default budget (staging_slots x 1 MiB), or the staging_bytes opt-in
@@ -770,7 +770,7 @@ struct IoEngine::Worker {
       }
       if (free_slots.empty()) return false;
       // the byte budget (a request alone may always start)
-      if (stage_inflight && stage_inflight + r.len > stage_budget()) return false;
+      if (cfg.stage_by_bytes && stage_inflight && stage_inflight + r.len > stage_budget()) return false;
       if (cfg.coalesce) {
         slot = free_slots.front();
         free_slots.pop_front();

@@ -103,6 +103,13 @@ constexpr uint32_t kCkNone = 0xffu;      // checkpoint: no sequence starts in th
 #define LZ4PAR_HOPS 3
 #endif
 constexpr uint32_t HOPS = LZ4PAR_HOPS;
+// The count's prefix over the slices: a wave shuffle scan plus the waves'
+// totals (2 barriers) instead of log2(NT) Hillis-Steele steps (2 each)
+#ifndef LZ4PAR_WSCAN
+#define LZ4PAR_WSCAN 1
+#endif
+constexpr bool WSCAN = LZ4PAR_WSCAN;
+static_assert(LZ4PAR_NT % 64 == 0, "whole waves");
 static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
@@ -1394,16 +1401,38 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           __syncthreads();
           ph_count<SN>(s, c, t, ent);
         }
-        for (uint32_t dd = 1; dd < NT; dd <<= 1) {
+        if (WSCAN) {
+          // inclusive scan of the slices' output bytes: in the wave by
+          // shuffles, then the earlier waves' totals through the pointer
+          // batch (free from the end of validation to the fill) — two
+          // barriers instead of two per Hillis-Steele step
+          const uint32_t lane = t & 63, wave = t >> 6;
+          uint32_t x = s.ost[t];
+#pragma unroll
+          for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
+          }
+          if (lane == 63) s.ptr[wave] = x;
+          __syncthreads();                 // the totals and every count's s.err
+          for (uint32_t v = 0; v < wave; ++v) x += s.ptr[v];
+          s.ost[t] = x;
+          if (t == NT - 1) {
+            s.total = x;
+            if (!s.err && (uint64_t)s.op + x > c.cap) s.err = kErrOverflow;
+          }
+        } else {
+          for (uint32_t dd = 1; dd < NT; dd <<= 1) {
+            __syncthreads();
+            const uint32_t v = ph_scan_read(s, t, dd);
+            __syncthreads();
+            ph_scan_write(s, t, v);
+          }
           __syncthreads();
-          const uint32_t v = ph_scan_read(s, t, dd);
-          __syncthreads();
-          ph_scan_write(s, t, v);
-        }
-        __syncthreads();
-        if (t == 0) {
-          s.total = s.ost[NT - 1];
-          if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
+          if (t == 0) {
+            s.total = s.ost[NT - 1];
+            if (!s.err && (uint64_t)s.op + s.total > c.cap) s.err = kErrOverflow;
+          }
         }
         __syncthreads();
         LP_MARK(kLpScan);
@@ -1427,7 +1456,9 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           LP_MARK(kLpDouble);
           Held h;
           ph_resolve(s, c, t, b0, nb, h);
-          __syncthreads();
+          // the write changes only what the resolve does not read (HBM
+          // past the batch start, the head bitmaps) unless there is a ring
+          if (HR) __syncthreads();
           LP_MARK(kLpResolve);
           ph_write(s, c, t, b0, nb, h);
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
