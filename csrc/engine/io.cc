@@ -32,6 +32,7 @@
 #include <x86intrin.h>
 
 #include <algorithm>
+#include <functional>
 #include <fstream>
 
 #include "engine.h"
@@ -1179,14 +1180,17 @@ extern "C" int strom_io_info(uint64_t *out) {
 // engine streams a window in).  The sweep prints it next to the engine's
 // SSD→HBM numbers.  `mode` bit 0: sequential; bit 1: buffered reads (the
 // page-cache ceiling the engine-only sweep compares against).
-extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
-                                   uint32_t qd, int mode, double *iops, double *gibps) {
-  const bool sequential = mode & 1;
-  // mode & 4: the reads land in 2 MiB-page memory registered with the ring
-  // (READ_FIXED), as the engine's pinned staging does — no per-read
-  // get_user_pages of 256 small pages per MiB in the comparator either
-  const bool fixed = (mode & 4) != 0;
+namespace {
+// One ring per thread kept `qd` deep with O_DIRECT (or buffered, mode bit 1)
+// reads into host memory (2 MiB pages registered with the ring for
+// READ_FIXED with mode bit 2); next(tid, k, &off, &len) names thread tid's
+// k-th read (false: the thread is done).  Returns the first error; *bytes
+// the bytes read, *sec the wall time.
+int raw_reads(int fd, int mode, uint32_t threads, uint32_t qd, uint64_t slot,
+              const std::function<bool(uint32_t, uint32_t, uint64_t *, uint32_t *)> &next,
+              uint64_t *bytes_out, double *sec_out) {
   using namespace strom;
+  const bool fixed = (mode & 4) != 0;
   // rings on the CPUs the engine's workers use (config numa_bind: the
   // current GPU's NUMA node), so the comparison is like for like
   int node = -1;
@@ -1195,30 +1199,18 @@ extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32
     (void)hipGetDevice(&dev);
     node = hip::numa_node_of_device(dev);
   }
-  if (block == 0 || (block & 4095) || nreq == 0 || threads == 0 || qd == 0 || qd > 256)
-    return -EINVAL;
-  struct stat st;
-  if (fstat(fd, &st) != 0) return -errno;
-  const uint64_t nblk = (uint64_t)st.st_size / block;
-  if (nblk == 0) return -ERANGE;
   char path[64];
   snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
   int d = open(path, O_RDONLY | ((mode & 2) ? 0 : O_DIRECT) | O_CLOEXEC);
   if (d < 0) return -errno;
   std::atomic<int> err{0};
-  // Every ring owns its share of the requests and, sequential, a disjoint
-  // run of the file read in order — as the engine's workers read theirs.
-  // No cursor is shared between rings: a common atomic cursor costs a
-  // contended cache line per request and interleaves the rings' reads,
-  // which made this "ceiling" slower than the engine at 4-16 KiB
-  // (VERDICT r4 weak #5).
-  const uint64_t run = std::max<uint64_t>(1, nblk / threads);
+  std::atomic<uint64_t> total{0};
   auto body = [&](uint32_t tid) {
     bind_to_node(node);
     Uring ring;
     int rc = ring.init(qd);
     void *buf = nullptr;
-    const size_t bytes = (size_t)block * qd, huge = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    const size_t bytes = (size_t)slot * qd, huge = (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
     bool mapped = false, reg = false;
     if (rc == 0 && fixed) {
       // 2 MiB aligned inside a larger anonymous map, huge pages advised
@@ -1235,27 +1227,28 @@ extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32
         reg = ring.register_buffer(buf, bytes) == 0;
       }
     }
-    if (rc == 0 && !buf && posix_memalign(&buf, 4096, block * qd) != 0) rc = -ENOMEM;
-    uint64_t x = 0x9e3779b97f4a7c15ull * (tid + 1);
-    const uint32_t mine = nreq / threads + (tid < nreq % threads ? 1 : 0);
-    const uint64_t base = (uint64_t)tid * run;
+    if (rc == 0 && !buf && posix_memalign(&buf, 4096, bytes) != 0) rc = -ENOMEM;
     uint32_t inflight = 0, k = 0;
+    uint64_t got_bytes = 0;
+    bool more = true;
     std::vector<uint32_t> freeslot;
     for (uint32_t s = 0; s < qd; ++s) freeslot.push_back(s);
     bool init_ok = rc == 0;
     while (init_ok) {
-      while (rc == 0 && !freeslot.empty() && k < mine) {
-        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      while (rc == 0 && more && !freeslot.empty()) {
+        uint64_t off = 0;
+        uint32_t len = 0;
+        if (!(more = next(tid, k, &off, &len))) break;
+        ++k;
         uint32_t s = freeslot.back();
         freeslot.pop_back();
         io_uring_sqe *q = ring.next_sqe();
         q->opcode = reg ? IORING_OP_READ_FIXED : IORING_OP_READ;
         q->buf_index = 0;
         q->fd = d;
-        q->addr = (uint64_t)buf + (uint64_t)s * block;
-        q->len = (uint32_t)block;
-        q->off = (sequential ? (base + k % run) % nblk : x % nblk) * block;
-        ++k;
+        q->addr = (uint64_t)buf + (uint64_t)s * slot;
+        q->len = len;
+        q->off = off;
         q->user_data = s;
         ++inflight;
       }
@@ -1268,26 +1261,27 @@ extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32
       if (r < 0 && r != -EINTR && rc == 0) rc = r;
       io_uring_cqe c;
       uint32_t got = 0;
-      for (uint64_t t0 = mono_ns(); !got && mono_ns() - t0 < 20000;) {
+      auto reap = [&] {
         while (ring.peek(&c)) {
           if (c.res < 0 && rc == 0) rc = c.res;
+          if (c.res > 0) got_bytes += (uint64_t)c.res;
           freeslot.push_back((uint32_t)c.user_data);
           --inflight;
           ++got;
         }
+      };
+      for (uint64_t t0 = mono_ns(); !got && mono_ns() - t0 < 20000;) {
+        reap();
         if (!got) _mm_pause();
       }
       if (!got) {
         r = ring.enter(1);  // in-flight reads drain even after an error
         if (r < 0 && r != -EINTR && rc == 0) rc = r;
-        while (ring.peek(&c)) {
-          if (c.res < 0 && rc == 0) rc = c.res;
-          freeslot.push_back((uint32_t)c.user_data);
-          --inflight;
-        }
+        reap();
       }
     }
     if (rc) err.store(rc);
+    total.fetch_add(got_bytes);
     if (reg) ring.unregister_buffers();
     if (mapped) munmap(buf, huge);
     else free(buf);
@@ -1296,10 +1290,85 @@ extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32
   std::vector<std::thread> th;
   for (uint32_t t = 0; t < threads; ++t) th.emplace_back(body, t);
   for (auto &t : th) t.join();
-  const double sec = (mono_ns() - t0) * 1e-9;
+  *sec_out = (mono_ns() - t0) * 1e-9;
+  *bytes_out = total.load();
   close(d);
-  if (err.load()) return err.load();
+  return err.load();
+}
+}  // namespace
+
+// The device's own limit for a block size, with no engine in the way:
+// `threads` threads, each with its own io_uring kept `qd` deep with O_DIRECT
+// reads of `block` bytes at random aligned offsets into host memory (or,
+// with `sequential`, the next block of a shared cursor: the order the
+// engine streams a window in).  The sweep prints it next to the engine's
+// SSD→HBM numbers.  `mode` bit 0: sequential; bit 1: buffered reads (the
+// page-cache ceiling the engine-only sweep compares against); bit 2: reads
+// into 2 MiB-page memory registered with the ring (READ_FIXED), as the
+// engine's pinned staging does.
+extern "C" int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads,
+                                   uint32_t qd, int mode, double *iops, double *gibps) {
+  const bool sequential = mode & 1;
+  if (block == 0 || (block & 4095) || block > (1ull << 30) || nreq == 0 || threads == 0 || qd == 0 ||
+      qd > 256)
+    return -EINVAL;
+  struct stat st;
+  if (fstat(fd, &st) != 0) return -errno;
+  const uint64_t nblk = (uint64_t)st.st_size / block;
+  if (nblk == 0) return -ERANGE;
+  // Every ring owns its share of the requests and, sequential, a disjoint
+  // run of the file read in order — as the engine's workers read theirs.
+  // No cursor is shared between rings: a common atomic cursor costs a
+  // contended cache line per request and interleaves the rings' reads,
+  // which made this "ceiling" slower than the engine at 4-16 KiB
+  // (VERDICT r4 weak #5).
+  const uint64_t run = std::max<uint64_t>(1, nblk / threads);
+  std::vector<uint64_t> x(threads);
+  for (uint32_t t = 0; t < threads; ++t) x[t] = 0x9e3779b97f4a7c15ull * (t + 1);
+  auto next = [&](uint32_t tid, uint32_t k, uint64_t *off, uint32_t *len) {
+    const uint32_t mine = nreq / threads + (tid < nreq % threads ? 1 : 0);
+    if (k >= mine) return false;
+    uint64_t &r = x[tid];
+    r ^= r << 13, r ^= r >> 7, r ^= r << 17;
+    *off = (sequential ? ((uint64_t)tid * run + k % run) % nblk : r % nblk) * block;
+    *len = (uint32_t)block;
+    return true;
+  };
+  uint64_t bytes = 0;
+  double sec = 0;
+  const int rc = raw_reads(fd, mode, threads, qd, block, next, &bytes, &sec);
+  if (rc) return rc;
   if (iops) *iops = nreq / sec;
   if (gibps) *gibps = (double)nreq * block / sec / (1 << 30);
+  return 0;
+}
+
+// The same rings reading exactly the requests (off[i], len[i]) — 4 KiB
+// aligned, in order, thread t taking the t-th contiguous share of the list:
+// the storage's own rate for an access pattern an engine call produced
+// (the Arrow read probe's comparator for a column's extent requests).
+extern "C" int strom_raw_read_list(int fd, const uint64_t *off, const uint32_t *len, uint32_t n,
+                                   uint32_t threads, uint32_t qd, int mode, double *iops,
+                                   double *gibps) {
+  if (!off || !len || n == 0 || threads == 0 || qd == 0 || qd > 256) return -EINVAL;
+  uint32_t slot = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if ((off[i] & 4095) || len[i] == 0 || (len[i] & 4095) || len[i] > (64u << 20)) return -EINVAL;
+    slot = std::max(slot, len[i]);
+  }
+  threads = std::min(threads, n);
+  auto next = [&](uint32_t tid, uint32_t k, uint64_t *o, uint32_t *l) {
+    const uint64_t lo = (uint64_t)n * tid / threads, hi = (uint64_t)n * (tid + 1) / threads;
+    if (lo + k >= hi) return false;
+    *o = off[lo + k];
+    *l = len[lo + k];
+    return true;
+  };
+  uint64_t bytes = 0;                           // a read at the end may come back short
+  double sec = 0;
+  const int rc = raw_reads(fd, mode & ~1, threads, qd, slot, next, &bytes, &sec);
+  if (rc) return rc;
+  if (iops) *iops = n / sec;
+  if (gibps) *gibps = (double)bytes / sec / (1 << 30);
   return 0;
 }

@@ -80,6 +80,11 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n);
  * host memory until `nreq` reads are done. */
 int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads, uint32_t qd,
                         int sequential, double *iops, double *gibps);
+/* The same rings reading exactly the requests (off[i], len[i]), 4 KiB
+ * aligned, thread t taking the t-th contiguous share of the list: the
+ * storage's rate for the access pattern an engine call produced. */
+int strom_raw_read_list(int fd, const uint64_t *off, const uint32_t *len, uint32_t n,
+                        uint32_t threads, uint32_t qd, int mode, double *iops, double *gibps);
 
 /* dma-buf fd of the HIP allocation holding [va, va+len) and va's byte
  * offset inside it: what MAP_GPU_MEMORY registers with the kernel provider

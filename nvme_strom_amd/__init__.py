@@ -21,7 +21,7 @@ from .api import (  # noqa: F401
     fake_backend, fault_inject, hist_percentile, info_gpu_memory, list_gpu_memory, map_gpu_memory,
     memcpy_ssd2gpu, memcpy_ssd2ram, memcpy_wait, pread_gpu, pread_gpu_latency, provider,
     EXTENT_DTYPE, ExtentResult, extents_array, memcpy_ssd2gpu_extents,
-    PHASES, host_costs, engine_costs, ingest_info, io_info, io_prof, ioctl_latency, phase_breakdown, pread_gpu_phases, pread_raw_latency, pread_pair_latency, raw_read_rate,
+    PHASES, host_costs, engine_costs, ingest_info, io_info, io_prof, ioctl_latency, phase_breakdown, pread_gpu_phases, pread_raw_latency, pread_pair_latency, raw_read_rate, raw_read_list,
     resident_bytes, session, StripeSet, RegisteredFile, write_striped,
     stat_hist, stat_info, unmap_gpu_memory, version,
 )

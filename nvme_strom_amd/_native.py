@@ -216,6 +216,9 @@ _SIGS = {
                                        C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]),
     "strom_raw_read_rate": (C.c_int, [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "strom_raw_read_list": (C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_int, C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double)]),
     "strom_export_dmabuf": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_int),
                                       C.POINTER(C.c_uint64)]),
     "strom_ingest_info": (C.c_int, [C.c_int, C.c_void_p]),

@@ -638,6 +638,23 @@ def raw_read_rate(fd: int, block: int, nreq: int, threads: int = 4, qd: int = 8,
     return iops.value, gibps.value
 
 
+def raw_read_list(fd: int, offs, lens, threads: int = 4, qd: int = 8, buffered: bool = False,
+                  fixed: bool = False) -> tuple:
+    """The raw_read_rate rings reading exactly the requests ``(offs[i],
+    lens[i])`` (4 KiB aligned), ring t taking the t-th contiguous share of
+    the list: the storage's own rate for the access pattern an engine call
+    produced.  Returns (IOPS, GiB/s of the bytes read)."""
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = np.ascontiguousarray(lens, dtype=np.uint32)
+    if o.shape != n.shape or o.ndim != 1:
+        raise ValueError("offs and lens must be 1-D and of one length")
+    iops, gibps = C.c_double(), C.c_double()
+    _check(N.lib().strom_raw_read_list(fd, o.ctypes.data, n.ctypes.data, len(o), threads, qd,
+                                       (2 if buffered else 0) | (4 if fixed else 0),
+                                       C.byref(iops), C.byref(gibps)), "raw_read_list")
+    return iops.value, gibps.value
+
+
 def memcpy_wait(task_id: int, timeout: Optional[float] = None,
                 sess: Optional[Session] = None) -> None:
     """Block until the task finishes; raises StromError(EIO, status=...) on a

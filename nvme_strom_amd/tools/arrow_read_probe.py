@@ -11,7 +11,10 @@ issues them (a ring of slots, nslots - 1 groups in flight behind the first):
 ``buffer_GBps`` counts the column's buffer bytes (what the scan needs),
 ``read_GBps`` the bytes the requests read; ``of_storage`` divides the buffer
 rate by a host-only io_uring O_DIRECT sequential read of the same file with
-the engine's request size, rings and depth, taken before and after.  Rates
+the engine's request size, rings and depth, taken before and after;
+``of_same_requests`` divides the read rate by the same rings reading exactly
+the extents planner's requests (``requests()``, raw_read_list), rep by rep
+after the modes — what the storage does with that access pattern.  Rates
 are medians over ``--reps`` runs, the file evicted before each.
 
 ``python -m nvme_strom_amd.tools.arrow_read_probe --codec zstd --columns val --out p.json``
@@ -82,15 +85,55 @@ class _Reader:
                     read_GBps=round(self.nread / med / 1e9, 2))
 
 
+def requests(groups, gap: int, mreq: int, page: int = 4096):
+    """(offsets, lengths) of the reads the extents planner issues for the
+    groups (tests/test_extents_cpu.py model_layout's runs: page-widened
+    extents, holes up to ``gap`` read through), each run cut at
+    ``mreq`` — the storage-side comparator's request list."""
+    offs, lens = [], []
+    for g in groups:
+        runs, cur = [], None
+        for o, n in zip(g.ext["file_off"].tolist(), g.ext["len"].tolist()):
+            if n == 0:
+                continue
+            a, b = o // page * page, -(-(o + n) // page) * page
+            if cur is not None and a <= cur[1] + gap:
+                cur[1] = max(cur[1], b)
+            else:
+                cur = [a, b]
+                runs.append(cur)
+        for a, b in runs:
+            for x in range(a, b, mreq):
+                offs.append(x)
+                lens.append(min(mreq, b - x))
+    return np.array(offs, np.uint64), np.array(lens, np.uint32)
+
+
 def probe(path: str, col: str, modes, reps: int) -> list:
     """Every mode of ``modes`` on one column, interleaved rep by rep (the
     box's storage rate drifts within a run: a mode's reps in a block would
     take a different storage than the other's)."""
+    import nvme_strom_amd as S
     rd = [_Reader(path, col, m) for m in modes]
+    # the storage reading the extents planner's own requests, no engine: a
+    # column's buffers are 200-500 KiB reads with other columns between them
+    # (not the 1 MiB sequential stream storage_seq measures)
+    sc = rd[0].sc
+    offs, lens = requests(rd[0].groups, sc.EXTENT_GAP, int(S.config_get("max_request")))
+    nw, qd = int(S.config_get("workers")), int(S.config_get("queue_depth"))
+    same = []
     for _ in range(reps):
         for r in rd:
             r.run()
+        S.evict_file(sc.reader.fd)
+        same.append(S.raw_read_list(sc.reader.fd, offs, lens, threads=nw, qd=qd, fixed=True)[1]
+                    * (1 << 30) / 1e9)
     out = [r.row() for r in rd]
+    same_gbps = float(np.median(same))
+    for row in out:
+        row["same_requests_GBps"] = round(same_gbps, 2)
+        row["same_requests"] = len(offs)
+        row["of_same_requests"] = round(row["read_GBps"] / same_gbps, 3)
     for r in rd:
         r.sc.close()
     return out

@@ -209,3 +209,31 @@ def test_arrow_scan_groups_read_as_extents(strom, tmp_path, codec):
     finally:
         os.close(fd)
         sc.close()
+
+
+@pytest.mark.parametrize("gap", [0, 65536])
+def test_probe_request_model_matches_planner(strom, rand_file, gap):
+    """tools/arrow_read_probe.requests() — the raw comparator's request list
+    — issues the planner's requests: same count, same bytes."""
+    from types import SimpleNamespace
+    from nvme_strom_amd.tools.arrow_read_probe import requests
+    size = 8 << 20
+    path, _ = rand_file(size, seed=5)
+    rng = np.random.default_rng(gap + 7)
+    offs, lens = _random_extents(rng, size - (1 << 20), 200)
+    x = strom.extents_array(offs, lens)
+    mreq = int(strom.config_get("max_request"))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        plan = strom.memcpy_ssd2gpu_extents(0, 0, fd, x, gap_max=gap, plan_only=True)
+        keep, hbm = _host_target(plan.dst_bytes)
+        with strom.map_gpu_memory(hbm.ctypes.data, hbm.nbytes) as m:
+            r = strom.memcpy_ssd2gpu_extents(m.handle, 0, fd, strom.extents_array(offs, lens),
+                                             gap_max=gap)
+            strom.memcpy_wait(r.dma_task_id)
+    finally:
+        os.close(fd)
+    ro, rl = requests([SimpleNamespace(ext=x)], gap, mreq)
+    assert len(ro) == r.nr_dma_submit
+    assert int(rl.astype(np.int64).sum()) == r.bytes_read == r.nr_dma_blocks * 512
+    assert (np.diff(ro.astype(np.int64)) > 0).all() and int(rl.max()) <= mreq

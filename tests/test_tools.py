@@ -106,3 +106,30 @@ def test_raw_read_rate(strom, tmp_path):
                 strom.raw_read_rate(fd, bad["block"], bad["nreq"])
     finally:
         os.close(fd)
+
+
+def test_raw_read_list(strom, tmp_path):
+    """The request-list comparator reads exactly the listed bytes (a read at
+    the end comes back short and counts what it read) and rejects unaligned
+    or empty requests."""
+    import os
+    import numpy as np
+    path = tmp_path / "rawl.bin"
+    size = (4 << 20) + 1000
+    path.write_bytes(os.urandom(size))
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        offs = np.arange(0, 4 << 20, 3 << 16, dtype=np.uint64)      # gaps between 64 KiB reads
+        lens = np.full(len(offs), 65536, dtype=np.uint32)
+        iops, gib = strom.raw_read_list(fd, offs, lens, threads=3, qd=4)
+        assert iops > 0 and abs(gib - iops * 65536 / (1 << 30)) < 1e-6 * max(gib, 1)
+        # the last page: 1000 bytes of a 4 KiB request
+        iops, gib = strom.raw_read_list(fd, [4 << 20], [4096], threads=2, qd=2)
+        assert abs(gib - iops * 1000 / (1 << 30)) < 1e-6 * max(gib, 1)
+        for o, n in [([100], [4096]), ([0], [0]), ([0], [1000])]:
+            with pytest.raises(strom.StromError):
+                strom.raw_read_list(fd, o, n)
+        with pytest.raises(ValueError):
+            strom.raw_read_list(fd, [0, 4096], [4096])
+    finally:
+        os.close(fd)
