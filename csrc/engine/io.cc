@@ -1173,13 +1173,6 @@ extern "C" int strom_io_info(uint64_t *out) {
 }
 
 // ----------------------------------------------------- raw storage ceiling
-// The device's own limit for a block size, with no engine in the way:
-// `threads` threads, each with its own io_uring kept `qd` deep with O_DIRECT
-// reads of `block` bytes at random aligned offsets into host memory (or,
-// with `sequential`, the next block of a shared cursor: the order the
-// engine streams a window in).  The sweep prints it next to the engine's
-// SSD→HBM numbers.  `mode` bit 0: sequential; bit 1: buffered reads (the
-// page-cache ceiling the engine-only sweep compares against).
 namespace {
 // One ring per thread kept `qd` deep with O_DIRECT (or buffered, mode bit 1)
 // reads into host memory (2 MiB pages registered with the ring for
@@ -1300,8 +1293,8 @@ int raw_reads(int fd, int mode, uint32_t threads, uint32_t qd, uint64_t slot,
 // The device's own limit for a block size, with no engine in the way:
 // `threads` threads, each with its own io_uring kept `qd` deep with O_DIRECT
 // reads of `block` bytes at random aligned offsets into host memory (or,
-// with `sequential`, the next block of a shared cursor: the order the
-// engine streams a window in).  The sweep prints it next to the engine's
+// with `sequential`, each ring its own run of the file in order: the order
+// the engine's workers stream a window in).  The sweep prints it next to the engine's
 // SSD→HBM numbers.  `mode` bit 0: sequential; bit 1: buffered reads (the
 // page-cache ceiling the engine-only sweep compares against); bit 2: reads
 // into 2 MiB-page memory registered with the ring (READ_FIXED), as the

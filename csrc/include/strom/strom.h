@@ -76,7 +76,7 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n);
 
 /* Storage ceiling for a block size, no engine: `threads` io_uring rings,
  * each `qd` deep, O_DIRECT reads of `block` bytes at random aligned
- * offsets (or in file order from a shared cursor when `sequential`) into
+ * offsets (or, `sequential`, each ring its own run in file order) into
  * host memory until `nreq` reads are done. */
 int strom_raw_read_rate(int fd, uint64_t block, uint32_t nreq, uint32_t threads, uint32_t qd,
                         int sequential, double *iops, double *gibps);
