@@ -1184,6 +1184,7 @@ int raw_reads(int fd, int mode, uint32_t threads, uint32_t qd, uint64_t slot,
               uint64_t *bytes_out, double *sec_out) {
   using namespace strom;
   const bool fixed = (mode & 4) != 0;
+  if (slot * qd > (4ull << 30)) return -E2BIG;   // per ring: qd reads of the largest request
   // rings on the CPUs the engine's workers use (config numa_bind: the
   // current GPU's NUMA node), so the comparison is like for like
   int node = -1;

@@ -31,6 +31,20 @@ def _hidden(r):
     return (r["load_s"] + r["gather_s"] - r["wall_s"]) / min(r["load_s"], r["gather_s"])
 
 
+def _pairs(OB, path, window, steps, n, reps, decoder=None, k=3):
+    """``k`` serial / overlap runs alternated (the pool boxes' storage rate
+    drifts within seconds); the pair with the median overlap/serial load
+    ratio is the one checked."""
+    rows = []
+    for _ in range(k):
+        ser = OB.run(path, window, steps, n, overlap=False, gather_reps=reps, decoder=decoder)
+        ovl = OB.run(path, window, steps, n, overlap=True, gather_reps=reps, decoder=decoder)
+        rows.append((ovl["load_GiBps"] / ser["load_GiBps"], ser, ovl))
+    rows.sort(key=lambda r: r[0])
+    print("ratios", [round(r[0], 3) for r in rows])
+    return rows[len(rows) // 2][1:]
+
+
 def _check(ser, ovl, steps=8):
     assert ser["verified"] and ovl["verified"]
     assert _hidden(ser) < 0.35, ser
@@ -47,8 +61,7 @@ def test_load_overlaps_side_stream_collective(S, tmp_path, n):
     path = str(tmp_path / "ov.bin")
     OB._mk(path, 1 << 30)
     reps = OB.calibrate(path, 128 << 20, n)
-    ser = OB.run(path, 128 << 20, 8, n, overlap=False, gather_reps=reps)
-    ovl = OB.run(path, 128 << 20, 8, n, overlap=True, gather_reps=reps)
+    ser, ovl = _pairs(OB, path, 128 << 20, 8, n, reps)
     print("reps", reps, "serial", ser)
     print("overlap", ovl)
     _check(ser, ovl)
@@ -66,8 +79,7 @@ def test_load_overlaps_lds_heavy_decoder(S, tmp_path):
     # its stream count: 512 MiB windows make a load the longer of the two
     dec = OB.Decoder(torch.device("cuda"), nstreams=256)
     reps = OB.calibrate(path, 512 << 20, 2, dec)
-    ser = OB.run(path, 512 << 20, 6, 2, overlap=False, gather_reps=reps, decoder=dec)
-    ovl = OB.run(path, 512 << 20, 6, 2, overlap=True, gather_reps=reps, decoder=dec)
+    ser, ovl = _pairs(OB, path, 512 << 20, 6, 2, reps, decoder=dec)
     print("reps", reps, "serial", ser)
     print("overlap", ovl)
     _check(ser, ovl, steps=6)

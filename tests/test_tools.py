@@ -131,5 +131,7 @@ def test_raw_read_list(strom, tmp_path):
                 strom.raw_read_list(fd, o, n)
         with pytest.raises(ValueError):
             strom.raw_read_list(fd, [0, 4096], [4096])
+        with pytest.raises(strom.StromError):           # 256 x 64 MiB of buffers per ring
+            strom.raw_read_list(fd, [0], [64 << 20], qd=256)
     finally:
         os.close(fd)
