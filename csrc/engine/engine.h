@@ -50,9 +50,13 @@ struct Config {
   int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
   int staging_slots = 4;         // minimum pinned slots per worker (GPU dest)
-  bool stage_by_bytes = true;    // at least queue_depth slots, in-flight reads bounded
-                                 // by staging bytes (short requests go deeper); off:
-                                 // the slot count alone bounds them (round-5 rule)
+  bool stage_by_bytes = false;   // opt-in: at least queue_depth slots, in-flight reads
+                                 // bounded by staging bytes (short requests go deeper).
+                                 // Off by default: the headline bench lost 12 % with
+                                 // 8 slots rotating instead of 4 at the same reads in
+                                 // flight (21.6 -> 18.9 GiB/s, three alternated rounds,
+                                 // profiles/r6/staging/*_r6m.json) and the Arrow probe
+                                 // gained nothing (profiles/r6/SUMMARY.md)
   uint32_t staging_bytes = 0;    // opt-in: pinned staging per worker, slots =
                                  // max(staging_slots, staging_bytes / max_request),
                                  // queue depth grows to match.  Off by default:
