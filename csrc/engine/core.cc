@@ -36,7 +36,7 @@ Config Config::from_env() {
                                "staging_slots", "staging_bytes", "spin_us", "inline_max",
                                "bar_map", "bar_max", "bar_nt", "inline_plain", "coalesce", "trace",
                                "ingest", "ingest_grid", "ingest_piece", "ingest_min", "ingest_prio", "hdp_sync",
-                               "fixed_bufs", "io_prof", "fd_kcmp", "stage_by_bytes",
+                               "fixed_bufs", "io_prof", "fd_kcmp", "stage_by_bytes", "slot_lifo",
                                "strict", "direct_io",
                                "pgcache_probe", "gpu_emulation", "numa_bind", "check_freed",
                                "stat_info", "verbose"};
@@ -97,6 +97,7 @@ int Config::set(const std::string &k, const std::string &v) {
   if (k == "io_prof") { io_prof = parse_bool(v); return 0; }
   if (k == "fd_kcmp") { fd_kcmp = parse_bool(v); return 0; }
   if (k == "stage_by_bytes") { stage_by_bytes = parse_bool(v); return 0; }
+  if (k == "slot_lifo") { slot_lifo = parse_bool(v); return 0; }
   if (k == "ingest_min") {
     if (n < 0 || n > (64l << 20)) return -EINVAL;
     ingest_min = (uint32_t)n;
@@ -160,6 +161,7 @@ int Config::get(const std::string &k, std::string *out) const {
   else if (k == "io_prof") v = io_prof;
   else if (k == "fd_kcmp") v = fd_kcmp;
   else if (k == "stage_by_bytes") v = stage_by_bytes;
+  else if (k == "slot_lifo") v = slot_lifo;
   else if (k == "ingest_min") v = ingest_min;
   else if (k == "trace") v = trace;
   else if (k == "bar_max") v = bar_max;

@@ -50,6 +50,8 @@ struct Config {
   int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
   int staging_slots = 4;         // minimum pinned slots per worker (GPU dest)
+  bool slot_lifo = false;        // hand out the most recently freed staging slot
+                                 // (FIFO otherwise: adjacent requests, adjacent slots)
   bool stage_by_bytes = false;   // opt-in: at least queue_depth slots, in-flight reads
                                  // bounded by staging bytes (short requests go deeper).
                                  // Off by default: the headline bench lost 12 % with

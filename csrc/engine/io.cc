@@ -773,7 +773,7 @@ struct IoEngine::Worker {
       if (free_slots.empty()) return false;
       // the byte budget (a request alone may always start)
       if (cfg.stage_by_bytes && stage_inflight && stage_inflight + r.len > stage_budget()) return false;
-      if (cfg.coalesce) {
+      if (cfg.coalesce && !cfg.slot_lifo) {
         slot = free_slots.front();
         free_slots.pop_front();
       } else {
