@@ -50,8 +50,12 @@ struct Config {
   int queue_depth = 8;           // in-flight reads per worker (uring)
   uint32_t max_request = 1u << 20;  // merge limit (bytes); v0.6 used 128 KiB
   int staging_slots = 4;         // minimum pinned slots per worker (GPU dest)
-  bool slot_lifo = false;        // hand out the most recently freed staging slot
-                                 // (FIFO otherwise: adjacent requests, adjacent slots)
+  bool slot_lifo = true;         // hand out the most recently freed staging slot
+                                 // (false: FIFO, adjacent requests in adjacent slots).
+                                 // Bench A/B over three boxes, 9 alternated pairs: LIFO
+                                 // ahead or level in 8, 18.5 -> 21.3 GiB/s mean on a
+                                 // noisy box, +3 % on a quiet one, and steadier
+                                 // (profiles/r6/staging/*_r6{n,o,p}.json)
   bool stage_by_bytes = false;   // opt-in: at least queue_depth slots, in-flight reads
                                  // bounded by staging bytes (short requests go deeper).
                                  // Off by default: the headline bench lost 12 % with
