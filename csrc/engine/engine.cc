@@ -904,15 +904,25 @@ using namespace strom;
 
 static std::mutex g_sess_mu;
 static int g_next_session = 1;
-static int g_kernel_fd = -2;  // -2 unknown, -1 none
+static std::atomic<int> g_kernel_fd{-2};  // -2 unknown, -1 none
 
+// the kernel provider's descriptor, probed once (under g_sess_mu); every
+// later call is one acquire load — no lock on the per-ioctl / QD1 path
 static int kernel_fd() {
-  if (g_kernel_fd != -2) return g_kernel_fd;
+  const int k = g_kernel_fd.load(std::memory_order_acquire);
+  if (k != -2) return k;
+  std::lock_guard<std::mutex> g(g_sess_mu);
+  int fd = g_kernel_fd.load(std::memory_order_relaxed);
+  if (fd != -2) return fd;
   const char *prov = getenv("STROM_PROVIDER");
-  if (prov && strcmp(prov, "user") == 0) return g_kernel_fd = -1;
-  int fd = open(STROM_DEVICE_PATHNAME, O_RDONLY | O_CLOEXEC);
-  if (fd < 0) fd = open(NVME_STROM_IOCTL_PATHNAME, O_RDONLY | O_CLOEXEC);
-  return g_kernel_fd = fd;
+  if (prov && strcmp(prov, "user") == 0) {
+    fd = -1;
+  } else {
+    fd = open(STROM_DEVICE_PATHNAME, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) fd = open(NVME_STROM_IOCTL_PATHNAME, O_RDONLY | O_CLOEXEC);
+  }
+  g_kernel_fd.store(fd, std::memory_order_release);
+  return fd;
 }
 
 // Kernel provider: MAP_GPU_MEMORY carries only a VA, which the kernel
@@ -946,10 +956,7 @@ extern "C" {
 
 const char *strom_version(void) { return "strom-mi355x 0.1.0 (abi nvme-strom 0.6)"; }
 
-int strom_provider(void) {
-  std::lock_guard<std::mutex> g(g_sess_mu);
-  return kernel_fd() >= 0 ? 1 : 0;
-}
+int strom_provider(void) { return kernel_fd() >= 0 ? 1 : 0; }
 
 int strom_open(void) {
   std::lock_guard<std::mutex> g(g_sess_mu);
@@ -964,11 +971,7 @@ int strom_close(int session) {
 }
 
 int strom_ioctl(int session, unsigned long cmd, void *arg) {
-  int kfd;
-  {
-    std::lock_guard<std::mutex> g(g_sess_mu);
-    kfd = kernel_fd();
-  }
+  const int kfd = kernel_fd();
   if (kfd >= 0) {
     if (cmd == STROM_IOCTL__MAP_GPU_MEMORY) return kernel_map_gpu(kfd, (strom_map_gpu_memory *)arg);
     int r = ioctl(kfd, cmd, arg);
@@ -993,11 +996,7 @@ long strom_pread_gpu(int session, unsigned long handle, size_t offset, int fd,
   if ((file_off | len) & 4095) return -EINVAL;
   if (len == 0) return 0;
   {
-    int kfd;
-    {
-      std::lock_guard<std::mutex> g(g_sess_mu);
-      kfd = kernel_fd();
-    }
+    const int kfd = kernel_fd();
     if (kfd < 0) {
       // userspace provider: task-less synchronous path
       const long r = engine().pread_sync(handle, offset, fd, file_off, len);
