@@ -56,13 +56,12 @@ struct Config {
                                  // ahead or level in 8, 18.5 -> 21.3 GiB/s mean on a
                                  // noisy box, +3 % on a quiet one, and steadier
                                  // (profiles/r6/staging/*_r6{n,o,p}.json)
-  bool stage_by_bytes = false;   // opt-in: at least queue_depth slots, in-flight reads
-                                 // bounded by staging bytes (short requests go deeper).
-                                 // Off by default: the headline bench lost 12 % with
-                                 // 8 slots rotating instead of 4 at the same reads in
-                                 // flight (21.6 -> 18.9 GiB/s, three alternated rounds,
-                                 // profiles/r6/staging/*_r6m.json) and the Arrow probe
-                                 // gained nothing (profiles/r6/SUMMARY.md)
+  bool stage_by_bytes = true;    // at least queue_depth slots, in-flight reads bounded
+                                 // by staging bytes (short requests go deeper).  With
+                                 // FIFO slots it cost the bench 12 % (8 slots rotating
+                                 // instead of 4, profiles/r6/staging/*_r6m.json); with
+                                 // slot_lifo the bench is level (27.7 vs 27.2 GiB/s) and
+                                 // 227-488 KiB extent reads gain 5-14 % (*_r6t.json)
   uint32_t staging_bytes = 0;    // opt-in: pinned staging per worker, slots =
                                  // max(staging_slots, staging_bytes / max_request),
                                  // queue depth grows to match.  Off by default:

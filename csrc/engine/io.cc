@@ -464,12 +464,11 @@ struct IoEngine::Worker {
   // raw ceiling's while earlier slots are still on their way to HBM (round 2
   // sweep: 4 slots capped 64 KiB reads at 0.72 of raw); staging_bytes opts
   // into more
-  // ... and, config stage_by_bytes (opt-in), at least queue_depth slots:
-  // requests shorter than max_request (an Arrow column's buffers, 200-500
-  // KiB) are held to the same in-flight BYTES as full ones (stage_budget),
-  // not to the same count.  Measured: no gain for 227 KiB reads, and 8
-  // slots rotating for 1 MiB reads cost the bench 12 % against 4 at the
-  // same reads in flight (profiles/r6/SUMMARY.md)
+  // ... and, config stage_by_bytes, at least queue_depth slots: requests
+  // shorter than max_request (an Arrow column's buffers, 200-500 KiB) are
+  // held to the same in-flight BYTES as full ones (stage_budget), not to the
+  // same count.  Only with slot_lifo: 8 slots handed out FIFO put twice the
+  // staging under 1 MiB reads and cost the bench 12 % (profiles/r6/SUMMARY.md)
   int nslots() const {
     const size_t budget = (size_t)cfg.staging_slots << 20;
     const size_t small = std::min<size_t>((size_t)cfg.queue_depth * 4, budget / cfg.max_request);
