@@ -2,7 +2,7 @@
 // (the reference's utils/nvme_test.c, re-designed; same options).
 //
 //   strom_test [-d gpu] [-n nr_segments] [-s segment_MiB] [-b chunk_KiB]
-//              [-c] [-f[KiB]] [-p] [-x passes] FILE
+//              [-c] [-f[KiB]] [-p] [-x passes] [-e LEN:STRIDE[:GAP]] FILE
 //
 //   -c      verify every chunk: per-chunk CRC32C computed ON THE GPU compared
 //           with the host CRC of the chunk that landed in that slot (the
@@ -10,6 +10,11 @@
 //           src/dst mapping inverted: SURVEY §4 defect #2)
 //   -f[KiB] VFS control: pread into pinned memory + hipMemcpyAsync
 //   -p      print the GPU mapping (LIST/INFO) and exit
+//   -e LEN:STRIDE[:GAP]  (KiB) byte-range reads instead of chunk ids: every
+//           segment's file range as extents of LEN every STRIDE, issued as
+//           one MEMCPY_SSD2GPU_EXTENTS (round-6 extension ioctl), holes up
+//           to GAP read through; -c copies each landed extent back and
+//           compares it with pread of its file range
 //
 // A ring of nr_segments segments lives in one hipMalloc allocation poisoned
 // with 0x41424344.  MEMCPY_SSD2GPU is issued per segment; page-cache chunks
@@ -54,6 +59,8 @@ struct Slot {
   unsigned long task = 0;
   bool busy = false;
   std::vector<uint32_t> ids;
+  std::vector<strom_file_extent> ext;   // -e: this segment's extents (dst_off filled in)
+  uint64_t dst_bytes = 0;
   uint32_t nr_ssd = 0, nr_ram = 0;
   char *wb = nullptr;
   hipStream_t st = nullptr;
@@ -62,9 +69,10 @@ struct Slot {
 int main(int argc, char **argv) {
   int dev = 0, nseg = 6, passes = 1;
   size_t seg_mib = 32, chunk_kib = 8, vfs_kib = 0;
-  bool check = false, print = false, vfs = false;
+  bool check = false, print = false, vfs = false, extents = false;
+  size_t ext_len = 0, ext_stride = 0, ext_gap = 0;
   int opt;
-  while ((opt = getopt(argc, argv, "d:n:s:b:cf::px:")) != -1) {
+  while ((opt = getopt(argc, argv, "d:n:s:b:cf::px:e:")) != -1) {
     switch (opt) {
       case 'd': dev = atoi(optarg); break;
       case 'n': nseg = atoi(optarg); break;
@@ -74,10 +82,22 @@ int main(int argc, char **argv) {
       case 'f': vfs = true; vfs_kib = optarg ? strtoul(optarg, nullptr, 0) : 0; break;
       case 'p': print = true; break;
       case 'x': passes = atoi(optarg); break;
+      case 'e': {
+        unsigned long a = 0, b = 0, g = 0;
+        if (sscanf(optarg, "%lu:%lu:%lu", &a, &b, &g) < 2 || a == 0 || b < a) {
+          fprintf(stderr, "-e LEN:STRIDE[:GAP] in KiB, STRIDE >= LEN > 0\n");
+          return 1;
+        }
+        extents = true;
+        ext_len = a << 10;
+        ext_stride = b << 10;
+        ext_gap = g << 10;
+        break;
+      }
       default:
         fprintf(stderr,
                 "usage: %s [-d gpu] [-n segments] [-s segment_MiB] [-b chunk_KiB] [-c] [-f[KiB]] "
-                "[-p] [-x passes] FILE\n",
+                "[-p] [-x passes] [-e LEN:STRIDE[:GAP]] FILE\n",
                 argv[0]);
         return 1;
     }
@@ -89,6 +109,14 @@ int main(int argc, char **argv) {
   const char *path = argv[optind];
   const size_t seg_sz = seg_mib << 20, chunk = chunk_kib << 10;
   const uint32_t per_seg = (uint32_t)(seg_sz / chunk);
+  if (extents && vfs) {
+    fprintf(stderr, "-e and -f are exclusive\n");
+    return 1;
+  }
+  // -e: a segment's extents land back to back, each widened to whole pages
+  // (at most 8 KiB more per extent than its bytes)
+  const size_t n_ext_max = extents ? (seg_sz + ext_stride - 1) / ext_stride : 0;
+  const size_t slot_cap = extents ? ((seg_sz + n_ext_max * 8192 + 65535) & ~(size_t)65535) : seg_sz;
   int fd = open(path, O_RDONLY);
   if (fd < 0) die(path);
   struct stat sb;
@@ -109,12 +137,12 @@ int main(int argc, char **argv) {
   CK(hipGetDeviceProperties(&prop, dev));
   CK(hipSetDevice(dev));
   void *dbuf = nullptr;
-  CK(hipMalloc(&dbuf, seg_sz * nseg));
-  CK(hipMemsetD32((hipDeviceptr_t)dbuf, 0x41424344, seg_sz * nseg / 4));
+  CK(hipMalloc(&dbuf, slot_cap * nseg));
+  CK(hipMemsetD32((hipDeviceptr_t)dbuf, 0x41424344, slot_cap * nseg / 4));
 
   strom_map_gpu_memory mg{};
   mg.vaddress = (uint64_t)dbuf;
-  mg.length = seg_sz * nseg;
+  mg.length = slot_cap * nseg;
   if (nvme_strom_ioctl(STROM_IOCTL__MAP_GPU_MEMORY, &mg) != 0) die("MAP_GPU_MEMORY");
 
   if (print) {
@@ -146,7 +174,9 @@ int main(int argc, char **argv) {
   std::vector<uint32_t> h_crc(per_seg);
   std::vector<char> cbuf(chunk);
   if (check) CK(hipMalloc((void **)&d_crc, sizeof(uint32_t) * per_seg));
+  std::vector<char> hland(extents && check ? slot_cap : 0), hfile(extents && check ? ext_len : 0);
   uint64_t nr_ram = 0, nr_ssd = 0, nr_submit = 0, nr_blocks = 0, bad = 0, checked = 0;
+  uint64_t ext_bytes = 0, ext_read = 0;
   double wait_s = 0;
 
   auto retire = [&](int k) {
@@ -163,7 +193,21 @@ int main(int argc, char **argv) {
     }
     CK(hipStreamSynchronize(s.st));
     wait_s += now() - w0;
-    if (check) {
+    if (check && extents) {
+      // the reference's -c way (copy back + compare), per extent
+      const char *seg = (const char *)dbuf + (size_t)k * slot_cap;
+      CK(hipMemcpy(hland.data(), seg, s.dst_bytes, hipMemcpyDeviceToHost));
+      for (const strom_file_extent &x : s.ext) {
+        ssize_t got = pread(fd, hfile.data(), x.len, (off_t)x.file_off);
+        if (got != (ssize_t)x.len || memcmp(hfile.data(), hland.data() + x.dst_off, x.len) != 0) {
+          if (bad < 8)
+            fprintf(stderr, "corruption: segment %d extent @%llu+%u (dst %llu)\n", k,
+                    (unsigned long long)x.file_off, x.len, (unsigned long long)x.dst_off);
+          ++bad;
+        }
+        ++checked;
+      }
+    } else if (check) {
       char *seg = (char *)dbuf + (size_t)k * seg_sz;
       uint32_t n = (uint32_t)s.ids.size();
       if (strom_crc32c_chunks(seg, (uint64_t)n * chunk, (uint32_t)chunk, d_crc, s.st) != 0) {
@@ -197,10 +241,33 @@ int main(int argc, char **argv) {
       Slot &s = ring[slot];
       size_t len = std::min(seg_sz, fsize - off);
       uint32_t n = (uint32_t)((len + chunk - 1) / chunk);
-      char *dst = (char *)dbuf + (size_t)slot * seg_sz;
+      char *dst = (char *)dbuf + (size_t)slot * slot_cap;
       s.ids.resize(n);
       for (uint32_t i = 0; i < n; ++i) s.ids[i] = (uint32_t)(off / chunk + i);
-      if (vfs) {
+      if (extents) {
+        s.ext.clear();
+        for (size_t p = off; p < off + len; p += ext_stride) {
+          strom_file_extent x{};
+          x.file_off = p;
+          x.len = (uint32_t)std::min(ext_len, fsize - p);
+          s.ext.push_back(x);
+          ext_bytes += x.len;
+        }
+        strom_memcpy_ssd2gpu_extents a{};
+        a.handle = mg.handle;
+        a.offset = (size_t)slot * slot_cap;
+        a.file_desc = fd;
+        a.nr_extents = (unsigned)s.ext.size();
+        a.gap_max = (unsigned)ext_gap;
+        a.extents = s.ext.data();
+        if (nvme_strom_ioctl(STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a) != 0)
+          die("MEMCPY_SSD2GPU_EXTENTS");
+        s.task = a.dma_task_id;
+        s.dst_bytes = a.dst_bytes;
+        nr_submit += a.nr_dma_submit;
+        nr_blocks += a.nr_dma_blocks;
+        ext_read += a.bytes_read;
+      } else if (vfs) {
         size_t unit = vfs_kib ? vfs_kib << 10 : len;
         for (size_t p = 0; p < len; p += unit) {
           ssize_t got = pread(fd, s.wb + p, std::min(unit, len - p), (off_t)(off + p));
@@ -238,12 +305,19 @@ int main(int argc, char **argv) {
   }
   for (int i = 0; i < nseg; ++i) retire((k + i) % nseg);
   double dt = now() - t0;
+  if (extents) total = ext_bytes;   // the bytes asked for; the bytes read are printed below
   printf("GPU[%d] %s (%s)\n", dev, prop.name, prop.gcnArchName);
   printf("file: %s, read: %zu MB, time: %.3f sec, throughput: %.2f GB/s (%.2f GiB/s)\n", path,
          total >> 20, dt, total / dt / 1e9, total / dt / (1 << 30));
   printf("mode: %s, segments: %d x %zu MiB, chunk: %zu KiB, wait: %.3f sec\n",
-         vfs ? "VFS (pread+HtoD)" : "SSD2GPU", nseg, seg_mib, chunk_kib, wait_s);
-  if (!vfs)
+         vfs ? "VFS (pread+HtoD)" : extents ? "SSD2GPU_EXTENTS" : "SSD2GPU", nseg, seg_mib,
+         chunk_kib, wait_s);
+  if (extents)
+    printf("extents: %zu KiB every %zu KiB, gap_max %zu KiB; bytes read: %llu MB (%.3f of the "
+           "extents), average request: %.1f KB\n",
+           ext_len >> 10, ext_stride >> 10, ext_gap >> 10, (unsigned long long)(ext_read >> 20),
+           ext_bytes ? (double)ext_read / ext_bytes : 0.0, nr_submit ? 0.5 * nr_blocks / nr_submit : 0.0);
+  else if (!vfs)
     printf("nr_ram2gpu: %llu, nr_ssd2gpu: %llu, average DMA size: %.1f KB\n",
            (unsigned long long)nr_ram, (unsigned long long)nr_ssd,
            nr_submit ? 0.5 * nr_blocks / nr_submit : 0.0);

@@ -54,6 +54,27 @@ def test_strom_test_cli_verify(rand_file):
     assert pr.returncode == 0 and "mapped region" in pr.stdout
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", ["100:300", "100:300:256", "13:13"])
+def test_strom_test_cli_extents(rand_file, spec):
+    """strom_test -e: MEMCPY_SSD2GPU_EXTENTS per segment, every landed extent
+    compared with pread of its file range; holes read through with a gap."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    path, _ = rand_file((40 << 20) + 12345)            # a partial last extent
+    out = subprocess.run([_tool("strom_test"), "-c", "-n", "3", "-s", "8", "-e", spec, path],
+                         capture_output=True, text=True, timeout=300, env=_env())
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "SSD2GPU_EXTENTS" in out.stdout and " 0 corrupted" in out.stdout, out.stdout
+    ln, stride = (int(v) for v in spec.split(":")[:2])
+    amp = float(out.stdout.split("(")[-1].split(" of the")[0]) if "of the" in out.stdout else None
+    if spec.count(":") == 2:                           # 200 KiB holes read through
+        assert amp is not None and amp > 2.5
+    elif ln == stride:
+        assert amp is not None and amp < 1.01
+
+
 def test_block_sweep_cpu(strom, tmp_path):
     """Block-size sweep tool end to end on emulated HBM (small sizes)."""
     from nvme_strom_amd.tools import sweep
