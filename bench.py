@@ -449,6 +449,9 @@ def main() -> int:
             "workers": int(S.config_get("workers")),
             "placement": placement,
             "max_request": int(S.config_get("max_request")),
+            "engine": {k: S.config_get(k) for k in ("queue_depth", "staging_slots", "stage_by_bytes",
+                                                     "slot_lifo", "ingest", "ingest_grid",
+                                                     "ingest_piece", "fixed_bufs")},
         },
     }
     if rank == 0:
