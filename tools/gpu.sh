@@ -41,6 +41,11 @@
 #   ceiling    engine + ingest ceiling: page-cache reads (backend=cache) vs O_DIRECT
 #   pg         end-to-end PostgreSQL heap scan (GPU ring vs the reference-shaped CPU scan)
 #   stripe     config-3 proxy: 4-member stripe set vs one file (tools.stripe_bench)
+#   probe      Arrow column reads alone vs storage_seq and vs the same requests read raw
+#              (tools.arrow_read_probe; PROBE_ARGS)
+#   benchab    bench.py arms alternated round by round, each with its own STROM_* settings:
+#              BENCHAB="def: lifo:SLOT_LIFO=1 s6:STAGING_SLOTS=6,QUEUE_DEPTH=8" BENCHAB_ROUNDS=3
+#              (how every staging / geometry A/B of profiles/r6/SUMMARY.md was run)
 # Output lands in gpurun_out/TAG/.  One-off recipes (several phases with
 # env overrides) live in tools/run/, which git ignores; the commands behind
 # every committed profile are written into its profiles/rN/*/SUMMARY.md.
@@ -174,6 +179,17 @@ for phase in "$@"; do
                 -- python3 -m nvme_strom_amd.tools.decomp_ab "$ROOT/${DECLIB:-nvme_strom_amd/lib/ab/base.so}" \
                    --rounds 1 --cases "${DECCASES:-lz4_words,lz4_ints}") || exit 1
             done ;;
+    probe) step probe 600 python -u -m nvme_strom_amd.tools.arrow_read_probe ${PROBE_ARGS:---codec zstd --columns val,x} \
+             --out "$OUT/probe.json" ;;
+    benchab) i=0
+      for r in $(seq 1 ${BENCHAB_ROUNDS:-2}); do
+        for arm in ${BENCHAB:-def:}; do
+          i=$((i + 1)); name=${arm%%:*}; kv=${arm#*:}; envs=()
+          for x in ${kv//,/ }; do envs+=("STROM_$x"); done
+          step "bench_${i}_$name" 300 env "${envs[@]}" python -u bench.py
+          grep '^{' "$OUT/bench_${i}_$name.log" | tail -1 > "$OUT/bench_${i}_$name.json"
+        done
+      done ;;
     pg) step pg 400 python -u -m nvme_strom_amd.tools.pg_bench --out "$OUT/pg.json" ;;
     stripe) step stripe 400 python -u -m nvme_strom_amd.tools.stripe_bench --out "$OUT/stripe.json" ;;
     ceiling) step ceiling 400 python -u -m nvme_strom_amd.tools.ceiling_bench --out "$OUT/ceiling.json" ;;
