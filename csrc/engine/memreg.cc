@@ -488,7 +488,7 @@ int DmaBufRegistry::gc() {
   if (DIR *d = opendir("/proc/self/fd")) {
     while (struct dirent *e = readdir(d)) {
       if (e->d_name[0] == '.') continue;
-      char path[64], tgt[256];
+      char path[16 + sizeof e->d_name], tgt[256];
       snprintf(path, sizeof path, "/proc/self/fd/%s", e->d_name);
       ssize_t n = readlink(path, tgt, sizeof tgt - 1);
       if (n <= 0) continue;

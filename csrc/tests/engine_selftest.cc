@@ -5,7 +5,8 @@
 // irqsave spinlocks, RCU and refcounts (kmod/nvme_strom.c:648-731,
 // 1148-1187): many threads issuing SSD2RAM tasks and waiting on them,
 // injected device errors racing with completions, session close reclaiming
-// failed tasks, emulated-GPU SSD2GPU with the page-cache hybrid, the fake
+// failed tasks, emulated-GPU SSD2GPU with the page-cache hybrid, byte-range
+// (extent) reads from several threads, the fake
 // backend's out-of-order completions over a stripe set, and engine teardown
 // while idle.
 #include <errno.h>
@@ -161,6 +162,61 @@ int main() {
           if (memcmp(dst + (t * per + i) * CH, data.data() + (size_t)ids[i] * CH, CH)) bad++;
         for (unsigned i = a.nr_ssd2gpu; i < per; ++i)
           if (memcmp(wb.data() + (t * per + i) * CH, data.data() + (size_t)ids[i] * CH, CH)) bad++;
+        strom_close(s);
+      });
+    }
+    for (auto &x : g) x.join();
+    CHECK(bad == 0);
+    strom_unmap_gpu_memory um{m.handle};
+    CHECK(nvme_strom_ioctl(STROM_IOCTL__UNMAP_GPU_MEMORY, &um) == 0);
+  }
+
+  // 4. MEMCPY_SSD2GPU_EXTENTS from 4 threads into emulated HBM: random
+  //    sorted extents (some empty, some holes read through), a plan-only call
+  //    first for the layout, every landed extent checked against the file
+  {
+    std::vector<uint8_t> hbm(2 * fsz + 65536);
+    uint8_t *dst = (uint8_t *)(((uintptr_t)hbm.data() + 65535) & ~(uintptr_t)65535);
+    strom_map_gpu_memory m{};
+    m.vaddress = (uint64_t)dst;
+    m.length = 2 * fsz;
+    CHECK(nvme_strom_ioctl(STROM_IOCTL__MAP_GPU_MEMORY, &m) == 0);
+    std::vector<std::thread> g;
+    for (int t = 0; t < 4; ++t) {
+      g.emplace_back([&, t] {
+        int s = strom_open();
+        std::mt19937_64 r(100 + t);
+        const size_t room = fsz / 2;                     // this thread's destination slice
+        for (int rep = 0; rep < 30; ++rep) {
+          std::vector<strom_file_extent> x;
+          uint64_t pos = r() % 5000;
+          while (x.size() < 64 && pos < fsz - 1) {
+            strom_file_extent e{};
+            e.file_off = pos;
+            e.len = (uint32_t)std::min<uint64_t>((r() % 3 == 0) ? 0 : 1 + r() % 40000, fsz - pos);
+            x.push_back(e);
+            pos += e.len + (r() % 2 ? r() % 64 : r() % 90000);
+          }
+          strom_memcpy_ssd2gpu_extents a{};
+          a.handle = m.handle;
+          a.offset = t * room;
+          a.file_desc = fd;
+          a.nr_extents = (unsigned)x.size();
+          a.gap_max = (unsigned)(r() % 2 ? 16384 : 0);
+          a.flags = STROM_EXTENTS_PLAN_ONLY;
+          a.extents = x.data();
+          if (strom_ioctl(s, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a) != 0) { bad++; continue; }
+          if (a.dst_bytes > room) continue;              // does not fit this slice: skip
+          const uint64_t span = a.dst_bytes;
+          a.flags = 0;
+          if (strom_ioctl(s, STROM_IOCTL__MEMCPY_SSD2GPU_EXTENTS, &a) != 0) { bad++; continue; }
+          strom_memcpy_wait w{};
+          w.dma_task_id = a.dma_task_id;
+          if (strom_ioctl(s, STROM_IOCTL__MEMCPY_WAIT, &w) != 0) bad++;
+          if (a.dst_bytes != span) bad++;
+          for (const strom_file_extent &e : x)
+            if (e.len && memcmp(dst + t * room + e.dst_off, data.data() + e.file_off, e.len)) bad++;
+        }
         strom_close(s);
       });
     }
