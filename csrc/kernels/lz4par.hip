@@ -114,12 +114,17 @@ static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
 static_assert((HR & (HR - 1)) == 0, "ring: a power of two");
 #ifndef LZ4PAR_LOOKBACK
-#define LZ4PAR_LOOKBACK 512
+#define LZ4PAR_LOOKBACK (LZ4PAR_NT == 512 ? 512 : 448)
 #endif
 // a speculative chain starts this many bytes before its slice (its bits
 // are recorded from the slice start on): a chain from a wrong start needs
 // ~100 bytes to fall onto the true token grid on int columns, and a slice
-// whose chain has not merged by its true entry costs a serial fix-up round
+// whose chain has not merged by its true entry costs a serial fix-up round.
+// 256-thread build, 2,048 / 8,192 streams (profiles/r6/lz4par/lookback_ab_r6y.json):
+// 448 beats 512 on every column (val 137.9 / 141.1 vs 136.7 / 140.0, ids
+// 126.6 / 130.7 vs 124.5 / 128.9, text level); 384 and 320 fall off the val
+// cliff (~100 GB/s) for ids 128-135.  The 512-thread build keeps 512 (not
+// measured at 448)
 constexpr uint32_t LB = LZ4PAR_LOOKBACK;
 // snappy's chains (with restarts) meet the true one within ~100 bytes:
 // 512 -> 128 bytes of run-in took 512 streams from 55 / 44 / 39 GB/s
