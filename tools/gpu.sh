@@ -10,6 +10,7 @@
 #   zpmc       two PMC passes (issue / wait / LDS / memory mix) over zstd_bench val + x
 #   lppmc      the same over the LP zstd kernels only (--modes lp), summarized (pmc_summary)
 #   lptrace    kernel trace + stats of the LP zstd kernels (time per kernel)
+#   lzpmc      two PMC passes over the block-parallel LZ4 decoder (lz4par_bench), summarized
 #   mvpmc      two PMC passes over the heap scan with / without the snapshot check (kbench mvcc)
 #   zarrow     config-5 Arrow scan of a ZSTD-written file
 #   ztrace     rocprofv3 kernel trace + stats of a short zstd_bench
@@ -98,6 +99,16 @@ for phase in "$@"; do
           (cd /tmp && step lptrace 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/lptrace" -o trace \
             -- python3 -m nvme_strom_amd.tools.zstd_bench --kinds ${ZKINDS:-val,ids,text} --levels 1 \
                --streams ${ZSTREAMS:-2048} --modes lp --no-lz4 --iters 3) || exit 1 ;;
+    lzpmc) n=0 # the block-parallel LZ4 decoder (lz4par_kernel_*): two PMC passes, summarized
+          for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
+                      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+            n=$((n + 1))
+            (cd /tmp && step lzpmc$n 120 rocprofv3 --pmc $pass --kernel-include-regex lz4par_kernel --output-format csv \
+              -d "$OUT/lzpmc$n" -o pmc -- python3 -m nvme_strom_amd.tools.lz4par_bench --kinds ${LZKINDS:-val,ids,text} \
+                 --streams ${LZSTREAMS:-2048} --distinct 32 --iters 1 --no-lanes) || exit 1
+          done
+          step lzpmcsum 60 python3 -m nvme_strom_amd.tools.pmc_summary "$OUT"/lzpmc1 "$OUT"/lzpmc2 \
+            --out "$OUT/lzpmc_summary.json" ;;
     mvpmc) n=0 # the heap scan's snapshot-check instance vs the plain one: two PMC passes over kbench mvcc
           for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \
                       "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
