@@ -109,6 +109,15 @@ constexpr uint32_t HOPS = LZ4PAR_HOPS;
 #define LZ4PAR_WSCAN 1
 #endif
 constexpr bool WSCAN = LZ4PAR_WSCAN;
+// Pointer doubling with no barrier per round (ph_double_async): off — the
+// waves advance on stale values of each other's entries and need more
+// passes than the round-synchronous loop saves in barriers (ids 118.7 vs
+// 126.3 GB/s at 2,048 streams, text 128.0 vs 132.9, val level, snappy
+// −1 to −6 %: profiles/r6/lz4par/async_doubling_ab_r6ad.json)
+#ifndef LZ4PAR_ASYNC_DOUBLE
+#define LZ4PAR_ASYNC_DOUBLE 0
+#endif
+constexpr bool ASYNC_DOUBLE = LZ4PAR_ASYNC_DOUBLE;
 static_assert(LZ4PAR_NT % 64 == 0, "whole waves");
 static_assert(SL % UB == 0 && SL < kCkNone, "fill units");
 static_assert(OB % NT == 0 && 32 % EPT == 0 && HW <= NT && 4 * KW <= 32, "expansion tiling");
@@ -960,6 +969,35 @@ HD bool ph_double(Smem &s, uint32_t t, uint32_t nb) {
   return more;
 }
 
+// (4b') the doubling without a barrier per round: each thread repeats
+// passes over its own unresolved entries until all of them hold a tagged
+// (final) pointer.  Correct without synchronization because every value an
+// entry ever holds is a valid pointer of its byte and pointers only move
+// towards the roots (v < e, roots are tagged and never change): a stale read
+// of another wave's entry is an earlier point of the same chain, so a pass
+// still moves each entry at least one step, and a thread ends in at most
+// (chain length) passes even if no other wave progressed.  LDS accesses are
+// volatile so each pass sees the other waves' latest replacements; the
+// caller's barrier after it publishes the result.
+__device__ __forceinline__ void ph_double_async(Smem &s, uint32_t t, uint32_t nb) {
+  volatile uint32_t *p = s.ptr;
+  bool more = true;
+  while (more) {
+    more = false;
+    for (uint32_t e = t; e < nb; e += NT) {
+      const uint32_t v = p[PI(e)];
+      if (v & kTag) continue;
+      uint32_t w = v < e ? p[PI(v)] : kLit;
+      for (uint32_t k = 1; k < HOPS && !(w & kTag); ++k) {
+        const uint32_t x = w;
+        w = x < e ? p[PI(x)] : kLit;
+      }
+      p[PI(e)] = w;
+      more |= !(w & kTag);
+    }
+  }
+}
+
 HD uint8_t hist_byte(const Ctx &c, uint32_t pos) {
 #ifdef __HIP_DEVICE_COMPILE__
   // stored by this workgroup in an earlier batch, visible after the
@@ -1453,11 +1491,17 @@ __device__ __forceinline__ void lz4par_body(Smem &s, int codec, const uint8_t *_
           ph_expand(s, t, nb);
           __syncthreads();
           LP_MARK(kLpExpand);
-          bool more;
-          do {
+          if (ASYNC_DOUBLE) {
             LP_CNT(kLpNDouble);
-            more = ph_double(s, t, nb);
-          } while (__syncthreads_or(more));
+            ph_double_async(s, t, nb);
+            __syncthreads();
+          } else {
+            bool more;
+            do {
+              LP_CNT(kLpNDouble);
+              more = ph_double(s, t, nb);
+            } while (__syncthreads_or(more));
+          }
           LP_MARK(kLpDouble);
           Held h;
           ph_resolve(s, c, t, b0, nb, h);
