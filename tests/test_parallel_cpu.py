@@ -246,12 +246,14 @@ def _deliver_worker(rank, world, port, path, window, q):
         q.put((rank, traceback.format_exc()))
 
 
-def test_fanout_delivers_shards_four_ranks(tmp_path):
+@pytest.mark.parametrize("world", [4, 8])
+def test_fanout_delivers_shards(tmp_path, world):
     """the fan-out delivers every step's gathered shards to a
     consumer (pulled while the next step loads, or via the callback), the
     ring never overwrites a held step, and a corrupted slice is caught at
-    its step with every rank agreeing."""
-    world, window = 4, 128 << 10
+    its step with every rank agreeing — at 4 ranks and at the 8 of an MI355X
+    node (the driver's scaling run)."""
+    window = 128 << 10
     path = str(tmp_path / "shard")
     for r in range(world):
         np.random.default_rng(40 + r).integers(0, 256, 4 * window, dtype=np.uint8).tofile(f"{path}.{r}")
