@@ -44,3 +44,17 @@ def test_bench_shard_sizing():
     assert b.shard_bytes(4 * G, G, 20 * G, 4 * G, 8) == 2 * G       # own old shard counts
     assert b.shard_bytes(4 * G, G, 1 * G, 0, 8) == G                # never below a window
     assert b.shard_bytes(4 * G, G, int(9.9 * G), 0, 2) == 3 * G     # whole windows
+
+
+def test_gpu_recipes_parse():
+    """tools/gpu.sh (every committed profile's recipe) is valid bash, and the
+    phases the round-6 summary cites exist in it."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tools", "gpu.sh")
+    assert subprocess.run(["bash", "-n", path]).returncode == 0
+    text = open(path).read()
+    for phase in ("tests", "smoke", "bench", "benchab", "probe", "lzpmc", "lppmc", "mvpmc",
+                  "zatrace", "sweep", "pg", "arrow"):
+        assert f"\n    {phase}) " in text, phase
