@@ -1298,7 +1298,7 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   out[5] = bench([&] { sink += (uint64_t)(engine().open_file_cached(fd, &err) != nullptr); });
   // a 4 KiB store through the BAR with its (posted) HDP flush, then the
   // first locked instruction after it: is the write's drain paid there?
-  out[6] = out[7] = out[8] = out[9] = 0;
+  for (int k = 6; k < 14; ++k) out[k] = 0;
   if (g->bar && g->length >= 4096 && g->va >= g->bar_va && g->va + 4096 <= g->bar_va + g->bar_len) {
     // the probe stores over the mapping's first 4 KiB: keep them and put
     // them back afterwards (one slow BAR read)
@@ -1306,7 +1306,9 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
     memcpy(keep, g->bar + (g->va - g->bar_va), 4096);
     memcpy(src, keep, 4096);
     std::atomic<uint64_t> ctr{0};
-    for (int mode = 0; mode < 2; ++mode) {
+    // modes: 0 memcpy, 1 whole-line non-temporal (the default), 2 the same
+    // last line first, 3 rep movsb
+    for (int mode = 0; mode < 4; ++mode) {
       uint64_t store = 0, lock = 0;
       for (int i = 0; i < n; ++i) {
         const uint64_t t0 = mono_ns();

@@ -77,10 +77,29 @@ __attribute__((target("avx2"))) static void bar_copy_nt256(uint8_t *d, const uin
   if (i < n) memcpy(d + i, s + i, n - i);
 }
 
+// probe-only orders (strom_engine_costs modes 2 / 3): whole lines last to
+// first, and the string move (ERMS) — does another store order shorten the
+// write-combining drain paid after a 4 KiB store?
+__attribute__((target("avx512f"))) static void bar_copy_nt512_rev(uint8_t *d, const uint8_t *s,
+                                                                  size_t n) {
+  size_t i = n & ~(size_t)63;
+  if (i < n) memcpy(d + i, s + i, n - i);
+  while (i) {
+    i -= 64;
+    _mm512_stream_si512((__m512i *)(d + i), _mm512_loadu_si512((const void *)(s + i)));
+  }
+}
+
+static void bar_copy_movsb(uint8_t *d, const uint8_t *s, size_t n) {
+  asm volatile("rep movsb" : "+D"(d), "+S"(s), "+c"(n) : : "memory");
+}
+
 static void bar_copy(uint8_t *d, const void *src, size_t n, int mode) {
   static const int have512 = __builtin_cpu_supports("avx512f") ? 1 : 0;
   static const int have256 = __builtin_cpu_supports("avx2") ? 1 : 0;
   const uint8_t *s = (const uint8_t *)src;
+  if (mode == 2 && have512 && !((uintptr_t)d & 63)) return bar_copy_nt512_rev(d, s, n);
+  if (mode == 3) return bar_copy_movsb(d, s, n);
   // 64-byte aligned destinations only: a line split over two WC buffers
   // gains nothing
   if (mode && !((uintptr_t)d & 63)) {
