@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <set>
+#include <thread>
 
 #include "engine.h"
 
@@ -1298,7 +1299,7 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
   out[5] = bench([&] { sink += (uint64_t)(engine().open_file_cached(fd, &err) != nullptr); });
   // a 4 KiB store through the BAR with its (posted) HDP flush, then the
   // first locked instruction after it: is the write's drain paid there?
-  for (int k = 6; k < 14; ++k) out[k] = 0;
+  for (int k = 6; k < 16; ++k) out[k] = 0;
   if (g->bar && g->length >= 4096 && g->va >= g->bar_va && g->va + 4096 <= g->bar_va + g->bar_len) {
     // the probe stores over the mapping's first 4 KiB: keep them and put
     // them back afterwards (one slow BAR read)
@@ -1321,6 +1322,39 @@ int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n) {
       }
       out[6 + 2 * mode] = store / (uint64_t)n;
       out[7 + 2 * mode] = lock / (uint64_t)n;
+    }
+    // the verdict's other idea: the 4 KiB split over two cores, each storing
+    // 2 KiB and draining it; out[14] = start to both halves drained (compare
+    // out[8] + out[9]), out[15] = the hand-off alone (a helper that stores
+    // nothing).  The helper spins on a counter: probe only.
+    for (int variant = 0; variant < 2; ++variant) {
+      std::atomic<uint64_t> go{0}, done{0};
+      std::atomic<bool> quit{false};
+      std::thread helper([&] {
+        uint64_t seen = 0;
+        while (!quit.load(std::memory_order_acquire)) {
+          const uint64_t v = go.load(std::memory_order_acquire);
+          if (v == seen) {
+            _mm_pause();
+            continue;
+          }
+          seen = v;
+          if (variant == 0) g->bar_write_mode(g->va + 2048, src + 2048, 2048, 1);
+          done.fetch_add(1, std::memory_order_acq_rel);   // its own drain paid here
+        }
+      });
+      uint64_t tot = 0;
+      for (int i = 0; i < n; ++i) {
+        const uint64_t t0 = mono_ns();
+        go.fetch_add(1, std::memory_order_acq_rel);
+        if (variant == 0) g->bar_write_mode(g->va, src, 2048, 1);
+        ctr.fetch_add(1);
+        while (done.load(std::memory_order_acquire) != (uint64_t)i + 1) _mm_pause();
+        tot += mono_ns() - t0;
+      }
+      quit.store(true, std::memory_order_release);
+      helper.join();
+      out[14 + variant] = tot / (uint64_t)n;
     }
     g->bar_write(g->va, keep, 4096, true);
     sink += ctr.load();

@@ -71,9 +71,11 @@ int strom_pread_pair_lat(int session, unsigned long handle, size_t offset, int f
  * bare syscall, mutex lock+unlock, condvar notify} -> out[7]. */
 int strom_host_costs(int fd, uint64_t *out, int n);
 /* the engine's own steps of a synchronous read (registry lookup, freed-range
- * check, file cache, completion bookkeeping), ns per call -> out[14]: the
- * last 8 are a 4 KiB BAR store and the first locked instruction after it,
- * for memcpy / whole-line non-temporal / the same last line first / rep movsb */
+ * check, file cache, completion bookkeeping), ns per call; out[6..13] are a
+ * 4 KiB BAR store and the first locked instruction after it,
+ * for memcpy / whole-line non-temporal / the same last line first / rep movsb,
+ * then the 4 KiB split over two cores (start to both halves drained) and
+ * that split's hand-off alone -> out[16] */
 int strom_engine_costs(unsigned long handle, int fd, uint64_t *out, int n);
 
 /* Storage ceiling for a block size, no engine: `threads` io_uring rings,

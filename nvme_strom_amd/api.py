@@ -181,7 +181,8 @@ def host_costs(fd: int, n: int = 20000) -> dict:
 ENGINE_COSTS = ("registry_get", "validate", "open_file", "completion", "registry_get_cached",
                 "open_file_cached", "bar_store_4k", "lock_after_bar_store", "bar_store_4k_nt",
                 "lock_after_bar_store_nt", "bar_store_4k_nt_rev", "lock_after_bar_store_nt_rev",
-                "bar_store_4k_movsb", "lock_after_bar_store_movsb")
+                "bar_store_4k_movsb", "lock_after_bar_store_movsb", "bar_store_4k_two_cores",
+                "two_core_handoff")
 
 
 def engine_costs(handle: int, fd: int, n: int = 20000) -> dict:
